@@ -1,0 +1,147 @@
+"""Python binding of the MI355X local-BA C ABI (include/amc_lba.h) via ctypes.
+
+The binding mirrors the drop-in boundary one to one: `Problem` owns an `lba_problem*`, takes the
+flat window arrays (numpy structured arrays with the dtypes of `abi`) and calls the HIP library.
+There is no CPU fallback: importing works anywhere, but every call goes to libamc_lba.so and
+fails loudly when the library or a GPU is missing.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from .abi import (CAM_DTYPE, KF_DTYPE, OBS_DTYPE, PRIOR_DTYPE, LbaConfig, LbaStats, make_config,  # noqa: F401
+                  ptr)
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libamc_lba.so")
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_lib = None
+
+
+class LbaError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"lba error {code}: {msg}")
+        self.code = code
+
+
+def lib():
+    """Load libamc_lba.so (built by __graft_entry__.build()); raises if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} not built: run python -c 'import __graft_entry__ as g; g.build()'")
+        L = ctypes.CDLL(LIB_PATH)
+        vp = ctypes.c_void_p
+        L.lba_abi_version.restype = ctypes.c_int
+        L.lba_create.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(LbaConfig)]
+        L.lba_destroy.argtypes = [vp]
+        L.lba_destroy.restype = None
+        L.lba_last_error.argtypes = [vp]
+        L.lba_last_error.restype = ctypes.c_char_p
+        L.lba_pose_dim.argtypes = [vp]
+        L.lba_set_problem.argtypes = [vp, vp, ctypes.c_int32, vp, ctypes.c_int32, vp, ctypes.c_int32, vp,
+                                      ctypes.c_int32, vp, ctypes.c_int32, vp, ctypes.c_int32]
+        L.lba_optimize.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(LbaStats)]
+        L.lba_get_state.argtypes = [vp, vp, _dp]
+        L.lba_set_state.argtypes = [vp, vp, _dp]
+        L.lba_eval.argtypes = [vp, _dp, _dp, vp]
+        L.lba_linearize.argtypes = [vp, _dp, _dp, _dp, _dp]
+        L.lba_solve_step.argtypes = [vp, ctypes.c_double, _dp]
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return ["lba_abi_version", "lba_create", "lba_destroy", "lba_last_error", "lba_set_problem", "lba_optimize",
+            "lba_get_state", "lba_set_state", "lba_eval", "lba_linearize", "lba_solve_step", "lba_pose_dim"]
+
+
+def _d(a):
+    return None if a is None else a.ctypes.data_as(_dp)
+
+
+class Problem:
+    """One local-BA window resident on one GPU (lba_create + lba_set_problem)."""
+
+    def __init__(self, win, cfg=None, device=0, **cfg_over):
+        L = lib()
+        if cfg is None:
+            kw = dict(win.cfg)
+            kw.update(cfg_over)
+            kw.setdefault("device", device)
+            cfg = make_config(**kw)
+        self.cfg = cfg
+        self.h = ctypes.c_void_p()
+        self._check(L.lba_create(ctypes.byref(self.h), ctypes.byref(cfg)), created=False)
+        self.win = win
+        self.n_obs, self.n_lm, self.n_kf = len(win.obs), len(win.lm), len(win.kfs)
+        self._keep = tuple(np.ascontiguousarray(a) for a in (win.kfs, win.lm, win.obs, win.priors, win.vel_kfs,
+                                                              win.cams))
+        kfs, lm, obs, pri, vel, cams = self._keep
+        self._check(L.lba_set_problem(self.h, ptr(kfs), len(kfs), ptr(lm), len(lm), ptr(obs), len(obs), ptr(pri),
+                                      len(pri), ptr(vel), len(vel), ptr(cams), len(cams)))
+
+    def _check(self, rc, created=True):
+        if rc < 0:
+            msg = lib().lba_last_error(self.h).decode() if created and self.h else "lba_create failed"
+            raise LbaError(rc, msg)
+        return rc
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().lba_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        self.close()
+
+    @property
+    def pose_dim(self):
+        return lib().lba_pose_dim(self.h)
+
+    @property
+    def lm_dim(self):
+        return 3 * int(np.unique(self.win.obs["lm"]).size)
+
+    def optimize(self, iters, stop_flag=None):
+        st = LbaStats()
+        flag = None if stop_flag is None else ctypes.byref(stop_flag)
+        n = self._check(lib().lba_optimize(self.h, iters, flag, ctypes.byref(st)))
+        return n, st
+
+    def state(self):
+        kfs = np.zeros(self.n_kf, KF_DTYPE)
+        lm = np.zeros((self.n_lm, 3))
+        self._check(lib().lba_get_state(self.h, ptr(kfs), _d(lm)))
+        return kfs, lm
+
+    def set_state(self, kfs=None, lm=None):
+        kfs = None if kfs is None else np.ascontiguousarray(kfs, dtype=KF_DTYPE)
+        lm = None if lm is None else np.ascontiguousarray(lm, dtype=np.float64)
+        self._check(lib().lba_set_state(self.h, ptr(kfs), _d(lm)))
+
+    def eval(self):
+        chi = ctypes.c_double()
+        c2 = np.zeros(self.n_obs)
+        ok = np.zeros(self.n_obs, np.uint8)
+        self._check(lib().lba_eval(self.h, ctypes.byref(chi), _d(c2), ptr(ok)))
+        return chi.value, c2, ok
+
+    def linearize(self):
+        np_ = self.pose_dim
+        H = np.zeros((np_, np_))
+        b = np.zeros(np_ + self.lm_dim)
+        Hll = np.zeros((self.n_lm, 9))
+        res = np.zeros((self.n_obs, 3))
+        self._check(lib().lba_linearize(self.h, _d(res), _d(H), _d(b), _d(Hll)))
+        return res, H, b, Hll
+
+    def solve_step(self, lam):
+        dx = np.zeros(self.pose_dim + self.lm_dim)
+        rc = lib().lba_solve_step(self.h, lam, _d(dx))
+        if rc == -2:
+            return False, dx
+        self._check(rc)
+        return True, dx

@@ -1,0 +1,106 @@
+"""numpy dtypes that mirror the C structs of include/amc_lba.h byte for byte.
+
+Used both by the ctypes binding of the product (`amc_lba.Problem`) and by the oracle
+binding under oracle/ (test infrastructure), so both sides read identical buffers.
+"""
+import ctypes
+
+import numpy as np
+
+KF_DTYPE = np.dtype([
+    ("q", "<f8", (4,)), ("t", "<f8", (3,)), ("vel", "<f8", (6,)),
+    ("time", "<f8"), ("bf", "<f8"), ("fixed", "<i4"), ("pad", "<i4"),
+], align=True)
+
+OBS_DTYPE = np.dtype([
+    ("kind", "<i4"), ("kf_a", "<i4"), ("kf_b", "<i4"), ("lm", "<i4"), ("cam", "<i4"), ("pad", "<i4"),
+    ("t", "<f8"), ("z", "<f8", (3,)), ("w", "<f8"),
+], align=True)
+
+PRIOR_DTYPE = np.dtype([("kf_a", "<i4"), ("kf_b", "<i4")], align=True)
+
+CAM_DTYPE = np.dtype([
+    ("q", "<f8", (4,)), ("t", "<f8", (3,)),
+    ("fx", "<f8"), ("fy", "<f8"), ("cx", "<f8"), ("cy", "<f8"),
+], align=True)
+
+assert KF_DTYPE.itemsize == 128
+assert OBS_DTYPE.itemsize == 64
+assert PRIOR_DTYPE.itemsize == 8
+assert CAM_DTYPE.itemsize == 88
+
+# observation kinds (LBA_MONO_GP ... LBA_STEREO)
+MONO_GP, STEREO_GP, MONO, STEREO = 0, 1, 2, 3
+
+# status codes
+LBA_OK, LBA_E_EMPTY, LBA_E_SOLVE, LBA_E_DIVERGED, LBA_E_ARG, LBA_E_HIP, LBA_E_LIMIT = 0, -1, -2, -3, -4, -5, -6
+
+
+class LbaConfig(ctypes.Structure):
+    _fields_ = [
+        ("qc", ctypes.c_double * 36),
+        ("huber_mono", ctypes.c_double),
+        ("huber_stereo", ctypes.c_double),
+        ("huber_prior", ctypes.c_double),
+        ("lambda_init", ctypes.c_double),
+        ("tau", ctypes.c_double),
+        ("max_trials", ctypes.c_int32),
+        ("early_stop", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
+    ]
+
+
+class LbaStats(ctypes.Structure):
+    _fields_ = [
+        ("iterations", ctypes.c_int32),
+        ("trials", ctypes.c_int32),
+        ("result", ctypes.c_int32),
+        ("solve_failures", ctypes.c_int32),
+        ("chi2_initial", ctypes.c_double),
+        ("chi2_final", ctypes.c_double),
+        ("lambda_final", ctypes.c_double),
+        ("ms_linearize", ctypes.c_double),
+        ("ms_schur", ctypes.c_double),
+        ("ms_solve", ctypes.c_double),
+        ("ms_update_eval", ctypes.c_double),
+        ("ms_total", ctypes.c_double),
+        ("ms_k_linearize", ctypes.c_double),
+        ("n_k_linearize", ctypes.c_int32),
+        ("pad", ctypes.c_int32),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+def make_config(qc_diag=(0.02, 0.02, 0.02, 0.002, 0.002, 0.002), huber_mono=None, huber_stereo=None,
+                huber_prior=0.0, lambda_init=1.0, tau=1e-5, max_trials=10, early_stop=1, device=0):
+    """LocalGPBA defaults: Huber deltas are float sqrt(5.991)/sqrt(7.815) widened to double
+    (src/Optimizer.cc:975-978), lambda0 = 1.0 (:848-856), tau 1e-5, 10 trials."""
+    cfg = LbaConfig()
+    qc = np.zeros((6, 6))
+    if np.ndim(qc_diag) == 2:
+        qc[:] = qc_diag
+    else:
+        qc[np.diag_indices(6)] = qc_diag
+    for i, v in enumerate(qc.ravel()):
+        cfg.qc[i] = float(v)
+    cfg.huber_mono = float(np.float32(np.sqrt(5.991))) if huber_mono is None else huber_mono
+    cfg.huber_stereo = float(np.float32(np.sqrt(7.815))) if huber_stereo is None else huber_stereo
+    cfg.huber_prior = huber_prior
+    cfg.lambda_init = lambda_init
+    cfg.tau = tau
+    cfg.max_trials = max_trials
+    cfg.early_stop = early_stop
+    cfg.device = device
+    cfg.flags = 0
+    return cfg
+
+
+def ptr(a, ctype=ctypes.c_void_p):
+    """ctypes pointer to a C-contiguous numpy array (None -> NULL)."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(ctype)

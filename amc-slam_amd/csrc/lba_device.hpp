@@ -1,0 +1,148 @@
+// lba_device.hpp — HBM layout of one local-BA window and the kernel launch interface.
+//
+// Layout (all fp64 unless noted; "device order" = landmarks sorted by the span of keyframes
+// that observe them, observations grouped by landmark, so a tile of consecutive landmarks
+// touches a narrow band of keyframes):
+//   kf state      [n_kf][16]   q(4) t(3) vel(6) time bf pad   — two copies (current / trial)
+//   lm state      [n_lm][3]                                     — two copies (current / trial)
+//   observations  SoA, device order: meta(kind|cam<<4), kf_a, kf_b, gp pair, landmark,
+//                 pair slots a/b, tile-local LDS row, t, z[3], w
+//   gp pairs      [n_gp][GPP_STRIDE] per (prev KF, KF) interpolation quantities (lba::GPPair)
+//   Hpl           [n_pairs][12][3] one block per unique (non-fixed KF, landmark)
+//   Hll, bl       [n_lm][9], [n_lm][3]
+//   slab          [n_entries][456] per (tile, pose-pair segment) partial of Hpp/b:
+//                 aa(144) ab(144) bb(144) ga(12) gb(12); priors / velocity edges append
+//   slab2         [n_sentries][144] per (tile, KF pair) Schur partial  V(k1) Hpl(k2)^T
+//   S             [np][np] reduced camera system (lower triangle), factored in place
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace lba {
+
+constexpr int KF_STRIDE = 16;
+constexpr int CAMD_STRIDE = 16;     // Rcb(9) tcb(3) fx fy cx cy
+constexpr int KFP_STRIDE = 12;      // Rwb(9) twb(3)
+constexpr int ENTRY = 456;          // slab entry: aa ab bb ga gb
+constexpr int E_AA = 0, E_AB = 144, E_BB = 288, E_GA = 432, E_GB = 444;
+
+// tile limits (one workgroup of TILE_OBS threads per tile)
+constexpr int TILE_OBS = 128;
+constexpr int TILE_ROWS = 288;
+constexpr int TILE_PAIRS = 128;
+constexpr int TILE_LMS = 64;
+constexpr int TILE_KF = 16;
+constexpr int ROW_STRIDE = 28;      // LDS Jacobian row: Ja(12) Jb(12) e(1) Jp(3)
+
+// Hpp source roles (assemble)
+constexpr int R_AA = 0, R_BB = 1, R_AB = 2, R_ABT = 3;
+
+constexpr int CHOL_NB = 32;         // Cholesky panel width
+
+struct DevProblem {
+    int n_kf, n_lm, n_obs, n_gp, n_pairs, n_tiles, n_pb, np, n_prior, n_vel, n_cam;
+    int n_entries, n_sentries, n_ublocks;
+    // observations (device order)
+    const int* ob_meta;
+    const int* ob_kfa;
+    const int* ob_kfb;
+    const int* ob_gp;
+    const int* ob_lm;
+    const int* ob_row;
+    const double* ob_t;
+    const double* ob_z;     // [n_obs][3]
+    const double* ob_w;
+    // keyframes
+    const int* kf_hidx;
+    const int* gp_kfa;
+    const int* gp_kfb;
+    const double* camd;     // [n_cam][CAMD_STRIDE]
+    // tiles
+    const int* tile_obs0;
+    const int* tile_nobs;
+    const int* tile_lm0;
+    const int* tile_nlm;
+    const int* tile_pair0;
+    const int* tile_npair;
+    const int* tile_seg0;
+    const int* tile_nseg;
+    const int* tile_sent0;
+    const int* tile_nsent;
+    const int* tile_kf0;
+    const int* tile_nkf;
+    const int* tkf_list;    // tile KF unions (pose block indices)
+    const int* seg_a;       // per segment entry: pose block of side a / b (-1 = none)
+    const int* seg_b;
+    const int* seg_row0;    // tile-local first row
+    const int* seg_nrows;
+    const int* sent_l1;     // per Schur entry: tile-local KF index of k1 / k2
+    const int* sent_l2;
+    // pairs / landmarks
+    const int* pair_lm;
+    const int* pair_kf;     // pose block index
+    const int* pair_r0;     // CSR into pair_rows: tile-local row | side << 16
+    const int* pair_rows;
+    const int* lm_r0;       // CSR into lm_rows: tile-local rows
+    const int* lm_rows;
+    const int* lm_pair0;    // [n_lm + 1] landmark -> pairs
+    // assemble sources
+    const int* ublk_i;      // per upper block: block row / col
+    const int* ublk_j;
+    const int* hsrc0;       // CSR per upper block: entry << 2 | role
+    const int* hsrc;
+    const int* ssrc0;       // CSR per upper block: Schur entries
+    const int* ssrc;
+    const int* bsrc0;       // CSR per pose block: entry << 1 | side(0 = a, 1 = b)
+    const int* bsrc;
+    const int* kfp0;        // CSR per pose block: pairs
+    const int* kfp;
+    // motion-prior / velocity edges
+    const int* pri_a;
+    const int* pri_b;
+    const int* vel_kf;
+    int pri_entry0;         // slab entry of prior 0 (velocity edges follow)
+    double qcinv[36];
+    double huber_mono, huber_stereo, huber_prior;
+    // work buffers
+    double* gpp;            // [n_gp][GPP_STRIDE]
+    double* kfp_pose;       // [n_kf][KFP_STRIDE]
+    double* slab;
+    double* slab2;
+    double* Hpl;
+    double* Hll;
+    double* bl;
+    double* Dinv;
+    double* V;
+    double* gpair;          // [n_pairs][12]
+    double* S;              // [np][np]
+    double* bp;             // [np]
+    double* xsol;           // [np] rhs -> solution
+    double* x;              // [np + 3 n_lm]
+    double* chi_lin;        // [n_tiles + n_prior + n_vel]
+    double* chi_eval;       // [n_tiles + n_prior + n_vel]
+    double* scale_part;     // [n_upd_blocks]
+    int n_upd_blocks;
+    int* info;              // [1] factorisation status
+    double* fin;            // [4] chi_lin, chi_eval, scale, info
+    double* ob_chi2;        // [n_obs]
+    double* ob_res;         // [n_obs][3]
+};
+
+// launchers (lba_kernels.hip)
+void launch_pair_prep(const DevProblem& P, const double* kst, hipStream_t s);
+void launch_linearize(const DevProblem& P, const double* kst, const double* lst, int write_res, hipStream_t s);
+void launch_prior_lin(const DevProblem& P, const double* kst, hipStream_t s);
+void launch_schur_prep(const DevProblem& P, double lambda, hipStream_t s);
+void launch_schur(const DevProblem& P, hipStream_t s);
+enum { ASM_SCHUR = 1, ASM_FULL = 2 };
+void launch_assemble(const DevProblem& P, double lambda, int flags, hipStream_t s);
+void launch_cholesky_solve(const DevProblem& P, hipStream_t s);
+void launch_update(const DevProblem& P, double lambda, const double* kst, const double* lst, double* kst_out,
+                   double* lst_out, hipStream_t s);
+void launch_eval(const DevProblem& P, const double* kst, const double* lst, hipStream_t s);
+void launch_finalize(const DevProblem& P, hipStream_t s);
+void launch_depth(const DevProblem& P, const double* kst, const double* lst, unsigned char* ok, hipStream_t s);
+
+constexpr int GPP_STRIDE = 171;     // doubles in lba::GPPair (static_assert in lba_kernels.hip)
+
+}  // namespace lba

@@ -1,0 +1,909 @@
+// lba_host.hip — host side of the MI355X local BA: window preprocessing into the HBM layout of
+// lba_device.hpp, the Levenberg-Marquardt driver (g2o OptimizationAlgorithmLevenberg semantics,
+// Thirdparty/g2o/g2o/core/optimization_algorithm_levenberg.cpp:61-194) and the C ABI of
+// include/amc_lba.h.
+//
+// State stays resident on the device between LM trials: the current and trial estimates are two
+// buffers, so g2o's push/pop/discardTop (sparse_optimizer.cpp:589-613) become a buffer swap.
+// The host reads back four doubles per trial (chi2 before, chi2 after, computeScale, factor status).
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/amc_lba.h"
+#include "lba_device.hpp"
+#include "lba_math.hpp"
+
+using namespace lba;
+
+struct lba_problem {
+    lba_config cfg{};
+    std::string err;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[8] = {};
+    bool has_problem = false;
+    bool linearized = false;
+    int n_kf = 0, n_lm = 0, n_obs = 0, n_cam = 0;
+    std::vector<int> kf_hidx;     // per KF: pose block or -1
+    std::vector<int> lm_dev;      // original landmark -> device index (-1 inactive)
+    std::vector<int> lm_orig;     // device index -> original landmark
+    std::vector<int> obs_dev;     // original observation -> device index
+    std::vector<double> lm_host;  // original landmark positions (inactive ones are returned as is)
+    std::vector<int> kf_fixed;
+    int n_lm_dev = 0, n_pb = 0, np = 0;
+    DevProblem D{};
+    double* kst[2] = {nullptr, nullptr};
+    double* lst[2] = {nullptr, nullptr};
+    int cur = 0;
+    std::vector<void*> allocs;
+    double* h_fin = nullptr;      // pinned [4]
+    double lambda = -1.0, ni = 2.0;
+    int nBad = 0;
+};
+
+namespace {
+
+struct HipError {
+    hipError_t e;
+    const char* what;
+};
+
+#define HIPCHK(x)                                   \
+    do {                                            \
+        hipError_t _e = (x);                        \
+        if (_e != hipSuccess) throw HipError{_e, #x}; \
+    } while (0)
+
+struct ApiError {
+    int code;
+    std::string msg;
+};
+
+void free_all(lba_problem* p) {
+    for (void* a : p->allocs) (void)hipFree(a);
+    p->allocs.clear();
+    p->kst[0] = p->kst[1] = p->lst[0] = p->lst[1] = nullptr;
+    p->D = DevProblem{};
+    p->has_problem = false;
+    p->linearized = false;
+}
+
+template <typename T>
+T* dalloc(lba_problem* p, size_t n) {
+    void* d = nullptr;
+    HIPCHK(hipMalloc(&d, std::max<size_t>(n, 1) * sizeof(T)));
+    p->allocs.push_back(d);
+    return static_cast<T*>(d);
+}
+template <typename T>
+T* dupload(lba_problem* p, const std::vector<T>& v) {
+    T* d = dalloc<T>(p, v.size());
+    if (!v.empty()) HIPCHK(hipMemcpy(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return d;
+}
+
+inline bool is_gp(int kind) { return kind == LBA_MONO_GP || kind == LBA_STEREO_GP; }
+inline int obs_dim(int kind) { return (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? 3 : 2; }
+
+void normalize_q(const double* q, double* o) {
+    const Quat n = qnormalize(Quat{q[0], q[1], q[2], q[3]});
+    o[0] = n.x; o[1] = n.y; o[2] = n.z; o[3] = n.w;
+}
+
+// 6x6 inverse (Gauss-Jordan, partial pivoting) for GaussianProcess::mQcInv = Qc.inverse()
+bool inverse6(const double* A, double* R) {
+    double M[6][12];
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 12; ++j) M[i][j] = j < 6 ? A[i * 6 + j] : (j - 6 == i ? 1.0 : 0.0);
+    for (int c = 0; c < 6; ++c) {
+        int piv = c;
+        for (int r = c + 1; r < 6; ++r)
+            if (std::fabs(M[r][c]) > std::fabs(M[piv][c])) piv = r;
+        if (M[piv][c] == 0.0) return false;
+        if (piv != c)
+            for (int j = 0; j < 12; ++j) std::swap(M[c][j], M[piv][j]);
+        const double d = M[c][c];
+        for (int j = 0; j < 12; ++j) M[c][j] /= d;
+        for (int r = 0; r < 6; ++r)
+            if (r != c) {
+                const double f = M[r][c];
+                if (f != 0.0)
+                    for (int j = 0; j < 12; ++j) M[r][j] -= f * M[c][j];
+            }
+    }
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) R[i * 6 + j] = M[i][6 + j];
+    return true;
+}
+
+inline int ublock_id(int n_pb, int bi, int bj) { return bi * n_pb - bi * (bi - 1) / 2 + (bj - bi); }
+
+// ------------------------------------------------------------------------------------------------
+int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xyz, int n_lm, const lba_obs* obs,
+                int n_obs, const lba_prior* priors, int n_priors, const int32_t* vel_kfs, int n_vel,
+                const lba_cam* cams, int n_cam) {
+    if (n_kf < 0 || n_lm < 0 || n_obs < 0 || n_priors < 0 || n_vel < 0 || n_cam < 0)
+        throw ApiError{LBA_E_ARG, "negative array size"};
+    if ((n_kf && !kfs) || (n_lm && !lm_xyz) || (n_obs && !obs) || (n_priors && !priors) || (n_vel && !vel_kfs) ||
+        (n_cam && !cams))
+        throw ApiError{LBA_E_ARG, "null array with non-zero size"};
+    for (int i = 0; i < n_obs; ++i) {
+        const lba_obs& o = obs[i];
+        if (o.kind < LBA_MONO_GP || o.kind > LBA_STEREO) throw ApiError{LBA_E_ARG, "obs " + std::to_string(i) + ": bad kind"};
+        if (o.kf_b < 0 || o.kf_b >= n_kf || o.lm < 0 || o.lm >= n_lm || o.cam < 0 || o.cam >= n_cam || o.cam > 255)
+            throw ApiError{LBA_E_ARG, "obs " + std::to_string(i) + ": index out of range"};
+        if (is_gp(o.kind)) {
+            if (o.kf_a < 0 || o.kf_a >= n_kf || o.kf_a == o.kf_b)
+                throw ApiError{LBA_E_ARG, "obs " + std::to_string(i) + ": bad kf_a"};
+            if (!(std::fabs(kfs[o.kf_b].time - kfs[o.kf_a].time) > 1e-6))   // QiInv assert (GaussianProcess.h:32)
+                throw ApiError{LBA_E_ARG, "obs " + std::to_string(i) + ": keyframe times too close"};
+        }
+    }
+    for (int i = 0; i < n_priors; ++i) {
+        const lba_prior& e = priors[i];
+        if (e.kf_a < 0 || e.kf_a >= n_kf || e.kf_b < 0 || e.kf_b >= n_kf || e.kf_a == e.kf_b)
+            throw ApiError{LBA_E_ARG, "prior " + std::to_string(i) + ": bad vertex"};
+        if (!(std::fabs(kfs[e.kf_b].time - kfs[e.kf_a].time) > 1e-6))
+            throw ApiError{LBA_E_ARG, "prior " + std::to_string(i) + ": keyframe times too close"};
+    }
+    for (int i = 0; i < n_vel; ++i)
+        if (vel_kfs[i] < 0 || vel_kfs[i] >= n_kf) throw ApiError{LBA_E_ARG, "velocity edge: bad vertex"};
+
+    free_all(p);
+    p->n_kf = n_kf; p->n_lm = n_lm; p->n_obs = n_obs; p->n_cam = n_cam;
+    p->lm_host.assign(lm_xyz, lm_xyz + 3 * (size_t)n_lm);
+    p->kf_fixed.resize(n_kf);
+    for (int k = 0; k < n_kf; ++k) p->kf_fixed[k] = kfs[k].fixed != 0;
+
+    // ---- active vertices (SparseOptimizer::initializeOptimization: a vertex is active if an edge
+    //      that is not all-fixed touches it, sparse_optimizer.cpp:197-267)
+    std::vector<char> kf_act(n_kf, 0), lm_act(n_lm, 0);
+    for (int i = 0; i < n_obs; ++i) {
+        lm_act[obs[i].lm] = 1;
+        kf_act[obs[i].kf_b] = 1;
+        if (is_gp(obs[i].kind)) kf_act[obs[i].kf_a] = 1;
+    }
+    std::vector<lba_prior> pri;
+    for (int i = 0; i < n_priors; ++i)
+        if (!(kfs[priors[i].kf_a].fixed && kfs[priors[i].kf_b].fixed)) {
+            pri.push_back(priors[i]);
+            kf_act[priors[i].kf_a] = kf_act[priors[i].kf_b] = 1;
+        }
+    std::vector<int> vel;
+    for (int i = 0; i < n_vel; ++i)
+        if (!kfs[vel_kfs[i]].fixed) {
+            vel.push_back(vel_kfs[i]);
+            kf_act[vel_kfs[i]] = 1;
+        }
+    p->kf_hidx.assign(n_kf, -1);
+    int n_pb = 0;
+    for (int k = 0; k < n_kf; ++k)
+        if (kf_act[k] && !kfs[k].fixed) p->kf_hidx[k] = n_pb++;
+    p->n_pb = n_pb;
+    p->np = 12 * n_pb;
+    if (p->np > 6144) throw ApiError{LBA_E_LIMIT, "pose system larger than 6144 (512 keyframes) not supported yet"};
+    const std::vector<int>& H = p->kf_hidx;
+
+    // ---- device landmark order: by the span of non-fixed KFs observing them
+    std::vector<int> lmin(n_lm, INT_MAX), lmax(n_lm, INT_MAX);
+    std::vector<int> lcnt(n_lm, 0);
+    for (int i = 0; i < n_obs; ++i) {
+        const lba_obs& o = obs[i];
+        lcnt[o.lm]++;
+        int ks[2] = {H[o.kf_b], is_gp(o.kind) ? H[o.kf_a] : -1};
+        for (int k : ks)
+            if (k >= 0) {
+                lmin[o.lm] = lmin[o.lm] == INT_MAX ? k : std::min(lmin[o.lm], k);
+                lmax[o.lm] = lmax[o.lm] == INT_MAX ? k : std::max(lmax[o.lm], k);
+            }
+    }
+    std::vector<int> order;
+    for (int l = 0; l < n_lm; ++l)
+        if (lm_act[l]) order.push_back(l);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+        if (lmin[a] != lmin[b]) return lmin[a] < lmin[b];
+        return lmax[a] < lmax[b];
+    });
+    const int nl = (int)order.size();
+    p->n_lm_dev = nl;
+    p->lm_orig = order;
+    p->lm_dev.assign(n_lm, -1);
+    for (int d = 0; d < nl; ++d) p->lm_dev[order[d]] = d;
+
+    // observations grouped by device landmark (stable)
+    std::vector<int> lobs0(nl + 1, 0);
+    for (int i = 0; i < n_obs; ++i) lobs0[p->lm_dev[obs[i].lm] + 1]++;
+    for (int d = 0; d < nl; ++d) lobs0[d + 1] += lobs0[d];
+    std::vector<int> obs_of(n_obs);
+    {
+        std::vector<int> fill(lobs0.begin(), lobs0.end() - 1);
+        for (int i = 0; i < n_obs; ++i) obs_of[fill[p->lm_dev[obs[i].lm]]++] = i;
+    }
+
+    // GP (prev KF, KF) pairs
+    std::map<std::pair<int, int>, int> gpmap;
+    std::vector<int> gp_a, gp_b;
+    for (int i = 0; i < n_obs; ++i)
+        if (is_gp(obs[i].kind)) {
+            auto key = std::make_pair(obs[i].kf_a, obs[i].kf_b);
+            if (!gpmap.count(key)) {
+                gpmap[key] = (int)gp_a.size();
+                gp_a.push_back(key.first);
+                gp_b.push_back(key.second);
+            }
+        }
+
+    // (KF, landmark) pairs, per device landmark, ascending pose block
+    std::vector<int> lm_pair0(nl + 1, 0), pair_lm, pair_kf;
+    std::vector<std::vector<int>> lm_kfs(nl);
+    for (int d = 0; d < nl; ++d) {
+        std::vector<int>& ks = lm_kfs[d];
+        for (int q = lobs0[d]; q < lobs0[d + 1]; ++q) {
+            const lba_obs& o = obs[obs_of[q]];
+            if (H[o.kf_b] >= 0) ks.push_back(H[o.kf_b]);
+            if (is_gp(o.kind) && H[o.kf_a] >= 0) ks.push_back(H[o.kf_a]);
+        }
+        std::sort(ks.begin(), ks.end());
+        ks.erase(std::unique(ks.begin(), ks.end()), ks.end());
+        lm_pair0[d + 1] = lm_pair0[d] + (int)ks.size();
+        for (int k : ks) { pair_lm.push_back(d); pair_kf.push_back(k); }
+    }
+    const int n_pairs = (int)pair_lm.size();
+
+    // ---- tiles: consecutive landmarks under the LDS limits of k_linearize / k_schur
+    std::vector<int> t_obs0, t_nobs, t_lm0, t_nlm, t_pair0, t_npair, t_seg0, t_nseg, t_sent0, t_nsent, t_kf0, t_nkf;
+    std::vector<int> tkf_list, seg_a, seg_b, seg_row0, seg_nrows, sent_l1, sent_l2, sent_k1, sent_k2;
+    std::vector<int> ob_row(n_obs, 0);
+    std::vector<int> pair_r0(n_pairs + 1, 0), pair_rows, lm_r0(nl + 1, 0), lm_rows;
+    {
+        int d = 0;
+        while (d < nl) {
+            int nobs = 0, rows = 0, npair = 0, nlmt = 0;
+            std::vector<int> uni;
+            int e = d;
+            while (e < nl) {
+                int no = lobs0[e + 1] - lobs0[e], nr = 0;
+                for (int q = lobs0[e]; q < lobs0[e + 1]; ++q) nr += obs_dim(obs[obs_of[q]].kind);
+                const int npl = lm_pair0[e + 1] - lm_pair0[e];
+                std::vector<int> u2 = uni;
+                for (int k : lm_kfs[e]) u2.push_back(k);
+                std::sort(u2.begin(), u2.end());
+                u2.erase(std::unique(u2.begin(), u2.end()), u2.end());
+                const bool fits = nobs + no <= TILE_OBS && rows + nr <= TILE_ROWS && npair + npl <= TILE_PAIRS &&
+                                  nlmt + 1 <= TILE_LMS && (int)u2.size() <= TILE_KF;
+                if (!fits) {
+                    if (e == d)
+                        throw ApiError{LBA_E_LIMIT, "landmark " + std::to_string(order[e]) +
+                                                        " exceeds tile limits (obs/rows/pairs/keyframes)"};
+                    break;
+                }
+                nobs += no; rows += nr; npair += npl; nlmt += 1; uni.swap(u2);
+                ++e;
+            }
+            const int tile = (int)t_obs0.size();
+            (void)tile;
+            t_obs0.push_back(lobs0[d]); t_nobs.push_back(nobs);
+            t_lm0.push_back(d); t_nlm.push_back(nlmt);
+            t_pair0.push_back(lm_pair0[d]); t_npair.push_back(npair);
+            t_kf0.push_back((int)tkf_list.size()); t_nkf.push_back((int)uni.size());
+            for (int k : uni) tkf_list.push_back(k);
+            auto local = [&](int k) { return (int)(std::lower_bound(uni.begin(), uni.end(), k) - uni.begin()); };
+            // segments: observations of the tile sorted by (pose block a, pose block b)
+            std::vector<int> tob;
+            for (int q = lobs0[d]; q < lobs0[e]; ++q) tob.push_back(q);
+            auto keyof = [&](int q) {
+                const lba_obs& o = obs[obs_of[q]];
+                return std::make_pair(is_gp(o.kind) ? H[o.kf_a] : -1, H[o.kf_b]);
+            };
+            std::stable_sort(tob.begin(), tob.end(), [&](int a, int b) { return keyof(a) < keyof(b); });
+            t_seg0.push_back((int)seg_a.size());
+            int row = 0;
+            for (size_t i = 0; i < tob.size();) {
+                const auto key = keyof(tob[i]);
+                const int r0 = row;
+                size_t j = i;
+                while (j < tob.size() && keyof(tob[j]) == key) {
+                    ob_row[tob[j]] = row;
+                    row += obs_dim(obs[obs_of[tob[j]]].kind);
+                    ++j;
+                }
+                seg_a.push_back(key.first); seg_b.push_back(key.second);
+                seg_row0.push_back(r0); seg_nrows.push_back(row - r0);
+                i = j;
+            }
+            t_nseg.push_back((int)seg_a.size() - t_seg0.back());
+            // row lists per pair and per landmark
+            for (int l = d; l < e; ++l) {
+                for (int q = lm_pair0[l]; q < lm_pair0[l + 1]; ++q) {
+                    const int k = pair_kf[q];
+                    for (int o = lobs0[l]; o < lobs0[l + 1]; ++o) {
+                        const lba_obs& ob = obs[obs_of[o]];
+                        const int dim = obs_dim(ob.kind);
+                        if (H[ob.kf_b] == k)
+                            for (int r = 0; r < dim; ++r) pair_rows.push_back((ob_row[o] + r) | (1 << 16));
+                        if (is_gp(ob.kind) && H[ob.kf_a] == k)
+                            for (int r = 0; r < dim; ++r) pair_rows.push_back(ob_row[o] + r);
+                    }
+                    pair_r0[q + 1] = (int)pair_rows.size();
+                }
+                for (int o = lobs0[l]; o < lobs0[l + 1]; ++o)
+                    for (int r = 0; r < obs_dim(obs[obs_of[o]].kind); ++r) lm_rows.push_back(ob_row[o] + r);
+                lm_r0[l + 1] = (int)lm_rows.size();
+            }
+            // Schur entries: every (k1 <= k2) pose-block pair co-observed by a landmark of the tile
+            std::vector<std::pair<int, int>> kp;
+            for (int l = d; l < e; ++l)
+                for (size_t a = 0; a < lm_kfs[l].size(); ++a)
+                    for (size_t b = a; b < lm_kfs[l].size(); ++b) kp.emplace_back(lm_kfs[l][a], lm_kfs[l][b]);
+            std::sort(kp.begin(), kp.end());
+            kp.erase(std::unique(kp.begin(), kp.end()), kp.end());
+            t_sent0.push_back((int)sent_l1.size());
+            for (auto& pr : kp) {
+                sent_l1.push_back(local(pr.first)); sent_l2.push_back(local(pr.second));
+                sent_k1.push_back(pr.first); sent_k2.push_back(pr.second);
+            }
+            t_nsent.push_back((int)kp.size());
+            d = e;
+        }
+    }
+    const int n_tiles = (int)t_obs0.size();
+    const int n_segs = (int)seg_a.size();
+    const int n_sent = (int)sent_l1.size();
+
+    // ---- slab entries (tile segments, priors, velocity edges) and the assemble source lists
+    std::vector<int> ent_a(seg_a), ent_b(seg_b);
+    for (auto& e : pri) { ent_a.push_back(H[e.kf_a]); ent_b.push_back(H[e.kf_b]); }
+    for (int k : vel) { ent_a.push_back(-1); ent_b.push_back(H[k]); }
+    const int n_entries = (int)ent_a.size();
+    const int n_ublocks = n_pb * (n_pb + 1) / 2;
+    std::vector<int> ublk_i(n_ublocks), ublk_j(n_ublocks);
+    for (int bi = 0; bi < n_pb; ++bi)
+        for (int bj = bi; bj < n_pb; ++bj) {
+            const int id = ublock_id(n_pb, bi, bj);
+            ublk_i[id] = bi; ublk_j[id] = bj;
+        }
+    std::vector<std::vector<int>> hs(n_ublocks), ss(n_ublocks), bs(n_pb), kps(n_pb);
+    for (int en = 0; en < n_entries; ++en) {
+        const int a = ent_a[en], b = ent_b[en];
+        if (a >= 0) { hs[ublock_id(n_pb, a, a)].push_back(en << 2 | R_AA); bs[a].push_back(en << 1 | 0); }
+        if (b >= 0) { hs[ublock_id(n_pb, b, b)].push_back(en << 2 | R_BB); bs[b].push_back(en << 1 | 1); }
+        if (a >= 0 && b >= 0) {
+            if (a < b) hs[ublock_id(n_pb, a, b)].push_back(en << 2 | R_AB);
+            else hs[ublock_id(n_pb, b, a)].push_back(en << 2 | R_ABT);
+        }
+    }
+    for (int s = 0; s < n_sent; ++s) ss[ublock_id(n_pb, sent_k1[s], sent_k2[s])].push_back(s);
+    for (int q = 0; q < n_pairs; ++q) kps[pair_kf[q]].push_back(q);
+    auto csr = [](const std::vector<std::vector<int>>& v, std::vector<int>& start, std::vector<int>& flat) {
+        start.assign(v.size() + 1, 0);
+        flat.clear();
+        for (size_t i = 0; i < v.size(); ++i) {
+            flat.insert(flat.end(), v[i].begin(), v[i].end());
+            start[i + 1] = (int)flat.size();
+        }
+    };
+    std::vector<int> hsrc0, hsrc, ssrc0, ssrc, bsrc0, bsrc, kfp0, kfpv;
+    csr(hs, hsrc0, hsrc);
+    csr(ss, ssrc0, ssrc);
+    csr(bs, bsrc0, bsrc);
+    csr(kps, kfp0, kfpv);
+
+    // ---- observations in device order
+    std::vector<int> ob_meta(n_obs), ob_kfa(n_obs), ob_kfb(n_obs), ob_gp(n_obs), ob_lm(n_obs);
+    std::vector<double> ob_t(n_obs), ob_z(3 * (size_t)n_obs), ob_w(n_obs);
+    p->obs_dev.assign(n_obs, -1);
+    for (int q = 0; q < n_obs; ++q) {
+        const lba_obs& o = obs[obs_of[q]];
+        p->obs_dev[obs_of[q]] = q;
+        ob_meta[q] = o.kind | (o.cam << 4);
+        ob_kfa[q] = is_gp(o.kind) ? o.kf_a : -1;
+        ob_kfb[q] = o.kf_b;
+        ob_gp[q] = is_gp(o.kind) ? gpmap[std::make_pair(o.kf_a, o.kf_b)] : -1;
+        ob_lm[q] = p->lm_dev[o.lm];
+        ob_t[q] = o.t;
+        ob_z[3 * (size_t)q] = o.z[0]; ob_z[3 * (size_t)q + 1] = o.z[1]; ob_z[3 * (size_t)q + 2] = o.z[2];
+        ob_w[q] = o.w;
+    }
+    // cameras: Tcb = Tbc^-1 as matrix (MultiKeyFrame::mTbc[c].cast<double>() normalises)
+    std::vector<double> camd(CAMD_STRIDE * (size_t)std::max(n_cam, 1), 0.0);
+    for (int c = 0; c < n_cam; ++c) {
+        Cam cm;
+        normalize_q(cams[c].q, cm.q);
+        for (int i = 0; i < 3; ++i) cm.t[i] = cams[c].t[i];
+        cm.fx = cams[c].fx; cm.fy = cams[c].fy; cm.cx = cams[c].cx; cm.cy = cams[c].cy;
+        CamD cd;
+        cam_derive(cm, &cd);
+        double* o = camd.data() + CAMD_STRIDE * c;
+        for (int i = 0; i < 9; ++i) o[i] = cd.Rcb[i];
+        o[9] = cd.tcb[0]; o[10] = cd.tcb[1]; o[11] = cd.tcb[2];
+        o[12] = cd.fx; o[13] = cd.fy; o[14] = cd.cx; o[15] = cd.cy;
+    }
+    // keyframe / landmark state
+    std::vector<double> kst(KF_STRIDE * (size_t)std::max(n_kf, 1), 0.0), lst(3 * (size_t)std::max(nl, 1), 0.0);
+    for (int k = 0; k < n_kf; ++k) {
+        double* o = kst.data() + KF_STRIDE * k;
+        normalize_q(kfs[k].q, o);
+        for (int i = 0; i < 3; ++i) o[4 + i] = kfs[k].t[i];
+        for (int i = 0; i < 6; ++i) o[7 + i] = kfs[k].vel[i];
+        o[13] = kfs[k].time;
+        o[14] = kfs[k].bf;
+    }
+    for (int d = 0; d < nl; ++d)
+        for (int i = 0; i < 3; ++i) lst[3 * (size_t)d + i] = lm_xyz[3 * (size_t)order[d] + i];
+    std::vector<int> pri_a, pri_b;
+    for (auto& e : pri) { pri_a.push_back(e.kf_a); pri_b.push_back(e.kf_b); }
+
+    // ---- device upload
+    DevProblem& D = p->D;
+    D.n_kf = n_kf; D.n_lm = nl; D.n_obs = n_obs; D.n_gp = (int)gp_a.size(); D.n_pairs = n_pairs;
+    D.n_tiles = n_tiles; D.n_pb = n_pb; D.np = p->np; D.n_prior = (int)pri.size(); D.n_vel = (int)vel.size();
+    D.n_cam = n_cam; D.n_entries = n_entries; D.n_sentries = n_sent; D.n_ublocks = n_ublocks;
+    D.ob_meta = dupload(p, ob_meta); D.ob_kfa = dupload(p, ob_kfa); D.ob_kfb = dupload(p, ob_kfb);
+    D.ob_gp = dupload(p, ob_gp); D.ob_lm = dupload(p, ob_lm);
+    std::vector<int> ob_row_dev(n_obs);
+    for (int q = 0; q < n_obs; ++q) ob_row_dev[q] = ob_row[q];
+    D.ob_row = dupload(p, ob_row_dev);
+    D.ob_t = dupload(p, ob_t); D.ob_z = dupload(p, ob_z); D.ob_w = dupload(p, ob_w);
+    D.kf_hidx = dupload(p, p->kf_hidx); D.gp_kfa = dupload(p, gp_a); D.gp_kfb = dupload(p, gp_b);
+    D.camd = dupload(p, camd);
+    D.tile_obs0 = dupload(p, t_obs0); D.tile_nobs = dupload(p, t_nobs); D.tile_lm0 = dupload(p, t_lm0);
+    D.tile_nlm = dupload(p, t_nlm); D.tile_pair0 = dupload(p, t_pair0); D.tile_npair = dupload(p, t_npair);
+    D.tile_seg0 = dupload(p, t_seg0); D.tile_nseg = dupload(p, t_nseg); D.tile_sent0 = dupload(p, t_sent0);
+    D.tile_nsent = dupload(p, t_nsent); D.tile_kf0 = dupload(p, t_kf0); D.tile_nkf = dupload(p, t_nkf);
+    D.tkf_list = dupload(p, tkf_list);
+    D.seg_a = dupload(p, seg_a); D.seg_b = dupload(p, seg_b); D.seg_row0 = dupload(p, seg_row0);
+    D.seg_nrows = dupload(p, seg_nrows); D.sent_l1 = dupload(p, sent_l1); D.sent_l2 = dupload(p, sent_l2);
+    D.pair_lm = dupload(p, pair_lm); D.pair_kf = dupload(p, pair_kf); D.pair_r0 = dupload(p, pair_r0);
+    D.pair_rows = dupload(p, pair_rows); D.lm_r0 = dupload(p, lm_r0); D.lm_rows = dupload(p, lm_rows);
+    D.lm_pair0 = dupload(p, lm_pair0);
+    D.ublk_i = dupload(p, ublk_i); D.ublk_j = dupload(p, ublk_j);
+    D.hsrc0 = dupload(p, hsrc0); D.hsrc = dupload(p, hsrc); D.ssrc0 = dupload(p, ssrc0); D.ssrc = dupload(p, ssrc);
+    D.bsrc0 = dupload(p, bsrc0); D.bsrc = dupload(p, bsrc); D.kfp0 = dupload(p, kfp0); D.kfp = dupload(p, kfpv);
+    D.pri_a = dupload(p, pri_a); D.pri_b = dupload(p, pri_b); D.vel_kf = dupload(p, vel);
+    D.pri_entry0 = n_segs;
+    double qcinv[36];
+    if (!inverse6(p->cfg.qc, qcinv)) throw ApiError{LBA_E_ARG, "Qc is singular"};
+    for (int i = 0; i < 36; ++i) D.qcinv[i] = qcinv[i];
+    D.huber_mono = p->cfg.huber_mono;
+    D.huber_stereo = p->cfg.huber_stereo;
+    D.huber_prior = p->cfg.huber_prior;
+    D.gpp = dalloc<double>(p, (size_t)GPP_STRIDE * std::max(D.n_gp, 1));
+    D.kfp_pose = dalloc<double>(p, (size_t)KFP_STRIDE * std::max(n_kf, 1));
+    D.slab = dalloc<double>(p, (size_t)ENTRY * std::max(n_entries, 1));
+    D.slab2 = dalloc<double>(p, (size_t)144 * std::max(n_sent, 1));
+    D.Hpl = dalloc<double>(p, (size_t)36 * std::max(n_pairs, 1));
+    D.Hll = dalloc<double>(p, (size_t)9 * std::max(nl, 1));
+    D.bl = dalloc<double>(p, (size_t)3 * std::max(nl, 1));
+    D.Dinv = dalloc<double>(p, (size_t)9 * std::max(nl, 1));
+    D.V = dalloc<double>(p, (size_t)36 * std::max(n_pairs, 1));
+    D.gpair = dalloc<double>(p, (size_t)12 * std::max(n_pairs, 1));
+    D.S = dalloc<double>(p, (size_t)p->np * p->np + 1);
+    D.bp = dalloc<double>(p, p->np + 1);
+    D.xsol = dalloc<double>(p, p->np + 1);
+    D.x = dalloc<double>(p, p->np + 3 * (size_t)nl + 1);
+    HIPCHK(hipMemset(D.x, 0, sizeof(double) * (p->np + 3 * (size_t)nl + 1)));   // BlockSolver::_x before any solve
+    const int nchi = n_tiles + D.n_prior + D.n_vel;
+    D.chi_lin = dalloc<double>(p, nchi + 1);
+    D.chi_eval = dalloc<double>(p, nchi + 1);
+    D.n_upd_blocks = (n_kf + nl + 255) / 256;
+    if (D.n_upd_blocks == 0) D.n_upd_blocks = 1;
+    D.scale_part = dalloc<double>(p, D.n_upd_blocks);
+    D.info = dalloc<int>(p, 1);
+    D.fin = dalloc<double>(p, 4);
+    D.ob_chi2 = dalloc<double>(p, std::max(n_obs, 1));
+    D.ob_res = dalloc<double>(p, 3 * (size_t)std::max(n_obs, 1));
+    HIPCHK(hipMemset(D.info, 0, sizeof(int)));
+    for (int s = 0; s < 2; ++s) {
+        p->kst[s] = dalloc<double>(p, kst.size());
+        p->lst[s] = dalloc<double>(p, lst.size());
+        HIPCHK(hipMemcpy(p->kst[s], kst.data(), kst.size() * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(p->lst[s], lst.data(), lst.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
+    p->cur = 0;
+    p->has_problem = true;
+    p->linearized = false;
+    return LBA_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+void linearize(lba_problem* p, int write_res, bool timed = false) {
+    const DevProblem& D = p->D;
+    launch_pair_prep(D, p->kst[p->cur], p->stream);
+    if (timed) HIPCHK(hipEventRecord(p->ev[6], p->stream));
+    launch_linearize(D, p->kst[p->cur], p->lst[p->cur], write_res, p->stream);
+    if (timed) HIPCHK(hipEventRecord(p->ev[7], p->stream));
+    launch_prior_lin(D, p->kst[p->cur], p->stream);
+    HIPCHK(hipGetLastError());
+    p->linearized = true;
+}
+
+// one damped solve + update into the trial buffers + evaluation of the trial state
+void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs) {
+    const DevProblem& D = p->D;
+    const int nx = 1 - p->cur;
+    HIPCHK(hipMemsetAsync(D.info, 0, sizeof(int), p->stream));
+    launch_schur_prep(D, lambda, p->stream);
+    launch_schur(D, p->stream);
+    launch_assemble(D, lambda, ASM_SCHUR, p->stream);
+    if (evs) HIPCHK(hipEventRecord(evs[0], p->stream));
+    launch_cholesky_solve(D, p->stream);
+    if (evs) HIPCHK(hipEventRecord(evs[1], p->stream));
+    launch_update(D, lambda, p->kst[p->cur], p->lst[p->cur], p->kst[nx], p->lst[nx], p->stream);
+    if (evaluate) {
+        launch_pair_prep(D, p->kst[nx], p->stream);
+        launch_eval(D, p->kst[nx], p->lst[nx], p->stream);
+    }
+    launch_finalize(D, p->stream);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(p->h_fin, D.fin, 4 * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+    if (evs) HIPCHK(hipEventRecord(evs[2], p->stream));
+    HIPCHK(hipStreamSynchronize(p->stream));
+}
+
+double eval_current(lba_problem* p) {
+    const DevProblem& D = p->D;
+    launch_pair_prep(D, p->kst[p->cur], p->stream);
+    launch_eval(D, p->kst[p->cur], p->lst[p->cur], p->stream);
+    launch_finalize(D, p->stream);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(p->h_fin, D.fin, 4 * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+    HIPCHK(hipStreamSynchronize(p->stream));
+    return p->h_fin[1];
+}
+
+double lambda_init(lba_problem* p) {   // computeLambdaInit (levenberg.cpp:171-185)
+    if (p->cfg.lambda_init > 0) return p->cfg.lambda_init;
+    const DevProblem& D = p->D;
+    launch_assemble(D, 0.0, ASM_FULL, p->stream);
+    std::vector<double> S((size_t)p->np * p->np), Hll(9 * (size_t)std::max(D.n_lm, 1));
+    HIPCHK(hipMemcpyAsync(S.data(), D.S, S.size() * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+    HIPCHK(hipMemcpyAsync(Hll.data(), D.Hll, 9 * (size_t)D.n_lm * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+    HIPCHK(hipStreamSynchronize(p->stream));
+    double m = 0.0;
+    for (int i = 0; i < p->np; ++i) m = std::max(m, std::fabs(S[(size_t)i * p->np + i]));
+    for (int l = 0; l < D.n_lm; ++l)
+        for (int d = 0; d < 3; ++d) m = std::max(m, std::fabs(Hll[9 * (size_t)l + 4 * d]));
+    return p->cfg.tau * m;
+}
+
+float elapsed(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.f;
+    return ms;
+}
+
+int optimize(lba_problem* p, int iters, volatile const int32_t* stop, lba_stats* st) {
+    if (!p->has_problem) throw ApiError{LBA_E_ARG, "no problem set"};
+    lba_stats s{};
+    if (p->np + 3 * p->n_lm_dev == 0) throw ApiError{LBA_E_EMPTY, "0 vertices to optimize"};
+    const auto t0 = std::chrono::steady_clock::now();
+    s.chi2_initial = eval_current(p);
+    double last_chi = s.chi2_initial;
+    int it = 0, result = LBA_RESULT_OK;
+    for (int i = 0; i < iters; ++i) {
+        if (stop && *stop) { result = LBA_RESULT_STOPPED; break; }
+        HIPCHK(hipEventRecord(p->ev[0], p->stream));
+        linearize(p, 0, true);
+        HIPCHK(hipEventRecord(p->ev[1], p->stream));
+        if (i == 0) {
+            p->lambda = lambda_init(p);
+            p->ni = 2.0;
+            p->nBad = 0;
+        }
+        double currentChi = 0.0, iniChi = 0.0, rho = 0.0;
+        int qmax = 0;
+        do {
+            trial(p, p->lambda, true, p->ev + 2);
+            if (qmax == 0) {
+                currentChi = iniChi = p->h_fin[0];
+                s.ms_linearize += elapsed(p->ev[0], p->ev[1]);
+                s.ms_k_linearize += elapsed(p->ev[6], p->ev[7]);
+                s.n_k_linearize += 1;
+            }
+            s.ms_schur += elapsed(qmax == 0 ? p->ev[1] : p->ev[5], p->ev[2]);
+            s.ms_solve += elapsed(p->ev[2], p->ev[3]);
+            s.ms_update_eval += elapsed(p->ev[3], p->ev[4]);
+            HIPCHK(hipEventRecord(p->ev[5], p->stream));
+            double tempChi = p->h_fin[1];
+            last_chi = tempChi;
+            const bool ok2 = p->h_fin[3] == 0.0;
+            if (!ok2) { tempChi = std::numeric_limits<double>::max(); s.solve_failures++; }
+            rho = currentChi - tempChi;
+            const double scale = p->h_fin[2] + 1e-3;
+            rho /= scale;
+            if (rho > 0 && std::isfinite(tempChi)) {
+                double alpha = 1. - std::pow((2 * rho - 1), 3);
+                alpha = std::min(alpha, 2. / 3.);
+                const double sf = std::max(1. / 3., alpha);
+                p->lambda *= sf;
+                p->ni = 2;
+                currentChi = tempChi;
+                p->cur = 1 - p->cur;   // discardTop: the trial state becomes current
+            } else {
+                p->lambda *= p->ni;
+                p->ni *= 2;           // pop: keep the current state
+            }
+            qmax++;
+        } while (rho < 0 && qmax < p->cfg.max_trials && !(stop && *stop));
+        s.trials += qmax;
+        ++it;
+        result = LBA_RESULT_OK;
+        if (qmax == p->cfg.max_trials || rho == 0) result = LBA_RESULT_TERMINATE;
+        else if (p->cfg.early_stop) {
+            if ((iniChi - currentChi) * 1e3 < iniChi) p->nBad++;
+            else p->nBad = 0;
+            if (p->nBad >= 3) result = LBA_RESULT_TERMINATE;
+        }
+        p->linearized = false;
+        if (result != LBA_RESULT_OK && p->cfg.early_stop) break;
+    }
+    s.iterations = it;
+    s.result = result;
+    s.chi2_final = last_chi;
+    s.lambda_final = p->lambda;
+    s.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (st) *st = s;
+    return it;
+}
+
+int map_error(lba_problem* p, const HipError& e) {
+    if (p) p->err = std::string(e.what) + ": " + hipGetErrorString(e.e);
+    return LBA_E_HIP;
+}
+
+}  // namespace
+
+// ==================================================================================================
+// C ABI
+extern "C" {
+
+int lba_abi_version(void) { return LBA_ABI_VERSION; }
+
+int lba_create(lba_problem** out, const lba_config* cfg) {
+    if (!out || !cfg) return LBA_E_ARG;
+    *out = nullptr;
+    lba_problem* p = new lba_problem();
+    p->cfg = *cfg;
+    if (p->cfg.max_trials <= 0) p->cfg.max_trials = 10;
+    if (p->cfg.tau <= 0) p->cfg.tau = 1e-5;
+    try {
+        int ndev = 0;
+        HIPCHK(hipGetDeviceCount(&ndev));
+        if (cfg->device < 0 || cfg->device >= ndev) {
+            p->err = "invalid device";
+            delete p;
+            return LBA_E_ARG;
+        }
+        HIPCHK(hipSetDevice(cfg->device));
+        HIPCHK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+        for (auto& e : p->ev) HIPCHK(hipEventCreate(&e));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&p->h_fin), 4 * sizeof(double), hipHostMallocDefault));
+    } catch (const HipError& e) {
+        delete p;
+        return LBA_E_HIP;
+    }
+    *out = p;
+    return LBA_OK;
+}
+
+void lba_destroy(lba_problem* p) {
+    if (!p) return;
+    (void)hipSetDevice(p->cfg.device);
+    if (p->stream) (void)hipStreamSynchronize(p->stream);
+    free_all(p);
+    for (auto& e : p->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (p->h_fin) (void)hipHostFree(p->h_fin);
+    if (p->stream) (void)hipStreamDestroy(p->stream);
+    delete p;
+}
+
+const char* lba_last_error(const lba_problem* p) { return p ? p->err.c_str() : "null problem"; }
+
+int lba_pose_dim(const lba_problem* p) { return p && p->has_problem ? p->np : 0; }
+
+int lba_set_problem(lba_problem* p, const lba_kf* kfs, int32_t n_kf, const double* lm_xyz, int32_t n_lm,
+                    const lba_obs* obs, int32_t n_obs, const lba_prior* priors, int32_t n_priors,
+                    const int32_t* vel_kfs, int32_t n_vel, const lba_cam* cams, int32_t n_cam) {
+    if (!p) return LBA_E_ARG;
+    try {
+        HIPCHK(hipSetDevice(p->cfg.device));
+        return set_problem(p, kfs, n_kf, lm_xyz, n_lm, obs, n_obs, priors, n_priors, vel_kfs, n_vel, cams, n_cam);
+    } catch (const ApiError& e) {
+        p->err = e.msg;
+        free_all(p);
+        return e.code;
+    } catch (const HipError& e) {
+        free_all(p);
+        return map_error(p, e);
+    }
+}
+
+int lba_optimize(lba_problem* p, int32_t iters, volatile const int32_t* stop_flag, lba_stats* out) {
+    if (!p) return LBA_E_ARG;
+    try {
+        HIPCHK(hipSetDevice(p->cfg.device));
+        return optimize(p, iters, stop_flag, out);
+    } catch (const ApiError& e) {
+        p->err = e.msg;
+        return e.code;
+    } catch (const HipError& e) {
+        return map_error(p, e);
+    }
+}
+
+int lba_get_state(lba_problem* p, lba_kf* kf_out, double* lm_out) {
+    if (!p || !p->has_problem) return LBA_E_ARG;
+    try {
+        HIPCHK(hipSetDevice(p->cfg.device));
+        std::vector<double> kst(KF_STRIDE * (size_t)std::max(p->n_kf, 1)), lst(3 * (size_t)std::max(p->n_lm_dev, 1));
+        HIPCHK(hipMemcpyAsync(kst.data(), p->kst[p->cur], KF_STRIDE * (size_t)p->n_kf * sizeof(double),
+                              hipMemcpyDeviceToHost, p->stream));
+        HIPCHK(hipMemcpyAsync(lst.data(), p->lst[p->cur], 3 * (size_t)p->n_lm_dev * sizeof(double),
+                              hipMemcpyDeviceToHost, p->stream));
+        HIPCHK(hipStreamSynchronize(p->stream));
+        if (kf_out)
+            for (int k = 0; k < p->n_kf; ++k) {
+                const double* s = kst.data() + KF_STRIDE * k;
+                lba_kf& o = kf_out[k];
+                for (int i = 0; i < 4; ++i) o.q[i] = s[i];
+                for (int i = 0; i < 3; ++i) o.t[i] = s[4 + i];
+                for (int i = 0; i < 6; ++i) o.vel[i] = s[7 + i];
+                o.time = s[13];
+                o.bf = s[14];
+                o.fixed = p->kf_fixed[k];
+                o.pad = 0;
+            }
+        if (lm_out)
+            for (int l = 0; l < p->n_lm; ++l) {
+                const int d = p->lm_dev[l];
+                for (int i = 0; i < 3; ++i) lm_out[3 * (size_t)l + i] = d >= 0 ? lst[3 * (size_t)d + i] : p->lm_host[3 * (size_t)l + i];
+            }
+        return LBA_OK;
+    } catch (const HipError& e) {
+        return map_error(p, e);
+    }
+}
+
+int lba_set_state(lba_problem* p, const lba_kf* kf_in, const double* lm_xyz) {
+    if (!p || !p->has_problem) return LBA_E_ARG;
+    try {
+        HIPCHK(hipSetDevice(p->cfg.device));
+        if (kf_in) {
+            std::vector<double> kst(KF_STRIDE * (size_t)std::max(p->n_kf, 1), 0.0);
+            for (int k = 0; k < p->n_kf; ++k) {
+                double* o = kst.data() + KF_STRIDE * k;
+                normalize_q(kf_in[k].q, o);
+                for (int i = 0; i < 3; ++i) o[4 + i] = kf_in[k].t[i];
+                for (int i = 0; i < 6; ++i) o[7 + i] = kf_in[k].vel[i];
+                o[13] = kf_in[k].time;
+                o[14] = kf_in[k].bf;
+            }
+            HIPCHK(hipMemcpyAsync(p->kst[p->cur], kst.data(), KF_STRIDE * (size_t)p->n_kf * sizeof(double),
+                                  hipMemcpyHostToDevice, p->stream));
+            HIPCHK(hipStreamSynchronize(p->stream));
+        }
+        if (lm_xyz) {
+            std::vector<double> lst(3 * (size_t)std::max(p->n_lm_dev, 1));
+            for (int d = 0; d < p->n_lm_dev; ++d)
+                for (int i = 0; i < 3; ++i) lst[3 * (size_t)d + i] = lm_xyz[3 * (size_t)p->lm_orig[d] + i];
+            for (int l = 0; l < p->n_lm; ++l)
+                for (int i = 0; i < 3; ++i) p->lm_host[3 * (size_t)l + i] = lm_xyz[3 * (size_t)l + i];
+            HIPCHK(hipMemcpyAsync(p->lst[p->cur], lst.data(), 3 * (size_t)p->n_lm_dev * sizeof(double),
+                                  hipMemcpyHostToDevice, p->stream));
+            HIPCHK(hipStreamSynchronize(p->stream));
+        }
+        p->linearized = false;
+        return LBA_OK;
+    } catch (const HipError& e) {
+        return map_error(p, e);
+    }
+}
+
+int lba_eval(lba_problem* p, double* chi2_robust, double* obs_chi2, uint8_t* depth_ok) {
+    if (!p || !p->has_problem) return LBA_E_ARG;
+    try {
+        HIPCHK(hipSetDevice(p->cfg.device));
+        const double chi = eval_current(p);
+        if (chi2_robust) *chi2_robust = chi;
+        if (obs_chi2 && p->n_obs) {
+            std::vector<double> c(p->n_obs);
+            HIPCHK(hipMemcpy(c.data(), p->D.ob_chi2, p->n_obs * sizeof(double), hipMemcpyDeviceToHost));
+            for (int i = 0; i < p->n_obs; ++i) obs_chi2[i] = c[p->obs_dev[i]];
+        }
+        if (depth_ok && p->n_obs) {
+            unsigned char* d = nullptr;
+            HIPCHK(hipMalloc(&d, p->n_obs));
+            launch_depth(p->D, p->kst[p->cur], p->lst[p->cur], d, p->stream);
+            std::vector<unsigned char> h(p->n_obs);
+            HIPCHK(hipMemcpyAsync(h.data(), d, p->n_obs, hipMemcpyDeviceToHost, p->stream));
+            HIPCHK(hipStreamSynchronize(p->stream));
+            (void)hipFree(d);
+            for (int i = 0; i < p->n_obs; ++i) depth_ok[i] = h[p->obs_dev[i]];
+        }
+        return LBA_OK;
+    } catch (const HipError& e) {
+        return map_error(p, e);
+    }
+}
+
+int lba_linearize(lba_problem* p, double* residuals, double* H_pp, double* b, double* H_ll) {
+    if (!p || !p->has_problem) return LBA_E_ARG;
+    try {
+        HIPCHK(hipSetDevice(p->cfg.device));
+        const DevProblem& D = p->D;
+        linearize(p, residuals ? 1 : 0);
+        launch_assemble(D, 0.0, ASM_FULL, p->stream);
+        HIPCHK(hipGetLastError());
+        const int np = p->np, nl = D.n_lm;
+        std::vector<double> bp(np + 1), bl(3 * (size_t)nl + 1), hll(9 * (size_t)nl + 1), res(3 * (size_t)p->n_obs + 1);
+        if (H_pp && np)
+            HIPCHK(hipMemcpyAsync(H_pp, D.S, (size_t)np * np * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+        HIPCHK(hipMemcpyAsync(bp.data(), D.bp, np * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+        HIPCHK(hipMemcpyAsync(bl.data(), D.bl, 3 * (size_t)nl * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+        HIPCHK(hipMemcpyAsync(hll.data(), D.Hll, 9 * (size_t)nl * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+        if (residuals)
+            HIPCHK(hipMemcpyAsync(res.data(), D.ob_res, 3 * (size_t)p->n_obs * sizeof(double), hipMemcpyDeviceToHost,
+                                  p->stream));
+        HIPCHK(hipStreamSynchronize(p->stream));
+        if (b) {
+            for (int i = 0; i < np; ++i) b[i] = bp[i];
+            int r = 0;   // landmarks in g2o order: active ones, original array order
+            for (int l = 0; l < p->n_lm; ++l) {
+                const int d = p->lm_dev[l];
+                if (d < 0) continue;
+                for (int i = 0; i < 3; ++i) b[np + 3 * r + i] = bl[3 * (size_t)d + i];
+                ++r;
+            }
+        }
+        if (H_ll)
+            for (int l = 0; l < p->n_lm; ++l) {
+                const int d = p->lm_dev[l];
+                for (int i = 0; i < 9; ++i) H_ll[9 * (size_t)l + i] = d >= 0 ? hll[9 * (size_t)d + i] : 0.0;
+            }
+        if (residuals)
+            for (int i = 0; i < p->n_obs; ++i)
+                for (int d = 0; d < 3; ++d) residuals[3 * (size_t)i + d] = res[3 * (size_t)p->obs_dev[i] + d];
+        return np;
+    } catch (const HipError& e) {
+        return map_error(p, e);
+    }
+}
+
+int lba_solve_step(lba_problem* p, double lambda, double* dx) {
+    if (!p || !p->has_problem) return LBA_E_ARG;
+    try {
+        HIPCHK(hipSetDevice(p->cfg.device));
+        if (!p->linearized) linearize(p, 0);
+        trial(p, lambda, false, nullptr);
+        const int np = p->np, nl = p->D.n_lm;
+        if (p->h_fin[3] != 0.0) {
+            p->err = "reduced camera system not positive definite";
+            return LBA_E_SOLVE;
+        }
+        if (dx) {
+            std::vector<double> x(np + 3 * (size_t)nl + 1);
+            HIPCHK(hipMemcpy(x.data(), p->D.x, (np + 3 * (size_t)nl) * sizeof(double), hipMemcpyDeviceToHost));
+            for (int i = 0; i < np; ++i) dx[i] = x[i];
+            int r = 0;
+            for (int l = 0; l < p->n_lm; ++l) {
+                const int d = p->lm_dev[l];
+                if (d < 0) continue;
+                for (int i = 0; i < 3; ++i) dx[np + 3 * r + i] = x[np + 3 * (size_t)d + i];
+                ++r;
+            }
+        }
+        return LBA_OK;
+    } catch (const HipError& e) {
+        return map_error(p, e);
+    }
+}
+
+}  // extern "C"

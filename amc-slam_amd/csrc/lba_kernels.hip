@@ -1,0 +1,786 @@
+// lba_kernels.hip — gfx950 kernels of the GP local bundle adjustment (fp64 throughout).
+//
+// One LM trial (OptimizationAlgorithmLevenberg::solve, optimization_algorithm_levenberg.cpp:61-169)
+// maps to:
+//   k_pair_prep      per (prev KF, KF) GP quantities + per-KF rotations       (GaussianProcess.cc:23-42)
+//   k_linearize      per tile of landmarks: residual, Huber, analytic J straight into an LDS row
+//                    buffer, then deterministic on-chip reductions into Hpp/b segment partials,
+//                    Hpl blocks and Hll/bl (BlockSolver::buildSystem, block_solver.hpp:502-560;
+//                    edge quadratic forms base_multi_edge.hpp:170-222)
+//   k_prior_lin      EdgeGaussianPrior / EdgeVelocity quadratic forms (src/G2oTypes.cc:100-118)
+//   k_schur_prep     Dinv = (Hll + lambda I)^-1, V = Hpl Dinv, g = V bl      (block_solver.hpp:381-401)
+//   k_schur          per tile: S partials V(k1) Hpl(k2)^T for every KF pair   (block_solver.hpp:403-430)
+//   k_assemble       S = Hpp + lambda I - sum partials, bS = b_p - sum g     (block_solver.hpp:432-445)
+//   k_chol_*         blocked Cholesky + forward/back substitution of S     (linear_solver_dense.h:65-113)
+//   k_update         landmark back-substitution + oplus into the trial state (block_solver.hpp:461-482,
+//                    sparse_optimizer.cpp:422-435) + computeScale partials
+//   k_eval           residuals / robust chi2 of the trial state           (sparse_optimizer.cpp:61-114)
+// All cross-workgroup sums are written as per-workgroup partials and reduced in a fixed order, so
+// results are bitwise reproducible run to run (no floating-point atomics).
+#include "lba_device.hpp"
+#include "lba_math.hpp"
+#include "../../include/amc_lba.h"
+
+namespace lba {
+
+static_assert(sizeof(GPPair) == GPP_STRIDE * sizeof(double), "GPPair layout drifted");
+
+__device__ __forceinline__ SE3 load_se3(const double* k) {
+    SE3 T;
+    T.q = Quat{k[0], k[1], k[2], k[3]};
+    T.t[0] = k[4]; T.t[1] = k[5]; T.t[2] = k[6];
+    return T;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    return v;
+}
+
+// deterministic block sum (blockDim multiple of 64, <= 1024); valid in thread 0
+template <int NT>
+__device__ __forceinline__ double block_sum(double v, double* red) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    double s = 0.0;
+    if (threadIdx.x == 0)
+        for (int w = 0; w < NT / 64; ++w) s += red[w];
+    return s;
+}
+
+__device__ __forceinline__ void load_cam(const double* c, CamD* d) {
+    for (int i = 0; i < 9; ++i) d->Rcb[i] = c[i];
+    d->tcb[0] = c[9]; d->tcb[1] = c[10]; d->tcb[2] = c[11];
+    d->fx = c[12]; d->fy = c[13]; d->cx = c[14]; d->cy = c[15];
+}
+
+// Pose of the body at the observation time: GP interpolation between (kf_a, kf_b) for GP edges,
+// the KF pose otherwise.  Returns the stereo bf of the edge's first KF vertex.
+__device__ __forceinline__ double obs_pose(const DevProblem& P, const double* kst, int o, bool gp, ObsPose* op,
+                                           GPScalars* g, const GPPair** pp) {
+    if (gp) {
+        const GPPair* q = reinterpret_cast<const GPPair*>(P.gpp + (size_t)P.ob_gp[o] * GPP_STRIDE);
+        *g = gp_scalars(q->t1, q->t2, P.ob_t[o]);
+        gp_pose(*q, *g, op);
+        *pp = q;
+        return kst[(size_t)P.ob_kfa[o] * KF_STRIDE + 14];
+    }
+    const int k = P.ob_kfb[o];
+    const double* kp = P.kfp_pose + (size_t)k * KFP_STRIDE;
+    for (int i = 0; i < 9; ++i) op->Rwb[i] = kp[i];
+    op->twb[0] = kp[9]; op->twb[1] = kp[10]; op->twb[2] = kp[11];
+    for (int i = 0; i < 6; ++i) op->xi[i] = 0.0;
+    *g = GPScalars{0.0, 0.0, 0.0};
+    *pp = nullptr;
+    return kst[(size_t)k * KF_STRIDE + 14];
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ void k_pair_prep(DevProblem P, const double* __restrict__ kst) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < P.n_gp) {
+        const double* ka = kst + (size_t)P.gp_kfa[i] * KF_STRIDE;
+        const double* kb = kst + (size_t)P.gp_kfb[i] * KF_STRIDE;
+        gp_pair_build(load_se3(ka), ka + 7, load_se3(kb), kb + 7, ka[13], kb[13],
+                      reinterpret_cast<GPPair*>(P.gpp + (size_t)i * GPP_STRIDE));
+    } else if (i < P.n_gp + P.n_kf) {
+        const int k = i - P.n_gp;
+        const double* kk = kst + (size_t)k * KF_STRIDE;
+        double R[9];
+        qmat(Quat{kk[0], kk[1], kk[2], kk[3]}, R);
+        double* o = P.kfp_pose + (size_t)k * KFP_STRIDE;
+        for (int j = 0; j < 9; ++j) o[j] = R[j];
+        o[9] = kk[4]; o[10] = kk[5]; o[11] = kk[6];
+    }
+}
+
+// upper-triangle 4x4 output blocks (bi <= bj) of the 25-column row [Ja Jb e]: bi <= 5, bj <= 6
+__constant__ unsigned char c_bi[27] = {0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5};
+__constant__ unsigned char c_bj[27] = {0, 1, 2, 3, 4, 5, 6, 1, 2, 3, 4, 5, 6, 2, 3, 4, 5, 6, 3, 4, 5, 6, 4, 5, 6, 5, 6};
+
+__global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, const double* __restrict__ kst,
+                                                        const double* __restrict__ lst, int write_res) {
+    __shared__ double rows[TILE_ROWS * ROW_STRIDE];
+    __shared__ double rw[TILE_ROWS];
+    __shared__ double part[4 * 32 * 16];
+    __shared__ double red[TILE_OBS / 64];
+    const int tile = blockIdx.x, tid = threadIdx.x;
+    const int obs0 = P.tile_obs0[tile], nobs = P.tile_nobs[tile];
+
+    // ---- phase 1: one observation per lane: residual, robust weight, Jacobian rows -> LDS
+    double rho0 = 0.0;
+    if (tid < nobs) {
+        const int o = obs0 + tid;
+        const int meta = P.ob_meta[o];
+        const int kind = meta & 15, cam = meta >> 4;
+        const int dim = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? 3 : 2;
+        const bool gp = kind <= LBA_STEREO_GP;
+        CamD cd;
+        load_cam(P.camd + (size_t)cam * CAMD_STRIDE, &cd);
+        ObsPose op;
+        GPScalars g;
+        const GPPair* pp;
+        const double bf = obs_pose(P, kst, o, gp, &op, &g, &pp);
+        const double* Xw = lst + (size_t)P.ob_lm[o] * 3;
+        const double z[3] = {P.ob_z[3 * o], P.ob_z[3 * o + 1], P.ob_z[3 * o + 2]};
+        const double w = P.ob_w[o];
+        double Xb[3], Xc[3], e[3];
+        project_residual(op, cd, Xw, z, bf, dim, Xb, Xc, e);
+        double chi = 0.0;
+        for (int d = 0; d < dim; ++d) chi += e[d] * (w * e[d]);
+        double r0, r1;
+        huber(chi, dim == 3 ? P.huber_stereo : P.huber_mono, &r0, &r1);
+        rho0 = r0;
+        const int row = P.ob_row[o];
+        double* R = rows + row * ROW_STRIDE;
+        obs_jacobian(op, cd, Xb, Xc, bf, dim, gp, pp, g, R, ROW_STRIDE, 25);
+        for (int d = 0; d < dim; ++d) {
+            R[d * ROW_STRIDE + 24] = e[d];
+            rw[row + d] = r1 * w;   // robustInformation = rho' * Omega (base_edge.h:96-102)
+        }
+        P.ob_chi2[o] = chi;
+        if (write_res)
+            for (int d = 0; d < 3; ++d) P.ob_res[3 * (size_t)o + d] = d < dim ? e[d] : 0.0;
+    }
+    const double tchi = block_sum<TILE_OBS>(rho0, red);
+    if (tid == 0) P.chi_lin[tile] = tchi;
+    __syncthreads();
+
+    // ---- phase 2: Hpp / b_p partial per pose-pair segment: H += s r r^T over the segment's rows
+    const int seg0 = P.tile_seg0[tile], nseg = P.tile_nseg[tile];
+    const int blk = tid & 31, rg = tid >> 5;
+    const bool act = blk < 27;
+    const int bi = act ? c_bi[blk] : 0, bj = act ? c_bj[blk] : 0;
+    for (int si = 0; si < nseg; ++si) {
+        const int sg = seg0 + si;
+        const int r0 = P.seg_row0[sg], nr = P.seg_nrows[sg];
+        double acc[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] = 0.0;
+        if (act) {
+            for (int r = r0 + rg; r < r0 + nr; r += 4) {
+                const double* Rr = rows + r * ROW_STRIDE;
+                const double s = rw[r];
+                double a[4], c[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) a[k] = s * Rr[4 * bi + k];
+#pragma unroll
+                for (int l = 0; l < 4; ++l) c[l] = (4 * bj + l <= 24) ? Rr[4 * bj + l] : 0.0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int l = 0; l < 4; ++l) acc[k * 4 + l] += a[k] * c[l];
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) part[(rg * 32 + blk) * 16 + q] = acc[q];
+        }
+        __syncthreads();
+        double* E = P.slab + (size_t)sg * ENTRY;
+        for (int out = tid; out < 27 * 16; out += TILE_OBS) {
+            const int b = out >> 4, q = out & 15;
+            const double v = part[(0 * 32 + b) * 16 + q] + part[(1 * 32 + b) * 16 + q] +
+                             part[(2 * 32 + b) * 16 + q] + part[(3 * 32 + b) * 16 + q];
+            const int i = 4 * c_bi[b] + (q >> 2), j = 4 * c_bj[b] + (q & 3);
+            if (j == 24) {
+                if (i < 12) E[E_GA + i] = -v;           // b = -J^T rho' Omega e
+                else if (i < 24) E[E_GB + i - 12] = -v;
+            } else if (j < 24 && i <= j) {
+                if (j < 12) { E[E_AA + i * 12 + j] = v; E[E_AA + j * 12 + i] = v; }
+                else if (i >= 12) { E[E_BB + (i - 12) * 12 + (j - 12)] = v; E[E_BB + (j - 12) * 12 + (i - 12)] = v; }
+                else E[E_AB + i * 12 + (j - 12)] = v;
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- phase 3: Hpl per (KF, landmark) pair, deterministic row lists
+    const int pair0 = P.tile_pair0[tile], npair = P.tile_npair[tile];
+    for (int task = tid; task < npair * 3; task += TILE_OBS) {
+        const int p = pair0 + task / 3, sb = task % 3;
+        double acc[12];
+#pragma unroll
+        for (int q = 0; q < 12; ++q) acc[q] = 0.0;
+        for (int q = P.pair_r0[p]; q < P.pair_r0[p + 1]; ++q) {
+            const int code = P.pair_rows[q];
+            const int r = code & 0xffff, side = code >> 16;
+            const double* Rr = rows + r * ROW_STRIDE;
+            const double s = rw[r];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const double ji = s * Rr[side * 12 + 4 * sb + i];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) acc[i * 3 + a] += ji * Rr[25 + a];
+            }
+        }
+        double* H = P.Hpl + (size_t)p * 36 + 12 * sb;
+#pragma unroll
+        for (int q = 0; q < 12; ++q) H[q] = acc[q];
+    }
+    // ---- phase 4: Hll / bl per landmark
+    const int lm0 = P.tile_lm0[tile], nlm = P.tile_nlm[tile];
+    for (int t = tid; t < nlm; t += TILE_OBS) {
+        const int l = lm0 + t;
+        double H[9], b[3];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) H[q] = 0.0;
+        b[0] = b[1] = b[2] = 0.0;
+        for (int q = P.lm_r0[l]; q < P.lm_r0[l + 1]; ++q) {
+            const double* Rr = rows + P.lm_rows[q] * ROW_STRIDE;
+            const double s = rw[P.lm_rows[q]];
+            const double e = Rr[24];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const double sa = s * Rr[25 + a];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) H[a * 3 + c] += sa * Rr[25 + c];
+                b[a] -= sa * e;
+            }
+        }
+        for (int q = 0; q < 9; ++q) P.Hll[(size_t)l * 9 + q] = H[q];
+        for (int q = 0; q < 3; ++q) P.bl[(size_t)l * 3 + q] = b[q];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_prior_lin(DevProblem P, const double* __restrict__ kst) {
+    __shared__ double Ji[144], Jj[144], WJi[144], WJj[144], Om[144], e[12], We[12];
+    __shared__ double wsh;
+    const int idx = blockIdx.x, tid = threadIdx.x;
+    double* E = P.slab + (size_t)(P.pri_entry0 + idx) * ENTRY;
+    if (idx < P.n_prior) {
+        if (tid == 0) {
+            const double* ka = kst + (size_t)P.pri_a[idx] * KF_STRIDE;
+            const double* kb = kst + (size_t)P.pri_b[idx] * KF_STRIDE;
+            prior_error_jac(load_se3(ka), ka + 7, ka[13], load_se3(kb), kb + 7, kb[13], e, Ji, Jj);
+            qi_inv(P.qcinv, kb[13] - ka[13], Om);
+            double chi = 0.0;
+            for (int i = 0; i < 12; ++i) {
+                double s = 0.0;
+                for (int k = 0; k < 12; ++k) s += Om[i * 12 + k] * e[k];
+                chi += e[i] * s;
+            }
+            double r0 = chi, r1 = 1.0;
+            if (P.huber_prior > 0) huber(chi, P.huber_prior, &r0, &r1);
+            P.chi_lin[P.n_tiles + idx] = r0;
+            wsh = r1;
+        }
+        __syncthreads();
+        const double w1 = wsh;
+        for (int t = tid; t < 288; t += 64) {
+            const int which = t / 144, ij = t % 144, i = ij / 12, j = ij % 12;
+            const double* J = which ? Jj : Ji;
+            double s = 0.0;
+            for (int k = 0; k < 12; ++k) s += Om[i * 12 + k] * J[k * 12 + j];
+            (which ? WJj : WJi)[ij] = w1 * s;
+        }
+        if (tid < 12) {
+            double s = 0.0;
+            for (int k = 0; k < 12; ++k) s += Om[tid * 12 + k] * e[k];
+            We[tid] = w1 * s;
+        }
+        __syncthreads();
+        for (int t = tid; t < ENTRY; t += 64) {
+            if (t < 432) {
+                const int bk = t / 144, ij = t % 144, i = ij / 12, j = ij % 12;
+                const double* A = (bk == 2) ? Jj : Ji;
+                const double* B = (bk == 0) ? WJi : WJj;
+                double s = 0.0;
+                for (int k = 0; k < 12; ++k) s += A[k * 12 + i] * B[k * 12 + j];
+                E[t] = s;
+            } else {
+                const int side = (t - 432) / 12, i = (t - 432) % 12;
+                const double* A = side ? Jj : Ji;
+                double s = 0.0;
+                for (int k = 0; k < 12; ++k) s += A[k * 12 + i] * We[k];
+                E[t] = -s;
+            }
+        }
+    } else {
+        // EdgeVelocity: e = Vel(2), J = [0_6, e_2^T], info QcInv(2,2) (include/G2oTypes.h:496-519)
+        const int v = idx - P.n_prior;
+        const double ev = kst[(size_t)P.vel_kf[v] * KF_STRIDE + 7 + 2];
+        const double q22 = P.qcinv[2 * 6 + 2];
+        for (int t = tid; t < ENTRY; t += 64) E[t] = 0.0;
+        __syncthreads();
+        if (tid == 0) {
+            E[E_BB + 8 * 12 + 8] = q22;
+            E[E_GB + 8] = -q22 * ev;
+            P.chi_lin[P.n_tiles + idx] = ev * (q22 * ev);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_schur_prep(DevProblem P, double lambda) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n_pairs + P.n_lm) return;
+    const int l = i < P.n_pairs ? P.pair_lm[i] : i - P.n_pairs;
+    double H[9], D[9];
+    for (int q = 0; q < 9; ++q) H[q] = P.Hll[(size_t)l * 9 + q];
+    H[0] += lambda; H[4] += lambda; H[8] += lambda;   // setLambda on Hll (block_solver.hpp:580-587)
+    inv3(H, D);
+    if (i >= P.n_pairs) {
+        for (int q = 0; q < 9; ++q) P.Dinv[(size_t)l * 9 + q] = D[q];
+        return;
+    }
+    const double* B = P.Hpl + (size_t)i * 36;
+    double* Vo = P.V + (size_t)i * 36;
+    const double b0 = P.bl[3 * (size_t)l], b1 = P.bl[3 * (size_t)l + 1], b2 = P.bl[3 * (size_t)l + 2];
+    for (int r = 0; r < 12; ++r) {
+        const double h0 = B[r * 3], h1 = B[r * 3 + 1], h2 = B[r * 3 + 2];
+        const double v0 = h0 * D[0] + h1 * D[3] + h2 * D[6];
+        const double v1 = h0 * D[1] + h1 * D[4] + h2 * D[7];
+        const double v2 = h0 * D[2] + h1 * D[5] + h2 * D[8];
+        Vo[r * 3] = v0; Vo[r * 3 + 1] = v1; Vo[r * 3 + 2] = v2;
+        P.gpair[(size_t)i * 12 + r] = v0 * b0 + v1 * b1 + v2 * b2;
+    }
+}
+
+__global__ __launch_bounds__(128) void k_schur(DevProblem P) {
+    __shared__ double Vs[TILE_PAIRS * 36];
+    __shared__ double Hs[TILE_PAIRS * 36];
+    __shared__ short slot[TILE_LMS * TILE_KF];
+    __shared__ int kfl[TILE_KF];
+    const int tile = blockIdx.x, tid = threadIdx.x;
+    const int pair0 = P.tile_pair0[tile], npair = P.tile_npair[tile];
+    const int lm0 = P.tile_lm0[tile], nlm = P.tile_nlm[tile];
+    const int kf0 = P.tile_kf0[tile], nkf = P.tile_nkf[tile];
+    for (int t = tid; t < npair * 36; t += 128) {
+        Vs[t] = P.V[(size_t)pair0 * 36 + t];
+        Hs[t] = P.Hpl[(size_t)pair0 * 36 + t];
+    }
+    for (int t = tid; t < TILE_LMS * TILE_KF; t += 128) slot[t] = -1;
+    if (tid < nkf) kfl[tid] = P.tkf_list[kf0 + tid];
+    __syncthreads();
+    for (int t = tid; t < npair; t += 128) {
+        const int p = pair0 + t, m = P.pair_lm[p] - lm0, k = P.pair_kf[p];
+        for (int l = 0; l < nkf; ++l)
+            if (kfl[l] == k) slot[m * TILE_KF + l] = (short)t;
+    }
+    __syncthreads();
+    const int sent0 = P.tile_sent0[tile], nsent = P.tile_nsent[tile];
+    for (int task = tid; task < nsent * 9; task += 128) {
+        const int e = task / 9, sub = task % 9, sr = sub / 3, sc = sub % 3;
+        const int l1 = P.sent_l1[sent0 + e], l2 = P.sent_l2[sent0 + e];
+        double acc[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] = 0.0;
+        for (int m = 0; m < nlm; ++m) {
+            const int s1 = slot[m * TILE_KF + l1], s2 = slot[m * TILE_KF + l2];
+            if (s1 < 0 || s2 < 0) continue;
+            const double* v = Vs + s1 * 36 + 12 * sr;
+            const double* h = Hs + s2 * 36 + 12 * sc;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int l = 0; l < 4; ++l)
+                    acc[k * 4 + l] += v[k * 3] * h[l * 3] + v[k * 3 + 1] * h[l * 3 + 1] + v[k * 3 + 2] * h[l * 3 + 2];
+        }
+        double* o = P.slab2 + (size_t)(sent0 + e) * 144;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int l = 0; l < 4; ++l) o[(4 * sr + k) * 12 + 4 * sc + l] = acc[k * 4 + l];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_assemble(DevProblem P, double lambda, int flags) {
+    const int b = blockIdx.x, t = threadIdx.x;
+    const int n = P.np;
+    if (b < P.n_ublocks) {
+        if (t >= 144) return;
+        const int bi = P.ublk_i[b], bj = P.ublk_j[b];
+        const int i = t / 12, j = t % 12;
+        double v = 0.0;
+        for (int q = P.hsrc0[b]; q < P.hsrc0[b + 1]; ++q) {
+            const int code = P.hsrc[q];
+            const double* E = P.slab + (size_t)(code >> 2) * ENTRY;
+            switch (code & 3) {
+                case R_AA: v += E[E_AA + i * 12 + j]; break;
+                case R_BB: v += E[E_BB + i * 12 + j]; break;
+                case R_AB: v += E[E_AB + i * 12 + j]; break;
+                default: v += E[E_AB + j * 12 + i]; break;
+            }
+        }
+        if (bi == bj && i == j) v += lambda;
+        if (flags & ASM_SCHUR)
+            for (int q = P.ssrc0[b]; q < P.ssrc0[b + 1]; ++q) v -= P.slab2[(size_t)P.ssrc[q] * 144 + i * 12 + j];
+        P.S[(size_t)(12 * bj + j) * n + 12 * bi + i] = v;
+        if (flags & ASM_FULL) P.S[(size_t)(12 * bi + i) * n + 12 * bj + j] = v;
+    } else {
+        const int k = b - P.n_ublocks;
+        if (t >= 12) return;
+        double v = 0.0;
+        for (int q = P.bsrc0[k]; q < P.bsrc0[k + 1]; ++q) {
+            const int code = P.bsrc[q];
+            v += P.slab[(size_t)(code >> 1) * ENTRY + ((code & 1) ? E_GB : E_GA) + t];
+        }
+        P.bp[12 * k + t] = v;
+        if (flags & ASM_SCHUR)
+            for (int q = P.kfp0[k]; q < P.kfp0[k + 1]; ++q) v -= P.gpair[(size_t)P.kfp[q] * 12 + t];
+        P.xsol[12 * k + t] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Dense Cholesky S = L L^T (lower, row-major, in place), with the forward substitution of the
+// right-hand side folded into the panels.  A non-positive pivot sets *info (LDLT !isPositive).
+constexpr int PANEL_ROWS = 64;
+
+__global__ __launch_bounds__(64) void k_chol_panel(double* __restrict__ A, int n, int p, int nbp, int* info,
+                                                   double* __restrict__ b) {
+    __shared__ double L[CHOL_NB][CHOL_NB + 1];
+    const int tid = threadIdx.x, w = blockIdx.x;
+    for (int t = tid; t < CHOL_NB * CHOL_NB; t += 64) {
+        const int i = t / CHOL_NB, j = t % CHOL_NB;
+        L[i][j] = (i < nbp && j <= i) ? A[(size_t)(p + i) * n + p + j] : 0.0;
+    }
+    __syncthreads();
+    for (int j = 0; j < nbp; ++j) {
+        if (tid == 0) {
+            double d = L[j][j];
+            if (!(d > 0.0)) {
+                if (w == 0) *info = 1 + p + j;
+                d = 1.0;
+            }
+            L[j][j] = sqrt(d);
+        }
+        __syncthreads();
+        const double ljj = L[j][j];
+        for (int i = j + 1 + tid; i < nbp; i += 64) L[i][j] /= ljj;
+        __syncthreads();
+        const int m = nbp - j - 1;
+        for (int t = tid; t < m * m; t += 64) {
+            const int i = j + 1 + t / m, k = j + 1 + t % m;
+            if (k <= i) L[i][k] -= L[i][j] * L[k][j];
+        }
+        __syncthreads();
+    }
+    if (w == 0) {
+        for (int t = tid; t < nbp * nbp; t += 64) {
+            const int i = t / nbp, j = t % nbp;
+            if (j <= i) A[(size_t)(p + i) * n + p + j] = L[i][j];
+        }
+        if (tid == 0)
+            for (int i = 0; i < nbp; ++i) {
+                double s = b[p + i];
+                for (int k = 0; k < i; ++k) s -= L[i][k] * b[p + k];
+                b[p + i] = s / L[i][i];
+            }
+        return;
+    }
+    const int r = p + nbp + (w - 1) * PANEL_ROWS + tid;
+    if (r >= n) return;
+    double xr[CHOL_NB];
+    double* Ar = A + (size_t)r * n + p;
+#pragma unroll
+    for (int j = 0; j < CHOL_NB; ++j) xr[j] = j < nbp ? Ar[j] : 0.0;
+#pragma unroll
+    for (int j = 0; j < CHOL_NB; ++j) {
+        if (j < nbp) {
+            double s = xr[j];
+#pragma unroll
+            for (int k = 0; k < j; ++k) s -= xr[k] * L[j][k];
+            xr[j] = s / L[j][j];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < CHOL_NB; ++j)
+        if (j < nbp) Ar[j] = xr[j];
+}
+
+__global__ __launch_bounds__(256) void k_chol_update(double* __restrict__ A, int n, int p, int nbp, double* __restrict__ b) {
+    __shared__ double Li[32][CHOL_NB + 1], Lj[32][CHOL_NB + 1];
+    const int q = p + nbp;
+    const int bid = blockIdx.x;
+    int ti = (int)((sqrt(8.0 * bid + 1.0) - 1.0) * 0.5);
+    while ((ti + 1) * (ti + 2) / 2 <= bid) ++ti;
+    while (ti * (ti + 1) / 2 > bid) --ti;
+    const int tj = bid - ti * (ti + 1) / 2;
+    const int r0 = q + ti * 32, c0 = q + tj * 32;
+    const int tid = threadIdx.x;
+    for (int t = tid; t < 32 * CHOL_NB; t += 256) {
+        const int r = t / CHOL_NB, k = t % CHOL_NB;
+        Li[r][k] = (r0 + r < n && k < nbp) ? A[(size_t)(r0 + r) * n + p + k] : 0.0;
+        Lj[r][k] = (c0 + r < n && k < nbp) ? A[(size_t)(c0 + r) * n + p + k] : 0.0;
+    }
+    __syncthreads();
+    const int tr = tid >> 4, tc = tid & 15;
+    double a00 = 0, a01 = 0, a10 = 0, a11 = 0;
+#pragma unroll 8
+    for (int k = 0; k < CHOL_NB; ++k) {
+        const double x0 = Li[2 * tr][k], x1 = Li[2 * tr + 1][k];
+        const double y0 = Lj[2 * tc][k], y1 = Lj[2 * tc + 1][k];
+        a00 += x0 * y0; a01 += x0 * y1; a10 += x1 * y0; a11 += x1 * y1;
+    }
+    const int ra = r0 + 2 * tr, ca = c0 + 2 * tc;
+    if (ra < n) {
+        if (ca < n) A[(size_t)ra * n + ca] -= a00;
+        if (ca + 1 < n) A[(size_t)ra * n + ca + 1] -= a01;
+    }
+    if (ra + 1 < n) {
+        if (ca < n) A[(size_t)(ra + 1) * n + ca] -= a10;
+        if (ca + 1 < n) A[(size_t)(ra + 1) * n + ca + 1] -= a11;
+    }
+    if (ti == tj && tid < 32 && r0 + tid < n) {
+        double s = 0.0;
+        for (int k = 0; k < nbp; ++k) s += Li[tid][k] * b[p + k];
+        b[r0 + tid] -= s;
+    }
+}
+
+constexpr int CHOL_MAXN = 6144;
+
+// L^T x = y, single workgroup; x overwrites b
+__global__ __launch_bounds__(256) void k_chol_backsolve(const double* __restrict__ A, int n, double* __restrict__ b) {
+    __shared__ double y[CHOL_MAXN];
+    __shared__ double xb[32];
+    const int tid = threadIdx.x;
+    for (int t = tid; t < n; t += 256) y[t] = b[t];
+    __syncthreads();
+    const int nblk = (n + 31) / 32;
+    for (int blk = nblk - 1; blk >= 0; --blk) {
+        const int r0 = blk * 32, len = min(32, n - r0);
+        if (tid < 64) {
+            double yl = tid < len ? y[r0 + tid] : 0.0;
+            for (int i = len - 1; i >= 0; --i) {
+                const double xi = __shfl(yl, i, 64) / A[(size_t)(r0 + i) * n + r0 + i];
+                if (tid < i) yl -= A[(size_t)(r0 + i) * n + r0 + tid] * xi;
+                if (tid == i) yl = xi;
+            }
+            if (tid < len) xb[tid] = yl;
+        }
+        __syncthreads();
+        if (tid < len) b[r0 + tid] = xb[tid];
+        for (int k = tid; k < r0; k += 256) {
+            double s = 0.0;
+            for (int i = 0; i < len; ++i) s += A[(size_t)(r0 + i) * n + k] * xb[i];
+            y[k] -= s;
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+constexpr int UPD_THREADS = 256;
+
+__global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lambda, const double* __restrict__ kst,
+                                                        const double* __restrict__ lst, double* __restrict__ ko,
+                                                        double* __restrict__ lo) {
+    __shared__ double red[UPD_THREADS / 64];
+    const int i = blockIdx.x * UPD_THREADS + threadIdx.x;
+    const bool ok = (*P.info == 0);
+    double sc = 0.0;
+    if (i < P.n_kf) {
+        const double* kc = kst + (size_t)i * KF_STRIDE;
+        double* kn = ko + (size_t)i * KF_STRIDE;
+        const int h = P.kf_hidx[i];
+        if (h >= 0) {
+            // BlockSolver leaves x untouched when the factorisation fails; g2o then applies and pops it
+            double d[12];
+            for (int j = 0; j < 12; ++j) {
+                d[j] = ok ? P.xsol[12 * h + j] : P.x[12 * h + j];
+                if (ok) P.x[12 * h + j] = d[j];
+                sc += d[j] * (lambda * d[j] + P.bp[12 * h + j]);
+            }
+            const SE3 T = se3_mul(load_se3(kc), se3_exp(d));   // Twb <- Twb exp(dxi) (G2oTypes.cc:41-46)
+            kn[0] = T.q.x; kn[1] = T.q.y; kn[2] = T.q.z; kn[3] = T.q.w;
+            kn[4] = T.t[0]; kn[5] = T.t[1]; kn[6] = T.t[2];
+            for (int j = 0; j < 6; ++j) kn[7 + j] = kc[7 + j] + d[6 + j];
+            for (int j = 13; j < KF_STRIDE; ++j) kn[j] = kc[j];
+        } else {
+            for (int j = 0; j < KF_STRIDE; ++j) kn[j] = kc[j];
+        }
+    } else if (i < P.n_kf + P.n_lm) {
+        const int l = i - P.n_kf;
+        double xl[3];
+        double* xd = P.x + P.np + 3 * (size_t)l;
+        if (ok) {
+            double c[3] = {P.bl[3 * (size_t)l], P.bl[3 * (size_t)l + 1], P.bl[3 * (size_t)l + 2]};
+            for (int p = P.lm_pair0[l]; p < P.lm_pair0[l + 1]; ++p) {
+                const double* B = P.Hpl + (size_t)p * 36;
+                const double* xp = P.xsol + 12 * (size_t)P.pair_kf[p];
+                for (int r = 0; r < 12; ++r) {
+                    c[0] -= B[r * 3] * xp[r];
+                    c[1] -= B[r * 3 + 1] * xp[r];
+                    c[2] -= B[r * 3 + 2] * xp[r];
+                }
+            }
+            const double* D = P.Dinv + (size_t)l * 9;
+            for (int a = 0; a < 3; ++a) {
+                xl[a] = D[a * 3] * c[0] + D[a * 3 + 1] * c[1] + D[a * 3 + 2] * c[2];
+                xd[a] = xl[a];
+            }
+        } else {
+            xl[0] = xd[0]; xl[1] = xd[1]; xl[2] = xd[2];
+        }
+        for (int a = 0; a < 3; ++a) {
+            lo[3 * (size_t)l + a] = lst[3 * (size_t)l + a] + xl[a];
+            sc += xl[a] * (lambda * xl[a] + P.bl[3 * (size_t)l + a]);
+        }
+    }
+    const double s = block_sum<UPD_THREADS>(sc, red);
+    if (threadIdx.x == 0) P.scale_part[blockIdx.x] = s;
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(TILE_OBS) void k_eval(DevProblem P, const double* __restrict__ kst,
+                                                   const double* __restrict__ lst) {
+    __shared__ double red[TILE_OBS / 64];
+    const int tile = blockIdx.x, tid = threadIdx.x;
+    double rho0 = 0.0;
+    if (tid < P.tile_nobs[tile]) {
+        const int o = P.tile_obs0[tile] + tid;
+        const int meta = P.ob_meta[o];
+        const int kind = meta & 15, cam = meta >> 4;
+        const int dim = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? 3 : 2;
+        const bool gp = kind <= LBA_STEREO_GP;
+        CamD cd;
+        load_cam(P.camd + (size_t)cam * CAMD_STRIDE, &cd);
+        ObsPose op;
+        GPScalars g;
+        const GPPair* pp;
+        const double bf = obs_pose(P, kst, o, gp, &op, &g, &pp);
+        const double z[3] = {P.ob_z[3 * o], P.ob_z[3 * o + 1], P.ob_z[3 * o + 2]};
+        const double w = P.ob_w[o];
+        double Xb[3], Xc[3], e[3];
+        project_residual(op, cd, lst + (size_t)P.ob_lm[o] * 3, z, bf, dim, Xb, Xc, e);
+        double chi = 0.0;
+        for (int d = 0; d < dim; ++d) chi += e[d] * (w * e[d]);
+        double r0, r1;
+        huber(chi, dim == 3 ? P.huber_stereo : P.huber_mono, &r0, &r1);
+        rho0 = r0;
+        P.ob_chi2[o] = chi;
+    }
+    const double s = block_sum<TILE_OBS>(rho0, red);
+    if (tid == 0) P.chi_eval[tile] = s;
+}
+
+__global__ __launch_bounds__(64) void k_prior_eval(DevProblem P, const double* __restrict__ kst) {
+    const int idx = blockIdx.x * 64 + threadIdx.x;
+    if (idx < P.n_prior) {
+        const double* ka = kst + (size_t)P.pri_a[idx] * KF_STRIDE;
+        const double* kb = kst + (size_t)P.pri_b[idx] * KF_STRIDE;
+        double e[12], Om[144];
+        prior_error_jac<double>(load_se3(ka), ka + 7, ka[13], load_se3(kb), kb + 7, kb[13], e, nullptr, nullptr);
+        qi_inv(P.qcinv, kb[13] - ka[13], Om);
+        double chi = 0.0;
+        for (int i = 0; i < 12; ++i) {
+            double s = 0.0;
+            for (int k = 0; k < 12; ++k) s += Om[i * 12 + k] * e[k];
+            chi += e[i] * s;
+        }
+        double r0 = chi, r1 = 1.0;
+        if (P.huber_prior > 0) huber(chi, P.huber_prior, &r0, &r1);
+        P.chi_eval[P.n_tiles + idx] = r0;
+    } else if (idx < P.n_prior + P.n_vel) {
+        const int v = idx - P.n_prior;
+        const double ev = kst[(size_t)P.vel_kf[v] * KF_STRIDE + 9];
+        P.chi_eval[P.n_tiles + idx] = ev * (P.qcinv[14] * ev);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_finalize(DevProblem P) {
+    __shared__ double red[4];
+    const int tid = threadIdx.x;
+    const int nc = P.n_tiles + P.n_prior + P.n_vel;
+    double a = 0.0, b = 0.0, c = 0.0;
+    for (int i = tid; i < nc; i += 256) { a += P.chi_lin[i]; b += P.chi_eval[i]; }
+    for (int i = tid; i < P.n_upd_blocks; i += 256) c += P.scale_part[i];
+    const double sa = block_sum<256>(a, red);
+    __syncthreads();
+    const double sb = block_sum<256>(b, red);
+    __syncthreads();
+    const double sc = block_sum<256>(c, red);
+    if (tid == 0) {
+        P.fin[0] = sa;
+        P.fin[1] = sb;
+        P.fin[2] = sc;
+        P.fin[3] = (double)(*P.info);
+    }
+}
+
+// isDepthPositive (src/G2oTypes.cc:65-81): GP edges test both KF poses (include/G2oTypes.h:305-314)
+__global__ __launch_bounds__(256) void k_depth(DevProblem P, const double* __restrict__ kst,
+                                               const double* __restrict__ lst, unsigned char* ok) {
+    const int o = blockIdx.x * 256 + threadIdx.x;
+    if (o >= P.n_obs) return;
+    const int meta = P.ob_meta[o];
+    const int kind = meta & 15, cam = meta >> 4;
+    CamD cd;
+    load_cam(P.camd + (size_t)cam * CAMD_STRIDE, &cd);
+    const double* Xw = lst + (size_t)P.ob_lm[o] * 3;
+    int good = 1;
+    const int ks[2] = {P.ob_kfb[o], kind <= LBA_STEREO_GP ? P.ob_kfa[o] : -1};
+    for (int s = 0; s < 2; ++s) {
+        if (ks[s] < 0) continue;
+        const double* kp = P.kfp_pose + (size_t)ks[s] * KFP_STRIDE;
+        const double d[3] = {Xw[0] - kp[9], Xw[1] - kp[10], Xw[2] - kp[11]};
+        double Xb[3];
+        mul33tv(kp, d, Xb);
+        const double zc = cd.Rcb[6] * Xb[0] + cd.Rcb[7] * Xb[1] + cd.Rcb[8] * Xb[2] + cd.tcb[2];
+        if (!(zc > 0)) good = 0;
+    }
+    ok[o] = (unsigned char)good;
+}
+
+// ------------------------------------------------------------------------------------------------ launchers
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+void launch_pair_prep(const DevProblem& P, const double* kst, hipStream_t s) {
+    const int n = P.n_gp + P.n_kf;
+    if (n) hipLaunchKernelGGL(k_pair_prep, dim3(cdiv(n, 64)), dim3(64), 0, s, P, kst);
+}
+void launch_linearize(const DevProblem& P, const double* kst, const double* lst, int write_res, hipStream_t s) {
+    if (P.n_tiles) hipLaunchKernelGGL(k_linearize, dim3(P.n_tiles), dim3(TILE_OBS), 0, s, P, kst, lst, write_res);
+}
+void launch_prior_lin(const DevProblem& P, const double* kst, hipStream_t s) {
+    const int n = P.n_prior + P.n_vel;
+    if (n) hipLaunchKernelGGL(k_prior_lin, dim3(n), dim3(64), 0, s, P, kst);
+}
+void launch_schur_prep(const DevProblem& P, double lambda, hipStream_t s) {
+    const int n = P.n_pairs + P.n_lm;
+    if (n) hipLaunchKernelGGL(k_schur_prep, dim3(cdiv(n, 256)), dim3(256), 0, s, P, lambda);
+}
+void launch_schur(const DevProblem& P, hipStream_t s) {
+    if (P.n_tiles) hipLaunchKernelGGL(k_schur, dim3(P.n_tiles), dim3(128), 0, s, P);
+}
+void launch_assemble(const DevProblem& P, double lambda, int flags, hipStream_t s) {
+    const int n = P.n_ublocks + P.n_pb;
+    if (n) hipLaunchKernelGGL(k_assemble, dim3(n), dim3(256), 0, s, P, lambda, flags);
+}
+void launch_cholesky_solve(const DevProblem& P, hipStream_t s) {
+    const int n = P.np;
+    for (int p = 0; p < n; p += CHOL_NB) {
+        const int nbp = n - p < CHOL_NB ? n - p : CHOL_NB;
+        const int rest = n - p - nbp;
+        hipLaunchKernelGGL(k_chol_panel, dim3(1 + cdiv(rest, PANEL_ROWS)), dim3(64), 0, s, P.S, n, p, nbp, P.info,
+                           P.xsol);
+        if (rest > 0) {
+            const int nt = cdiv(rest, 32);
+            hipLaunchKernelGGL(k_chol_update, dim3(nt * (nt + 1) / 2), dim3(256), 0, s, P.S, n, p, nbp, P.xsol);
+        }
+    }
+    if (n) hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(256), 0, s, P.S, n, P.xsol);
+}
+void launch_update(const DevProblem& P, double lambda, const double* kst, const double* lst, double* kst_out,
+                   double* lst_out, hipStream_t s) {
+    hipLaunchKernelGGL(k_update, dim3(P.n_upd_blocks), dim3(UPD_THREADS), 0, s, P, lambda, kst, lst, kst_out, lst_out);
+}
+void launch_eval(const DevProblem& P, const double* kst, const double* lst, hipStream_t s) {
+    if (P.n_tiles) hipLaunchKernelGGL(k_eval, dim3(P.n_tiles), dim3(TILE_OBS), 0, s, P, kst, lst);
+    const int n = P.n_prior + P.n_vel;
+    if (n) hipLaunchKernelGGL(k_prior_eval, dim3(cdiv(n, 64)), dim3(64), 0, s, P, kst);
+}
+void launch_finalize(const DevProblem& P, hipStream_t s) {
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, P);
+}
+void launch_depth(const DevProblem& P, const double* kst, const double* lst, unsigned char* ok, hipStream_t s) {
+    if (P.n_obs) hipLaunchKernelGGL(k_depth, dim3(cdiv(P.n_obs, 256)), dim3(256), 0, s, P, kst, lst, ok);
+}
+
+}  // namespace lba

@@ -1,0 +1,550 @@
+// lba_math.hpp — fp64 Lie-group / GP / projection math for the MI355X local-BA kernels.
+//
+// Every function is LBA_HD (host+device) so the exact code the kernels run can also be
+// checked on the CPU against the oracle (tests/test_math_host.py builds a host harness).
+// Formulas follow the published algorithms the reference uses:
+//   Sophus SO3/SE3 (Thirdparty/Sophus/sophus/so3.hpp:247-290,297-303,325-339,358-367,583-618;
+//   se3.hpp:103-111,208-211,223-252,304-308,761-781; epsilon 1e-10 common.hpp:94),
+//   Pose3utils (src/Pose3utils.cc:5-73,111-119), Pinhole (src/CameraModels/Pinhole.cpp:35-81).
+// The GP interpolation uses the closed form of QueryPose's 12x12 products
+// (src/GaussianProcess.cc:5-42): Pt1 = [l1 I, l2 I], At1 = [(1-l1) I, p2 I] with
+// s = tau/T, l1 = 3s^2 - 2s^3, l2 = tau^2 (tau - T)/T^2, p2 = tau (1 - s)^2.
+// Storage is row-major; tangent order is [translation; rotation].
+#pragma once
+
+#include <math.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define LBA_HD __host__ __device__ __forceinline__
+#else
+#define LBA_HD static inline
+#endif
+
+namespace lba {
+
+constexpr double kEps = 1e-10;   // Sophus::Constants<double>::epsilon()
+
+struct Quat { double x, y, z, w; };
+
+// ---------------------------------------------------------------- small dense helpers
+LBA_HD void hat3(const double* w, double* H) {
+    H[0] = 0.0;   H[1] = -w[2]; H[2] = w[1];
+    H[3] = w[2];  H[4] = 0.0;   H[5] = -w[0];
+    H[6] = -w[1]; H[7] = w[0];  H[8] = 0.0;
+}
+LBA_HD void mul33(const double* A, const double* B, double* C) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            C[i * 3 + j] = A[i * 3 + 0] * B[0 * 3 + j] + A[i * 3 + 1] * B[1 * 3 + j] + A[i * 3 + 2] * B[2 * 3 + j];
+}
+LBA_HD void mul33v(const double* A, const double* v, double* o) {
+    o[0] = A[0] * v[0] + A[1] * v[1] + A[2] * v[2];
+    o[1] = A[3] * v[0] + A[4] * v[1] + A[5] * v[2];
+    o[2] = A[6] * v[0] + A[7] * v[1] + A[8] * v[2];
+}
+LBA_HD void mul33tv(const double* A, const double* v, double* o) {   // A^T v
+    o[0] = A[0] * v[0] + A[3] * v[1] + A[6] * v[2];
+    o[1] = A[1] * v[0] + A[4] * v[1] + A[7] * v[2];
+    o[2] = A[2] * v[0] + A[5] * v[1] + A[8] * v[2];
+}
+// C[m x n] = A[m x k] * B[k x n]
+LBA_HD void matmul(const double* A, const double* B, double* C, int m, int k, int n) {
+    for (int i = 0; i < m; ++i)
+        for (int j = 0; j < n; ++j) {
+            double s = 0.0;
+            for (int l = 0; l < k; ++l) s += A[i * k + l] * B[l * n + j];
+            C[i * n + j] = s;
+        }
+}
+
+// ---------------------------------------------------------------- SO3 (unit quaternion)
+LBA_HD Quat qnormalize(Quat q) {
+    const double len = sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    return Quat{q.x / len, q.y / len, q.z / len, q.w / len};
+}
+// Sophus SO3 product: Hamilton product, then normalisation by the SO3 constructor
+LBA_HD Quat qmul(const Quat& a, const Quat& b) {
+    Quat r;
+    r.w = a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z;
+    r.x = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
+    r.y = a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z;
+    r.z = a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x;
+    return qnormalize(r);
+}
+LBA_HD Quat qinv(const Quat& q) { return qnormalize(Quat{-q.x, -q.y, -q.z, q.w}); }
+// rotate p by q (Sophus SO3::operator* on points)
+LBA_HD void qrot(const Quat& q, const double* p, double* o) {
+    double uv0 = q.y * p[2] - q.z * p[1], uv1 = q.z * p[0] - q.x * p[2], uv2 = q.x * p[1] - q.y * p[0];
+    uv0 += uv0; uv1 += uv1; uv2 += uv2;
+    o[0] = p[0] + q.w * uv0 + (q.y * uv2 - q.z * uv1);
+    o[1] = p[1] + q.w * uv1 + (q.z * uv0 - q.x * uv2);
+    o[2] = p[2] + q.w * uv2 + (q.x * uv1 - q.y * uv0);
+}
+// Eigen toRotationMatrix
+LBA_HD void qmat(const Quat& q, double* R) {
+    const double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
+    const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+    const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+    const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
+    R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
+}
+LBA_HD Quat so3_exp(const double* w, double* theta_out) {
+    const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    double imag, real, th;
+    if (th2 < kEps * kEps) {
+        th = 0.0;
+        const double th4 = th2 * th2;
+        imag = 0.5 - (1.0 / 48.0) * th2 + (1.0 / 3840.0) * th4;
+        real = 1.0 - (1.0 / 8.0) * th2 + (1.0 / 384.0) * th4;
+    } else {
+        th = sqrt(th2);
+        const double h = 0.5 * th;
+        imag = sin(h) / th;
+        real = cos(h);
+    }
+    *theta_out = th;
+    return Quat{imag * w[0], imag * w[1], imag * w[2], real};
+}
+LBA_HD void so3_log(const Quat& q, double* w, double* theta_out) {
+    const double sn = q.x * q.x + q.y * q.y + q.z * q.z;
+    double f;
+    if (sn < kEps * kEps) {
+        const double w2 = q.w * q.w;
+        f = 2.0 / q.w - (2.0 / 3.0) * sn / (q.w * w2);
+        *theta_out = 2.0 * sn / q.w;
+    } else {
+        const double n = sqrt(sn);
+        if (fabs(q.w) < kEps)
+            f = (q.w > 0 ? M_PI : -M_PI) / n;
+        else
+            f = 2.0 * atan(n / q.w) / n;
+        *theta_out = f * n;
+    }
+    w[0] = f * q.x; w[1] = f * q.y; w[2] = f * q.z;
+}
+
+// ---------------------------------------------------------------- SE3 = (q, t)
+struct SE3 { Quat q; double t[3]; };
+
+LBA_HD SE3 se3_mul(const SE3& a, const SE3& b) {
+    SE3 r;
+    r.q = qmul(a.q, b.q);
+    double tb[3];
+    qrot(a.q, b.t, tb);
+    r.t[0] = a.t[0] + tb[0]; r.t[1] = a.t[1] + tb[1]; r.t[2] = a.t[2] + tb[2];
+    return r;
+}
+LBA_HD SE3 se3_inv(const SE3& a) {
+    SE3 r;
+    r.q = qinv(a.q);
+    const double mt[3] = {-a.t[0], -a.t[1], -a.t[2]};
+    qrot(r.q, mt, r.t);
+    return r;
+}
+LBA_HD SE3 se3_exp(const double* a) {
+    SE3 r;
+    double th;
+    r.q = so3_exp(a + 3, &th);
+    double Om[9], Om2[9], V[9];
+    hat3(a + 3, Om);
+    mul33(Om, Om, Om2);
+    if (th < kEps) {
+        qmat(r.q, V);
+    } else {
+        const double th2 = th * th;
+        const double c1 = (1.0 - cos(th)) / th2, c2 = (th - sin(th)) / (th2 * th);
+        for (int i = 0; i < 9; ++i) V[i] = ((i & 3) == 0 ? 1.0 : 0.0) + c1 * Om[i] + c2 * Om2[i];
+    }
+    mul33v(V, a, r.t);
+    return r;
+}
+LBA_HD void se3_log(const SE3& T, double* xi) {
+    double th, w[3];
+    so3_log(T.q, w, &th);
+    xi[3] = w[0]; xi[4] = w[1]; xi[5] = w[2];
+    double Om[9], Om2[9], Vi[9];
+    hat3(w, Om);
+    mul33(Om, Om, Om2);
+    double c;
+    if (fabs(th) < kEps) {
+        c = 1.0 / 12.0;
+    } else {
+        const double h = 0.5 * th;
+        c = (1.0 - th * cos(h) / (2.0 * sin(h))) / (th * th);
+    }
+    for (int i = 0; i < 9; ++i) Vi[i] = ((i & 3) == 0 ? 1.0 : 0.0) - 0.5 * Om[i] + c * Om2[i];
+    mul33v(Vi, T.t, xi);
+}
+// Ad(T) = [R, t^R; 0, R] (6x6)
+LBA_HD void se3_adj(const SE3& T, double* A) {
+    double R[9], H[9], tR[9];
+    qmat(T.q, R);
+    hat3(T.t, H);
+    mul33(H, R, tR);
+    for (int i = 0; i < 36; ++i) A[i] = 0.0;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            A[i * 6 + j] = R[i * 3 + j];
+            A[(3 + i) * 6 + 3 + j] = R[i * 3 + j];
+            A[i * 6 + 3 + j] = tR[i * 3 + j];
+        }
+}
+
+// ---------------------------------------------------------------- Pose3utils
+// LeftJacobianPose3Q (src/Pose3utils.cc:5-24), including the reference's small-angle branch
+LBA_HD void left_jac_q(const double* xi, double* Q) {
+    const double* om = xi + 3;
+    const double th = sqrt(om[0] * om[0] + om[1] * om[1] + om[2] * om[2]);
+    double X[9], Y[9], XY[9], YX[9], XYX[9], T1[9], T2[9], T3[9], T4[9];
+    hat3(om, X);
+    hat3(xi, Y);
+    mul33(X, Y, XY);
+    mul33(Y, X, YX);
+    mul33(X, YX, XYX);
+    double a, b, c;
+    if (fabs(th) > 1e-5) {
+        const double s = sin(th), co = cos(th);
+        const double t2 = th * th, t3 = t2 * th, t4 = t3 * th, t5 = t4 * th;
+        a = (th - s) / t3;
+        b = (1.0 - 0.5 * t2 - co) / t4;
+        c = 0.5 * ((1.0 - 0.5 * t2 - co) / t4 - 3.0 * (th - s - t3 / 6.0) / t5);
+    } else {
+        a = 1.0 / 6.0;
+        b = 1.0 / 24.0;
+        c = 0.5 * (1.0 / 24.0 + 3.0 / 120.0);
+    }
+    mul33(X, XY, T1);    // X*XY
+    mul33(YX, X, T2);    // YX*X
+    mul33(XYX, X, T3);   // XYX*X
+    mul33(X, XYX, T4);   // X*XYX
+    for (int i = 0; i < 9; ++i)
+        Q[i] = 0.5 * Y[i] + a * (XY[i] + YX[i] + XYX[i]) - b * (T1[i] + T2[i] - 3.0 * XYX[i]) - c * (T3[i] + T4[i]);
+}
+// LeftJacobianRot3 (:48-59)
+LBA_HD void left_jac_rot3(const double* w, double* J) {
+    const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    if (th2 <= 2.220446049250313e-16) {
+        for (int i = 0; i < 9; ++i) J[i] = ((i & 3) == 0) ? 1.0 : 0.0;
+        return;
+    }
+    const double th = sqrt(th2);
+    const double d[3] = {w[0] / th, w[1] / th, w[2] / th};
+    const double s = sin(th);
+    const double c1 = s / th, c2 = 1.0 - s / th, c3 = (1.0 - cos(th)) / th;
+    double A[9];
+    hat3(w, A);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            J[i * 3 + j] = (i == j ? c1 : 0.0) + c2 * d[i] * d[j] + c3 * (A[i * 3 + j] / th);
+}
+// LeftJacobianRot3Inv (:61-73)
+LBA_HD void left_jac_rot3_inv(const double* w, double* J) {
+    const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    if (th2 <= 2.220446049250313e-16) {
+        for (int i = 0; i < 9; ++i) J[i] = ((i & 3) == 0) ? 1.0 : 0.0;
+        return;
+    }
+    const double th = sqrt(th2);
+    const double d[3] = {w[0] / th, w[1] / th, w[2] / th};
+    const double h = th / 2.0, hc = h * (1.0 / tan(h));
+    double A[9];
+    hat3(w, A);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            J[i * 3 + j] = (i == j ? hc : 0.0) + (1.0 - hc) * d[i] * d[j] - h * (A[i * 3 + j] / th);
+}
+// Right Jacobian of SE(3) as blocks: Jr(xi) = LeftJacobianPose3(-xi) = [J, Q; 0, J]
+LBA_HD void right_jac_blocks(const double* xi, double* J, double* Q) {
+    const double m[6] = {-xi[0], -xi[1], -xi[2], -xi[3], -xi[4], -xi[5]};
+    left_jac_q(m, Q);
+    left_jac_rot3(m + 3, J);
+}
+// Inverse right Jacobian: Jr^-1(xi) = LeftJacobianPose3Inv(-xi) = [Ji, -Ji Q Ji; 0, Ji] (6x6)
+LBA_HD void right_jac_inv(const double* xi, double* Jr) {
+    const double m[6] = {-xi[0], -xi[1], -xi[2], -xi[3], -xi[4], -xi[5]};
+    double Q[9], Ji[9], T[9], U[9];
+    left_jac_q(m, Q);
+    left_jac_rot3_inv(m + 3, Ji);
+    mul33(Ji, Q, T);
+    mul33(T, Ji, U);
+    for (int i = 0; i < 36; ++i) Jr[i] = 0.0;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            Jr[i * 6 + j] = Ji[i * 3 + j];
+            Jr[(3 + i) * 6 + 3 + j] = Ji[i * 3 + j];
+            Jr[i * 6 + 3 + j] = -U[i * 3 + j];
+        }
+}
+// se3Adj(v) = [w^, v^; 0, w^] (:111-119)
+LBA_HD void se3_ad(const double* v, double* A) {
+    double Hw[9], Hv[9];
+    hat3(v + 3, Hw);
+    hat3(v, Hv);
+    for (int i = 0; i < 36; ++i) A[i] = 0.0;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            A[i * 6 + j] = Hw[i * 3 + j];
+            A[(3 + i) * 6 + 3 + j] = Hw[i * 3 + j];
+            A[i * 6 + 3 + j] = Hv[i * 3 + j];
+        }
+}
+
+// ---------------------------------------------------------------- GP closed form
+struct GPScalars { double l1, l2, p2; };
+LBA_HD GPScalars gp_scalars(double t1, double t2, double t) {
+    const double T = t2 - t1, tau = t - t1, s = tau / T, om = 1.0 - s;
+    GPScalars g;
+    g.l1 = s * s * (3.0 - 2.0 * s);
+    g.l2 = tau * tau * (tau - T) / (T * T);
+    g.p2 = tau * om * om;
+    return g;
+}
+
+// Per GP KF-pair quantities (depend on the two KF states only), staged once per pair.
+struct GPPair {
+    double T1q[4], T1t[3];   // Twb of KF_a
+    double v1[6];            // velocity of KF_a
+    double xi12[6];          // log(T1^-1 T2)
+    double w2[6];            // Jr^-1(xi12) v2
+    double G1a[36];          // A1 = -Jr^-1(xi12) Ad(exp(xi12))^-1
+    double G1b[36];          // B1 = -1/2 ad(v2) A1
+    double G2a[36];          // C  = Jr^-1(xi12)
+    double G2b[36];          // D  = -1/2 ad(v2) C
+    double t1, t2;
+};
+
+LBA_HD void gp_pair_build(const SE3& Ta, const double* va, const SE3& Tb, const double* vb, double ta, double tb,
+                          GPPair* P) {
+    P->T1q[0] = Ta.q.x; P->T1q[1] = Ta.q.y; P->T1q[2] = Ta.q.z; P->T1q[3] = Ta.q.w;
+    for (int i = 0; i < 3; ++i) P->T1t[i] = Ta.t[i];
+    for (int i = 0; i < 6; ++i) P->v1[i] = va[i];
+    const SE3 Tai = se3_inv(Ta);
+    const SE3 T12 = se3_mul(Tai, Tb);
+    se3_log(T12, P->xi12);
+    right_jac_inv(P->xi12, P->G2a);
+    matmul(P->G2a, vb, P->w2, 6, 6, 1);
+    // Ad(exp(xi12))^-1 = Ad(exp(xi12)^-1)
+    const SE3 E = se3_exp(P->xi12);
+    const SE3 Ei = se3_inv(E);
+    double AdI[36], ad2[36];
+    se3_adj(Ei, AdI);
+    matmul(P->G2a, AdI, P->G1a, 6, 6, 6);
+    for (int i = 0; i < 36; ++i) P->G1a[i] = -P->G1a[i];
+    se3_ad(vb, ad2);
+    matmul(ad2, P->G1a, P->G1b, 6, 6, 6);
+    matmul(ad2, P->G2a, P->G2b, 6, 6, 6);
+    for (int i = 0; i < 36; ++i) { P->G1b[i] *= -0.5; P->G2b[i] *= -0.5; }
+    P->t1 = ta;
+    P->t2 = tb;
+}
+
+// ---------------------------------------------------------------- observation model
+struct Cam { double q[4], t[3], fx, fy, cx, cy; };
+
+// Derived camera quantities: Tcb = Tbc^-1 as rotation matrix + translation
+struct CamD { double Rcb[9], tcb[3], fx, fy, cx, cy; };
+
+LBA_HD void cam_derive(const Cam& c, CamD* d) {
+    SE3 Tbc;
+    Tbc.q = Quat{c.q[0], c.q[1], c.q[2], c.q[3]};
+    Tbc.t[0] = c.t[0]; Tbc.t[1] = c.t[1]; Tbc.t[2] = c.t[2];
+    const SE3 Tcb = se3_inv(Tbc);
+    qmat(Tcb.q, d->Rcb);
+    d->tcb[0] = Tcb.t[0]; d->tcb[1] = Tcb.t[1]; d->tcb[2] = Tcb.t[2];
+    d->fx = c.fx; d->fy = c.fy; d->cx = c.cx; d->cy = c.cy;
+}
+
+// Body pose used for one observation: rotation Rwb, translation twb, and for GP edges the
+// interpolation tangent xi(t).
+struct ObsPose { double Rwb[9], twb[3]; double xi[6]; };
+
+// GP-interpolated body pose at time t (QueryPose): Twb = T1 exp(p2 v1 + l1 xi12 + l2 w2)
+LBA_HD void gp_pose(const GPPair& P, const GPScalars& g, ObsPose* op) {
+    for (int i = 0; i < 6; ++i) op->xi[i] = g.p2 * P.v1[i] + g.l1 * P.xi12[i] + g.l2 * P.w2[i];
+    const SE3 dT = se3_exp(op->xi);
+    SE3 T1;
+    T1.q = Quat{P.T1q[0], P.T1q[1], P.T1q[2], P.T1q[3]};
+    T1.t[0] = P.T1t[0]; T1.t[1] = P.T1t[1]; T1.t[2] = P.T1t[2];
+    const SE3 T = se3_mul(T1, dT);
+    qmat(T.q, op->Rwb);
+    op->twb[0] = T.t[0]; op->twb[1] = T.t[1]; op->twb[2] = T.t[2];
+}
+
+// Xb = Rwb^T (Xw - twb), Xc = Rcb Xb + tcb; residual e = z - pi(Xc) (3rd row u - bf/z)
+LBA_HD void project_residual(const ObsPose& op, const CamD& c, const double* Xw, const double* z, double bf,
+                             int dim, double* Xb, double* Xc, double* e) {
+    const double d[3] = {Xw[0] - op.twb[0], Xw[1] - op.twb[1], Xw[2] - op.twb[2]};
+    mul33tv(op.Rwb, d, Xb);
+    mul33v(c.Rcb, Xb, Xc);
+    Xc[0] += c.tcb[0]; Xc[1] += c.tcb[1]; Xc[2] += c.tcb[2];
+    const double u = c.fx * Xc[0] / Xc[2] + c.cx;
+    const double v = c.fy * Xc[1] / Xc[2] + c.cy;
+    e[0] = z[0] - u;
+    e[1] = z[1] - v;
+    e[2] = (dim == 3) ? z[2] - (u - bf * (1.0 / Xc[2])) : 0.0;
+}
+
+// Jacobian rows of one reprojection observation, columns
+// [KF_a pose(6) vel(6) | KF_b pose(6) vel(6) | point(3)] (27), dim rows.
+// GP chain (src/G2oTypes.cc:258-314 with the four-scalar closed form):
+//   K = J1 Jr(xi); J_a = [K (l1 A1 + l2 B1) + J1 Ad(exp(-xi)), p2 K]; J_b = [K (l1 C + l2 D), l2 K C]
+// Output row r: pose/vel columns 0..23 at J[r*ldJ + c], point columns at J[r*ldJ + pcol + j]
+// (host harness: ldJ 27, pcol 24; kernels write straight into an LDS row buffer).
+template <typename OutT>
+LBA_HD void obs_jacobian(const ObsPose& op, const CamD& c, const double* Xb, const double* Xc, double bf, int dim,
+                         bool gp, const GPPair* P, const GPScalars& g, OutT* J, int ldJ, int pcol) {
+    // projection Jacobian P (dim x 3)
+    const double iz = 1.0 / Xc[2];
+    double Pj[9];
+    Pj[0] = c.fx * iz; Pj[1] = 0.0; Pj[2] = -c.fx * Xc[0] / (Xc[2] * Xc[2]);
+    Pj[3] = 0.0; Pj[4] = c.fy * iz; Pj[5] = -c.fy * Xc[1] / (Xc[2] * Xc[2]);
+    if (dim == 3) { Pj[6] = Pj[0]; Pj[7] = Pj[1]; Pj[8] = Pj[2] + bf * (1.0 / (Xc[2] * Xc[2])); }
+    // M = P Rcb (dim x 3);  J1 = [M, -M Xb^] ;  Jpt = -M Rwb^T
+    double M[9], H[9], MH[9];
+    for (int r = 0; r < dim; ++r)
+        for (int j = 0; j < 3; ++j)
+            M[r * 3 + j] = Pj[r * 3 + 0] * c.Rcb[0 * 3 + j] + Pj[r * 3 + 1] * c.Rcb[1 * 3 + j] + Pj[r * 3 + 2] * c.Rcb[2 * 3 + j];
+    hat3(Xb, H);
+    for (int r = 0; r < dim; ++r)
+        for (int j = 0; j < 3; ++j)
+            MH[r * 3 + j] = M[r * 3 + 0] * H[0 * 3 + j] + M[r * 3 + 1] * H[1 * 3 + j] + M[r * 3 + 2] * H[2 * 3 + j];
+    double J1[18];
+    for (int r = 0; r < dim; ++r)
+        for (int j = 0; j < 3; ++j) { J1[r * 6 + j] = M[r * 3 + j]; J1[r * 6 + 3 + j] = -MH[r * 3 + j]; }
+    for (int r = 0; r < dim; ++r)
+        for (int j = 0; j < 3; ++j)   // -M Rwb^T : (M Rbw)_{rj} = sum_k M_rk Rwb_jk
+            J[r * ldJ + pcol + j] = -(M[r * 3 + 0] * op.Rwb[j * 3 + 0] + M[r * 3 + 1] * op.Rwb[j * 3 + 1] + M[r * 3 + 2] * op.Rwb[j * 3 + 2]);
+    if (!gp) {
+        for (int r = 0; r < dim; ++r) {
+            for (int j = 0; j < 12; ++j) J[r * ldJ + j] = 0.0;
+            for (int j = 0; j < 6; ++j) { J[r * ldJ + 12 + j] = J1[r * 6 + j]; J[r * ldJ + 18 + j] = 0.0; }
+        }
+        return;
+    }
+    // Jr(xi) = [Jl, Q; 0, Jl] with Jl = LeftJacobianRot3(-w), Q = LeftJacobianPose3Q(-xi)
+    double Jl[9], Q[9];
+    right_jac_blocks(op.xi, Jl, Q);
+    double K[18];   // K = J1 Jr = [J1a Jl, J1a Q + J1b Jl]
+    for (int r = 0; r < dim; ++r)
+        for (int j = 0; j < 3; ++j) {
+            const double* a = J1 + r * 6;
+            K[r * 6 + j] = a[0] * Jl[0 * 3 + j] + a[1] * Jl[1 * 3 + j] + a[2] * Jl[2 * 3 + j];
+            K[r * 6 + 3 + j] = a[0] * Q[0 * 3 + j] + a[1] * Q[1 * 3 + j] + a[2] * Q[2 * 3 + j] +
+                               a[3] * Jl[0 * 3 + j] + a[4] * Jl[1 * 3 + j] + a[5] * Jl[2 * 3 + j];
+        }
+    // Ad(exp(-xi)) = [R', t'^ R'; 0, R']
+    const double mxi[6] = {-op.xi[0], -op.xi[1], -op.xi[2], -op.xi[3], -op.xi[4], -op.xi[5]};
+    const SE3 Em = se3_exp(mxi);
+    double Rm[9], Ht[9], tR[9];
+    qmat(Em.q, Rm);
+    hat3(Em.t, Ht);
+    mul33(Ht, Rm, tR);
+    for (int r = 0; r < dim; ++r) {
+        const double* k = K + r * 6;
+        const double* a = J1 + r * 6;
+        OutT* Ja = J + r * ldJ;
+        OutT* Jb = J + r * ldJ + 12;
+        double kc[6];
+        double ja[6];
+        for (int j = 0; j < 6; ++j) {
+            double sa = 0.0, sb = 0.0, sc = 0.0, sd = 0.0;
+            for (int l = 0; l < 6; ++l) {
+                sa += k[l] * P->G1a[l * 6 + j];
+                sb += k[l] * P->G1b[l * 6 + j];
+                sc += k[l] * P->G2a[l * 6 + j];
+                sd += k[l] * P->G2b[l * 6 + j];
+            }
+            ja[j] = g.l1 * sa + g.l2 * sb;
+            Jb[j] = g.l1 * sc + g.l2 * sd;
+            kc[j] = sc;
+        }
+        for (int j = 0; j < 3; ++j) {   // + J1 Ad(exp(-xi))
+            Ja[j] = ja[j] + (a[0] * Rm[0 * 3 + j] + a[1] * Rm[1 * 3 + j] + a[2] * Rm[2 * 3 + j]);
+            Ja[3 + j] = ja[3 + j] + (a[0] * tR[0 * 3 + j] + a[1] * tR[1 * 3 + j] + a[2] * tR[2 * 3 + j] +
+                                     a[3] * Rm[0 * 3 + j] + a[4] * Rm[1 * 3 + j] + a[5] * Rm[2 * 3 + j]);
+        }
+        for (int j = 0; j < 6; ++j) {
+            Ja[6 + j] = g.p2 * k[j];
+            Jb[6 + j] = g.l2 * kc[j];
+        }
+    }
+}
+
+// Eigen compute_inverse<3,3>: adjugate / determinant (used by the Schur step,
+// Thirdparty/g2o/g2o/core/block_solver.hpp:389)
+LBA_HD void inv3(const double* m, double* r) {
+    const double c00 = m[4] * m[8] - m[5] * m[7];
+    const double c10 = m[7] * m[2] - m[8] * m[1];
+    const double c20 = m[1] * m[5] - m[2] * m[4];
+    const double invdet = 1.0 / (c00 * m[0] + c10 * m[3] + c20 * m[6]);
+    r[0] = c00 * invdet; r[1] = c10 * invdet; r[2] = c20 * invdet;
+    r[3] = (m[5] * m[6] - m[3] * m[8]) * invdet;
+    r[4] = (m[8] * m[0] - m[6] * m[2]) * invdet;
+    r[5] = (m[2] * m[3] - m[0] * m[5]) * invdet;
+    r[6] = (m[3] * m[7] - m[4] * m[6]) * invdet;
+    r[7] = (m[6] * m[1] - m[7] * m[0]) * invdet;
+    r[8] = (m[0] * m[4] - m[1] * m[3]) * invdet;
+}
+
+// GaussianProcess::QiInv(dt) (include/GaussianProcess.h:31-41), 12x12 row-major
+LBA_HD void qi_inv(const double* qcinv, double dt, double* Om) {
+    const double dt2 = dt * dt, dt3 = dt2 * dt;
+    const double a = 12.0 / dt3, b = -6.0 / dt2, c = 4.0 / dt;
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) {
+            const double q = qcinv[i * 6 + j];
+            Om[i * 12 + j] = a * q;
+            Om[i * 12 + 6 + j] = b * q;
+            Om[(6 + i) * 12 + j] = b * q;
+            Om[(6 + i) * 12 + 6 + j] = c * q;
+        }
+}
+
+// EdgeGaussianPrior (include/G2oTypes.h:155-163, src/G2oTypes.cc:100-118):
+//   e = [xi - dt v1 ; Jr^-1(xi) v2 - v1], xi = log(T1^-1 T2)
+//   Ji = [-Jr^-1 Ad(T)^-1, -dt I ; -1/2 ad(v2)(-Jr^-1 Ad(T)^-1), -I],  Jj = [Jr^-1, 0 ; -1/2 ad(v2) Jr^-1, Jr^-1]
+// Ji / Jj may be null (error only).
+template <typename OutT>
+LBA_HD void prior_error_jac(const SE3& Ta, const double* va, double ta, const SE3& Tb, const double* vb, double tb,
+                            OutT* e, OutT* Ji, OutT* Jj) {
+    const SE3 T = se3_mul(se3_inv(Ta), Tb);
+    double xi[6], Jri[36];
+    se3_log(T, xi);
+    right_jac_inv(xi, Jri);
+    const double dt = tb - ta;
+    for (int i = 0; i < 6; ++i) {
+        double s = 0.0;
+        for (int k = 0; k < 6; ++k) s += Jri[i * 6 + k] * vb[k];
+        e[i] = xi[i] - dt * va[i];
+        e[6 + i] = s - va[i];
+    }
+    if (!Ji) return;
+    double AdI[36], ad2[36], top[36];
+    se3_adj(se3_inv(T), AdI);
+    se3_ad(vb, ad2);
+    matmul(Jri, AdI, top, 6, 6, 6);
+    for (int i = 0; i < 144; ++i) { Ji[i] = 0.0; Jj[i] = 0.0; }
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) {
+            double bi = 0.0, bj = 0.0;
+            for (int k = 0; k < 6; ++k) { bi += ad2[i * 6 + k] * (-top[k * 6 + j]); bj += ad2[i * 6 + k] * Jri[k * 6 + j]; }
+            Ji[i * 12 + j] = -top[i * 6 + j];
+            Ji[(6 + i) * 12 + j] = -0.5 * bi;
+            Jj[i * 12 + j] = Jri[i * 6 + j];
+            Jj[(6 + i) * 12 + j] = -0.5 * bj;
+            Jj[(6 + i) * 12 + 6 + j] = Jri[i * 6 + j];
+        }
+    for (int i = 0; i < 6; ++i) { Ji[i * 12 + 6 + i] = -dt; Ji[(6 + i) * 12 + 6 + i] = -1.0; }
+}
+
+// Huber (RobustKernelHuber::robustify, robust_kernel_impl.cpp:76-90): rho(e), rho'(e)
+LBA_HD void huber(double e, double delta, double* r0, double* r1) {
+    const double d2 = delta * delta;
+    if (e <= d2) { *r0 = e; *r1 = 1.0; }
+    else { const double s = sqrt(e); *r0 = 2 * s * delta - d2; *r1 = delta / s; }
+}
+
+}  // namespace lba

@@ -1,0 +1,194 @@
+"""Benchmark: local-BA LM iterations/s on MI355X (BASELINE.json metric).
+
+One "step" is one Levenberg-Marquardt iteration (OptimizationAlgorithmLevenberg::solve:
+linearize + Schur + dense reduced-camera solve + update + re-evaluation) of the GP local BA on a
+synthetic BASELINE config-1 window (50 optimisable KF + 1 fixed, 20k landmarks, ~120k
+observations, 4 asynchronous cameras, fp64), with the early-stop rule disabled so the iteration
+count is fixed.  Inputs are resident in HBM before the timed region.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+With N > 1 every rank optimises its own window (window farming, BASELINE config 3): windows are
+cut from one trajectory so neighbouring windows share keyframes and landmarks, and at every
+window boundary (each --window-iters iterations) the owners of shared landmarks publish their
+estimates with one all_gather over RCCL (xGMI).  value = iterations of all ranks / max-rank time.
+"""
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "amc-slam_amd"))
+
+METRIC = "local-BA iterations/sec (50 KF, 20k landmarks, 120k obs) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+FP64_PEAK_TFLOPS = 78.6        # MI355X fp64 vector/matrix spec
+
+
+def sweep_bytes(win):
+    """SURVEY.md §8(d) algorithmic bytes of the residual/Jacobian/J^T W J sweep per launch:
+    72 B per observation of compulsory input, 288 B per unique (KF, landmark) Hpl block written,
+    96 B per landmark (Hll + bl), 2 x (1152 B per KF-pair Hpp block + 96 B per KF)."""
+    n_obs = len(win.obs)
+    n_lm = len(np.unique(win.obs["lm"]))
+    n_kf = int((win.kfs["fixed"] == 0).sum())
+    n_kfpairs = max(n_kf - 1, 0)
+    return 72 * n_obs + 288 * win.n_pairs + 96 * n_lm + 2 * (1152 * n_kfpairs + 96 * n_kf)
+
+
+def sweep_flops(win):
+    """Algorithmic fp64 FLOPs of the sweep: per GP observation ~3.25 kFLOP, per non-GP ~1.2 kFLOP
+    (interpolation + exp + projection + Jacobian chain + 27x27 J^T W J)."""
+    gp = int(np.isin(win.obs["kind"], (0, 1)).sum())
+    return 3250.0 * gp + 1200.0 * (len(win.obs) - gp)
+
+
+def pmc_traffic(workload):
+    """HBM bytes per k_linearize launch from the committed rocprofv3 PMC summary (FETCH_SIZE
+    doubled per the gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md §HBM), or None."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_k_linearize_*.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
+            return float(d["hbm_bytes_per_launch"])
+    return None
+
+
+def cpu_baseline(win, seconds):
+    """The oracle (C restatement of the reference CPU path, single thread, like the reference's
+    G2O_USE_OPENMP OFF build) on the same window: a bounded number of LM iterations."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import orc
+    o = orc.Oracle(win, early_stop=0)
+    t = time.perf_counter()
+    o.optimize(1)
+    t_cal = time.perf_counter() - t
+    n = int(max(1, min(50, round(seconds / max(t_cal, 1e-6)))))
+    o2 = orc.Oracle(win, early_stop=0)
+    t = time.perf_counter()
+    n_run, _ = o2.optimize(n)
+    dt = time.perf_counter() - t
+    return {"value": n_run / dt, "unit": "LM iterations/s", "cores": 1, "kind": "port",
+            "sample": f"{n_run} LM iterations of the same {win.name} window, oracle/lba_oracle.c (-O3, 1 thread), "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="cfg1_local_50kf")
+    ap.add_argument("--window-iters", type=int, default=10, help="LM iterations per window (LocalGPBA optimize(10))")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--seed", type=int, default=20250912)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import amc_lba
+    from amc_lba import farm
+    from amc_lba.synth import make_config_window
+
+    if world > 1:
+        win, shared = farm.make_rank_window(args.config, rank, world, seed=args.seed)
+        ex = farm.SharedExchange(win, shared, rank, world, device=torch.device("cuda", local))
+    else:
+        win = make_config_window(args.config, seed=args.seed)
+        ex = None
+    prob = amc_lba.Problem(win, device=local, early_stop=0)
+
+    # warmup (not timed)
+    if args.warmup > 0:
+        prob.optimize(args.warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    done, ms_k, n_k = 0, 0.0, 0
+    phase = {"ms_linearize": 0.0, "ms_schur": 0.0, "ms_solve": 0.0, "ms_update_eval": 0.0, "trials": 0}
+    while done < args.steps:
+        it = min(args.window_iters, args.steps - done)
+        n, st = prob.optimize(it)
+        done += n
+        ms_k += st.ms_k_linearize
+        n_k += st.n_k_linearize
+        for k in phase:
+            phase[k] += getattr(st, k)
+        if ex is not None:
+            ex.exchange(prob)           # window boundary: publish owned shared landmarks
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    if rank == 0:
+        total_iters = done * world
+        value = total_iters / dt
+        k_ms = ms_k / max(n_k, 1)
+        B = sweep_bytes(win)
+        F = sweep_flops(win)
+        achieved = B / (k_ms * 1e-3) / 1e9 if n_k else None
+        workload = f"{args.config}: {win.name or args.config} synthetic window"
+        traffic = pmc_traffic(args.config)
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "LM iterations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt * 1e3 / done,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (deterministic generator, amc_lba/synth.py, seed %d)" % args.seed,
+            "config": {"workload": workload, "n_kf": int(len(win.kfs)), "n_opt_kf": int((win.kfs["fixed"] == 0).sum()),
+                       "n_lm": int(len(win.lm)), "n_obs": int(len(win.obs)), "n_pairs": int(win.n_pairs),
+                       "n_cam": int(len(win.cams)), "window_iters": args.window_iters,
+                       "parallelism": f"window farm x{world}" if world > 1 else "single window"},
+            "roofline": {"bound": "hbm", "kernel": "k_linearize", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                         "traffic": traffic, "bytes_per_launch": B, "avg_launch_ms": k_ms},
+            "roofline_fp64": {"kernel": "k_linearize", "flops_per_launch": F,
+                              "achieved": F / (k_ms * 1e-3) / 1e12 if n_k else None,
+                              "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                              "frac": (F / (k_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS) if n_k else None},
+            "phases_ms_per_step": {k: (v / done if k != "trials" else v / done) for k, v in phase.items()},
+        }
+        if not args.no_cpu and world == 1:
+            line["cpu_baseline"] = cpu_baseline(win, args.cpu_seconds)
+            line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

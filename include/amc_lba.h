@@ -1,0 +1,167 @@
+/*
+ * amc_lba.h — C ABI of the MI355X-native continuous-time (GP) local bundle adjustment.
+ *
+ * This is the drop-in boundary for AMC-SLAM's local BA hot path.  The reference builds a
+ * g2o::SparseOptimizer inside Optimizer::LocalGPBA (src/Optimizer.cc:713-1432, declared at
+ * include/Optimizer.h:58) and calls SparseOptimizer::optimize (Thirdparty/g2o/g2o/core/
+ * sparse_optimizer.cpp:354-419).  A caller using this library keeps LocalGPBA's window
+ * selection and post-pass, fills the flat arrays below instead of g2o vertices/edges, and
+ * calls lba_optimize().  Plain C types only; every array is caller-owned and copied.
+ *
+ * Conventions (mirroring g2o):
+ *   - Tangent order is Sophus [translation; rotation]; pose update T <- T*exp(d)
+ *     (src/G2oTypes.cc:41-46), velocity and landmark updates are additive.
+ *   - Quaternions are stored (x, y, z, w) like Eigen::Quaternion::coeffs().
+ *   - Hessian vertex order: non-fixed keyframes in array order, then landmarks in array
+ *     order (g2o sorts active vertices by id and puts non-marginalized first,
+ *     sparse_optimizer.cpp:166-190).  Callers that want g2o's exact ordering pass
+ *     keyframes sorted by mnId.
+ *   - b = -sum J^T rho' Omega e, H dx = b (base_multi_edge.hpp:35-48, 170-222).
+ *   - Status codes: >= 0 success (lba_optimize: iterations run), LBA_E_* < 0 on error.
+ */
+#ifndef AMC_LBA_H
+#define AMC_LBA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LBA_ABI_VERSION 1
+
+/* status codes */
+#define LBA_OK              0
+#define LBA_E_EMPTY        -1   /* empty graph: no edges or no free vertices (sparse_optimizer.cpp:358-361) */
+#define LBA_E_SOLVE        -2   /* reduced-camera factorisation not positive (linear_solver_dense.h:108-112) */
+#define LBA_E_DIVERGED     -3   /* LocalGPBA divergence guard (src/Optimizer.cc:1354-1358), set by host adapter */
+#define LBA_E_ARG          -4   /* invalid argument / malformed problem */
+#define LBA_E_HIP          -5   /* HIP runtime error */
+#define LBA_E_LIMIT        -6   /* problem exceeds a compiled limit (see lba_last_error) */
+
+/* observation kinds (the reprojection edges of include/G2oTypes.h) */
+#define LBA_MONO_GP    0   /* EdgeMonoGPExtrinsic / EdgeMonoGP: 2-d, vertices (kf_a=prev KF, kf_b=KF, lm), cam extrinsic fixed
+                              (include/G2oTypes.h:292-402, src/G2oTypes.cc:225-367) */
+#define LBA_STEREO_GP  1   /* EdgeStereoGP: 3-d [u, v, u_r] (include/G2oTypes.h:404-421, src/G2oTypes.cc:369-443) */
+#define LBA_MONO       2   /* EdgeMono: 2-d, vertices (kf_b, lm) at KF time (include/G2oTypes.h:423-446, src/G2oTypes.cc:445-468) */
+#define LBA_STEREO     3   /* EdgeStereo: 3-d (include/G2oTypes.h:448-468, src/G2oTypes.cc:470-495) */
+
+/* LM termination codes in lba_stats.result (OptimizationAlgorithm::SolverResult) */
+#define LBA_RESULT_OK         0
+#define LBA_RESULT_TERMINATE  1
+#define LBA_RESULT_STOPPED    2   /* stop flag raised (SparseOptimizer::terminate) */
+
+typedef struct lba_config {
+    double qc[36];          /* GaussianProcess::mQc, 6x6 row-major (Tracking.cc:753-758 builds diag(Gaussian.Qc)) */
+    double huber_mono;      /* Huber delta for 2-d edges; LocalGPBA: (double)(float)sqrt(5.991)  (Optimizer.cc:975) */
+    double huber_stereo;    /* Huber delta for 3-d edges; (double)(float)sqrt(7.815)           (Optimizer.cc:977) */
+    double huber_prior;     /* Huber delta on EdgeGaussianPrior; <= 0: none (LocalGPBA), 21.026 in BundleAdjustment (:99-136) */
+    double lambda_init;     /* OptimizationAlgorithmLevenberg userLambdaInit; <= 0 -> tau * max diag (levenberg.cpp:171-185) */
+    double tau;             /* 1e-5 (levenberg.cpp:47) */
+    int    max_trials;      /* _maxTrialsAfterFailure, 10 (levenberg.cpp:51) */
+    int    early_stop;      /* 1: g2o stop rules active (3 iterations of <1e-3 gain, levenberg.cpp:157-166); 0: fixed count */
+    int    device;          /* HIP device ordinal */
+    int    flags;           /* reserved, 0 */
+} lba_config;
+
+typedef struct lba_kf {     /* VertexPoseVel / PoseVelocity (include/G2oTypes.h:59-80,104-126) */
+    double q[4];            /* Twb rotation (x,y,z,w) */
+    double t[3];            /* Twb translation */
+    double vel[6];          /* PoseVelocity::Vel, world-frame twist [v; w] */
+    double time;            /* PoseVelocity::time (KF time stamp) */
+    double bf;              /* PoseVelocity::bf (stereo baseline * fx) */
+    int32_t fixed;          /* vertex fixed (no Hessian rows) */
+    int32_t pad;
+} lba_kf;
+
+typedef struct lba_obs {
+    int32_t kind;           /* LBA_MONO_GP .. LBA_STEREO */
+    int32_t kf_a;           /* GP kinds: previous KF (vertex 0); non-GP: ignored (-1) */
+    int32_t kf_b;           /* GP kinds: KF (vertex 1); non-GP: the KF (vertex 0) */
+    int32_t lm;             /* landmark index */
+    int32_t cam;            /* camera index (EdgeMono/EdgeStereo use the reference camera = n_cam-1) */
+    int32_t pad;
+    double  t;              /* observation time (GP kinds: pKFi->mvTimeStamps[c]) */
+    double  z[3];           /* u, v, (u_right for stereo) */
+    double  w;              /* information weight invSigma2 / unc2 (Omega = w * I) */
+} lba_obs;
+
+typedef struct lba_prior {  /* EdgeGaussianPrior(v0 = kf_a older, v1 = kf_b newer), info QiInv(t_b - t_a) */
+    int32_t kf_a;
+    int32_t kf_b;
+} lba_prior;
+
+typedef struct lba_cam {    /* GeometricCamera (Pinhole) + MultiKeyFrame::mTbc[c] */
+    double q[4];            /* Tbc rotation (x,y,z,w) */
+    double t[3];            /* Tbc translation */
+    double fx, fy, cx, cy;  /* Pinhole::mvParameters (float values widened) */
+} lba_cam;
+
+typedef struct lba_stats {
+    int32_t iterations;     /* LM iterations run (SparseOptimizer::optimize return) */
+    int32_t trials;         /* total LM trials (sum of qmax) */
+    int32_t result;         /* LBA_RESULT_* of the last iteration */
+    int32_t solve_failures; /* trials whose factorisation was not positive */
+    double  chi2_initial;   /* activeRobustChi2 before the first iteration */
+    double  chi2_final;     /* activeRobustChi2 of the last computed errors (g2o semantics) */
+    double  lambda_final;
+    double  ms_linearize;   /* device time per phase, summed (HIP events) */
+    double  ms_schur;
+    double  ms_solve;
+    double  ms_update_eval;
+    double  ms_total;       /* host wall time of lba_optimize */
+    double  ms_k_linearize; /* device time of the fused residual/Jacobian/J^T W J sweep kernel, summed */
+    int32_t n_k_linearize;  /* launches of that kernel */
+    int32_t pad;
+} lba_stats;
+
+typedef struct lba_problem lba_problem;   /* opaque: owns device buffers + stream */
+
+/* lifecycle */
+int         lba_create(lba_problem** out, const lba_config* cfg);
+void        lba_destroy(lba_problem* p);
+const char* lba_last_error(const lba_problem* p);
+int         lba_abi_version(void);
+
+/* Copy a window to the device (replaces SparseOptimizer::addVertex/addEdge +
+ * initializeOptimization, sparse_optimizer.cpp:197-267).  vel_kfs lists the KFs carrying an
+ * EdgeVelocity (info QcInv(2,2), Optimizer.cc:858-870). */
+int lba_set_problem(lba_problem* p,
+                    const lba_kf* kfs, int32_t n_kf,
+                    const double* lm_xyz, int32_t n_lm,
+                    const lba_obs* obs, int32_t n_obs,
+                    const lba_prior* priors, int32_t n_priors,
+                    const int32_t* vel_kfs, int32_t n_vel,
+                    const lba_cam* cams, int32_t n_cam);
+
+/* Levenberg-Marquardt (OptimizationAlgorithmLevenberg::solve x iters).  stop_flag is polled
+ * between iterations and trials like SparseOptimizer::terminate().  Returns iterations run
+ * (>= 0) or an LBA_E_* code. */
+int lba_optimize(lba_problem* p, int32_t iters, volatile const int32_t* stop_flag, lba_stats* out);
+
+/* write-back: current (accepted) estimates */
+int lba_get_state(lba_problem* p, lba_kf* kf_out, double* lm_out);
+/* overwrite the current estimates (window-boundary exchange of shared keyframes/landmarks in a
+ * multi-GPU window farm); either pointer may be NULL to keep that part.  Quaternions are
+ * re-normalised like the Sophus cast. */
+int lba_set_state(lba_problem* p, const lba_kf* kf_in, const double* lm_xyz);
+
+/* Errors of the current estimate: robust chi2 sum, per-observation chi2 (e^T Omega e) and
+ * the LocalGPBA depth test (both KF poses for GP edges, include/G2oTypes.h:305-314).
+ * Any output pointer may be NULL. */
+int lba_eval(lba_problem* p, double* chi2_robust, double* obs_chi2, uint8_t* depth_ok);
+
+/* Parity/debug entry points (no LM).  lba_linearize: computeActiveErrors + buildSystem at the
+ * current estimate: residuals [n_obs*3] (unused components 0), H_pp dense [np*np] full
+ * symmetric, b [np + 3*n_lm], H_ll [n_lm*9].  Any pointer may be NULL.  Returns np. */
+int lba_linearize(lba_problem* p, double* residuals, double* H_pp, double* b, double* H_ll);
+/* One damped solve at lambda on the last linearisation: dx [np + 3*n_lm] (poses then
+ * landmarks), BlockSolver::solve with setLambda/restoreDiagonal (block_solver.hpp:354-486). */
+int lba_solve_step(lba_problem* p, double lambda, double* dx);
+/* Dimension of the pose system (12 * number of non-fixed KFs). */
+int lba_pose_dim(const lba_problem* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AMC_LBA_H */

@@ -1,0 +1,72 @@
+// Test-only host harness: evaluates the product's per-observation math (lba_math.hpp, the
+// same inline functions the HIP kernels execute) on the CPU so tests/test_math_host.py can
+// compare it with the oracle without a GPU.  Not part of the shipped library.
+#include <string.h>
+
+#include "../../amc-slam_amd/csrc/lba_math.hpp"
+#include "../../include/amc_lba.h"
+
+using namespace lba;
+
+static SE3 mk(const double* q, const double* t) {
+    SE3 T;
+    T.q = qnormalize(Quat{q[0], q[1], q[2], q[3]});
+    T.t[0] = t[0]; T.t[1] = t[1]; T.t[2] = t[2];
+    return T;
+}
+
+extern "C" int mh_obs_linearize(const lba_kf* kfs, const double* lm, const lba_obs* o, const lba_cam* cams,
+                                double* err, double* J) {
+    const int dim = (o->kind == LBA_STEREO_GP || o->kind == LBA_STEREO) ? 3 : 2;
+    const bool gp = (o->kind == LBA_MONO_GP || o->kind == LBA_STEREO_GP);
+    Cam c;
+    memcpy(c.q, cams[o->cam].q, sizeof(c.q));
+    {
+        Quat cq = qnormalize(Quat{c.q[0], c.q[1], c.q[2], c.q[3]});
+        c.q[0] = cq.x; c.q[1] = cq.y; c.q[2] = cq.z; c.q[3] = cq.w;
+    }
+    memcpy(c.t, cams[o->cam].t, sizeof(c.t));
+    c.fx = cams[o->cam].fx; c.fy = cams[o->cam].fy; c.cx = cams[o->cam].cx; c.cy = cams[o->cam].cy;
+    CamD cd;
+    cam_derive(c, &cd);
+    ObsPose op;
+    GPPair P;
+    GPScalars g{0, 0, 0};
+    double bf;
+    if (gp) {
+        const lba_kf& a = kfs[o->kf_a];
+        const lba_kf& b = kfs[o->kf_b];
+        gp_pair_build(mk(a.q, a.t), a.vel, mk(b.q, b.t), b.vel, a.time, b.time, &P);
+        g = gp_scalars(P.t1, P.t2, o->t);
+        gp_pose(P, g, &op);
+        bf = a.bf;
+    } else {
+        const lba_kf& b = kfs[o->kf_b];
+        SE3 T = mk(b.q, b.t);
+        qmat(T.q, op.Rwb);
+        op.twb[0] = T.t[0]; op.twb[1] = T.t[1]; op.twb[2] = T.t[2];
+        for (int i = 0; i < 6; ++i) op.xi[i] = 0.0;
+        bf = b.bf;
+    }
+    double Xb[3], Xc[3];
+    project_residual(op, cd, lm + 3 * o->lm, o->z, bf, dim, Xb, Xc, err);
+    obs_jacobian(op, cd, Xb, Xc, bf, dim, gp, &P, g, J, 27, 24);
+    return dim;
+}
+
+extern "C" void mh_gp_scalars(double t1, double t2, double t, double* out3) {
+    GPScalars g = gp_scalars(t1, t2, t);
+    out3[0] = g.l1; out3[1] = g.l2; out3[2] = g.p2;
+}
+
+extern "C" void mh_se3_exp(const double* xi, double* q, double* t) {
+    SE3 T = se3_exp(xi);
+    q[0] = T.q.x; q[1] = T.q.y; q[2] = T.q.z; q[3] = T.q.w;
+    t[0] = T.t[0]; t[1] = T.t[1]; t[2] = T.t[2];
+}
+extern "C" void mh_se3_log(const double* q, const double* t, double* xi) { se3_log(mk(q, t), xi); }
+extern "C" void mh_right_jac_inv(const double* xi, double* J) { right_jac_inv(xi, J); }
+
+extern "C" void mh_prior(const lba_kf* a, const lba_kf* b, double* e, double* Ji, double* Jj) {
+    prior_error_jac(mk(a->q, a->t), a->vel, a->time, mk(b->q, b->t), b->vel, b->time, e, Ji, Jj);
+}

@@ -1,0 +1,84 @@
+"""The drop-in boundary: libamc_lba.so loads, exports every function include/amc_lba.h declares,
+the numpy/ctypes mirrors of the structs have the C layout, and the product fails loudly (no
+silent CPU fallback) when the library or the GPU is missing.  No compute calls here."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import amc_lba
+from amc_lba import abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "amc_lba.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(lba_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for n in ("lba_create", "lba_set_problem", "lba_optimize", "lba_get_state", "lba_eval", "lba_linearize",
+              "lba_solve_step", "lba_destroy"):
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol():
+    L = amc_lba.lib()
+    exported = subprocess.run(["nm", "-D", "--defined-only", amc_lba.LIB_PATH], capture_output=True,
+                              text=True).stdout
+    for n in declared_functions():
+        assert hasattr(L, n), n
+        assert re.search(rf"\bT {n}\b", exported), n
+    assert set(amc_lba.exported_symbols()) <= set(declared_functions())
+    assert L.lba_abi_version() == 1
+
+
+def _c_sizeof(struct):
+    code = f'#include "{HEADER}"\n#include <stdio.h>\n#include <stddef.h>\nint main(void){{printf("%zu", sizeof({struct}));return 0;}}'
+    exe = "/tmp/_abi_sz"
+    subprocess.run(["gcc", "-x", "c", "-", "-o", exe], input=code, text=True, check=True)
+    return int(subprocess.run([exe], capture_output=True, text=True, check=True).stdout)
+
+
+@pytest.mark.parametrize("struct,dtype", [("lba_kf", abi.KF_DTYPE), ("lba_obs", abi.OBS_DTYPE),
+                                          ("lba_prior", abi.PRIOR_DTYPE), ("lba_cam", abi.CAM_DTYPE)])
+def test_struct_layouts_match_header(struct, dtype):
+    assert _c_sizeof(struct) == dtype.itemsize
+
+
+def test_ctypes_structs_match_header():
+    assert _c_sizeof("lba_config") == ctypes.sizeof(abi.LbaConfig)
+    assert _c_sizeof("lba_stats") == ctypes.sizeof(abi.LbaStats)
+
+
+def test_create_without_gpu_fails_cleanly():
+    """No GPU in the build container: lba_create must return an error code, never crash."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by the gpu tests")
+    h = ctypes.c_void_p()
+    cfg = abi.make_config()
+    rc = amc_lba.lib().lba_create(ctypes.byref(h), ctypes.byref(cfg))
+    assert rc in (abi.LBA_E_HIP, abi.LBA_E_ARG)
+    assert not h.value
+
+
+def test_missing_library_fails_loudly(monkeypatch):
+    monkeypatch.setattr(amc_lba, "_lib", None)
+    monkeypatch.setattr(amc_lba, "LIB_PATH", "/nonexistent/libamc_lba.so")
+    with pytest.raises(RuntimeError):
+        amc_lba.lib()
+
+
+def test_null_arguments_rejected():
+    L = amc_lba.lib()
+    assert L.lba_create(None, None) == abi.LBA_E_ARG
+    assert L.lba_optimize(None, 1, None, None) == abi.LBA_E_ARG
+    assert L.lba_get_state(None, None, None) == abi.LBA_E_ARG
