@@ -10,10 +10,12 @@
 //   gp pairs      [n_gp][GPP_STRIDE] per (prev KF, KF) interpolation quantities (lba::GPPair)
 //   Hpl           [n_pairs][12][3] one block per unique (non-fixed KF, landmark)
 //   Hll, bl       [n_lm][9], [n_lm][3]
-//   slab          [n_entries][456] per (tile, pose-pair segment) partial of Hpp/b:
-//                 aa(144) ab(144) bb(144) ga(12) gb(12); priors / velocity edges append
-//   slab2         [n_sentries][144] per (tile, KF pair) Schur partial  V(k1) Hpl(k2)^T
-//   S             [np][np] reduced camera system (lower triangle), factored in place
+//   hslab/gslab   per (tile, pose-pair segment) partial of Hpp blocks / b_p (and per prior /
+//                 velocity edge), each block stored at a slot sorted by its target upper block
+//   sslab/gpslab  per (tile, KF pair) Schur partials V(k1) Hpl(k2)^T and per (tile, KF) rhs
+//                 partials, target-sorted likewise
+//   Hblk, Sblk    [n_ublocks][144] reduced Hpp / damped Schur complement, upper blocks
+//   S, Lm         [np][np] dense reduced camera system (lower) and its Cholesky factor
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -23,8 +25,6 @@ namespace lba {
 constexpr int KF_STRIDE = 16;
 constexpr int CAMD_STRIDE = 16;     // Rcb(9) tcb(3) fx fy cx cy
 constexpr int KFP_STRIDE = 12;      // Rwb(9) twb(3)
-constexpr int ENTRY = 456;          // slab entry: aa ab bb ga gb
-constexpr int E_AA = 0, E_AB = 144, E_BB = 288, E_GA = 432, E_GB = 444;
 
 // tile limits (one workgroup of TILE_OBS threads per tile)
 constexpr int TILE_OBS = 128;
@@ -34,10 +34,8 @@ constexpr int TILE_LMS = 64;
 constexpr int TILE_KF = 16;
 constexpr int ROW_STRIDE = 28;      // LDS Jacobian row: Ja(12) Jb(12) e(1) Jp(3)
 
-// Hpp source roles (assemble)
-constexpr int R_AA = 0, R_BB = 1, R_AB = 2, R_ABT = 3;
-
-constexpr int CHOL_NB = 32;         // Cholesky panel width
+constexpr int CHOL_NB = 32;         // Cholesky panel / tile width
+constexpr int RED_GROUPS = 4;       // reduction kernels: 4 groups x 144 threads
 
 struct DevProblem {
     int n_kf, n_lm, n_obs, n_gp, n_pairs, n_tiles, n_pb, np, n_prior, n_vel, n_cam;
@@ -85,38 +83,46 @@ struct DevProblem {
     const int* lm_r0;       // CSR into lm_rows: tile-local rows
     const int* lm_rows;
     const int* lm_pair0;    // [n_lm + 1] landmark -> pairs
-    // assemble sources
-    const int* ublk_i;      // per upper block: block row / col
-    const int* ublk_j;
-    const int* hsrc0;       // CSR per upper block: entry << 2 | role
-    const int* hsrc;
-    const int* ssrc0;       // CSR per upper block: Schur entries
-    const int* ssrc;
-    const int* bsrc0;       // CSR per pose block: entry << 1 | side(0 = a, 1 = b)
-    const int* bsrc;
-    const int* kfp0;        // CSR per pose block: pairs
-    const int* kfp;
+    // partial-sum slabs are sorted by their reduction target, so every reduction below reads
+    // one contiguous range (coalesced) instead of chasing a source list
+    const int* seg_slot;    // per slab entry (segments, priors, velocity edges): 5 ints
+                            //   aa, ab, bb slot in hslab (-1 = none), ab transposed flag, -
+    const int* seg_gslot;   // per slab entry: ga, gb slot in gslab (-1 = none)
+    const int* hub_list;    // upper blocks that receive Hpp sources
+    int n_hub;
+    const int* hs0;         // [n_ublocks + 1] hslab range per upper block
+    const int* gs0;         // [n_pb + 1] gslab range per pose block
+    const int* ub_i;        // per upper block: block row / col
+    const int* ub_j;
+    const int* sslot;       // per Schur entry: slot in sslab
+    const int* ss0;         // [n_ublocks + 1] sslab range per upper block
+    const int* tkf_gslot;   // per tile KF: slot in gpslab (Schur g partials)
+    const int* gps0;        // [n_pb + 1] gpslab range per pose block
     // motion-prior / velocity edges
     const int* pri_a;
     const int* pri_b;
     const int* vel_kf;
-    int pri_entry0;         // slab entry of prior 0 (velocity edges follow)
+    int pri_entry0;         // slab entry index of prior 0 (velocity edges follow)
     double qcinv[36];
     double huber_mono, huber_stereo, huber_prior;
     // work buffers
     double* gpp;            // [n_gp][GPP_STRIDE]
     double* kfp_pose;       // [n_kf][KFP_STRIDE]
-    double* slab;
-    double* slab2;
+    double* hslab;          // [n_hslots][144] Hpp partial blocks, target-sorted
+    double* gslab;          // [n_gslots][12] b_p partials, target-sorted
+    double* sslab;          // [n_sslots][144] Schur partial blocks, target-sorted
+    double* gpslab;         // [n_gpslots][12] Schur rhs partials, target-sorted
+    double* Hblk;           // [n_ublocks][144] reduced Hpp (upper blocks)
+    double* Sblk;           // [n_ublocks][144] assembled reduced camera system (upper blocks)
+    double* Lm;             // [np][np] Cholesky factor (lower)
     double* Hpl;
     double* Hll;
     double* bl;
     double* Dinv;
-    double* V;
-    double* gpair;          // [n_pairs][12]
     double* S;              // [np][np]
     double* bp;             // [np]
     double* xsol;           // [np] rhs -> solution
+    double* yv;             // [np] forward-substituted rhs
     double* x;              // [np + 3 n_lm]
     double* chi_lin;        // [n_tiles + n_prior + n_vel]
     double* chi_eval;       // [n_tiles + n_prior + n_vel]
@@ -132,8 +138,8 @@ struct DevProblem {
 void launch_pair_prep(const DevProblem& P, const double* kst, hipStream_t s);
 void launch_linearize(const DevProblem& P, const double* kst, const double* lst, int write_res, hipStream_t s);
 void launch_prior_lin(const DevProblem& P, const double* kst, hipStream_t s);
-void launch_schur_prep(const DevProblem& P, double lambda, hipStream_t s);
-void launch_schur(const DevProblem& P, hipStream_t s);
+void launch_schur(const DevProblem& P, double lambda, hipStream_t s);
+void launch_hpp_reduce(const DevProblem& P, hipStream_t s);
 enum { ASM_SCHUR = 1, ASM_FULL = 2 };
 void launch_assemble(const DevProblem& P, double lambda, int flags, hipStream_t s);
 void launch_cholesky_solve(const DevProblem& P, hipStream_t s);

@@ -357,43 +357,54 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     const int n_segs = (int)seg_a.size();
     const int n_sent = (int)sent_l1.size();
 
-    // ---- slab entries (tile segments, priors, velocity edges) and the assemble source lists
+    // ---- partial-sum slots, sorted by reduction target (tile segments, priors, velocity edges)
     std::vector<int> ent_a(seg_a), ent_b(seg_b);
     for (auto& e : pri) { ent_a.push_back(H[e.kf_a]); ent_b.push_back(H[e.kf_b]); }
     for (int k : vel) { ent_a.push_back(-1); ent_b.push_back(H[k]); }
     const int n_entries = (int)ent_a.size();
     const int n_ublocks = n_pb * (n_pb + 1) / 2;
-    std::vector<int> ublk_i(n_ublocks), ublk_j(n_ublocks);
+    std::vector<int> ub_i(n_ublocks), ub_j(n_ublocks);
     for (int bi = 0; bi < n_pb; ++bi)
         for (int bj = bi; bj < n_pb; ++bj) {
             const int id = ublock_id(n_pb, bi, bj);
-            ublk_i[id] = bi; ublk_j[id] = bj;
+            ub_i[id] = bi; ub_j[id] = bj;
         }
-    std::vector<std::vector<int>> hs(n_ublocks), ss(n_ublocks), bs(n_pb), kps(n_pb);
+    std::vector<int> hcnt(n_ublocks + 1, 0), gcnt(n_pb + 1, 0);
     for (int en = 0; en < n_entries; ++en) {
         const int a = ent_a[en], b = ent_b[en];
-        if (a >= 0) { hs[ublock_id(n_pb, a, a)].push_back(en << 2 | R_AA); bs[a].push_back(en << 1 | 0); }
-        if (b >= 0) { hs[ublock_id(n_pb, b, b)].push_back(en << 2 | R_BB); bs[b].push_back(en << 1 | 1); }
-        if (a >= 0 && b >= 0) {
-            if (a < b) hs[ublock_id(n_pb, a, b)].push_back(en << 2 | R_AB);
-            else hs[ublock_id(n_pb, b, a)].push_back(en << 2 | R_ABT);
-        }
+        if (a >= 0) { hcnt[ublock_id(n_pb, a, a)]++; gcnt[a]++; }
+        if (b >= 0) { hcnt[ublock_id(n_pb, b, b)]++; gcnt[b]++; }
+        if (a >= 0 && b >= 0) hcnt[ublock_id(n_pb, std::min(a, b), std::max(a, b))]++;
     }
-    for (int s = 0; s < n_sent; ++s) ss[ublock_id(n_pb, sent_k1[s], sent_k2[s])].push_back(s);
-    for (int q = 0; q < n_pairs; ++q) kps[pair_kf[q]].push_back(q);
-    auto csr = [](const std::vector<std::vector<int>>& v, std::vector<int>& start, std::vector<int>& flat) {
-        start.assign(v.size() + 1, 0);
-        flat.clear();
-        for (size_t i = 0; i < v.size(); ++i) {
-            flat.insert(flat.end(), v[i].begin(), v[i].end());
-            start[i + 1] = (int)flat.size();
-        }
+    auto prefix = [](const std::vector<int>& c) {
+        std::vector<int> s(c.size(), 0);
+        for (size_t i = 1; i < c.size(); ++i) s[i] = s[i - 1] + c[i - 1];
+        return s;
     };
-    std::vector<int> hsrc0, hsrc, ssrc0, ssrc, bsrc0, bsrc, kfp0, kfpv;
-    csr(hs, hsrc0, hsrc);
-    csr(ss, ssrc0, ssrc);
-    csr(bs, bsrc0, bsrc);
-    csr(kps, kfp0, kfpv);
+    std::vector<int> hs0 = prefix(hcnt), gs0 = prefix(gcnt);
+    std::vector<int> hfill(hs0), gfill(gs0);
+    std::vector<int> seg_slot(5 * (size_t)std::max(n_entries, 1), -1), seg_gslot(2 * (size_t)std::max(n_entries, 1), -1);
+    for (int en = 0; en < n_entries; ++en) {
+        const int a = ent_a[en], b = ent_b[en];
+        int* sl = seg_slot.data() + 5 * (size_t)en;
+        sl[3] = 0; sl[4] = 0;
+        if (a >= 0) { sl[0] = hfill[ublock_id(n_pb, a, a)]++; seg_gslot[2 * (size_t)en] = gfill[a]++; }
+        if (a >= 0 && b >= 0) { sl[1] = hfill[ublock_id(n_pb, std::min(a, b), std::max(a, b))]++; sl[3] = a > b; }
+        if (b >= 0) { sl[2] = hfill[ublock_id(n_pb, b, b)]++; seg_gslot[2 * (size_t)en + 1] = gfill[b]++; }
+    }
+    std::vector<int> hub_list;
+    for (int u = 0; u < n_ublocks; ++u)
+        if (hcnt[u] > 0) hub_list.push_back(u);
+    // Schur partial blocks per (tile, KF pair) and rhs partials per (tile, KF)
+    std::vector<int> scnt(n_ublocks + 1, 0), gpcnt(n_pb + 1, 0);
+    for (int s = 0; s < n_sent; ++s) scnt[ublock_id(n_pb, sent_k1[s], sent_k2[s])]++;
+    for (int k : tkf_list) gpcnt[k]++;
+    std::vector<int> ss0 = prefix(scnt), gps0 = prefix(gpcnt);
+    std::vector<int> sfill(ss0), gpfill(gps0);
+    std::vector<int> sslot(std::max(n_sent, 1)), tkf_gslot(std::max((int)tkf_list.size(), 1));
+    for (int s = 0; s < n_sent; ++s) sslot[s] = sfill[ublock_id(n_pb, sent_k1[s], sent_k2[s])]++;
+    for (size_t t = 0; t < tkf_list.size(); ++t) tkf_gslot[t] = gpfill[tkf_list[t]]++;
+    const int n_hslots = hs0[n_ublocks], n_gslots = gs0[n_pb], n_sslots = ss0[n_ublocks], n_gpslots = gps0[n_pb];
 
     // ---- observations in device order
     std::vector<int> ob_meta(n_obs), ob_kfa(n_obs), ob_kfb(n_obs), ob_gp(n_obs), ob_lm(n_obs);
@@ -463,9 +474,11 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.pair_lm = dupload(p, pair_lm); D.pair_kf = dupload(p, pair_kf); D.pair_r0 = dupload(p, pair_r0);
     D.pair_rows = dupload(p, pair_rows); D.lm_r0 = dupload(p, lm_r0); D.lm_rows = dupload(p, lm_rows);
     D.lm_pair0 = dupload(p, lm_pair0);
-    D.ublk_i = dupload(p, ublk_i); D.ublk_j = dupload(p, ublk_j);
-    D.hsrc0 = dupload(p, hsrc0); D.hsrc = dupload(p, hsrc); D.ssrc0 = dupload(p, ssrc0); D.ssrc = dupload(p, ssrc);
-    D.bsrc0 = dupload(p, bsrc0); D.bsrc = dupload(p, bsrc); D.kfp0 = dupload(p, kfp0); D.kfp = dupload(p, kfpv);
+    D.seg_slot = dupload(p, seg_slot); D.seg_gslot = dupload(p, seg_gslot);
+    D.hub_list = dupload(p, hub_list); D.n_hub = (int)hub_list.size();
+    D.hs0 = dupload(p, hs0); D.gs0 = dupload(p, gs0); D.ub_i = dupload(p, ub_i); D.ub_j = dupload(p, ub_j);
+    D.sslot = dupload(p, sslot); D.ss0 = dupload(p, ss0); D.tkf_gslot = dupload(p, tkf_gslot);
+    D.gps0 = dupload(p, gps0);
     D.pri_a = dupload(p, pri_a); D.pri_b = dupload(p, pri_b); D.vel_kf = dupload(p, vel);
     D.pri_entry0 = n_segs;
     double qcinv[36];
@@ -476,17 +489,22 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.huber_prior = p->cfg.huber_prior;
     D.gpp = dalloc<double>(p, (size_t)GPP_STRIDE * std::max(D.n_gp, 1));
     D.kfp_pose = dalloc<double>(p, (size_t)KFP_STRIDE * std::max(n_kf, 1));
-    D.slab = dalloc<double>(p, (size_t)ENTRY * std::max(n_entries, 1));
-    D.slab2 = dalloc<double>(p, (size_t)144 * std::max(n_sent, 1));
+    D.hslab = dalloc<double>(p, (size_t)144 * std::max(n_hslots, 1));
+    D.gslab = dalloc<double>(p, (size_t)12 * std::max(n_gslots, 1));
+    D.sslab = dalloc<double>(p, (size_t)144 * std::max(n_sslots, 1));
+    D.gpslab = dalloc<double>(p, (size_t)12 * std::max(n_gpslots, 1));
+    D.Hblk = dalloc<double>(p, (size_t)144 * std::max(n_ublocks, 1));
+    HIPCHK(hipMemset(D.Hblk, 0, sizeof(double) * 144 * (size_t)std::max(n_ublocks, 1)));   // blocks without sources
+    D.Sblk = dalloc<double>(p, (size_t)144 * std::max(n_ublocks, 1));
+    D.Lm = dalloc<double>(p, (size_t)p->np * p->np + 1);
     D.Hpl = dalloc<double>(p, (size_t)36 * std::max(n_pairs, 1));
     D.Hll = dalloc<double>(p, (size_t)9 * std::max(nl, 1));
     D.bl = dalloc<double>(p, (size_t)3 * std::max(nl, 1));
     D.Dinv = dalloc<double>(p, (size_t)9 * std::max(nl, 1));
-    D.V = dalloc<double>(p, (size_t)36 * std::max(n_pairs, 1));
-    D.gpair = dalloc<double>(p, (size_t)12 * std::max(n_pairs, 1));
     D.S = dalloc<double>(p, (size_t)p->np * p->np + 1);
     D.bp = dalloc<double>(p, p->np + 1);
     D.xsol = dalloc<double>(p, p->np + 1);
+    D.yv = dalloc<double>(p, p->np + 1);
     D.x = dalloc<double>(p, p->np + 3 * (size_t)nl + 1);
     HIPCHK(hipMemset(D.x, 0, sizeof(double) * (p->np + 3 * (size_t)nl + 1)));   // BlockSolver::_x before any solve
     const int nchi = n_tiles + D.n_prior + D.n_vel;
@@ -520,6 +538,7 @@ void linearize(lba_problem* p, int write_res, bool timed = false) {
     launch_linearize(D, p->kst[p->cur], p->lst[p->cur], write_res, p->stream);
     if (timed) HIPCHK(hipEventRecord(p->ev[7], p->stream));
     launch_prior_lin(D, p->kst[p->cur], p->stream);
+    launch_hpp_reduce(D, p->stream);
     HIPCHK(hipGetLastError());
     p->linearized = true;
 }
@@ -529,8 +548,7 @@ void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs) {
     const DevProblem& D = p->D;
     const int nx = 1 - p->cur;
     HIPCHK(hipMemsetAsync(D.info, 0, sizeof(int), p->stream));
-    launch_schur_prep(D, lambda, p->stream);
-    launch_schur(D, p->stream);
+    launch_schur(D, lambda, p->stream);
     launch_assemble(D, lambda, ASM_SCHUR, p->stream);
     if (evs) HIPCHK(hipEventRecord(evs[0], p->stream));
     launch_cholesky_solve(D, p->stream);

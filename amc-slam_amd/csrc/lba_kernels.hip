@@ -8,8 +8,9 @@
 //                    Hpl blocks and Hll/bl (BlockSolver::buildSystem, block_solver.hpp:502-560;
 //                    edge quadratic forms base_multi_edge.hpp:170-222)
 //   k_prior_lin      EdgeGaussianPrior / EdgeVelocity quadratic forms (src/G2oTypes.cc:100-118)
-//   k_schur_prep     Dinv = (Hll + lambda I)^-1, V = Hpl Dinv, g = V bl      (block_solver.hpp:381-401)
-//   k_schur          per tile: S partials V(k1) Hpl(k2)^T for every KF pair   (block_solver.hpp:403-430)
+//   k_hpp_reduce     Hpp / b_p from the target-sorted tile partials (once per iteration)
+//   k_schur          per tile: Dinv = (Hll + lambda I)^-1, V = Hpl Dinv, g = V bl, S partials
+//                    V(k1) Hpl(k2)^T and rhs partials                   (block_solver.hpp:381-430)
 //   k_assemble       S = Hpp + lambda I - sum partials, bS = b_p - sum g     (block_solver.hpp:432-445)
 //   k_chol_*         blocked Cholesky + forward/back substitution of S     (linear_solver_dense.h:65-113)
 //   k_update         landmark back-substitution + oplus into the trial state (block_solver.hpp:461-482,
@@ -178,19 +179,30 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, const doub
             for (int q = 0; q < 16; ++q) part[(rg * 32 + blk) * 16 + q] = acc[q];
         }
         __syncthreads();
-        double* E = P.slab + (size_t)sg * ENTRY;
+        const int* sl = P.seg_slot + 5 * (size_t)sg;
+        const int* gl = P.seg_gslot + 2 * (size_t)sg;
         for (int out = tid; out < 27 * 16; out += TILE_OBS) {
             const int b = out >> 4, q = out & 15;
             const double v = part[(0 * 32 + b) * 16 + q] + part[(1 * 32 + b) * 16 + q] +
                              part[(2 * 32 + b) * 16 + q] + part[(3 * 32 + b) * 16 + q];
             const int i = 4 * c_bi[b] + (q >> 2), j = 4 * c_bj[b] + (q & 3);
-            if (j == 24) {
-                if (i < 12) E[E_GA + i] = -v;           // b = -J^T rho' Omega e
-                else if (i < 24) E[E_GB + i - 12] = -v;
+            if (j == 24) {   // b = -J^T rho' Omega e
+                if (i < 12) { if (gl[0] >= 0) P.gslab[(size_t)gl[0] * 12 + i] = -v; }
+                else if (i < 24) { if (gl[1] >= 0) P.gslab[(size_t)gl[1] * 12 + i - 12] = -v; }
             } else if (j < 24 && i <= j) {
-                if (j < 12) { E[E_AA + i * 12 + j] = v; E[E_AA + j * 12 + i] = v; }
-                else if (i >= 12) { E[E_BB + (i - 12) * 12 + (j - 12)] = v; E[E_BB + (j - 12) * 12 + (i - 12)] = v; }
-                else E[E_AB + i * 12 + (j - 12)] = v;
+                if (j < 12) {
+                    if (sl[0] >= 0) { double* H = P.hslab + (size_t)sl[0] * 144; H[i * 12 + j] = v; H[j * 12 + i] = v; }
+                } else if (i >= 12) {
+                    if (sl[2] >= 0) {
+                        double* H = P.hslab + (size_t)sl[2] * 144;
+                        H[(i - 12) * 12 + (j - 12)] = v;
+                        H[(j - 12) * 12 + (i - 12)] = v;
+                    }
+                } else if (sl[1] >= 0) {
+                    double* H = P.hslab + (size_t)sl[1] * 144;
+                    if (sl[3]) H[(j - 12) * 12 + i] = v;   // block stored for (b, a): transposed
+                    else H[i * 12 + (j - 12)] = v;
+                }
             }
         }
         __syncthreads();
@@ -249,7 +261,9 @@ __global__ __launch_bounds__(64) void k_prior_lin(DevProblem P, const double* __
     __shared__ double Ji[144], Jj[144], WJi[144], WJj[144], Om[144], e[12], We[12];
     __shared__ double wsh;
     const int idx = blockIdx.x, tid = threadIdx.x;
-    double* E = P.slab + (size_t)(P.pri_entry0 + idx) * ENTRY;
+    const int ent = P.pri_entry0 + idx;
+    const int* sl = P.seg_slot + 5 * (size_t)ent;
+    const int* gl = P.seg_gslot + 2 * (size_t)ent;
     if (idx < P.n_prior) {
         if (tid == 0) {
             const double* ka = kst + (size_t)P.pri_a[idx] * KF_STRIDE;
@@ -282,20 +296,26 @@ __global__ __launch_bounds__(64) void k_prior_lin(DevProblem P, const double* __
             We[tid] = w1 * s;
         }
         __syncthreads();
-        for (int t = tid; t < ENTRY; t += 64) {
+        // aa = Ji^T W Ji, ab = Ji^T W Jj, bb = Jj^T W Jj, ga/gb = -J^T W e (base_binary_edge.hpp:54-120)
+        for (int t = tid; t < 456; t += 64) {
             if (t < 432) {
                 const int bk = t / 144, ij = t % 144, i = ij / 12, j = ij % 12;
+                const int slot = sl[bk == 0 ? 0 : (bk == 1 ? 1 : 2)];
+                if (slot < 0) continue;
                 const double* A = (bk == 2) ? Jj : Ji;
                 const double* B = (bk == 0) ? WJi : WJj;
                 double s = 0.0;
                 for (int k = 0; k < 12; ++k) s += A[k * 12 + i] * B[k * 12 + j];
-                E[t] = s;
+                double* H = P.hslab + (size_t)slot * 144;
+                if (bk == 1 && sl[3]) H[j * 12 + i] = s;
+                else H[i * 12 + j] = s;
             } else {
                 const int side = (t - 432) / 12, i = (t - 432) % 12;
+                if (gl[side] < 0) continue;
                 const double* A = side ? Jj : Ji;
                 double s = 0.0;
                 for (int k = 0; k < 12; ++k) s += A[k * 12 + i] * We[k];
-                E[t] = -s;
+                P.gslab[(size_t)gl[side] * 12 + i] = -s;
             }
         }
     } else {
@@ -303,66 +323,92 @@ __global__ __launch_bounds__(64) void k_prior_lin(DevProblem P, const double* __
         const int v = idx - P.n_prior;
         const double ev = kst[(size_t)P.vel_kf[v] * KF_STRIDE + 7 + 2];
         const double q22 = P.qcinv[2 * 6 + 2];
-        for (int t = tid; t < ENTRY; t += 64) E[t] = 0.0;
+        double* H = P.hslab + (size_t)sl[2] * 144;
+        for (int t = tid; t < 144; t += 64) H[t] = (t == 8 * 12 + 8) ? q22 : 0.0;
+        if (tid < 12) P.gslab[(size_t)gl[1] * 12 + tid] = (tid == 8) ? -q22 * ev : 0.0;
+        if (tid == 0) P.chi_lin[P.n_tiles + idx] = ev * (q22 * ev);
+    }
+}
+
+// Hpp / b_p reduction (once per LM iteration): each upper block sums its contiguous slab range
+__global__ __launch_bounds__(144 * RED_GROUPS) void k_hpp_reduce(DevProblem P) {
+    __shared__ double red[144 * RED_GROUPS];
+    const int tid = threadIdx.x;
+    if ((int)blockIdx.x < P.n_hub) {
+        const int ub = P.hub_list[blockIdx.x];
+        const int e = tid % 144, g = tid / 144;
+        double v = 0.0;
+        for (int s = P.hs0[ub] + g; s < P.hs0[ub + 1]; s += RED_GROUPS) v += P.hslab[(size_t)s * 144 + e];
+        red[tid] = v;
         __syncthreads();
-        if (tid == 0) {
-            E[E_BB + 8 * 12 + 8] = q22;
-            E[E_GB + 8] = -q22 * ev;
-            P.chi_lin[P.n_tiles + idx] = ev * (q22 * ev);
+        if (g == 0) P.Hblk[(size_t)ub * 144 + e] = red[e] + red[144 + e] + red[288 + e] + red[432 + e];
+    } else {
+        const int k = blockIdx.x - P.n_hub;
+        const int e = tid % 12, g = tid / 12;   // 48 groups
+        double v = 0.0;
+        for (int s = P.gs0[k] + g; s < P.gs0[k + 1]; s += 48) v += P.gslab[(size_t)s * 12 + e];
+        red[tid] = v;
+        __syncthreads();
+        if (tid < 12) {
+            double t = 0.0;
+            for (int q = 0; q < 48; ++q) t += red[q * 12 + tid];
+            P.bp[12 * k + tid] = t;
         }
     }
 }
 
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_schur_prep(DevProblem P, double lambda) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.n_pairs + P.n_lm) return;
-    const int l = i < P.n_pairs ? P.pair_lm[i] : i - P.n_pairs;
-    double H[9], D[9];
-    for (int q = 0; q < 9; ++q) H[q] = P.Hll[(size_t)l * 9 + q];
-    H[0] += lambda; H[4] += lambda; H[8] += lambda;   // setLambda on Hll (block_solver.hpp:580-587)
-    inv3(H, D);
-    if (i >= P.n_pairs) {
-        for (int q = 0; q < 9; ++q) P.Dinv[(size_t)l * 9 + q] = D[q];
-        return;
-    }
-    const double* B = P.Hpl + (size_t)i * 36;
-    double* Vo = P.V + (size_t)i * 36;
-    const double b0 = P.bl[3 * (size_t)l], b1 = P.bl[3 * (size_t)l + 1], b2 = P.bl[3 * (size_t)l + 2];
-    for (int r = 0; r < 12; ++r) {
-        const double h0 = B[r * 3], h1 = B[r * 3 + 1], h2 = B[r * 3 + 2];
-        const double v0 = h0 * D[0] + h1 * D[3] + h2 * D[6];
-        const double v1 = h0 * D[1] + h1 * D[4] + h2 * D[7];
-        const double v2 = h0 * D[2] + h1 * D[5] + h2 * D[8];
-        Vo[r * 3] = v0; Vo[r * 3 + 1] = v1; Vo[r * 3 + 2] = v2;
-        P.gpair[(size_t)i * 12 + r] = v0 * b0 + v1 * b1 + v2 * b2;
-    }
-}
-
-__global__ __launch_bounds__(128) void k_schur(DevProblem P) {
+// Landmark elimination for one tile of landmarks (BlockSolver::solve's Schur loop,
+// block_solver.hpp:381-430): Dinv = (Hll + lambda I)^-1 (Eigen 3x3 adjugate inverse), V = Hpl Dinv,
+// g = V bl, then S partials V(k1) Hpl(k2)^T for every KF pair the tile's landmarks couple and rhs
+// partials sum g per KF.  Everything stays in LDS; Dinv is kept for the back-substitution.
+__global__ __launch_bounds__(256) void k_schur(DevProblem P, double lambda) {
     __shared__ double Vs[TILE_PAIRS * 36];
     __shared__ double Hs[TILE_PAIRS * 36];
+    __shared__ double gs[TILE_PAIRS * 12];
+    __shared__ double Dl[TILE_LMS * 12];   // Dinv (9) + bl (3) per landmark
     __shared__ short slot[TILE_LMS * TILE_KF];
+    __shared__ signed char pl[TILE_PAIRS]; // tile-local KF index of each pair
     __shared__ int kfl[TILE_KF];
     const int tile = blockIdx.x, tid = threadIdx.x;
     const int pair0 = P.tile_pair0[tile], npair = P.tile_npair[tile];
     const int lm0 = P.tile_lm0[tile], nlm = P.tile_nlm[tile];
     const int kf0 = P.tile_kf0[tile], nkf = P.tile_nkf[tile];
-    for (int t = tid; t < npair * 36; t += 128) {
-        Vs[t] = P.V[(size_t)pair0 * 36 + t];
-        Hs[t] = P.Hpl[(size_t)pair0 * 36 + t];
-    }
-    for (int t = tid; t < TILE_LMS * TILE_KF; t += 128) slot[t] = -1;
+    for (int t = tid; t < npair * 36; t += 256) Hs[t] = P.Hpl[(size_t)pair0 * 36 + t];
+    for (int t = tid; t < TILE_LMS * TILE_KF; t += 256) slot[t] = -1;
     if (tid < nkf) kfl[tid] = P.tkf_list[kf0 + tid];
+    if (tid < nlm) {
+        const int l = lm0 + tid;
+        double H[9], D[9];
+        for (int q = 0; q < 9; ++q) H[q] = P.Hll[(size_t)l * 9 + q];
+        H[0] += lambda; H[4] += lambda; H[8] += lambda;   // setLambda on Hll (block_solver.hpp:580-587)
+        inv3(H, D);
+        for (int q = 0; q < 9; ++q) { Dl[tid * 12 + q] = D[q]; P.Dinv[(size_t)l * 9 + q] = D[q]; }
+        for (int q = 0; q < 3; ++q) Dl[tid * 12 + 9 + q] = P.bl[(size_t)l * 3 + q];
+    }
     __syncthreads();
-    for (int t = tid; t < npair; t += 128) {
+    for (int t = tid; t < npair; t += 256) {
         const int p = pair0 + t, m = P.pair_lm[p] - lm0, k = P.pair_kf[p];
+        int lk = 0;
         for (int l = 0; l < nkf; ++l)
-            if (kfl[l] == k) slot[m * TILE_KF + l] = (short)t;
+            if (kfl[l] == k) lk = l;
+        slot[m * TILE_KF + lk] = (short)t;
+        pl[t] = (signed char)lk;
+    }
+    // V = Hpl Dinv, g = V bl : one (pair, row) per task
+    for (int task = tid; task < npair * 12; task += 256) {
+        const int t = task / 12, r = task % 12;
+        const int m = P.pair_lm[pair0 + t] - lm0;
+        const double* D = Dl + m * 12;
+        const double h0 = Hs[t * 36 + r * 3], h1 = Hs[t * 36 + r * 3 + 1], h2 = Hs[t * 36 + r * 3 + 2];
+        const double v0 = h0 * D[0] + h1 * D[3] + h2 * D[6];
+        const double v1 = h0 * D[1] + h1 * D[4] + h2 * D[7];
+        const double v2 = h0 * D[2] + h1 * D[5] + h2 * D[8];
+        Vs[t * 36 + r * 3] = v0; Vs[t * 36 + r * 3 + 1] = v1; Vs[t * 36 + r * 3 + 2] = v2;
+        gs[t * 12 + r] = v0 * D[9] + v1 * D[10] + v2 * D[11];
     }
     __syncthreads();
     const int sent0 = P.tile_sent0[tile], nsent = P.tile_nsent[tile];
-    for (int task = tid; task < nsent * 9; task += 128) {
+    for (int task = tid; task < nsent * 9; task += 256) {
         const int e = task / 9, sub = task % 9, sr = sub / 3, sc = sub % 3;
         const int l1 = P.sent_l1[sent0 + e], l2 = P.sent_l2[sent0 + e];
         double acc[16];
@@ -379,187 +425,270 @@ __global__ __launch_bounds__(128) void k_schur(DevProblem P) {
                 for (int l = 0; l < 4; ++l)
                     acc[k * 4 + l] += v[k * 3] * h[l * 3] + v[k * 3 + 1] * h[l * 3 + 1] + v[k * 3 + 2] * h[l * 3 + 2];
         }
-        double* o = P.slab2 + (size_t)(sent0 + e) * 144;
+        double* o = P.sslab + (size_t)P.sslot[sent0 + e] * 144;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
 #pragma unroll
             for (int l = 0; l < 4; ++l) o[(4 * sr + k) * 12 + 4 * sc + l] = acc[k * 4 + l];
     }
-}
-
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_assemble(DevProblem P, double lambda, int flags) {
-    const int b = blockIdx.x, t = threadIdx.x;
-    const int n = P.np;
-    if (b < P.n_ublocks) {
-        if (t >= 144) return;
-        const int bi = P.ublk_i[b], bj = P.ublk_j[b];
-        const int i = t / 12, j = t % 12;
+    // rhs partials: sum over the tile's pairs of g = V bl for every tile KF (block_solver.hpp:395-401)
+    for (int task = tid; task < nkf * 12; task += 256) {
+        const int l = task / 12, r = task % 12;
         double v = 0.0;
-        for (int q = P.hsrc0[b]; q < P.hsrc0[b + 1]; ++q) {
-            const int code = P.hsrc[q];
-            const double* E = P.slab + (size_t)(code >> 2) * ENTRY;
-            switch (code & 3) {
-                case R_AA: v += E[E_AA + i * 12 + j]; break;
-                case R_BB: v += E[E_BB + i * 12 + j]; break;
-                case R_AB: v += E[E_AB + i * 12 + j]; break;
-                default: v += E[E_AB + j * 12 + i]; break;
-            }
-        }
-        if (bi == bj && i == j) v += lambda;
-        if (flags & ASM_SCHUR)
-            for (int q = P.ssrc0[b]; q < P.ssrc0[b + 1]; ++q) v -= P.slab2[(size_t)P.ssrc[q] * 144 + i * 12 + j];
-        P.S[(size_t)(12 * bj + j) * n + 12 * bi + i] = v;
-        if (flags & ASM_FULL) P.S[(size_t)(12 * bi + i) * n + 12 * bj + j] = v;
-    } else {
-        const int k = b - P.n_ublocks;
-        if (t >= 12) return;
-        double v = 0.0;
-        for (int q = P.bsrc0[k]; q < P.bsrc0[k + 1]; ++q) {
-            const int code = P.bsrc[q];
-            v += P.slab[(size_t)(code >> 1) * ENTRY + ((code & 1) ? E_GB : E_GA) + t];
-        }
-        P.bp[12 * k + t] = v;
-        if (flags & ASM_SCHUR)
-            for (int q = P.kfp0[k]; q < P.kfp0[k + 1]; ++q) v -= P.gpair[(size_t)P.kfp[q] * 12 + t];
-        P.xsol[12 * k + t] = v;
+        for (int t = 0; t < npair; ++t)
+            if (pl[t] == l) v += gs[t * 12 + r];
+        P.gpslab[(size_t)P.tkf_gslot[kf0 + l] * 12 + r] = v;
     }
 }
 
-// ------------------------------------------------------------------------------------------------
-// Dense Cholesky S = L L^T (lower, row-major, in place), with the forward substitution of the
-// right-hand side folded into the panels.  A non-positive pivot sets *info (LDLT !isPositive).
-constexpr int PANEL_ROWS = 64;
-
-__global__ __launch_bounds__(64) void k_chol_panel(double* __restrict__ A, int n, int p, int nbp, int* info,
-                                                   double* __restrict__ b) {
-    __shared__ double L[CHOL_NB][CHOL_NB + 1];
-    const int tid = threadIdx.x, w = blockIdx.x;
-    for (int t = tid; t < CHOL_NB * CHOL_NB; t += 64) {
-        const int i = t / CHOL_NB, j = t % CHOL_NB;
-        L[i][j] = (i < nbp && j <= i) ? A[(size_t)(p + i) * n + p + j] : 0.0;
-    }
-    __syncthreads();
-    for (int j = 0; j < nbp; ++j) {
-        if (tid == 0) {
-            double d = L[j][j];
-            if (!(d > 0.0)) {
-                if (w == 0) *info = 1 + p + j;
-                d = 1.0;
-            }
-            L[j][j] = sqrt(d);
-        }
-        __syncthreads();
-        const double ljj = L[j][j];
-        for (int i = j + 1 + tid; i < nbp; i += 64) L[i][j] /= ljj;
-        __syncthreads();
-        const int m = nbp - j - 1;
-        for (int t = tid; t < m * m; t += 64) {
-            const int i = j + 1 + t / m, k = j + 1 + t % m;
-            if (k <= i) L[i][k] -= L[i][j] * L[k][j];
-        }
-        __syncthreads();
-    }
-    if (w == 0) {
-        for (int t = tid; t < nbp * nbp; t += 64) {
-            const int i = t / nbp, j = t % nbp;
-            if (j <= i) A[(size_t)(p + i) * n + p + j] = L[i][j];
-        }
-        if (tid == 0)
-            for (int i = 0; i < nbp; ++i) {
-                double s = b[p + i];
-                for (int k = 0; k < i; ++k) s -= L[i][k] * b[p + k];
-                b[p + i] = s / L[i][i];
-            }
-        return;
-    }
-    const int r = p + nbp + (w - 1) * PANEL_ROWS + tid;
-    if (r >= n) return;
-    double xr[CHOL_NB];
-    double* Ar = A + (size_t)r * n + p;
-#pragma unroll
-    for (int j = 0; j < CHOL_NB; ++j) xr[j] = j < nbp ? Ar[j] : 0.0;
-#pragma unroll
-    for (int j = 0; j < CHOL_NB; ++j) {
-        if (j < nbp) {
-            double s = xr[j];
-#pragma unroll
-            for (int k = 0; k < j; ++k) s -= xr[k] * L[j][k];
-            xr[j] = s / L[j][j];
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < CHOL_NB; ++j)
-        if (j < nbp) Ar[j] = xr[j];
-}
-
-__global__ __launch_bounds__(256) void k_chol_update(double* __restrict__ A, int n, int p, int nbp, double* __restrict__ b) {
-    __shared__ double Li[32][CHOL_NB + 1], Lj[32][CHOL_NB + 1];
-    const int q = p + nbp;
-    const int bid = blockIdx.x;
-    int ti = (int)((sqrt(8.0 * bid + 1.0) - 1.0) * 0.5);
-    while ((ti + 1) * (ti + 2) / 2 <= bid) ++ti;
-    while (ti * (ti + 1) / 2 > bid) --ti;
-    const int tj = bid - ti * (ti + 1) / 2;
-    const int r0 = q + ti * 32, c0 = q + tj * 32;
+__global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, double lambda, int flags) {
+    __shared__ double red[144 * RED_GROUPS];
     const int tid = threadIdx.x;
-    for (int t = tid; t < 32 * CHOL_NB; t += 256) {
-        const int r = t / CHOL_NB, k = t % CHOL_NB;
-        Li[r][k] = (r0 + r < n && k < nbp) ? A[(size_t)(r0 + r) * n + p + k] : 0.0;
-        Lj[r][k] = (c0 + r < n && k < nbp) ? A[(size_t)(c0 + r) * n + p + k] : 0.0;
+    const int n = P.np;
+    if ((int)blockIdx.x < P.n_ublocks) {
+        const int ub = blockIdx.x;
+        const int bi = P.ub_i[ub], bj = P.ub_j[ub];
+        const int e = tid % 144, g = tid / 144;
+        double v = 0.0;
+        if (g == 0) {
+            v = P.Hblk[(size_t)ub * 144 + e];
+            if (bi == bj && e % 13 == 0) v += lambda;   // setLambda on Hpp (block_solver.hpp:573-579)
+        }
+        if (flags & ASM_SCHUR)
+            for (int s = P.ss0[ub] + g; s < P.ss0[ub + 1]; s += RED_GROUPS) v -= P.sslab[(size_t)s * 144 + e];
+        red[tid] = v;
+        __syncthreads();
+        if (g == 0) {
+            const double t = red[e] + red[144 + e] + red[288 + e] + red[432 + e];
+            const int i = e / 12, j = e % 12;
+            P.Sblk[(size_t)ub * 144 + e] = t;
+            P.S[(size_t)(12 * bj + j) * n + 12 * bi + i] = t;
+            if (flags & ASM_FULL) P.S[(size_t)(12 * bi + i) * n + 12 * bj + j] = t;
+        }
+    } else {
+        const int k = blockIdx.x - P.n_ublocks;
+        const int e = tid % 12, g = tid / 12;   // 48 groups
+        double v = (g == 0) ? P.bp[12 * k + e] : 0.0;
+        if (flags & ASM_SCHUR)
+            for (int s = P.gps0[k] + g; s < P.gps0[k + 1]; s += 48) v -= P.gpslab[(size_t)s * 12 + e];
+        red[tid] = v;
+        __syncthreads();
+        if (tid < 12) {
+            double t = 0.0;
+            for (int q = 0; q < 48; ++q) t += red[q * 12 + tid];
+            P.xsol[12 * k + tid] = t;   // bS = b_p - sum Hpl Dinv bl
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Dense Cholesky S = L L^T (right-looking, panel width CHOL_NB, one launch per panel).
+// Every workgroup owns one lower tile of the trailing matrix; it factors the panel's diagonal
+// block itself (one wave, rows in registers) and solves the panel rows its tile needs, so a
+// launch has no inter-workgroup communication.  The final factor goes to Lm, the running
+// right-hand side b is forward-substituted on the fly (y -> yv).  A non-positive pivot sets *info
+// (the LDLT !isPositive failure of linear_solver_dense.h:108-112).
+constexpr int CNB = CHOL_NB;
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    const unsigned long long u = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, lane);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), lane);
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restrict__ A, double* __restrict__ Lm,
+                                                   double* __restrict__ b, double* __restrict__ yv, int* info) {
+    __shared__ double D[CNB][CNB + 1];
+    __shared__ double Pi[CNB][CNB + 1];
+    __shared__ double Pj[CNB][CNB + 1];
+    __shared__ double colb[CNB];
+    __shared__ double yp[CNB];
+    const int tid = threadIdx.x;
+    const int nbp = min(CNB, n - p), q = p + nbp, m = n - q, nt = (m + CNB - 1) / CNB;
+    int ti = 0, tj = 0;
+    if (nt > 0) {
+        const int bid = blockIdx.x;
+        ti = (int)((sqrt(8.0 * bid + 1.0) - 1.0) * 0.5);
+        while ((ti + 1) * (ti + 2) / 2 <= bid) ++ti;
+        while (ti * (ti + 1) / 2 > bid) --ti;
+        tj = bid - ti * (ti + 1) / 2;
+    }
+    // (1) diagonal block: one row per lane of wave 0; the pivot column is broadcast through LDS
+    //     (one write per lane, then all reads issued back to back before any use)
+    if (tid < 64) {
+        double row[CNB];
+#pragma unroll
+        for (int c = 0; c < CNB; ++c) row[c] = (tid < nbp && c <= tid) ? A[(size_t)(p + tid) * n + p + c] : 0.0;
+        bool bad = false;
+#pragma unroll
+        for (int j = 0; j < CNB; ++j) {
+            if (j < nbp) {
+                double d = readlane_d(row[j], j);
+                if (!(d > 0.0)) { bad = true; d = 1.0; }
+                const double ljj = sqrt(d), inv = 1.0 / ljj;
+                const double lij = (tid == j) ? ljj : ((tid > j && tid < nbp) ? row[j] * inv : 0.0);
+                row[j] = lij;
+                if (tid < CNB) colb[tid] = lij;
+                wave_sync();
+                double cb[CNB];
+#pragma unroll
+                for (int k = j + 1; k < CNB; ++k) cb[k] = colb[k];
+#pragma unroll
+                for (int k = j + 1; k < CNB; ++k)
+                    if (tid >= k && tid < nbp) row[k] -= lij * cb[k];
+                wave_sync();
+            }
+        }
+        if (tid < CNB)
+#pragma unroll
+            for (int c = 0; c < CNB; ++c) D[tid][c] = row[c];
+        if (bad && tid == 0 && blockIdx.x == 0) *info = 1 + p;
     }
     __syncthreads();
-    const int tr = tid >> 4, tc = tid & 15;
-    double a00 = 0, a01 = 0, a10 = 0, a11 = 0;
+    // (2) panel rows of tiles ti / tj: x D^T = a (triangular solve per row, D rows read in one burst)
+    if (tid < 2 * CNB && nt > 0) {
+        const int which = tid / CNB, i = tid % CNB;
+        if (!(which == 1 && tj == ti)) {
+            const int r = q + (which ? tj : ti) * CNB + i;
+            double x[CNB];
+#pragma unroll
+            for (int c = 0; c < CNB; ++c) x[c] = (r < n && c < nbp) ? A[(size_t)r * n + p + c] : 0.0;
+#pragma unroll
+            for (int j = 0; j < CNB; ++j)
+                if (j < nbp) {
+                    double s = x[j];
+#pragma unroll
+                    for (int c = 0; c < j; ++c) s -= x[c] * D[j][c];
+                    x[j] = s / D[j][j];
+                }
+            double (*dst)[CNB + 1] = which ? Pj : Pi;
+#pragma unroll
+            for (int c = 0; c < CNB; ++c) dst[i][c] = (r < n) ? x[c] : 0.0;
+        }
+    }
+    // y_p = D^-1 b_p by wave 3: lane l holds b_{p+l}
+    const bool need_y = (ti == tj) || blockIdx.x == 0;
+    if (tid >= 192 && need_y) {
+        const int l = tid - 192;
+        double bl = (l < nbp) ? b[p + l] : 0.0;
+        const double dll = (l < nbp) ? D[l][l] : 1.0;
+        double drow[CNB];
+#pragma unroll
+        for (int c = 0; c < CNB; ++c) drow[c] = (l < CNB) ? D[l & (CNB - 1)][c] : 0.0;
+#pragma unroll
+        for (int j = 0; j < CNB; ++j)
+            if (j < nbp) {
+                const double yj = readlane_d(bl, j) / readlane_d(dll, j);
+                if (l == j) bl = yj;
+                else if (l > j) bl -= drow[j] * yj;
+            }
+        if (l < nbp) yp[l] = bl;
+    }
+    __syncthreads();
+    if (blockIdx.x == 0) {
+        for (int t = tid; t < nbp * nbp; t += 256) {
+            const int i = t / nbp, c = t % nbp;
+            if (c <= i) Lm[(size_t)(p + i) * n + p + c] = D[i][c];
+        }
+        if (tid < nbp) yv[p + tid] = yp[tid];
+    }
+    if (nt == 0) return;
+    const double (*Qj)[CNB + 1] = (ti == tj) ? Pi : Pj;
+    // (3) trailing tile update A(ti, tj) -= Pi Pj^T
+    {
+        const int tr = tid >> 4, tc = tid & 15;
+        double a00 = 0, a01 = 0, a10 = 0, a11 = 0;
 #pragma unroll 8
-    for (int k = 0; k < CHOL_NB; ++k) {
-        const double x0 = Li[2 * tr][k], x1 = Li[2 * tr + 1][k];
-        const double y0 = Lj[2 * tc][k], y1 = Lj[2 * tc + 1][k];
-        a00 += x0 * y0; a01 += x0 * y1; a10 += x1 * y0; a11 += x1 * y1;
+        for (int k = 0; k < CNB; ++k) {
+            const double x0 = Pi[2 * tr][k], x1 = Pi[2 * tr + 1][k];
+            const double y0 = Qj[2 * tc][k], y1 = Qj[2 * tc + 1][k];
+            a00 += x0 * y0; a01 += x0 * y1; a10 += x1 * y0; a11 += x1 * y1;
+        }
+        const int ra = q + ti * CNB + 2 * tr, ca = q + tj * CNB + 2 * tc;
+        if (ra < n) {
+            if (ca < n) A[(size_t)ra * n + ca] -= a00;
+            if (ca + 1 < n) A[(size_t)ra * n + ca + 1] -= a01;
+        }
+        if (ra + 1 < n) {
+            if (ca < n) A[(size_t)(ra + 1) * n + ca] -= a10;
+            if (ca + 1 < n) A[(size_t)(ra + 1) * n + ca + 1] -= a11;
+        }
     }
-    const int ra = r0 + 2 * tr, ca = c0 + 2 * tc;
-    if (ra < n) {
-        if (ca < n) A[(size_t)ra * n + ca] -= a00;
-        if (ca + 1 < n) A[(size_t)ra * n + ca + 1] -= a01;
-    }
-    if (ra + 1 < n) {
-        if (ca < n) A[(size_t)(ra + 1) * n + ca] -= a10;
-        if (ca + 1 < n) A[(size_t)(ra + 1) * n + ca + 1] -= a11;
-    }
-    if (ti == tj && tid < 32 && r0 + tid < n) {
-        double s = 0.0;
-        for (int k = 0; k < nbp; ++k) s += Li[tid][k] * b[p + k];
-        b[r0 + tid] -= s;
+    // (4) the tj == 0 workgroups publish the panel rows of L
+    if (tj == 0)
+        for (int t = tid; t < CNB * nbp; t += 256) {
+            const int i = t / nbp, c = t % nbp;
+            const int r = q + ti * CNB + i;
+            if (r < n) Lm[(size_t)r * n + p + c] = Pi[i][c];
+        }
+    // (5) forward substitution of the trailing right-hand side
+    if (ti == tj && tid < CNB) {
+        const int r = q + ti * CNB + tid;
+        if (r < n) {
+            double s = 0.0;
+            for (int c = 0; c < nbp; ++c) s += Pi[tid][c] * yp[c];
+            b[r] -= s;
+        }
     }
 }
 
 constexpr int CHOL_MAXN = 6144;
 
-// L^T x = y, single workgroup; x overwrites b
-__global__ __launch_bounds__(256) void k_chol_backsolve(const double* __restrict__ A, int n, double* __restrict__ b) {
+// L^T x = y, single workgroup, diagonal blocks staged in LDS; x -> out
+__global__ __launch_bounds__(256) void k_chol_backsolve(const double* __restrict__ Lm, int n,
+                                                        const double* __restrict__ yv, double* __restrict__ out) {
     __shared__ double y[CHOL_MAXN];
+    __shared__ double Dg[32][33];
     __shared__ double xb[32];
     const int tid = threadIdx.x;
-    for (int t = tid; t < n; t += 256) y[t] = b[t];
-    __syncthreads();
+    for (int t = tid; t < n; t += 256) y[t] = yv[t];
     const int nblk = (n + 31) / 32;
     for (int blk = nblk - 1; blk >= 0; --blk) {
         const int r0 = blk * 32, len = min(32, n - r0);
+        for (int t = tid; t < len * len; t += 256) {
+            const int i = t / len, c = t % len;
+            Dg[i][c] = (c <= i) ? Lm[(size_t)(r0 + i) * n + r0 + c] : 0.0;
+        }
+        __syncthreads();
         if (tid < 64) {
             double yl = tid < len ? y[r0 + tid] : 0.0;
             for (int i = len - 1; i >= 0; --i) {
-                const double xi = __shfl(yl, i, 64) / A[(size_t)(r0 + i) * n + r0 + i];
-                if (tid < i) yl -= A[(size_t)(r0 + i) * n + r0 + tid] * xi;
+                const double xi = __shfl(yl, i, 64) / Dg[i][i];
+                if (tid < i) yl -= Dg[i][tid] * xi;
                 if (tid == i) yl = xi;
             }
             if (tid < len) xb[tid] = yl;
         }
         __syncthreads();
-        if (tid < len) b[r0 + tid] = xb[tid];
-        for (int k = tid; k < r0; k += 256) {
-            double s = 0.0;
-            for (int i = 0; i < len; ++i) s += A[(size_t)(r0 + i) * n + k] * xb[i];
-            y[k] -= s;
+        if (tid < len) out[r0 + tid] = xb[tid];
+        if (len == 32) {
+            double xr[32];
+#pragma unroll
+            for (int i = 0; i < 32; ++i) xr[i] = xb[i];
+            for (int k = tid; k < r0; k += 256) {
+                double lv[32];
+#pragma unroll
+                for (int i = 0; i < 32; ++i) lv[i] = Lm[(size_t)(r0 + i) * n + k];
+                double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+#pragma unroll
+                for (int i = 0; i < 32; i += 4) {
+                    s0 += lv[i] * xr[i]; s1 += lv[i + 1] * xr[i + 1]; s2 += lv[i + 2] * xr[i + 2]; s3 += lv[i + 3] * xr[i + 3];
+                }
+                y[k] -= (s0 + s1) + (s2 + s3);
+            }
+        } else {
+            for (int k = tid; k < r0; k += 256) {
+                double s = 0.0;
+                for (int i = 0; i < len; ++i) s += Lm[(size_t)(r0 + i) * n + k] * xb[i];
+                y[k] -= s;
+            }
         }
         __syncthreads();
     }
@@ -742,30 +871,27 @@ void launch_prior_lin(const DevProblem& P, const double* kst, hipStream_t s) {
     const int n = P.n_prior + P.n_vel;
     if (n) hipLaunchKernelGGL(k_prior_lin, dim3(n), dim3(64), 0, s, P, kst);
 }
-void launch_schur_prep(const DevProblem& P, double lambda, hipStream_t s) {
-    const int n = P.n_pairs + P.n_lm;
-    if (n) hipLaunchKernelGGL(k_schur_prep, dim3(cdiv(n, 256)), dim3(256), 0, s, P, lambda);
+void launch_schur(const DevProblem& P, double lambda, hipStream_t s) {
+    if (P.n_tiles) hipLaunchKernelGGL(k_schur, dim3(P.n_tiles), dim3(256), 0, s, P, lambda);
 }
-void launch_schur(const DevProblem& P, hipStream_t s) {
-    if (P.n_tiles) hipLaunchKernelGGL(k_schur, dim3(P.n_tiles), dim3(128), 0, s, P);
+void launch_hpp_reduce(const DevProblem& P, hipStream_t s) {
+    const int n = P.n_hub + P.n_pb;
+    if (n) hipLaunchKernelGGL(k_hpp_reduce, dim3(n), dim3(144 * RED_GROUPS), 0, s, P);
 }
 void launch_assemble(const DevProblem& P, double lambda, int flags, hipStream_t s) {
     const int n = P.n_ublocks + P.n_pb;
-    if (n) hipLaunchKernelGGL(k_assemble, dim3(n), dim3(256), 0, s, P, lambda, flags);
+    if (n) hipLaunchKernelGGL(k_assemble, dim3(n), dim3(144 * RED_GROUPS), 0, s, P, lambda, flags);
 }
 void launch_cholesky_solve(const DevProblem& P, hipStream_t s) {
     const int n = P.np;
+    if (n == 0) return;
     for (int p = 0; p < n; p += CHOL_NB) {
         const int nbp = n - p < CHOL_NB ? n - p : CHOL_NB;
-        const int rest = n - p - nbp;
-        hipLaunchKernelGGL(k_chol_panel, dim3(1 + cdiv(rest, PANEL_ROWS)), dim3(64), 0, s, P.S, n, p, nbp, P.info,
-                           P.xsol);
-        if (rest > 0) {
-            const int nt = cdiv(rest, 32);
-            hipLaunchKernelGGL(k_chol_update, dim3(nt * (nt + 1) / 2), dim3(256), 0, s, P.S, n, p, nbp, P.xsol);
-        }
+        const int nt = cdiv(n - p - nbp, CHOL_NB);
+        hipLaunchKernelGGL(k_chol_step, dim3(nt ? nt * (nt + 1) / 2 : 1), dim3(256), 0, s, n, p, P.S, P.Lm, P.xsol,
+                           P.yv, P.info);
     }
-    if (n) hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(256), 0, s, P.S, n, P.xsol);
+    hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(256), 0, s, P.Lm, n, P.yv, P.xsol);
 }
 void launch_update(const DevProblem& P, double lambda, const double* kst, const double* lst, double* kst_out,
                    double* lst_out, hipStream_t s) {
