@@ -15,7 +15,8 @@
 //   sslab/gpslab  per (tile, KF pair) Schur partials V(k1) Hpl(k2)^T and per (tile, KF) rhs
 //                 partials, target-sorted likewise
 //   Hblk, Sblk    [n_ublocks][144] reduced Hpp / damped Schur complement, upper blocks
-//   S, Lm         [np][np] dense reduced camera system (lower) and its Cholesky factor
+//   S, Lm         [npad][npad] dense reduced camera system (lower) and its Cholesky factor; npad =
+//                 np rounded up to CHOL_NB with an identity tail, so every Cholesky panel is full
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -39,6 +40,7 @@ constexpr int RED_GROUPS = 4;       // reduction kernels: 4 groups x 144 threads
 
 struct DevProblem {
     int n_kf, n_lm, n_obs, n_gp, n_pairs, n_tiles, n_pb, np, n_prior, n_vel, n_cam;
+    int npad;               // np rounded up to CHOL_NB: leading dimension of S / Lm (identity tail)
     int n_entries, n_sentries, n_ublocks;
     // observations (device order)
     const int* ob_meta;
@@ -114,12 +116,13 @@ struct DevProblem {
     double* gpslab;         // [n_gpslots][12] Schur rhs partials, target-sorted
     double* Hblk;           // [n_ublocks][144] reduced Hpp (upper blocks)
     double* Sblk;           // [n_ublocks][144] assembled reduced camera system (upper blocks)
-    double* Lm;             // [np][np] Cholesky factor (lower)
+    double* Lm;             // [npad][npad] Cholesky factor, stored transposed (U = L^T, upper)
+    double* Ldinv;          // [npad] 1 / L(i, i)
     double* Hpl;
     double* Hll;
     double* bl;
     double* Dinv;
-    double* S;              // [np][np]
+    double* S;              // [npad][npad], rows/cols >= np: identity
     double* bp;             // [np]
     double* xsol;           // [np] rhs -> solution
     double* yv;             // [np] forward-substituted rhs

@@ -496,15 +496,26 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.Hblk = dalloc<double>(p, (size_t)144 * std::max(n_ublocks, 1));
     HIPCHK(hipMemset(D.Hblk, 0, sizeof(double) * 144 * (size_t)std::max(n_ublocks, 1)));   // blocks without sources
     D.Sblk = dalloc<double>(p, (size_t)144 * std::max(n_ublocks, 1));
-    D.Lm = dalloc<double>(p, (size_t)p->np * p->np + 1);
+    const int npad = (p->np + CHOL_NB - 1) / CHOL_NB * CHOL_NB;
+    D.npad = npad;
+    D.Lm = dalloc<double>(p, (size_t)npad * npad + 1);
+    D.Ldinv = dalloc<double>(p, npad + 1);
     D.Hpl = dalloc<double>(p, (size_t)36 * std::max(n_pairs, 1));
     D.Hll = dalloc<double>(p, (size_t)9 * std::max(nl, 1));
     D.bl = dalloc<double>(p, (size_t)3 * std::max(nl, 1));
     D.Dinv = dalloc<double>(p, (size_t)9 * std::max(nl, 1));
-    D.S = dalloc<double>(p, (size_t)p->np * p->np + 1);
+    D.S = dalloc<double>(p, (size_t)npad * npad + 1);
     D.bp = dalloc<double>(p, p->np + 1);
-    D.xsol = dalloc<double>(p, p->np + 1);
-    D.yv = dalloc<double>(p, p->np + 1);
+    D.xsol = dalloc<double>(p, npad + 1);
+    D.yv = dalloc<double>(p, npad + 1);
+    {   // S padding: identity tail (never touched by assembly or factorisation), zero rhs tail
+        HIPCHK(hipMemset(D.S, 0, sizeof(double) * ((size_t)npad * npad + 1)));
+        HIPCHK(hipMemset(D.Lm, 0, sizeof(double) * ((size_t)npad * npad + 1)));
+        HIPCHK(hipMemset(D.xsol, 0, sizeof(double) * (npad + 1)));
+        const double one = 1.0;
+        for (int i = p->np; i < npad; ++i)
+            HIPCHK(hipMemcpy(D.S + (size_t)i * npad + i, &one, sizeof(double), hipMemcpyHostToDevice));
+    }
     D.x = dalloc<double>(p, p->np + 3 * (size_t)nl + 1);
     HIPCHK(hipMemset(D.x, 0, sizeof(double) * (p->np + 3 * (size_t)nl + 1)));   // BlockSolver::_x before any solve
     const int nchi = n_tiles + D.n_prior + D.n_vel;
@@ -581,7 +592,9 @@ double lambda_init(lba_problem* p) {   // computeLambdaInit (levenberg.cpp:171-1
     const DevProblem& D = p->D;
     launch_assemble(D, 0.0, ASM_FULL, p->stream);
     std::vector<double> S((size_t)p->np * p->np), Hll(9 * (size_t)std::max(D.n_lm, 1));
-    HIPCHK(hipMemcpyAsync(S.data(), D.S, S.size() * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+    if (p->np)
+        HIPCHK(hipMemcpy2DAsync(S.data(), p->np * sizeof(double), D.S, D.npad * sizeof(double),
+                                p->np * sizeof(double), p->np, hipMemcpyDeviceToHost, p->stream));
     HIPCHK(hipMemcpyAsync(Hll.data(), D.Hll, 9 * (size_t)D.n_lm * sizeof(double), hipMemcpyDeviceToHost, p->stream));
     HIPCHK(hipStreamSynchronize(p->stream));
     double m = 0.0;
@@ -863,7 +876,8 @@ int lba_linearize(lba_problem* p, double* residuals, double* H_pp, double* b, do
         const int np = p->np, nl = D.n_lm;
         std::vector<double> bp(np + 1), bl(3 * (size_t)nl + 1), hll(9 * (size_t)nl + 1), res(3 * (size_t)p->n_obs + 1);
         if (H_pp && np)
-            HIPCHK(hipMemcpyAsync(H_pp, D.S, (size_t)np * np * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+            HIPCHK(hipMemcpy2DAsync(H_pp, np * sizeof(double), D.S, D.npad * sizeof(double), np * sizeof(double), np,
+                                    hipMemcpyDeviceToHost, p->stream));
         HIPCHK(hipMemcpyAsync(bp.data(), D.bp, np * sizeof(double), hipMemcpyDeviceToHost, p->stream));
         HIPCHK(hipMemcpyAsync(bl.data(), D.bl, 3 * (size_t)nl * sizeof(double), hipMemcpyDeviceToHost, p->stream));
         HIPCHK(hipMemcpyAsync(hll.data(), D.Hll, 9 * (size_t)nl * sizeof(double), hipMemcpyDeviceToHost, p->stream));

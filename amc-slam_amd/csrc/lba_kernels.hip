@@ -444,7 +444,7 @@ __global__ __launch_bounds__(256) void k_schur(DevProblem P, double lambda) {
 __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, double lambda, int flags) {
     __shared__ double red[144 * RED_GROUPS];
     const int tid = threadIdx.x;
-    const int n = P.np;
+    const int n = P.npad;   // leading dimension of S
     if ((int)blockIdx.x < P.n_ublocks) {
         const int ub = blockIdx.x;
         const int bi = P.ub_i[ub], bj = P.ub_j[ub];
@@ -482,12 +482,18 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
 }
 
 // ------------------------------------------------------------------------------------------------
-// Dense Cholesky S = L L^T (right-looking, panel width CHOL_NB, one launch per panel).
+// Dense Cholesky S = L L^T (right-looking, one launch per CNB-wide panel).  The system is padded
+// to a multiple of CNB with an identity tail (set once at upload; the factorisation never changes
+// it), so every panel is exactly CNB wide and all loops below are compile-time.
 // Every workgroup owns one lower tile of the trailing matrix; it factors the panel's diagonal
-// block itself (one wave, rows in registers) and solves the panel rows its tile needs, so a
-// launch has no inter-workgroup communication.  The final factor goes to Lm, the running
-// right-hand side b is forward-substituted on the fly (y -> yv).  A non-positive pivot sets *info
-// (the LDLT !isPositive failure of linear_solver_dense.h:108-112).
+// block itself (wave 0, one row per lane, pivot by readlane, column broadcast through LDS), solves
+// the panel rows its tile needs (wave 1) and the panel's forward substitution (wave 2), then
+// updates its tile, so a launch has no inter-workgroup communication.  All global operands are
+// loaded at kernel entry, before the dependent chain starts.  The factor goes to Lm transposed
+// (U = L^T, upper, row-major: what the back-substitution streams) with the
+// reciprocal diagonal in Ldinv; the running right-hand side b is forward-substituted on the fly
+// (y -> yv).  A non-positive pivot sets *info (the LDLT !isPositive failure of
+// linear_solver_dense.h:108-112).
 constexpr int CNB = CHOL_NB;
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
@@ -503,15 +509,29 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// empty asm that "modifies" v: forces an update to be materialised where it is written (stops the
+// compiler from sinking a rank-1 update down to its first use, which keeps O(n^2) operands live)
+__device__ __forceinline__ void pin(double& v) { asm volatile("" : "+v"(v)); }
+
+// 1/sqrt(d): hardware estimate + two Newton steps (full fp64 precision for the pivots of an SPD S)
+__device__ __forceinline__ double rsqrt_nr(double d) {
+    double r = __builtin_amdgcn_rsq(d);
+    r = r * (1.5 - 0.5 * d * r * r);
+    r = r * (1.5 - 0.5 * d * r * r);
+    return r;
+}
+
 __global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restrict__ A, double* __restrict__ Lm,
-                                                   double* __restrict__ b, double* __restrict__ yv, int* info) {
-    __shared__ double D[CNB][CNB + 1];
+                                                   double* __restrict__ Ldinv, double* __restrict__ b,
+                                                   double* __restrict__ yv, int* info) {
+    __shared__ double Lt[CNB][CNB + 1];   // diagonal factor, transposed: Lt[c][r] = L(p + r, p + c)
     __shared__ double Pi[CNB][CNB + 1];
     __shared__ double Pj[CNB][CNB + 1];
+    __shared__ double dinv[CNB];
     __shared__ double colb[CNB];
     __shared__ double yp[CNB];
-    const int tid = threadIdx.x;
-    const int nbp = min(CNB, n - p), q = p + nbp, m = n - q, nt = (m + CNB - 1) / CNB;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & (CNB - 1);
+    const int q = p + CNB, nt = (n - q) / CNB;
     int ti = 0, tj = 0;
     if (nt > 0) {
         const int bid = blockIdx.x;
@@ -520,174 +540,204 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restr
         while (ti * (ti + 1) / 2 > bid) --ti;
         tj = bid - ti * (ti + 1) / 2;
     }
-    // (1) diagonal block: one row per lane of wave 0; the pivot column is broadcast through LDS
-    //     (one write per lane, then all reads issued back to back before any use)
-    if (tid < 64) {
-        double row[CNB];
+    // ---- prefetch: diagonal rows (wave 0), panel rows of tiles ti / tj (wave 1), b_p (wave 2),
+    //      and every thread's 2x2 piece of the trailing tile
+    double row[CNB];
+    if (wave == 0) {
 #pragma unroll
-        for (int c = 0; c < CNB; ++c) row[c] = (tid < nbp && c <= tid) ? A[(size_t)(p + tid) * n + p + c] : 0.0;
+        for (int c = 0; c < CNB; ++c) row[c] = A[(size_t)(p + l32) * n + p + c];
+    } else if (wave == 1 && nt > 0) {
+        const int r = q + (lane < CNB ? ti : tj) * CNB + l32;
+#pragma unroll
+        for (int c = 0; c < CNB; ++c) row[c] = A[(size_t)r * n + p + c];
+    }
+    double bw = 0.0;
+    if (wave == 2) bw = b[p + l32];
+    const int tr = tid >> 4, tc = tid & 15;
+    const size_t ra = (size_t)q + ti * CNB + 2 * tr, ca = (size_t)q + tj * CNB + 2 * tc;
+    double a00 = 0.0, a01 = 0.0, a10 = 0.0, a11 = 0.0;
+    if (nt > 0) {
+        a00 = A[ra * n + ca]; a01 = A[ra * n + ca + 1];
+        a10 = A[(ra + 1) * n + ca]; a11 = A[(ra + 1) * n + ca + 1];
+    }
+    // ---- (1) diagonal block
+    if (wave == 0) {
         bool bad = false;
+        double myinv = 1.0;
 #pragma unroll
         for (int j = 0; j < CNB; ++j) {
-            if (j < nbp) {
-                double d = readlane_d(row[j], j);
-                if (!(d > 0.0)) { bad = true; d = 1.0; }
-                const double ljj = sqrt(d), inv = 1.0 / ljj;
-                const double lij = (tid == j) ? ljj : ((tid > j && tid < nbp) ? row[j] * inv : 0.0);
-                row[j] = lij;
-                if (tid < CNB) colb[tid] = lij;
-                wave_sync();
-                double cb[CNB];
+            double d = readlane_d(row[j], j);
+            if (!(d > 0.0)) { bad = true; d = 1.0; }
+            const double r = rsqrt_nr(d);
+            const double lij = row[j] * r;   // lane j: sqrt(d); lanes > j: L(l, j); lanes < j: unused
+            row[j] = lij;
+            if (lane == j) myinv = r;
+            if (lane < CNB) colb[lane] = lij;
+            wave_sync();
+            double cb[CNB];
 #pragma unroll
-                for (int k = j + 1; k < CNB; ++k) cb[k] = colb[k];
+            for (int k = j + 1; k < CNB; ++k) cb[k] = colb[k];
+            // lanes < k only touch their (unused) upper triangle, so no predication is needed
 #pragma unroll
-                for (int k = j + 1; k < CNB; ++k)
-                    if (tid >= k && tid < nbp) row[k] -= lij * cb[k];
-                wave_sync();
-            }
+            for (int k = j + 1; k < CNB; ++k) { row[k] -= lij * cb[k]; pin(row[k]); }
+            wave_sync();
+            __builtin_amdgcn_sched_barrier(0);   // keep the unrolled pivots from being interleaved
         }
-        if (tid < CNB)
+        if (lane < CNB) {
 #pragma unroll
-            for (int c = 0; c < CNB; ++c) D[tid][c] = row[c];
-        if (bad && tid == 0 && blockIdx.x == 0) *info = 1 + p;
+            for (int c = 0; c < CNB; ++c) Lt[c][lane] = (c <= lane) ? row[c] : 0.0;
+            dinv[lane] = myinv;
+        }
+        if (bad && lane == 0 && blockIdx.x == 0) *info = 1 + p;
     }
     __syncthreads();
-    // (2) panel rows of tiles ti / tj: x D^T = a (triangular solve per row, D rows read in one burst)
-    if (tid < 2 * CNB && nt > 0) {
-        const int which = tid / CNB, i = tid % CNB;
-        if (!(which == 1 && tj == ti)) {
-            const int r = q + (which ? tj : ti) * CNB + i;
-            double x[CNB];
+    // ---- (2) panel rows: x L_pp^T = a, right-looking (column j of L_pp is Lt[j][*])
+    if (wave == 1 && nt > 0) {
 #pragma unroll
-            for (int c = 0; c < CNB; ++c) x[c] = (r < n && c < nbp) ? A[(size_t)r * n + p + c] : 0.0;
+        for (int j = 0; j < CNB; ++j) {
+            const double xj = row[j] * dinv[j];
+            row[j] = xj;
+            double lc[CNB];
 #pragma unroll
-            for (int j = 0; j < CNB; ++j)
-                if (j < nbp) {
-                    double s = x[j];
+            for (int k = j + 1; k < CNB; ++k) lc[k] = Lt[j][k];
 #pragma unroll
-                    for (int c = 0; c < j; ++c) s -= x[c] * D[j][c];
-                    x[j] = s / D[j][j];
-                }
-            double (*dst)[CNB + 1] = which ? Pj : Pi;
+            for (int k = j + 1; k < CNB; ++k) { row[k] -= xj * lc[k]; pin(row[k]); }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (lane < CNB || tj != ti) {
+            double (*dst)[CNB + 1] = (lane < CNB) ? Pi : Pj;
 #pragma unroll
-            for (int c = 0; c < CNB; ++c) dst[i][c] = (r < n) ? x[c] : 0.0;
+            for (int c = 0; c < CNB; ++c) dst[l32][c] = row[c];
         }
     }
-    // y_p = D^-1 b_p by wave 3: lane l holds b_{p+l}
-    const bool need_y = (ti == tj) || blockIdx.x == 0;
-    if (tid >= 192 && need_y) {
-        const int l = tid - 192;
-        double bl = (l < nbp) ? b[p + l] : 0.0;
-        const double dll = (l < nbp) ? D[l][l] : 1.0;
-        double drow[CNB];
+    // ---- y_p = L_pp^-1 b_p (wave 2, lane l holds b_{p+l})
+    if (wave == 2 && (ti == tj || blockIdx.x == 0)) {
+        double lr[CNB];
 #pragma unroll
-        for (int c = 0; c < CNB; ++c) drow[c] = (l < CNB) ? D[l & (CNB - 1)][c] : 0.0;
+        for (int c = 0; c < CNB; ++c) lr[c] = Lt[c][l32];
 #pragma unroll
-        for (int j = 0; j < CNB; ++j)
-            if (j < nbp) {
-                const double yj = readlane_d(bl, j) / readlane_d(dll, j);
-                if (l == j) bl = yj;
-                else if (l > j) bl -= drow[j] * yj;
-            }
-        if (l < nbp) yp[l] = bl;
+        for (int j = 0; j < CNB; ++j) {
+            const double yj = readlane_d(bw, j) * dinv[j];
+            bw = (lane == j) ? yj : ((lane > j) ? bw - lr[j] * yj : bw);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (lane < CNB) yp[lane] = bw;
     }
     __syncthreads();
     if (blockIdx.x == 0) {
-        for (int t = tid; t < nbp * nbp; t += 256) {
-            const int i = t / nbp, c = t % nbp;
-            if (c <= i) Lm[(size_t)(p + i) * n + p + c] = D[i][c];
+        for (int t = tid; t < CNB * CNB; t += 256) {   // U = L^T: U(p + c, p + i) = L(p + i, p + c)
+            const int c = t / CNB, i = t % CNB;
+            Lm[(size_t)(p + c) * n + p + i] = Lt[c][i];
         }
-        if (tid < nbp) yv[p + tid] = yp[tid];
+        if (tid < CNB) {
+            Ldinv[p + tid] = dinv[tid];
+            yv[p + tid] = yp[tid];
+        }
     }
     if (nt == 0) return;
-    const double (*Qj)[CNB + 1] = (ti == tj) ? Pi : Pj;
-    // (3) trailing tile update A(ti, tj) -= Pi Pj^T
+    // ---- (3) trailing tile update A(ti, tj) -= Pi Pj^T
     {
-        const int tr = tid >> 4, tc = tid & 15;
-        double a00 = 0, a01 = 0, a10 = 0, a11 = 0;
+        const double (*Qj)[CNB + 1] = (ti == tj) ? Pi : Pj;
+        double s00 = 0, s01 = 0, s10 = 0, s11 = 0;
 #pragma unroll 8
         for (int k = 0; k < CNB; ++k) {
             const double x0 = Pi[2 * tr][k], x1 = Pi[2 * tr + 1][k];
             const double y0 = Qj[2 * tc][k], y1 = Qj[2 * tc + 1][k];
-            a00 += x0 * y0; a01 += x0 * y1; a10 += x1 * y0; a11 += x1 * y1;
+            s00 += x0 * y0; s01 += x0 * y1; s10 += x1 * y0; s11 += x1 * y1;
         }
-        const int ra = q + ti * CNB + 2 * tr, ca = q + tj * CNB + 2 * tc;
-        if (ra < n) {
-            if (ca < n) A[(size_t)ra * n + ca] -= a00;
-            if (ca + 1 < n) A[(size_t)ra * n + ca + 1] -= a01;
-        }
-        if (ra + 1 < n) {
-            if (ca < n) A[(size_t)(ra + 1) * n + ca] -= a10;
-            if (ca + 1 < n) A[(size_t)(ra + 1) * n + ca + 1] -= a11;
-        }
+        A[ra * n + ca] = a00 - s00; A[ra * n + ca + 1] = a01 - s01;
+        A[(ra + 1) * n + ca] = a10 - s10; A[(ra + 1) * n + ca + 1] = a11 - s11;
     }
-    // (4) the tj == 0 workgroups publish the panel rows of L
+    // ---- (4) the tj == 0 workgroups publish the panel rows of L (stored transposed, U = L^T)
     if (tj == 0)
-        for (int t = tid; t < CNB * nbp; t += 256) {
-            const int i = t / nbp, c = t % nbp;
-            const int r = q + ti * CNB + i;
-            if (r < n) Lm[(size_t)r * n + p + c] = Pi[i][c];
+        for (int t = tid; t < CNB * CNB; t += 256) {
+            const int c = t / CNB, i = t % CNB;
+            Lm[(size_t)(p + c) * n + q + ti * CNB + i] = Pi[i][c];
         }
-    // (5) forward substitution of the trailing right-hand side
+    // ---- (5) forward substitution of the trailing right-hand side
     if (ti == tj && tid < CNB) {
-        const int r = q + ti * CNB + tid;
-        if (r < n) {
-            double s = 0.0;
-            for (int c = 0; c < nbp; ++c) s += Pi[tid][c] * yp[c];
-            b[r] -= s;
-        }
+        double s = 0.0;
+#pragma unroll 8
+        for (int c = 0; c < CNB; ++c) s += Pi[tid][c] * yp[c];
+        b[q + ti * CNB + tid] -= s;
     }
 }
 
 constexpr int CHOL_MAXN = 6144;
+constexpr int BS_GEMV = 448;                  // trailing-update threads (one prefetched column each per pass)
+constexpr int BS_THREADS = 64 + BS_GEMV;
 
-// L^T x = y, single workgroup, diagonal blocks staged in LDS; x -> out
-__global__ __launch_bounds__(256) void k_chol_backsolve(const double* __restrict__ Lm, int n,
-                                                        const double* __restrict__ yv, double* __restrict__ out) {
+// L^T x = y with the factor stored transposed (U = L^T row-major, so every load below is one
+// row segment: base pointer + immediate offsets), one workgroup.  Wave 0 solves the 32x32 diagonal blocks from the bottom up (x_i by
+// readlane, diagonal rows of the next block prefetched one block ahead); the other waves apply
+// each solved block to the rows above (y_k -= sum_i L(r0+i, k) x_i), their column loads issued
+// before the diagonal solve so the load latency hides behind it.  x -> out.
+__global__ __launch_bounds__(BS_THREADS) void k_chol_backsolve(const double* __restrict__ Lm,
+                                                               const double* __restrict__ Ldinv, int n,
+                                                               const double* __restrict__ yv,
+                                                               double* __restrict__ out) {
     __shared__ double y[CHOL_MAXN];
-    __shared__ double Dg[32][33];
-    __shared__ double xb[32];
-    const int tid = threadIdx.x;
-    for (int t = tid; t < n; t += 256) y[t] = yv[t];
-    const int nblk = (n + 31) / 32;
+    __shared__ double xb[CNB];
+    const int tid = threadIdx.x, lane = tid & 63, l32 = lane & (CNB - 1);
+    for (int t = tid; t < n; t += BS_THREADS) y[t] = yv[t];
+    const int nblk = n / CNB;
+    // pre[]: wave 0 = diagonal rows of the next block; other waves = this block's loads of column k0
+    double dg[CNB], pre[CNB];
+    double dl = 0.0, dln = 0.0;
+    if (tid < 64) {
+        const int r0 = (nblk - 1) * CNB;
+#pragma unroll
+        for (int i = 0; i < CNB; ++i) dg[i] = Lm[(size_t)(r0 + l32) * n + r0 + i];
+        dl = Ldinv[r0 + l32];
+    }
+    __syncthreads();
+    const int k0 = tid - 64;
     for (int blk = nblk - 1; blk >= 0; --blk) {
-        const int r0 = blk * 32, len = min(32, n - r0);
-        for (int t = tid; t < len * len; t += 256) {
-            const int i = t / len, c = t % len;
-            Dg[i][c] = (c <= i) ? Lm[(size_t)(r0 + i) * n + r0 + c] : 0.0;
-        }
-        __syncthreads();
+        const int r0 = blk * CNB;
         if (tid < 64) {
-            double yl = tid < len ? y[r0 + tid] : 0.0;
-            for (int i = len - 1; i >= 0; --i) {
-                const double xi = __shfl(yl, i, 64) / Dg[i][i];
-                if (tid < i) yl -= Dg[i][tid] * xi;
-                if (tid == i) yl = xi;
+            if (blk > 0) {
+                const int rn = r0 - CNB;
+#pragma unroll
+                for (int i = 0; i < CNB; ++i) pre[i] = Lm[(size_t)(rn + l32) * n + rn + i];
+                dln = Ldinv[rn + l32];
             }
-            if (tid < len) xb[tid] = yl;
+            double yl = y[r0 + l32];
+#pragma unroll
+            for (int i = CNB - 1; i >= 0; --i) {
+                const double xi = readlane_d(yl * dl, i);
+                yl = (lane == i) ? xi : ((lane < i) ? yl - dg[i] * xi : yl);
+            }
+            if (lane < CNB) {
+                xb[lane] = yl;
+                out[r0 + lane] = yl;
+            }
+#pragma unroll
+            for (int i = 0; i < CNB; ++i) dg[i] = pre[i];
+            dl = dln;
+        } else {
+            if (k0 < r0)
+#pragma unroll
+                for (int i = 0; i < CNB; ++i) pre[i] = Lm[(size_t)k0 * n + r0 + i];
         }
         __syncthreads();
-        if (tid < len) out[r0 + tid] = xb[tid];
-        if (len == 32) {
-            double xr[32];
-#pragma unroll
-            for (int i = 0; i < 32; ++i) xr[i] = xb[i];
-            for (int k = tid; k < r0; k += 256) {
-                double lv[32];
-#pragma unroll
-                for (int i = 0; i < 32; ++i) lv[i] = Lm[(size_t)(r0 + i) * n + k];
+        if (tid >= 64) {
+            if (k0 < r0) {
                 double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
 #pragma unroll
-                for (int i = 0; i < 32; i += 4) {
-                    s0 += lv[i] * xr[i]; s1 += lv[i + 1] * xr[i + 1]; s2 += lv[i + 2] * xr[i + 2]; s3 += lv[i + 3] * xr[i + 3];
+                for (int i = 0; i < CNB; i += 4) {
+                    s0 += pre[i] * xb[i]; s1 += pre[i + 1] * xb[i + 1];
+                    s2 += pre[i + 2] * xb[i + 2]; s3 += pre[i + 3] * xb[i + 3];
+                }
+                y[k0] -= (s0 + s1) + (s2 + s3);
+            }
+            for (int k = k0 + BS_GEMV; k < r0; k += BS_GEMV) {
+                double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+#pragma unroll
+                for (int i = 0; i < CNB; i += 4) {
+                    const double* u = Lm + (size_t)k * n + r0 + i;
+                    s0 += u[0] * xb[i]; s1 += u[1] * xb[i + 1]; s2 += u[2] * xb[i + 2]; s3 += u[3] * xb[i + 3];
                 }
                 y[k] -= (s0 + s1) + (s2 + s3);
-            }
-        } else {
-            for (int k = tid; k < r0; k += 256) {
-                double s = 0.0;
-                for (int i = 0; i < len; ++i) s += Lm[(size_t)(r0 + i) * n + k] * xb[i];
-                y[k] -= s;
             }
         }
         __syncthreads();
@@ -883,15 +933,14 @@ void launch_assemble(const DevProblem& P, double lambda, int flags, hipStream_t 
     if (n) hipLaunchKernelGGL(k_assemble, dim3(n), dim3(144 * RED_GROUPS), 0, s, P, lambda, flags);
 }
 void launch_cholesky_solve(const DevProblem& P, hipStream_t s) {
-    const int n = P.np;
+    const int n = P.npad;   // multiple of CHOL_NB (identity tail)
     if (n == 0) return;
     for (int p = 0; p < n; p += CHOL_NB) {
-        const int nbp = n - p < CHOL_NB ? n - p : CHOL_NB;
-        const int nt = cdiv(n - p - nbp, CHOL_NB);
-        hipLaunchKernelGGL(k_chol_step, dim3(nt ? nt * (nt + 1) / 2 : 1), dim3(256), 0, s, n, p, P.S, P.Lm, P.xsol,
-                           P.yv, P.info);
+        const int nt = (n - p - CHOL_NB) / CHOL_NB;
+        hipLaunchKernelGGL(k_chol_step, dim3(nt ? nt * (nt + 1) / 2 : 1), dim3(256), 0, s, n, p, P.S, P.Lm, P.Ldinv,
+                           P.xsol, P.yv, P.info);
     }
-    hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(256), 0, s, P.Lm, n, P.yv, P.xsol);
+    hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(BS_THREADS), 0, s, P.Lm, P.Ldinv, n, P.yv, P.xsol);
 }
 void launch_update(const DevProblem& P, double lambda, const double* kst, const double* lst, double* kst_out,
                    double* lst_out, hipStream_t s) {
