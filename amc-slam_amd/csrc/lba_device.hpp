@@ -34,6 +34,10 @@ constexpr int TILE_PAIRS = 128;
 constexpr int TILE_LMS = 64;
 constexpr int TILE_KF = 16;
 constexpr int ROW_STRIDE = 28;      // LDS Jacobian row: Ja(12) Jb(12) e(1) Jp(3)
+constexpr int TILE_SEGS = 48;       // pose-pair segments per tile (k_linearize stages their metadata)
+constexpr int SEG_MAX_ROWS = 48;    // longer (a, b) runs are split so the segment tasks stay balanced
+constexpr int TILE_PROWS = 2 * TILE_ROWS;   // pair row-list entries per tile (each row feeds <= 2 pairs)
+constexpr int SEGM_STRIDE = 8;      // staged segment record: row0 nrows aa ab bb ab_transposed ga gb
 
 constexpr int CHOL_NB = 32;         // Cholesky panel / tile width
 constexpr int RED_GROUPS = 4;       // reduction kernels: 4 groups x 144 threads
@@ -71,6 +75,7 @@ struct DevProblem {
     const int* tile_kf0;
     const int* tile_nkf;
     const int* tkf_list;    // tile KF unions (pose block indices)
+    const int* seg_meta;    // per tile segment: SEGM_STRIDE ints (row0 nrows aa ab bb ab_tr ga gb)
     const int* seg_a;       // per segment entry: pose block of side a / b (-1 = none)
     const int* seg_b;
     const int* seg_row0;    // tile-local first row
@@ -135,6 +140,9 @@ struct DevProblem {
     double* fin;            // [4] chi_lin, chi_eval, scale, info
     double* ob_chi2;        // [n_obs]
     double* ob_res;         // [n_obs][3]
+    // diagnostics (LBA_PHASE_TIMING=<file>): per-workgroup clock64() stamps at phase boundaries
+    unsigned long long* tdbg_lin;     // [n_tiles][16] k_linearize
+    unsigned long long* tdbg_schur;   // [n_tiles][16] k_schur
 };
 
 // launchers (lba_kernels.hip)

@@ -11,6 +11,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <map>
@@ -66,7 +67,33 @@ struct ApiError {
     std::string msg;
 };
 
+// LBA_PHASE_TIMING=<file>: dump the per-workgroup phase stamps of the last k_linearize / k_schur
+// launch and the tile shapes (diagnostics; scripts/phase_times.py reads it)
+void dump_phase_times(lba_problem* p) {
+    const DevProblem& D = p->D;
+    const char* path = std::getenv("LBA_PHASE_TIMING");
+    if (!path || !D.tdbg_lin || D.n_tiles <= 0) return;
+    const size_t n = (size_t)D.n_tiles * 16;
+    std::vector<unsigned long long> lin(n), sch(n);
+    const int* cols[6] = {D.tile_nobs, D.tile_nseg, D.tile_npair, D.tile_nlm, D.tile_nsent, D.tile_nkf};
+    std::vector<int> shape(6 * (size_t)D.n_tiles);
+    if (hipDeviceSynchronize() != hipSuccess) return;
+    (void)hipMemcpy(lin.data(), D.tdbg_lin, n * 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(sch.data(), D.tdbg_schur, n * 8, hipMemcpyDeviceToHost);
+    for (int c = 0; c < 6; ++c)
+        (void)hipMemcpy(shape.data() + (size_t)c * D.n_tiles, cols[c], 4 * (size_t)D.n_tiles, hipMemcpyDeviceToHost);
+    if (FILE* f = std::fopen(path, "wb")) {
+        const int nt = D.n_tiles;
+        std::fwrite(&nt, 4, 1, f);
+        std::fwrite(lin.data(), 8, n, f);
+        std::fwrite(sch.data(), 8, n, f);
+        std::fwrite(shape.data(), 4, shape.size(), f);
+        std::fclose(f);
+    }
+}
+
 void free_all(lba_problem* p) {
+    dump_phase_times(p);
     for (void* a : p->allocs) (void)hipFree(a);
     p->allocs.clear();
     p->kst[0] = p->kst[1] = p->lst[0] = p->lst[1] = nullptr;
@@ -263,28 +290,42 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     std::vector<int> ob_row(n_obs, 0);
     std::vector<int> pair_r0(n_pairs + 1, 0), pair_rows, lm_r0(nl + 1, 0), lm_rows;
     {
+        // segment key of an observation: (pose block a, pose block b)
+        auto keyof = [&](int q) {
+            const lba_obs& o = obs[obs_of[q]];
+            return std::make_pair(is_gp(o.kind) ? H[o.kf_a] : -1, H[o.kf_b]);
+        };
+        // segments a key's rows will need (runs are split at SEG_MAX_ROWS, on observation bounds)
+        auto nseg_of = [](int rows_of_key) { return (rows_of_key + SEG_MAX_ROWS - 3) / (SEG_MAX_ROWS - 2); };
         int d = 0;
         while (d < nl) {
             int nobs = 0, rows = 0, npair = 0, nlmt = 0;
             std::vector<int> uni;
+            std::map<std::pair<int, int>, int> keyrows;
             int e = d;
             while (e < nl) {
                 int no = lobs0[e + 1] - lobs0[e], nr = 0;
-                for (int q = lobs0[e]; q < lobs0[e + 1]; ++q) nr += obs_dim(obs[obs_of[q]].kind);
+                std::map<std::pair<int, int>, int> k2 = keyrows;
+                for (int q = lobs0[e]; q < lobs0[e + 1]; ++q) {
+                    nr += obs_dim(obs[obs_of[q]].kind);
+                    k2[keyof(q)] += obs_dim(obs[obs_of[q]].kind);
+                }
+                int nsg = 0;
+                for (auto& kv : k2) nsg += nseg_of(kv.second);
                 const int npl = lm_pair0[e + 1] - lm_pair0[e];
                 std::vector<int> u2 = uni;
                 for (int k : lm_kfs[e]) u2.push_back(k);
                 std::sort(u2.begin(), u2.end());
                 u2.erase(std::unique(u2.begin(), u2.end()), u2.end());
                 const bool fits = nobs + no <= TILE_OBS && rows + nr <= TILE_ROWS && npair + npl <= TILE_PAIRS &&
-                                  nlmt + 1 <= TILE_LMS && (int)u2.size() <= TILE_KF;
+                                  nlmt + 1 <= TILE_LMS && (int)u2.size() <= TILE_KF && nsg <= TILE_SEGS;
                 if (!fits) {
                     if (e == d)
                         throw ApiError{LBA_E_LIMIT, "landmark " + std::to_string(order[e]) +
                                                         " exceeds tile limits (obs/rows/pairs/keyframes)"};
                     break;
                 }
-                nobs += no; rows += nr; npair += npl; nlmt += 1; uni.swap(u2);
+                nobs += no; rows += nr; npair += npl; nlmt += 1; uni.swap(u2); keyrows.swap(k2);
                 ++e;
             }
             const int tile = (int)t_obs0.size();
@@ -295,13 +336,10 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             t_kf0.push_back((int)tkf_list.size()); t_nkf.push_back((int)uni.size());
             for (int k : uni) tkf_list.push_back(k);
             auto local = [&](int k) { return (int)(std::lower_bound(uni.begin(), uni.end(), k) - uni.begin()); };
-            // segments: observations of the tile sorted by (pose block a, pose block b)
+            // segments: observations of the tile sorted by (pose block a, pose block b), runs of
+            // one key split at SEG_MAX_ROWS rows
             std::vector<int> tob;
             for (int q = lobs0[d]; q < lobs0[e]; ++q) tob.push_back(q);
-            auto keyof = [&](int q) {
-                const lba_obs& o = obs[obs_of[q]];
-                return std::make_pair(is_gp(o.kind) ? H[o.kf_a] : -1, H[o.kf_b]);
-            };
             std::stable_sort(tob.begin(), tob.end(), [&](int a, int b) { return keyof(a) < keyof(b); });
             t_seg0.push_back((int)seg_a.size());
             int row = 0;
@@ -309,7 +347,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 const auto key = keyof(tob[i]);
                 const int r0 = row;
                 size_t j = i;
-                while (j < tob.size() && keyof(tob[j]) == key) {
+                while (j < tob.size() && keyof(tob[j]) == key &&
+                       row - r0 + obs_dim(obs[obs_of[tob[j]]].kind) <= SEG_MAX_ROWS) {
                     ob_row[tob[j]] = row;
                     row += obs_dim(obs[obs_of[tob[j]]].kind);
                     ++j;
@@ -319,6 +358,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 i = j;
             }
             t_nseg.push_back((int)seg_a.size() - t_seg0.back());
+            if (t_nseg.back() > TILE_SEGS) throw ApiError{LBA_E_LIMIT, "internal: tile segment count exceeds TILE_SEGS"};
             // row lists per pair and per landmark
             for (int l = d; l < e; ++l) {
                 for (int q = lm_pair0[l]; q < lm_pair0[l + 1]; ++q) {
@@ -391,6 +431,13 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         if (a >= 0) { sl[0] = hfill[ublock_id(n_pb, a, a)]++; seg_gslot[2 * (size_t)en] = gfill[a]++; }
         if (a >= 0 && b >= 0) { sl[1] = hfill[ublock_id(n_pb, std::min(a, b), std::max(a, b))]++; sl[3] = a > b; }
         if (b >= 0) { sl[2] = hfill[ublock_id(n_pb, b, b)]++; seg_gslot[2 * (size_t)en + 1] = gfill[b]++; }
+    }
+    std::vector<int> seg_meta(SEGM_STRIDE * (size_t)std::max(n_segs, 1), -1);   // staged by k_linearize
+    for (int sg = 0; sg < n_segs; ++sg) {
+        int* m = seg_meta.data() + SEGM_STRIDE * (size_t)sg;
+        m[0] = seg_row0[sg]; m[1] = seg_nrows[sg];
+        for (int f = 0; f < 4; ++f) m[2 + f] = seg_slot[5 * (size_t)sg + f];
+        m[6] = seg_gslot[2 * (size_t)sg]; m[7] = seg_gslot[2 * (size_t)sg + 1];
     }
     std::vector<int> hub_list;
     for (int u = 0; u < n_ublocks; ++u)
@@ -469,11 +516,18 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.tile_seg0 = dupload(p, t_seg0); D.tile_nseg = dupload(p, t_nseg); D.tile_sent0 = dupload(p, t_sent0);
     D.tile_nsent = dupload(p, t_nsent); D.tile_kf0 = dupload(p, t_kf0); D.tile_nkf = dupload(p, t_nkf);
     D.tkf_list = dupload(p, tkf_list);
+    D.seg_meta = dupload(p, seg_meta);
     D.seg_a = dupload(p, seg_a); D.seg_b = dupload(p, seg_b); D.seg_row0 = dupload(p, seg_row0);
     D.seg_nrows = dupload(p, seg_nrows); D.sent_l1 = dupload(p, sent_l1); D.sent_l2 = dupload(p, sent_l2);
     D.pair_lm = dupload(p, pair_lm); D.pair_kf = dupload(p, pair_kf); D.pair_r0 = dupload(p, pair_r0);
     D.pair_rows = dupload(p, pair_rows); D.lm_r0 = dupload(p, lm_r0); D.lm_rows = dupload(p, lm_rows);
     D.lm_pair0 = dupload(p, lm_pair0);
+    if (std::getenv("LBA_PHASE_TIMING")) {
+        D.tdbg_lin = dalloc<unsigned long long>(p, (size_t)n_tiles * 16);
+        D.tdbg_schur = dalloc<unsigned long long>(p, (size_t)n_tiles * 16);
+        HIPCHK(hipMemset(D.tdbg_lin, 0, (size_t)n_tiles * 16 * 8));
+        HIPCHK(hipMemset(D.tdbg_schur, 0, (size_t)n_tiles * 16 * 8));
+    }
     D.seg_slot = dupload(p, seg_slot); D.seg_gslot = dupload(p, seg_gslot);
     D.hub_list = dupload(p, hub_list); D.n_hub = (int)hub_list.size();
     D.hs0 = dupload(p, hs0); D.gs0 = dupload(p, gs0); D.ub_i = dupload(p, ub_i); D.ub_j = dupload(p, ub_j);

@@ -26,6 +26,16 @@ namespace lba {
 
 static_assert(sizeof(GPPair) == GPP_STRIDE * sizeof(double), "GPPair layout drifted");
 
+// phase stamps for diagnostics only (buffer allocated when LBA_PHASE_TIMING is set; the uniform
+// null test costs one scalar branch otherwise)
+#define LBA_TMARK(buf, k)                                                           \
+    do {                                                                            \
+        if (buf) {                                                                  \
+            __syncthreads();                                                        \
+            if (threadIdx.x == 0) (buf)[(size_t)blockIdx.x * 16 + (k)] = clock64(); \
+        }                                                                           \
+    } while (0)
+
 __device__ __forceinline__ SE3 load_se3(const double* k) {
     SE3 T;
     T.q = Quat{k[0], k[1], k[2], k[3]};
@@ -80,7 +90,8 @@ __device__ __forceinline__ double obs_pose(const DevProblem& P, const double* ks
 }
 
 // ------------------------------------------------------------------------------------------------
-__global__ void k_pair_prep(DevProblem P, const double* __restrict__ kst) {
+constexpr int PREP_THREADS = 64;
+__global__ __launch_bounds__(PREP_THREADS) void k_pair_prep(DevProblem P, const double* __restrict__ kst) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < P.n_gp) {
         const double* ka = kst + (size_t)P.gp_kfa[i] * KF_STRIDE;
@@ -98,18 +109,110 @@ __global__ void k_pair_prep(DevProblem P, const double* __restrict__ kst) {
     }
 }
 
-// upper-triangle 4x4 output blocks (bi <= bj) of the 25-column row [Ja Jb e]: bi <= 5, bj <= 6
-__constant__ unsigned char c_bi[27] = {0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5};
-__constant__ unsigned char c_bj[27] = {0, 1, 2, 3, 4, 5, 6, 1, 2, 3, 4, 5, 6, 2, 3, 4, 5, 6, 3, 4, 5, 6, 4, 5, 6, 5, 6};
+// upper-triangle 4x4 output blocks (bi <= bj) of the 25-column row [Ja Jb e]: bi <= 5, bi <= bj <= 6,
+// enumerated row by row (7, 6, 5, 4, 3, 2 blocks)
+__device__ __forceinline__ void seg_block(int blk, int* bi, int* bj) {
+    const int i = (blk >= 7) + (blk >= 13) + (blk >= 18) + (blk >= 22) + (blk >= 25);
+    *bi = i;
+    *bj = i + blk - (7 * i - i * (i - 1) / 2);
+}
+
+// one (segment, 4x4 block) task: acc = sum over the segment's rows of (s r)[4bi..] r[4bj..]^T, written
+// to the segment's Hpp / b_p slab slots (upper block + mirror; b = -J^T rho' Omega e)
+__device__ __forceinline__ void seg_task(const DevProblem& P, const double* rows, const double* rw, const int* sm,
+                                         int bi, int bj) {
+    const int r0 = sm[0], nr = sm[1];
+    double acc[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.0;
+    for (int r = r0; r < r0 + nr; ++r) {
+        const double* Rr = rows + r * ROW_STRIDE;
+        const double s = rw[r];
+        double a[4], c[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { a[k] = s * Rr[4 * bi + k]; c[k] = Rr[4 * bj + k]; }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int l = 0; l < 4; ++l) acc[k * 4 + l] += a[k] * c[l];
+    }
+    if (bj == 6) {   // column 24 = e (columns 25..27 are the point block: not part of this product)
+        const int slot = (bi < 3) ? sm[6] : sm[7];
+        if (slot >= 0) {
+            double* g = P.gslab + (size_t)slot * 12 + 4 * (bi % 3);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) g[k] = -acc[k * 4];
+        }
+        return;
+    }
+    const bool bb = bi >= 3, ab = bi < 3 && bj >= 3;
+    const int slot = ab ? sm[3] : (bb ? sm[4] : sm[2]);
+    if (slot < 0) return;
+    double* H = P.hslab + (size_t)slot * 144;
+    const int i0 = 4 * (bi % 3), j0 = 4 * (bj % 3);
+    if (ab) {
+        const bool tr = sm[5] != 0;   // block stored for (b, a): transposed
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int l = 0; l < 4; ++l) {
+                if (tr) H[(j0 + l) * 12 + i0 + k] = acc[k * 4 + l];
+                else H[(i0 + k) * 12 + j0 + l] = acc[k * 4 + l];
+            }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int l = 0; l < 4; ++l) {
+                H[(i0 + k) * 12 + j0 + l] = acc[k * 4 + l];
+                if (bi != bj) H[(j0 + l) * 12 + i0 + k] = acc[k * 4 + l];
+            }
+    }
+}
 
 __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, const double* __restrict__ kst,
                                                         const double* __restrict__ lst, int write_res) {
     __shared__ double rows[TILE_ROWS * ROW_STRIDE];
     __shared__ double rw[TILE_ROWS];
-    __shared__ double part[4 * 32 * 16];
+    __shared__ int segm[TILE_SEGS * SEGM_STRIDE];
+    __shared__ int prow[TILE_PROWS];
+    __shared__ int pr0[TILE_PAIRS + 1];
+    __shared__ int lrow[TILE_ROWS];
+    __shared__ int lr0[TILE_LMS + 1];
     __shared__ double red[TILE_OBS / 64];
     const int tile = blockIdx.x, tid = threadIdx.x;
     const int obs0 = P.tile_obs0[tile], nobs = P.tile_nobs[tile];
+    const int seg0 = P.tile_seg0[tile], nseg = P.tile_nseg[tile];
+    const int pair0 = P.tile_pair0[tile], npair = P.tile_npair[tile];
+    const int lm0 = P.tile_lm0[tile], nlm = P.tile_nlm[tile];
+    LBA_TMARK(P.tdbg_lin, 0);
+
+    // ---- stage the tile's index lists in LDS (fixed-count loops: all loads issue before the stores)
+    {
+        const int q0 = P.pair_r0[pair0], nq = P.pair_r0[pair0 + npair] - q0;
+        const int m0 = P.lm_r0[lm0], nm = P.lm_r0[lm0 + nlm] - m0;
+#pragma unroll
+        for (int k = 0; k < (TILE_SEGS * SEGM_STRIDE + TILE_OBS - 1) / TILE_OBS; ++k) {
+            const int t = tid + k * TILE_OBS;
+            if (t < nseg * SEGM_STRIDE) segm[t] = P.seg_meta[(size_t)seg0 * SEGM_STRIDE + t];
+        }
+#pragma unroll
+        for (int k = 0; k < TILE_PROWS / TILE_OBS; ++k) {
+            const int t = tid + k * TILE_OBS;
+            if (t < nq) prow[t] = P.pair_rows[q0 + t];
+        }
+#pragma unroll
+        for (int k = 0; k < TILE_ROWS / TILE_OBS + 1; ++k) {
+            const int t = tid + k * TILE_OBS;
+            if (t < nm) lrow[t] = P.lm_rows[m0 + t];
+        }
+#pragma unroll
+        for (int k = 0; k < (TILE_PAIRS + TILE_OBS) / TILE_OBS; ++k) {
+            const int t = tid + k * TILE_OBS;
+            if (t <= npair) pr0[t] = P.pair_r0[pair0 + t] - q0;
+        }
+        if (tid <= nlm) lr0[tid] = P.lm_r0[lm0 + tid] - m0;
+    }
 
     // ---- phase 1: one observation per lane: residual, robust weight, Jacobian rows -> LDS
     double rho0 = 0.0;
@@ -146,77 +249,27 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, const doub
         if (write_res)
             for (int d = 0; d < 3; ++d) P.ob_res[3 * (size_t)o + d] = d < dim ? e[d] : 0.0;
     }
-    const double tchi = block_sum<TILE_OBS>(rho0, red);
+    const double tchi = block_sum<TILE_OBS>(rho0, red);   // (its barrier also publishes rows / lists)
     if (tid == 0) P.chi_lin[tile] = tchi;
-    __syncthreads();
+    LBA_TMARK(P.tdbg_lin, 1);
 
-    // ---- phase 2: Hpp / b_p partial per pose-pair segment: H += s r r^T over the segment's rows
-    const int seg0 = P.tile_seg0[tile], nseg = P.tile_nseg[tile];
-    const int blk = tid & 31, rg = tid >> 5;
-    const bool act = blk < 27;
-    const int bi = act ? c_bi[blk] : 0, bj = act ? c_bj[blk] : 0;
-    for (int si = 0; si < nseg; ++si) {
-        const int sg = seg0 + si;
-        const int r0 = P.seg_row0[sg], nr = P.seg_nrows[sg];
-        double acc[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[q] = 0.0;
-        if (act) {
-            for (int r = r0 + rg; r < r0 + nr; r += 4) {
-                const double* Rr = rows + r * ROW_STRIDE;
-                const double s = rw[r];
-                double a[4], c[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) a[k] = s * Rr[4 * bi + k];
-#pragma unroll
-                for (int l = 0; l < 4; ++l) c[l] = (4 * bj + l <= 24) ? Rr[4 * bj + l] : 0.0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-#pragma unroll
-                    for (int l = 0; l < 4; ++l) acc[k * 4 + l] += a[k] * c[l];
-            }
-#pragma unroll
-            for (int q = 0; q < 16; ++q) part[(rg * 32 + blk) * 16 + q] = acc[q];
-        }
-        __syncthreads();
-        const int* sl = P.seg_slot + 5 * (size_t)sg;
-        const int* gl = P.seg_gslot + 2 * (size_t)sg;
-        for (int out = tid; out < 27 * 16; out += TILE_OBS) {
-            const int b = out >> 4, q = out & 15;
-            const double v = part[(0 * 32 + b) * 16 + q] + part[(1 * 32 + b) * 16 + q] +
-                             part[(2 * 32 + b) * 16 + q] + part[(3 * 32 + b) * 16 + q];
-            const int i = 4 * c_bi[b] + (q >> 2), j = 4 * c_bj[b] + (q & 3);
-            if (j == 24) {   // b = -J^T rho' Omega e
-                if (i < 12) { if (gl[0] >= 0) P.gslab[(size_t)gl[0] * 12 + i] = -v; }
-                else if (i < 24) { if (gl[1] >= 0) P.gslab[(size_t)gl[1] * 12 + i - 12] = -v; }
-            } else if (j < 24 && i <= j) {
-                if (j < 12) {
-                    if (sl[0] >= 0) { double* H = P.hslab + (size_t)sl[0] * 144; H[i * 12 + j] = v; H[j * 12 + i] = v; }
-                } else if (i >= 12) {
-                    if (sl[2] >= 0) {
-                        double* H = P.hslab + (size_t)sl[2] * 144;
-                        H[(i - 12) * 12 + (j - 12)] = v;
-                        H[(j - 12) * 12 + (i - 12)] = v;
-                    }
-                } else if (sl[1] >= 0) {
-                    double* H = P.hslab + (size_t)sl[1] * 144;
-                    if (sl[3]) H[(j - 12) * 12 + i] = v;   // block stored for (b, a): transposed
-                    else H[i * 12 + (j - 12)] = v;
-                }
-            }
-        }
-        __syncthreads();
+    // ---- phase 2: Hpp / b_p partial per pose-pair segment, one (segment, 4x4 block) per task
+    for (int task = tid; task < nseg * 27; task += TILE_OBS) {
+        const int si = task / 27;
+        int bi, bj;
+        seg_block(task - si * 27, &bi, &bj);
+        seg_task(P, rows, rw, segm + si * SEGM_STRIDE, bi, bj);
     }
+    LBA_TMARK(P.tdbg_lin, 2);
 
-    // ---- phase 3: Hpl per (KF, landmark) pair, deterministic row lists
-    const int pair0 = P.tile_pair0[tile], npair = P.tile_npair[tile];
+    // ---- phase 3: Hpl per (KF, landmark) pair from the staged row lists
     for (int task = tid; task < npair * 3; task += TILE_OBS) {
-        const int p = pair0 + task / 3, sb = task % 3;
+        const int pl = task / 3, sb = task % 3;
         double acc[12];
 #pragma unroll
         for (int q = 0; q < 12; ++q) acc[q] = 0.0;
-        for (int q = P.pair_r0[p]; q < P.pair_r0[p + 1]; ++q) {
-            const int code = P.pair_rows[q];
+        for (int q = pr0[pl]; q < pr0[pl + 1]; ++q) {
+            const int code = prow[q];
             const int r = code & 0xffff, side = code >> 16;
             const double* Rr = rows + r * ROW_STRIDE;
             const double s = rw[r];
@@ -227,21 +280,22 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, const doub
                 for (int a = 0; a < 3; ++a) acc[i * 3 + a] += ji * Rr[25 + a];
             }
         }
-        double* H = P.Hpl + (size_t)p * 36 + 12 * sb;
+        double* H = P.Hpl + (size_t)(pair0 + pl) * 36 + 12 * sb;
 #pragma unroll
         for (int q = 0; q < 12; ++q) H[q] = acc[q];
     }
+    LBA_TMARK(P.tdbg_lin, 3);
     // ---- phase 4: Hll / bl per landmark
-    const int lm0 = P.tile_lm0[tile], nlm = P.tile_nlm[tile];
     for (int t = tid; t < nlm; t += TILE_OBS) {
         const int l = lm0 + t;
         double H[9], b[3];
 #pragma unroll
         for (int q = 0; q < 9; ++q) H[q] = 0.0;
         b[0] = b[1] = b[2] = 0.0;
-        for (int q = P.lm_r0[l]; q < P.lm_r0[l + 1]; ++q) {
-            const double* Rr = rows + P.lm_rows[q] * ROW_STRIDE;
-            const double s = rw[P.lm_rows[q]];
+        for (int q = lr0[t]; q < lr0[t + 1]; ++q) {
+            const int r = lrow[q];
+            const double* Rr = rows + r * ROW_STRIDE;
+            const double s = rw[r];
             const double e = Rr[24];
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
@@ -254,6 +308,7 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, const doub
         for (int q = 0; q < 9; ++q) P.Hll[(size_t)l * 9 + q] = H[q];
         for (int q = 0; q < 3; ++q) P.bl[(size_t)l * 3 + q] = b[q];
     }
+    LBA_TMARK(P.tdbg_lin, 4);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -368,12 +423,18 @@ __global__ __launch_bounds__(256) void k_schur(DevProblem P, double lambda) {
     __shared__ double Dl[TILE_LMS * 12];   // Dinv (9) + bl (3) per landmark
     __shared__ short slot[TILE_LMS * TILE_KF];
     __shared__ signed char pl[TILE_PAIRS]; // tile-local KF index of each pair
+    __shared__ signed char pm[TILE_PAIRS]; // tile-local landmark index of each pair
     __shared__ int kfl[TILE_KF];
     const int tile = blockIdx.x, tid = threadIdx.x;
     const int pair0 = P.tile_pair0[tile], npair = P.tile_npair[tile];
     const int lm0 = P.tile_lm0[tile], nlm = P.tile_nlm[tile];
     const int kf0 = P.tile_kf0[tile], nkf = P.tile_nkf[tile];
-    for (int t = tid; t < npair * 36; t += 256) Hs[t] = P.Hpl[(size_t)pair0 * 36 + t];
+    LBA_TMARK(P.tdbg_schur, 0);
+#pragma unroll
+    for (int k = 0; k < TILE_PAIRS * 36 / 256; ++k) {   // fixed count: all loads issue before the stores
+        const int t = tid + k * 256;
+        if (t < npair * 36) Hs[t] = P.Hpl[(size_t)pair0 * 36 + t];
+    }
     for (int t = tid; t < TILE_LMS * TILE_KF; t += 256) slot[t] = -1;
     if (tid < nkf) kfl[tid] = P.tkf_list[kf0 + tid];
     if (tid < nlm) {
@@ -386,6 +447,7 @@ __global__ __launch_bounds__(256) void k_schur(DevProblem P, double lambda) {
         for (int q = 0; q < 3; ++q) Dl[tid * 12 + 9 + q] = P.bl[(size_t)l * 3 + q];
     }
     __syncthreads();
+    LBA_TMARK(P.tdbg_schur, 1);
     for (int t = tid; t < npair; t += 256) {
         const int p = pair0 + t, m = P.pair_lm[p] - lm0, k = P.pair_kf[p];
         int lk = 0;
@@ -393,12 +455,14 @@ __global__ __launch_bounds__(256) void k_schur(DevProblem P, double lambda) {
             if (kfl[l] == k) lk = l;
         slot[m * TILE_KF + lk] = (short)t;
         pl[t] = (signed char)lk;
+        pm[t] = (signed char)m;
     }
+    __syncthreads();
+    LBA_TMARK(P.tdbg_schur, 2);
     // V = Hpl Dinv, g = V bl : one (pair, row) per task
     for (int task = tid; task < npair * 12; task += 256) {
         const int t = task / 12, r = task % 12;
-        const int m = P.pair_lm[pair0 + t] - lm0;
-        const double* D = Dl + m * 12;
+        const double* D = Dl + pm[t] * 12;
         const double h0 = Hs[t * 36 + r * 3], h1 = Hs[t * 36 + r * 3 + 1], h2 = Hs[t * 36 + r * 3 + 2];
         const double v0 = h0 * D[0] + h1 * D[3] + h2 * D[6];
         const double v1 = h0 * D[1] + h1 * D[4] + h2 * D[7];
@@ -407,6 +471,7 @@ __global__ __launch_bounds__(256) void k_schur(DevProblem P, double lambda) {
         gs[t * 12 + r] = v0 * D[9] + v1 * D[10] + v2 * D[11];
     }
     __syncthreads();
+    LBA_TMARK(P.tdbg_schur, 3);
     const int sent0 = P.tile_sent0[tile], nsent = P.tile_nsent[tile];
     for (int task = tid; task < nsent * 9; task += 256) {
         const int e = task / 9, sub = task % 9, sr = sub / 3, sc = sub % 3;
@@ -431,14 +496,18 @@ __global__ __launch_bounds__(256) void k_schur(DevProblem P, double lambda) {
 #pragma unroll
             for (int l = 0; l < 4; ++l) o[(4 * sr + k) * 12 + 4 * sc + l] = acc[k * 4 + l];
     }
+    LBA_TMARK(P.tdbg_schur, 4);
     // rhs partials: sum over the tile's pairs of g = V bl for every tile KF (block_solver.hpp:395-401)
     for (int task = tid; task < nkf * 12; task += 256) {
         const int l = task / 12, r = task % 12;
         double v = 0.0;
-        for (int t = 0; t < npair; ++t)
-            if (pl[t] == l) v += gs[t * 12 + r];
+        for (int m = 0; m < nlm; ++m) {   // pairs of KF l, in pair order (one per landmark at most)
+            const int t = slot[m * TILE_KF + l];
+            if (t >= 0) v += gs[t * 12 + r];
+        }
         P.gpslab[(size_t)P.tkf_gslot[kf0 + l] * 12 + r] = v;
     }
+    LBA_TMARK(P.tdbg_schur, 5);
 }
 
 __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, double lambda, int flags) {
@@ -912,7 +981,7 @@ static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 void launch_pair_prep(const DevProblem& P, const double* kst, hipStream_t s) {
     const int n = P.n_gp + P.n_kf;
-    if (n) hipLaunchKernelGGL(k_pair_prep, dim3(cdiv(n, 64)), dim3(64), 0, s, P, kst);
+    if (n) hipLaunchKernelGGL(k_pair_prep, dim3(cdiv(n, PREP_THREADS)), dim3(PREP_THREADS), 0, s, P, kst);
 }
 void launch_linearize(const DevProblem& P, const double* kst, const double* lst, int write_res, hipStream_t s) {
     if (P.n_tiles) hipLaunchKernelGGL(k_linearize, dim3(P.n_tiles), dim3(TILE_OBS), 0, s, P, kst, lst, write_res);

@@ -1,0 +1,73 @@
+"""Per-phase cycle breakdown of k_linearize / k_schur (diagnostics).
+
+Runs a window with LBA_PHASE_TIMING set (the library then records clock64() at the phase boundaries of
+every workgroup and dumps them when the problem is destroyed), then prints per-phase averages and how
+the per-tile time depends on the tile shape.
+
+    python scripts/phase_times.py [--config cfg1_local_50kf] [--iters 3] [--out gpurun_out/phases.txt]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "amc-slam_amd"))
+
+LIN_PHASES = ["obs residual+J -> LDS", "Hpp segments", "Hpl pairs", "Hll/bl"]
+SCHUR_PHASES = ["stage Hpl + Dinv", "slot map", "V = Hpl Dinv", "S partials", "rhs partials"]
+SHAPE = ["nobs", "nseg", "npair", "nlm", "nsent", "nkf"]
+
+
+def load(path):
+    raw = open(path, "rb").read()
+    nt = int(np.frombuffer(raw[:4], np.int32)[0])
+    off = 4
+    lin = np.frombuffer(raw[off:off + nt * 16 * 8], np.uint64).reshape(nt, 16).astype(np.int64)
+    off += nt * 16 * 8
+    sch = np.frombuffer(raw[off:off + nt * 16 * 8], np.uint64).reshape(nt, 16).astype(np.int64)
+    off += nt * 16 * 8
+    shape = np.frombuffer(raw[off:off + 6 * nt * 4], np.int32).reshape(6, nt)
+    return nt, lin, sch, shape
+
+
+def report(name, stamps, phases, shape, out):
+    d = np.diff(stamps[:, :len(phases) + 1], axis=1)
+    tot = stamps[:, len(phases)] - stamps[:, 0]
+    out.append(f"== {name}: {stamps.shape[0]} workgroups, cycles per workgroup (clock64)")
+    out.append(f"   total: mean {tot.mean():10.0f}  p50 {np.median(tot):10.0f}  p95 {np.percentile(tot, 95):10.0f}  max {tot.max():10.0f}")
+    for i, ph in enumerate(phases):
+        out.append(f"   {ph:24s} mean {d[:, i].mean():10.0f} ({100 * d[:, i].mean() / tot.mean():5.1f} %)  p95 {np.percentile(d[:, i], 95):10.0f}")
+    for j, s in enumerate(SHAPE):
+        v = shape[j].astype(float)
+        c = np.corrcoef(v, tot)[0, 1] if v.std() > 0 else float("nan")
+        out.append(f"   shape {s:6s} mean {v.mean():7.1f} max {v.max():6.0f}  corr(total) {c:+.2f}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfg1_local_50kf")
+    ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "phases.txt"))
+    ap.add_argument("--dump", default="/tmp/lba_phase_times.bin")
+    args = ap.parse_args()
+    os.environ["LBA_PHASE_TIMING"] = args.dump
+    from amc_lba import Problem
+    from amc_lba.synth import make_config_window
+    win = make_config_window(args.config)
+    p = Problem(win, early_stop=0)
+    p.optimize(args.iters)
+    p.close()
+    nt, lin, sch, shape = load(args.dump)
+    out = [f"config {args.config}: {nt} tiles"]
+    report("k_linearize", lin, LIN_PHASES, shape, out)
+    report("k_schur", sch, SCHUR_PHASES, shape, out)
+    text = "\n".join(out)
+    print(text)
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    open(args.out, "w").write(text + "\n")
+
+
+if __name__ == "__main__":
+    main()
