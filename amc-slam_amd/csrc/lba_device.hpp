@@ -7,7 +7,8 @@
 //   lm state      [n_lm][3]                                     — two copies (current / trial)
 //   observations  SoA, device order: meta(kind|cam<<4), kf_a, kf_b, gp pair, landmark,
 //                 pair slots a/b, tile-local LDS row, t, z[3], w
-//   gp pairs      [n_gp][GPP_STRIDE] per (prev KF, KF) interpolation quantities (lba::GPPair)
+//   gp samples    [n_gps][GPS_STRIDE] per (prev KF, KF, observation time): interpolated pose and the
+//                 6x24 Jacobian factor N (lba::GPSample); one per camera time stamp, not per observation
 //   Hpl           [n_pairs][12][3] one block per unique (non-fixed KF, landmark)
 //   Hll, bl       [n_lm][9], [n_lm][3]
 //   hslab/gslab   per (tile, pose-pair segment) partial of Hpp blocks / b_p (and per prior /
@@ -50,16 +51,18 @@ struct DevProblem {
     const int* ob_meta;
     const int* ob_kfa;
     const int* ob_kfb;
-    const int* ob_gp;
+    const int* ob_gp;       // GP observations: GP pose sample (lba::GPSample) index, else -1
     const int* ob_lm;
     const int* ob_row;
-    const double* ob_t;
     const double* ob_z;     // [n_obs][3]
     const double* ob_w;
     // keyframes
     const int* kf_hidx;
-    const int* gp_kfa;
+    const int* gp_kfa;      // per GP pair (prev KF, KF)
     const int* gp_kfb;
+    const int* gp_s0;       // [n_gp + 1] the pair's pose samples (contiguous)
+    const double* gps_t;    // per sample: observation time
+    int n_gps;
     const double* camd;     // [n_cam][CAMD_STRIDE]
     // tiles
     const int* tile_obs0;
@@ -113,8 +116,8 @@ struct DevProblem {
     double qcinv[36];
     double huber_mono, huber_stereo, huber_prior;
     // work buffers
-    double* gpp;            // [n_gp][GPP_STRIDE]
-    double* kfp_pose;       // [n_kf][KFP_STRIDE]
+    double* gps;            // [n_gps][GPS_STRIDE] GP pose samples: Rwb twb N (lba::GPSample)
+    double* kfp_pose;       // [n_kf][KFP_STRIDE] Rwb twb (same prefix as a sample)
     double* hslab;          // [n_hslots][144] Hpp partial blocks, target-sorted
     double* gslab;          // [n_gslots][12] b_p partials, target-sorted
     double* sslab;          // [n_sslots][144] Schur partial blocks, target-sorted
@@ -146,7 +149,7 @@ struct DevProblem {
 };
 
 // launchers (lba_kernels.hip)
-void launch_pair_prep(const DevProblem& P, const double* kst, hipStream_t s);
+void launch_gp_prep(const DevProblem& P, const double* kst, int jac, hipStream_t s);
 void launch_linearize(const DevProblem& P, const double* kst, const double* lst, int write_res, hipStream_t s);
 void launch_prior_lin(const DevProblem& P, const double* kst, hipStream_t s);
 void launch_schur(const DevProblem& P, double lambda, hipStream_t s);
@@ -160,6 +163,6 @@ void launch_eval(const DevProblem& P, const double* kst, const double* lst, hipS
 void launch_finalize(const DevProblem& P, hipStream_t s);
 void launch_depth(const DevProblem& P, const double* kst, const double* lst, unsigned char* ok, hipStream_t s);
 
-constexpr int GPP_STRIDE = 171;     // doubles in lba::GPPair (static_assert in lba_kernels.hip)
+constexpr int GPS_STRIDE = 156;     // doubles in lba::GPSample (static_assert in lba_kernels.hip)
 
 }  // namespace lba

@@ -267,6 +267,28 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             }
         }
 
+    // GP pose samples: distinct observation times per GP pair (one per camera time stamp in
+    // LocalGPBA), contiguous per pair
+    std::vector<int> gp_s0(gp_a.size() + 1, 0), sample_of(n_obs, -1);
+    std::vector<double> gps_t;
+    {
+        std::vector<std::vector<double>> ts(gp_a.size());
+        for (int i = 0; i < n_obs; ++i)
+            if (is_gp(obs[i].kind)) ts[gpmap[std::make_pair(obs[i].kf_a, obs[i].kf_b)]].push_back(obs[i].t);
+        for (size_t g = 0; g < ts.size(); ++g) {
+            std::sort(ts[g].begin(), ts[g].end());
+            ts[g].erase(std::unique(ts[g].begin(), ts[g].end()), ts[g].end());
+            gp_s0[g + 1] = gp_s0[g] + (int)ts[g].size();
+            for (double t : ts[g]) gps_t.push_back(t);
+        }
+        for (int i = 0; i < n_obs; ++i)
+            if (is_gp(obs[i].kind)) {
+                const int g = gpmap[std::make_pair(obs[i].kf_a, obs[i].kf_b)];
+                const double* b = gps_t.data() + gp_s0[g];
+                sample_of[i] = gp_s0[g] + (int)(std::lower_bound(b, b + (gp_s0[g + 1] - gp_s0[g]), obs[i].t) - b);
+            }
+    }
+
     // (KF, landmark) pairs, per device landmark, ascending pose block
     std::vector<int> lm_pair0(nl + 1, 0), pair_lm, pair_kf;
     std::vector<std::vector<int>> lm_kfs(nl);
@@ -455,7 +477,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
 
     // ---- observations in device order
     std::vector<int> ob_meta(n_obs), ob_kfa(n_obs), ob_kfb(n_obs), ob_gp(n_obs), ob_lm(n_obs);
-    std::vector<double> ob_t(n_obs), ob_z(3 * (size_t)n_obs), ob_w(n_obs);
+    std::vector<double> ob_z(3 * (size_t)n_obs), ob_w(n_obs);
     p->obs_dev.assign(n_obs, -1);
     for (int q = 0; q < n_obs; ++q) {
         const lba_obs& o = obs[obs_of[q]];
@@ -463,9 +485,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         ob_meta[q] = o.kind | (o.cam << 4);
         ob_kfa[q] = is_gp(o.kind) ? o.kf_a : -1;
         ob_kfb[q] = o.kf_b;
-        ob_gp[q] = is_gp(o.kind) ? gpmap[std::make_pair(o.kf_a, o.kf_b)] : -1;
+        ob_gp[q] = is_gp(o.kind) ? sample_of[obs_of[q]] : -1;
         ob_lm[q] = p->lm_dev[o.lm];
-        ob_t[q] = o.t;
         ob_z[3 * (size_t)q] = o.z[0]; ob_z[3 * (size_t)q + 1] = o.z[1]; ob_z[3 * (size_t)q + 2] = o.z[2];
         ob_w[q] = o.w;
     }
@@ -508,7 +529,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     std::vector<int> ob_row_dev(n_obs);
     for (int q = 0; q < n_obs; ++q) ob_row_dev[q] = ob_row[q];
     D.ob_row = dupload(p, ob_row_dev);
-    D.ob_t = dupload(p, ob_t); D.ob_z = dupload(p, ob_z); D.ob_w = dupload(p, ob_w);
+    D.ob_z = dupload(p, ob_z); D.ob_w = dupload(p, ob_w);
+    D.gp_s0 = dupload(p, gp_s0); D.gps_t = dupload(p, gps_t); D.n_gps = (int)gps_t.size();
     D.kf_hidx = dupload(p, p->kf_hidx); D.gp_kfa = dupload(p, gp_a); D.gp_kfb = dupload(p, gp_b);
     D.camd = dupload(p, camd);
     D.tile_obs0 = dupload(p, t_obs0); D.tile_nobs = dupload(p, t_nobs); D.tile_lm0 = dupload(p, t_lm0);
@@ -541,7 +563,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.huber_mono = p->cfg.huber_mono;
     D.huber_stereo = p->cfg.huber_stereo;
     D.huber_prior = p->cfg.huber_prior;
-    D.gpp = dalloc<double>(p, (size_t)GPP_STRIDE * std::max(D.n_gp, 1));
+    D.gps = dalloc<double>(p, (size_t)GPS_STRIDE * std::max(D.n_gps, 1));
     D.kfp_pose = dalloc<double>(p, (size_t)KFP_STRIDE * std::max(n_kf, 1));
     D.hslab = dalloc<double>(p, (size_t)144 * std::max(n_hslots, 1));
     D.gslab = dalloc<double>(p, (size_t)12 * std::max(n_gslots, 1));
@@ -598,7 +620,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
 // ------------------------------------------------------------------------------------------------
 void linearize(lba_problem* p, int write_res, bool timed = false) {
     const DevProblem& D = p->D;
-    launch_pair_prep(D, p->kst[p->cur], p->stream);
+    launch_gp_prep(D, p->kst[p->cur], 1, p->stream);
     if (timed) HIPCHK(hipEventRecord(p->ev[6], p->stream));
     launch_linearize(D, p->kst[p->cur], p->lst[p->cur], write_res, p->stream);
     if (timed) HIPCHK(hipEventRecord(p->ev[7], p->stream));
@@ -620,7 +642,7 @@ void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs) {
     if (evs) HIPCHK(hipEventRecord(evs[1], p->stream));
     launch_update(D, lambda, p->kst[p->cur], p->lst[p->cur], p->kst[nx], p->lst[nx], p->stream);
     if (evaluate) {
-        launch_pair_prep(D, p->kst[nx], p->stream);
+        launch_gp_prep(D, p->kst[nx], 0, p->stream);
         launch_eval(D, p->kst[nx], p->lst[nx], p->stream);
     }
     launch_finalize(D, p->stream);
@@ -632,7 +654,7 @@ void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs) {
 
 double eval_current(lba_problem* p) {
     const DevProblem& D = p->D;
-    launch_pair_prep(D, p->kst[p->cur], p->stream);
+    launch_gp_prep(D, p->kst[p->cur], 0, p->stream);
     launch_eval(D, p->kst[p->cur], p->lst[p->cur], p->stream);
     launch_finalize(D, p->stream);
     HIPCHK(hipGetLastError());

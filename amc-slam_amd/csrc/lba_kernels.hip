@@ -2,7 +2,8 @@
 //
 // One LM trial (OptimizationAlgorithmLevenberg::solve, optimization_algorithm_levenberg.cpp:61-169)
 // maps to:
-//   k_pair_prep      per (prev KF, KF) GP quantities + per-KF rotations       (GaussianProcess.cc:23-42)
+//   k_gp_prep        per GP pair and observation time: interpolated pose + Jacobian factor, per-KF
+//                    poses                                                  (GaussianProcess.cc:23-42)
 //   k_linearize      per tile of landmarks: residual, Huber, analytic J straight into an LDS row
 //                    buffer, then deterministic on-chip reductions into Hpp/b segment partials,
 //                    Hpl blocks and Hll/bl (BlockSolver::buildSystem, block_solver.hpp:502-560;
@@ -24,7 +25,7 @@
 
 namespace lba {
 
-static_assert(sizeof(GPPair) == GPP_STRIDE * sizeof(double), "GPPair layout drifted");
+static_assert(sizeof(GPSample) == GPS_STRIDE * sizeof(double), "GPSample layout drifted");
 
 // phase stamps for diagnostics only (buffer allocated when LBA_PHASE_TIMING is set; the uniform
 // null test costs one scalar branch otherwise)
@@ -68,38 +69,112 @@ __device__ __forceinline__ void load_cam(const double* c, CamD* d) {
     d->fx = c[12]; d->fy = c[13]; d->cx = c[14]; d->cy = c[15];
 }
 
-// Pose of the body at the observation time: GP interpolation between (kf_a, kf_b) for GP edges,
-// the KF pose otherwise.  Returns the stereo bf of the edge's first KF vertex.
-__device__ __forceinline__ double obs_pose(const DevProblem& P, const double* kst, int o, bool gp, ObsPose* op,
-                                           GPScalars* g, const GPPair** pp) {
-    if (gp) {
-        const GPPair* q = reinterpret_cast<const GPPair*>(P.gpp + (size_t)P.ob_gp[o] * GPP_STRIDE);
-        *g = gp_scalars(q->t1, q->t2, P.ob_t[o]);
-        gp_pose(*q, *g, op);
-        *pp = q;
-        return kst[(size_t)P.ob_kfa[o] * KF_STRIDE + 14];
+// Pose of the body at the observation time (Rwb, twb) and, for GP edges, the observation's
+// Jacobian factor N: both come from the GP pose sample (GP edges) or the KF pose (EdgeMono /
+// EdgeStereo), whose records share the Rwb(9) twb(3) prefix.  Returns the stereo bf of the edge's
+// first KF vertex.
+__device__ __forceinline__ double obs_pose(const DevProblem& P, const double* kst, int o, bool gp, double* Rwb,
+                                           double* twb, const double** N) {
+    const int ka = gp ? P.ob_kfa[o] : P.ob_kfb[o];
+    const double* S = gp ? P.gps + (size_t)P.ob_gp[o] * GPS_STRIDE : P.kfp_pose + (size_t)P.ob_kfb[o] * KFP_STRIDE;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Rwb[i] = S[i];
+    twb[0] = S[9]; twb[1] = S[10]; twb[2] = S[11];
+    *N = gp ? S + 12 : nullptr;
+    return kst[(size_t)ka * KF_STRIDE + 14];
+}
+
+// One observation of the linearisation (DIM compile-time so every per-row array stays in
+// registers): residual, Huber weight, Jacobian rows into the LDS row buffer; returns rho(chi2).
+template <int DIM>
+__device__ __forceinline__ double lin_obs(const DevProblem& P, const double* kst, const double* lst, int o, int cam,
+                                          bool gp, double* rows, double* rw, int write_res) {
+    CamD cd;
+    load_cam(P.camd + (size_t)cam * CAMD_STRIDE, &cd);
+    double Rwb[9], twb[3];
+    const double* N;
+    const double bf = obs_pose(P, kst, o, gp, Rwb, twb, &N);
+    const double* Xw = lst + (size_t)P.ob_lm[o] * 3;
+    double z[DIM];
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) z[d] = P.ob_z[3 * (size_t)o + d];
+    const double w = P.ob_w[o];
+    double Xb[3], Xc[3], e[DIM];
+    project_residual<DIM>(Rwb, twb, cd, Xw, z, bf, Xb, Xc, e);
+    double chi = 0.0;
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) chi += e[d] * (w * e[d]);
+    double r0, r1;
+    huber(chi, DIM == 3 ? P.huber_stereo : P.huber_mono, &r0, &r1);
+    const int row = P.ob_row[o];
+    double* R = rows + row * ROW_STRIDE;
+    obs_jacobian<DIM>(Rwb, cd, Xb, Xc, bf, N, R, ROW_STRIDE, 25);
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) {
+        R[d * ROW_STRIDE + 24] = e[d];
+        rw[row + d] = r1 * w;   // robustInformation = rho' * Omega (base_edge.h:96-102)
     }
-    const int k = P.ob_kfb[o];
-    const double* kp = P.kfp_pose + (size_t)k * KFP_STRIDE;
-    for (int i = 0; i < 9; ++i) op->Rwb[i] = kp[i];
-    op->twb[0] = kp[9]; op->twb[1] = kp[10]; op->twb[2] = kp[11];
-    for (int i = 0; i < 6; ++i) op->xi[i] = 0.0;
-    *g = GPScalars{0.0, 0.0, 0.0};
-    *pp = nullptr;
-    return kst[(size_t)k * KF_STRIDE + 14];
+    P.ob_chi2[o] = chi;
+    if (write_res)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) P.ob_res[3 * (size_t)o + d] = d < DIM ? e[d] : 0.0;
+    return r0;
+}
+
+// Residual-only evaluation of one observation (computeError + robust chi2); returns rho(chi2).
+template <int DIM>
+__device__ __forceinline__ double eval_obs(const DevProblem& P, const double* kst, const double* lst, int o,
+                                           int cam, bool gp) {
+    CamD cd;
+    load_cam(P.camd + (size_t)cam * CAMD_STRIDE, &cd);
+    double Rwb[9], twb[3];
+    const double* N;
+    const double bf = obs_pose(P, kst, o, gp, Rwb, twb, &N);
+    double z[DIM];
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) z[d] = P.ob_z[3 * (size_t)o + d];
+    const double w = P.ob_w[o];
+    double Xb[3], Xc[3], e[DIM];
+    project_residual<DIM>(Rwb, twb, cd, lst + (size_t)P.ob_lm[o] * 3, z, bf, Xb, Xc, e);
+    double chi = 0.0;
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) chi += e[d] * (w * e[d]);
+    double r0, r1;
+    huber(chi, DIM == 3 ? P.huber_stereo : P.huber_mono, &r0, &r1);
+    P.ob_chi2[o] = chi;
+    return r0;
 }
 
 // ------------------------------------------------------------------------------------------------
+// GP pose samples: one workgroup per GP pair builds the pair quantities once (lane 0, into LDS),
+// then one lane per sample of that pair evaluates the interpolated pose and (jac) the Jacobian
+// factor N.  Trailing workgroups write the KF poses used by the non-GP edges.
 constexpr int PREP_THREADS = 64;
-__global__ __launch_bounds__(PREP_THREADS) void k_pair_prep(DevProblem P, const double* __restrict__ kst) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < P.n_gp) {
-        const double* ka = kst + (size_t)P.gp_kfa[i] * KF_STRIDE;
-        const double* kb = kst + (size_t)P.gp_kfb[i] * KF_STRIDE;
-        gp_pair_build(load_se3(ka), ka + 7, load_se3(kb), kb + 7, ka[13], kb[13],
-                      reinterpret_cast<GPPair*>(P.gpp + (size_t)i * GPP_STRIDE));
-    } else if (i < P.n_gp + P.n_kf) {
-        const int k = i - P.n_gp;
+__global__ __launch_bounds__(PREP_THREADS) void k_gp_prep(DevProblem P, const double* __restrict__ kst, int jac) {
+    __shared__ GPPair pr;
+    const int tid = threadIdx.x;
+    if ((int)blockIdx.x < P.n_gp) {
+        const int i = blockIdx.x;
+        if (tid == 0) {
+            const double* ka = kst + (size_t)P.gp_kfa[i] * KF_STRIDE;
+            const double* kb = kst + (size_t)P.gp_kfb[i] * KF_STRIDE;
+            gp_pair_build(load_se3(ka), ka + 7, load_se3(kb), kb + 7, ka[13], kb[13], &pr, jac != 0);
+        }
+        __syncthreads();
+        for (int sidx = P.gp_s0[i] + tid; sidx < P.gp_s0[i + 1]; sidx += PREP_THREADS) {
+            GPSample* S = reinterpret_cast<GPSample*>(P.gps + (size_t)sidx * GPS_STRIDE);
+            if (jac) {
+                gp_sample_build(pr, P.gps_t[sidx], S);
+            } else {
+                double xi[6];
+                GPScalars g;
+                gp_sample_pose(pr, P.gps_t[sidx], S->Rwb, S->twb, xi, &g);
+            }
+        }
+        return;
+    }
+    const int k = (blockIdx.x - P.n_gp) * PREP_THREADS + tid;
+    if (k < P.n_kf) {
         const double* kk = kst + (size_t)k * KF_STRIDE;
         double R[9];
         qmat(Quat{kk[0], kk[1], kk[2], kk[3]}, R);
@@ -220,34 +295,9 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, const doub
         const int o = obs0 + tid;
         const int meta = P.ob_meta[o];
         const int kind = meta & 15, cam = meta >> 4;
-        const int dim = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? 3 : 2;
         const bool gp = kind <= LBA_STEREO_GP;
-        CamD cd;
-        load_cam(P.camd + (size_t)cam * CAMD_STRIDE, &cd);
-        ObsPose op;
-        GPScalars g;
-        const GPPair* pp;
-        const double bf = obs_pose(P, kst, o, gp, &op, &g, &pp);
-        const double* Xw = lst + (size_t)P.ob_lm[o] * 3;
-        const double z[3] = {P.ob_z[3 * o], P.ob_z[3 * o + 1], P.ob_z[3 * o + 2]};
-        const double w = P.ob_w[o];
-        double Xb[3], Xc[3], e[3];
-        project_residual(op, cd, Xw, z, bf, dim, Xb, Xc, e);
-        double chi = 0.0;
-        for (int d = 0; d < dim; ++d) chi += e[d] * (w * e[d]);
-        double r0, r1;
-        huber(chi, dim == 3 ? P.huber_stereo : P.huber_mono, &r0, &r1);
-        rho0 = r0;
-        const int row = P.ob_row[o];
-        double* R = rows + row * ROW_STRIDE;
-        obs_jacobian(op, cd, Xb, Xc, bf, dim, gp, pp, g, R, ROW_STRIDE, 25);
-        for (int d = 0; d < dim; ++d) {
-            R[d * ROW_STRIDE + 24] = e[d];
-            rw[row + d] = r1 * w;   // robustInformation = rho' * Omega (base_edge.h:96-102)
-        }
-        P.ob_chi2[o] = chi;
-        if (write_res)
-            for (int d = 0; d < 3; ++d) P.ob_res[3 * (size_t)o + d] = d < dim ? e[d] : 0.0;
+        rho0 = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? lin_obs<3>(P, kst, lst, o, cam, gp, rows, rw, write_res)
+                                                             : lin_obs<2>(P, kst, lst, o, cam, gp, rows, rw, write_res);
     }
     const double tchi = block_sum<TILE_OBS>(rho0, red);   // (its barrier also publishes rows / lists)
     if (tid == 0) P.chi_lin[tile] = tchi;
@@ -885,24 +935,9 @@ __global__ __launch_bounds__(TILE_OBS) void k_eval(DevProblem P, const double* _
         const int o = P.tile_obs0[tile] + tid;
         const int meta = P.ob_meta[o];
         const int kind = meta & 15, cam = meta >> 4;
-        const int dim = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? 3 : 2;
         const bool gp = kind <= LBA_STEREO_GP;
-        CamD cd;
-        load_cam(P.camd + (size_t)cam * CAMD_STRIDE, &cd);
-        ObsPose op;
-        GPScalars g;
-        const GPPair* pp;
-        const double bf = obs_pose(P, kst, o, gp, &op, &g, &pp);
-        const double z[3] = {P.ob_z[3 * o], P.ob_z[3 * o + 1], P.ob_z[3 * o + 2]};
-        const double w = P.ob_w[o];
-        double Xb[3], Xc[3], e[3];
-        project_residual(op, cd, lst + (size_t)P.ob_lm[o] * 3, z, bf, dim, Xb, Xc, e);
-        double chi = 0.0;
-        for (int d = 0; d < dim; ++d) chi += e[d] * (w * e[d]);
-        double r0, r1;
-        huber(chi, dim == 3 ? P.huber_stereo : P.huber_mono, &r0, &r1);
-        rho0 = r0;
-        P.ob_chi2[o] = chi;
+        rho0 = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? eval_obs<3>(P, kst, lst, o, cam, gp)
+                                                             : eval_obs<2>(P, kst, lst, o, cam, gp);
     }
     const double s = block_sum<TILE_OBS>(rho0, red);
     if (tid == 0) P.chi_eval[tile] = s;
@@ -979,9 +1014,9 @@ __global__ __launch_bounds__(256) void k_depth(DevProblem P, const double* __res
 // ------------------------------------------------------------------------------------------------ launchers
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
-void launch_pair_prep(const DevProblem& P, const double* kst, hipStream_t s) {
-    const int n = P.n_gp + P.n_kf;
-    if (n) hipLaunchKernelGGL(k_pair_prep, dim3(cdiv(n, PREP_THREADS)), dim3(PREP_THREADS), 0, s, P, kst);
+void launch_gp_prep(const DevProblem& P, const double* kst, int jac, hipStream_t s) {
+    const int nb = P.n_gp + cdiv(P.n_kf, PREP_THREADS);
+    if (nb) hipLaunchKernelGGL(k_gp_prep, dim3(nb), dim3(PREP_THREADS), 0, s, P, kst, jac);
 }
 void launch_linearize(const DevProblem& P, const double* kst, const double* lst, int write_res, hipStream_t s) {
     if (P.n_tiles) hipLaunchKernelGGL(k_linearize, dim3(P.n_tiles), dim3(TILE_OBS), 0, s, P, kst, lst, write_res);

@@ -316,8 +316,9 @@ struct GPPair {
     double t1, t2;
 };
 
+// full = false: only what the interpolated pose needs (T1, v1, xi12, w2; residual evaluation)
 LBA_HD void gp_pair_build(const SE3& Ta, const double* va, const SE3& Tb, const double* vb, double ta, double tb,
-                          GPPair* P) {
+                          GPPair* P, bool full = true) {
     P->T1q[0] = Ta.q.x; P->T1q[1] = Ta.q.y; P->T1q[2] = Ta.q.z; P->T1q[3] = Ta.q.w;
     for (int i = 0; i < 3; ++i) P->T1t[i] = Ta.t[i];
     for (int i = 0; i < 6; ++i) P->v1[i] = va[i];
@@ -326,6 +327,9 @@ LBA_HD void gp_pair_build(const SE3& Ta, const double* va, const SE3& Tb, const 
     se3_log(T12, P->xi12);
     right_jac_inv(P->xi12, P->G2a);
     matmul(P->G2a, vb, P->w2, 6, 6, 1);
+    P->t1 = ta;
+    P->t2 = tb;
+    if (!full) return;
     // Ad(exp(xi12))^-1 = Ad(exp(xi12)^-1)
     const SE3 E = se3_exp(P->xi12);
     const SE3 Ei = se3_inv(E);
@@ -337,8 +341,6 @@ LBA_HD void gp_pair_build(const SE3& Ta, const double* va, const SE3& Tb, const 
     matmul(ad2, P->G1a, P->G1b, 6, 6, 6);
     matmul(ad2, P->G2a, P->G2b, 6, 6, 6);
     for (int i = 0; i < 36; ++i) { P->G1b[i] *= -0.5; P->G2b[i] *= -0.5; }
-    P->t1 = ta;
-    P->t2 = tb;
 }
 
 // ---------------------------------------------------------------- observation model
@@ -357,118 +359,134 @@ LBA_HD void cam_derive(const Cam& c, CamD* d) {
     d->fx = c.fx; d->fy = c.fy; d->cx = c.cx; d->cy = c.cy;
 }
 
-// Body pose used for one observation: rotation Rwb, translation twb, and for GP edges the
-// interpolation tangent xi(t).
-struct ObsPose { double Rwb[9], twb[3]; double xi[6]; };
+// GP pose sample: everything an observation at time t between (KF_a, KF_b) needs.  All observations
+// of one camera of one keyframe share t, so a window has O(pairs x cameras) samples for O(obs) GP
+// observations and the interpolation + Jacobian chain is evaluated once per sample.
+//   T(t) = T1 exp(xi),  xi = p2 v1 + l1 xi12 + l2 Jr^-1(xi12) v2        (QueryPose, GaussianProcess.cc:23-42)
+// The reference chain (src/G2oTypes.cc:258-314) J_a = [K (l1 A1 + l2 B1) + J1 Ad(exp(-xi)), p2 K],
+// J_b = [K (l1 C + l2 D), l2 K C] with K = J1 Jr(xi) is refactored as J = J1 N with the 6x24 matrix
+//   N = [Jr (l1 A1 + l2 B1) + Ad(exp(-xi)) | p2 Jr | Jr (l1 C + l2 D) | l2 Jr C].
+constexpr int GPS_N = 6 * 24;
+struct GPSample {
+    double Rwb[9], twb[3];
+    double N[GPS_N];   // stored transposed: N[c * 6 + l] = N(l, c), so one column is 48 contiguous bytes
+};
 
-// GP-interpolated body pose at time t (QueryPose): Twb = T1 exp(p2 v1 + l1 xi12 + l2 w2)
-LBA_HD void gp_pose(const GPPair& P, const GPScalars& g, ObsPose* op) {
-    for (int i = 0; i < 6; ++i) op->xi[i] = g.p2 * P.v1[i] + g.l1 * P.xi12[i] + g.l2 * P.w2[i];
-    const SE3 dT = se3_exp(op->xi);
+LBA_HD void gp_sample_pose(const GPPair& P, double t, double* Rwb, double* twb, double* xi, GPScalars* g) {
+    *g = gp_scalars(P.t1, P.t2, t);
+    for (int i = 0; i < 6; ++i) xi[i] = g->p2 * P.v1[i] + g->l1 * P.xi12[i] + g->l2 * P.w2[i];
+    const SE3 dT = se3_exp(xi);
     SE3 T1;
     T1.q = Quat{P.T1q[0], P.T1q[1], P.T1q[2], P.T1q[3]};
     T1.t[0] = P.T1t[0]; T1.t[1] = P.T1t[1]; T1.t[2] = P.T1t[2];
     const SE3 T = se3_mul(T1, dT);
-    qmat(T.q, op->Rwb);
-    op->twb[0] = T.t[0]; op->twb[1] = T.t[1]; op->twb[2] = T.t[2];
+    qmat(T.q, Rwb);
+    twb[0] = T.t[0]; twb[1] = T.t[1]; twb[2] = T.t[2];
+}
+
+LBA_HD void gp_sample_build(const GPPair& P, double t, GPSample* S) {
+    double xi[6];
+    GPScalars g;
+    gp_sample_pose(P, t, S->Rwb, S->twb, xi, &g);
+    // Jr(xi) = [Jl, Q; 0, Jl] with Jl = LeftJacobianRot3(-w), Q = LeftJacobianPose3Q(-xi)
+    double Jl[9], Q[9];
+    right_jac_blocks(xi, Jl, Q);
+    double Jr[36];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            Jr[i * 6 + j] = Jl[i * 3 + j];
+            Jr[i * 6 + 3 + j] = Q[i * 3 + j];
+            Jr[(3 + i) * 6 + j] = 0.0;
+            Jr[(3 + i) * 6 + 3 + j] = Jl[i * 3 + j];
+        }
+    // Ad(exp(-xi)) = [R', t'^ R'; 0, R']
+    const double mxi[6] = {-xi[0], -xi[1], -xi[2], -xi[3], -xi[4], -xi[5]};
+    const SE3 Em = se3_exp(mxi);
+    double Rm[9], Ht[9], tR[9];
+    qmat(Em.q, Rm);
+    hat3(Em.t, Ht);
+    mul33(Ht, Rm, tR);
+    double MA[36], MC[36];
+    for (int i = 0; i < 36; ++i) {
+        MA[i] = g.l1 * P.G1a[i] + g.l2 * P.G1b[i];
+        MC[i] = g.l1 * P.G2a[i] + g.l2 * P.G2b[i];
+    }
+    for (int r = 0; r < 6; ++r)
+        for (int c = 0; c < 6; ++c) {
+            double na = 0.0, nb = 0.0, nc = 0.0;
+            for (int l = 0; l < 6; ++l) {
+                na += Jr[r * 6 + l] * MA[l * 6 + c];
+                nb += Jr[r * 6 + l] * MC[l * 6 + c];
+                nc += Jr[r * 6 + l] * P.G2a[l * 6 + c];
+            }
+            double ad = 0.0;
+            if (r < 3) ad = (c < 3) ? Rm[r * 3 + c] : tR[r * 3 + c - 3];
+            else if (c >= 3) ad = Rm[(r - 3) * 3 + c - 3];
+            S->N[c * 6 + r] = na + ad;
+            S->N[(6 + c) * 6 + r] = g.p2 * Jr[r * 6 + c];
+            S->N[(12 + c) * 6 + r] = nb;
+            S->N[(18 + c) * 6 + r] = g.l2 * nc;
+        }
 }
 
 // Xb = Rwb^T (Xw - twb), Xc = Rcb Xb + tcb; residual e = z - pi(Xc) (3rd row u - bf/z)
-LBA_HD void project_residual(const ObsPose& op, const CamD& c, const double* Xw, const double* z, double bf,
-                             int dim, double* Xb, double* Xc, double* e) {
-    const double d[3] = {Xw[0] - op.twb[0], Xw[1] - op.twb[1], Xw[2] - op.twb[2]};
-    mul33tv(op.Rwb, d, Xb);
+template <int DIM>
+LBA_HD void project_residual(const double* Rwb, const double* twb, const CamD& c, const double* Xw, const double* z,
+                             double bf, double* Xb, double* Xc, double* e) {
+    const double d[3] = {Xw[0] - twb[0], Xw[1] - twb[1], Xw[2] - twb[2]};
+    mul33tv(Rwb, d, Xb);
     mul33v(c.Rcb, Xb, Xc);
     Xc[0] += c.tcb[0]; Xc[1] += c.tcb[1]; Xc[2] += c.tcb[2];
     const double u = c.fx * Xc[0] / Xc[2] + c.cx;
     const double v = c.fy * Xc[1] / Xc[2] + c.cy;
     e[0] = z[0] - u;
     e[1] = z[1] - v;
-    e[2] = (dim == 3) ? z[2] - (u - bf * (1.0 / Xc[2])) : 0.0;
+    if (DIM == 3) e[2] = z[2] - (u - bf * (1.0 / Xc[2]));
 }
 
-// Jacobian rows of one reprojection observation, columns
-// [KF_a pose(6) vel(6) | KF_b pose(6) vel(6) | point(3)] (27), dim rows.
-// GP chain (src/G2oTypes.cc:258-314 with the four-scalar closed form):
-//   K = J1 Jr(xi); J_a = [K (l1 A1 + l2 B1) + J1 Ad(exp(-xi)), p2 K]; J_b = [K (l1 C + l2 D), l2 K C]
+// Jacobian rows of one reprojection observation (DIM = 2 mono, 3 stereo), columns
+// [KF_a pose(6) vel(6) | KF_b pose(6) vel(6) | point(3)] (27):
+//   J1 = P Rcb [I, -Xb^] (pose at the observation time), J_pt = -P Rcb Rwb^T
+//   GP edges: pose/vel columns = J1 N (N of the observation's GP sample, stored transposed);
+//   EdgeMono/EdgeStereo (src/G2oTypes.cc:445-495): KF_b pose columns = J1, velocity columns 0.
 // Output row r: pose/vel columns 0..23 at J[r*ldJ + c], point columns at J[r*ldJ + pcol + j]
 // (host harness: ldJ 27, pcol 24; kernels write straight into an LDS row buffer).
-template <typename OutT>
-LBA_HD void obs_jacobian(const ObsPose& op, const CamD& c, const double* Xb, const double* Xc, double bf, int dim,
-                         bool gp, const GPPair* P, const GPScalars& g, OutT* J, int ldJ, int pcol) {
-    // projection Jacobian P (dim x 3)
+template <int DIM, typename OutT, typename NT>
+LBA_HD void obs_jacobian(const double* Rwb, const CamD& c, const double* Xb, const double* Xc, double bf,
+                         const NT* N, OutT* J, int ldJ, int pcol) {
+    // projection Jacobian P (DIM x 3)
     const double iz = 1.0 / Xc[2];
     double Pj[9];
     Pj[0] = c.fx * iz; Pj[1] = 0.0; Pj[2] = -c.fx * Xc[0] / (Xc[2] * Xc[2]);
     Pj[3] = 0.0; Pj[4] = c.fy * iz; Pj[5] = -c.fy * Xc[1] / (Xc[2] * Xc[2]);
-    if (dim == 3) { Pj[6] = Pj[0]; Pj[7] = Pj[1]; Pj[8] = Pj[2] + bf * (1.0 / (Xc[2] * Xc[2])); }
-    // M = P Rcb (dim x 3);  J1 = [M, -M Xb^] ;  Jpt = -M Rwb^T
-    double M[9], H[9], MH[9];
-    for (int r = 0; r < dim; ++r)
+    if (DIM == 3) { Pj[6] = Pj[0]; Pj[7] = Pj[1]; Pj[8] = Pj[2] + bf * (1.0 / (Xc[2] * Xc[2])); }
+    // M = P Rcb (DIM x 3);  J1 = [M, -M Xb^] ;  Jpt = -M Rwb^T
+    double M[3 * DIM], H[9], J1[6 * DIM];
+    for (int r = 0; r < DIM; ++r)
         for (int j = 0; j < 3; ++j)
             M[r * 3 + j] = Pj[r * 3 + 0] * c.Rcb[0 * 3 + j] + Pj[r * 3 + 1] * c.Rcb[1 * 3 + j] + Pj[r * 3 + 2] * c.Rcb[2 * 3 + j];
     hat3(Xb, H);
-    for (int r = 0; r < dim; ++r)
-        for (int j = 0; j < 3; ++j)
-            MH[r * 3 + j] = M[r * 3 + 0] * H[0 * 3 + j] + M[r * 3 + 1] * H[1 * 3 + j] + M[r * 3 + 2] * H[2 * 3 + j];
-    double J1[18];
-    for (int r = 0; r < dim; ++r)
-        for (int j = 0; j < 3; ++j) { J1[r * 6 + j] = M[r * 3 + j]; J1[r * 6 + 3 + j] = -MH[r * 3 + j]; }
-    for (int r = 0; r < dim; ++r)
+    for (int r = 0; r < DIM; ++r)
+        for (int j = 0; j < 3; ++j) {
+            J1[r * 6 + j] = M[r * 3 + j];
+            J1[r * 6 + 3 + j] = -(M[r * 3 + 0] * H[0 * 3 + j] + M[r * 3 + 1] * H[1 * 3 + j] + M[r * 3 + 2] * H[2 * 3 + j]);
+        }
+    for (int r = 0; r < DIM; ++r)
         for (int j = 0; j < 3; ++j)   // -M Rwb^T : (M Rbw)_{rj} = sum_k M_rk Rwb_jk
-            J[r * ldJ + pcol + j] = -(M[r * 3 + 0] * op.Rwb[j * 3 + 0] + M[r * 3 + 1] * op.Rwb[j * 3 + 1] + M[r * 3 + 2] * op.Rwb[j * 3 + 2]);
-    if (!gp) {
-        for (int r = 0; r < dim; ++r) {
+            J[r * ldJ + pcol + j] = -(M[r * 3 + 0] * Rwb[j * 3 + 0] + M[r * 3 + 1] * Rwb[j * 3 + 1] + M[r * 3 + 2] * Rwb[j * 3 + 2]);
+    if (!N) {
+        for (int r = 0; r < DIM; ++r) {
             for (int j = 0; j < 12; ++j) J[r * ldJ + j] = 0.0;
             for (int j = 0; j < 6; ++j) { J[r * ldJ + 12 + j] = J1[r * 6 + j]; J[r * ldJ + 18 + j] = 0.0; }
         }
         return;
     }
-    // Jr(xi) = [Jl, Q; 0, Jl] with Jl = LeftJacobianRot3(-w), Q = LeftJacobianPose3Q(-xi)
-    double Jl[9], Q[9];
-    right_jac_blocks(op.xi, Jl, Q);
-    double K[18];   // K = J1 Jr = [J1a Jl, J1a Q + J1b Jl]
-    for (int r = 0; r < dim; ++r)
-        for (int j = 0; j < 3; ++j) {
+    for (int cc = 0; cc < 24; ++cc) {
+        double n[6];
+        for (int l = 0; l < 6; ++l) n[l] = N[cc * 6 + l];
+        for (int r = 0; r < DIM; ++r) {
             const double* a = J1 + r * 6;
-            K[r * 6 + j] = a[0] * Jl[0 * 3 + j] + a[1] * Jl[1 * 3 + j] + a[2] * Jl[2 * 3 + j];
-            K[r * 6 + 3 + j] = a[0] * Q[0 * 3 + j] + a[1] * Q[1 * 3 + j] + a[2] * Q[2 * 3 + j] +
-                               a[3] * Jl[0 * 3 + j] + a[4] * Jl[1 * 3 + j] + a[5] * Jl[2 * 3 + j];
-        }
-    // Ad(exp(-xi)) = [R', t'^ R'; 0, R']
-    const double mxi[6] = {-op.xi[0], -op.xi[1], -op.xi[2], -op.xi[3], -op.xi[4], -op.xi[5]};
-    const SE3 Em = se3_exp(mxi);
-    double Rm[9], Ht[9], tR[9];
-    qmat(Em.q, Rm);
-    hat3(Em.t, Ht);
-    mul33(Ht, Rm, tR);
-    for (int r = 0; r < dim; ++r) {
-        const double* k = K + r * 6;
-        const double* a = J1 + r * 6;
-        OutT* Ja = J + r * ldJ;
-        OutT* Jb = J + r * ldJ + 12;
-        double kc[6];
-        double ja[6];
-        for (int j = 0; j < 6; ++j) {
-            double sa = 0.0, sb = 0.0, sc = 0.0, sd = 0.0;
-            for (int l = 0; l < 6; ++l) {
-                sa += k[l] * P->G1a[l * 6 + j];
-                sb += k[l] * P->G1b[l * 6 + j];
-                sc += k[l] * P->G2a[l * 6 + j];
-                sd += k[l] * P->G2b[l * 6 + j];
-            }
-            ja[j] = g.l1 * sa + g.l2 * sb;
-            Jb[j] = g.l1 * sc + g.l2 * sd;
-            kc[j] = sc;
-        }
-        for (int j = 0; j < 3; ++j) {   // + J1 Ad(exp(-xi))
-            Ja[j] = ja[j] + (a[0] * Rm[0 * 3 + j] + a[1] * Rm[1 * 3 + j] + a[2] * Rm[2 * 3 + j]);
-            Ja[3 + j] = ja[3 + j] + (a[0] * tR[0 * 3 + j] + a[1] * tR[1 * 3 + j] + a[2] * tR[2 * 3 + j] +
-                                     a[3] * Rm[0 * 3 + j] + a[4] * Rm[1 * 3 + j] + a[5] * Rm[2 * 3 + j]);
-        }
-        for (int j = 0; j < 6; ++j) {
-            Ja[6 + j] = g.p2 * k[j];
-            Jb[6 + j] = g.l2 * kc[j];
+            J[r * ldJ + cc] = a[0] * n[0] + a[1] * n[1] + a[2] * n[2] + a[3] * n[3] + a[4] * n[4] + a[5] * n[5];
         }
     }
 }

@@ -29,28 +29,35 @@ extern "C" int mh_obs_linearize(const lba_kf* kfs, const double* lm, const lba_o
     c.fx = cams[o->cam].fx; c.fy = cams[o->cam].fy; c.cx = cams[o->cam].cx; c.cy = cams[o->cam].cy;
     CamD cd;
     cam_derive(c, &cd);
-    ObsPose op;
-    GPPair P;
-    GPScalars g{0, 0, 0};
+    double Rwb[9], twb[3];
+    GPSample S;
     double bf;
-    if (gp) {
+    if (gp) {   // the kernels' path: GP pair -> pose sample at the observation time -> J = J1 N
         const lba_kf& a = kfs[o->kf_a];
         const lba_kf& b = kfs[o->kf_b];
+        GPPair P;
         gp_pair_build(mk(a.q, a.t), a.vel, mk(b.q, b.t), b.vel, a.time, b.time, &P);
-        g = gp_scalars(P.t1, P.t2, o->t);
-        gp_pose(P, g, &op);
+        gp_sample_build(P, o->t, &S);
+        memcpy(Rwb, S.Rwb, sizeof(Rwb));
+        memcpy(twb, S.twb, sizeof(twb));
         bf = a.bf;
     } else {
         const lba_kf& b = kfs[o->kf_b];
         SE3 T = mk(b.q, b.t);
-        qmat(T.q, op.Rwb);
-        op.twb[0] = T.t[0]; op.twb[1] = T.t[1]; op.twb[2] = T.t[2];
-        for (int i = 0; i < 6; ++i) op.xi[i] = 0.0;
+        qmat(T.q, Rwb);
+        twb[0] = T.t[0]; twb[1] = T.t[1]; twb[2] = T.t[2];
         bf = b.bf;
     }
     double Xb[3], Xc[3];
-    project_residual(op, cd, lm + 3 * o->lm, o->z, bf, dim, Xb, Xc, err);
-    obs_jacobian(op, cd, Xb, Xc, bf, dim, gp, &P, g, J, 27, 24);
+    const double* N = gp ? S.N : nullptr;
+    err[2] = 0.0;
+    if (dim == 3) {
+        project_residual<3>(Rwb, twb, cd, lm + 3 * o->lm, o->z, bf, Xb, Xc, err);
+        obs_jacobian<3>(Rwb, cd, Xb, Xc, bf, N, J, 27, 24);
+    } else {
+        project_residual<2>(Rwb, twb, cd, lm + 3 * o->lm, o->z, bf, Xb, Xc, err);
+        obs_jacobian<2>(Rwb, cd, Xb, Xc, bf, N, J, 27, 24);
+    }
     return dim;
 }
 
