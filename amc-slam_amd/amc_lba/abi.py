@@ -74,8 +74,13 @@ class LbaStats(ctypes.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+# lba_config.flags (include/amc_lba.h)
+FLAG_TIME_SWEEP = 1
+FLAG_TIME_PHASES = 2
+
+
 def make_config(qc_diag=(0.02, 0.02, 0.02, 0.002, 0.002, 0.002), huber_mono=None, huber_stereo=None,
-                huber_prior=0.0, lambda_init=1.0, tau=1e-5, max_trials=10, early_stop=1, device=0):
+                huber_prior=0.0, lambda_init=1.0, tau=1e-5, max_trials=10, early_stop=1, device=0, flags=0):
     """LocalGPBA defaults: Huber deltas are float sqrt(5.991)/sqrt(7.815) widened to double
     (src/Optimizer.cc:975-978), lambda0 = 1.0 (:848-856), tau 1e-5, 10 trials."""
     cfg = LbaConfig()
@@ -94,7 +99,7 @@ def make_config(qc_diag=(0.02, 0.02, 0.02, 0.002, 0.002, 0.002), huber_mono=None
     cfg.max_trials = max_trials
     cfg.early_stop = early_stop
     cfg.device = device
-    cfg.flags = 0
+    cfg.flags = flags
     return cfg
 
 

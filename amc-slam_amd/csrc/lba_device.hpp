@@ -38,6 +38,8 @@ constexpr int ROW_STRIDE = 28;      // LDS Jacobian row: Ja(12) Jb(12) e(1) Jp(3
 constexpr int TILE_SEGS = 48;       // pose-pair segments per tile (k_linearize stages their metadata)
 constexpr int SEG_MAX_ROWS = 48;    // longer (a, b) runs are split so the segment tasks stay balanced
 constexpr int TILE_PROWS = 2 * TILE_ROWS;   // pair row-list entries per tile (each row feeds <= 2 pairs)
+constexpr int TILE_SLIST = 1024;    // Schur (pair, pair, landmark) triples per tile (k_schur stages them)
+constexpr int TILE_SENT = TILE_KF * (TILE_KF + 1) / 2;   // KF-pair Schur entries per tile
 constexpr int SEGM_STRIDE = 8;      // staged segment record: row0 nrows aa ab bb ab_transposed ga gb
 
 constexpr int CHOL_NB = 32;         // Cholesky panel / tile width
@@ -83,6 +85,8 @@ struct DevProblem {
     const int* seg_b;
     const int* seg_row0;    // tile-local first row
     const int* seg_nrows;
+    const int* sent_r0;     // [n_sentries + 1] CSR into sent_list
+    const int* sent_list;   // per entry: landmarks coupling k1, k2: pair1 | pair2 << 8 | lm << 16 (tile-local)
     const int* sent_l1;     // per Schur entry: tile-local KF index of k1 / k2
     const int* sent_l2;
     // pairs / landmarks
@@ -141,6 +145,7 @@ struct DevProblem {
     int n_upd_blocks;
     int* info;              // [1] factorisation status
     double* fin;            // [4] chi_lin, chi_eval, scale, info
+    double* hfin;           // host-mapped coherent [4] copy of fin + [4] sequence number (as bits)
     double* ob_chi2;        // [n_obs]
     double* ob_res;         // [n_obs][3]
     // diagnostics (LBA_PHASE_TIMING=<file>): per-workgroup clock64() stamps at phase boundaries
@@ -160,7 +165,7 @@ void launch_cholesky_solve(const DevProblem& P, hipStream_t s);
 void launch_update(const DevProblem& P, double lambda, const double* kst, const double* lst, double* kst_out,
                    double* lst_out, hipStream_t s);
 void launch_eval(const DevProblem& P, const double* kst, const double* lst, hipStream_t s);
-void launch_finalize(const DevProblem& P, hipStream_t s);
+void launch_finalize(const DevProblem& P, unsigned long long seq, hipStream_t s);
 void launch_depth(const DevProblem& P, const double* kst, const double* lst, unsigned char* ok, hipStream_t s);
 
 constexpr int GPS_STRIDE = 156;     // doubles in lba::GPSample (static_assert in lba_kernels.hip)

@@ -7,6 +7,7 @@
 // buffers, so g2o's push/pop/discardTop (sparse_optimizer.cpp:589-613) become a buffer swap.
 // The host reads back four doubles per trial (chi2 before, chi2 after, computeScale, factor status).
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <climits>
 #include <cmath>
@@ -44,7 +45,9 @@ struct lba_problem {
     double* lst[2] = {nullptr, nullptr};
     int cur = 0;
     std::vector<void*> allocs;
-    double* h_fin = nullptr;      // pinned [4]
+    double* h_fin = nullptr;      // host-mapped coherent [8]: trial summary [4] + sequence number
+    double* d_hfin = nullptr;     // its device address
+    unsigned long long fin_seq = 0;
     double lambda = -1.0, ni = 2.0;
     int nBad = 0;
 };
@@ -311,6 +314,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     std::vector<int> tkf_list, seg_a, seg_b, seg_row0, seg_nrows, sent_l1, sent_l2, sent_k1, sent_k2;
     std::vector<int> ob_row(n_obs, 0);
     std::vector<int> pair_r0(n_pairs + 1, 0), pair_rows, lm_r0(nl + 1, 0), lm_rows;
+    std::vector<int> sent_r0(1, 0), sent_list;   // Schur entry -> (pair, pair, landmark) triples
     {
         // segment key of an observation: (pose block a, pose block b)
         auto keyof = [&](int q) {
@@ -324,6 +328,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             int nobs = 0, rows = 0, npair = 0, nlmt = 0;
             std::vector<int> uni;
             std::map<std::pair<int, int>, int> keyrows;
+            int ncomb = 0;   // Schur triples of the tile (sum over landmarks of P (P + 1) / 2)
             int e = d;
             while (e < nl) {
                 int no = lobs0[e + 1] - lobs0[e], nr = 0;
@@ -339,15 +344,17 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 for (int k : lm_kfs[e]) u2.push_back(k);
                 std::sort(u2.begin(), u2.end());
                 u2.erase(std::unique(u2.begin(), u2.end()), u2.end());
+                const int ncl = npl * (npl + 1) / 2;
                 const bool fits = nobs + no <= TILE_OBS && rows + nr <= TILE_ROWS && npair + npl <= TILE_PAIRS &&
-                                  nlmt + 1 <= TILE_LMS && (int)u2.size() <= TILE_KF && nsg <= TILE_SEGS;
+                                  nlmt + 1 <= TILE_LMS && (int)u2.size() <= TILE_KF && nsg <= TILE_SEGS &&
+                                  ncomb + ncl <= TILE_SLIST;
                 if (!fits) {
                     if (e == d)
                         throw ApiError{LBA_E_LIMIT, "landmark " + std::to_string(order[e]) +
                                                         " exceeds tile limits (obs/rows/pairs/keyframes)"};
                     break;
                 }
-                nobs += no; rows += nr; npair += npl; nlmt += 1; uni.swap(u2); keyrows.swap(k2);
+                nobs += no; rows += nr; npair += npl; nlmt += 1; uni.swap(u2); keyrows.swap(k2); ncomb += ncl;
                 ++e;
             }
             const int tile = (int)t_obs0.size();
@@ -412,6 +419,24 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 sent_k1.push_back(pr.first); sent_k2.push_back(pr.second);
             }
             t_nsent.push_back((int)kp.size());
+            // per entry: the tile's landmarks coupling its two KFs, as packed
+            // (tile-local pair of k1) | (tile-local pair of k2) << 8 | (tile-local landmark) << 16
+            {
+                std::vector<std::vector<int>> lists(kp.size());
+                for (int l = d; l < e; ++l) {
+                    const std::vector<int>& ks = lm_kfs[l];
+                    for (size_t a = 0; a < ks.size(); ++a)
+                        for (size_t b = a; b < ks.size(); ++b) {
+                            const size_t en = std::lower_bound(kp.begin(), kp.end(), std::make_pair(ks[a], ks[b])) - kp.begin();
+                            const int t1 = lm_pair0[l] + (int)a - lm_pair0[d], t2 = lm_pair0[l] + (int)b - lm_pair0[d];
+                            lists[en].push_back(t1 | (t2 << 8) | ((l - d) << 16));
+                        }
+                }
+                for (auto& li : lists) {
+                    for (int v : li) sent_list.push_back(v);
+                    sent_r0.push_back((int)sent_list.size());
+                }
+            }
             d = e;
         }
     }
@@ -539,11 +564,13 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.tile_nsent = dupload(p, t_nsent); D.tile_kf0 = dupload(p, t_kf0); D.tile_nkf = dupload(p, t_nkf);
     D.tkf_list = dupload(p, tkf_list);
     D.seg_meta = dupload(p, seg_meta);
+    D.sent_r0 = dupload(p, sent_r0); D.sent_list = dupload(p, sent_list);
     D.seg_a = dupload(p, seg_a); D.seg_b = dupload(p, seg_b); D.seg_row0 = dupload(p, seg_row0);
     D.seg_nrows = dupload(p, seg_nrows); D.sent_l1 = dupload(p, sent_l1); D.sent_l2 = dupload(p, sent_l2);
     D.pair_lm = dupload(p, pair_lm); D.pair_kf = dupload(p, pair_kf); D.pair_r0 = dupload(p, pair_r0);
     D.pair_rows = dupload(p, pair_rows); D.lm_r0 = dupload(p, lm_r0); D.lm_rows = dupload(p, lm_rows);
     D.lm_pair0 = dupload(p, lm_pair0);
+    D.hfin = p->d_hfin;
     if (std::getenv("LBA_PHASE_TIMING")) {
         D.tdbg_lin = dalloc<unsigned long long>(p, (size_t)n_tiles * 16);
         D.tdbg_schur = dalloc<unsigned long long>(p, (size_t)n_tiles * 16);
@@ -630,12 +657,31 @@ void linearize(lba_problem* p, int write_res, bool timed = false) {
     p->linearized = true;
 }
 
+// Publish the trial summary (k_finalize writes it into host-mapped memory) and wait for it by
+// polling its sequence number; the stream is queried now and then so a device fault is reported
+// instead of spinning forever.  sync: also synchronise the stream (callers that copy device
+// buffers afterwards, or read timing events).
+void finalize_and_wait(lba_problem* p, bool sync) {
+    const unsigned long long seq = ++p->fin_seq;
+    launch_finalize(p->D, seq, p->stream);
+    HIPCHK(hipGetLastError());
+    volatile unsigned long long* flag = reinterpret_cast<volatile unsigned long long*>(p->h_fin + 4);
+    for (unsigned it = 1; *flag != seq; ++it) {
+        if ((it & 1023) == 0) {
+            const hipError_t e = hipStreamQuery(p->stream);
+            if (e != hipSuccess && e != hipErrorNotReady) throw HipError{e, "trial kernels"};
+            if (e == hipSuccess && *flag != seq) throw HipError{hipErrorUnknown, "trial summary not published"};
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (sync) HIPCHK(hipStreamSynchronize(p->stream));
+}
+
 // one damped solve + update into the trial buffers + evaluation of the trial state
-void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs) {
+void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs, bool sync = true) {
     const DevProblem& D = p->D;
     const int nx = 1 - p->cur;
-    HIPCHK(hipMemsetAsync(D.info, 0, sizeof(int), p->stream));
-    launch_schur(D, lambda, p->stream);
+    launch_schur(D, lambda, p->stream);   // also clears the factorisation status
     launch_assemble(D, lambda, ASM_SCHUR, p->stream);
     if (evs) HIPCHK(hipEventRecord(evs[0], p->stream));
     launch_cholesky_solve(D, p->stream);
@@ -645,21 +691,15 @@ void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs) {
         launch_gp_prep(D, p->kst[nx], 0, p->stream);
         launch_eval(D, p->kst[nx], p->lst[nx], p->stream);
     }
-    launch_finalize(D, p->stream);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(p->h_fin, D.fin, 4 * sizeof(double), hipMemcpyDeviceToHost, p->stream));
     if (evs) HIPCHK(hipEventRecord(evs[2], p->stream));
-    HIPCHK(hipStreamSynchronize(p->stream));
+    finalize_and_wait(p, sync || evs);
 }
 
 double eval_current(lba_problem* p) {
     const DevProblem& D = p->D;
     launch_gp_prep(D, p->kst[p->cur], 0, p->stream);
     launch_eval(D, p->kst[p->cur], p->lst[p->cur], p->stream);
-    launch_finalize(D, p->stream);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(p->h_fin, D.fin, 4 * sizeof(double), hipMemcpyDeviceToHost, p->stream));
-    HIPCHK(hipStreamSynchronize(p->stream));
+    finalize_and_wait(p, true);
     return p->h_fin[1];
 }
 
@@ -694,11 +734,13 @@ int optimize(lba_problem* p, int iters, volatile const int32_t* stop, lba_stats*
     s.chi2_initial = eval_current(p);
     double last_chi = s.chi2_initial;
     int it = 0, result = LBA_RESULT_OK;
+    const bool tphase = (p->cfg.flags & LBA_FLAG_TIME_PHASES) != 0;
+    const bool tsweep = tphase || (p->cfg.flags & LBA_FLAG_TIME_SWEEP) != 0;
     for (int i = 0; i < iters; ++i) {
         if (stop && *stop) { result = LBA_RESULT_STOPPED; break; }
-        HIPCHK(hipEventRecord(p->ev[0], p->stream));
-        linearize(p, 0, true);
-        HIPCHK(hipEventRecord(p->ev[1], p->stream));
+        if (tphase) HIPCHK(hipEventRecord(p->ev[0], p->stream));
+        linearize(p, 0, tsweep);
+        if (tphase) HIPCHK(hipEventRecord(p->ev[1], p->stream));
         if (i == 0) {
             p->lambda = lambda_init(p);
             p->ni = 2.0;
@@ -707,17 +749,21 @@ int optimize(lba_problem* p, int iters, volatile const int32_t* stop, lba_stats*
         double currentChi = 0.0, iniChi = 0.0, rho = 0.0;
         int qmax = 0;
         do {
-            trial(p, p->lambda, true, p->ev + 2);
+            trial(p, p->lambda, true, tphase ? p->ev + 2 : nullptr, false);
             if (qmax == 0) {
                 currentChi = iniChi = p->h_fin[0];
-                s.ms_linearize += elapsed(p->ev[0], p->ev[1]);
-                s.ms_k_linearize += elapsed(p->ev[6], p->ev[7]);
-                s.n_k_linearize += 1;
+                if (tphase) s.ms_linearize += elapsed(p->ev[0], p->ev[1]);
+                if (tsweep) {
+                    s.ms_k_linearize += elapsed(p->ev[6], p->ev[7]);
+                    s.n_k_linearize += 1;
+                }
             }
-            s.ms_schur += elapsed(qmax == 0 ? p->ev[1] : p->ev[5], p->ev[2]);
-            s.ms_solve += elapsed(p->ev[2], p->ev[3]);
-            s.ms_update_eval += elapsed(p->ev[3], p->ev[4]);
-            HIPCHK(hipEventRecord(p->ev[5], p->stream));
+            if (tphase) {
+                s.ms_schur += elapsed(qmax == 0 ? p->ev[1] : p->ev[5], p->ev[2]);
+                s.ms_solve += elapsed(p->ev[2], p->ev[3]);
+                s.ms_update_eval += elapsed(p->ev[3], p->ev[4]);
+                HIPCHK(hipEventRecord(p->ev[5], p->stream));
+            }
             double tempChi = p->h_fin[1];
             last_chi = tempChi;
             const bool ok2 = p->h_fin[3] == 0.0;
@@ -751,6 +797,7 @@ int optimize(lba_problem* p, int iters, volatile const int32_t* stop, lba_stats*
         p->linearized = false;
         if (result != LBA_RESULT_OK && p->cfg.early_stop) break;
     }
+    HIPCHK(hipStreamSynchronize(p->stream));
     s.iterations = it;
     s.result = result;
     s.chi2_final = last_chi;
@@ -791,7 +838,10 @@ int lba_create(lba_problem** out, const lba_config* cfg) {
         HIPCHK(hipSetDevice(cfg->device));
         HIPCHK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
         for (auto& e : p->ev) HIPCHK(hipEventCreate(&e));
-        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&p->h_fin), 4 * sizeof(double), hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&p->h_fin), 8 * sizeof(double),
+                             hipHostMallocMapped | hipHostMallocCoherent));
+        for (int i = 0; i < 8; ++i) p->h_fin[i] = 0.0;
+        HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->d_hfin), p->h_fin, 0));
     } catch (const HipError& e) {
         delete p;
         return LBA_E_HIP;

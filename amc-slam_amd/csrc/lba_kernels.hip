@@ -37,6 +37,8 @@ static_assert(sizeof(GPSample) == GPS_STRIDE * sizeof(double), "GPSample layout 
         }                                                                           \
     } while (0)
 
+typedef double d4 __attribute__((ext_vector_type(4)));   // v_mfma_f64_16x16x4 accumulator
+
 __device__ __forceinline__ SE3 load_se3(const double* k) {
     SE3 T;
     T.q = Quat{k[0], k[1], k[2], k[3]};
@@ -193,14 +195,32 @@ __device__ __forceinline__ void seg_block(int blk, int* bi, int* bj) {
 }
 
 // one (segment, 4x4 block) task: acc = sum over the segment's rows of (s r)[4bi..] r[4bj..]^T, written
-// to the segment's Hpp / b_p slab slots (upper block + mirror; b = -J^T rho' Omega e)
+// to the segment's Hpp / b_p slab slots (upper block + mirror; b = -J^T rho' Omega e).  Rows are
+// consumed four at a time so their LDS reads are all in flight before the FMAs.
 __device__ __forceinline__ void seg_task(const DevProblem& P, const double* rows, const double* rw, const int* sm,
                                          int bi, int bj) {
-    const int r0 = sm[0], nr = sm[1];
+    const int r0 = sm[0], rend = sm[0] + sm[1];
     double acc[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[q] = 0.0;
-    for (int r = r0; r < r0 + nr; ++r) {
+    int r = r0;
+    for (; r + 4 <= rend; r += 4) {
+        double a[4][4], c[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const double* Rr = rows + (r + u) * ROW_STRIDE;
+            const double s = rw[r + u];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { a[u][k] = s * Rr[4 * bi + k]; c[u][k] = Rr[4 * bj + k]; }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int l = 0; l < 4; ++l) acc[k * 4 + l] += a[u][k] * c[u][l];
+    }
+    for (; r < rend; ++r) {
         const double* Rr = rows + r * ROW_STRIDE;
         const double s = rw[r];
         double a[4], c[4];
@@ -463,97 +483,121 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_hpp_reduce(DevProblem P) {
 }
 
 // Landmark elimination for one tile of landmarks (BlockSolver::solve's Schur loop,
-// block_solver.hpp:381-430): Dinv = (Hll + lambda I)^-1 (Eigen 3x3 adjugate inverse), V = Hpl Dinv,
-// g = V bl, then S partials V(k1) Hpl(k2)^T for every KF pair the tile's landmarks couple and rhs
-// partials sum g per KF.  Everything stays in LDS; Dinv is kept for the back-substitution.
+// block_solver.hpp:381-430): Dinv = (Hll + lambda I)^-1 (Eigen 3x3 adjugate inverse), then for every
+// KF pair (k1, k2) the tile's landmarks couple, the S partial sum_m Hpl(m,k1) Dinv_m Hpl(m,k2)^T, and
+// per tile KF the rhs partial sum_m Hpl(m,k) Dinv_m bl_m.  The S partial of one KF pair is one fp64
+// MFMA product on one wave: K runs over (landmark, 3) with A = Hpl(m,k1) Dinv_m formed on the fly
+// from LDS (so V = Hpl Dinv is never stored) and B = Hpl(m,k2)^T.  Dinv is kept for the
+// back-substitution.  Block 0 also clears the factorisation status for the solve that follows.
 __global__ __launch_bounds__(256) void k_schur(DevProblem P, double lambda) {
-    __shared__ double Vs[TILE_PAIRS * 36];
     __shared__ double Hs[TILE_PAIRS * 36];
-    __shared__ double gs[TILE_PAIRS * 12];
-    __shared__ double Dl[TILE_LMS * 12];   // Dinv (9) + bl (3) per landmark
+    __shared__ double Dl[TILE_LMS * 12];   // Dinv (9) + x = Dinv bl (3) per landmark
+    __shared__ int slst[TILE_SLIST];
+    __shared__ int sl0[TILE_SENT + 1];
     __shared__ short slot[TILE_LMS * TILE_KF];
-    __shared__ signed char pl[TILE_PAIRS]; // tile-local KF index of each pair
-    __shared__ signed char pm[TILE_PAIRS]; // tile-local landmark index of each pair
     __shared__ int kfl[TILE_KF];
-    const int tile = blockIdx.x, tid = threadIdx.x;
+    const int tile = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int pair0 = P.tile_pair0[tile], npair = P.tile_npair[tile];
     const int lm0 = P.tile_lm0[tile], nlm = P.tile_nlm[tile];
     const int kf0 = P.tile_kf0[tile], nkf = P.tile_nkf[tile];
+    const int sent0 = P.tile_sent0[tile], nsent = P.tile_nsent[tile];
     LBA_TMARK(P.tdbg_schur, 0);
+    if (tile == 0 && tid == 0) *P.info = 0;
+    // ---- stage Hpl and the Schur triple lists (fixed-count loops of unconditional loads)
+    const int nh = npair * 36;
+    if (nh > 0) {
+        constexpr int NK = TILE_PAIRS * 36 / 256;
+        double hv[NK];
 #pragma unroll
-    for (int k = 0; k < TILE_PAIRS * 36 / 256; ++k) {   // fixed count: all loads issue before the stores
-        const int t = tid + k * 256;
-        if (t < npair * 36) Hs[t] = P.Hpl[(size_t)pair0 * 36 + t];
+        for (int k = 0; k < NK; ++k) hv[k] = P.Hpl[(size_t)pair0 * 36 + min(tid + k * 256, nh - 1)];
+#pragma unroll
+        for (int k = 0; k < NK; ++k)
+            if (tid + k * 256 < nh) Hs[tid + k * 256] = hv[k];
+    }
+    {
+        const int q0 = P.sent_r0[sent0], nq = P.sent_r0[sent0 + nsent] - q0;
+#pragma unroll
+        for (int k = 0; k < TILE_SLIST / 256; ++k) {
+            const int t = tid + k * 256;
+            if (t < nq) slst[t] = P.sent_list[q0 + t];
+        }
+        if (tid <= nsent) sl0[tid] = P.sent_r0[sent0 + tid] - q0;
     }
     for (int t = tid; t < TILE_LMS * TILE_KF; t += 256) slot[t] = -1;
     if (tid < nkf) kfl[tid] = P.tkf_list[kf0 + tid];
     if (tid < nlm) {
         const int l = lm0 + tid;
-        double H[9], D[9];
+        double H[9], D[9], bl[3];
+#pragma unroll
         for (int q = 0; q < 9; ++q) H[q] = P.Hll[(size_t)l * 9 + q];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) bl[q] = P.bl[(size_t)l * 3 + q];
         H[0] += lambda; H[4] += lambda; H[8] += lambda;   // setLambda on Hll (block_solver.hpp:580-587)
         inv3(H, D);
+#pragma unroll
         for (int q = 0; q < 9; ++q) { Dl[tid * 12 + q] = D[q]; P.Dinv[(size_t)l * 9 + q] = D[q]; }
-        for (int q = 0; q < 3; ++q) Dl[tid * 12 + 9 + q] = P.bl[(size_t)l * 3 + q];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) Dl[tid * 12 + 9 + q] = D[q * 3] * bl[0] + D[q * 3 + 1] * bl[1] + D[q * 3 + 2] * bl[2];
     }
     __syncthreads();
     LBA_TMARK(P.tdbg_schur, 1);
     for (int t = tid; t < npair; t += 256) {
-        const int p = pair0 + t, m = P.pair_lm[p] - lm0, k = P.pair_kf[p];
+        const int m = P.pair_lm[pair0 + t] - lm0, k = P.pair_kf[pair0 + t];
         int lk = 0;
         for (int l = 0; l < nkf; ++l)
             if (kfl[l] == k) lk = l;
         slot[m * TILE_KF + lk] = (short)t;
-        pl[t] = (signed char)lk;
-        pm[t] = (signed char)m;
     }
-    __syncthreads();
     LBA_TMARK(P.tdbg_schur, 2);
-    // V = Hpl Dinv, g = V bl : one (pair, row) per task
-    for (int task = tid; task < npair * 12; task += 256) {
-        const int t = task / 12, r = task % 12;
-        const double* D = Dl + pm[t] * 12;
-        const double h0 = Hs[t * 36 + r * 3], h1 = Hs[t * 36 + r * 3 + 1], h2 = Hs[t * 36 + r * 3 + 2];
-        const double v0 = h0 * D[0] + h1 * D[3] + h2 * D[6];
-        const double v1 = h0 * D[1] + h1 * D[4] + h2 * D[7];
-        const double v2 = h0 * D[2] + h1 * D[5] + h2 * D[8];
-        Vs[t * 36 + r * 3] = v0; Vs[t * 36 + r * 3 + 1] = v1; Vs[t * 36 + r * 3 + 2] = v2;
-        gs[t * 12 + r] = v0 * D[9] + v1 * D[10] + v2 * D[11];
-    }
-    __syncthreads();
-    LBA_TMARK(P.tdbg_schur, 3);
-    const int sent0 = P.tile_sent0[tile], nsent = P.tile_nsent[tile];
-    for (int task = tid; task < nsent * 9; task += 256) {
-        const int e = task / 9, sub = task % 9, sr = sub / 3, sc = sub % 3;
-        const int l1 = P.sent_l1[sent0 + e], l2 = P.sent_l2[sent0 + e];
-        double acc[16];
+    // ---- S partials: one wave per KF pair
+    {
+        const int kq = lane >> 4, cl = lane & 15, cr = min(cl, 11);
+        for (int e = wave; e < nsent; e += 4) {
+            const int qb = sl0[e], nk = 3 * (sl0[e + 1] - qb);
+            d4 c0 = {0.0, 0.0, 0.0, 0.0}, c1 = c0;
+            // K = (landmark, 3): lane k = k0 + kq; two accumulators break the MFMA dependency chain
+            for (int k0 = 0; k0 < nk; k0 += 8) {
+                double av[2], bv[2];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) acc[q] = 0.0;
-        for (int m = 0; m < nlm; ++m) {
-            const int s1 = slot[m * TILE_KF + l1], s2 = slot[m * TILE_KF + l2];
-            if (s1 < 0 || s2 < 0) continue;
-            const double* v = Vs + s1 * 36 + 12 * sr;
-            const double* h = Hs + s2 * 36 + 12 * sc;
+                for (int h = 0; h < 2; ++h) {
+                    const int k = k0 + 4 * h + kq;
+                    const bool ok = k < nk && cl < 12;
+                    const int kk = k < nk ? k : 0;
+                    const int mi = kk / 3, a = kk - 3 * mi;
+                    const int code = slst[qb + mi];
+                    const int t1 = code & 255, t2 = (code >> 8) & 255, m = code >> 16;
+                    const double* h1 = Hs + t1 * 36 + cr * 3;
+                    const double* D = Dl + m * 12;
+                    const double x = h1[0] * D[a] + h1[1] * D[3 + a] + h1[2] * D[6 + a];
+                    const double y = Hs[t2 * 36 + cr * 3 + a];
+                    av[h] = ok ? x : 0.0;
+                    bv[h] = ok ? y : 0.0;
+                }
+                c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0], bv[0], c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1], bv[1], c1, 0, 0, 0);
+            }
+            const d4 c = c0 + c1;
+            double* o = P.sslab + (size_t)P.sslot[sent0 + e] * 144;
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-#pragma unroll
-                for (int l = 0; l < 4; ++l)
-                    acc[k * 4 + l] += v[k * 3] * h[l * 3] + v[k * 3 + 1] * h[l * 3 + 1] + v[k * 3 + 2] * h[l * 3 + 2];
+            for (int q = 0; q < 4; ++q) {
+                const int i = kq + 4 * q;
+                if (i < 12 && cl < 12) o[i * 12 + cl] = c[q];
+            }
         }
-        double* o = P.sslab + (size_t)P.sslot[sent0 + e] * 144;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int l = 0; l < 4; ++l) o[(4 * sr + k) * 12 + 4 * sc + l] = acc[k * 4 + l];
     }
+    LBA_TMARK(P.tdbg_schur, 3);
     LBA_TMARK(P.tdbg_schur, 4);
-    // rhs partials: sum over the tile's pairs of g = V bl for every tile KF (block_solver.hpp:395-401)
+    // ---- rhs partials: sum over the KF's landmarks of Hpl(m,k) (Dinv_m bl_m) (block_solver.hpp:395-401)
     for (int task = tid; task < nkf * 12; task += 256) {
         const int l = task / 12, r = task % 12;
         double v = 0.0;
-        for (int m = 0; m < nlm; ++m) {   // pairs of KF l, in pair order (one per landmark at most)
+        for (int m = 0; m < nlm; ++m) {
             const int t = slot[m * TILE_KF + l];
-            if (t >= 0) v += gs[t * 12 + r];
+            if (t >= 0) {
+                const double* h = Hs + t * 36 + r * 3;
+                const double* x = Dl + m * 12 + 9;
+                v += h[0] * x[0] + h[1] * x[1] + h[2] * x[2];
+            }
         }
         P.gpslab[(size_t)P.tkf_gslot[kf0 + l] * 12 + r] = v;
     }
@@ -604,11 +648,11 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
 // Dense Cholesky S = L L^T (right-looking, one launch per CNB-wide panel).  The system is padded
 // to a multiple of CNB with an identity tail (set once at upload; the factorisation never changes
 // it), so every panel is exactly CNB wide and all loops below are compile-time.
-// Every workgroup owns one lower tile of the trailing matrix; it factors the panel's diagonal
-// block itself (wave 0, one row per lane, pivot by readlane, column broadcast through LDS), solves
-// the panel rows its tile needs (wave 1) and the panel's forward substitution (wave 2), then
-// updates its tile, so a launch has no inter-workgroup communication.  All global operands are
-// loaded at kernel entry, before the dependent chain starts.  The factor goes to Lm transposed
+// Every workgroup owns one lower tile of the trailing matrix; it factors the stacked panel
+// [diagonal block; its tile rows; b_p^T] itself (two waves, one row per lane, pivot by readlane,
+// column broadcast through LDS), which yields L_pp, the panel rows of its tile and y_p = L_pp^-1 b_p
+// in one pass, then updates its tile, so a launch has no inter-workgroup communication.  All
+// global operands are loaded at kernel entry, before the dependent chain starts.  The factor goes to Lm transposed
 // (U = L^T, upper, row-major: what the back-substitution streams) with the
 // reciprocal diagonal in Ldinv; the running right-hand side b is forward-substituted on the fly
 // (y -> yv).  A non-positive pivot sets *info (the LDLT !isPositive failure of
@@ -646,8 +690,8 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restr
     __shared__ double Lt[CNB][CNB + 1];   // diagonal factor, transposed: Lt[c][r] = L(p + r, p + c)
     __shared__ double Pi[CNB][CNB + 1];
     __shared__ double Pj[CNB][CNB + 1];
+    __shared__ double colb[2][CNB];
     __shared__ double dinv[CNB];
-    __shared__ double colb[CNB];
     __shared__ double yp[CNB];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & (CNB - 1);
     const int q = p + CNB, nt = (n - q) / CNB;
@@ -659,19 +703,18 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restr
         while (ti * (ti + 1) / 2 > bid) --ti;
         tj = bid - ti * (ti + 1) / 2;
     }
-    // ---- prefetch: diagonal rows (wave 0), panel rows of tiles ti / tj (wave 1), b_p (wave 2),
-    //      and every thread's 2x2 piece of the trailing tile
+    // ---- prefetch.  Waves 0 and 1 each hold a stacked 64 x 32 panel: lanes 0..31 the diagonal
+    //      block rows, lanes 32..63 the panel rows of tile ti (wave 0) / tile tj (wave 1), or, when
+    //      tj == ti, b_p^T in lane 32 of wave 1 (factorising it as one more row gives y_p = L^-1 b_p).
     double row[CNB];
-    if (wave == 0) {
+    if (wave < 2) {
+        const double* src = nullptr;
+        if (lane < CNB) src = A + (size_t)(p + lane) * n + p;
+        else if (nt > 0 && (wave == 0 || tj != ti)) src = A + (size_t)(q + (wave ? tj : ti) * CNB + l32) * n + p;
+        else if (wave == 1 && lane == CNB) src = b + p;
 #pragma unroll
-        for (int c = 0; c < CNB; ++c) row[c] = A[(size_t)(p + l32) * n + p + c];
-    } else if (wave == 1 && nt > 0) {
-        const int r = q + (lane < CNB ? ti : tj) * CNB + l32;
-#pragma unroll
-        for (int c = 0; c < CNB; ++c) row[c] = A[(size_t)r * n + p + c];
+        for (int c = 0; c < CNB; ++c) row[c] = src ? src[c] : 0.0;
     }
-    double bw = 0.0;
-    if (wave == 2) bw = b[p + l32];
     const int tr = tid >> 4, tc = tid & 15;
     const size_t ra = (size_t)q + ti * CNB + 2 * tr, ca = (size_t)q + tj * CNB + 2 * tc;
     double a00 = 0.0, a01 = 0.0, a10 = 0.0, a11 = 0.0;
@@ -679,68 +722,59 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restr
         a00 = A[ra * n + ca]; a01 = A[ra * n + ca + 1];
         a10 = A[(ra + 1) * n + ca]; a11 = A[(ra + 1) * n + ca + 1];
     }
-    // ---- (1) diagonal block
-    if (wave == 0) {
+    // ---- right-looking panel factorisation, pivots software-pipelined: only l(j+1, j) is on the
+    //      path to the next pivot (one readlane), so the next rsq chain overlaps this pivot's
+    //      column broadcast (LDS) and rank-1 update.  Lanes < k only touch their unused upper triangle.
+    if (wave < 2) {
         bool bad = false;
         double myinv = 1.0;
+        double d0 = readlane_d(row[0], 0);
+        if (!(d0 > 0.0)) { bad = true; d0 = 1.0; }
+        double r = rsqrt_nr(d0);
 #pragma unroll
         for (int j = 0; j < CNB; ++j) {
-            double d = readlane_d(row[j], j);
-            if (!(d > 0.0)) { bad = true; d = 1.0; }
-            const double r = rsqrt_nr(d);
-            const double lij = row[j] * r;   // lane j: sqrt(d); lanes > j: L(l, j); lanes < j: unused
+            const double lij = row[j] * r;   // lane j: sqrt(d); lanes > j: L(l, j)
             row[j] = lij;
             if (lane == j) myinv = r;
-            if (lane < CNB) colb[lane] = lij;
+            double rn = 1.0;
+            if (j + 1 < CNB) {
+                const double c1 = readlane_d(lij, j + 1);
+                row[j + 1] -= lij * c1;
+                pin(row[j + 1]);
+                double dn = readlane_d(row[j + 1], j + 1);
+                if (!(dn > 0.0)) { bad = true; dn = 1.0; }
+                rn = rsqrt_nr(dn);
+            }
+            if (lane < CNB) colb[wave][lane] = lij;
             wave_sync();
             double cb[CNB];
 #pragma unroll
-            for (int k = j + 1; k < CNB; ++k) cb[k] = colb[k];
-            // lanes < k only touch their (unused) upper triangle, so no predication is needed
+            for (int k = j + 2; k < CNB; ++k) cb[k] = colb[wave][k];
 #pragma unroll
-            for (int k = j + 1; k < CNB; ++k) { row[k] -= lij * cb[k]; pin(row[k]); }
+            for (int k = j + 2; k < CNB; ++k) { row[k] -= lij * cb[k]; pin(row[k]); }
             wave_sync();
-            __builtin_amdgcn_sched_barrier(0);   // keep the unrolled pivots from being interleaved
-        }
-        if (lane < CNB) {
-#pragma unroll
-            for (int c = 0; c < CNB; ++c) Lt[c][lane] = (c <= lane) ? row[c] : 0.0;
-            dinv[lane] = myinv;
-        }
-        if (bad && lane == 0 && blockIdx.x == 0) *info = 1 + p;
-    }
-    __syncthreads();
-    // ---- (2) panel rows: x L_pp^T = a, right-looking (column j of L_pp is Lt[j][*])
-    if (wave == 1 && nt > 0) {
-#pragma unroll
-        for (int j = 0; j < CNB; ++j) {
-            const double xj = row[j] * dinv[j];
-            row[j] = xj;
-            double lc[CNB];
-#pragma unroll
-            for (int k = j + 1; k < CNB; ++k) lc[k] = Lt[j][k];
-#pragma unroll
-            for (int k = j + 1; k < CNB; ++k) { row[k] -= xj * lc[k]; pin(row[k]); }
             __builtin_amdgcn_sched_barrier(0);
+            r = rn;
         }
-        if (lane < CNB || tj != ti) {
-            double (*dst)[CNB + 1] = (lane < CNB) ? Pi : Pj;
+        if (wave == 0) {
+            if (lane < CNB) {
 #pragma unroll
-            for (int c = 0; c < CNB; ++c) dst[l32][c] = row[c];
+                for (int c = 0; c < CNB; ++c) Lt[c][lane] = (c <= lane) ? row[c] : 0.0;
+                dinv[lane] = myinv;
+            } else if (nt > 0) {
+#pragma unroll
+                for (int c = 0; c < CNB; ++c) Pi[l32][c] = row[c];
+            }
+            if (bad && lane == 0 && blockIdx.x == 0) *info = 1 + p;
+        } else if (lane >= CNB) {
+            if (nt > 0 && tj != ti) {
+#pragma unroll
+                for (int c = 0; c < CNB; ++c) Pj[l32][c] = row[c];
+            } else if (lane == CNB) {
+#pragma unroll
+                for (int c = 0; c < CNB; ++c) yp[c] = row[c];
+            }
         }
-    }
-    // ---- y_p = L_pp^-1 b_p (wave 2, lane l holds b_{p+l})
-    if (wave == 2 && (ti == tj || blockIdx.x == 0)) {
-        double lr[CNB];
-#pragma unroll
-        for (int c = 0; c < CNB; ++c) lr[c] = Lt[c][l32];
-#pragma unroll
-        for (int j = 0; j < CNB; ++j) {
-            const double yj = readlane_d(bw, j) * dinv[j];
-            bw = (lane == j) ? yj : ((lane > j) ? bw - lr[j] * yj : bw);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (lane < CNB) yp[lane] = bw;
     }
     __syncthreads();
     if (blockIdx.x == 0) {
@@ -754,7 +788,7 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restr
         }
     }
     if (nt == 0) return;
-    // ---- (3) trailing tile update A(ti, tj) -= Pi Pj^T
+    // ---- trailing tile update A(ti, tj) -= Pi Pj^T
     {
         const double (*Qj)[CNB + 1] = (ti == tj) ? Pi : Pj;
         double s00 = 0, s01 = 0, s10 = 0, s11 = 0;
@@ -767,13 +801,13 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restr
         A[ra * n + ca] = a00 - s00; A[ra * n + ca + 1] = a01 - s01;
         A[(ra + 1) * n + ca] = a10 - s10; A[(ra + 1) * n + ca + 1] = a11 - s11;
     }
-    // ---- (4) the tj == 0 workgroups publish the panel rows of L (stored transposed, U = L^T)
+    // ---- the tj == 0 workgroups publish the panel rows of L (stored transposed, U = L^T)
     if (tj == 0)
         for (int t = tid; t < CNB * CNB; t += 256) {
             const int c = t / CNB, i = t % CNB;
             Lm[(size_t)(p + c) * n + q + ti * CNB + i] = Pi[i][c];
         }
-    // ---- (5) forward substitution of the trailing right-hand side
+    // ---- forward substitution of the trailing right-hand side
     if (ti == tj && tid < CNB) {
         double s = 0.0;
 #pragma unroll 8
@@ -967,7 +1001,11 @@ __global__ __launch_bounds__(64) void k_prior_eval(DevProblem P, const double* _
     }
 }
 
-__global__ __launch_bounds__(256) void k_finalize(DevProblem P) {
+// Trial summary: chi2 of the linearisation point, chi2 of the trial state, computeScale, factor
+// status.  Besides the device copy it is published straight into host-mapped coherent memory,
+// followed (after a system-scope fence) by the trial's sequence number, which the host polls:
+// no copy kernel and no stream synchronisation per trial.
+__global__ __launch_bounds__(256) void k_finalize(DevProblem P, unsigned long long seq) {
     __shared__ double red[4];
     const int tid = threadIdx.x;
     const int nc = P.n_tiles + P.n_prior + P.n_vel;
@@ -980,10 +1018,15 @@ __global__ __launch_bounds__(256) void k_finalize(DevProblem P) {
     __syncthreads();
     const double sc = block_sum<256>(c, red);
     if (tid == 0) {
-        P.fin[0] = sa;
-        P.fin[1] = sb;
-        P.fin[2] = sc;
-        P.fin[3] = (double)(*P.info);
+        const double v[4] = {sa, sb, sc, (double)(*P.info)};
+        for (int i = 0; i < 4; ++i) P.fin[i] = v[i];
+        if (P.hfin) {
+            volatile double* h = P.hfin;
+            for (int i = 0; i < 4; ++i) h[i] = v[i];
+            __threadfence_system();
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(P.hfin + 4), seq, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -1055,8 +1098,8 @@ void launch_eval(const DevProblem& P, const double* kst, const double* lst, hipS
     const int n = P.n_prior + P.n_vel;
     if (n) hipLaunchKernelGGL(k_prior_eval, dim3(cdiv(n, 64)), dim3(64), 0, s, P, kst);
 }
-void launch_finalize(const DevProblem& P, hipStream_t s) {
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, P);
+void launch_finalize(const DevProblem& P, unsigned long long seq, hipStream_t s) {
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, P, seq);
 }
 void launch_depth(const DevProblem& P, const double* kst, const double* lst, unsigned char* ok, hipStream_t s) {
     if (P.n_obs) hipLaunchKernelGGL(k_depth, dim3(cdiv(P.n_obs, 256)), dim3(256), 0, s, P, kst, lst, ok);

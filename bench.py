@@ -44,10 +44,15 @@ def sweep_bytes(win):
 
 
 def sweep_flops(win):
-    """Algorithmic fp64 FLOPs of the sweep: per GP observation ~3.25 kFLOP, per non-GP ~1.2 kFLOP
-    (interpolation + exp + projection + Jacobian chain + 27x27 J^T W J)."""
-    gp = int(np.isin(win.obs["kind"], (0, 1)).sum())
-    return 3250.0 * gp + 1200.0 * (len(win.obs) - gp)
+    """Algorithmic fp64 FLOPs of the sweep as this implementation formulates it:
+    per observation row-pair: residual (~60) + Jacobian (GP: J = J1 N, ~700; EdgeMono: ~150) +
+    the J^T W J products over the row's non-zero columns (GP row: 24 pose + e + 3 point columns,
+    ~812 FLOP; EdgeMono row: 12 pose columns, ~272 FLOP).  Stereo observations have 3 rows."""
+    k = win.obs["kind"]
+    gp = np.isin(k, (0, 1))
+    rows = np.where(np.isin(k, (1, 3)), 3, 2)
+    f = np.where(gp, 60 + 700 + 812 * rows, 60 + 150 + 272 * rows)
+    return float(f.sum())
 
 
 def pmc_traffic(workload):
@@ -114,7 +119,9 @@ def main():
     else:
         win = make_config_window(args.config, seed=args.seed)
         ex = None
-    prob = amc_lba.Problem(win, device=local, early_stop=0)
+    # the timed run records HIP events around k_linearize only (LBA_FLAG_TIME_SWEEP): the roofline
+    # below is measured live, per launch, over the timed region
+    prob = amc_lba.Problem(win, device=local, early_stop=0, flags=amc_lba.abi.FLAG_TIME_SWEEP)
 
     # warmup (not timed)
     if args.warmup > 0:
@@ -124,16 +131,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    done, ms_k, n_k = 0, 0.0, 0
-    phase = {"ms_linearize": 0.0, "ms_schur": 0.0, "ms_solve": 0.0, "ms_update_eval": 0.0, "trials": 0}
+    done, ms_k, n_k, trials = 0, 0.0, 0, 0
     while done < args.steps:
         it = min(args.window_iters, args.steps - done)
         n, st = prob.optimize(it)
         done += n
         ms_k += st.ms_k_linearize
         n_k += st.n_k_linearize
-        for k in phase:
-            phase[k] += getattr(st, k)
+        trials += st.trials
         if ex is not None:
             ex.exchange(prob)           # window boundary: publish owned shared landmarks
     torch.cuda.synchronize()
@@ -147,6 +152,12 @@ def main():
         dt = float(tt.item())
 
     if rank == 0:
+        # phase breakdown from a separate, untimed run with every phase evented
+        ph = amc_lba.Problem(win, device=local, early_stop=0, flags=amc_lba.abi.FLAG_TIME_PHASES)
+        n_ph, st_ph = ph.optimize(args.window_iters)
+        phase = {k: getattr(st_ph, k) / max(n_ph, 1) for k in ("ms_linearize", "ms_schur", "ms_solve", "ms_update_eval")}
+        phase["trials"] = st_ph.trials / max(n_ph, 1)
+        ph.close()
         total_iters = done * world
         value = total_iters / dt
         k_ms = ms_k / max(n_k, 1)
@@ -179,7 +190,8 @@ def main():
                               "achieved": F / (k_ms * 1e-3) / 1e12 if n_k else None,
                               "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                               "frac": (F / (k_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS) if n_k else None},
-            "phases_ms_per_step": {k: (v / done if k != "trials" else v / done) for k, v in phase.items()},
+            "trials_per_step": trials / max(done, 1),
+            "phases_ms_per_step": phase,
         }
         if not args.no_cpu and world == 1:
             line["cpu_baseline"] = cpu_baseline(win, args.cpu_seconds)

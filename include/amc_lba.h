@@ -46,6 +46,11 @@ extern "C" {
 #define LBA_MONO       2   /* EdgeMono: 2-d, vertices (kf_b, lm) at KF time (include/G2oTypes.h:423-446, src/G2oTypes.cc:445-468) */
 #define LBA_STEREO     3   /* EdgeStereo: 3-d (include/G2oTypes.h:448-468, src/G2oTypes.cc:470-495) */
 
+/* lba_config.flags.  Timing inserts HIP events into the stream (each costs a few us of
+ * device idle time), so both are off by default. */
+#define LBA_FLAG_TIME_SWEEP   1   /* time the residual/Jacobian sweep kernel (lba_stats.ms_k_linearize) */
+#define LBA_FLAG_TIME_PHASES  2   /* also time every phase (ms_linearize .. ms_update_eval) */
+
 /* LM termination codes in lba_stats.result (OptimizationAlgorithm::SolverResult) */
 #define LBA_RESULT_OK         0
 #define LBA_RESULT_TERMINATE  1
@@ -61,7 +66,7 @@ typedef struct lba_config {
     int    max_trials;      /* _maxTrialsAfterFailure, 10 (levenberg.cpp:51) */
     int    early_stop;      /* 1: g2o stop rules active (3 iterations of <1e-3 gain, levenberg.cpp:157-166); 0: fixed count */
     int    device;          /* HIP device ordinal */
-    int    flags;           /* reserved, 0 */
+    int    flags;           /* LBA_FLAG_* bits, 0 for production use */
 } lba_config;
 
 typedef struct lba_kf {     /* VertexPoseVel / PoseVelocity (include/G2oTypes.h:59-80,104-126) */
@@ -105,12 +110,13 @@ typedef struct lba_stats {
     double  chi2_initial;   /* activeRobustChi2 before the first iteration */
     double  chi2_final;     /* activeRobustChi2 of the last computed errors (g2o semantics) */
     double  lambda_final;
-    double  ms_linearize;   /* device time per phase, summed (HIP events) */
+    double  ms_linearize;   /* device time per phase, summed (HIP events; LBA_FLAG_TIME_PHASES) */
     double  ms_schur;
     double  ms_solve;
     double  ms_update_eval;
     double  ms_total;       /* host wall time of lba_optimize */
-    double  ms_k_linearize; /* device time of the fused residual/Jacobian/J^T W J sweep kernel, summed */
+    double  ms_k_linearize; /* device time of the fused residual/Jacobian/J^T W J sweep kernel, summed
+                               (LBA_FLAG_TIME_SWEEP or LBA_FLAG_TIME_PHASES) */
     int32_t n_k_linearize;  /* launches of that kernel */
     int32_t pad;
 } lba_stats;

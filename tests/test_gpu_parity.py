@@ -6,6 +6,7 @@ g2o adds edge by edge, the kernels reduce per tile segment).  Integer outputs (i
 counts, depth flags) must be identical.
 """
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -165,3 +166,13 @@ def test_landmark_spanning_too_many_keyframes_is_reported():
     with pytest.raises(LbaError) as ei:
         Problem(win)
     assert ei.value.code == LBA_E_LIMIT
+
+
+def test_mfma_f64_layout(tmp_path):
+    """The v_mfma_f64_16x16x4 lane layout k_schur's Schur products rely on (exact integers)."""
+    import subprocess
+    src = os.path.join(os.path.dirname(__file__), "native", "mfma_f64_probe.hip")
+    exe = str(tmp_path / "mfma_probe")
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", src, "-o", exe])
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
