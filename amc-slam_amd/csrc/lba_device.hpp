@@ -128,8 +128,8 @@ struct DevProblem {
     double* gpslab;         // [n_gpslots][12] Schur rhs partials, target-sorted
     double* Hblk;           // [n_ublocks][144] reduced Hpp (upper blocks)
     double* Sblk;           // [n_ublocks][144] assembled reduced camera system (upper blocks)
-    double* Lm;             // [npad][npad] Cholesky factor, stored transposed (U = L^T, upper)
-    double* Ldinv;          // [npad] 1 / L(i, i)
+    double* Lm;             // [npad][npad] Cholesky factor (lower, row-major)
+    double* LinvT;          // [npad / CHOL_NB][CHOL_NB][CHOL_NB] inverse diagonal blocks L_bb^-T (row-major)
     double* Hpl;
     double* Hll;
     double* bl;
@@ -151,6 +151,8 @@ struct DevProblem {
     // diagnostics (LBA_PHASE_TIMING=<file>): per-workgroup clock64() stamps at phase boundaries
     unsigned long long* tdbg_lin;     // [n_tiles][16] k_linearize
     unsigned long long* tdbg_schur;   // [n_tiles][16] k_schur
+    unsigned long long* tdbg_chol;    // [npad / CHOL_NB][16] k_chol_step (workgroup 0 of each panel)
+    unsigned long long* tdbg_bs;      // [npad / CHOL_NB][16] k_chol_backsolve (per block)
 };
 
 // launchers (lba_kernels.hip)

@@ -85,12 +85,19 @@ void dump_phase_times(lba_problem* p) {
     (void)hipMemcpy(sch.data(), D.tdbg_schur, n * 8, hipMemcpyDeviceToHost);
     for (int c = 0; c < 6; ++c)
         (void)hipMemcpy(shape.data() + (size_t)c * D.n_tiles, cols[c], 4 * (size_t)D.n_tiles, hipMemcpyDeviceToHost);
+    const int nblk = D.npad / CHOL_NB + 1;
+    std::vector<unsigned long long> ch((size_t)nblk * 16), bs((size_t)nblk * 16);
+    (void)hipMemcpy(ch.data(), D.tdbg_chol, ch.size() * 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(bs.data(), D.tdbg_bs, bs.size() * 8, hipMemcpyDeviceToHost);
     if (FILE* f = std::fopen(path, "wb")) {
         const int nt = D.n_tiles;
         std::fwrite(&nt, 4, 1, f);
         std::fwrite(lin.data(), 8, n, f);
         std::fwrite(sch.data(), 8, n, f);
         std::fwrite(shape.data(), 4, shape.size(), f);
+        std::fwrite(&nblk, 4, 1, f);
+        std::fwrite(ch.data(), 8, ch.size(), f);
+        std::fwrite(bs.data(), 8, bs.size(), f);
         std::fclose(f);
     }
 }
@@ -576,6 +583,11 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         D.tdbg_schur = dalloc<unsigned long long>(p, (size_t)n_tiles * 16);
         HIPCHK(hipMemset(D.tdbg_lin, 0, (size_t)n_tiles * 16 * 8));
         HIPCHK(hipMemset(D.tdbg_schur, 0, (size_t)n_tiles * 16 * 8));
+        const int nblk = (p->np + CHOL_NB - 1) / CHOL_NB + 1;
+        D.tdbg_chol = dalloc<unsigned long long>(p, (size_t)nblk * 16);
+        D.tdbg_bs = dalloc<unsigned long long>(p, (size_t)nblk * 16);
+        HIPCHK(hipMemset(D.tdbg_chol, 0, (size_t)nblk * 16 * 8));
+        HIPCHK(hipMemset(D.tdbg_bs, 0, (size_t)nblk * 16 * 8));
     }
     D.seg_slot = dupload(p, seg_slot); D.seg_gslot = dupload(p, seg_gslot);
     D.hub_list = dupload(p, hub_list); D.n_hub = (int)hub_list.size();
@@ -602,7 +614,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     const int npad = (p->np + CHOL_NB - 1) / CHOL_NB * CHOL_NB;
     D.npad = npad;
     D.Lm = dalloc<double>(p, (size_t)npad * npad + 1);
-    D.Ldinv = dalloc<double>(p, npad + 1);
+    D.LinvT = dalloc<double>(p, (size_t)npad * CHOL_NB + 1);
     D.Hpl = dalloc<double>(p, (size_t)36 * std::max(n_pairs, 1));
     D.Hll = dalloc<double>(p, (size_t)9 * std::max(nl, 1));
     D.bl = dalloc<double>(p, (size_t)3 * std::max(nl, 1));

@@ -652,11 +652,10 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
 // [diagonal block; its tile rows; b_p^T] itself (two waves, one row per lane, pivot by readlane,
 // column broadcast through LDS), which yields L_pp, the panel rows of its tile and y_p = L_pp^-1 b_p
 // in one pass, then updates its tile, so a launch has no inter-workgroup communication.  All
-// global operands are loaded at kernel entry, before the dependent chain starts.  The factor goes to Lm transposed
-// (U = L^T, upper, row-major: what the back-substitution streams) with the
-// reciprocal diagonal in Ldinv; the running right-hand side b is forward-substituted on the fly
-// (y -> yv).  A non-positive pivot sets *info (the LDLT !isPositive failure of
-// linear_solver_dense.h:108-112).
+// global operands are loaded at kernel entry, before the dependent chain starts.  The factor goes
+// to Lm (row-major) with the inverse diagonal blocks in LinvT; the running right-hand side b is
+// forward-substituted on the fly (y -> yv).  A non-positive pivot sets *info (the LDLT
+// !isPositive failure of linear_solver_dense.h:108-112).
 constexpr int CNB = CHOL_NB;
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
@@ -685,13 +684,15 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
 }
 
 __global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restrict__ A, double* __restrict__ Lm,
-                                                   double* __restrict__ Ldinv, double* __restrict__ b,
-                                                   double* __restrict__ yv, int* info) {
+                                                   double* __restrict__ LinvT, double* __restrict__ b,
+                                                   double* __restrict__ yv, int* info, unsigned long long* tdbg) {
+    // diagnostics: stamps of workgroup 0 (entry, operands loaded, pivots done, end)
+    unsigned long long* ts = (tdbg && blockIdx.x == 0) ? tdbg + (size_t)(p / CNB) * 16 : nullptr;
+    if (ts && threadIdx.x == 0) ts[0] = clock64();
     __shared__ double Lt[CNB][CNB + 1];   // diagonal factor, transposed: Lt[c][r] = L(p + r, p + c)
     __shared__ double Pi[CNB][CNB + 1];
     __shared__ double Pj[CNB][CNB + 1];
-    __shared__ double colb[2][CNB];
-    __shared__ double dinv[CNB];
+    __shared__ double colb[3][CNB];
     __shared__ double yp[CNB];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & (CNB - 1);
     const int q = p + CNB, nt = (n - q) / CNB;
@@ -706,14 +707,27 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restr
     // ---- prefetch.  Waves 0 and 1 each hold a stacked 64 x 32 panel: lanes 0..31 the diagonal
     //      block rows, lanes 32..63 the panel rows of tile ti (wave 0) / tile tj (wave 1), or, when
     //      tj == ti, b_p^T in lane 32 of wave 1 (factorising it as one more row gives y_p = L^-1 b_p).
+    //      In workgroup 0, wave 2 stacks the identity under the diagonal block: its lanes 32 + k
+    //      end up holding row k of L_pp^-T (the back-substitution's inverse diagonal block).
+    const bool fact = wave < 2 || (wave == 2 && blockIdx.x == 0);
     double row[CNB];
-    if (wave < 2) {
-        const double* src = nullptr;
-        if (lane < CNB) src = A + (size_t)(p + lane) * n + p;
-        else if (nt > 0 && (wave == 0 || tj != ti)) src = A + (size_t)(q + (wave ? tj : ti) * CNB + l32) * n + p;
-        else if (wave == 1 && lane == CNB) src = b + p;
+    if (fact) {
+        // unconditional loads from a valid row (branch-free), then select the identity / zero rows
+        const double* src = A + (size_t)(p + l32) * n + p;
+        bool use = lane < CNB;
+        if (lane >= CNB && wave < 2 && nt > 0 && (wave == 0 || tj != ti)) {
+            src = A + (size_t)(q + (wave ? tj : ti) * CNB + l32) * n + p;
+            use = true;
+        } else if (wave == 1 && lane == CNB) {
+            src = b + p;
+            use = true;
+        }
+        const double idv = (wave == 2) ? 1.0 : 0.0;
 #pragma unroll
-        for (int c = 0; c < CNB; ++c) row[c] = src ? src[c] : 0.0;
+        for (int c = 0; c < CNB; ++c) {
+            const double v = src[c];
+            row[c] = use ? v : (c == l32 ? idv : 0.0);
+        }
     }
     const int tr = tid >> 4, tc = tid & 15;
     const size_t ra = (size_t)q + ti * CNB + 2 * tr, ca = (size_t)q + tj * CNB + 2 * tc;
@@ -722,36 +736,36 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restr
         a00 = A[ra * n + ca]; a01 = A[ra * n + ca + 1];
         a10 = A[(ra + 1) * n + ca]; a11 = A[(ra + 1) * n + ca + 1];
     }
-    // ---- right-looking panel factorisation, pivots software-pipelined: only l(j+1, j) is on the
-    //      path to the next pivot (one readlane), so the next rsq chain overlaps this pivot's
-    //      column broadcast (LDS) and rank-1 update.  Lanes < k only touch their unused upper triangle.
-    if (wave < 2) {
-        bool bad = false;
-        double myinv = 1.0;
-        double d0 = readlane_d(row[0], 0);
-        if (!(d0 > 0.0)) { bad = true; d0 = 1.0; }
-        double r = rsqrt_nr(d0);
+    if (ts) {
+        __builtin_amdgcn_s_waitcnt(0);   // operands arrived
+        __syncthreads();
+        if (threadIdx.x == 0) ts[1] = clock64();
+    }
+    // ---- right-looking panel factorisation.  The next pivot only needs lane j+1's own
+    //      d = a(j+1, j+1) - l(j+1, j)^2: every lane runs the rsq chain on its own value in VALU
+    //      and the result is read from lane j+1 (no SALU / SGPR round trip on the chain), while the
+    //      column broadcast (LDS) is in flight.  A non-positive pivot turns into NaN and is flagged
+    //      off the chain.  Lanes < k only touch their unused upper triangle.
+    if (fact) {
+        bool bad = lane == 0 && !(row[0] > 0.0);
+        double r = readlane_d(rsqrt_nr(row[0]), 0);
 #pragma unroll
         for (int j = 0; j < CNB; ++j) {
             const double lij = row[j] * r;   // lane j: sqrt(d); lanes > j: L(l, j)
             row[j] = lij;
-            if (lane == j) myinv = r;
+            if (lane < CNB) colb[wave][lane] = lij;
             double rn = 1.0;
             if (j + 1 < CNB) {
-                const double c1 = readlane_d(lij, j + 1);
-                row[j + 1] -= lij * c1;
-                pin(row[j + 1]);
-                double dn = readlane_d(row[j + 1], j + 1);
-                if (!(dn > 0.0)) { bad = true; dn = 1.0; }
-                rn = rsqrt_nr(dn);
+                const double own = row[j + 1] - lij * lij;
+                bad = bad || (lane == j + 1 && !(own > 0.0));
+                rn = readlane_d(rsqrt_nr(own), j + 1);
             }
-            if (lane < CNB) colb[wave][lane] = lij;
             wave_sync();
             double cb[CNB];
 #pragma unroll
-            for (int k = j + 2; k < CNB; ++k) cb[k] = colb[wave][k];
+            for (int k = j + 1; k < CNB; ++k) cb[k] = colb[wave][k];
 #pragma unroll
-            for (int k = j + 2; k < CNB; ++k) { row[k] -= lij * cb[k]; pin(row[k]); }
+            for (int k = j + 1; k < CNB; ++k) { row[k] -= lij * cb[k]; pin(row[k]); }
             wave_sync();
             __builtin_amdgcn_sched_barrier(0);
             r = rn;
@@ -760,34 +774,44 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restr
             if (lane < CNB) {
 #pragma unroll
                 for (int c = 0; c < CNB; ++c) Lt[c][lane] = (c <= lane) ? row[c] : 0.0;
-                dinv[lane] = myinv;
             } else if (nt > 0) {
 #pragma unroll
                 for (int c = 0; c < CNB; ++c) Pi[l32][c] = row[c];
             }
-            if (bad && lane == 0 && blockIdx.x == 0) *info = 1 + p;
-        } else if (lane >= CNB) {
-            if (nt > 0 && tj != ti) {
+            if (__ballot(bad) != 0 && lane == 0 && blockIdx.x == 0) *info = 1 + p;
+        } else if (wave == 1) {
+            if (lane >= CNB) {
+                if (nt > 0 && tj != ti) {
 #pragma unroll
-                for (int c = 0; c < CNB; ++c) Pj[l32][c] = row[c];
-            } else if (lane == CNB) {
+                    for (int c = 0; c < CNB; ++c) Pj[l32][c] = row[c];
+                } else if (lane == CNB) {
 #pragma unroll
-                for (int c = 0; c < CNB; ++c) yp[c] = row[c];
+                    for (int c = 0; c < CNB; ++c) yp[c] = row[c];
+                }
             }
+        } else if (lane >= CNB) {   // wave 2 of workgroup 0: row l32 of L_pp^-T
+            double* o = LinvT + (size_t)p * CNB + (size_t)l32 * CNB;
+#pragma unroll
+            for (int c = 0; c < CNB; ++c) o[c] = row[c];
         }
     }
     __syncthreads();
+    if (ts && threadIdx.x == 0) ts[2] = clock64();
     if (blockIdx.x == 0) {
-        for (int t = tid; t < CNB * CNB; t += 256) {   // U = L^T: U(p + c, p + i) = L(p + i, p + c)
-            const int c = t / CNB, i = t % CNB;
-            Lm[(size_t)(p + c) * n + p + i] = Lt[c][i];
+        for (int t = tid; t < CNB * CNB; t += 256) {   // diagonal block of L (row-major)
+            const int i = t / CNB, c = t % CNB;
+            Lm[(size_t)(p + i) * n + p + c] = Lt[c][i];
         }
-        if (tid < CNB) {
-            Ldinv[p + tid] = dinv[tid];
-            yv[p + tid] = yp[tid];
-        }
+        if (tid < CNB) yv[p + tid] = yp[tid];
     }
-    if (nt == 0) return;
+    if (nt == 0) {
+        if (ts) {
+            __builtin_amdgcn_s_waitcnt(0);
+            __syncthreads();
+            if (threadIdx.x == 0) ts[3] = clock64();
+        }
+        return;
+    }
     // ---- trailing tile update A(ti, tj) -= Pi Pj^T
     {
         const double (*Qj)[CNB + 1] = (ti == tj) ? Pi : Pj;
@@ -801,11 +825,11 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restr
         A[ra * n + ca] = a00 - s00; A[ra * n + ca + 1] = a01 - s01;
         A[(ra + 1) * n + ca] = a10 - s10; A[(ra + 1) * n + ca + 1] = a11 - s11;
     }
-    // ---- the tj == 0 workgroups publish the panel rows of L (stored transposed, U = L^T)
+    // ---- the tj == 0 workgroups publish the panel rows of L (row-major)
     if (tj == 0)
         for (int t = tid; t < CNB * CNB; t += 256) {
-            const int c = t / CNB, i = t % CNB;
-            Lm[(size_t)(p + c) * n + q + ti * CNB + i] = Pi[i][c];
+            const int i = t / CNB, c = t % CNB;
+            Lm[(size_t)(q + ti * CNB + i) * n + p + c] = Pi[i][c];
         }
     // ---- forward substitution of the trailing right-hand side
     if (ti == tj && tid < CNB) {
@@ -814,65 +838,80 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restr
         for (int c = 0; c < CNB; ++c) s += Pi[tid][c] * yp[c];
         b[q + ti * CNB + tid] -= s;
     }
+    if (ts) {
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        if (threadIdx.x == 0) ts[3] = clock64();
+    }
 }
 
 constexpr int CHOL_MAXN = 6144;
-constexpr int BS_GEMV = 448;                  // trailing-update threads (one prefetched column each per pass)
+constexpr int BS_GEMV = 640;                  // trailing-update threads (one prefetched column each per pass)
 constexpr int BS_THREADS = 64 + BS_GEMV;
 
-// L^T x = y with the factor stored transposed (U = L^T row-major, so every load below is one
-// row segment: base pointer + immediate offsets), one workgroup.  Wave 0 solves the 32x32 diagonal blocks from the bottom up (x_i by
-// readlane, diagonal rows of the next block prefetched one block ahead); the other waves apply
-// each solved block to the rows above (y_k -= sum_i L(r0+i, k) x_i), their column loads issued
-// before the diagonal solve so the load latency hides behind it.  x -> out.
+// L^T x = y, one workgroup, bottom block first (L row-major: a column of a block row is read
+// coalesced across the threads that own consecutive columns).  Wave 0
+// applies the block's inverse diagonal (L_bb^-T from k_chol_step: a 32-wide GEMV instead of a
+// 32-step substitution chain); the other waves apply the solved block to the rows above
+// (y_k -= sum_i L(r0+i, k) x_i), with their column loads and the next block's L^-T tile (into a
+// double-buffered LDS tile) issued before the diagonal step, so load latency hides behind it.
 __global__ __launch_bounds__(BS_THREADS) void k_chol_backsolve(const double* __restrict__ Lm,
-                                                               const double* __restrict__ Ldinv, int n,
+                                                               const double* __restrict__ LinvT, int n,
                                                                const double* __restrict__ yv,
-                                                               double* __restrict__ out) {
+                                                               double* __restrict__ out,
+                                                               unsigned long long* tdbg) {
     __shared__ double y[CHOL_MAXN];
+    __shared__ double Mb[2][CNB][CNB + 1];
     __shared__ double xb[CNB];
-    const int tid = threadIdx.x, lane = tid & 63, l32 = lane & (CNB - 1);
-    for (int t = tid; t < n; t += BS_THREADS) y[t] = yv[t];
+    const int tid = threadIdx.x, lane = tid & 63;
     const int nblk = n / CNB;
-    // pre[]: wave 0 = diagonal rows of the next block; other waves = this block's loads of column k0
-    double dg[CNB], pre[CNB];
-    double dl = 0.0, dln = 0.0;
-    if (tid < 64) {
-        const int r0 = (nblk - 1) * CNB;
-#pragma unroll
-        for (int i = 0; i < CNB; ++i) dg[i] = Lm[(size_t)(r0 + l32) * n + r0 + i];
-        dl = Ldinv[r0 + l32];
-    }
-    __syncthreads();
     const int k0 = tid - 64;
+    for (int t = tid; t < n; t += BS_THREADS) y[t] = yv[t];
+    for (int t = tid; t < CNB * CNB; t += BS_THREADS)
+        Mb[(nblk - 1) & 1][t / CNB][t % CNB] = LinvT[(size_t)(nblk - 1) * CNB * CNB + t];
+    __syncthreads();
+    if (tdbg && tid == 0) tdbg[(size_t)nblk * 16] = clock64();
+    constexpr int MPT = (CNB * CNB + BS_GEMV - 1) / BS_GEMV;   // next-tile elements per GEMV thread
     for (int blk = nblk - 1; blk >= 0; --blk) {
         const int r0 = blk * CNB;
+        if (tdbg && tid == 0) tdbg[(size_t)blk * 16] = clock64();
+        double pre[CNB];
         if (tid < 64) {
-            if (blk > 0) {
-                const int rn = r0 - CNB;
-#pragma unroll
-                for (int i = 0; i < CNB; ++i) pre[i] = Lm[(size_t)(rn + l32) * n + rn + i];
-                dln = Ldinv[rn + l32];
-            }
-            double yl = y[r0 + l32];
-#pragma unroll
-            for (int i = CNB - 1; i >= 0; --i) {
-                const double xi = readlane_d(yl * dl, i);
-                yl = (lane == i) ? xi : ((lane < i) ? yl - dg[i] * xi : yl);
-            }
             if (lane < CNB) {
-                xb[lane] = yl;
-                out[r0 + lane] = yl;
+                const double* m = Mb[blk & 1][lane];
+                double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+#pragma unroll
+                for (int i = 0; i < CNB; i += 4) {
+                    s0 += m[i] * y[r0 + i]; s1 += m[i + 1] * y[r0 + i + 1];
+                    s2 += m[i + 2] * y[r0 + i + 2]; s3 += m[i + 3] * y[r0 + i + 3];
+                }
+                const double xl = (s0 + s1) + (s2 + s3);
+                xb[lane] = xl;
+                out[r0 + lane] = xl;
             }
-#pragma unroll
-            for (int i = 0; i < CNB; ++i) dg[i] = pre[i];
-            dl = dln;
+            if (tdbg && tid == 0) tdbg[(size_t)blk * 16 + 1] = clock64();   // diagonal block done
         } else {
-            if (k0 < r0)
+            if (k0 < r0) {   // column k0 of the block's rows of L: coalesced across the threads
+                const double* col = Lm + (size_t)r0 * n + k0;
 #pragma unroll
-                for (int i = 0; i < CNB; ++i) pre[i] = Lm[(size_t)k0 * n + r0 + i];
+                for (int i = 0; i < CNB; ++i) pre[i] = col[(size_t)i * n];
+            }
+            if (blk > 0) {   // next block's inverse diagonal tile -> the other LDS buffer
+                double mv[MPT];
+#pragma unroll
+                for (int u = 0; u < MPT; ++u) {
+                    const int t = k0 + u * BS_GEMV;
+                    mv[u] = LinvT[(size_t)(blk - 1) * CNB * CNB + (t < CNB * CNB ? t : 0)];
+                }
+#pragma unroll
+                for (int u = 0; u < MPT; ++u) {
+                    const int t = k0 + u * BS_GEMV;
+                    if (t < CNB * CNB) Mb[(blk - 1) & 1][t / CNB][t % CNB] = mv[u];
+                }
+            }
         }
         __syncthreads();
+        if (tdbg && tid == 0) tdbg[(size_t)blk * 16 + 2] = clock64();   // block x published
         if (tid >= 64) {
             if (k0 < r0) {
                 double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
@@ -887,8 +926,8 @@ __global__ __launch_bounds__(BS_THREADS) void k_chol_backsolve(const double* __r
                 double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
 #pragma unroll
                 for (int i = 0; i < CNB; i += 4) {
-                    const double* u = Lm + (size_t)k * n + r0 + i;
-                    s0 += u[0] * xb[i]; s1 += u[1] * xb[i + 1]; s2 += u[2] * xb[i + 2]; s3 += u[3] * xb[i + 3];
+                    const double* u = Lm + (size_t)(r0 + i) * n + k;
+                    s0 += u[0] * xb[i]; s1 += u[n] * xb[i + 1]; s2 += u[2 * n] * xb[i + 2]; s3 += u[3 * n] * xb[i + 3];
                 }
                 y[k] -= (s0 + s1) + (s2 + s3);
             }
@@ -1084,10 +1123,10 @@ void launch_cholesky_solve(const DevProblem& P, hipStream_t s) {
     if (n == 0) return;
     for (int p = 0; p < n; p += CHOL_NB) {
         const int nt = (n - p - CHOL_NB) / CHOL_NB;
-        hipLaunchKernelGGL(k_chol_step, dim3(nt ? nt * (nt + 1) / 2 : 1), dim3(256), 0, s, n, p, P.S, P.Lm, P.Ldinv,
-                           P.xsol, P.yv, P.info);
+        hipLaunchKernelGGL(k_chol_step, dim3(nt ? nt * (nt + 1) / 2 : 1), dim3(256), 0, s, n, p, P.S, P.Lm, P.LinvT,
+                           P.xsol, P.yv, P.info, P.tdbg_chol);
     }
-    hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(BS_THREADS), 0, s, P.Lm, P.Ldinv, n, P.yv, P.xsol);
+    hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(BS_THREADS), 0, s, P.Lm, P.LinvT, n, P.yv, P.xsol, P.tdbg_bs);
 }
 void launch_update(const DevProblem& P, double lambda, const double* kst, const double* lst, double* kst_out,
                    double* lst_out, hipStream_t s) {

@@ -29,7 +29,15 @@ def load(path):
     sch = np.frombuffer(raw[off:off + nt * 16 * 8], np.uint64).reshape(nt, 16).astype(np.int64)
     off += nt * 16 * 8
     shape = np.frombuffer(raw[off:off + 6 * nt * 4], np.int32).reshape(6, nt)
-    return nt, lin, sch, shape
+    off += 6 * nt * 4
+    chol = bs = None
+    if len(raw) > off:
+        nb = int(np.frombuffer(raw[off:off + 4], np.int32)[0])
+        off += 4
+        chol = np.frombuffer(raw[off:off + nb * 16 * 8], np.uint64).reshape(nb, 16).astype(np.int64)
+        off += nb * 16 * 8
+        bs = np.frombuffer(raw[off:off + nb * 16 * 8], np.uint64).reshape(nb, 16).astype(np.int64)
+    return nt, lin, sch, shape, chol, bs
 
 
 def report(name, stamps, phases, shape, out):
@@ -59,10 +67,23 @@ def main():
     p = Problem(win, early_stop=0)
     p.optimize(args.iters)
     p.close()
-    nt, lin, sch, shape = load(args.dump)
+    nt, lin, sch, shape, chol, bs = load(args.dump)
     out = [f"config {args.config}: {nt} tiles"]
     report("k_linearize", lin, LIN_PHASES, shape, out)
     report("k_schur", sch, SCHUR_PHASES, shape, out)
+    if chol is not None:
+        npan = int((chol[:, 0] != 0).sum())
+        c = chol[:npan]
+        out.append(f"== k_chol_step (workgroup 0 of each of {npan} panels), cycles: load / pivots / update+store")
+        for i in range(npan):
+            out.append(f"   panel {i:3d}: {c[i, 1] - c[i, 0]:7d} {c[i, 2] - c[i, 1]:7d} {c[i, 3] - c[i, 2]:7d}")
+        nb = npan
+        b = bs[:nb + 1]
+        out.append(f"== k_chol_backsolve, cycles per block: diagonal solve / barrier wait / trailing GEMV")
+        for blk in range(nb - 1, -1, -1):
+            end = b[blk - 1, 0] if blk > 0 else 0
+            gemv = (end - b[blk, 2]) if blk > 0 else 0
+            out.append(f"   block {blk:3d}: {b[blk, 1] - b[blk, 0]:7d} {b[blk, 2] - b[blk, 1]:7d} {gemv:7d}")
     text = "\n".join(out)
     print(text)
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
