@@ -129,6 +129,7 @@ struct DevProblem {
     double* Hblk;           // [n_ublocks][144] reduced Hpp (upper blocks)
     double* Sblk;           // [n_ublocks][144] assembled reduced camera system (upper blocks)
     double* Lm;             // [npad][npad] Cholesky factor (lower, row-major)
+    const int* pfirst;      // [npad / CHOL_NB] first panel each panel of rows of S / L has non-zeros in
     double* LinvT;          // [npad / CHOL_NB][CHOL_NB][CHOL_NB] inverse diagonal blocks L_bb^-T (row-major)
     double* Hpl;
     double* Hll;

@@ -612,6 +612,21 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     HIPCHK(hipMemset(D.Hblk, 0, sizeof(double) * 144 * (size_t)std::max(n_ublocks, 1)));   // blocks without sources
     D.Sblk = dalloc<double>(p, (size_t)144 * std::max(n_ublocks, 1));
     const int npad = (p->np + CHOL_NB - 1) / CHOL_NB * CHOL_NB;
+    // envelope of S (and so of its Cholesky factor, whose fill stays inside it): per CHOL_NB panel
+    // of rows, the first panel any of its rows has a structural non-zero in
+    {
+        std::vector<int> fk(n_pb);
+        for (int b = 0; b < n_pb; ++b) fk[b] = b;   // diagonal (damping)
+        for (int u = 0; u < n_ublocks; ++u)
+            if (hcnt[u] > 0 || scnt[u] > 0) fk[ub_j[u]] = std::min(fk[ub_j[u]], ub_i[u]);
+        std::vector<int> pfirst(npad / CHOL_NB);
+        for (int P = 0; P < npad / CHOL_NB; ++P) {
+            int f = P;
+            for (int r = P * CHOL_NB; r < (P + 1) * CHOL_NB && r < p->np; ++r) f = std::min(f, 12 * fk[r / 12] / CHOL_NB);
+            pfirst[P] = f;
+        }
+        D.pfirst = dupload(p, pfirst);
+    }
     D.npad = npad;
     D.Lm = dalloc<double>(p, (size_t)npad * npad + 1);
     D.LinvT = dalloc<double>(p, (size_t)npad * CHOL_NB + 1);

@@ -19,6 +19,8 @@
 //   k_eval           residuals / robust chi2 of the trial state           (sparse_optimizer.cpp:61-114)
 // All cross-workgroup sums are written as per-workgroup partials and reduced in a fixed order, so
 // results are bitwise reproducible run to run (no floating-point atomics).
+#include <utility>
+
 #include "lba_device.hpp"
 #include "lba_math.hpp"
 #include "../../include/amc_lba.h"
@@ -649,8 +651,8 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
 // to a multiple of CNB with an identity tail (set once at upload; the factorisation never changes
 // it), so every panel is exactly CNB wide and all loops below are compile-time.
 // Every workgroup owns one lower tile of the trailing matrix; it factors the stacked panel
-// [diagonal block; its tile rows; b_p^T] itself (two waves, one row per lane, pivot by readlane,
-// column broadcast through LDS), which yields L_pp, the panel rows of its tile and y_p = L_pp^-1 b_p
+// [diagonal block; its tile rows; b_p^T] itself (two waves, one row per lane, pivots and column
+// broadcast by readlane), which yields L_pp, the panel rows of its tile and y_p = L_pp^-1 b_p
 // in one pass, then updates its tile, so a launch has no inter-workgroup communication.  All
 // global operands are loaded at kernel entry, before the dependent chain starts.  The factor goes
 // to Lm (row-major) with the inverse diagonal blocks in LinvT; the running right-hand side b is
@@ -683,16 +685,78 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
     return r;
 }
 
+// Panel pivot sequence, generated at compile time (pivot J, update step T, chain op OP) so every
+// row[] index is a constant.  Pivot J: l = row[J] r; column J by readlane; then the rank-1
+// update row[k] -= l cb[k] (k > J), with the next pivot's chain spread through it in source order
+// (the pins keep that order): d = row[J+1] - l^2 on lane J+1, rsq, two Newton steps
+// r <- r (1.5 - 0.5 d r^2), readlane of r from lane J+1 (op s after update step floor(s NF / 7)).
+struct Pivot {
+    double lij, hh, c, m, u, rn;
+};
+
+template <int J, int T, int OP>
+__device__ __forceinline__ void piv_chain(Pivot& x) {
+    constexpr int NF = CNB - 1 - J;
+    if constexpr (OP < 7) {
+        if constexpr ((OP * NF) / 7 == T) {
+            if constexpr (OP == 0 || OP == 3) { x.m = x.hh * x.c; pin(x.m); }
+            else if constexpr (OP == 1 || OP == 4) { x.u = fma(-x.c, x.m, 1.5); pin(x.u); }
+            else if constexpr (OP == 2 || OP == 5) { x.c = x.c * x.u; pin(x.c); }
+            else { x.rn = readlane_d(x.c, J + 1); pin(x.rn); }
+        }
+        piv_chain<J, T, OP + 1>(x);
+    }
+}
+
+template <int J, int... T>
+__device__ __forceinline__ void piv_update(double (&row)[CNB], const double (&cb)[CNB], Pivot& x,
+                                           std::integer_sequence<int, T...>) {
+    constexpr int NF = CNB - 1 - J;
+    auto step = [&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        if constexpr (t < NF) {
+            row[J + 1 + t] -= x.lij * cb[J + 1 + t];
+            pin(row[J + 1 + t]);
+        }
+        if constexpr (J + 1 < CNB) piv_chain<J, t, 0>(x);
+    };
+    (step(std::integral_constant<int, T>{}), ...);
+}
+
+template <int J>
+__device__ __forceinline__ void piv_seq(double (&row)[CNB], double r, int lane, bool& bad) {
+    if constexpr (J < CNB) {
+        Pivot x;
+        x.lij = row[J] * r;   // lane J: sqrt(d); lanes > J: L(l, J)
+        row[J] = x.lij;
+        x.hh = 0.5; x.c = 1.0; x.m = 0.0; x.u = 0.0; x.rn = 1.0;
+        if constexpr (J + 1 < CNB) {
+            const double own = row[J + 1] - x.lij * x.lij;
+            bad = bad || (lane == J + 1 && !(own > 0.0));
+            x.c = __builtin_amdgcn_rsq(own);
+            x.hh = 0.5 * own;
+        }
+        // column J of L_pp by readlane into SGPRs (an LDS broadcast costs (31 - J) doubles per lane
+        // of every factoring wave on the CU's shared LDS return path: no faster, measured)
+        double cb[CNB];
+#pragma unroll
+        for (int k = J + 1; k < CNB; ++k) cb[k] = readlane_d(x.lij, k);
+        constexpr int NT = (CNB - 1 - J) > 0 ? (CNB - 1 - J) : 1;
+        piv_update<J>(row, cb, x, std::make_integer_sequence<int, NT>{});
+        piv_seq<J + 1>(row, x.rn, lane, bad);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restrict__ A, double* __restrict__ Lm,
                                                    double* __restrict__ LinvT, double* __restrict__ b,
-                                                   double* __restrict__ yv, int* info, unsigned long long* tdbg) {
+                                                   double* __restrict__ yv, int* info, const int* __restrict__ pfirst,
+                                                   unsigned long long* tdbg) {
     // diagnostics: stamps of workgroup 0 (entry, operands loaded, pivots done, end)
     unsigned long long* ts = (tdbg && blockIdx.x == 0) ? tdbg + (size_t)(p / CNB) * 16 : nullptr;
     if (ts && threadIdx.x == 0) ts[0] = clock64();
     __shared__ double Lt[CNB][CNB + 1];   // diagonal factor, transposed: Lt[c][r] = L(p + r, p + c)
     __shared__ double Pi[CNB][CNB + 1];
     __shared__ double Pj[CNB][CNB + 1];
-    __shared__ double colb[3][CNB];
     __shared__ double yp[CNB];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & (CNB - 1);
     const int q = p + CNB, nt = (n - q) / CNB;
@@ -703,6 +767,10 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restr
         while ((ti + 1) * (ti + 2) / 2 <= bid) ++ti;
         while (ti * (ti + 1) / 2 > bid) --ti;
         tj = bid - ti * (ti + 1) / 2;
+        // outside the envelope the panel rows of tile ti or tj are structurally zero: nothing to
+        // update (workgroup 0 always runs: it publishes the diagonal block)
+        const int pc = p / CNB, Pq = q / CNB;
+        if (blockIdx.x != 0 && (pfirst[Pq + ti] > pc || pfirst[Pq + tj] > pc)) return;
     }
     // ---- prefetch.  Waves 0 and 1 each hold a stacked 64 x 32 panel: lanes 0..31 the diagonal
     //      block rows, lanes 32..63 the panel rows of tile ti (wave 0) / tile tj (wave 1), or, when
@@ -741,35 +809,14 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restr
         __syncthreads();
         if (threadIdx.x == 0) ts[1] = clock64();
     }
-    // ---- right-looking panel factorisation.  The next pivot only needs lane j+1's own
-    //      d = a(j+1, j+1) - l(j+1, j)^2: every lane runs the rsq chain on its own value in VALU
-    //      and the result is read from lane j+1 (no SALU / SGPR round trip on the chain), while the
-    //      column broadcast (LDS) is in flight.  A non-positive pivot turns into NaN and is flagged
-    //      off the chain.  Lanes < k only touch their unused upper triangle.
+    // ---- right-looking panel factorisation (piv_seq).  The next pivot only needs lane j+1's own
+    //      d = a(j+1, j+1) - l(j+1, j)^2: every lane runs the rsq chain on its own value in VALU and
+    //      the result is read from lane j+1, interleaved with this pivot's rank-1 update.  A
+    //      non-positive pivot turns into NaN and is flagged off the chain.  Lanes < k only touch
+    //      their unused upper triangle.
     if (fact) {
         bool bad = lane == 0 && !(row[0] > 0.0);
-        double r = readlane_d(rsqrt_nr(row[0]), 0);
-#pragma unroll
-        for (int j = 0; j < CNB; ++j) {
-            const double lij = row[j] * r;   // lane j: sqrt(d); lanes > j: L(l, j)
-            row[j] = lij;
-            if (lane < CNB) colb[wave][lane] = lij;
-            double rn = 1.0;
-            if (j + 1 < CNB) {
-                const double own = row[j + 1] - lij * lij;
-                bad = bad || (lane == j + 1 && !(own > 0.0));
-                rn = readlane_d(rsqrt_nr(own), j + 1);
-            }
-            wave_sync();
-            double cb[CNB];
-#pragma unroll
-            for (int k = j + 1; k < CNB; ++k) cb[k] = colb[wave][k];
-#pragma unroll
-            for (int k = j + 1; k < CNB; ++k) { row[k] -= lij * cb[k]; pin(row[k]); }
-            wave_sync();
-            __builtin_amdgcn_sched_barrier(0);
-            r = rn;
-        }
+        piv_seq<0>(row, readlane_d(rsqrt_nr(row[0]), 0), lane, bad);
         if (wave == 0) {
             if (lane < CNB) {
 #pragma unroll
@@ -859,6 +906,7 @@ __global__ __launch_bounds__(BS_THREADS) void k_chol_backsolve(const double* __r
                                                                const double* __restrict__ LinvT, int n,
                                                                const double* __restrict__ yv,
                                                                double* __restrict__ out,
+                                                               const int* __restrict__ pfirst,
                                                                unsigned long long* tdbg) {
     __shared__ double y[CHOL_MAXN];
     __shared__ double Mb[2][CNB][CNB + 1];
@@ -874,6 +922,7 @@ __global__ __launch_bounds__(BS_THREADS) void k_chol_backsolve(const double* __r
     constexpr int MPT = (CNB * CNB + BS_GEMV - 1) / BS_GEMV;   // next-tile elements per GEMV thread
     for (int blk = nblk - 1; blk >= 0; --blk) {
         const int r0 = blk * CNB;
+        const int c0 = pfirst[blk] * CNB;   // the block's rows of L are zero left of its envelope
         if (tdbg && tid == 0) tdbg[(size_t)blk * 16] = clock64();
         double pre[CNB];
         if (tid < 64) {
@@ -891,8 +940,8 @@ __global__ __launch_bounds__(BS_THREADS) void k_chol_backsolve(const double* __r
             }
             if (tdbg && tid == 0) tdbg[(size_t)blk * 16 + 1] = clock64();   // diagonal block done
         } else {
-            if (k0 < r0) {   // column k0 of the block's rows of L: coalesced across the threads
-                const double* col = Lm + (size_t)r0 * n + k0;
+            if (k0 + c0 < r0) {   // column c0 + k0 of the block's rows of L: coalesced across the threads
+                const double* col = Lm + (size_t)r0 * n + c0 + k0;
 #pragma unroll
                 for (int i = 0; i < CNB; ++i) pre[i] = col[(size_t)i * n];
             }
@@ -913,16 +962,16 @@ __global__ __launch_bounds__(BS_THREADS) void k_chol_backsolve(const double* __r
         __syncthreads();
         if (tdbg && tid == 0) tdbg[(size_t)blk * 16 + 2] = clock64();   // block x published
         if (tid >= 64) {
-            if (k0 < r0) {
+            if (k0 + c0 < r0) {
                 double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
 #pragma unroll
                 for (int i = 0; i < CNB; i += 4) {
                     s0 += pre[i] * xb[i]; s1 += pre[i + 1] * xb[i + 1];
                     s2 += pre[i + 2] * xb[i + 2]; s3 += pre[i + 3] * xb[i + 3];
                 }
-                y[k0] -= (s0 + s1) + (s2 + s3);
+                y[c0 + k0] -= (s0 + s1) + (s2 + s3);
             }
-            for (int k = k0 + BS_GEMV; k < r0; k += BS_GEMV) {
+            for (int k = c0 + k0 + BS_GEMV; k < r0; k += BS_GEMV) {
                 double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
 #pragma unroll
                 for (int i = 0; i < CNB; i += 4) {
@@ -1124,9 +1173,10 @@ void launch_cholesky_solve(const DevProblem& P, hipStream_t s) {
     for (int p = 0; p < n; p += CHOL_NB) {
         const int nt = (n - p - CHOL_NB) / CHOL_NB;
         hipLaunchKernelGGL(k_chol_step, dim3(nt ? nt * (nt + 1) / 2 : 1), dim3(256), 0, s, n, p, P.S, P.Lm, P.LinvT,
-                           P.xsol, P.yv, P.info, P.tdbg_chol);
+                           P.xsol, P.yv, P.info, P.pfirst, P.tdbg_chol);
     }
-    hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(BS_THREADS), 0, s, P.Lm, P.LinvT, n, P.yv, P.xsol, P.tdbg_bs);
+    hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(BS_THREADS), 0, s, P.Lm, P.LinvT, n, P.yv, P.xsol, P.pfirst,
+                       P.tdbg_bs);
 }
 void launch_update(const DevProblem& P, double lambda, const double* kst, const double* lst, double* kst_out,
                    double* lst_out, hipStream_t s) {
