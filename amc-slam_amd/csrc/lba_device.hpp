@@ -40,7 +40,9 @@ constexpr int SEG_MAX_ROWS = 48;    // longer (a, b) runs are split so the segme
 constexpr int TILE_PROWS = 2 * TILE_ROWS;   // pair row-list entries per tile (each row feeds <= 2 pairs)
 constexpr int TILE_SLIST = 1024;    // Schur (pair, pair, landmark) triples per tile (k_schur stages them)
 constexpr int TILE_SENT = TILE_KF * (TILE_KF + 1) / 2;   // KF-pair Schur entries per tile
-constexpr int SEGM_STRIDE = 8;      // staged segment record: row0 nrows aa ab bb ab_transposed ga gb
+constexpr int TILE_TGT = 64;        // Hpp target blocks per tile (k_linearize stages their records)
+constexpr int TILE_RUNS = 3 * TILE_SEGS;   // row runs of a tile's targets
+constexpr int TGT_STRIDE = 4;       // staged target record: flags | nrun << 8, hslot, gslot, first run
 
 constexpr int CHOL_NB = 32;         // Cholesky panel / tile width
 constexpr int RED_GROUPS = 4;       // reduction kernels: 4 groups x 144 threads
@@ -80,7 +82,12 @@ struct DevProblem {
     const int* tile_kf0;
     const int* tile_nkf;
     const int* tkf_list;    // tile KF unions (pose block indices)
-    const int* seg_meta;    // per tile segment: SEGM_STRIDE ints (row0 nrows aa ab bb ab_tr ga gb)
+    const int* tgt_meta;    // per tile Hpp target: TGT_STRIDE ints (see lba_host.hip)
+    const int* tile_tgt0;   // per tile: first target / count
+    const int* tile_ntgt;
+    const int* tile_run0;   // per tile: first run
+    const int* run_rows;    // per run: row0 | nrows << 16 (tile-local rows)
+    const int* run_offs;    // per run: column offsets offA | offB << 8 in the LDS Jacobian row
     const int* seg_a;       // per segment entry: pose block of side a / b (-1 = none)
     const int* seg_b;
     const int* seg_row0;    // tile-local first row
@@ -99,7 +106,7 @@ struct DevProblem {
     const int* lm_pair0;    // [n_lm + 1] landmark -> pairs
     // partial-sum slabs are sorted by their reduction target, so every reduction below reads
     // one contiguous range (coalesced) instead of chasing a source list
-    const int* seg_slot;    // per slab entry (segments, priors, velocity edges): 5 ints
+    const int* seg_slot;    // per slab entry (motion priors, velocity edges): 5 ints
                             //   aa, ab, bb slot in hslab (-1 = none), ab transposed flag, -
     const int* seg_gslot;   // per slab entry: ga, gb slot in gslab (-1 = none)
     const int* hub_list;    // upper blocks that receive Hpp sources

@@ -448,14 +448,37 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         }
     }
     const int n_tiles = (int)t_obs0.size();
-    const int n_segs = (int)seg_a.size();
     const int n_sent = (int)sent_l1.size();
 
     // ---- partial-sum slots, sorted by reduction target (tile segments, priors, velocity edges)
-    std::vector<int> ent_a(seg_a), ent_b(seg_b);
-    for (auto& e : pri) { ent_a.push_back(H[e.kf_a]); ent_b.push_back(H[e.kf_b]); }
-    for (int k : vel) { ent_a.push_back(-1); ent_b.push_back(H[k]); }
-    const int n_entries = (int)ent_a.size();
+    // per-tile Hpp targets: every tile writes one partial per distinct target block.  A diagonal
+    // target (k, k) (+ b_k) sums the a-side rows (columns 0..11) and b-side rows (12..23) of all the
+    // tile's segments touching k; an off-diagonal target sums Ja^T W Jb over its (a, b) segments.
+    // Runs: row0 | nrows << 16, column offsets offA | offB << 8.
+    std::vector<int> tg_k1, tg_k2, tg_diag, t_tgt0, t_ntgt, tg_run0, tg_nrun, run_rows, run_offs;
+    for (int t = 0; t < n_tiles; ++t) {
+        std::map<int, std::vector<std::pair<int, int>>> dg;
+        std::map<std::pair<int, int>, std::vector<std::pair<int, int>>> od;
+        for (int sg = t_seg0[t]; sg < t_seg0[t] + t_nseg[t]; ++sg) {
+            const int a = seg_a[sg], b = seg_b[sg], rr = seg_row0[sg] | (seg_nrows[sg] << 16);
+            if (a >= 0) dg[a].emplace_back(rr, 0);
+            if (b >= 0) dg[b].emplace_back(rr, 12 | (12 << 8));
+            if (a >= 0 && b >= 0) od[std::make_pair(a, b)].emplace_back(rr, 0 | (12 << 8));
+        }
+        t_tgt0.push_back((int)tg_k1.size());
+        auto add = [&](int k1, int k2, bool diag, const std::vector<std::pair<int, int>>& runs) {
+            tg_k1.push_back(k1); tg_k2.push_back(k2); tg_diag.push_back(diag);
+            tg_run0.push_back((int)run_rows.size()); tg_nrun.push_back((int)runs.size());
+            for (auto& r : runs) { run_rows.push_back(r.first); run_offs.push_back(r.second); }
+        };
+        for (auto& kv : dg) add(kv.first, kv.first, true, kv.second);
+        for (auto& kv : od) add(kv.first.first, kv.first.second, false, kv.second);
+        t_ntgt.push_back((int)tg_k1.size() - t_tgt0.back());
+        if (t_ntgt.back() > TILE_TGT || (int)run_rows.size() - tg_run0[t_tgt0.back()] > TILE_RUNS)
+            throw ApiError{LBA_E_LIMIT, "internal: tile target / run count exceeds its limit"};
+    }
+    const int n_tgt = (int)tg_k1.size();
+    // slab entries: tile targets, then motion priors, then velocity edges
     const int n_ublocks = n_pb * (n_pb + 1) / 2;
     std::vector<int> ub_i(n_ublocks), ub_j(n_ublocks);
     for (int bi = 0; bi < n_pb; ++bi)
@@ -463,7 +486,15 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             const int id = ublock_id(n_pb, bi, bj);
             ub_i[id] = bi; ub_j[id] = bj;
         }
+    std::vector<int> ent_a, ent_b;
+    for (auto& e : pri) { ent_a.push_back(H[e.kf_a]); ent_b.push_back(H[e.kf_b]); }
+    for (int k : vel) { ent_a.push_back(-1); ent_b.push_back(H[k]); }
+    const int n_entries = (int)ent_a.size();
     std::vector<int> hcnt(n_ublocks + 1, 0), gcnt(n_pb + 1, 0);
+    for (int g = 0; g < n_tgt; ++g) {
+        hcnt[ublock_id(n_pb, std::min(tg_k1[g], tg_k2[g]), std::max(tg_k1[g], tg_k2[g]))]++;
+        if (tg_diag[g]) gcnt[tg_k1[g]]++;
+    }
     for (int en = 0; en < n_entries; ++en) {
         const int a = ent_a[en], b = ent_b[en];
         if (a >= 0) { hcnt[ublock_id(n_pb, a, a)]++; gcnt[a]++; }
@@ -477,6 +508,20 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     };
     std::vector<int> hs0 = prefix(hcnt), gs0 = prefix(gcnt);
     std::vector<int> hfill(hs0), gfill(gs0);
+    // target records (staged by k_linearize): flags (1 diagonal, 2 stored transposed, nrun << 8),
+    // hslab slot, gslab slot, tile-local first run
+    std::vector<int> tgt_meta(TGT_STRIDE * (size_t)std::max(n_tgt, 1), -1);
+    for (int t = 0; t < n_tiles; ++t)
+        for (int g = t_tgt0[t]; g < t_tgt0[t] + t_ntgt[t]; ++g) {
+            const int k1 = tg_k1[g], k2 = tg_k2[g];
+            int* m = tgt_meta.data() + TGT_STRIDE * (size_t)g;
+            m[0] = (tg_diag[g] ? 1 : 0) | (k1 > k2 ? 2 : 0) | (tg_nrun[g] << 8);
+            m[1] = hfill[ublock_id(n_pb, std::min(k1, k2), std::max(k1, k2))]++;
+            m[2] = tg_diag[g] ? gfill[k1]++ : -1;
+            m[3] = tg_run0[g] - tg_run0[t_tgt0[t]];
+        }
+    std::vector<int> tile_run0(n_tiles);
+    for (int t = 0; t < n_tiles; ++t) tile_run0[t] = t_ntgt[t] ? tg_run0[t_tgt0[t]] : 0;
     std::vector<int> seg_slot(5 * (size_t)std::max(n_entries, 1), -1), seg_gslot(2 * (size_t)std::max(n_entries, 1), -1);
     for (int en = 0; en < n_entries; ++en) {
         const int a = ent_a[en], b = ent_b[en];
@@ -485,13 +530,6 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         if (a >= 0) { sl[0] = hfill[ublock_id(n_pb, a, a)]++; seg_gslot[2 * (size_t)en] = gfill[a]++; }
         if (a >= 0 && b >= 0) { sl[1] = hfill[ublock_id(n_pb, std::min(a, b), std::max(a, b))]++; sl[3] = a > b; }
         if (b >= 0) { sl[2] = hfill[ublock_id(n_pb, b, b)]++; seg_gslot[2 * (size_t)en + 1] = gfill[b]++; }
-    }
-    std::vector<int> seg_meta(SEGM_STRIDE * (size_t)std::max(n_segs, 1), -1);   // staged by k_linearize
-    for (int sg = 0; sg < n_segs; ++sg) {
-        int* m = seg_meta.data() + SEGM_STRIDE * (size_t)sg;
-        m[0] = seg_row0[sg]; m[1] = seg_nrows[sg];
-        for (int f = 0; f < 4; ++f) m[2 + f] = seg_slot[5 * (size_t)sg + f];
-        m[6] = seg_gslot[2 * (size_t)sg]; m[7] = seg_gslot[2 * (size_t)sg + 1];
     }
     std::vector<int> hub_list;
     for (int u = 0; u < n_ublocks; ++u)
@@ -570,7 +608,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.tile_seg0 = dupload(p, t_seg0); D.tile_nseg = dupload(p, t_nseg); D.tile_sent0 = dupload(p, t_sent0);
     D.tile_nsent = dupload(p, t_nsent); D.tile_kf0 = dupload(p, t_kf0); D.tile_nkf = dupload(p, t_nkf);
     D.tkf_list = dupload(p, tkf_list);
-    D.seg_meta = dupload(p, seg_meta);
+    D.tgt_meta = dupload(p, tgt_meta); D.tile_tgt0 = dupload(p, t_tgt0); D.tile_ntgt = dupload(p, t_ntgt);
+    D.tile_run0 = dupload(p, tile_run0); D.run_rows = dupload(p, run_rows); D.run_offs = dupload(p, run_offs);
     D.sent_r0 = dupload(p, sent_r0); D.sent_list = dupload(p, sent_list);
     D.seg_a = dupload(p, seg_a); D.seg_b = dupload(p, seg_b); D.seg_row0 = dupload(p, seg_row0);
     D.seg_nrows = dupload(p, seg_nrows); D.sent_l1 = dupload(p, sent_l1); D.sent_l2 = dupload(p, sent_l2);
@@ -595,7 +634,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.sslot = dupload(p, sslot); D.ss0 = dupload(p, ss0); D.tkf_gslot = dupload(p, tkf_gslot);
     D.gps0 = dupload(p, gps0);
     D.pri_a = dupload(p, pri_a); D.pri_b = dupload(p, pri_b); D.vel_kf = dupload(p, vel);
-    D.pri_entry0 = n_segs;
+    D.pri_entry0 = 0;
     double qcinv[36];
     if (!inverse6(p->cfg.qc, qcinv)) throw ApiError{LBA_E_ARG, "Qc is singular"};
     for (int i = 0; i < 36; ++i) D.qcinv[i] = qcinv[i];

@@ -188,81 +188,73 @@ __global__ __launch_bounds__(PREP_THREADS) void k_gp_prep(DevProblem P, const do
     }
 }
 
-// upper-triangle 4x4 output blocks (bi <= bj) of the 25-column row [Ja Jb e]: bi <= 5, bi <= bj <= 6,
-// enumerated row by row (7, 6, 5, 4, 3, 2 blocks)
-__device__ __forceinline__ void seg_block(int blk, int* bi, int* bj) {
-    const int i = (blk >= 7) + (blk >= 13) + (blk >= 18) + (blk >= 22) + (blk >= 25);
-    *bi = i;
-    *bj = i + blk - (7 * i - i * (i - 1) / 2);
-}
-
-// one (segment, 4x4 block) task: acc = sum over the segment's rows of (s r)[4bi..] r[4bj..]^T, written
-// to the segment's Hpp / b_p slab slots (upper block + mirror; b = -J^T rho' Omega e).  Rows are
-// consumed four at a time so their LDS reads are all in flight before the FMAs.
-__device__ __forceinline__ void seg_task(const DevProblem& P, const double* rows, const double* rw, const int* sm,
-                                         int bi, int bj) {
-    const int r0 = sm[0], rend = sm[0] + sm[1];
+// One (Hpp target, 4x4 sub-block) task of a tile: acc = sum over the target's row runs of
+// (s r)[offA + 4 ia ..] r[offB + 4 jb ..]^T (jb = -1: the e column, for b_k), written to the target's
+// slab slot (diagonal targets: upper sub-blocks + mirror; off-diagonal: the Ja^T W Jb block, stored
+// transposed when the block's upper position is (b, a)).  Rows are consumed four at a time so their
+// LDS reads are all in flight before the FMAs.
+__device__ __forceinline__ void tgt_task(const DevProblem& P, const double* rows, const double* rw, const int* tm,
+                                         const int* rr, const int* ro, int ia, int jb) {
+    const int nrun = tm[0] >> 8, run0 = tm[3];
     double acc[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[q] = 0.0;
-    int r = r0;
-    for (; r + 4 <= rend; r += 4) {
-        double a[4][4], c[4][4];
+    for (int u = run0; u < run0 + nrun; ++u) {
+        const int r0 = rr[u] & 0xffff, rend = r0 + (rr[u] >> 16);
+        const int ca = (ro[u] & 0xff) + 4 * ia, cb = jb < 0 ? 24 : (ro[u] >> 8) + 4 * jb;
+        int r = r0;
+        for (; r + 4 <= rend; r += 4) {
+            double a[4][4], c[4][4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const double* Rr = rows + (r + u) * ROW_STRIDE;
-            const double s = rw[r + u];
+            for (int v = 0; v < 4; ++v) {
+                const double* Rr = rows + (r + v) * ROW_STRIDE;
+                const double s = rw[r + v];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) { a[u][k] = s * Rr[4 * bi + k]; c[u][k] = Rr[4 * bj + k]; }
+                for (int k = 0; k < 4; ++k) { a[v][k] = s * Rr[ca + k]; c[v][k] = Rr[cb + k]; }
+            }
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int l = 0; l < 4; ++l) acc[k * 4 + l] += a[v][k] * c[v][l];
         }
+        for (; r < rend; ++r) {
+            const double* Rr = rows + r * ROW_STRIDE;
+            const double s = rw[r];
+            double a[4], c[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+            for (int k = 0; k < 4; ++k) { a[k] = s * Rr[ca + k]; c[k] = Rr[cb + k]; }
 #pragma unroll
             for (int k = 0; k < 4; ++k)
 #pragma unroll
-                for (int l = 0; l < 4; ++l) acc[k * 4 + l] += a[u][k] * c[u][l];
+                for (int l = 0; l < 4; ++l) acc[k * 4 + l] += a[k] * c[l];
+        }
     }
-    for (; r < rend; ++r) {
-        const double* Rr = rows + r * ROW_STRIDE;
-        const double s = rw[r];
-        double a[4], c[4];
+    if (jb < 0) {   // b_k = -J_k^T rho' Omega e
+        double* g = P.gslab + (size_t)tm[2] * 12 + 4 * ia;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) { a[k] = s * Rr[4 * bi + k]; c[k] = Rr[4 * bj + k]; }
+        for (int k = 0; k < 4; ++k) g[k] = -acc[k * 4];
+        return;
+    }
+    double* H = P.hslab + (size_t)tm[1] * 144;
+    const int i0 = 4 * ia, j0 = 4 * jb;
+    if (tm[0] & 1) {
 #pragma unroll
         for (int k = 0; k < 4; ++k)
 #pragma unroll
-            for (int l = 0; l < 4; ++l) acc[k * 4 + l] += a[k] * c[l];
-    }
-    if (bj == 6) {   // column 24 = e (columns 25..27 are the point block: not part of this product)
-        const int slot = (bi < 3) ? sm[6] : sm[7];
-        if (slot >= 0) {
-            double* g = P.gslab + (size_t)slot * 12 + 4 * (bi % 3);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) g[k] = -acc[k * 4];
-        }
-        return;
-    }
-    const bool bb = bi >= 3, ab = bi < 3 && bj >= 3;
-    const int slot = ab ? sm[3] : (bb ? sm[4] : sm[2]);
-    if (slot < 0) return;
-    double* H = P.hslab + (size_t)slot * 144;
-    const int i0 = 4 * (bi % 3), j0 = 4 * (bj % 3);
-    if (ab) {
-        const bool tr = sm[5] != 0;   // block stored for (b, a): transposed
+            for (int l = 0; l < 4; ++l) {
+                H[(i0 + k) * 12 + j0 + l] = acc[k * 4 + l];
+                if (ia != jb) H[(j0 + l) * 12 + i0 + k] = acc[k * 4 + l];
+            }
+    } else {
+        const bool tr = (tm[0] & 2) != 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
 #pragma unroll
             for (int l = 0; l < 4; ++l) {
                 if (tr) H[(j0 + l) * 12 + i0 + k] = acc[k * 4 + l];
                 else H[(i0 + k) * 12 + j0 + l] = acc[k * 4 + l];
-            }
-    } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int l = 0; l < 4; ++l) {
-                H[(i0 + k) * 12 + j0 + l] = acc[k * 4 + l];
-                if (bi != bj) H[(j0 + l) * 12 + i0 + k] = acc[k * 4 + l];
             }
     }
 }
@@ -271,7 +263,9 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, const doub
                                                         const double* __restrict__ lst, int write_res) {
     __shared__ double rows[TILE_ROWS * ROW_STRIDE];
     __shared__ double rw[TILE_ROWS];
-    __shared__ int segm[TILE_SEGS * SEGM_STRIDE];
+    __shared__ int tgtm[TILE_TGT * TGT_STRIDE];
+    __shared__ int trr[TILE_RUNS];
+    __shared__ int tro[TILE_RUNS];
     __shared__ int prow[TILE_PROWS];
     __shared__ int pr0[TILE_PAIRS + 1];
     __shared__ int lrow[TILE_ROWS];
@@ -279,7 +273,7 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, const doub
     __shared__ double red[TILE_OBS / 64];
     const int tile = blockIdx.x, tid = threadIdx.x;
     const int obs0 = P.tile_obs0[tile], nobs = P.tile_nobs[tile];
-    const int seg0 = P.tile_seg0[tile], nseg = P.tile_nseg[tile];
+    const int tg0 = P.tile_tgt0[tile], ntg = P.tile_ntgt[tile];
     const int pair0 = P.tile_pair0[tile], npair = P.tile_npair[tile];
     const int lm0 = P.tile_lm0[tile], nlm = P.tile_nlm[tile];
     LBA_TMARK(P.tdbg_lin, 0);
@@ -288,10 +282,18 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, const doub
     {
         const int q0 = P.pair_r0[pair0], nq = P.pair_r0[pair0 + npair] - q0;
         const int m0 = P.lm_r0[lm0], nm = P.lm_r0[lm0 + nlm] - m0;
+        const int u0 = P.tile_run0[tile];
+        const int nu = ntg ? P.tgt_meta[(size_t)(tg0 + ntg - 1) * TGT_STRIDE + 3] +
+                                 (P.tgt_meta[(size_t)(tg0 + ntg - 1) * TGT_STRIDE] >> 8) : 0;
 #pragma unroll
-        for (int k = 0; k < (TILE_SEGS * SEGM_STRIDE + TILE_OBS - 1) / TILE_OBS; ++k) {
+        for (int k = 0; k < (TILE_TGT * TGT_STRIDE + TILE_OBS - 1) / TILE_OBS; ++k) {
             const int t = tid + k * TILE_OBS;
-            if (t < nseg * SEGM_STRIDE) segm[t] = P.seg_meta[(size_t)seg0 * SEGM_STRIDE + t];
+            if (t < ntg * TGT_STRIDE) tgtm[t] = P.tgt_meta[(size_t)tg0 * TGT_STRIDE + t];
+        }
+#pragma unroll
+        for (int k = 0; k < (TILE_RUNS + TILE_OBS - 1) / TILE_OBS; ++k) {
+            const int t = tid + k * TILE_OBS;
+            if (t < nu) { trr[t] = P.run_rows[u0 + t]; tro[t] = P.run_offs[u0 + t]; }
         }
 #pragma unroll
         for (int k = 0; k < TILE_PROWS / TILE_OBS; ++k) {
@@ -325,12 +327,22 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, const doub
     if (tid == 0) P.chi_lin[tile] = tchi;
     LBA_TMARK(P.tdbg_lin, 1);
 
-    // ---- phase 2: Hpp / b_p partial per pose-pair segment, one (segment, 4x4 block) per task
-    for (int task = tid; task < nseg * 27; task += TILE_OBS) {
-        const int si = task / 27;
-        int bi, bj;
-        seg_block(task - si * 27, &bi, &bj);
-        seg_task(P, rows, rw, segm + si * SEGM_STRIDE, bi, bj);
+    // ---- phase 2: one Hpp / b_p partial per target block of the tile, one (target, 4x4 sub-block)
+    //      per task: diagonal targets 6 upper sub-blocks + 3 b_k pieces, off-diagonal 9 sub-blocks
+    for (int task = tid; task < ntg * 9; task += TILE_OBS) {
+        const int g = task / 9, sub = task - g * 9;
+        const int* tm = tgtm + g * TGT_STRIDE;
+        int ia, jb;
+        if (tm[0] & 1) {
+            constexpr unsigned char dia[9] = {0, 0, 0, 1, 1, 2, 0, 1, 2};
+            constexpr signed char djb[9] = {0, 1, 2, 1, 2, 2, -1, -1, -1};
+            ia = dia[sub];
+            jb = djb[sub];
+        } else {
+            ia = sub / 3;
+            jb = sub - 3 * ia;
+        }
+        tgt_task(P, rows, rw, tm, trr, tro, ia, jb);
     }
     LBA_TMARK(P.tdbg_lin, 2);
 
