@@ -15,7 +15,6 @@
 //                 velocity edge), each block stored at a slot sorted by its target upper block
 //   sslab/gpslab  per (tile, KF pair) Schur partials V(k1) Hpl(k2)^T and per (tile, KF) rhs
 //                 partials, target-sorted likewise
-//   Hblk, Sblk    [n_ublocks][144] reduced Hpp / damped Schur complement, upper blocks
 //   S, Lm         [npad][npad] dense reduced camera system (lower) and its Cholesky factor; npad =
 //                 np rounded up to CHOL_NB with an identity tail, so every Cholesky panel is full
 #pragma once
@@ -109,8 +108,8 @@ struct DevProblem {
     const int* seg_slot;    // per slab entry (motion priors, velocity edges): 5 ints
                             //   aa, ab, bb slot in hslab (-1 = none), ab transposed flag, -
     const int* seg_gslot;   // per slab entry: ga, gb slot in gslab (-1 = none)
-    const int* hub_list;    // upper blocks that receive Hpp sources
-    int n_hub;
+    const int* asm_list;    // upper blocks inside the structural pattern of S (diagonal + any source)
+    int n_asm;
     const int* hs0;         // [n_ublocks + 1] hslab range per upper block
     const int* gs0;         // [n_pb + 1] gslab range per pose block
     const int* ub_i;        // per upper block: block row / col
@@ -133,8 +132,6 @@ struct DevProblem {
     double* gslab;          // [n_gslots][12] b_p partials, target-sorted
     double* sslab;          // [n_sslots][144] Schur partial blocks, target-sorted
     double* gpslab;         // [n_gpslots][12] Schur rhs partials, target-sorted
-    double* Hblk;           // [n_ublocks][144] reduced Hpp (upper blocks)
-    double* Sblk;           // [n_ublocks][144] assembled reduced camera system (upper blocks)
     double* Lm;             // [npad][npad] Cholesky factor (lower, row-major)
     const int* pfirst;      // [npad / CHOL_NB] first panel each panel of rows of S / L has non-zeros in
     double* LinvT;          // [npad / CHOL_NB][CHOL_NB][CHOL_NB] inverse diagonal blocks L_bb^-T (row-major)
@@ -168,7 +165,6 @@ void launch_gp_prep(const DevProblem& P, const double* kst, int jac, hipStream_t
 void launch_linearize(const DevProblem& P, const double* kst, const double* lst, int write_res, hipStream_t s);
 void launch_prior_lin(const DevProblem& P, const double* kst, hipStream_t s);
 void launch_schur(const DevProblem& P, double lambda, hipStream_t s);
-void launch_hpp_reduce(const DevProblem& P, hipStream_t s);
 enum { ASM_SCHUR = 1, ASM_FULL = 2 };
 void launch_assemble(const DevProblem& P, double lambda, int flags, hipStream_t s);
 void launch_cholesky_solve(const DevProblem& P, hipStream_t s);

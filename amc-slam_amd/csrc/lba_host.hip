@@ -531,9 +531,6 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         if (a >= 0 && b >= 0) { sl[1] = hfill[ublock_id(n_pb, std::min(a, b), std::max(a, b))]++; sl[3] = a > b; }
         if (b >= 0) { sl[2] = hfill[ublock_id(n_pb, b, b)]++; seg_gslot[2 * (size_t)en + 1] = gfill[b]++; }
     }
-    std::vector<int> hub_list;
-    for (int u = 0; u < n_ublocks; ++u)
-        if (hcnt[u] > 0) hub_list.push_back(u);
     // Schur partial blocks per (tile, KF pair) and rhs partials per (tile, KF)
     std::vector<int> scnt(n_ublocks + 1, 0), gpcnt(n_pb + 1, 0);
     for (int s = 0; s < n_sent; ++s) scnt[ublock_id(n_pb, sent_k1[s], sent_k2[s])]++;
@@ -544,6 +541,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     for (int s = 0; s < n_sent; ++s) sslot[s] = sfill[ublock_id(n_pb, sent_k1[s], sent_k2[s])]++;
     for (size_t t = 0; t < tkf_list.size(); ++t) tkf_gslot[t] = gpfill[tkf_list[t]]++;
     const int n_hslots = hs0[n_ublocks], n_gslots = gs0[n_pb], n_sslots = ss0[n_ublocks], n_gpslots = gps0[n_pb];
+
 
     // ---- observations in device order
     std::vector<int> ob_meta(n_obs), ob_kfa(n_obs), ob_kfb(n_obs), ob_gp(n_obs), ob_lm(n_obs);
@@ -629,7 +627,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         HIPCHK(hipMemset(D.tdbg_bs, 0, (size_t)nblk * 16 * 8));
     }
     D.seg_slot = dupload(p, seg_slot); D.seg_gslot = dupload(p, seg_gslot);
-    D.hub_list = dupload(p, hub_list); D.n_hub = (int)hub_list.size();
+
     D.hs0 = dupload(p, hs0); D.gs0 = dupload(p, gs0); D.ub_i = dupload(p, ub_i); D.ub_j = dupload(p, ub_j);
     D.sslot = dupload(p, sslot); D.ss0 = dupload(p, ss0); D.tkf_gslot = dupload(p, tkf_gslot);
     D.gps0 = dupload(p, gps0);
@@ -647,9 +645,6 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.gslab = dalloc<double>(p, (size_t)12 * std::max(n_gslots, 1));
     D.sslab = dalloc<double>(p, (size_t)144 * std::max(n_sslots, 1));
     D.gpslab = dalloc<double>(p, (size_t)12 * std::max(n_gpslots, 1));
-    D.Hblk = dalloc<double>(p, (size_t)144 * std::max(n_ublocks, 1));
-    HIPCHK(hipMemset(D.Hblk, 0, sizeof(double) * 144 * (size_t)std::max(n_ublocks, 1)));   // blocks without sources
-    D.Sblk = dalloc<double>(p, (size_t)144 * std::max(n_ublocks, 1));
     const int npad = (p->np + CHOL_NB - 1) / CHOL_NB * CHOL_NB;
     // envelope of S (and so of its Cholesky factor, whose fill stays inside it): per CHOL_NB panel
     // of rows, the first panel any of its rows has a structural non-zero in
@@ -665,6 +660,18 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             pfirst[P] = f;
         }
         D.pfirst = dupload(p, pfirst);
+        // blocks k_assemble rewrites every trial: every upper block of S that intersects that
+        // panel envelope, i.e. everything the factorisation may write (structural non-zeros and
+        // fill-in); the rest of S stays zero from the upload
+        std::vector<int> asm_list;
+        for (int u = 0; u < n_ublocks; ++u) {
+            const int bi = ub_i[u], bj = ub_j[u];
+            bool in = bi == bj;
+            for (int r = 12 * bj; r < 12 * bj + 12 && !in; ++r) in = pfirst[r / CHOL_NB] * CHOL_NB <= 12 * bi + 11;
+            if (in) asm_list.push_back(u);
+        }
+        D.asm_list = dupload(p, asm_list);
+        D.n_asm = (int)asm_list.size();
     }
     D.npad = npad;
     D.Lm = dalloc<double>(p, (size_t)npad * npad + 1);
@@ -718,7 +725,6 @@ void linearize(lba_problem* p, int write_res, bool timed = false) {
     launch_linearize(D, p->kst[p->cur], p->lst[p->cur], write_res, p->stream);
     if (timed) HIPCHK(hipEventRecord(p->ev[7], p->stream));
     launch_prior_lin(D, p->kst[p->cur], p->stream);
-    launch_hpp_reduce(D, p->stream);
     HIPCHK(hipGetLastError());
     p->linearized = true;
 }

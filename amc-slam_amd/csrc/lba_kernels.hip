@@ -9,10 +9,10 @@
 //                    Hpl blocks and Hll/bl (BlockSolver::buildSystem, block_solver.hpp:502-560;
 //                    edge quadratic forms base_multi_edge.hpp:170-222)
 //   k_prior_lin      EdgeGaussianPrior / EdgeVelocity quadratic forms (src/G2oTypes.cc:100-118)
-//   k_hpp_reduce     Hpp / b_p from the target-sorted tile partials (once per iteration)
 //   k_schur          per tile: Dinv = (Hll + lambda I)^-1, V = Hpl Dinv, g = V bl, S partials
 //                    V(k1) Hpl(k2)^T and rhs partials                   (block_solver.hpp:381-430)
-//   k_assemble       S = Hpp + lambda I - sum partials, bS = b_p - sum g     (block_solver.hpp:432-445)
+//   k_assemble       S = sum Hpp partials + lambda I - sum Schur partials, b_p, bS = b_p - sum g
+//                    (block_solver.hpp:432-445)
 //   k_chol_*         blocked Cholesky + forward/back substitution of S     (linear_solver_dense.h:65-113)
 //   k_update         landmark back-substitution + oplus into the trial state (block_solver.hpp:461-482,
 //                    sparse_optimizer.cpp:422-435) + computeScale partials
@@ -469,33 +469,6 @@ __global__ __launch_bounds__(64) void k_prior_lin(DevProblem P, const double* __
     }
 }
 
-// Hpp / b_p reduction (once per LM iteration): each upper block sums its contiguous slab range
-__global__ __launch_bounds__(144 * RED_GROUPS) void k_hpp_reduce(DevProblem P) {
-    __shared__ double red[144 * RED_GROUPS];
-    const int tid = threadIdx.x;
-    if ((int)blockIdx.x < P.n_hub) {
-        const int ub = P.hub_list[blockIdx.x];
-        const int e = tid % 144, g = tid / 144;
-        double v = 0.0;
-        for (int s = P.hs0[ub] + g; s < P.hs0[ub + 1]; s += RED_GROUPS) v += P.hslab[(size_t)s * 144 + e];
-        red[tid] = v;
-        __syncthreads();
-        if (g == 0) P.Hblk[(size_t)ub * 144 + e] = red[e] + red[144 + e] + red[288 + e] + red[432 + e];
-    } else {
-        const int k = blockIdx.x - P.n_hub;
-        const int e = tid % 12, g = tid / 12;   // 48 groups
-        double v = 0.0;
-        for (int s = P.gs0[k] + g; s < P.gs0[k + 1]; s += 48) v += P.gslab[(size_t)s * 12 + e];
-        red[tid] = v;
-        __syncthreads();
-        if (tid < 12) {
-            double t = 0.0;
-            for (int q = 0; q < 48; ++q) t += red[q * 12 + tid];
-            P.bp[12 * k + tid] = t;
-        }
-    }
-}
-
 // Landmark elimination for one tile of landmarks (BlockSolver::solve's Schur loop,
 // block_solver.hpp:381-430): Dinv = (Hll + lambda I)^-1 (Eigen 3x3 adjugate inverse), then for every
 // KF pair (k1, k2) the tile's landmarks couple, the S partial sum_m Hpl(m,k1) Dinv_m Hpl(m,k2)^T, and
@@ -618,42 +591,53 @@ __global__ __launch_bounds__(256) void k_schur(DevProblem P, double lambda) {
     LBA_TMARK(P.tdbg_schur, 5);
 }
 
+// Reduced camera system of one trial, straight from the target-sorted partial slabs (each
+// output block sums one contiguous range, so the reads are coalesced and the order is fixed):
+//   S(bi, bj) = sum Hpp partials + lambda I (diagonal) - sum Schur partials   (block_solver.hpp:432-445,
+//   setLambda :573-579), only for the blocks inside the structural pattern (the rest of S is zero
+//   from the upload and never written);  b_p = sum b partials;  bS = b_p - sum Schur rhs partials.
 __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, double lambda, int flags) {
     __shared__ double red[144 * RED_GROUPS];
     const int tid = threadIdx.x;
     const int n = P.npad;   // leading dimension of S
-    if ((int)blockIdx.x < P.n_ublocks) {
-        const int ub = blockIdx.x;
+    if ((int)blockIdx.x < P.n_asm) {
+        const int ub = P.asm_list[blockIdx.x];
         const int bi = P.ub_i[ub], bj = P.ub_j[ub];
         const int e = tid % 144, g = tid / 144;
         double v = 0.0;
-        if (g == 0) {
-            v = P.Hblk[(size_t)ub * 144 + e];
-            if (bi == bj && e % 13 == 0) v += lambda;   // setLambda on Hpp (block_solver.hpp:573-579)
-        }
+        for (int s = P.hs0[ub] + g; s < P.hs0[ub + 1]; s += RED_GROUPS) v += P.hslab[(size_t)s * 144 + e];
         if (flags & ASM_SCHUR)
             for (int s = P.ss0[ub] + g; s < P.ss0[ub + 1]; s += RED_GROUPS) v -= P.sslab[(size_t)s * 144 + e];
         red[tid] = v;
         __syncthreads();
         if (g == 0) {
-            const double t = red[e] + red[144 + e] + red[288 + e] + red[432 + e];
+            double t = red[e] + red[144 + e] + red[288 + e] + red[432 + e];
+            if (bi == bj && e % 13 == 0) t += lambda;
             const int i = e / 12, j = e % 12;
-            P.Sblk[(size_t)ub * 144 + e] = t;
             P.S[(size_t)(12 * bj + j) * n + 12 * bi + i] = t;
             if (flags & ASM_FULL) P.S[(size_t)(12 * bi + i) * n + 12 * bj + j] = t;
         }
     } else {
-        const int k = blockIdx.x - P.n_ublocks;
+        const int k = blockIdx.x - P.n_asm;
         const int e = tid % 12, g = tid / 12;   // 48 groups
-        double v = (g == 0) ? P.bp[12 * k + e] : 0.0;
+        double v = 0.0, w = 0.0;
+        for (int s = P.gs0[k] + g; s < P.gs0[k + 1]; s += 48) v += P.gslab[(size_t)s * 12 + e];
         if (flags & ASM_SCHUR)
-            for (int s = P.gps0[k] + g; s < P.gps0[k + 1]; s += 48) v -= P.gpslab[(size_t)s * 12 + e];
+            for (int s = P.gps0[k] + g; s < P.gps0[k + 1]; s += 48) w += P.gpslab[(size_t)s * 12 + e];
         red[tid] = v;
+        __syncthreads();
+        double bpv = 0.0;
+        if (tid < 12) {
+            for (int q = 0; q < 48; ++q) bpv += red[q * 12 + tid];
+            P.bp[12 * k + tid] = bpv;
+        }
+        __syncthreads();
+        red[tid] = w;
         __syncthreads();
         if (tid < 12) {
             double t = 0.0;
             for (int q = 0; q < 48; ++q) t += red[q * 12 + tid];
-            P.xsol[12 * k + tid] = t;   // bS = b_p - sum Hpl Dinv bl
+            P.xsol[12 * k + tid] = bpv - t;   // bS = b_p - sum Hpl Dinv bl
         }
     }
 }
@@ -770,6 +754,7 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restr
     __shared__ double Pi[CNB][CNB + 1];
     __shared__ double Pj[CNB][CNB + 1];
     __shared__ double yp[CNB];
+    __shared__ double stg[3][2 * CNB][CNB + 1];   // per factoring wave: its stacked panel, row-major
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & (CNB - 1);
     const int q = p + CNB, nt = (n - q) / CNB;
     int ti = 0, tj = 0;
@@ -792,22 +777,34 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restr
     const bool fact = wave < 2 || (wave == 2 && blockIdx.x == 0);
     double row[CNB];
     if (fact) {
-        // unconditional loads from a valid row (branch-free), then select the identity / zero rows
-        const double* src = A + (size_t)(p + l32) * n + p;
-        bool use = lane < CNB;
-        if (lane >= CNB && wave < 2 && nt > 0 && (wave == 0 || tj != ti)) {
-            src = A + (size_t)(q + (wave ? tj : ti) * CNB + l32) * n + p;
-            use = true;
-        } else if (wave == 1 && lane == CNB) {
-            src = b + p;
-            use = true;
-        }
-        const double idv = (wave == 2) ? 1.0 : 0.0;
+        // The wave's 64 x 32 stacked panel is read coalesced (16 lanes x 16 B per row, 4 rows per
+        // instruction) into LDS, then every lane takes its row: a lane-per-row gather would touch
+        // 64 cache lines per instruction.  Rows 32..63: tile rows, b_p^T (lane 32 of wave 1 when
+        // tj == ti), the identity (wave 2) or zero.
+        double (*st)[CNB + 1] = stg[wave];
+        const int cq = (lane & 15) * 2;
 #pragma unroll
-        for (int c = 0; c < CNB; ++c) {
-            const double v = src[c];
-            row[c] = use ? v : (c == l32 ? idv : 0.0);
+        for (int k = 0; k < 16; ++k) {
+            const int rr = 4 * k + (lane >> 4), r32 = rr & (CNB - 1);
+            const double* src = A + (size_t)(p + r32) * n + p;   // always valid (diagonal rows)
+            bool use = rr < CNB;
+            if (rr >= CNB && wave < 2 && nt > 0 && (wave == 0 || tj != ti)) {
+                src = A + (size_t)(q + (wave ? tj : ti) * CNB + r32) * n + p;
+                use = true;
+            } else if (wave == 1 && rr == CNB) {
+                src = b + p;
+                use = true;
+            }
+            const double2 v = *reinterpret_cast<const double2*>(src + cq);
+            const double idv = (wave == 2) ? 1.0 : 0.0;
+            st[rr][cq] = use ? v.x : (cq == r32 ? idv : 0.0);
+            st[rr][cq + 1] = use ? v.y : (cq + 1 == r32 ? idv : 0.0);
         }
+        // a wave's LDS accesses execute in order; the wave barrier keeps the compiler from moving
+        // the row reads above the staging stores
+        wave_sync();
+#pragma unroll
+        for (int c = 0; c < CNB; ++c) row[c] = st[lane][c];
     }
     const int tr = tid >> 4, tc = tid & 15;
     const size_t ra = (size_t)q + ti * CNB + 2 * tr, ca = (size_t)q + tj * CNB + 2 * tc;
@@ -1171,12 +1168,8 @@ void launch_prior_lin(const DevProblem& P, const double* kst, hipStream_t s) {
 void launch_schur(const DevProblem& P, double lambda, hipStream_t s) {
     if (P.n_tiles) hipLaunchKernelGGL(k_schur, dim3(P.n_tiles), dim3(256), 0, s, P, lambda);
 }
-void launch_hpp_reduce(const DevProblem& P, hipStream_t s) {
-    const int n = P.n_hub + P.n_pb;
-    if (n) hipLaunchKernelGGL(k_hpp_reduce, dim3(n), dim3(144 * RED_GROUPS), 0, s, P);
-}
 void launch_assemble(const DevProblem& P, double lambda, int flags, hipStream_t s) {
-    const int n = P.n_ublocks + P.n_pb;
+    const int n = P.n_asm + P.n_pb;
     if (n) hipLaunchKernelGGL(k_assemble, dim3(n), dim3(144 * RED_GROUPS), 0, s, P, lambda, flags);
 }
 void launch_cholesky_solve(const DevProblem& P, hipStream_t s) {
