@@ -110,6 +110,8 @@ struct DevProblem {
     const int* seg_gslot;   // per slab entry: ga, gb slot in gslab (-1 = none)
     const int* asm_list;    // upper blocks inside the structural pattern of S (diagonal + any source)
     int n_asm;
+    const int* ztiles;      // tiles (i | j << 16) of the permuted envelope, zeroed before each assembly
+    int n_ztiles;
     const int* hs0;         // [n_ublocks + 1] hslab range per upper block
     const int* gs0;         // [n_pb + 1] gslab range per pose block
     const int* ub_i;        // per upper block: block row / col
@@ -133,13 +135,21 @@ struct DevProblem {
     double* sslab;          // [n_sslots][144] Schur partial blocks, target-sorted
     double* gpslab;         // [n_gpslots][12] Schur rhs partials, target-sorted
     double* Lm;             // [npad][npad] Cholesky factor (lower, row-major)
-    const int* pfirst;      // [npad / CHOL_NB] first panel each panel of rows of S / L has non-zeros in
+    // dense solve in the factorisation (nested-dissection) order of the panels: position = ppos[natural],
+    // natural = pnat[position]; pfirst = envelope of the permuted matrix; chol_items = work items of the
+    // schedule h_steps (host memory: panel A, panel B, first item, end item per step)
+    const int* pfirst;
+    const int* ppos;
+    const int* pnat;
+    const int* chol_items;
+    const int* h_steps;
+    int n_steps;
     double* LinvT;          // [npad / CHOL_NB][CHOL_NB][CHOL_NB] inverse diagonal blocks L_bb^-T (row-major)
     double* Hpl;
     double* Hll;
     double* bl;
     double* Dinv;
-    double* S;              // [npad][npad], rows/cols >= np: identity
+    double* S;              // [npad][npad] (factorisation order; natural order for ASM_FULL), padding: identity
     double* bp;             // [np]
     double* xsol;           // [np] rhs -> solution
     double* yv;             // [np] forward-substituted rhs

@@ -47,6 +47,8 @@ struct lba_problem {
     std::vector<void*> allocs;
     double* h_fin = nullptr;      // host-mapped coherent [8]: trial summary [4] + sequence number
     double* d_hfin = nullptr;     // its device address
+    std::vector<int> chol_steps;  // dense-solve schedule: (panel A, panel B, first item, end item) per step
+    int s_layout = 0;             // layout last assembled into S: 0 factorisation order, 1 natural (full)
     unsigned long long fin_seq = 0;
     double lambda = -1.0, ni = 2.0;
     int nBad = 0;
@@ -646,30 +648,83 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.sslab = dalloc<double>(p, (size_t)144 * std::max(n_sslots, 1));
     D.gpslab = dalloc<double>(p, (size_t)12 * std::max(n_gpslots, 1));
     const int npad = (p->np + CHOL_NB - 1) / CHOL_NB * CHOL_NB;
-    // envelope of S (and so of its Cholesky factor, whose fill stays inside it): per CHOL_NB panel
-    // of rows, the first panel any of its rows has a structural non-zero in
+    // ---- dense solve layout.  Envelope of S at panel granularity (per CHOL_NB panel of rows, the
+    // first panel any of its rows has a structural non-zero in), then a one-level nested-dissection
+    // ordering of the panels: [left | right | separator], where the right block's rows do not touch
+    // the left block's columns.  The factorisation then eliminates left and right panels pairwise in
+    // the same launch and the separator afterwards, so the dependent chain is
+    // max(left, right) + separator panels instead of all of them.  Cholesky fill stays inside the
+    // envelope of the permuted matrix, which bounds everything the solver touches.
     {
+        const int NP = npad / CHOL_NB;
         std::vector<int> fk(n_pb);
         for (int b = 0; b < n_pb; ++b) fk[b] = b;   // diagonal (damping)
         for (int u = 0; u < n_ublocks; ++u)
             if (hcnt[u] > 0 || scnt[u] > 0) fk[ub_j[u]] = std::min(fk[ub_j[u]], ub_i[u]);
-        std::vector<int> pfirst(npad / CHOL_NB);
-        for (int P = 0; P < npad / CHOL_NB; ++P) {
+        std::vector<int> pfirst(NP);
+        for (int P = 0; P < NP; ++P) {
             int f = P;
             for (int r = P * CHOL_NB; r < (P + 1) * CHOL_NB && r < p->np; ++r) f = std::min(f, 12 * fk[r / 12] / CHOL_NB);
             pfirst[P] = f;
         }
-        D.pfirst = dupload(p, pfirst);
-        // blocks k_assemble rewrites every trial: every upper block of S that intersects that
-        // panel envelope, i.e. everything the factorisation may write (structural non-zeros and
-        // fill-in); the rest of S stays zero from the upload
-        std::vector<int> asm_list;
-        for (int u = 0; u < n_ublocks; ++u) {
-            const int bi = ub_i[u], bj = ub_j[u];
-            bool in = bi == bj;
-            for (int r = 12 * bj; r < 12 * bj + 12 && !in; ++r) in = pfirst[r / CHOL_NB] * CHOL_NB <= 12 * bi + 11;
-            if (in) asm_list.push_back(u);
+        int sa = NP, sb = NP, best = NP;
+        for (int a = 1; a < NP; ++a) {
+            int b = NP;
+            while (b > a && pfirst[b - 1] >= a) --b;   // [b, NP): rows with no entry left of a
+            if (b >= NP) continue;
+            const int len = std::max(a, NP - b) + (b - a);
+            if (len < best) { best = len; sa = a; sb = b; }
         }
+        const int nl = sa, nr = NP - sb, ns = sb - sa;
+        std::vector<int> ppos(NP), pnat(NP);
+        for (int P = 0; P < NP; ++P)
+            ppos[P] = P < sa ? P : (P >= sb ? nl + (P - sb) : nl + nr + (P - sa));
+        for (int P = 0; P < NP; ++P) pnat[ppos[P]] = P;
+        // envelope of the permuted matrix (lower part, panel positions)
+        std::vector<int> pfh(NP);
+        for (int i = 0; i < NP; ++i) pfh[i] = i;
+        for (int P = 0; P < NP; ++P)
+            for (int Q = pfirst[P]; Q <= P; ++Q) {
+                const int i = std::max(ppos[P], ppos[Q]), j = std::min(ppos[P], ppos[Q]);
+                pfh[i] = std::min(pfh[i], j);
+            }
+        // launch schedule: steps of (panel A, panel B); work items per step: a diagonal item per panel
+        // (publishes L_pp, L_pp^-T, y_p) and every trailing tile inside the envelope with the mask
+        // of the step's panels that update it.  Item: i | j << 10 | mask << 20 | diag << 22.
+        std::vector<int> steps, items;
+        auto add_step = [&](int pa, int pb) {
+            const int it0 = (int)items.size();
+            if (pa >= 0) items.push_back(pa | (pa << 10) | (1 << 20) | (1 << 22));
+            if (pb >= 0) items.push_back(pb | (pb << 10) | (2 << 20) | (1 << 22));
+            const int pmin = pa >= 0 ? pa : pb;
+            for (int i = pmin + 1; i < NP; ++i)
+                for (int j = pmin + 1; j <= i; ++j) {
+                    int mask = 0;
+                    if (pa >= 0 && j > pa && pfh[i] <= pa && pfh[j] <= pa) mask |= 1;
+                    if (pb >= 0 && j > pb && pfh[i] <= pb && pfh[j] <= pb) mask |= 2;
+                    if (mask) items.push_back(i | (j << 10) | (mask << 20));
+                }
+            steps.push_back(pa); steps.push_back(pb); steps.push_back(it0); steps.push_back((int)items.size());
+        };
+        for (int k = 0; k < std::max(nl, nr); ++k) add_step(k < nl ? k : -1, k < nr ? nl + k : -1);
+        for (int k = 0; k < ns; ++k) add_step(nl + nr + k, -1);
+        p->chol_steps = steps;
+        D.h_steps = p->chol_steps.data();
+        D.n_steps = (int)steps.size() / 4;
+        D.chol_items = dupload(p, items);
+        D.pfirst = dupload(p, pfh);
+        D.ppos = dupload(p, ppos);
+        D.pnat = dupload(p, pnat);
+        // every trial, k_schur zeroes the tiles of S inside the permuted envelope (everything the
+        // factorisation may write: structural non-zeros and fill-in) and k_assemble then writes the
+        // structurally non-zero blocks; the rest of S stays zero from the upload
+        std::vector<int> ztiles, asm_list;
+        for (int i = 0; i < NP; ++i)
+            for (int j = pfh[i]; j <= i; ++j) ztiles.push_back(i | (j << 16));
+        for (int u = 0; u < n_ublocks; ++u)
+            if (hcnt[u] > 0 || scnt[u] > 0 || ub_i[u] == ub_j[u]) asm_list.push_back(u);
+        D.ztiles = dupload(p, ztiles);
+        D.n_ztiles = (int)ztiles.size();
         D.asm_list = dupload(p, asm_list);
         D.n_asm = (int)asm_list.size();
     }
@@ -684,14 +739,11 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.bp = dalloc<double>(p, p->np + 1);
     D.xsol = dalloc<double>(p, npad + 1);
     D.yv = dalloc<double>(p, npad + 1);
-    {   // S padding: identity tail (never touched by assembly or factorisation), zero rhs tail
-        HIPCHK(hipMemset(D.S, 0, sizeof(double) * ((size_t)npad * npad + 1)));
-        HIPCHK(hipMemset(D.Lm, 0, sizeof(double) * ((size_t)npad * npad + 1)));
-        HIPCHK(hipMemset(D.xsol, 0, sizeof(double) * (npad + 1)));
-        const double one = 1.0;
-        for (int i = p->np; i < npad; ++i)
-            HIPCHK(hipMemcpy(D.S + (size_t)i * npad + i, &one, sizeof(double), hipMemcpyHostToDevice));
-    }
+    // S and L start zero (k_assemble writes the identity of the padding rows every time)
+    HIPCHK(hipMemset(D.S, 0, sizeof(double) * ((size_t)npad * npad + 1)));
+    HIPCHK(hipMemset(D.Lm, 0, sizeof(double) * ((size_t)npad * npad + 1)));
+    HIPCHK(hipMemset(D.xsol, 0, sizeof(double) * (npad + 1)));
+    p->s_layout = 0;
     D.x = dalloc<double>(p, p->np + 3 * (size_t)nl + 1);
     HIPCHK(hipMemset(D.x, 0, sizeof(double) * (p->np + 3 * (size_t)nl + 1)));   // BlockSolver::_x before any solve
     const int nchi = n_tiles + D.n_prior + D.n_vel;
@@ -749,12 +801,23 @@ void finalize_and_wait(lba_problem* p, bool sync) {
     if (sync) HIPCHK(hipStreamSynchronize(p->stream));
 }
 
+// S holds either the factorisation-order lower triangle (trials) or the natural full matrix
+// (ASM_FULL: lba_linearize / lambda init); switching layouts clears it first, since each layout only
+// rewrites its own pattern
+void assemble_layout(lba_problem* p, double lambda, int flags) {
+    const int want = (flags & ASM_FULL) ? 1 : 0;
+    if (want != p->s_layout || want == 1)
+        HIPCHK(hipMemsetAsync(p->D.S, 0, sizeof(double) * ((size_t)p->D.npad * p->D.npad), p->stream));
+    p->s_layout = want;
+    launch_assemble(p->D, lambda, flags, p->stream);
+}
+
 // one damped solve + update into the trial buffers + evaluation of the trial state
 void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs, bool sync = true) {
     const DevProblem& D = p->D;
     const int nx = 1 - p->cur;
     launch_schur(D, lambda, p->stream);   // also clears the factorisation status
-    launch_assemble(D, lambda, ASM_SCHUR, p->stream);
+    assemble_layout(p, lambda, ASM_SCHUR);
     if (evs) HIPCHK(hipEventRecord(evs[0], p->stream));
     launch_cholesky_solve(D, p->stream);
     if (evs) HIPCHK(hipEventRecord(evs[1], p->stream));
@@ -778,7 +841,7 @@ double eval_current(lba_problem* p) {
 double lambda_init(lba_problem* p) {   // computeLambdaInit (levenberg.cpp:171-185)
     if (p->cfg.lambda_init > 0) return p->cfg.lambda_init;
     const DevProblem& D = p->D;
-    launch_assemble(D, 0.0, ASM_FULL, p->stream);
+    assemble_layout(p, 0.0, ASM_FULL);
     std::vector<double> S((size_t)p->np * p->np), Hll(9 * (size_t)std::max(D.n_lm, 1));
     if (p->np)
         HIPCHK(hipMemcpy2DAsync(S.data(), p->np * sizeof(double), D.S, D.npad * sizeof(double),
@@ -1069,7 +1132,7 @@ int lba_linearize(lba_problem* p, double* residuals, double* H_pp, double* b, do
         HIPCHK(hipSetDevice(p->cfg.device));
         const DevProblem& D = p->D;
         linearize(p, residuals ? 1 : 0);
-        launch_assemble(D, 0.0, ASM_FULL, p->stream);
+        assemble_layout(p, 0.0, ASM_FULL);
         HIPCHK(hipGetLastError());
         const int np = p->np, nl = D.n_lm;
         std::vector<double> bp(np + 1), bl(3 * (size_t)nl + 1), hll(9 * (size_t)nl + 1), res(3 * (size_t)p->n_obs + 1);

@@ -470,19 +470,24 @@ __global__ __launch_bounds__(64) void k_prior_lin(DevProblem P, const double* __
 }
 
 // Landmark elimination for one tile of landmarks (BlockSolver::solve's Schur loop,
-// block_solver.hpp:381-430): Dinv = (Hll + lambda I)^-1 (Eigen 3x3 adjugate inverse), then for every
-// KF pair (k1, k2) the tile's landmarks couple, the S partial sum_m Hpl(m,k1) Dinv_m Hpl(m,k2)^T, and
-// per tile KF the rhs partial sum_m Hpl(m,k) Dinv_m bl_m.  The S partial of one KF pair is one fp64
-// MFMA product on one wave: K runs over (landmark, 3) with A = Hpl(m,k1) Dinv_m formed on the fly
-// from LDS (so V = Hpl Dinv is never stored) and B = Hpl(m,k2)^T.  Dinv is kept for the
-// back-substitution.  Block 0 also clears the factorisation status for the solve that follows.
-__global__ __launch_bounds__(256) void k_schur(DevProblem P, double lambda) {
+// block_solver.hpp:381-430): Dinv = (Hll + lambda I)^-1 (Eigen 3x3 adjugate inverse) and
+// V = Hpl Dinv per (KF, landmark) pair into LDS; then for every KF pair (k1, k2) the tile's landmarks
+// couple, the S partial sum_m V(m,k1) Hpl(m,k2)^T as one fp64-MFMA product on one wave, K running
+// over the (pair, pair, landmark) triples of that KF pair; and per tile KF the rhs partial
+// sum_m V(m,k) bl_m.  Dinv is kept for the back-substitution.  Block 0 also clears the
+// factorisation status for the solve that follows, and the first blocks zero the envelope of S.
+constexpr int SCHUR_THREADS = 512;
+
+__global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double lambda) {
     __shared__ double Hs[TILE_PAIRS * 36];
-    __shared__ double Dl[TILE_LMS * 12];   // Dinv (9) + x = Dinv bl (3) per landmark
+    __shared__ double Vs[TILE_PAIRS * 36];
+    __shared__ double Dl[TILE_LMS * 12];   // Dinv (9) + bl (3) per landmark
     __shared__ int slst[TILE_SLIST];
     __shared__ int sl0[TILE_SENT + 1];
     __shared__ short slot[TILE_LMS * TILE_KF];
+    __shared__ signed char pm[TILE_PAIRS];
     __shared__ int kfl[TILE_KF];
+    constexpr int NT = SCHUR_THREADS, NW = NT / 64;
     const int tile = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int pair0 = P.tile_pair0[tile], npair = P.tile_npair[tile];
     const int lm0 = P.tile_lm0[tile], nlm = P.tile_nlm[tile];
@@ -490,59 +495,74 @@ __global__ __launch_bounds__(256) void k_schur(DevProblem P, double lambda) {
     const int sent0 = P.tile_sent0[tile], nsent = P.tile_nsent[tile];
     LBA_TMARK(P.tdbg_schur, 0);
     if (tile == 0 && tid == 0) *P.info = 0;
+    // clear the envelope tiles of S for this trial's assembly (the previous factorisation left its
+    // fill-in there); k_assemble runs after this kernel
+    for (int z = tile; z < P.n_ztiles; z += gridDim.x) {
+        const int zi = P.ztiles[z] & 0xffff, zj = P.ztiles[z] >> 16;
+        for (int t = tid; t < CHOL_NB * CHOL_NB; t += NT)
+            P.S[(size_t)(zi * CHOL_NB + t / CHOL_NB) * P.npad + zj * CHOL_NB + t % CHOL_NB] = 0.0;
+    }
     // ---- stage Hpl and the Schur triple lists (fixed-count loops of unconditional loads)
     const int nh = npair * 36;
     if (nh > 0) {
-        constexpr int NK = TILE_PAIRS * 36 / 256;
+        constexpr int NK = (TILE_PAIRS * 36 + NT - 1) / NT;
         double hv[NK];
 #pragma unroll
-        for (int k = 0; k < NK; ++k) hv[k] = P.Hpl[(size_t)pair0 * 36 + min(tid + k * 256, nh - 1)];
+        for (int k = 0; k < NK; ++k) hv[k] = P.Hpl[(size_t)pair0 * 36 + min(tid + k * NT, nh - 1)];
 #pragma unroll
         for (int k = 0; k < NK; ++k)
-            if (tid + k * 256 < nh) Hs[tid + k * 256] = hv[k];
+            if (tid + k * NT < nh) Hs[tid + k * NT] = hv[k];
     }
     {
         const int q0 = P.sent_r0[sent0], nq = P.sent_r0[sent0 + nsent] - q0;
 #pragma unroll
-        for (int k = 0; k < TILE_SLIST / 256; ++k) {
-            const int t = tid + k * 256;
+        for (int k = 0; k < (TILE_SLIST + NT - 1) / NT; ++k) {
+            const int t = tid + k * NT;
             if (t < nq) slst[t] = P.sent_list[q0 + t];
         }
         if (tid <= nsent) sl0[tid] = P.sent_r0[sent0 + tid] - q0;
     }
-    for (int t = tid; t < TILE_LMS * TILE_KF; t += 256) slot[t] = -1;
+    for (int t = tid; t < TILE_LMS * TILE_KF; t += NT) slot[t] = -1;
     if (tid < nkf) kfl[tid] = P.tkf_list[kf0 + tid];
     if (tid < nlm) {
         const int l = lm0 + tid;
-        double H[9], D[9], bl[3];
+        double H[9], D[9];
 #pragma unroll
         for (int q = 0; q < 9; ++q) H[q] = P.Hll[(size_t)l * 9 + q];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) bl[q] = P.bl[(size_t)l * 3 + q];
         H[0] += lambda; H[4] += lambda; H[8] += lambda;   // setLambda on Hll (block_solver.hpp:580-587)
         inv3(H, D);
 #pragma unroll
         for (int q = 0; q < 9; ++q) { Dl[tid * 12 + q] = D[q]; P.Dinv[(size_t)l * 9 + q] = D[q]; }
 #pragma unroll
-        for (int q = 0; q < 3; ++q) Dl[tid * 12 + 9 + q] = D[q * 3] * bl[0] + D[q * 3 + 1] * bl[1] + D[q * 3 + 2] * bl[2];
+        for (int q = 0; q < 3; ++q) Dl[tid * 12 + 9 + q] = P.bl[(size_t)l * 3 + q];
     }
     __syncthreads();
     LBA_TMARK(P.tdbg_schur, 1);
-    for (int t = tid; t < npair; t += 256) {
+    for (int t = tid; t < npair; t += NT) {
         const int m = P.pair_lm[pair0 + t] - lm0, k = P.pair_kf[pair0 + t];
         int lk = 0;
         for (int l = 0; l < nkf; ++l)
             if (kfl[l] == k) lk = l;
         slot[m * TILE_KF + lk] = (short)t;
+        pm[t] = (signed char)m;
     }
+    __syncthreads();
+    // ---- V = Hpl Dinv, one (pair, row) per task
+    for (int task = tid; task < npair * 12; task += NT) {
+        const int t = task / 12, r = task - 12 * t;
+        const double* D = Dl + pm[t] * 12;
+        const double h0 = Hs[t * 36 + r * 3], h1 = Hs[t * 36 + r * 3 + 1], h2 = Hs[t * 36 + r * 3 + 2];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) Vs[t * 36 + r * 3 + a] = h0 * D[a] + h1 * D[3 + a] + h2 * D[6 + a];
+    }
+    __syncthreads();
     LBA_TMARK(P.tdbg_schur, 2);
-    // ---- S partials: one wave per KF pair
+    // ---- S partials: one wave per KF pair, K = (landmark, 3), two accumulators
     {
         const int kq = lane >> 4, cl = lane & 15, cr = min(cl, 11);
-        for (int e = wave; e < nsent; e += 4) {
+        for (int e = wave; e < nsent; e += NW) {
             const int qb = sl0[e], nk = 3 * (sl0[e + 1] - qb);
             d4 c0 = {0.0, 0.0, 0.0, 0.0}, c1 = c0;
-            // K = (landmark, 3): lane k = k0 + kq; two accumulators break the MFMA dependency chain
             for (int k0 = 0; k0 < nk; k0 += 8) {
                 double av[2], bv[2];
 #pragma unroll
@@ -552,10 +572,8 @@ __global__ __launch_bounds__(256) void k_schur(DevProblem P, double lambda) {
                     const int kk = k < nk ? k : 0;
                     const int mi = kk / 3, a = kk - 3 * mi;
                     const int code = slst[qb + mi];
-                    const int t1 = code & 255, t2 = (code >> 8) & 255, m = code >> 16;
-                    const double* h1 = Hs + t1 * 36 + cr * 3;
-                    const double* D = Dl + m * 12;
-                    const double x = h1[0] * D[a] + h1[1] * D[3 + a] + h1[2] * D[6 + a];
+                    const int t1 = code & 255, t2 = (code >> 8) & 255;
+                    const double x = Vs[t1 * 36 + cr * 3 + a];
                     const double y = Hs[t2 * 36 + cr * 3 + a];
                     av[h] = ok ? x : 0.0;
                     bv[h] = ok ? y : 0.0;
@@ -574,16 +592,16 @@ __global__ __launch_bounds__(256) void k_schur(DevProblem P, double lambda) {
     }
     LBA_TMARK(P.tdbg_schur, 3);
     LBA_TMARK(P.tdbg_schur, 4);
-    // ---- rhs partials: sum over the KF's landmarks of Hpl(m,k) (Dinv_m bl_m) (block_solver.hpp:395-401)
-    for (int task = tid; task < nkf * 12; task += 256) {
+    // ---- rhs partials: sum over the KF's landmarks of V(m,k) bl_m (block_solver.hpp:395-401)
+    for (int task = tid; task < nkf * 12; task += NT) {
         const int l = task / 12, r = task % 12;
         double v = 0.0;
         for (int m = 0; m < nlm; ++m) {
             const int t = slot[m * TILE_KF + l];
             if (t >= 0) {
-                const double* h = Hs + t * 36 + r * 3;
-                const double* x = Dl + m * 12 + 9;
-                v += h[0] * x[0] + h[1] * x[1] + h[2] * x[2];
+                const double* vv = Vs + t * 36 + r * 3;
+                const double* b = Dl + m * 12 + 9;
+                v += vv[0] * b[0] + vv[1] * b[1] + vv[2] * b[2];
             }
         }
         P.gpslab[(size_t)P.tkf_gslot[kf0 + l] * 12 + r] = v;
@@ -614,9 +632,24 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
             double t = red[e] + red[144 + e] + red[288 + e] + red[432 + e];
             if (bi == bj && e % 13 == 0) t += lambda;
             const int i = e / 12, j = e % 12;
-            P.S[(size_t)(12 * bj + j) * n + 12 * bi + i] = t;
-            if (flags & ASM_FULL) P.S[(size_t)(12 * bi + i) * n + 12 * bj + j] = t;
+            const int r = 12 * bj + j, c = 12 * bi + i;   // element (row r, col c) of S, r >= c in blocks
+            if (flags & ASM_FULL) {                       // natural order, both triangles
+                P.S[(size_t)r * n + c] = t;
+                P.S[(size_t)c * n + r] = t;
+            } else if (bi != bj || j >= i) {               // factorisation order, lower triangle: one
+                // write per unordered pair (the natural-lower entry; a diagonal block's partial sums
+                // are not bitwise symmetric, so writing both would race)
+                const int rh = P.ppos[r / CHOL_NB] * CHOL_NB + r % CHOL_NB;
+                const int ch = P.ppos[c / CHOL_NB] * CHOL_NB + c % CHOL_NB;
+                P.S[(size_t)max(rh, ch) * n + min(rh, ch)] = t;
+            }
         }
+        if (blockIdx.x == 0)   // padding rows: identity
+            for (int r = P.np + tid; r < n; r += 144 * RED_GROUPS) {
+                const int rh = (flags & ASM_FULL) ? r : P.ppos[r / CHOL_NB] * CHOL_NB + r % CHOL_NB;
+                P.S[(size_t)rh * n + rh] = 1.0;
+                P.xsol[rh] = 0.0;   // (the back-substitution leaves natural-order values here)
+            }
     } else {
         const int k = blockIdx.x - P.n_asm;
         const int e = tid % 12, g = tid / 12;   // 48 groups
@@ -637,23 +670,24 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
         if (tid < 12) {
             double t = 0.0;
             for (int q = 0; q < 48; ++q) t += red[q * 12 + tid];
-            P.xsol[12 * k + tid] = bpv - t;   // bS = b_p - sum Hpl Dinv bl
+            const int r = 12 * k + tid;
+            const int rh = (flags & ASM_FULL) ? r : P.ppos[r / CHOL_NB] * CHOL_NB + r % CHOL_NB;
+            P.xsol[rh] = bpv - t;   // bS = b_p - sum Hpl Dinv bl (factorisation order)
         }
     }
 }
 
 // ------------------------------------------------------------------------------------------------
-// Dense Cholesky S = L L^T (right-looking, one launch per CNB-wide panel).  The system is padded
-// to a multiple of CNB with an identity tail (set once at upload; the factorisation never changes
-// it), so every panel is exactly CNB wide and all loops below are compile-time.
-// Every workgroup owns one lower tile of the trailing matrix; it factors the stacked panel
-// [diagonal block; its tile rows; b_p^T] itself (two waves, one row per lane, pivots and column
-// broadcast by readlane), which yields L_pp, the panel rows of its tile and y_p = L_pp^-1 b_p
-// in one pass, then updates its tile, so a launch has no inter-workgroup communication.  All
-// global operands are loaded at kernel entry, before the dependent chain starts.  The factor goes
-// to Lm (row-major) with the inverse diagonal blocks in LinvT; the running right-hand side b is
-// forward-substituted on the fly (y -> yv).  A non-positive pivot sets *info (the LDLT
-// !isPositive failure of linear_solver_dense.h:108-112).
+// Dense Cholesky S = L L^T of the reduced camera system in its factorisation order (panels
+// permuted [left | right | separator] by a one-level nested dissection of the band, lba_host.hip),
+// right-looking, one launch per step of up to two panels that do not update each other.  The
+// system is padded to a multiple of CNB with an identity tail, so every panel is exactly CNB wide
+// and all loops below are compile-time.  Every workgroup factors the stacked panels it needs
+// itself (one row per lane, pivots and column broadcast by readlane), which yields L_pp, the
+// panel rows of its tiles and y_p = L_pp^-1 b_p in one pass, then updates its tile, so a launch has
+// no inter-workgroup communication.  The factor goes to Lm (row-major) with the inverse diagonal
+// blocks in LinvT; the running right-hand side b is forward-substituted on the fly (y -> yv).  A
+// non-positive pivot sets *info (the LDLT !isPositive failure of linear_solver_dense.h:108-112).
 constexpr int CNB = CHOL_NB;
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
@@ -743,161 +777,157 @@ __device__ __forceinline__ void piv_seq(double (&row)[CNB], double r, int lane, 
     }
 }
 
-__global__ __launch_bounds__(256) void k_chol_step(int n, int p, double* __restrict__ A, double* __restrict__ Lm,
-                                                   double* __restrict__ LinvT, double* __restrict__ b,
-                                                   double* __restrict__ yv, int* info, const int* __restrict__ pfirst,
-                                                   unsigned long long* tdbg) {
-    // diagnostics: stamps of workgroup 0 (entry, operands loaded, pivots done, end)
-    unsigned long long* ts = (tdbg && blockIdx.x == 0) ? tdbg + (size_t)(p / CNB) * 16 : nullptr;
-    if (ts && threadIdx.x == 0) ts[0] = clock64();
-    __shared__ double Lt[CNB][CNB + 1];   // diagonal factor, transposed: Lt[c][r] = L(p + r, p + c)
-    __shared__ double Pi[CNB][CNB + 1];
-    __shared__ double Pj[CNB][CNB + 1];
-    __shared__ double yp[CNB];
-    __shared__ double stg[3][2 * CNB][CNB + 1];   // per factoring wave: its stacked panel, row-major
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & (CNB - 1);
-    const int q = p + CNB, nt = (n - q) / CNB;
-    int ti = 0, tj = 0;
-    if (nt > 0) {
-        const int bid = blockIdx.x;
-        ti = (int)((sqrt(8.0 * bid + 1.0) - 1.0) * 0.5);
-        while ((ti + 1) * (ti + 2) / 2 <= bid) ++ti;
-        while (ti * (ti + 1) / 2 > bid) --ti;
-        tj = bid - ti * (ti + 1) / 2;
-        // outside the envelope the panel rows of tile ti or tj are structurally zero: nothing to
-        // update (workgroup 0 always runs: it publishes the diagonal block)
-        const int pc = p / CNB, Pq = q / CNB;
-        if (blockIdx.x != 0 && (pfirst[Pq + ti] > pc || pfirst[Pq + tj] > pc)) return;
-    }
-    // ---- prefetch.  Waves 0 and 1 each hold a stacked 64 x 32 panel: lanes 0..31 the diagonal
-    //      block rows, lanes 32..63 the panel rows of tile ti (wave 0) / tile tj (wave 1), or, when
-    //      tj == ti, b_p^T in lane 32 of wave 1 (factorising it as one more row gives y_p = L^-1 b_p).
-    //      In workgroup 0, wave 2 stacks the identity under the diagonal block: its lanes 32 + k
-    //      end up holding row k of L_pp^-T (the back-substitution's inverse diagonal block).
-    const bool fact = wave < 2 || (wave == 2 && blockIdx.x == 0);
-    double row[CNB];
-    if (fact) {
-        // The wave's 64 x 32 stacked panel is read coalesced (16 lanes x 16 B per row, 4 rows per
-        // instruction) into LDS, then every lane takes its row: a lane-per-row gather would touch
-        // 64 cache lines per instruction.  Rows 32..63: tile rows, b_p^T (lane 32 of wave 1 when
-        // tj == ti), the identity (wave 2) or zero.
-        double (*st)[CNB + 1] = stg[wave];
-        const int cq = (lane & 15) * 2;
+// Load one wave's stacked 64 x 32 panel (rows 0..31: the diagonal block of panel p; rows 32..63:
+// the panel rows of tile `ti` (ti >= 0), b_p^T in row 32 (ti == -1), the identity (ti == -2) or zero
+// (ti == -3)) coalesced through LDS (16 lanes x 16 B per row, 4 rows per instruction), then every lane
+// takes its row.
+__device__ __forceinline__ void load_stacked(const double* __restrict__ A, const double* __restrict__ b, int n, int p,
+                                             int ti, double (*st)[CNB + 1], int lane, double (&row)[CNB]) {
+    const int cq = (lane & 15) * 2;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int rr = 4 * k + (lane >> 4), r32 = rr & (CNB - 1);
-            const double* src = A + (size_t)(p + r32) * n + p;   // always valid (diagonal rows)
-            bool use = rr < CNB;
-            if (rr >= CNB && wave < 2 && nt > 0 && (wave == 0 || tj != ti)) {
-                src = A + (size_t)(q + (wave ? tj : ti) * CNB + r32) * n + p;
-                use = true;
-            } else if (wave == 1 && rr == CNB) {
-                src = b + p;
-                use = true;
-            }
-            const double2 v = *reinterpret_cast<const double2*>(src + cq);
-            const double idv = (wave == 2) ? 1.0 : 0.0;
-            st[rr][cq] = use ? v.x : (cq == r32 ? idv : 0.0);
-            st[rr][cq + 1] = use ? v.y : (cq + 1 == r32 ? idv : 0.0);
+    for (int k = 0; k < 16; ++k) {
+        const int rr = 4 * k + (lane >> 4), r32 = rr & (CNB - 1);
+        const double* src = A + (size_t)(p * CNB + r32) * n + p * CNB;   // always valid (diagonal rows)
+        bool use = rr < CNB;
+        if (rr >= CNB && ti >= 0) {
+            src = A + (size_t)(ti * CNB + r32) * n + p * CNB;
+            use = true;
+        } else if (rr == CNB && ti == -1) {
+            src = b + p * CNB;
+            use = true;
         }
-        // a wave's LDS accesses execute in order; the wave barrier keeps the compiler from moving
-        // the row reads above the staging stores
-        wave_sync();
-#pragma unroll
-        for (int c = 0; c < CNB; ++c) row[c] = st[lane][c];
+        const double2 v = *reinterpret_cast<const double2*>(src + cq);
+        const double idv = (ti == -2) ? 1.0 : 0.0;
+        st[rr][cq] = use ? v.x : (cq == r32 ? idv : 0.0);
+        st[rr][cq + 1] = use ? v.y : (cq + 1 == r32 ? idv : 0.0);
     }
+    // a wave's LDS accesses execute in order; the wave barrier keeps the compiler from moving the
+    // row reads above the staging stores
+    wave_sync();
+#pragma unroll
+    for (int c = 0; c < CNB; ++c) row[c] = st[lane][c];
+}
+
+// One step of the dense factorisation of the permuted system (factorisation order, see lba_host.hip):
+// up to two panels pa, pb (panel positions; -1 = none) that do not update each other, one work item
+// per workgroup (P.chol_items[it0 + blockIdx.x]):
+//   diagonal item of panel p: wave 0 factors [L_pp] (-> Lm), wave 1 [L_pp; b_p^T] (-> y_p), wave 2
+//     [L_pp; I] (-> L_pp^-T for the back-substitution); a non-positive pivot sets *info
+//   tile item (i, j, mask): for each panel of the mask, two waves factor the stacked panels
+//     [L_pp; rows of tile i] and [L_pp; rows of tile j] (or [L_pp; b_p^T] when i == j); then
+//     A(i, j) -= sum over the mask of P_i P_j^T, and when i == j the tile's rows of L are published
+//     and b_i -= sum P_i y_p (forward substitution)
+// so a launch has no inter-workgroup communication.  All global operands are loaded at entry.
+__global__ __launch_bounds__(256) void k_chol_step(int n, int pa, int pb, int it0, const int* __restrict__ items,
+                                                   double* __restrict__ A, double* __restrict__ Lm,
+                                                   double* __restrict__ LinvT, double* __restrict__ b,
+                                                   double* __restrict__ yv, int* info) {
+    __shared__ double stg[4][2 * CNB][CNB + 1];   // per factoring wave: its stacked panel, row-major
+    __shared__ double Pt[4][CNB][CNB + 1];        // factored tile rows: [panel A i, panel A j, panel B i, panel B j]
+    __shared__ double yp[2][CNB];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & (CNB - 1);
+    const int it = items[it0 + blockIdx.x];
+    const int ti = it & 1023, tj = (it >> 10) & 1023, mask = (it >> 20) & 3;
+    const bool diag_item = (it >> 22) & 1;
+    // this wave's stacked panel
+    int panel = -1, other = -3;
+    if (diag_item) {
+        panel = (mask & 1) ? pa : pb;
+        if (wave < 3) other = wave == 0 ? -3 : (wave == 1 ? -1 : -2);
+        else panel = -1;
+    } else {
+        const int pw = (wave < 2) ? ((mask & 1) ? pa : -1) : ((mask & 2) ? pb : -1);
+        if (pw >= 0) {
+            panel = pw;
+            other = ((wave & 1) == 0) ? ti : (tj == ti ? -1 : tj);
+        }
+    }
+    double row[CNB];
+    if (panel >= 0) load_stacked(A, b, n, panel, other, stg[wave], lane, row);
     const int tr = tid >> 4, tc = tid & 15;
-    const size_t ra = (size_t)q + ti * CNB + 2 * tr, ca = (size_t)q + tj * CNB + 2 * tc;
+    const size_t ra = (size_t)ti * CNB + 2 * tr, ca = (size_t)tj * CNB + 2 * tc;
     double a00 = 0.0, a01 = 0.0, a10 = 0.0, a11 = 0.0;
-    if (nt > 0) {
+    if (!diag_item) {
         a00 = A[ra * n + ca]; a01 = A[ra * n + ca + 1];
         a10 = A[(ra + 1) * n + ca]; a11 = A[(ra + 1) * n + ca + 1];
     }
-    if (ts) {
-        __builtin_amdgcn_s_waitcnt(0);   // operands arrived
-        __syncthreads();
-        if (threadIdx.x == 0) ts[1] = clock64();
-    }
-    // ---- right-looking panel factorisation (piv_seq).  The next pivot only needs lane j+1's own
-    //      d = a(j+1, j+1) - l(j+1, j)^2: every lane runs the rsq chain on its own value in VALU and
-    //      the result is read from lane j+1, interleaved with this pivot's rank-1 update.  A
+    // ---- right-looking panel factorisation (piv_seq): the next pivot only needs lane j+1's own
+    //      d = a(j+1, j+1) - l(j+1, j)^2, so every lane runs the rsq chain on its own value in VALU
+    //      and the result is read from lane j+1, interleaved with this pivot's rank-1 update.  A
     //      non-positive pivot turns into NaN and is flagged off the chain.  Lanes < k only touch
     //      their unused upper triangle.
-    if (fact) {
+    if (panel >= 0) {
         bool bad = lane == 0 && !(row[0] > 0.0);
         piv_seq<0>(row, readlane_d(rsqrt_nr(row[0]), 0), lane, bad);
-        if (wave == 0) {
-            if (lane < CNB) {
+        if (diag_item) {
+            const size_t p0 = (size_t)panel * CNB;
+            if (wave == 0) {
+                if (lane < CNB)   // diagonal block of L (row-major), zero upper part
 #pragma unroll
-                for (int c = 0; c < CNB; ++c) Lt[c][lane] = (c <= lane) ? row[c] : 0.0;
-            } else if (nt > 0) {
+                    for (int c = 0; c < CNB; ++c) Lm[(p0 + lane) * n + p0 + c] = (c <= lane) ? row[c] : 0.0;
+                if (__ballot(bad) != 0 && lane == 0) *info = 1 + (int)p0;
+            } else if (wave == 1 && lane == CNB) {
 #pragma unroll
-                for (int c = 0; c < CNB; ++c) Pi[l32][c] = row[c];
+                for (int c = 0; c < CNB; ++c) yv[p0 + c] = row[c];
+            } else if (wave == 2 && lane >= CNB) {   // row l32 of L_pp^-T
+                double* o = LinvT + p0 * CNB + (size_t)l32 * CNB;
+#pragma unroll
+                for (int c = 0; c < CNB; ++c) o[c] = row[c];
             }
-            if (__ballot(bad) != 0 && lane == 0 && blockIdx.x == 0) *info = 1 + p;
-        } else if (wave == 1) {
-            if (lane >= CNB) {
-                if (nt > 0 && tj != ti) {
+        } else if (lane >= CNB) {
+            const int hb = (wave >> 1) * 2;   // 0: panel A, 2: panel B
+            if ((wave & 1) == 0) {
 #pragma unroll
-                    for (int c = 0; c < CNB; ++c) Pj[l32][c] = row[c];
-                } else if (lane == CNB) {
+                for (int c = 0; c < CNB; ++c) Pt[hb][l32][c] = row[c];
+            } else if (tj != ti) {
 #pragma unroll
-                    for (int c = 0; c < CNB; ++c) yp[c] = row[c];
-                }
+                for (int c = 0; c < CNB; ++c) Pt[hb + 1][l32][c] = row[c];
+            } else if (lane == CNB) {
+#pragma unroll
+                for (int c = 0; c < CNB; ++c) yp[wave >> 1][c] = row[c];
             }
-        } else if (lane >= CNB) {   // wave 2 of workgroup 0: row l32 of L_pp^-T
-            double* o = LinvT + (size_t)p * CNB + (size_t)l32 * CNB;
-#pragma unroll
-            for (int c = 0; c < CNB; ++c) o[c] = row[c];
         }
     }
+    if (diag_item) return;
     __syncthreads();
-    if (ts && threadIdx.x == 0) ts[2] = clock64();
-    if (blockIdx.x == 0) {
-        for (int t = tid; t < CNB * CNB; t += 256) {   // diagonal block of L (row-major)
-            const int i = t / CNB, c = t % CNB;
-            Lm[(size_t)(p + i) * n + p + c] = Lt[c][i];
-        }
-        if (tid < CNB) yv[p + tid] = yp[tid];
-    }
-    if (nt == 0) {
-        if (ts) {
-            __builtin_amdgcn_s_waitcnt(0);
-            __syncthreads();
-            if (threadIdx.x == 0) ts[3] = clock64();
-        }
-        return;
-    }
-    // ---- trailing tile update A(ti, tj) -= Pi Pj^T
+    // ---- tile update A(i, j) -= sum over the step's panels of P_i P_j^T
     {
-        const double (*Qj)[CNB + 1] = (ti == tj) ? Pi : Pj;
         double s00 = 0, s01 = 0, s10 = 0, s11 = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (!(mask & (1 << h))) continue;
+            const double (*Pi)[CNB + 1] = Pt[2 * h];
+            const double (*Qj)[CNB + 1] = (ti == tj) ? Pt[2 * h] : Pt[2 * h + 1];
 #pragma unroll 8
-        for (int k = 0; k < CNB; ++k) {
-            const double x0 = Pi[2 * tr][k], x1 = Pi[2 * tr + 1][k];
-            const double y0 = Qj[2 * tc][k], y1 = Qj[2 * tc + 1][k];
-            s00 += x0 * y0; s01 += x0 * y1; s10 += x1 * y0; s11 += x1 * y1;
+            for (int k = 0; k < CNB; ++k) {
+                const double x0 = Pi[2 * tr][k], x1 = Pi[2 * tr + 1][k];
+                const double y0 = Qj[2 * tc][k], y1 = Qj[2 * tc + 1][k];
+                s00 += x0 * y0; s01 += x0 * y1; s10 += x1 * y0; s11 += x1 * y1;
+            }
         }
         A[ra * n + ca] = a00 - s00; A[ra * n + ca + 1] = a01 - s01;
         A[(ra + 1) * n + ca] = a10 - s10; A[(ra + 1) * n + ca + 1] = a11 - s11;
     }
-    // ---- the tj == 0 workgroups publish the panel rows of L (row-major)
-    if (tj == 0)
+    if (ti != tj) return;
+    // ---- diagonal tile: publish the tile's rows of L for each panel and forward-substitute b_i
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (!(mask & (1 << h))) continue;
+        const int pp = h ? pb : pa;
         for (int t = tid; t < CNB * CNB; t += 256) {
             const int i = t / CNB, c = t % CNB;
-            Lm[(size_t)(q + ti * CNB + i) * n + p + c] = Pi[i][c];
+            Lm[(size_t)(ti * CNB + i) * n + pp * CNB + c] = Pt[2 * h][i][c];
         }
-    // ---- forward substitution of the trailing right-hand side
-    if (ti == tj && tid < CNB) {
-        double s = 0.0;
-#pragma unroll 8
-        for (int c = 0; c < CNB; ++c) s += Pi[tid][c] * yp[c];
-        b[q + ti * CNB + tid] -= s;
     }
-    if (ts) {
-        __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
-        if (threadIdx.x == 0) ts[3] = clock64();
+    if (tid < CNB) {
+        double sum = 0.0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (!(mask & (1 << h))) continue;
+#pragma unroll 8
+            for (int c = 0; c < CNB; ++c) sum += Pt[2 * h][tid][c] * yp[h][c];
+        }
+        b[ti * CNB + tid] -= sum;
     }
 }
 
@@ -916,6 +946,7 @@ __global__ __launch_bounds__(BS_THREADS) void k_chol_backsolve(const double* __r
                                                                const double* __restrict__ yv,
                                                                double* __restrict__ out,
                                                                const int* __restrict__ pfirst,
+                                                               const int* __restrict__ pnat,
                                                                unsigned long long* tdbg) {
     __shared__ double y[CHOL_MAXN];
     __shared__ double Mb[2][CNB][CNB + 1];
@@ -945,7 +976,7 @@ __global__ __launch_bounds__(BS_THREADS) void k_chol_backsolve(const double* __r
                 }
                 const double xl = (s0 + s1) + (s2 + s3);
                 xb[lane] = xl;
-                out[r0 + lane] = xl;
+                out[pnat[blk] * CNB + lane] = xl;   // natural order
             }
             if (tdbg && tid == 0) tdbg[(size_t)blk * 16 + 1] = clock64();   // diagonal block done
         } else {
@@ -1166,7 +1197,7 @@ void launch_prior_lin(const DevProblem& P, const double* kst, hipStream_t s) {
     if (n) hipLaunchKernelGGL(k_prior_lin, dim3(n), dim3(64), 0, s, P, kst);
 }
 void launch_schur(const DevProblem& P, double lambda, hipStream_t s) {
-    if (P.n_tiles) hipLaunchKernelGGL(k_schur, dim3(P.n_tiles), dim3(256), 0, s, P, lambda);
+    if (P.n_tiles) hipLaunchKernelGGL(k_schur, dim3(P.n_tiles), dim3(SCHUR_THREADS), 0, s, P, lambda);
 }
 void launch_assemble(const DevProblem& P, double lambda, int flags, hipStream_t s) {
     const int n = P.n_asm + P.n_pb;
@@ -1175,13 +1206,13 @@ void launch_assemble(const DevProblem& P, double lambda, int flags, hipStream_t 
 void launch_cholesky_solve(const DevProblem& P, hipStream_t s) {
     const int n = P.npad;   // multiple of CHOL_NB (identity tail)
     if (n == 0) return;
-    for (int p = 0; p < n; p += CHOL_NB) {
-        const int nt = (n - p - CHOL_NB) / CHOL_NB;
-        hipLaunchKernelGGL(k_chol_step, dim3(nt ? nt * (nt + 1) / 2 : 1), dim3(256), 0, s, n, p, P.S, P.Lm, P.LinvT,
-                           P.xsol, P.yv, P.info, P.pfirst, P.tdbg_chol);
+    for (int st = 0; st < P.n_steps; ++st) {
+        const int* h = P.h_steps + 4 * st;
+        hipLaunchKernelGGL(k_chol_step, dim3(h[3] - h[2]), dim3(256), 0, s, n, h[0], h[1], h[2], P.chol_items, P.S,
+                           P.Lm, P.LinvT, P.xsol, P.yv, P.info);
     }
     hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(BS_THREADS), 0, s, P.Lm, P.LinvT, n, P.yv, P.xsol, P.pfirst,
-                       P.tdbg_bs);
+                       P.pnat, P.tdbg_bs);
 }
 void launch_update(const DevProblem& P, double lambda, const double* kst, const double* lst, double* kst_out,
                    double* lst_out, hipStream_t s) {

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "amc-slam_amd"))
 
 LIN_PHASES = ["obs residual+J -> LDS", "Hpp segments", "Hpl pairs", "Hll/bl"]
-SCHUR_PHASES = ["stage Hpl + lists + Dinv", "slot map", "S partials (MFMA)", "-", "rhs partials"]
+SCHUR_PHASES = ["stage Hpl + lists + Dinv", "slot map + V", "S partials (MFMA)", "-", "rhs partials"]
 SHAPE = ["nobs", "nseg", "npair", "nlm", "nsent", "nkf"]
 
 
