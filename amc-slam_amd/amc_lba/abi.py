@@ -77,6 +77,7 @@ class LbaStats(ctypes.Structure):
 # lba_config.flags (include/amc_lba.h)
 FLAG_TIME_SWEEP = 1
 FLAG_TIME_PHASES = 2
+FLAG_HOST_LOOP = 4         # host-driven LM loop (default: queued trials decided on the device)
 
 
 def make_config(qc_diag=(0.02, 0.02, 0.02, 0.002, 0.002, 0.002), huber_mono=None, huber_stereo=None,

@@ -46,6 +46,36 @@ constexpr int TGT_STRIDE = 4;       // staged target record: flags | nrun << 8, 
 constexpr int CHOL_NB = 32;         // Cholesky panel / tile width
 constexpr int RED_GROUPS = 4;       // reduction kernels: 4 groups x 144 threads
 
+// Levenberg-Marquardt controller of a queued optimisation (lba_host.hip: optimize_queued).  The host
+// enqueues whole trials without waiting for their outcome; k_finalize applies g2o's acceptance rule
+// (optimization_algorithm_levenberg.cpp:56-140) to this record, and the kernels of the next trial read
+// from it which state buffer is current, the damping, and whether they run at all.
+struct LMCtl {
+    double lambda, ni;
+    double cur_chi, ini_chi;   // currentChi / iniChi of the iteration in progress
+    double last_chi;           // chi2 of the last evaluated trial state (g2o's activeRobustChi2)
+    double chi0;               // chi2 of the starting state (lba_stats.chi2_initial)
+    int cur;                   // state buffer holding the current estimate (the other one: trial)
+    int qmax;                  // trials of the iteration in progress
+    int it, iters;             // iterations completed / requested
+    int done;                  // 1: every further kernel of the queue is a no-op
+    int need_lin;              // 1: the next trial starts a new iteration (relinearise first)
+    int nbad, trials, failures, result;
+    int max_trials, early_stop;
+    int slot;                  // trials finalised (queue position)
+    int pad2;
+};
+constexpr int LMCTL_DOUBLES = sizeof(LMCtl) / sizeof(double);
+static_assert(sizeof(LMCtl) % sizeof(double) == 0, "LMCtl mirrors into a double array");
+
+// state-buffer selection of a launch: a fixed buffer (host-driven trials), or the controller's
+// current / trial buffer (queued trials)
+enum { SEL_CUR = 2, SEL_NEXT = 3 };
+// launch gating in a queued optimisation: run always, unless the queue is done, or only when the
+// trial starts a new iteration
+enum { GATE_NONE = 0, GATE_TRIAL = 1, GATE_LIN = 2 };
+constexpr double LAMBDA_CTL = -1.0;   // lambda argument: take the controller's damping
+
 struct DevProblem {
     int n_kf, n_lm, n_obs, n_gp, n_pairs, n_tiles, n_pb, np, n_prior, n_vel, n_cam;
     int npad;               // np rounded up to CHOL_NB: leading dimension of S / Lm (identity tail)
@@ -158,6 +188,10 @@ struct DevProblem {
     double* chi_eval;       // [n_tiles + n_prior + n_vel]
     double* scale_part;     // [n_upd_blocks]
     int n_upd_blocks;
+    double* kbuf[2];        // kf state buffers [n_kf][KF_STRIDE] (current / trial, see LMCtl::cur)
+    double* lbuf[2];        // landmark state buffers [n_lm][3]
+    LMCtl* ctl;             // queued-optimisation controller
+    int* hlog;              // host-mapped [HLOG_CAP]: per queued trial, 1 if it relinearised
     int* info;              // [1] factorisation status
     double* fin;            // [4] chi_lin, chi_eval, scale, info
     double* hfin;           // host-mapped coherent [4] copy of fin + [4] sequence number (as bits)
@@ -170,19 +204,23 @@ struct DevProblem {
     unsigned long long* tdbg_bs;      // [npad / CHOL_NB][16] k_chol_backsolve (per block)
 };
 
-// launchers (lba_kernels.hip)
-void launch_gp_prep(const DevProblem& P, const double* kst, int jac, hipStream_t s);
-void launch_linearize(const DevProblem& P, const double* kst, const double* lst, int write_res, hipStream_t s);
-void launch_prior_lin(const DevProblem& P, const double* kst, hipStream_t s);
-void launch_schur(const DevProblem& P, double lambda, hipStream_t s);
+// launchers (lba_kernels.hip).  sel: state buffer (0 / 1, or SEL_CUR / SEL_NEXT from the controller);
+// gate: GATE_*; lambda: the damping, or LAMBDA_CTL
+constexpr int HLOG_CAP = 4096;
+void launch_gp_prep(const DevProblem& P, int sel, int jac, int gate, hipStream_t s);
+void launch_linearize(const DevProblem& P, int sel, int write_res, int gate, hipStream_t s);
+void launch_prior_lin(const DevProblem& P, int sel, int gate, hipStream_t s);
+void launch_schur(const DevProblem& P, double lambda, int gate, hipStream_t s);
 enum { ASM_SCHUR = 1, ASM_FULL = 2 };
-void launch_assemble(const DevProblem& P, double lambda, int flags, hipStream_t s);
-void launch_cholesky_solve(const DevProblem& P, hipStream_t s);
-void launch_update(const DevProblem& P, double lambda, const double* kst, const double* lst, double* kst_out,
-                   double* lst_out, hipStream_t s);
-void launch_eval(const DevProblem& P, const double* kst, const double* lst, hipStream_t s);
-void launch_finalize(const DevProblem& P, unsigned long long seq, hipStream_t s);
-void launch_depth(const DevProblem& P, const double* kst, const double* lst, unsigned char* ok, hipStream_t s);
+void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hipStream_t s);
+void launch_cholesky_solve(const DevProblem& P, int gate, hipStream_t s);
+void launch_update(const DevProblem& P, double lambda, int sel, int gate, hipStream_t s);
+void launch_eval(const DevProblem& P, int sel, int gate, hipStream_t s);
+enum { FIN_HOST = 0, FIN_QUEUED = 1, FIN_QUEUED_PUBLISH = 2, FIN_INITIAL = 3 };
+void launch_finalize(const DevProblem& P, unsigned long long seq, int mode, hipStream_t s);
+void launch_ctl_init(const DevProblem& P, const LMCtl& c, hipStream_t s);
+void launch_lambda_init(const DevProblem& P, double tau, hipStream_t s);
+void launch_depth(const DevProblem& P, int sel, unsigned char* ok, hipStream_t s);
 
 constexpr int GPS_STRIDE = 156;     // doubles in lba::GPSample (static_assert in lba_kernels.hip)
 

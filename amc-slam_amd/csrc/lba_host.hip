@@ -45,8 +45,12 @@ struct lba_problem {
     double* lst[2] = {nullptr, nullptr};
     int cur = 0;
     std::vector<void*> allocs;
-    double* h_fin = nullptr;      // host-mapped coherent [8]: trial summary [4] + sequence number
+    double* h_fin = nullptr;      // host-mapped coherent [HFIN_DOUBLES]: trial summary [4], sequence
+                                  // number [4], LMCtl mirror [8..] (queued optimisation)
     double* d_hfin = nullptr;     // its device address
+    int* h_log = nullptr;         // host-mapped [HLOG_CAP]: per queued trial, 1 if it relinearised
+    int* d_hlog = nullptr;
+    std::vector<hipEvent_t> qev;  // queued optimisation, LBA_FLAG_TIME_SWEEP: 2 events per trial
     std::vector<int> chol_steps;  // dense-solve schedule: (panel A, panel B, first item, end item) per step
     int s_layout = 0;             // layout last assembled into S: 0 factorisation order, 1 natural (full)
     unsigned long long fin_seq = 0;
@@ -55,6 +59,8 @@ struct lba_problem {
 };
 
 namespace {
+
+constexpr int HFIN_DOUBLES = 8 + LMCTL_DOUBLES;
 
 struct HipError {
     hipError_t e;
@@ -617,6 +623,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.pair_rows = dupload(p, pair_rows); D.lm_r0 = dupload(p, lm_r0); D.lm_rows = dupload(p, lm_rows);
     D.lm_pair0 = dupload(p, lm_pair0);
     D.hfin = p->d_hfin;
+    D.hlog = p->d_hlog;
     if (std::getenv("LBA_PHASE_TIMING")) {
         D.tdbg_lin = dalloc<unsigned long long>(p, (size_t)n_tiles * 16);
         D.tdbg_schur = dalloc<unsigned long long>(p, (size_t)n_tiles * 16);
@@ -753,6 +760,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     if (D.n_upd_blocks == 0) D.n_upd_blocks = 1;
     D.scale_part = dalloc<double>(p, D.n_upd_blocks);
     D.info = dalloc<int>(p, 1);
+    D.ctl = dalloc<LMCtl>(p, 1);
     D.fin = dalloc<double>(p, 4);
     D.ob_chi2 = dalloc<double>(p, std::max(n_obs, 1));
     D.ob_res = dalloc<double>(p, 3 * (size_t)std::max(n_obs, 1));
@@ -762,7 +770,10 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         p->lst[s] = dalloc<double>(p, lst.size());
         HIPCHK(hipMemcpy(p->kst[s], kst.data(), kst.size() * sizeof(double), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(p->lst[s], lst.data(), lst.size() * sizeof(double), hipMemcpyHostToDevice));
+        D.kbuf[s] = p->kst[s];
+        D.lbuf[s] = p->lst[s];
     }
+    HIPCHK(hipMemset(D.ctl, 0, sizeof(LMCtl)));
     p->cur = 0;
     p->has_problem = true;
     p->linearized = false;
@@ -772,23 +783,17 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
 // ------------------------------------------------------------------------------------------------
 void linearize(lba_problem* p, int write_res, bool timed = false) {
     const DevProblem& D = p->D;
-    launch_gp_prep(D, p->kst[p->cur], 1, p->stream);
+    launch_gp_prep(D, p->cur, 1, GATE_NONE, p->stream);
     if (timed) HIPCHK(hipEventRecord(p->ev[6], p->stream));
-    launch_linearize(D, p->kst[p->cur], p->lst[p->cur], write_res, p->stream);
+    launch_linearize(D, p->cur, write_res, GATE_NONE, p->stream);
     if (timed) HIPCHK(hipEventRecord(p->ev[7], p->stream));
-    launch_prior_lin(D, p->kst[p->cur], p->stream);
+    launch_prior_lin(D, p->cur, GATE_NONE, p->stream);
     HIPCHK(hipGetLastError());
     p->linearized = true;
 }
 
-// Publish the trial summary (k_finalize writes it into host-mapped memory) and wait for it by
-// polling its sequence number; the stream is queried now and then so a device fault is reported
-// instead of spinning forever.  sync: also synchronise the stream (callers that copy device
-// buffers afterwards, or read timing events).
-void finalize_and_wait(lba_problem* p, bool sync) {
-    const unsigned long long seq = ++p->fin_seq;
-    launch_finalize(p->D, seq, p->stream);
-    HIPCHK(hipGetLastError());
+// poll the published sequence number (see finalize_and_wait)
+void wait_seq(lba_problem* p, unsigned long long seq) {
     volatile unsigned long long* flag = reinterpret_cast<volatile unsigned long long*>(p->h_fin + 4);
     for (unsigned it = 1; *flag != seq; ++it) {
         if ((it & 1023) == 0) {
@@ -798,33 +803,45 @@ void finalize_and_wait(lba_problem* p, bool sync) {
         }
     }
     std::atomic_thread_fence(std::memory_order_acquire);
+}
+
+// Publish the trial summary (k_finalize writes it into host-mapped memory) and wait for it by
+// polling its sequence number; the stream is queried now and then so a device fault is reported
+// instead of spinning forever.  sync: also synchronise the stream (callers that copy device
+// buffers afterwards, or read timing events).
+void finalize_and_wait(lba_problem* p, bool sync) {
+    const unsigned long long seq = ++p->fin_seq;
+    launch_finalize(p->D, seq, 0, p->stream);
+    HIPCHK(hipGetLastError());
+    wait_seq(p, seq);
     if (sync) HIPCHK(hipStreamSynchronize(p->stream));
 }
+
 
 // S holds either the factorisation-order lower triangle (trials) or the natural full matrix
 // (ASM_FULL: lba_linearize / lambda init); switching layouts clears it first, since each layout only
 // rewrites its own pattern
-void assemble_layout(lba_problem* p, double lambda, int flags) {
+void assemble_layout(lba_problem* p, double lambda, int flags, int gate = GATE_NONE) {
     const int want = (flags & ASM_FULL) ? 1 : 0;
     if (want != p->s_layout || want == 1)
         HIPCHK(hipMemsetAsync(p->D.S, 0, sizeof(double) * ((size_t)p->D.npad * p->D.npad), p->stream));
     p->s_layout = want;
-    launch_assemble(p->D, lambda, flags, p->stream);
+    launch_assemble(p->D, lambda, flags, gate, p->stream);
 }
 
 // one damped solve + update into the trial buffers + evaluation of the trial state
 void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs, bool sync = true) {
     const DevProblem& D = p->D;
     const int nx = 1 - p->cur;
-    launch_schur(D, lambda, p->stream);   // also clears the factorisation status
+    launch_schur(D, lambda, GATE_NONE, p->stream);   // also clears the factorisation status
     assemble_layout(p, lambda, ASM_SCHUR);
     if (evs) HIPCHK(hipEventRecord(evs[0], p->stream));
-    launch_cholesky_solve(D, p->stream);
+    launch_cholesky_solve(D, GATE_NONE, p->stream);
     if (evs) HIPCHK(hipEventRecord(evs[1], p->stream));
-    launch_update(D, lambda, p->kst[p->cur], p->lst[p->cur], p->kst[nx], p->lst[nx], p->stream);
+    launch_update(D, lambda, p->cur, GATE_NONE, p->stream);
     if (evaluate) {
-        launch_gp_prep(D, p->kst[nx], 0, p->stream);
-        launch_eval(D, p->kst[nx], p->lst[nx], p->stream);
+        launch_gp_prep(D, nx, 0, GATE_NONE, p->stream);
+        launch_eval(D, nx, GATE_NONE, p->stream);
     }
     if (evs) HIPCHK(hipEventRecord(evs[2], p->stream));
     finalize_and_wait(p, sync || evs);
@@ -832,8 +849,8 @@ void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs, bool s
 
 double eval_current(lba_problem* p) {
     const DevProblem& D = p->D;
-    launch_gp_prep(D, p->kst[p->cur], 0, p->stream);
-    launch_eval(D, p->kst[p->cur], p->lst[p->cur], p->stream);
+    launch_gp_prep(D, p->cur, 0, GATE_NONE, p->stream);
+    launch_eval(D, p->cur, GATE_NONE, p->stream);
     finalize_and_wait(p, true);
     return p->h_fin[1];
 }
@@ -861,10 +878,108 @@ float elapsed(hipEvent_t a, hipEvent_t b) {
     return ms;
 }
 
+// Queued optimisation: the same iterations as the host-driven loop in optimize() below, but the LM
+// decisions are taken on the device (k_finalize / lm_decide on the LMCtl record), so the host enqueues
+// one trial per remaining iteration without waiting for any outcome, and synchronises once per batch.
+// Launches of a queued trial take their state buffer and damping from the controller; the
+// relinearisation kernels only run when the previous trial ended an iteration (a rejected trial keeps
+// the linearisation), and k_update is a no-op once the controller is done (the other kernels of such
+// a trial only touch scratch buffers).  A batch is one trial per iteration still to run, which is exact
+// when every trial is accepted; after rejected trials the next batch covers the rest (a trial
+// completes at most one iteration and an iteration takes at most max_trials trials, so this
+// terminates).  The starting-state evaluation and computeLambdaInit run in the queue too.
+int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
+    lba_stats s{};
+    const auto t0 = std::chrono::steady_clock::now();
+    const DevProblem& D = p->D;
+    const bool tsweep = (p->cfg.flags & LBA_FLAG_TIME_SWEEP) != 0;
+    LMCtl c{};
+    c.lambda = p->cfg.lambda_init > 0 ? p->cfg.lambda_init : 0.0;
+    c.ni = 2.0;
+    c.cur = p->cur;
+    c.iters = iters;
+    c.need_lin = 1;
+    c.max_trials = p->cfg.max_trials;
+    c.early_stop = p->cfg.early_stop;
+    c.result = LBA_RESULT_OK;
+    launch_ctl_init(D, c, p->stream);
+    // starting state: poses + GP samples (with the Jacobian factors the first linearisation uses), chi2
+    launch_gp_prep(D, p->cur, 1, GATE_NONE, p->stream);
+    launch_eval(D, p->cur, GATE_NONE, p->stream);
+    launch_finalize(D, 0, FIN_INITIAL, p->stream);
+    int issued = 0;
+    const LMCtl* hc = reinterpret_cast<const LMCtl*>(p->h_fin + 8);
+    while (true) {
+        const int n = iters - c.it;
+        const int first = issued;
+        const auto te0 = std::chrono::steady_clock::now();
+        for (int k = 0; k < n; ++k, ++issued) {
+            // LBA_FLAG_TIME_SWEEP: events bracket the first k_linearize launch of the call (it always
+            // relinearises); one launch per call keeps the timing overhead off the loop
+            const bool tq = tsweep && issued == 0;
+            if (tq && (size_t)issued * 2 + 2 > p->qev.size()) {
+                const size_t old = p->qev.size();
+                p->qev.resize(std::max<size_t>(2 * (size_t)issued + 2, 2 * old));
+                for (size_t e = old; e < p->qev.size(); ++e) HIPCHK(hipEventCreate(&p->qev[e]));
+            }
+            if (issued > 0) launch_gp_prep(D, SEL_CUR, 1, GATE_LIN, p->stream);
+            if (tq) HIPCHK(hipEventRecord(p->qev[2 * issued], p->stream));
+            launch_linearize(D, SEL_CUR, 0, GATE_LIN, p->stream);
+            if (tq) HIPCHK(hipEventRecord(p->qev[2 * issued + 1], p->stream));
+            launch_prior_lin(D, SEL_CUR, GATE_LIN, p->stream);
+            if (issued == 0 && p->cfg.lambda_init <= 0) {
+                assemble_layout(p, 0.0, ASM_FULL);
+                launch_lambda_init(D, p->cfg.tau, p->stream);
+            }
+            launch_schur(D, LAMBDA_CTL, GATE_NONE, p->stream);
+            assemble_layout(p, LAMBDA_CTL, ASM_SCHUR);
+            launch_cholesky_solve(D, GATE_NONE, p->stream);
+            launch_update(D, LAMBDA_CTL, SEL_CUR, GATE_TRIAL, p->stream);
+            launch_gp_prep(D, SEL_NEXT, 0, GATE_NONE, p->stream);
+            launch_eval(D, SEL_NEXT, GATE_NONE, p->stream);
+            launch_finalize(D, ++p->fin_seq, k == n - 1 ? FIN_QUEUED_PUBLISH : FIN_QUEUED, p->stream);
+            HIPCHK(hipGetLastError());
+        }
+        if (std::getenv("LBA_ENQ_TIMING"))
+            std::fprintf(stderr, "enqueue %d trials: %.1f us/trial\n", n,
+                         std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - te0).count() /
+                             std::max(n, 1));
+        wait_seq(p, p->fin_seq);
+        std::memcpy(&c, hc, sizeof(LMCtl));
+        if (tsweep) {
+            HIPCHK(hipStreamSynchronize(p->stream));
+            for (int q = first; q < issued && q < HLOG_CAP; ++q)
+                if (p->h_log[q]) {
+                    s.ms_k_linearize += elapsed(p->qev[2 * q], p->qev[2 * q + 1]);
+                    s.n_k_linearize += 1;
+                }
+        }
+        if (c.done || n <= 0) break;
+    }
+    HIPCHK(hipStreamSynchronize(p->stream));
+    p->cur = c.cur;
+    p->lambda = c.lambda;
+    p->ni = c.ni;
+    p->nBad = c.nbad;
+    p->linearized = false;
+    s.chi2_initial = c.chi0;
+    s.iterations = c.it;
+    s.trials = c.trials;
+    s.solve_failures = c.failures;
+    s.result = c.result;
+    s.chi2_final = c.last_chi;
+    s.lambda_final = c.lambda;
+    s.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (st) *st = s;
+    return c.it;
+}
+
 int optimize(lba_problem* p, int iters, volatile const int32_t* stop, lba_stats* st) {
     if (!p->has_problem) throw ApiError{LBA_E_ARG, "no problem set"};
     lba_stats s{};
     if (p->np + 3 * p->n_lm_dev == 0) throw ApiError{LBA_E_EMPTY, "0 vertices to optimize"};
+    if (!stop && iters > 0 && !(p->cfg.flags & (LBA_FLAG_TIME_PHASES | LBA_FLAG_HOST_LOOP)))
+        return optimize_queued(p, iters, st);
     const auto t0 = std::chrono::steady_clock::now();
     s.chi2_initial = eval_current(p);
     double last_chi = s.chi2_initial;
@@ -907,7 +1022,8 @@ int optimize(lba_problem* p, int iters, volatile const int32_t* stop, lba_stats*
             const double scale = p->h_fin[2] + 1e-3;
             rho /= scale;
             if (rho > 0 && std::isfinite(tempChi)) {
-                double alpha = 1. - std::pow((2 * rho - 1), 3);
+                const double t3 = 2 * rho - 1;   // (2 rho - 1)^3 as in lm_decide (lba_kernels.hip)
+                double alpha = 1. - t3 * t3 * t3;
                 alpha = std::min(alpha, 2. / 3.);
                 const double sf = std::max(1. / 3., alpha);
                 p->lambda *= sf;
@@ -973,10 +1089,14 @@ int lba_create(lba_problem** out, const lba_config* cfg) {
         HIPCHK(hipSetDevice(cfg->device));
         HIPCHK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
         for (auto& e : p->ev) HIPCHK(hipEventCreate(&e));
-        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&p->h_fin), 8 * sizeof(double),
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&p->h_fin), HFIN_DOUBLES * sizeof(double),
                              hipHostMallocMapped | hipHostMallocCoherent));
-        for (int i = 0; i < 8; ++i) p->h_fin[i] = 0.0;
+        for (int i = 0; i < HFIN_DOUBLES; ++i) p->h_fin[i] = 0.0;
         HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->d_hfin), p->h_fin, 0));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&p->h_log), HLOG_CAP * sizeof(int),
+                             hipHostMallocMapped | hipHostMallocCoherent));
+        for (int i = 0; i < HLOG_CAP; ++i) p->h_log[i] = 0;
+        HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->d_hlog), p->h_log, 0));
     } catch (const HipError& e) {
         delete p;
         return LBA_E_HIP;
@@ -992,7 +1112,10 @@ void lba_destroy(lba_problem* p) {
     free_all(p);
     for (auto& e : p->ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto& e : p->qev)
+        if (e) (void)hipEventDestroy(e);
     if (p->h_fin) (void)hipHostFree(p->h_fin);
+    if (p->h_log) (void)hipHostFree(p->h_log);
     if (p->stream) (void)hipStreamDestroy(p->stream);
     delete p;
 }
@@ -1113,7 +1236,7 @@ int lba_eval(lba_problem* p, double* chi2_robust, double* obs_chi2, uint8_t* dep
         if (depth_ok && p->n_obs) {
             unsigned char* d = nullptr;
             HIPCHK(hipMalloc(&d, p->n_obs));
-            launch_depth(p->D, p->kst[p->cur], p->lst[p->cur], d, p->stream);
+            launch_depth(p->D, p->cur, d, p->stream);
             std::vector<unsigned char> h(p->n_obs);
             HIPCHK(hipMemcpyAsync(h.data(), d, p->n_obs, hipMemcpyDeviceToHost, p->stream));
             HIPCHK(hipStreamSynchronize(p->stream));

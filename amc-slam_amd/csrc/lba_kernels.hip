@@ -19,6 +19,7 @@
 //   k_eval           residuals / robust chi2 of the trial state           (sparse_optimizer.cpp:61-114)
 // All cross-workgroup sums are written as per-workgroup partials and reduced in a fixed order, so
 // results are bitwise reproducible run to run (no floating-point atomics).
+#include <cfloat>
 #include <utility>
 
 #include "lba_device.hpp"
@@ -40,6 +41,17 @@ static_assert(sizeof(GPSample) == GPS_STRIDE * sizeof(double), "GPSample layout 
     } while (0)
 
 typedef double d4 __attribute__((ext_vector_type(4)));   // v_mfma_f64_16x16x4 accumulator
+
+// queued optimisation (LMCtl): the state buffer a launch works on, whether it runs, its damping
+__device__ __forceinline__ int state_idx(const DevProblem& P, int sel) {
+    return sel < SEL_CUR ? sel : (P.ctl->cur ^ (sel - SEL_CUR));
+}
+__device__ __forceinline__ bool gated_off(const LMCtl* c, int gate) {
+    return gate != GATE_NONE && (c->done || (gate == GATE_LIN && !c->need_lin));
+}
+__device__ __forceinline__ double damping(const DevProblem& P, double lambda) {
+    return lambda < 0.0 ? P.ctl->lambda : lambda;
+}
 
 __device__ __forceinline__ SE3 load_se3(const double* k) {
     SE3 T;
@@ -154,9 +166,11 @@ __device__ __forceinline__ double eval_obs(const DevProblem& P, const double* ks
 // then one lane per sample of that pair evaluates the interpolated pose and (jac) the Jacobian
 // factor N.  Trailing workgroups write the KF poses used by the non-GP edges.
 constexpr int PREP_THREADS = 64;
-__global__ __launch_bounds__(PREP_THREADS) void k_gp_prep(DevProblem P, const double* __restrict__ kst, int jac) {
+__global__ __launch_bounds__(PREP_THREADS) void k_gp_prep(DevProblem P, int sel, int jac, int gate) {
     __shared__ GPPair pr;
     const int tid = threadIdx.x;
+    if (gated_off(P.ctl, gate)) return;
+    const double* __restrict__ kst = P.kbuf[state_idx(P, sel)];
     if ((int)blockIdx.x < P.n_gp) {
         const int i = blockIdx.x;
         if (tid == 0) {
@@ -259,8 +273,7 @@ __device__ __forceinline__ void tgt_task(const DevProblem& P, const double* rows
     }
 }
 
-__global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, const double* __restrict__ kst,
-                                                        const double* __restrict__ lst, int write_res) {
+__global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, int write_res, int gate) {
     __shared__ double rows[TILE_ROWS * ROW_STRIDE];
     __shared__ double rw[TILE_ROWS];
     __shared__ int tgtm[TILE_TGT * TGT_STRIDE];
@@ -276,6 +289,10 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, const doub
     const int tg0 = P.tile_tgt0[tile], ntg = P.tile_ntgt[tile];
     const int pair0 = P.tile_pair0[tile], npair = P.tile_npair[tile];
     const int lm0 = P.tile_lm0[tile], nlm = P.tile_nlm[tile];
+    if (gated_off(P.ctl, gate)) return;
+    const int si = state_idx(P, sel);
+    const double* __restrict__ kst = P.kbuf[si];
+    const double* __restrict__ lst = P.lbuf[si];
     LBA_TMARK(P.tdbg_lin, 0);
 
     // ---- stage the tile's index lists in LDS (fixed-count loops: all loads issue before the stores)
@@ -396,10 +413,12 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, const doub
 }
 
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_prior_lin(DevProblem P, const double* __restrict__ kst) {
+__global__ __launch_bounds__(64) void k_prior_lin(DevProblem P, int sel, int gate) {
     __shared__ double Ji[144], Jj[144], WJi[144], WJj[144], Om[144], e[12], We[12];
     __shared__ double wsh;
     const int idx = blockIdx.x, tid = threadIdx.x;
+    if (gated_off(P.ctl, gate)) return;
+    const double* __restrict__ kst = P.kbuf[state_idx(P, sel)];
     const int ent = P.pri_entry0 + idx;
     const int* sl = P.seg_slot + 5 * (size_t)ent;
     const int* gl = P.seg_gslot + 2 * (size_t)ent;
@@ -478,7 +497,7 @@ __global__ __launch_bounds__(64) void k_prior_lin(DevProblem P, const double* __
 // factorisation status for the solve that follows, and the first blocks zero the envelope of S.
 constexpr int SCHUR_THREADS = 512;
 
-__global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double lambda) {
+__global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double lambda_arg, int gate) {
     __shared__ double Hs[TILE_PAIRS * 36];
     __shared__ double Vs[TILE_PAIRS * 36];
     __shared__ double Dl[TILE_LMS * 12];   // Dinv (9) + bl (3) per landmark
@@ -493,6 +512,8 @@ __global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double la
     const int lm0 = P.tile_lm0[tile], nlm = P.tile_nlm[tile];
     const int kf0 = P.tile_kf0[tile], nkf = P.tile_nkf[tile];
     const int sent0 = P.tile_sent0[tile], nsent = P.tile_nsent[tile];
+    if (gated_off(P.ctl, gate)) return;
+    const double lambda = damping(P, lambda_arg);
     LBA_TMARK(P.tdbg_schur, 0);
     if (tile == 0 && tid == 0) *P.info = 0;
     // clear the envelope tiles of S for this trial's assembly (the previous factorisation left its
@@ -614,9 +635,11 @@ __global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double la
 //   S(bi, bj) = sum Hpp partials + lambda I (diagonal) - sum Schur partials   (block_solver.hpp:432-445,
 //   setLambda :573-579), only for the blocks inside the structural pattern (the rest of S is zero
 //   from the upload and never written);  b_p = sum b partials;  bS = b_p - sum Schur rhs partials.
-__global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, double lambda, int flags) {
+__global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, double lambda_arg, int flags, int gate) {
     __shared__ double red[144 * RED_GROUPS];
     const int tid = threadIdx.x;
+    if (gated_off(P.ctl, gate)) return;
+    const double lambda = damping(P, lambda_arg);
     const int n = P.npad;   // leading dimension of S
     if ((int)blockIdx.x < P.n_asm) {
         const int ub = P.asm_list[blockIdx.x];
@@ -821,11 +844,13 @@ __device__ __forceinline__ void load_stacked(const double* __restrict__ A, const
 __global__ __launch_bounds__(256) void k_chol_step(int n, int pa, int pb, int it0, const int* __restrict__ items,
                                                    double* __restrict__ A, double* __restrict__ Lm,
                                                    double* __restrict__ LinvT, double* __restrict__ b,
-                                                   double* __restrict__ yv, int* info) {
+                                                   double* __restrict__ yv, int* info, const LMCtl* ctl,
+                                                   int gate) {
     __shared__ double stg[4][2 * CNB][CNB + 1];   // per factoring wave: its stacked panel, row-major
     __shared__ double Pt[4][CNB][CNB + 1];        // factored tile rows: [panel A i, panel A j, panel B i, panel B j]
     __shared__ double yp[2][CNB];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & (CNB - 1);
+    if (gated_off(ctl, gate)) return;
     const int it = items[it0 + blockIdx.x];
     const int ti = it & 1023, tj = (it >> 10) & 1023, mask = (it >> 20) & 3;
     const bool diag_item = (it >> 22) & 1;
@@ -947,13 +972,15 @@ __global__ __launch_bounds__(BS_THREADS) void k_chol_backsolve(const double* __r
                                                                double* __restrict__ out,
                                                                const int* __restrict__ pfirst,
                                                                const int* __restrict__ pnat,
-                                                               unsigned long long* tdbg) {
+                                                               unsigned long long* tdbg, const LMCtl* ctl,
+                                                               int gate) {
     __shared__ double y[CHOL_MAXN];
     __shared__ double Mb[2][CNB][CNB + 1];
     __shared__ double xb[CNB];
     const int tid = threadIdx.x, lane = tid & 63;
     const int nblk = n / CNB;
     const int k0 = tid - 64;
+    if (gated_off(ctl, gate)) return;
     for (int t = tid; t < n; t += BS_THREADS) y[t] = yv[t];
     for (int t = tid; t < CNB * CNB; t += BS_THREADS)
         Mb[(nblk - 1) & 1][t / CNB][t % CNB] = LinvT[(size_t)(nblk - 1) * CNB * CNB + t];
@@ -1028,10 +1055,15 @@ __global__ __launch_bounds__(BS_THREADS) void k_chol_backsolve(const double* __r
 // ------------------------------------------------------------------------------------------------
 constexpr int UPD_THREADS = 256;
 
-__global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lambda, const double* __restrict__ kst,
-                                                        const double* __restrict__ lst, double* __restrict__ ko,
-                                                        double* __restrict__ lo) {
+__global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lambda_arg, int sel, int gate) {
     __shared__ double red[UPD_THREADS / 64];
+    if (gated_off(P.ctl, gate)) return;
+    const double lambda = damping(P, lambda_arg);
+    const int si = state_idx(P, sel);
+    const double* __restrict__ kst = P.kbuf[si];
+    const double* __restrict__ lst = P.lbuf[si];
+    double* __restrict__ ko = P.kbuf[si ^ 1];
+    double* __restrict__ lo = P.lbuf[si ^ 1];
     const int i = blockIdx.x * UPD_THREADS + threadIdx.x;
     const bool ok = (*P.info == 0);
     double sc = 0.0;
@@ -1088,10 +1120,13 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
 }
 
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(TILE_OBS) void k_eval(DevProblem P, const double* __restrict__ kst,
-                                                   const double* __restrict__ lst) {
+__global__ __launch_bounds__(TILE_OBS) void k_eval(DevProblem P, int sel, int gate) {
     __shared__ double red[TILE_OBS / 64];
     const int tile = blockIdx.x, tid = threadIdx.x;
+    if (gated_off(P.ctl, gate)) return;
+    const int si = state_idx(P, sel);
+    const double* __restrict__ kst = P.kbuf[si];
+    const double* __restrict__ lst = P.lbuf[si];
     double rho0 = 0.0;
     if (tid < P.tile_nobs[tile]) {
         const int o = P.tile_obs0[tile] + tid;
@@ -1105,8 +1140,10 @@ __global__ __launch_bounds__(TILE_OBS) void k_eval(DevProblem P, const double* _
     if (tid == 0) P.chi_eval[tile] = s;
 }
 
-__global__ __launch_bounds__(64) void k_prior_eval(DevProblem P, const double* __restrict__ kst) {
+__global__ __launch_bounds__(64) void k_prior_eval(DevProblem P, int sel, int gate) {
     const int idx = blockIdx.x * 64 + threadIdx.x;
+    if (gated_off(P.ctl, gate)) return;
+    const double* __restrict__ kst = P.kbuf[state_idx(P, sel)];
     if (idx < P.n_prior) {
         const double* ka = kst + (size_t)P.pri_a[idx] * KF_STRIDE;
         const double* kb = kst + (size_t)P.pri_b[idx] * KF_STRIDE;
@@ -1133,7 +1170,56 @@ __global__ __launch_bounds__(64) void k_prior_eval(DevProblem P, const double* _
 // status.  Besides the device copy it is published straight into host-mapped coherent memory,
 // followed (after a system-scope fence) by the trial's sequence number, which the host polls:
 // no copy kernel and no stream synchronisation per trial.
-__global__ __launch_bounds__(256) void k_finalize(DevProblem P, unsigned long long seq) {
+// queued: also take the LM decision of this trial on the device controller (the host-driven loop in
+// lba_host.hip: optimize, i.e. OptimizationAlgorithmLevenberg::solve,
+// optimization_algorithm_levenberg.cpp:61-169, and SparseOptimizer::optimize's iteration loop,
+// sparse_optimizer.cpp:360-400), log whether the trial relinearised, and publish the controller.
+__device__ void lm_decide(LMCtl& c, double chi_lin, double chi_trial, double scale, bool solved, int* hlog) {
+    if (hlog) hlog[c.slot % HLOG_CAP] = (!c.done && c.need_lin) ? 1 : 0;
+    c.slot++;
+    if (c.done) return;
+    if (c.qmax == 0) c.cur_chi = c.ini_chi = chi_lin;
+    double temp = chi_trial;
+    c.last_chi = chi_trial;
+    if (!solved) { temp = DBL_MAX; c.failures++; }
+    const double rho = (c.cur_chi - temp) / (scale + 1e-3);
+    if (rho > 0 && isfinite(temp)) {
+        const double t = 2 * rho - 1;
+        double alpha = 1. - t * t * t;
+        alpha = fmin(alpha, 2. / 3.);
+        c.lambda *= fmax(1. / 3., alpha);
+        c.ni = 2;
+        c.cur_chi = temp;
+        c.cur ^= 1;               // discardTop: the trial state becomes current
+    } else {
+        c.lambda *= c.ni;         // pop: keep the current state
+        c.ni *= 2;
+    }
+    c.qmax++;
+    if (rho < 0 && c.qmax < c.max_trials) {   // another trial of the same iteration
+        c.need_lin = 0;
+        return;
+    }
+    c.trials += c.qmax;
+    c.it++;
+    int result = LBA_RESULT_OK;
+    if (c.qmax == c.max_trials || rho == 0) {
+        result = LBA_RESULT_TERMINATE;
+    } else if (c.early_stop) {
+        if ((c.ini_chi - c.cur_chi) * 1e3 < c.ini_chi) c.nbad++;
+        else c.nbad = 0;
+        if (c.nbad >= 3) result = LBA_RESULT_TERMINATE;
+    }
+    c.result = result;
+    c.qmax = 0;
+    c.need_lin = 1;
+    if ((result != LBA_RESULT_OK && c.early_stop) || c.it >= c.iters) c.done = 1;
+}
+
+// mode (FIN_*): host-driven trial (publish the summary); queued trial (decide, and publish the
+// controller mirror when it is the last trial of a batch); starting-state evaluation of a queue
+// (chi2 only, into the controller)
+__global__ __launch_bounds__(256) void k_finalize(DevProblem P, unsigned long long seq, int mode) {
     __shared__ double red[4];
     const int tid = threadIdx.x;
     const int nc = P.n_tiles + P.n_prior + P.n_vel;
@@ -1145,24 +1231,62 @@ __global__ __launch_bounds__(256) void k_finalize(DevProblem P, unsigned long lo
     const double sb = block_sum<256>(b, red);
     __syncthreads();
     const double sc = block_sum<256>(c, red);
-    if (tid == 0) {
-        const double v[4] = {sa, sb, sc, (double)(*P.info)};
+    if (tid != 0) return;
+    const double v[4] = {sa, sb, sc, (double)(*P.info)};
+    if (mode == FIN_INITIAL) {
+        P.ctl->chi0 = sb;
+        return;
+    }
+    if (mode == FIN_HOST) {
         for (int i = 0; i < 4; ++i) P.fin[i] = v[i];
-        if (P.hfin) {
-            volatile double* h = P.hfin;
-            for (int i = 0; i < 4; ++i) h[i] = v[i];
-            __threadfence_system();
-            __hip_atomic_store(reinterpret_cast<unsigned long long*>(P.hfin + 4), seq, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+    } else {
+        LMCtl ctl = *P.ctl;
+        if (!ctl.done)
+            for (int i = 0; i < 4; ++i) P.fin[i] = v[i];
+        lm_decide(ctl, sa, sb, sc, *P.info == 0, P.hlog);
+        *P.ctl = ctl;
+        if (mode != FIN_QUEUED_PUBLISH) return;
+        volatile double* h = P.hfin + 8;
+        const double* src = reinterpret_cast<const double*>(&ctl);
+        for (int i = 0; i < LMCTL_DOUBLES; ++i) h[i] = src[i];
+    }
+    if (P.hfin) {
+        volatile double* h = P.hfin;
+        for (int i = 0; i < 4; ++i) h[i] = v[i];
+        __threadfence_system();
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(P.hfin + 4), seq, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+__global__ void k_ctl_init(DevProblem P, LMCtl c) {
+    if (threadIdx.x == 0) *P.ctl = c;
+}
+
+// computeLambdaInit (optimization_algorithm_levenberg.cpp:171-185) on the device for a queued
+// optimisation: tau * max |H_ii| over the pose diagonal (S assembled in natural order with
+// lambda = 0, no Schur terms: Hpp) and the landmark diagonals.  A max is exact in any order.
+__global__ __launch_bounds__(1024) void k_lambda_init(DevProblem P, double tau) {
+    __shared__ double red[16];
+    const int tid = threadIdx.x;
+    double m = 0.0;
+    for (int i = tid; i < P.np; i += 1024) m = fmax(m, fabs(P.S[(size_t)i * P.npad + i]));
+    for (int i = tid; i < 3 * P.n_lm; i += 1024) m = fmax(m, fabs(P.Hll[9 * (size_t)(i / 3) + 4 * (i % 3)]));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_down(m, off, 64));
+    if ((tid & 63) == 0) red[tid >> 6] = m;
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < 16; ++w) m = fmax(m, red[w]);
+        P.ctl->lambda = tau * m;
     }
 }
 
 // isDepthPositive (src/G2oTypes.cc:65-81): GP edges test both KF poses (include/G2oTypes.h:305-314)
-__global__ __launch_bounds__(256) void k_depth(DevProblem P, const double* __restrict__ kst,
-                                               const double* __restrict__ lst, unsigned char* ok) {
+__global__ __launch_bounds__(256) void k_depth(DevProblem P, int sel, unsigned char* ok) {
     const int o = blockIdx.x * 256 + threadIdx.x;
     if (o >= P.n_obs) return;
+    const double* __restrict__ lst = P.lbuf[state_idx(P, sel)];
     const int meta = P.ob_meta[o];
     const int kind = meta & 15, cam = meta >> 4;
     CamD cd;
@@ -1185,49 +1309,54 @@ __global__ __launch_bounds__(256) void k_depth(DevProblem P, const double* __res
 // ------------------------------------------------------------------------------------------------ launchers
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
-void launch_gp_prep(const DevProblem& P, const double* kst, int jac, hipStream_t s) {
+void launch_gp_prep(const DevProblem& P, int sel, int jac, int gate, hipStream_t s) {
     const int nb = P.n_gp + cdiv(P.n_kf, PREP_THREADS);
-    if (nb) hipLaunchKernelGGL(k_gp_prep, dim3(nb), dim3(PREP_THREADS), 0, s, P, kst, jac);
+    if (nb) hipLaunchKernelGGL(k_gp_prep, dim3(nb), dim3(PREP_THREADS), 0, s, P, sel, jac, gate);
 }
-void launch_linearize(const DevProblem& P, const double* kst, const double* lst, int write_res, hipStream_t s) {
-    if (P.n_tiles) hipLaunchKernelGGL(k_linearize, dim3(P.n_tiles), dim3(TILE_OBS), 0, s, P, kst, lst, write_res);
+void launch_linearize(const DevProblem& P, int sel, int write_res, int gate, hipStream_t s) {
+    if (P.n_tiles) hipLaunchKernelGGL(k_linearize, dim3(P.n_tiles), dim3(TILE_OBS), 0, s, P, sel, write_res, gate);
 }
-void launch_prior_lin(const DevProblem& P, const double* kst, hipStream_t s) {
+void launch_prior_lin(const DevProblem& P, int sel, int gate, hipStream_t s) {
     const int n = P.n_prior + P.n_vel;
-    if (n) hipLaunchKernelGGL(k_prior_lin, dim3(n), dim3(64), 0, s, P, kst);
+    if (n) hipLaunchKernelGGL(k_prior_lin, dim3(n), dim3(64), 0, s, P, sel, gate);
 }
-void launch_schur(const DevProblem& P, double lambda, hipStream_t s) {
-    if (P.n_tiles) hipLaunchKernelGGL(k_schur, dim3(P.n_tiles), dim3(SCHUR_THREADS), 0, s, P, lambda);
+void launch_schur(const DevProblem& P, double lambda, int gate, hipStream_t s) {
+    if (P.n_tiles) hipLaunchKernelGGL(k_schur, dim3(P.n_tiles), dim3(SCHUR_THREADS), 0, s, P, lambda, gate);
 }
-void launch_assemble(const DevProblem& P, double lambda, int flags, hipStream_t s) {
+void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hipStream_t s) {
     const int n = P.n_asm + P.n_pb;
-    if (n) hipLaunchKernelGGL(k_assemble, dim3(n), dim3(144 * RED_GROUPS), 0, s, P, lambda, flags);
+    if (n) hipLaunchKernelGGL(k_assemble, dim3(n), dim3(144 * RED_GROUPS), 0, s, P, lambda, flags, gate);
 }
-void launch_cholesky_solve(const DevProblem& P, hipStream_t s) {
+void launch_cholesky_solve(const DevProblem& P, int gate, hipStream_t s) {
     const int n = P.npad;   // multiple of CHOL_NB (identity tail)
     if (n == 0) return;
     for (int st = 0; st < P.n_steps; ++st) {
         const int* h = P.h_steps + 4 * st;
         hipLaunchKernelGGL(k_chol_step, dim3(h[3] - h[2]), dim3(256), 0, s, n, h[0], h[1], h[2], P.chol_items, P.S,
-                           P.Lm, P.LinvT, P.xsol, P.yv, P.info);
+                           P.Lm, P.LinvT, P.xsol, P.yv, P.info, P.ctl, gate);
     }
     hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(BS_THREADS), 0, s, P.Lm, P.LinvT, n, P.yv, P.xsol, P.pfirst,
-                       P.pnat, P.tdbg_bs);
+                       P.pnat, P.tdbg_bs, P.ctl, gate);
 }
-void launch_update(const DevProblem& P, double lambda, const double* kst, const double* lst, double* kst_out,
-                   double* lst_out, hipStream_t s) {
-    hipLaunchKernelGGL(k_update, dim3(P.n_upd_blocks), dim3(UPD_THREADS), 0, s, P, lambda, kst, lst, kst_out, lst_out);
+void launch_update(const DevProblem& P, double lambda, int sel, int gate, hipStream_t s) {
+    hipLaunchKernelGGL(k_update, dim3(P.n_upd_blocks), dim3(UPD_THREADS), 0, s, P, lambda, sel, gate);
 }
-void launch_eval(const DevProblem& P, const double* kst, const double* lst, hipStream_t s) {
-    if (P.n_tiles) hipLaunchKernelGGL(k_eval, dim3(P.n_tiles), dim3(TILE_OBS), 0, s, P, kst, lst);
+void launch_eval(const DevProblem& P, int sel, int gate, hipStream_t s) {
+    if (P.n_tiles) hipLaunchKernelGGL(k_eval, dim3(P.n_tiles), dim3(TILE_OBS), 0, s, P, sel, gate);
     const int n = P.n_prior + P.n_vel;
-    if (n) hipLaunchKernelGGL(k_prior_eval, dim3(cdiv(n, 64)), dim3(64), 0, s, P, kst);
+    if (n) hipLaunchKernelGGL(k_prior_eval, dim3(cdiv(n, 64)), dim3(64), 0, s, P, sel, gate);
 }
-void launch_finalize(const DevProblem& P, unsigned long long seq, hipStream_t s) {
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, P, seq);
+void launch_finalize(const DevProblem& P, unsigned long long seq, int mode, hipStream_t s) {
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, P, seq, mode);
 }
-void launch_depth(const DevProblem& P, const double* kst, const double* lst, unsigned char* ok, hipStream_t s) {
-    if (P.n_obs) hipLaunchKernelGGL(k_depth, dim3(cdiv(P.n_obs, 256)), dim3(256), 0, s, P, kst, lst, ok);
+void launch_ctl_init(const DevProblem& P, const LMCtl& c, hipStream_t s) {
+    hipLaunchKernelGGL(k_ctl_init, dim3(1), dim3(64), 0, s, P, c);
+}
+void launch_lambda_init(const DevProblem& P, double tau, hipStream_t s) {
+    hipLaunchKernelGGL(k_lambda_init, dim3(1), dim3(1024), 0, s, P, tau);
+}
+void launch_depth(const DevProblem& P, int sel, unsigned char* ok, hipStream_t s) {
+    if (P.n_obs) hipLaunchKernelGGL(k_depth, dim3(cdiv(P.n_obs, 256)), dim3(256), 0, s, P, sel, ok);
 }
 
 }  // namespace lba

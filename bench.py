@@ -119,8 +119,9 @@ def main():
     else:
         win = make_config_window(args.config, seed=args.seed)
         ex = None
-    # the timed run records HIP events around k_linearize only (LBA_FLAG_TIME_SWEEP): the roofline
-    # below is measured live, per launch, over the timed region
+    # the timed run records HIP events around k_linearize only (LBA_FLAG_TIME_SWEEP: its first launch
+    # in each optimize call, i.e. one launch per window): the roofline below is measured live, per
+    # launch, over the timed region
     prob = amc_lba.Problem(win, device=local, early_stop=0, flags=amc_lba.abi.FLAG_TIME_SWEEP)
 
     # warmup (not timed)
@@ -185,7 +186,8 @@ def main():
                        "parallelism": f"window farm x{world}" if world > 1 else "single window"},
             "roofline": {"bound": "hbm", "kernel": "k_linearize", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                         "traffic": traffic, "bytes_per_launch": B, "avg_launch_ms": k_ms},
+                         "traffic": traffic, "bytes_per_launch": B, "avg_launch_ms": k_ms,
+                         "timed_launches": n_k},
             "roofline_fp64": {"kernel": "k_linearize", "flops_per_launch": F,
                               "achieved": F / (k_ms * 1e-3) / 1e12 if n_k else None,
                               "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",

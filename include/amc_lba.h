@@ -48,8 +48,12 @@ extern "C" {
 
 /* lba_config.flags.  Timing inserts HIP events into the stream (each costs a few us of
  * device idle time), so both are off by default. */
-#define LBA_FLAG_TIME_SWEEP   1   /* time the residual/Jacobian sweep kernel (lba_stats.ms_k_linearize) */
-#define LBA_FLAG_TIME_PHASES  2   /* also time every phase (ms_linearize .. ms_update_eval) */
+#define LBA_FLAG_TIME_SWEEP   1   /* time the residual/Jacobian sweep kernel (lba_stats.ms_k_linearize);
+                                     queued loop: its first launch of each lba_optimize call */
+#define LBA_FLAG_TIME_PHASES  2   /* also time every phase (ms_linearize .. ms_update_eval); runs the
+                                     host-driven loop */
+#define LBA_FLAG_HOST_LOOP    4   /* take every LM decision on the host, one trial at a time (default:
+                                     the trials are queued and decided on the device; same results) */
 
 /* LM termination codes in lba_stats.result (OptimizationAlgorithm::SolverResult) */
 #define LBA_RESULT_OK         0

@@ -135,6 +135,37 @@ def test_cfg1_full_size_lm_properties():
     assert np.array_equal(lm1, lm2) and np.array_equal(kf1["t"], kf2["t"])
 
 
+@pytest.mark.parametrize("early_stop", [1, 0])
+def test_queued_loop_matches_host_loop(early_stop):
+    """The device-decided (queued) LM loop takes exactly the decisions of the host-driven loop:
+    same iterations / trials / results, bitwise-identical states and damping.  Long runs so rejected
+    trials, multi-trial iterations and (early_stop=1) the TERMINATE exit all occur."""
+    from amc_lba.abi import FLAG_HOST_LOOP
+    rejected = 0
+    cases = [(name, {}) for name in WINDOWS] + [("gp_small", dict(lambda_init=0.0)),
+                                                 ("mono_only", dict(lambda_init=0.0, tau=1e-3))]
+    for name, over in cases:   # lambda_init <= 0: computeLambdaInit (queued: on the device)
+        win = _win(name)
+        runs = []
+        for flags in (0, FLAG_HOST_LOOP):
+            p = Problem(win, early_stop=early_stop, flags=flags, **over)
+            n, st = p.optimize(25)
+            n2, st2 = p.optimize(3)   # a second call re-initialises lambda, like g2o
+            kf, lm = p.state()
+            runs.append((n, st, n2, st2, kf, lm))
+        (n, st, n2, st2, kf, lm), (hn, hst, hn2, hst2, hkf, hlm) = runs
+        assert (n, n2) == (hn, hn2), name
+        for a, b in ((st, hst), (st2, hst2)):
+            assert (a.iterations, a.trials, a.result, a.solve_failures) == \
+                (b.iterations, b.trials, b.result, b.solve_failures), name
+            assert a.chi2_initial == b.chi2_initial and a.chi2_final == b.chi2_final, name
+            assert a.lambda_final == b.lambda_final, name
+        assert np.array_equal(lm, hlm) and np.array_equal(kf["t"], hkf["t"]), name
+        assert np.array_equal(kf["q"], hkf["q"]) and np.array_equal(kf["vel"], hkf["vel"]), name
+        rejected += st.trials - st.iterations
+    assert rejected > 0   # the multi-trial path was exercised
+
+
 def test_stop_flag_stops_before_first_iteration():
     win = _win("gp_small")
     p = Problem(win)
