@@ -5,14 +5,17 @@
 // touches a narrow band of keyframes):
 //   kf state      [n_kf][16]   q(4) t(3) vel(6) time bf pad   — two copies (current / trial)
 //   lm state      [n_lm][3]                                     — two copies (current / trial)
-//   observations  SoA, device order: meta(kind|cam<<4), kf_a, kf_b, gp pair, landmark,
-//                 pair slots a/b, tile-local LDS row, t, z[3], w
-//   gp samples    [n_gps][GPS_STRIDE] per (prev KF, KF, observation time): interpolated pose and the
-//                 6x24 Jacobian factor N (lba::GPSample); one per camera time stamp, not per observation
+//   observations  SoA, device order: meta(kind|cam<<4), kf_a, kf_b, pose sample, landmark,
+//                 tile-local LDS row, z[3], w
+//   pose samples  [n_smp][GPS_STRIDE]: per GP (prev KF, KF, observation time) the interpolated pose
+//                 and the 6x24 Jacobian factor N (lba::GPSample; one per camera time stamp, not per
+//                 observation), then one per KF (its pose, N = [0 | I 0]) for EdgeMono / EdgeStereo
 //   Hpl           [n_pairs][12][3] one block per unique (non-fixed KF, landmark)
 //   Hll, bl       [n_lm][9], [n_lm][3]
-//   hslab/gslab   per (tile, pose-pair segment) partial of Hpp blocks / b_p (and per prior /
-//                 velocity edge), each block stored at a slot sorted by its target upper block
+//   mslab         per (tile, pose sample) partial of M = sum rho' w J1^T J1 and g = sum rho' w J1^T e
+//                 (J1 w.r.t. the sample's pose), slots sorted by sample
+//   hslab/gslab   per pose sample N^T M N / -N^T g as Hpp blocks (aa, ab, bb) / b_p pieces, and per
+//                 prior / velocity edge, each block stored at a slot sorted by its target upper block
 //   sslab/gpslab  per (tile, KF pair) Schur partials V(k1) Hpl(k2)^T and per (tile, KF) rhs
 //                 partials, target-sorted likewise
 //   S, Lm         [npad][npad] dense reduced camera system (lower) and its Cholesky factor; npad =
@@ -33,15 +36,14 @@ constexpr int TILE_ROWS = 288;
 constexpr int TILE_PAIRS = 128;
 constexpr int TILE_LMS = 64;
 constexpr int TILE_KF = 16;
-constexpr int ROW_STRIDE = 28;      // LDS Jacobian row: Ja(12) Jb(12) e(1) Jp(3)
-constexpr int TILE_SEGS = 48;       // pose-pair segments per tile (k_linearize stages their metadata)
-constexpr int SEG_MAX_ROWS = 48;    // longer (a, b) runs are split so the segment tasks stay balanced
-constexpr int TILE_PROWS = 2 * TILE_ROWS;   // pair row-list entries per tile (each row feeds <= 2 pairs)
+constexpr int ROW_STRIDE = 10;      // LDS Jacobian row: J1(6) e(1) Jp(3) (J1: w.r.t. the pose sample)
+constexpr int G_STRIDE = 18;        // per observation: G = rho' w sum_rows J1^T Jp (6 x 3, row-major)
+constexpr int SM_STRIDE = 27;       // per (tile, sample) partial: M = sum rho' w J1^T J1 (21, upper
+                                    // row-major) and g = sum rho' w J1^T e (6)
+constexpr int TILE_SMP = 64;        // pose samples per tile (k_linearize stages their row runs)
+constexpr int TILE_PROWS = 2 * TILE_OBS;    // pair entry-list entries per tile (each obs feeds <= 2 pairs)
 constexpr int TILE_SLIST = 1024;    // Schur (pair, pair, landmark) triples per tile (k_schur stages them)
 constexpr int TILE_SENT = TILE_KF * (TILE_KF + 1) / 2;   // KF-pair Schur entries per tile
-constexpr int TILE_TGT = 64;        // Hpp target blocks per tile (k_linearize stages their records)
-constexpr int TILE_RUNS = 3 * TILE_SEGS;   // row runs of a tile's targets
-constexpr int TGT_STRIDE = 4;       // staged target record: flags | nrun << 8, hslot, gslot, first run
 
 constexpr int CHOL_NB = 32;         // Cholesky panel / tile width
 constexpr int RED_GROUPS = 4;       // reduction kernels: 4 groups x 144 threads
@@ -84,7 +86,7 @@ struct DevProblem {
     const int* ob_meta;
     const int* ob_kfa;
     const int* ob_kfb;
-    const int* ob_gp;       // GP observations: GP pose sample (lba::GPSample) index, else -1
+    const int* ob_smp;      // pose sample (lba::GPSample): GP sample, or n_gps + kf_b for EdgeMono/Stereo
     const int* ob_lm;
     const int* ob_row;
     const double* ob_z;     // [n_obs][3]
@@ -94,8 +96,9 @@ struct DevProblem {
     const int* gp_kfa;      // per GP pair (prev KF, KF)
     const int* gp_kfb;
     const int* gp_s0;       // [n_gp + 1] the pair's pose samples (contiguous)
-    const double* gps_t;    // per sample: observation time
-    int n_gps;
+    const double* gps_t;    // per GP sample: observation time
+    int n_gps;              // GP samples; samples n_gps .. n_gps + n_kf - 1 are the KF poses (N = [0 | I 0])
+    int n_smp;              // n_gps + n_kf
     const double* camd;     // [n_cam][CAMD_STRIDE]
     // tiles
     const int* tile_obs0;
@@ -104,23 +107,14 @@ struct DevProblem {
     const int* tile_nlm;
     const int* tile_pair0;
     const int* tile_npair;
-    const int* tile_seg0;
-    const int* tile_nseg;
+    const int* tile_smp0;   // per tile: first tile-sample record / count
+    const int* tile_nsmp;
+    const int* tsm_meta;    // per tile sample: row0 | nrows << 16 (tile-local LDS rows), mslab slot
     const int* tile_sent0;
     const int* tile_nsent;
     const int* tile_kf0;
     const int* tile_nkf;
     const int* tkf_list;    // tile KF unions (pose block indices)
-    const int* tgt_meta;    // per tile Hpp target: TGT_STRIDE ints (see lba_host.hip)
-    const int* tile_tgt0;   // per tile: first target / count
-    const int* tile_ntgt;
-    const int* tile_run0;   // per tile: first run
-    const int* run_rows;    // per run: row0 | nrows << 16 (tile-local rows)
-    const int* run_offs;    // per run: column offsets offA | offB << 8 in the LDS Jacobian row
-    const int* seg_a;       // per segment entry: pose block of side a / b (-1 = none)
-    const int* seg_b;
-    const int* seg_row0;    // tile-local first row
-    const int* seg_nrows;
     const int* sent_r0;     // [n_sentries + 1] CSR into sent_list
     const int* sent_list;   // per entry: landmarks coupling k1, k2: pair1 | pair2 << 8 | lm << 16 (tile-local)
     const int* sent_l1;     // per Schur entry: tile-local KF index of k1 / k2
@@ -128,14 +122,14 @@ struct DevProblem {
     // pairs / landmarks
     const int* pair_lm;
     const int* pair_kf;     // pose block index
-    const int* pair_r0;     // CSR into pair_rows: tile-local row | side << 16
+    const int* pair_r0;     // CSR into pair_rows: tile-local observation | side << 16 (0: KF a, 1: KF b)
     const int* pair_rows;
     const int* lm_r0;       // CSR into lm_rows: tile-local rows
     const int* lm_rows;
     const int* lm_pair0;    // [n_lm + 1] landmark -> pairs
     // partial-sum slabs are sorted by their reduction target, so every reduction below reads
     // one contiguous range (coalesced) instead of chasing a source list
-    const int* seg_slot;    // per slab entry (motion priors, velocity edges): 5 ints
+    const int* seg_slot;    // per slab entry (pose samples, motion priors, velocity edges): 5 ints
                             //   aa, ab, bb slot in hslab (-1 = none), ab transposed flag, -
     const int* seg_gslot;   // per slab entry: ga, gb slot in gslab (-1 = none)
     const int* asm_list;    // upper blocks inside the structural pattern of S (diagonal + any source)
@@ -154,11 +148,13 @@ struct DevProblem {
     const int* pri_a;
     const int* pri_b;
     const int* vel_kf;
-    int pri_entry0;         // slab entry index of prior 0 (velocity edges follow)
+    int pri_entry0;         // slab entry index of prior 0 (velocity edges follow); samples are 0..n_smp-1
+    const int* ms0;         // [n_smp + 1] mslab range per sample
     double qcinv[36];
     double huber_mono, huber_stereo, huber_prior;
     // work buffers
-    double* gps;            // [n_gps][GPS_STRIDE] GP pose samples: Rwb twb N (lba::GPSample)
+    double* gps;            // [n_smp][GPS_STRIDE] pose samples: Rwb twb N (lba::GPSample)
+    double* mslab;          // [n_mslots][SM_STRIDE] per (tile, sample) M / g partials, sample-sorted
     double* kfp_pose;       // [n_kf][KFP_STRIDE] Rwb twb (same prefix as a sample)
     double* hslab;          // [n_hslots][144] Hpp partial blocks, target-sorted
     double* gslab;          // [n_gslots][12] b_p partials, target-sorted

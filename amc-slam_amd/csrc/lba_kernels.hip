@@ -85,31 +85,30 @@ __device__ __forceinline__ void load_cam(const double* c, CamD* d) {
     d->fx = c[12]; d->fy = c[13]; d->cx = c[14]; d->cy = c[15];
 }
 
-// Pose of the body at the observation time (Rwb, twb) and, for GP edges, the observation's
-// Jacobian factor N: both come from the GP pose sample (GP edges) or the KF pose (EdgeMono /
-// EdgeStereo), whose records share the Rwb(9) twb(3) prefix.  Returns the stereo bf of the edge's
-// first KF vertex.
+// Pose of the body at the observation time (Rwb, twb): the observation's pose sample (a GP sample for
+// GP edges, the KF pose record for EdgeMono / EdgeStereo).  Returns the stereo bf of the edge's first
+// KF vertex.
 __device__ __forceinline__ double obs_pose(const DevProblem& P, const double* kst, int o, bool gp, double* Rwb,
-                                           double* twb, const double** N) {
+                                           double* twb) {
     const int ka = gp ? P.ob_kfa[o] : P.ob_kfb[o];
-    const double* S = gp ? P.gps + (size_t)P.ob_gp[o] * GPS_STRIDE : P.kfp_pose + (size_t)P.ob_kfb[o] * KFP_STRIDE;
+    const double* S = P.gps + (size_t)P.ob_smp[o] * GPS_STRIDE;
 #pragma unroll
     for (int i = 0; i < 9; ++i) Rwb[i] = S[i];
     twb[0] = S[9]; twb[1] = S[10]; twb[2] = S[11];
-    *N = gp ? S + 12 : nullptr;
     return kst[(size_t)ka * KF_STRIDE + 14];
 }
 
 // One observation of the linearisation (DIM compile-time so every per-row array stays in
-// registers): residual, Huber weight, Jacobian rows into the LDS row buffer; returns rho(chi2).
+// registers): residual, Huber weight, the rows [J1 e Jp] into the LDS row buffer (J1 w.r.t. the
+// pose sample: the pose / velocity Jacobian J1 N is never formed, see k_linearize) and
+// G = rho' w sum_rows J1^T Jp; returns rho(chi2).
 template <int DIM>
 __device__ __forceinline__ double lin_obs(const DevProblem& P, const double* kst, const double* lst, int o, int cam,
-                                          bool gp, double* rows, double* rw, int write_res) {
+                                          bool gp, double* rows, double* rw, double* G, int write_res) {
     CamD cd;
     load_cam(P.camd + (size_t)cam * CAMD_STRIDE, &cd);
     double Rwb[9], twb[3];
-    const double* N;
-    const double bf = obs_pose(P, kst, o, gp, Rwb, twb, &N);
+    const double bf = obs_pose(P, kst, o, gp, Rwb, twb);
     const double* Xw = lst + (size_t)P.ob_lm[o] * 3;
     double z[DIM];
 #pragma unroll
@@ -122,14 +121,29 @@ __device__ __forceinline__ double lin_obs(const DevProblem& P, const double* kst
     for (int d = 0; d < DIM; ++d) chi += e[d] * (w * e[d]);
     double r0, r1;
     huber(chi, DIM == 3 ? P.huber_stereo : P.huber_mono, &r0, &r1);
+    double J1[6 * DIM], Jp[3 * DIM];
+    obs_j1<DIM>(Rwb, cd, Xb, Xc, bf, J1, Jp);
+    const double s = r1 * w;   // robustInformation = rho' * Omega (base_edge.h:96-102), Omega = w I
     const int row = P.ob_row[o];
-    double* R = rows + row * ROW_STRIDE;
-    obs_jacobian<DIM>(Rwb, cd, Xb, Xc, bf, N, R, ROW_STRIDE, 25);
 #pragma unroll
     for (int d = 0; d < DIM; ++d) {
-        R[d * ROW_STRIDE + 24] = e[d];
-        rw[row + d] = r1 * w;   // robustInformation = rho' * Omega (base_edge.h:96-102)
+        double* R = rows + (row + d) * ROW_STRIDE;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) R[j] = J1[d * 6 + j];
+        R[6] = e[d];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) R[7 + j] = Jp[d * 3 + j];
+        rw[row + d] = s;
     }
+#pragma unroll
+    for (int l = 0; l < 6; ++l)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            double g = 0.0;
+#pragma unroll
+            for (int d = 0; d < DIM; ++d) g += J1[d * 6 + l] * Jp[d * 3 + a];
+            G[l * 3 + a] = s * g;
+        }
     P.ob_chi2[o] = chi;
     if (write_res)
 #pragma unroll
@@ -144,8 +158,7 @@ __device__ __forceinline__ double eval_obs(const DevProblem& P, const double* ks
     CamD cd;
     load_cam(P.camd + (size_t)cam * CAMD_STRIDE, &cd);
     double Rwb[9], twb[3];
-    const double* N;
-    const double bf = obs_pose(P, kst, o, gp, Rwb, twb, &N);
+    const double bf = obs_pose(P, kst, o, gp, Rwb, twb);
     double z[DIM];
 #pragma unroll
     for (int d = 0; d < DIM; ++d) z[d] = P.ob_z[3 * (size_t)o + d];
@@ -192,93 +205,54 @@ __global__ __launch_bounds__(PREP_THREADS) void k_gp_prep(DevProblem P, int sel,
         return;
     }
     const int k = (blockIdx.x - P.n_gp) * PREP_THREADS + tid;
-    if (k < P.n_kf) {
+    if (k < P.n_kf) {   // KF pose record and the KF's pose sample (its constant N was uploaded once)
         const double* kk = kst + (size_t)k * KF_STRIDE;
         double R[9];
         qmat(Quat{kk[0], kk[1], kk[2], kk[3]}, R);
         double* o = P.kfp_pose + (size_t)k * KFP_STRIDE;
-        for (int j = 0; j < 9; ++j) o[j] = R[j];
-        o[9] = kk[4]; o[10] = kk[5]; o[11] = kk[6];
+        double* so = P.gps + (size_t)(P.n_gps + k) * GPS_STRIDE;
+        for (int j = 0; j < 9; ++j) o[j] = so[j] = R[j];
+        o[9] = so[9] = kk[4]; o[10] = so[10] = kk[5]; o[11] = so[11] = kk[6];
     }
 }
 
-// One (Hpp target, 4x4 sub-block) task of a tile: acc = sum over the target's row runs of
-// (s r)[offA + 4 ia ..] r[offB + 4 jb ..]^T (jb = -1: the e column, for b_k), written to the target's
-// slab slot (diagonal targets: upper sub-blocks + mirror; off-diagonal: the Ja^T W Jb block, stored
-// transposed when the block's upper position is (b, a)).  Rows are consumed four at a time so their
-// LDS reads are all in flight before the FMAs.
-__device__ __forceinline__ void tgt_task(const DevProblem& P, const double* rows, const double* rw, const int* tm,
-                                         const int* rr, const int* ro, int ia, int jb) {
-    const int nrun = tm[0] >> 8, run0 = tm[3];
-    double acc[16];
+// One (tile sample, 9-output chunk) task: outputs 9 CH .. 9 CH + 8 of the sample's partial, i.e. the
+// upper triangle of M = sum_rows s J1^T J1 (outputs 0..20, row-major) and g = sum_rows s J1^T e
+// (21..26), over the sample's contiguous rows.
+template <int CH>
+__device__ __forceinline__ void smp_task(const DevProblem& P, const double* rows, const double* rw, int r0, int nr,
+                                         int mslot) {
+    constexpr unsigned char ui[21] = {0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 4, 4, 5};
+    constexpr unsigned char uj[21] = {0, 1, 2, 3, 4, 5, 1, 2, 3, 4, 5, 2, 3, 4, 5, 3, 4, 5, 4, 5, 5};
+    double acc[9];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) acc[q] = 0.0;
-    for (int u = run0; u < run0 + nrun; ++u) {
-        const int r0 = rr[u] & 0xffff, rend = r0 + (rr[u] >> 16);
-        const int ca = (ro[u] & 0xff) + 4 * ia, cb = jb < 0 ? 24 : (ro[u] >> 8) + 4 * jb;
-        int r = r0;
-        for (; r + 4 <= rend; r += 4) {
-            double a[4][4], c[4][4];
+    for (int q = 0; q < 9; ++q) acc[q] = 0.0;
+    for (int r = r0; r < r0 + nr; ++r) {
+        const double* R = rows + r * ROW_STRIDE;
+        const double sw = rw[r];
+        double j[7];
 #pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                const double* Rr = rows + (r + v) * ROW_STRIDE;
-                const double s = rw[r + v];
+        for (int c = 0; c < 7; ++c) j[c] = R[c];   // J1 (6), e
 #pragma unroll
-                for (int k = 0; k < 4; ++k) { a[v][k] = s * Rr[ca + k]; c[v][k] = Rr[cb + k]; }
-            }
-#pragma unroll
-            for (int v = 0; v < 4; ++v)
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-#pragma unroll
-                    for (int l = 0; l < 4; ++l) acc[k * 4 + l] += a[v][k] * c[v][l];
-        }
-        for (; r < rend; ++r) {
-            const double* Rr = rows + r * ROW_STRIDE;
-            const double s = rw[r];
-            double a[4], c[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) { a[k] = s * Rr[ca + k]; c[k] = Rr[cb + k]; }
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-#pragma unroll
-                for (int l = 0; l < 4; ++l) acc[k * 4 + l] += a[k] * c[l];
+        for (int q = 0; q < 9; ++q) {
+            constexpr int base = 9 * CH;
+            const int idx = base + q;
+            const double x = idx < 21 ? j[ui[idx < 21 ? idx : 0]] : j[idx - 21];
+            const double y = idx < 21 ? j[uj[idx < 21 ? idx : 0]] : j[6];
+            acc[q] += (sw * x) * y;
         }
     }
-    if (jb < 0) {   // b_k = -J_k^T rho' Omega e
-        double* g = P.gslab + (size_t)tm[2] * 12 + 4 * ia;
+    double* m = P.mslab + (size_t)mslot * SM_STRIDE + 9 * CH;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) g[k] = -acc[k * 4];
-        return;
-    }
-    double* H = P.hslab + (size_t)tm[1] * 144;
-    const int i0 = 4 * ia, j0 = 4 * jb;
-    if (tm[0] & 1) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int l = 0; l < 4; ++l) {
-                H[(i0 + k) * 12 + j0 + l] = acc[k * 4 + l];
-                if (ia != jb) H[(j0 + l) * 12 + i0 + k] = acc[k * 4 + l];
-            }
-    } else {
-        const bool tr = (tm[0] & 2) != 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int l = 0; l < 4; ++l) {
-                if (tr) H[(j0 + l) * 12 + i0 + k] = acc[k * 4 + l];
-                else H[(i0 + k) * 12 + j0 + l] = acc[k * 4 + l];
-            }
-    }
+    for (int q = 0; q < 9; ++q) m[q] = acc[q];
 }
 
 __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, int write_res, int gate) {
     __shared__ double rows[TILE_ROWS * ROW_STRIDE];
     __shared__ double rw[TILE_ROWS];
-    __shared__ int tgtm[TILE_TGT * TGT_STRIDE];
-    __shared__ int trr[TILE_RUNS];
-    __shared__ int tro[TILE_RUNS];
+    __shared__ double Gs[TILE_OBS * G_STRIDE];
+    __shared__ int tsm[2 * TILE_SMP];
+    __shared__ int osm[TILE_OBS];
     __shared__ int prow[TILE_PROWS];
     __shared__ int pr0[TILE_PAIRS + 1];
     __shared__ int lrow[TILE_ROWS];
@@ -286,7 +260,7 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
     __shared__ double red[TILE_OBS / 64];
     const int tile = blockIdx.x, tid = threadIdx.x;
     const int obs0 = P.tile_obs0[tile], nobs = P.tile_nobs[tile];
-    const int tg0 = P.tile_tgt0[tile], ntg = P.tile_ntgt[tile];
+    const int ts0 = P.tile_smp0[tile], nts = P.tile_nsmp[tile];
     const int pair0 = P.tile_pair0[tile], npair = P.tile_npair[tile];
     const int lm0 = P.tile_lm0[tile], nlm = P.tile_nlm[tile];
     if (gated_off(P.ctl, gate)) return;
@@ -299,18 +273,10 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
     {
         const int q0 = P.pair_r0[pair0], nq = P.pair_r0[pair0 + npair] - q0;
         const int m0 = P.lm_r0[lm0], nm = P.lm_r0[lm0 + nlm] - m0;
-        const int u0 = P.tile_run0[tile];
-        const int nu = ntg ? P.tgt_meta[(size_t)(tg0 + ntg - 1) * TGT_STRIDE + 3] +
-                                 (P.tgt_meta[(size_t)(tg0 + ntg - 1) * TGT_STRIDE] >> 8) : 0;
 #pragma unroll
-        for (int k = 0; k < (TILE_TGT * TGT_STRIDE + TILE_OBS - 1) / TILE_OBS; ++k) {
+        for (int k = 0; k < (2 * TILE_SMP + TILE_OBS - 1) / TILE_OBS; ++k) {
             const int t = tid + k * TILE_OBS;
-            if (t < ntg * TGT_STRIDE) tgtm[t] = P.tgt_meta[(size_t)tg0 * TGT_STRIDE + t];
-        }
-#pragma unroll
-        for (int k = 0; k < (TILE_RUNS + TILE_OBS - 1) / TILE_OBS; ++k) {
-            const int t = tid + k * TILE_OBS;
-            if (t < nu) { trr[t] = P.run_rows[u0 + t]; tro[t] = P.run_offs[u0 + t]; }
+            if (t < 2 * nts) tsm[t] = P.tsm_meta[2 * (size_t)ts0 + t];
         }
 #pragma unroll
         for (int k = 0; k < TILE_PROWS / TILE_OBS; ++k) {
@@ -330,40 +296,37 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
         if (tid <= nlm) lr0[tid] = P.lm_r0[lm0 + tid] - m0;
     }
 
-    // ---- phase 1: one observation per lane: residual, robust weight, Jacobian rows -> LDS
+    // ---- phase 1: one observation per lane: residual, robust weight, rows [J1 e Jp] and G -> LDS
     double rho0 = 0.0;
     if (tid < nobs) {
         const int o = obs0 + tid;
         const int meta = P.ob_meta[o];
         const int kind = meta & 15, cam = meta >> 4;
         const bool gp = kind <= LBA_STEREO_GP;
-        rho0 = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? lin_obs<3>(P, kst, lst, o, cam, gp, rows, rw, write_res)
-                                                             : lin_obs<2>(P, kst, lst, o, cam, gp, rows, rw, write_res);
+        osm[tid] = P.ob_smp[o];
+        double* G = Gs + tid * G_STRIDE;
+        rho0 = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? lin_obs<3>(P, kst, lst, o, cam, gp, rows, rw, G, write_res)
+                                                             : lin_obs<2>(P, kst, lst, o, cam, gp, rows, rw, G, write_res);
     }
     const double tchi = block_sum<TILE_OBS>(rho0, red);   // (its barrier also publishes rows / lists)
     if (tid == 0) P.chi_lin[tile] = tchi;
     LBA_TMARK(P.tdbg_lin, 1);
 
-    // ---- phase 2: one Hpp / b_p partial per target block of the tile, one (target, 4x4 sub-block)
-    //      per task: diagonal targets 6 upper sub-blocks + 3 b_k pieces, off-diagonal 9 sub-blocks
-    for (int task = tid; task < ntg * 9; task += TILE_OBS) {
-        const int g = task / 9, sub = task - g * 9;
-        const int* tm = tgtm + g * TGT_STRIDE;
-        int ia, jb;
-        if (tm[0] & 1) {
-            constexpr unsigned char dia[9] = {0, 0, 0, 1, 1, 2, 0, 1, 2};
-            constexpr signed char djb[9] = {0, 1, 2, 1, 2, 2, -1, -1, -1};
-            ia = dia[sub];
-            jb = djb[sub];
-        } else {
-            ia = sub / 3;
-            jb = sub - 3 * ia;
-        }
-        tgt_task(P, rows, rw, tm, trr, tro, ia, jb);
+    // ---- phase 2: the tile's partial of every pose sample it observes, in the sample's 6-dim space
+    //      (J = J1 N, so sum J^T W J = N^T M N with M = sum J1^T W J1: the 24 x 24 products are formed
+    //      once per sample in k_prior_lin instead of once per row here)
+    for (int task = tid; task < nts * 3; task += TILE_OBS) {
+        const int ts = task / 3, ch = task - 3 * ts;
+        const int meta = tsm[2 * ts], mslot = tsm[2 * ts + 1];
+        const int r0 = meta & 0xffff, nr = meta >> 16;
+        if (ch == 0) smp_task<0>(P, rows, rw, r0, nr, mslot);
+        else if (ch == 1) smp_task<1>(P, rows, rw, r0, nr, mslot);
+        else smp_task<2>(P, rows, rw, r0, nr, mslot);
     }
     LBA_TMARK(P.tdbg_lin, 2);
 
-    // ---- phase 3: Hpl per (KF, landmark) pair from the staged row lists
+    // ---- phase 3: Hpl per (KF, landmark) pair: sum over its (observation, side) entries of
+    //      N_side^T G (N_side: the 6 x 12 block of the sample's factor for that KF), four Hpl rows per task
     for (int task = tid; task < npair * 3; task += TILE_OBS) {
         const int pl = task / 3, sb = task % 3;
         double acc[12];
@@ -371,14 +334,22 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
         for (int q = 0; q < 12; ++q) acc[q] = 0.0;
         for (int q = pr0[pl]; q < pr0[pl + 1]; ++q) {
             const int code = prow[q];
-            const int r = code & 0xffff, side = code >> 16;
-            const double* Rr = rows + r * ROW_STRIDE;
-            const double s = rw[r];
+            const int ol = code & 0xffff, side = code >> 16;
+            // N stored transposed: column c of N (6 values) at 12 + 6 c
+            const double* Nc = P.gps + (size_t)osm[ol] * GPS_STRIDE + 12 + 6 * (12 * side + 4 * sb);
+            const double* G = Gs + ol * G_STRIDE;
+            double g[18];
+#pragma unroll
+            for (int u = 0; u < 18; ++u) g[u] = G[u];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const double ji = s * Rr[side * 12 + 4 * sb + i];
+                double n[6];
 #pragma unroll
-                for (int a = 0; a < 3; ++a) acc[i * 3 + a] += ji * Rr[25 + a];
+                for (int l = 0; l < 6; ++l) n[l] = Nc[6 * i + l];
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+                    acc[i * 3 + a] += n[0] * g[a] + n[1] * g[3 + a] + n[2] * g[6 + a] + n[3] * g[9 + a] +
+                                      n[4] * g[12 + a] + n[5] * g[15 + a];
             }
         }
         double* H = P.Hpl + (size_t)(pair0 + pl) * 36 + 12 * sb;
@@ -397,12 +368,12 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
             const int r = lrow[q];
             const double* Rr = rows + r * ROW_STRIDE;
             const double s = rw[r];
-            const double e = Rr[24];
+            const double e = Rr[6];
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
-                const double sa = s * Rr[25 + a];
+                const double sa = s * Rr[7 + a];
 #pragma unroll
-                for (int c = 0; c < 3; ++c) H[a * 3 + c] += sa * Rr[25 + c];
+                for (int c = 0; c < 3; ++c) H[a * 3 + c] += sa * Rr[7 + c];
                 b[a] -= sa * e;
             }
         }
@@ -413,11 +384,94 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
 }
 
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_prior_lin(DevProblem P, int sel, int gate) {
+// Pose sample s: reduce its M / g partials (fixed slot order) and expand them through the sample's
+// Jacobian factor N (6 x 24, columns [KF a pose vel | KF b pose vel]) into Hpp blocks and b_p pieces:
+// aa = Na^T M Na, ab = Na^T M Nb, bb = Nb^T M Nb, b_a = -Na^T g, b_b = -Nb^T g, written to the sample's
+// slab slots (the same slots / transposition rule as the prior edges).  Equal to summing J^T W J
+// per observation row with J = J1 N (base_multi_edge.hpp:170-222) up to rounding.
+constexpr int PRI_THREADS = 256;
+constexpr int EXP_GROUPS = PRI_THREADS / SM_STRIDE;   // 9 partial sums per output
+
+__device__ void sample_expand(const DevProblem& P, int smp, double* Msh, double* Nsh, double* MN, double* part) {
+    const int tid = threadIdx.x;
+    const int* sl = P.seg_slot + 5 * (size_t)smp;
+    const int* gl = P.seg_gslot + 2 * (size_t)smp;
+    if (sl[0] < 0 && sl[1] < 0 && sl[2] < 0) return;   // no optimisable KF (uniform per workgroup)
+    // M / g: group q of the 9 sums every 9th slot of its output (4 loads in flight), then a fixed
+    // combination order over the groups
+    if (tid < EXP_GROUPS * SM_STRIDE) {
+        const int q = tid / SM_STRIDE, o = tid - q * SM_STRIDE;
+        const int k0 = P.ms0[smp] + q, k1 = P.ms0[smp + 1];
+        const double* m = P.mslab + o;
+        double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+        int k = k0;
+        for (; k + 3 * EXP_GROUPS < k1; k += 4 * EXP_GROUPS) {
+            v0 += m[(size_t)k * SM_STRIDE];
+            v1 += m[(size_t)(k + EXP_GROUPS) * SM_STRIDE];
+            v2 += m[(size_t)(k + 2 * EXP_GROUPS) * SM_STRIDE];
+            v3 += m[(size_t)(k + 3 * EXP_GROUPS) * SM_STRIDE];
+        }
+        for (; k < k1; k += EXP_GROUPS) v0 += m[(size_t)k * SM_STRIDE];
+        part[tid] = (v0 + v1) + (v2 + v3);
+    }
+    const double* Ng = P.gps + (size_t)smp * GPS_STRIDE + 12;
+    if (tid < 144) Nsh[tid] = Ng[tid];   // N(l, c) at Nsh[6 c + l]
+    __syncthreads();
+    if (tid < SM_STRIDE) {
+        double v = 0.0;
+#pragma unroll
+        for (int q = 0; q < EXP_GROUPS; ++q) v += part[q * SM_STRIDE + tid];
+        Msh[tid] = v;
+    }
+    __syncthreads();
+    // M (symmetric) from its upper triangle: index of (i, j), i <= j, in row-major upper order
+    auto mref = [&](int i, int j) {
+        const int a = i < j ? i : j, b = i < j ? j : i;
+        return Msh[a * 6 - a * (a - 1) / 2 + (b - a)];
+    };
+    if (tid < 144) {   // MN(l, c) = sum_m M(l, m) N(m, c), stored MN[6 c + l]
+        const int t = tid, c = t / 6, l = t % 6;
+        double v = 0.0;
+#pragma unroll
+        for (int m = 0; m < 6; ++m) v += mref(l, m) * Nsh[6 * c + m];
+        MN[t] = v;
+    }
+    __syncthreads();
+    for (int t = tid; t < 3 * 144; t += PRI_THREADS) {
+        const int bk = t / 144, ij = t % 144, i = ij / 12, j = ij % 12;
+        const int slot = sl[bk];
+        if (slot < 0) continue;
+        const int ci = (bk == 2 ? 12 : 0) + i, cj = (bk == 0 ? 0 : 12) + j;
+        double v = 0.0;
+#pragma unroll
+        for (int l = 0; l < 6; ++l) v += Nsh[6 * ci + l] * MN[6 * cj + l];
+        double* H = P.hslab + (size_t)slot * 144;
+        if (bk == 1 && sl[3]) H[j * 12 + i] = v;
+        else H[i * 12 + j] = v;
+    }
+    if (tid < 24) {
+        const int side = tid / 12, i = tid % 12;
+        if (gl[side] >= 0) {
+            double v = 0.0;
+#pragma unroll
+            for (int l = 0; l < 6; ++l) v += Nsh[6 * (12 * side + i) + l] * Msh[21 + l];
+            P.gslab[(size_t)gl[side] * 12 + i] = -v;
+        }
+    }
+}
+
+// Workgroups 0 .. n_prior + n_vel - 1: EdgeGaussianPrior / EdgeVelocity quadratic forms; then one
+// workgroup per pose sample (sample_expand).
+__global__ __launch_bounds__(PRI_THREADS) void k_prior_lin(DevProblem P, int sel, int gate) {
     __shared__ double Ji[144], Jj[144], WJi[144], WJj[144], Om[144], e[12], We[12];
     __shared__ double wsh;
+    __shared__ double part[EXP_GROUPS * SM_STRIDE];
     const int idx = blockIdx.x, tid = threadIdx.x;
     if (gated_off(P.ctl, gate)) return;
+    if (idx >= P.n_prior + P.n_vel) {
+        sample_expand(P, idx - P.n_prior - P.n_vel, Ji, Jj, WJi, part);
+        return;
+    }
     const double* __restrict__ kst = P.kbuf[state_idx(P, sel)];
     const int ent = P.pri_entry0 + idx;
     const int* sl = P.seg_slot + 5 * (size_t)ent;
@@ -441,7 +495,7 @@ __global__ __launch_bounds__(64) void k_prior_lin(DevProblem P, int sel, int gat
         }
         __syncthreads();
         const double w1 = wsh;
-        for (int t = tid; t < 288; t += 64) {
+        for (int t = tid; t < 288; t += PRI_THREADS) {
             const int which = t / 144, ij = t % 144, i = ij / 12, j = ij % 12;
             const double* J = which ? Jj : Ji;
             double s = 0.0;
@@ -455,7 +509,7 @@ __global__ __launch_bounds__(64) void k_prior_lin(DevProblem P, int sel, int gat
         }
         __syncthreads();
         // aa = Ji^T W Ji, ab = Ji^T W Jj, bb = Jj^T W Jj, ga/gb = -J^T W e (base_binary_edge.hpp:54-120)
-        for (int t = tid; t < 456; t += 64) {
+        for (int t = tid; t < 456; t += PRI_THREADS) {
             if (t < 432) {
                 const int bk = t / 144, ij = t % 144, i = ij / 12, j = ij % 12;
                 const int slot = sl[bk == 0 ? 0 : (bk == 1 ? 1 : 2)];
@@ -482,7 +536,7 @@ __global__ __launch_bounds__(64) void k_prior_lin(DevProblem P, int sel, int gat
         const double ev = kst[(size_t)P.vel_kf[v] * KF_STRIDE + 7 + 2];
         const double q22 = P.qcinv[2 * 6 + 2];
         double* H = P.hslab + (size_t)sl[2] * 144;
-        for (int t = tid; t < 144; t += 64) H[t] = (t == 8 * 12 + 8) ? q22 : 0.0;
+        for (int t = tid; t < 144; t += PRI_THREADS) H[t] = (t == 8 * 12 + 8) ? q22 : 0.0;
         if (tid < 12) P.gslab[(size_t)gl[1] * 12 + tid] = (tid == 8) ? -q22 * ev : 0.0;
         if (tid == 0) P.chi_lin[P.n_tiles + idx] = ev * (q22 * ev);
     }
@@ -1175,6 +1229,7 @@ __global__ __launch_bounds__(64) void k_prior_eval(DevProblem P, int sel, int ga
 // optimization_algorithm_levenberg.cpp:61-169, and SparseOptimizer::optimize's iteration loop,
 // sparse_optimizer.cpp:360-400), log whether the trial relinearised, and publish the controller.
 __device__ void lm_decide(LMCtl& c, double chi_lin, double chi_trial, double scale, bool solved, int* hlog) {
+#pragma clang fp contract(off)   // round every operation like the host loop (no fused multiply-add)
     if (hlog) hlog[c.slot % HLOG_CAP] = (!c.done && c.need_lin) ? 1 : 0;
     c.slot++;
     if (c.done) return;
@@ -1317,8 +1372,8 @@ void launch_linearize(const DevProblem& P, int sel, int write_res, int gate, hip
     if (P.n_tiles) hipLaunchKernelGGL(k_linearize, dim3(P.n_tiles), dim3(TILE_OBS), 0, s, P, sel, write_res, gate);
 }
 void launch_prior_lin(const DevProblem& P, int sel, int gate, hipStream_t s) {
-    const int n = P.n_prior + P.n_vel;
-    if (n) hipLaunchKernelGGL(k_prior_lin, dim3(n), dim3(64), 0, s, P, sel, gate);
+    const int n = P.n_prior + P.n_vel + P.n_smp;
+    if (n) hipLaunchKernelGGL(k_prior_lin, dim3(n), dim3(PRI_THREADS), 0, s, P, sel, gate);
 }
 void launch_schur(const DevProblem& P, double lambda, int gate, hipStream_t s) {
     if (P.n_tiles) hipLaunchKernelGGL(k_schur, dim3(P.n_tiles), dim3(SCHUR_THREADS), 0, s, P, lambda, gate);

@@ -444,16 +444,13 @@ LBA_HD void project_residual(const double* Rwb, const double* twb, const CamD& c
     if (DIM == 3) e[2] = z[2] - (u - bf * (1.0 / Xc[2]));
 }
 
-// Jacobian rows of one reprojection observation (DIM = 2 mono, 3 stereo), columns
-// [KF_a pose(6) vel(6) | KF_b pose(6) vel(6) | point(3)] (27):
-//   J1 = P Rcb [I, -Xb^] (pose at the observation time), J_pt = -P Rcb Rwb^T
-//   GP edges: pose/vel columns = J1 N (N of the observation's GP sample, stored transposed);
-//   EdgeMono/EdgeStereo (src/G2oTypes.cc:445-495): KF_b pose columns = J1, velocity columns 0.
-// Output row r: pose/vel columns 0..23 at J[r*ldJ + c], point columns at J[r*ldJ + pcol + j]
-// (host harness: ldJ 27, pcol 24; kernels write straight into an LDS row buffer).
-template <int DIM, typename OutT, typename NT>
-LBA_HD void obs_jacobian(const double* Rwb, const CamD& c, const double* Xb, const double* Xc, double bf,
-                         const NT* N, OutT* J, int ldJ, int pcol) {
+// Jacobian rows of one reprojection observation (DIM = 2 mono, 3 stereo) w.r.t. the body pose at
+// the observation time and the point:
+//   J1 = P Rcb [I, -Xb^] (DIM x 6, row-major), J_pt = -P Rcb Rwb^T (DIM x 3)
+// (src/G2oTypes.cc:445-495; the GP edges chain J1 with their sample's factor N, see obs_jacobian).
+template <int DIM>
+LBA_HD void obs_j1(const double* Rwb, const CamD& c, const double* Xb, const double* Xc, double bf, double* J1,
+                   double* Jp) {
     // projection Jacobian P (DIM x 3)
     const double iz = 1.0 / Xc[2];
     double Pj[9];
@@ -461,7 +458,7 @@ LBA_HD void obs_jacobian(const double* Rwb, const CamD& c, const double* Xb, con
     Pj[3] = 0.0; Pj[4] = c.fy * iz; Pj[5] = -c.fy * Xc[1] / (Xc[2] * Xc[2]);
     if (DIM == 3) { Pj[6] = Pj[0]; Pj[7] = Pj[1]; Pj[8] = Pj[2] + bf * (1.0 / (Xc[2] * Xc[2])); }
     // M = P Rcb (DIM x 3);  J1 = [M, -M Xb^] ;  Jpt = -M Rwb^T
-    double M[3 * DIM], H[9], J1[6 * DIM];
+    double M[3 * DIM], H[9];
     for (int r = 0; r < DIM; ++r)
         for (int j = 0; j < 3; ++j)
             M[r * 3 + j] = Pj[r * 3 + 0] * c.Rcb[0 * 3 + j] + Pj[r * 3 + 1] * c.Rcb[1 * 3 + j] + Pj[r * 3 + 2] * c.Rcb[2 * 3 + j];
@@ -473,7 +470,21 @@ LBA_HD void obs_jacobian(const double* Rwb, const CamD& c, const double* Xb, con
         }
     for (int r = 0; r < DIM; ++r)
         for (int j = 0; j < 3; ++j)   // -M Rwb^T : (M Rbw)_{rj} = sum_k M_rk Rwb_jk
-            J[r * ldJ + pcol + j] = -(M[r * 3 + 0] * Rwb[j * 3 + 0] + M[r * 3 + 1] * Rwb[j * 3 + 1] + M[r * 3 + 2] * Rwb[j * 3 + 2]);
+            Jp[r * 3 + j] = -(M[r * 3 + 0] * Rwb[j * 3 + 0] + M[r * 3 + 1] * Rwb[j * 3 + 1] + M[r * 3 + 2] * Rwb[j * 3 + 2]);
+}
+
+// Full Jacobian rows, columns [KF_a pose(6) vel(6) | KF_b pose(6) vel(6) | point(3)] (27):
+//   GP edges: pose/vel columns = J1 N (N of the observation's GP sample, stored transposed);
+//   EdgeMono/EdgeStereo: KF_b pose columns = J1, velocity columns 0.
+// Output row r: pose/vel columns 0..23 at J[r*ldJ + c], point columns at J[r*ldJ + pcol + j]
+// (host harness: ldJ 27, pcol 24).  The kernels keep J1 and reduce in the sample's space instead.
+template <int DIM, typename OutT, typename NT>
+LBA_HD void obs_jacobian(const double* Rwb, const CamD& c, const double* Xb, const double* Xc, double bf,
+                         const NT* N, OutT* J, int ldJ, int pcol) {
+    double J1[6 * DIM], Jp[3 * DIM];
+    obs_j1<DIM>(Rwb, c, Xb, Xc, bf, J1, Jp);
+    for (int r = 0; r < DIM; ++r)
+        for (int j = 0; j < 3; ++j) J[r * ldJ + pcol + j] = Jp[r * 3 + j];
     if (!N) {
         for (int r = 0; r < DIM; ++r) {
             for (int j = 0; j < 12; ++j) J[r * ldJ + j] = 0.0;

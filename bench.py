@@ -44,14 +44,16 @@ def sweep_bytes(win):
 
 
 def sweep_flops(win):
-    """Algorithmic fp64 FLOPs of the sweep as this implementation formulates it:
-    per observation row-pair: residual (~60) + Jacobian (GP: J = J1 N, ~700; EdgeMono: ~150) +
-    the J^T W J products over the row's non-zero columns (GP row: 24 pose + e + 3 point columns,
-    ~812 FLOP; EdgeMono row: 12 pose columns, ~272 FLOP).  Stereo observations have 3 rows."""
+    """Algorithmic fp64 FLOPs of the sweep as this implementation formulates it: per
+    observation, residual (~60) and the Jacobian w.r.t. its pose sample and point (~150); per row,
+    the sample-space products M += s J1^T J1, g += s J1^T e (27 FMA), G += s J1^T Jp (18 FMA) and
+    Hll / bl (12 FMA); per (observation, KF side) the Hpl block N_side^T G (12 x 3 x 6 FMA).  The
+    24 x 24 expansion N^T M N happens once per pose sample (k_prior_lin), not per row."""
     k = win.obs["kind"]
     gp = np.isin(k, (0, 1))
     rows = np.where(np.isin(k, (1, 3)), 3, 2)
-    f = np.where(gp, 60 + 700 + 812 * rows, 60 + 150 + 272 * rows)
+    sides = np.where(gp, 2, 1)
+    f = 60 + 150 + 2 * (27 + 18 + 12) * rows + 2 * 216 * sides
     return float(f.sum())
 
 
