@@ -170,6 +170,7 @@ struct DevProblem {
     const int* chol_items;
     const int* h_steps;
     int n_steps;
+    int nd_left, nd_right;  // panels of the left / right blocks of the ordering (separator: the rest)
     double* LinvT;          // [npad / CHOL_NB][CHOL_NB][CHOL_NB] inverse diagonal blocks L_bb^-T (row-major)
     double* Hpl;
     double* Hll;
@@ -211,9 +212,10 @@ enum { ASM_SCHUR = 1, ASM_FULL = 2 };
 void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hipStream_t s);
 void launch_cholesky_solve(const DevProblem& P, int gate, hipStream_t s);
 void launch_update(const DevProblem& P, double lambda, int sel, int gate, hipStream_t s);
-void launch_eval(const DevProblem& P, int sel, int gate, hipStream_t s);
-enum { FIN_HOST = 0, FIN_QUEUED = 1, FIN_QUEUED_PUBLISH = 2, FIN_INITIAL = 3 };
+enum { FIN_NONE = -1, FIN_HOST = 0, FIN_QUEUED = 1, FIN_QUEUED_PUBLISH = 2, FIN_INITIAL = 3 };
 void launch_finalize(const DevProblem& P, unsigned long long seq, int mode, hipStream_t s);
+// residual evaluation of a state, then (mode != FIN_NONE) the trial summary (k_finalize)
+void launch_eval(const DevProblem& P, int sel, int gate, unsigned long long seq, int mode, hipStream_t s);
 void launch_ctl_init(const DevProblem& P, const LMCtl& c, hipStream_t s);
 void launch_lambda_init(const DevProblem& P, double tau, hipStream_t s);
 void launch_depth(const DevProblem& P, int sel, unsigned char* ok, hipStream_t s);

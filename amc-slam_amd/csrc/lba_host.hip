@@ -650,6 +650,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             if (len < best) { best = len; sa = a; sb = b; }
         }
         const int nl = sa, nr = NP - sb, ns = sb - sa;
+        D.nd_left = nl;
+        D.nd_right = nr;
         std::vector<int> ppos(NP), pnat(NP);
         for (int P = 0; P < NP; ++P)
             ppos[P] = P < sa ? P : (P >= sb ? nl + (P - sb) : nl + nr + (P - sa));
@@ -723,7 +725,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     const int nchi = n_tiles + D.n_prior + D.n_vel;
     D.chi_lin = dalloc<double>(p, nchi + 1);
     D.chi_eval = dalloc<double>(p, nchi + 1);
-    D.n_upd_blocks = (n_kf + nl + 255) / 256;
+    D.n_upd_blocks = (n_kf + nl + 63) / 64;   // k_update: UPD_THREADS (64) per block
     if (D.n_upd_blocks == 0) D.n_upd_blocks = 1;
     D.scale_part = dalloc<double>(p, D.n_upd_blocks);
     D.info = dalloc<int>(p, 1);
@@ -776,9 +778,11 @@ void wait_seq(lba_problem* p, unsigned long long seq) {
 // polling its sequence number; the stream is queried now and then so a device fault is reported
 // instead of spinning forever.  sync: also synchronise the stream (callers that copy device
 // buffers afterwards, or read timing events).
-void finalize_and_wait(lba_problem* p, bool sync) {
+// eval_sel >= 0: evaluate that state buffer first (k_eval).
+void finalize_and_wait(lba_problem* p, bool sync, int eval_sel = -1) {
     const unsigned long long seq = ++p->fin_seq;
-    launch_finalize(p->D, seq, 0, p->stream);
+    if (eval_sel >= 0) launch_eval(p->D, eval_sel, GATE_NONE, seq, FIN_HOST, p->stream);
+    else launch_finalize(p->D, seq, FIN_HOST, p->stream);
     HIPCHK(hipGetLastError());
     wait_seq(p, seq);
     if (sync) HIPCHK(hipStreamSynchronize(p->stream));
@@ -806,19 +810,15 @@ void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs, bool s
     launch_cholesky_solve(D, GATE_NONE, p->stream);
     if (evs) HIPCHK(hipEventRecord(evs[1], p->stream));
     launch_update(D, lambda, p->cur, GATE_NONE, p->stream);
-    if (evaluate) {
-        launch_gp_prep(D, nx, 0, GATE_NONE, p->stream);
-        launch_eval(D, nx, GATE_NONE, p->stream);
-    }
+    if (evaluate) launch_gp_prep(D, nx, 0, GATE_NONE, p->stream);
+    finalize_and_wait(p, sync || evs, evaluate ? nx : -1);
     if (evs) HIPCHK(hipEventRecord(evs[2], p->stream));
-    finalize_and_wait(p, sync || evs);
 }
 
 double eval_current(lba_problem* p) {
     const DevProblem& D = p->D;
     launch_gp_prep(D, p->cur, 0, GATE_NONE, p->stream);
-    launch_eval(D, p->cur, GATE_NONE, p->stream);
-    finalize_and_wait(p, true);
+    finalize_and_wait(p, true, p->cur);
     return p->h_fin[1];
 }
 
@@ -872,8 +872,7 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
     launch_ctl_init(D, c, p->stream);
     // starting state: poses + GP samples (with the Jacobian factors the first linearisation uses), chi2
     launch_gp_prep(D, p->cur, 1, GATE_NONE, p->stream);
-    launch_eval(D, p->cur, GATE_NONE, p->stream);
-    launch_finalize(D, 0, FIN_INITIAL, p->stream);
+    launch_eval(D, p->cur, GATE_NONE, 0, FIN_INITIAL, p->stream);
     int issued = 0;
     const LMCtl* hc = reinterpret_cast<const LMCtl*>(p->h_fin + 8);
     while (true) {
@@ -902,8 +901,8 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
             launch_cholesky_solve(D, GATE_NONE, p->stream);
             launch_update(D, LAMBDA_CTL, SEL_CUR, GATE_TRIAL, p->stream);
             launch_gp_prep(D, SEL_NEXT, 0, GATE_NONE, p->stream);
-            launch_eval(D, SEL_NEXT, GATE_NONE, p->stream);
-            launch_finalize(D, ++p->fin_seq, k == n - 1 ? FIN_QUEUED_PUBLISH : FIN_QUEUED, p->stream);
+            launch_eval(D, SEL_NEXT, GATE_NONE, ++p->fin_seq, k == n - 1 ? FIN_QUEUED_PUBLISH : FIN_QUEUED,
+                        p->stream);
             HIPCHK(hipGetLastError());
         }
         if (std::getenv("LBA_ENQ_TIMING"))

@@ -175,32 +175,117 @@ __device__ __forceinline__ double eval_obs(const DevProblem& P, const double* ks
 }
 
 // ------------------------------------------------------------------------------------------------
-// GP pose samples: one workgroup per GP pair builds the pair quantities once (lane 0, into LDS),
-// then one lane per sample of that pair evaluates the interpolated pose and (jac) the Jacobian
-// factor N.  Trailing workgroups write the KF poses used by the non-GP edges.
+// GP pose samples: one workgroup per GP pair.  The pair quantities (gp_pair_build) and the per-sample
+// factor N (gp_sample_build) are computed with the same per-output operation order as those serial
+// functions, but spread over the wave: lane 0 the SE(3) log, then lanes 0-2 Jr^-1, Ad(exp(xi12))^-1
+// and ad(v2) side by side, one lane per 6x6 product entry, one lane per sample for its pose /
+// Jr / Ad(exp(-xi)), one lane per (sample, row, column) of N.  Trailing workgroups write the KF pose
+// records.
 constexpr int PREP_THREADS = 64;
+constexpr int PREP_SCHUNK = 16;   // samples per pass (LDS staging of their Jr / Ad blocks)
 __global__ __launch_bounds__(PREP_THREADS) void k_gp_prep(DevProblem P, int sel, int jac, int gate) {
     __shared__ GPPair pr;
+    __shared__ double AdI[36], ad2[36], vbs[6];
+    __shared__ double sJr[PREP_SCHUNK][36], sRm[PREP_SCHUNK][9], stR[PREP_SCHUNK][9], sg[PREP_SCHUNK][3];
     const int tid = threadIdx.x;
     if (gated_off(P.ctl, gate)) return;
     const double* __restrict__ kst = P.kbuf[state_idx(P, sel)];
     if ((int)blockIdx.x < P.n_gp) {
         const int i = blockIdx.x;
+        const double* ka = kst + (size_t)P.gp_kfa[i] * KF_STRIDE;
+        const double* kb = kst + (size_t)P.gp_kfb[i] * KF_STRIDE;
         if (tid == 0) {
-            const double* ka = kst + (size_t)P.gp_kfa[i] * KF_STRIDE;
-            const double* kb = kst + (size_t)P.gp_kfb[i] * KF_STRIDE;
-            gp_pair_build(load_se3(ka), ka + 7, load_se3(kb), kb + 7, ka[13], kb[13], &pr, jac != 0);
+            const SE3 Ta = load_se3(ka), Tb = load_se3(kb);
+            pr.T1q[0] = Ta.q.x; pr.T1q[1] = Ta.q.y; pr.T1q[2] = Ta.q.z; pr.T1q[3] = Ta.q.w;
+            for (int j = 0; j < 3; ++j) pr.T1t[j] = Ta.t[j];
+            for (int j = 0; j < 6; ++j) pr.v1[j] = ka[7 + j];
+            pr.t1 = ka[13];
+            pr.t2 = kb[13];
+            const SE3 T12 = se3_mul(se3_inv(Ta), Tb);
+            se3_log(T12, pr.xi12);
+        }
+        if (tid < 6) vbs[tid] = kb[7 + tid];
+        __syncthreads();
+        if (tid == 0) {
+            right_jac_inv(pr.xi12, pr.G2a);                 // C = Jr^-1(xi12)
+        } else if (jac && tid == 1) {
+            const SE3 E = se3_exp(pr.xi12);                 // Ad(exp(xi12))^-1 = Ad(exp(xi12)^-1)
+            se3_adj(se3_inv(E), AdI);
+        } else if (jac && tid == 2) {
+            se3_ad(vbs, ad2);
         }
         __syncthreads();
-        for (int sidx = P.gp_s0[i] + tid; sidx < P.gp_s0[i + 1]; sidx += PREP_THREADS) {
-            GPSample* S = reinterpret_cast<GPSample*>(P.gps + (size_t)sidx * GPS_STRIDE);
-            if (jac) {
-                gp_sample_build(pr, P.gps_t[sidx], S);
-            } else {
+        if (tid < 6) {                                      // w2 = Jr^-1(xi12) v2
+            double w = 0.0;
+            for (int l = 0; l < 6; ++l) w += pr.G2a[tid * 6 + l] * vbs[l];
+            pr.w2[tid] = w;
+        }
+        if (jac && tid < 36) {                              // A1 = -C Ad^-1
+            const int r = tid / 6, c = tid % 6;
+            double v = 0.0;
+            for (int l = 0; l < 6; ++l) v += pr.G2a[r * 6 + l] * AdI[l * 6 + c];
+            pr.G1a[tid] = -v;
+        }
+        __syncthreads();
+        if (jac)
+            for (int t = tid; t < 72; t += PREP_THREADS) {   // B1 = -1/2 ad(v2) A1, D = -1/2 ad(v2) C
+                const int e = t % 36, r = e / 6, c = e % 6;
+                const double* src = t < 36 ? pr.G1a : pr.G2a;
+                double v = 0.0;
+                for (int l = 0; l < 6; ++l) v += ad2[r * 6 + l] * src[l * 6 + c];
+                (t < 36 ? pr.G1b : pr.G2b)[e] = v * -0.5;
+            }
+        __syncthreads();
+        for (int c0 = P.gp_s0[i]; c0 < P.gp_s0[i + 1]; c0 += PREP_SCHUNK) {
+            const int ns = min(PREP_SCHUNK, P.gp_s0[i + 1] - c0);
+            if (tid < ns) {
+                GPSample* S = reinterpret_cast<GPSample*>(P.gps + (size_t)(c0 + tid) * GPS_STRIDE);
                 double xi[6];
                 GPScalars g;
-                gp_sample_pose(pr, P.gps_t[sidx], S->Rwb, S->twb, xi, &g);
+                gp_sample_pose(pr, P.gps_t[c0 + tid], S->Rwb, S->twb, xi, &g);
+                if (jac) {
+                    double Jl[9], Q[9];                     // Jr(xi) = [Jl, Q; 0, Jl]
+                    right_jac_blocks(xi, Jl, Q);
+                    for (int r = 0; r < 3; ++r)
+                        for (int c = 0; c < 3; ++c) {
+                            sJr[tid][r * 6 + c] = Jl[r * 3 + c];
+                            sJr[tid][r * 6 + 3 + c] = Q[r * 3 + c];
+                            sJr[tid][(3 + r) * 6 + c] = 0.0;
+                            sJr[tid][(3 + r) * 6 + 3 + c] = Jl[r * 3 + c];
+                        }
+                    const double mxi[6] = {-xi[0], -xi[1], -xi[2], -xi[3], -xi[4], -xi[5]};
+                    const SE3 Em = se3_exp(mxi);            // Ad(exp(-xi)) = [R', t'^ R'; 0, R']
+                    double Ht[9];
+                    qmat(Em.q, sRm[tid]);
+                    hat3(Em.t, Ht);
+                    mul33(Ht, sRm[tid], stR[tid]);
+                    sg[tid][0] = g.l1; sg[tid][1] = g.l2; sg[tid][2] = g.p2;
+                }
             }
+            __syncthreads();
+            if (jac)
+                for (int t = tid; t < ns * 36; t += PREP_THREADS) {   // one (row, column) of each N block
+                    const int sl = t / 36, r = (t % 36) / 6, c = t % 6;
+                    const double l1 = sg[sl][0], l2 = sg[sl][1], p2 = sg[sl][2];
+                    const double* Jr = sJr[sl];
+                    double na = 0.0, nb = 0.0, nc = 0.0;
+                    for (int l = 0; l < 6; ++l) {
+                        const double ma = l1 * pr.G1a[l * 6 + c] + l2 * pr.G1b[l * 6 + c];
+                        const double mc = l1 * pr.G2a[l * 6 + c] + l2 * pr.G2b[l * 6 + c];
+                        na += Jr[r * 6 + l] * ma;
+                        nb += Jr[r * 6 + l] * mc;
+                        nc += Jr[r * 6 + l] * pr.G2a[l * 6 + c];
+                    }
+                    double ad = 0.0;
+                    if (r < 3) ad = (c < 3) ? sRm[sl][r * 3 + c] : stR[sl][r * 3 + c - 3];
+                    else if (c >= 3) ad = sRm[sl][(r - 3) * 3 + c - 3];
+                    double* N = P.gps + (size_t)(c0 + sl) * GPS_STRIDE + 12;
+                    N[c * 6 + r] = na + ad;
+                    N[(6 + c) * 6 + r] = p2 * Jr[r * 6 + c];
+                    N[(12 + c) * 6 + r] = nb;
+                    N[(18 + c) * 6 + r] = l2 * nc;
+                }
+            __syncthreads();
         }
         return;
     }
@@ -543,18 +628,19 @@ __global__ __launch_bounds__(PRI_THREADS) void k_prior_lin(DevProblem P, int sel
 }
 
 // Landmark elimination for one tile of landmarks (BlockSolver::solve's Schur loop,
-// block_solver.hpp:381-430): Dinv = (Hll + lambda I)^-1 (Eigen 3x3 adjugate inverse) and
-// V = Hpl Dinv per (KF, landmark) pair into LDS; then for every KF pair (k1, k2) the tile's landmarks
-// couple, the S partial sum_m V(m,k1) Hpl(m,k2)^T as one fp64-MFMA product on one wave, K running
-// over the (pair, pair, landmark) triples of that KF pair; and per tile KF the rhs partial
-// sum_m V(m,k) bl_m.  Dinv is kept for the back-substitution.  Block 0 also clears the
-// factorisation status for the solve that follows, and the first blocks zero the envelope of S.
+// block_solver.hpp:381-430).  Per landmark, Dinv = (Hll + lambda I)^-1 (Eigen 3x3 adjugate inverse,
+// kept for the back-substitution in k_update) and, for the Schur terms, Hll + lambda I = L D L^T:
+// Dinv = L^-T D^-1 L^-1, so with W = Hpl L^-T (transformed in place in LDS, one array instead of
+// Hpl and V = Hpl Dinv) the S partial of a KF pair (k1, k2) the tile's landmarks couple is
+// sum_m W(m,k1) D_m^-1 W(m,k2)^T, one fp64-MFMA product on one wave with K running over the
+// (pair, pair, landmark) triples and D^-1 applied while loading the A operand; and the rhs partial
+// of a tile KF, sum_m V(m,k) bl_m = sum_m W(m,k) u_m with u = D^-1 L^-1 bl.  Block 0 also clears
+// the factorisation status for the solve that follows, and the first blocks zero the envelope of S.
 constexpr int SCHUR_THREADS = 512;
 
 __global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double lambda_arg, int gate) {
-    __shared__ double Hs[TILE_PAIRS * 36];
-    __shared__ double Vs[TILE_PAIRS * 36];
-    __shared__ double Dl[TILE_LMS * 12];   // Dinv (9) + bl (3) per landmark
+    __shared__ double Hs[TILE_PAIRS * 36];   // Hpl, then W = Hpl L^-T
+    __shared__ double Dl[TILE_LMS * 9];      // per landmark: L^-T terms l10, l21, l10 l21 - l20; D^-1 (3); u (3)
     __shared__ int slst[TILE_SLIST];
     __shared__ int sl0[TILE_SENT + 1];
     __shared__ short slot[TILE_LMS * TILE_KF];
@@ -607,9 +693,18 @@ __global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double la
         H[0] += lambda; H[4] += lambda; H[8] += lambda;   // setLambda on Hll (block_solver.hpp:580-587)
         inv3(H, D);
 #pragma unroll
-        for (int q = 0; q < 9; ++q) { Dl[tid * 12 + q] = D[q]; P.Dinv[(size_t)l * 9 + q] = D[q]; }
-#pragma unroll
-        for (int q = 0; q < 3; ++q) Dl[tid * 12 + 9 + q] = P.bl[(size_t)l * 3 + q];
+        for (int q = 0; q < 9; ++q) P.Dinv[(size_t)l * 9 + q] = D[q];
+        // H = L D L^T (unit lower L)
+        const double d0 = H[0], l10 = H[3] / d0, l20 = H[6] / d0;
+        const double d1 = H[4] - l10 * l10 * d0;
+        const double l21 = (H[7] - l20 * l10 * d0) / d1;
+        const double d2 = H[8] - l20 * l20 * d0 - l21 * l21 * d1;
+        const double b0 = P.bl[(size_t)l * 3], b1 = P.bl[(size_t)l * 3 + 1], b2 = P.bl[(size_t)l * 3 + 2];
+        const double y1 = b1 - l10 * b0, y2 = b2 - l20 * b0 - l21 * y1;   // L^-1 bl
+        double* o = Dl + tid * 9;
+        o[0] = l10; o[1] = l21; o[2] = l10 * l21 - l20;
+        o[3] = 1.0 / d0; o[4] = 1.0 / d1; o[5] = 1.0 / d2;
+        o[6] = b0 / d0; o[7] = y1 / d1; o[8] = y2 / d2;
     }
     __syncthreads();
     LBA_TMARK(P.tdbg_schur, 1);
@@ -622,13 +717,15 @@ __global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double la
         pm[t] = (signed char)m;
     }
     __syncthreads();
-    // ---- V = Hpl Dinv, one (pair, row) per task
+    // ---- W = Hpl L^-T in place, one (pair, row) per task:
+    //      L^-1 = [1 0 0; -l10 1 0; l10 l21 - l20, -l21, 1], w_a = sum_b h_b (L^-1)(a, b)
     for (int task = tid; task < npair * 12; task += NT) {
         const int t = task / 12, r = task - 12 * t;
-        const double* D = Dl + pm[t] * 12;
-        const double h0 = Hs[t * 36 + r * 3], h1 = Hs[t * 36 + r * 3 + 1], h2 = Hs[t * 36 + r * 3 + 2];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) Vs[t * 36 + r * 3 + a] = h0 * D[a] + h1 * D[3 + a] + h2 * D[6 + a];
+        const double* D = Dl + pm[t] * 9;
+        double* h = Hs + t * 36 + r * 3;
+        const double h0 = h[0], h1 = h[1], h2 = h[2];
+        h[1] = h1 - D[0] * h0;
+        h[2] = h2 - D[1] * h1 + D[2] * h0;
     }
     __syncthreads();
     LBA_TMARK(P.tdbg_schur, 2);
@@ -647,8 +744,8 @@ __global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double la
                     const int kk = k < nk ? k : 0;
                     const int mi = kk / 3, a = kk - 3 * mi;
                     const int code = slst[qb + mi];
-                    const int t1 = code & 255, t2 = (code >> 8) & 255;
-                    const double x = Vs[t1 * 36 + cr * 3 + a];
+                    const int t1 = code & 255, t2 = (code >> 8) & 255, m = code >> 16;
+                    const double x = Hs[t1 * 36 + cr * 3 + a] * Dl[m * 9 + 3 + a];
                     const double y = Hs[t2 * 36 + cr * 3 + a];
                     av[h] = ok ? x : 0.0;
                     bv[h] = ok ? y : 0.0;
@@ -674,9 +771,9 @@ __global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double la
         for (int m = 0; m < nlm; ++m) {
             const int t = slot[m * TILE_KF + l];
             if (t >= 0) {
-                const double* vv = Vs + t * 36 + r * 3;
-                const double* b = Dl + m * 12 + 9;
-                v += vv[0] * b[0] + vv[1] * b[1] + vv[2] * b[2];
+                const double* w = Hs + t * 36 + r * 3;
+                const double* u = Dl + m * 9 + 6;
+                v += w[0] * u[0] + w[1] * u[1] + w[2] * u[2];
             }
         }
         P.gpslab[(size_t)P.tkf_gslot[kf0 + l] * 12 + r] = v;
@@ -1014,7 +1111,11 @@ constexpr int CHOL_MAXN = 6144;
 constexpr int BS_GEMV = 640;                  // trailing-update threads (one prefetched column each per pass)
 constexpr int BS_THREADS = 64 + BS_GEMV;
 
-// L^T x = y, one workgroup, bottom block first (L row-major: a column of a block row is read
+// L^T x = y over the block range [lo, hi) of this workgroup (launch arguments per blockIdx), bottom
+// block first; the nested-dissection order makes the separator range one launch and the left / right
+// ranges two independent workgroups of the next (right rows have no entries in left columns, so
+// neither updates the other).  write_y: store the updated right-hand side below lo back for them.
+// Within a range (L row-major: a column of a block row is read
 // coalesced across the threads that own consecutive columns).  Wave 0
 // applies the block's inverse diagonal (L_bb^-T from k_chol_step: a 32-wide GEMV instead of a
 // 32-step substitution chain); the other waves apply the solved block to the rows above
@@ -1022,26 +1123,28 @@ constexpr int BS_THREADS = 64 + BS_GEMV;
 // double-buffered LDS tile) issued before the diagonal step, so load latency hides behind it.
 __global__ __launch_bounds__(BS_THREADS) void k_chol_backsolve(const double* __restrict__ Lm,
                                                                const double* __restrict__ LinvT, int n,
-                                                               const double* __restrict__ yv,
+                                                               double* __restrict__ yv,
                                                                double* __restrict__ out,
                                                                const int* __restrict__ pfirst,
                                                                const int* __restrict__ pnat,
                                                                unsigned long long* tdbg, const LMCtl* ctl,
-                                                               int gate) {
+                                                               int gate, int lo0, int hi0, int lo1, int hi1,
+                                                               int write_y) {
     __shared__ double y[CHOL_MAXN];
     __shared__ double Mb[2][CNB][CNB + 1];
     __shared__ double xb[CNB];
     const int tid = threadIdx.x, lane = tid & 63;
     const int nblk = n / CNB;
     const int k0 = tid - 64;
-    if (gated_off(ctl, gate)) return;
-    for (int t = tid; t < n; t += BS_THREADS) y[t] = yv[t];
+    const int lo = blockIdx.x ? lo1 : lo0, hi = blockIdx.x ? hi1 : hi0;
+    if (gated_off(ctl, gate) || hi <= lo) return;
+    for (int t = tid; t < hi * CNB; t += BS_THREADS) y[t] = yv[t];
     for (int t = tid; t < CNB * CNB; t += BS_THREADS)
-        Mb[(nblk - 1) & 1][t / CNB][t % CNB] = LinvT[(size_t)(nblk - 1) * CNB * CNB + t];
+        Mb[(hi - 1) & 1][t / CNB][t % CNB] = LinvT[(size_t)(hi - 1) * CNB * CNB + t];
     __syncthreads();
-    if (tdbg && tid == 0) tdbg[(size_t)nblk * 16] = clock64();
+    if (tdbg && tid == 0 && hi == nblk) tdbg[(size_t)nblk * 16] = clock64();
     constexpr int MPT = (CNB * CNB + BS_GEMV - 1) / BS_GEMV;   // next-tile elements per GEMV thread
-    for (int blk = nblk - 1; blk >= 0; --blk) {
+    for (int blk = hi - 1; blk >= lo; --blk) {
         const int r0 = blk * CNB;
         const int c0 = pfirst[blk] * CNB;   // the block's rows of L are zero left of its envelope
         if (tdbg && tid == 0) tdbg[(size_t)blk * 16] = clock64();
@@ -1066,7 +1169,7 @@ __global__ __launch_bounds__(BS_THREADS) void k_chol_backsolve(const double* __r
 #pragma unroll
                 for (int i = 0; i < CNB; ++i) pre[i] = col[(size_t)i * n];
             }
-            if (blk > 0) {   // next block's inverse diagonal tile -> the other LDS buffer
+            if (blk > lo) {   // next block's inverse diagonal tile -> the other LDS buffer
                 double mv[MPT];
 #pragma unroll
                 for (int u = 0; u < MPT; ++u) {
@@ -1104,10 +1207,12 @@ __global__ __launch_bounds__(BS_THREADS) void k_chol_backsolve(const double* __r
         }
         __syncthreads();
     }
+    if (write_y)
+        for (int t = tid; t < lo * CNB; t += BS_THREADS) yv[t] = y[t];
 }
 
 // ------------------------------------------------------------------------------------------------
-constexpr int UPD_THREADS = 256;
+constexpr int UPD_THREADS = 64;     // one landmark (or KF) per thread: many small blocks for latency hiding
 
 __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lambda_arg, int sel, int gate) {
     __shared__ double red[UPD_THREADS / 64];
@@ -1174,6 +1279,12 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
 }
 
 // ------------------------------------------------------------------------------------------------
+__device__ void prior_eval(const DevProblem& P, const double* __restrict__ kst, int idx);
+
+// Robust chi2 of the state: one workgroup per observation tile, then workgroups of TILE_OBS prior /
+// velocity edges.  (The trial summary stays a separate k_finalize launch: having the last workgroup
+// do it needs a device-scope release per workgroup, i.e. an L2 writeback each on this multi-XCD
+// part, measured 3x slower than the extra launch.)
 __global__ __launch_bounds__(TILE_OBS) void k_eval(DevProblem P, int sel, int gate) {
     __shared__ double red[TILE_OBS / 64];
     const int tile = blockIdx.x, tid = threadIdx.x;
@@ -1181,23 +1292,25 @@ __global__ __launch_bounds__(TILE_OBS) void k_eval(DevProblem P, int sel, int ga
     const int si = state_idx(P, sel);
     const double* __restrict__ kst = P.kbuf[si];
     const double* __restrict__ lst = P.lbuf[si];
-    double rho0 = 0.0;
-    if (tid < P.tile_nobs[tile]) {
-        const int o = P.tile_obs0[tile] + tid;
-        const int meta = P.ob_meta[o];
-        const int kind = meta & 15, cam = meta >> 4;
-        const bool gp = kind <= LBA_STEREO_GP;
-        rho0 = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? eval_obs<3>(P, kst, lst, o, cam, gp)
-                                                             : eval_obs<2>(P, kst, lst, o, cam, gp);
+    if (tile < P.n_tiles) {
+        double rho0 = 0.0;
+        if (tid < P.tile_nobs[tile]) {
+            const int o = P.tile_obs0[tile] + tid;
+            const int meta = P.ob_meta[o];
+            const int kind = meta & 15, cam = meta >> 4;
+            const bool gp = kind <= LBA_STEREO_GP;
+            rho0 = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? eval_obs<3>(P, kst, lst, o, cam, gp)
+                                                                 : eval_obs<2>(P, kst, lst, o, cam, gp);
+        }
+        const double s = block_sum<TILE_OBS>(rho0, red);
+        if (tid == 0) P.chi_eval[tile] = s;
+    } else {
+        prior_eval(P, kst, (tile - P.n_tiles) * TILE_OBS + tid);
     }
-    const double s = block_sum<TILE_OBS>(rho0, red);
-    if (tid == 0) P.chi_eval[tile] = s;
 }
 
-__global__ __launch_bounds__(64) void k_prior_eval(DevProblem P, int sel, int gate) {
-    const int idx = blockIdx.x * 64 + threadIdx.x;
-    if (gated_off(P.ctl, gate)) return;
-    const double* __restrict__ kst = P.kbuf[state_idx(P, sel)];
+// motion-prior / velocity edge idx: robust chi2 of the state kst into chi_eval
+__device__ void prior_eval(const DevProblem& P, const double* __restrict__ kst, int idx) {
     if (idx < P.n_prior) {
         const double* ka = kst + (size_t)P.pri_a[idx] * KF_STRIDE;
         const double* kb = kst + (size_t)P.pri_b[idx] * KF_STRIDE;
@@ -1274,18 +1387,18 @@ __device__ void lm_decide(LMCtl& c, double chi_lin, double chi_trial, double sca
 // mode (FIN_*): host-driven trial (publish the summary); queued trial (decide, and publish the
 // controller mirror when it is the last trial of a batch); starting-state evaluation of a queue
 // (chi2 only, into the controller)
-__global__ __launch_bounds__(256) void k_finalize(DevProblem P, unsigned long long seq, int mode) {
-    __shared__ double red[4];
+template <int NT>
+__device__ void finalize_body(const DevProblem& P, unsigned long long seq, int mode, double* red) {
     const int tid = threadIdx.x;
     const int nc = P.n_tiles + P.n_prior + P.n_vel;
     double a = 0.0, b = 0.0, c = 0.0;
-    for (int i = tid; i < nc; i += 256) { a += P.chi_lin[i]; b += P.chi_eval[i]; }
-    for (int i = tid; i < P.n_upd_blocks; i += 256) c += P.scale_part[i];
-    const double sa = block_sum<256>(a, red);
+    for (int i = tid; i < nc; i += NT) { a += P.chi_lin[i]; b += P.chi_eval[i]; }
+    for (int i = tid; i < P.n_upd_blocks; i += NT) c += P.scale_part[i];
+    const double sa = block_sum<NT>(a, red);
     __syncthreads();
-    const double sb = block_sum<256>(b, red);
+    const double sb = block_sum<NT>(b, red);
     __syncthreads();
-    const double sc = block_sum<256>(c, red);
+    const double sc = block_sum<NT>(c, red);
     if (tid != 0) return;
     const double v[4] = {sa, sb, sc, (double)(*P.info)};
     if (mode == FIN_INITIAL) {
@@ -1312,6 +1425,11 @@ __global__ __launch_bounds__(256) void k_finalize(DevProblem P, unsigned long lo
         __hip_atomic_store(reinterpret_cast<unsigned long long*>(P.hfin + 4), seq, __ATOMIC_RELEASE,
                            __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+__global__ __launch_bounds__(256) void k_finalize(DevProblem P, unsigned long long seq, int mode) {
+    __shared__ double red[4];
+    finalize_body<256>(P, seq, mode, red);
 }
 
 __global__ void k_ctl_init(DevProblem P, LMCtl c) {
@@ -1390,16 +1508,22 @@ void launch_cholesky_solve(const DevProblem& P, int gate, hipStream_t s) {
         hipLaunchKernelGGL(k_chol_step, dim3(h[3] - h[2]), dim3(256), 0, s, n, h[0], h[1], h[2], P.chol_items, P.S,
                            P.Lm, P.LinvT, P.xsol, P.yv, P.info, P.ctl, gate);
     }
-    hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(BS_THREADS), 0, s, P.Lm, P.LinvT, n, P.yv, P.xsol, P.pfirst,
-                       P.pnat, P.tdbg_bs, P.ctl, gate);
+    // back-substitution: separator positions [nl + nr, NP) first, then left [0, nl) and right
+    // [nl, nl + nr) side by side
+    const int NP = n / CHOL_NB, nl = P.nd_left, nr = P.nd_right;
+    if (nl + nr < NP)
+        hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(BS_THREADS), 0, s, P.Lm, P.LinvT, n, P.yv, P.xsol,
+                           P.pfirst, P.pnat, P.tdbg_bs, P.ctl, gate, nl + nr, NP, 0, 0, 1);
+    hipLaunchKernelGGL(k_chol_backsolve, dim3(nr > 0 ? 2 : 1), dim3(BS_THREADS), 0, s, P.Lm, P.LinvT, n, P.yv,
+                       P.xsol, P.pfirst, P.pnat, P.tdbg_bs, P.ctl, gate, 0, nl, nl, nl + nr, 0);
 }
 void launch_update(const DevProblem& P, double lambda, int sel, int gate, hipStream_t s) {
     hipLaunchKernelGGL(k_update, dim3(P.n_upd_blocks), dim3(UPD_THREADS), 0, s, P, lambda, sel, gate);
 }
-void launch_eval(const DevProblem& P, int sel, int gate, hipStream_t s) {
-    if (P.n_tiles) hipLaunchKernelGGL(k_eval, dim3(P.n_tiles), dim3(TILE_OBS), 0, s, P, sel, gate);
-    const int n = P.n_prior + P.n_vel;
-    if (n) hipLaunchKernelGGL(k_prior_eval, dim3(cdiv(n, 64)), dim3(64), 0, s, P, sel, gate);
+void launch_eval(const DevProblem& P, int sel, int gate, unsigned long long seq, int mode, hipStream_t s) {
+    const int nb = P.n_tiles + cdiv(P.n_prior + P.n_vel, TILE_OBS);
+    if (nb) hipLaunchKernelGGL(k_eval, dim3(nb), dim3(TILE_OBS), 0, s, P, sel, gate);
+    if (mode != FIN_NONE) launch_finalize(P, seq, mode, s);
 }
 void launch_finalize(const DevProblem& P, unsigned long long seq, int mode, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, P, seq, mode);
