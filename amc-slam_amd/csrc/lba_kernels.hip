@@ -1020,13 +1020,14 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int pa, int pb, int it
     }
     double row[CNB];
     if (panel >= 0) load_stacked(A, b, n, panel, other, stg[wave], lane, row);
-    const int tr = tid >> 4, tc = tid & 15;
-    const size_t ra = (size_t)ti * CNB + 2 * tr, ca = (size_t)tj * CNB + 2 * tc;
-    double a00 = 0.0, a01 = 0.0, a10 = 0.0, a11 = 0.0;
-    if (!diag_item) {
-        a00 = A[ra * n + ca]; a01 = A[ra * n + ca + 1];
-        a10 = A[(ra + 1) * n + ca]; a11 = A[(ra + 1) * n + ca + 1];
-    }
+    // this wave's 16 x 16 quadrant of A(i, j) in the v_mfma_f64_16x16x4 output layout: rows
+    // rb*16 + kq + 4q (q = 0..3), column cb*16 + lr
+    const int rb = wave >> 1, cb = wave & 1, lr = lane & 15, kq = lane >> 4;
+    const size_t ra = (size_t)ti * CNB + rb * 16 + kq, ca = (size_t)tj * CNB + cb * 16 + lr;
+    double aold[4] = {0.0, 0.0, 0.0, 0.0};
+    if (!diag_item)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) aold[q] = A[(ra + 4 * q) * n + ca];
     // ---- right-looking panel factorisation (piv_seq): the next pivot only needs lane j+1's own
     //      d = a(j+1, j+1) - l(j+1, j)^2, so every lane runs the rsq chain on its own value in VALU
     //      and the result is read from lane j+1, interleaved with this pivot's rank-1 update.  A
@@ -1066,23 +1067,22 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int pa, int pb, int it
     }
     if (diag_item) return;
     __syncthreads();
-    // ---- tile update A(i, j) -= sum over the step's panels of P_i P_j^T
+    // ---- tile update A(i, j) -= sum over the step's panels of P_i P_j^T: one 16 x 16 quadrant per
+    //      wave, v_mfma_f64_16x16x4 with K running over each panel's 32 columns
     {
-        double s00 = 0, s01 = 0, s10 = 0, s11 = 0;
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (!(mask & (1 << h))) continue;
             const double (*Pi)[CNB + 1] = Pt[2 * h];
             const double (*Qj)[CNB + 1] = (ti == tj) ? Pt[2 * h] : Pt[2 * h + 1];
-#pragma unroll 8
-            for (int k = 0; k < CNB; ++k) {
-                const double x0 = Pi[2 * tr][k], x1 = Pi[2 * tr + 1][k];
-                const double y0 = Qj[2 * tc][k], y1 = Qj[2 * tc + 1][k];
-                s00 += x0 * y0; s01 += x0 * y1; s10 += x1 * y0; s11 += x1 * y1;
-            }
+#pragma unroll
+            for (int k0 = 0; k0 < CNB; k0 += 4)
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Pi[rb * 16 + lr][k0 + kq], Qj[cb * 16 + lr][k0 + kq], acc,
+                                                           0, 0, 0);
         }
-        A[ra * n + ca] = a00 - s00; A[ra * n + ca + 1] = a01 - s01;
-        A[(ra + 1) * n + ca] = a10 - s10; A[(ra + 1) * n + ca + 1] = a11 - s11;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) A[(ra + 4 * q) * n + ca] = aold[q] - acc[q];
     }
     if (ti != tj) return;
     // ---- diagonal tile: publish the tile's rows of L for each panel and forward-substitute b_i
