@@ -889,18 +889,21 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
     return r;
 }
 
-// Panel pivot sequence, generated at compile time (pivot J, update step T, chain op OP) so every
-// row[] index is a constant.  Pivot J: l = row[J] r; column J by readlane; then the rank-1
-// update row[k] -= l cb[k] (k > J), with the next pivot's chain spread through it in source order
-// (the pins keep that order): d = row[J+1] - l^2 on lane J+1, rsq, two Newton steps
+// Panel pivot sequence over columns [J, E), generated at compile time (pivot J, update step T,
+// chain op OP) so every row[] index is a constant.  Pivot J: l = row[J] r; column J by readlane;
+// then the rank-1 update row[k] -= l cb[k] (J < k < E), with the next pivot's chain spread through it
+// in source order (the pins keep that order): d = row[J+1] - l^2 on lane J+1, rsq, two Newton steps
 // r <- r (1.5 - 0.5 d r^2), readlane of r from lane J+1 (op s after update step floor(s NF / 7)).
+// The panel is factored as two 16-column halves (piv_seq<0, 16>, cross_update, piv_seq<16, 32>), so
+// the pivots' readlane broadcasts cover 2 x 120 entries instead of 496; the 256 products between the
+// halves go through the matrix cores.
 struct Pivot {
     double lij, hh, c, m, u, rn;
 };
 
-template <int J, int T, int OP>
+template <int J, int E, int T, int OP>
 __device__ __forceinline__ void piv_chain(Pivot& x) {
-    constexpr int NF = CNB - 1 - J;
+    constexpr int NF = E - 1 - J;
     if constexpr (OP < 7) {
         if constexpr ((OP * NF) / 7 == T) {
             if constexpr (OP == 0 || OP == 3) { x.m = x.hh * x.c; pin(x.m); }
@@ -908,47 +911,75 @@ __device__ __forceinline__ void piv_chain(Pivot& x) {
             else if constexpr (OP == 2 || OP == 5) { x.c = x.c * x.u; pin(x.c); }
             else { x.rn = readlane_d(x.c, J + 1); pin(x.rn); }
         }
-        piv_chain<J, T, OP + 1>(x);
+        piv_chain<J, E, T, OP + 1>(x);
     }
 }
 
-template <int J, int... T>
+template <int J, int E, int... T>
 __device__ __forceinline__ void piv_update(double (&row)[CNB], const double (&cb)[CNB], Pivot& x,
                                            std::integer_sequence<int, T...>) {
-    constexpr int NF = CNB - 1 - J;
+    constexpr int NF = E - 1 - J;
     auto step = [&](auto tc) {
         constexpr int t = decltype(tc)::value;
         if constexpr (t < NF) {
             row[J + 1 + t] -= x.lij * cb[J + 1 + t];
             pin(row[J + 1 + t]);
         }
-        if constexpr (J + 1 < CNB) piv_chain<J, t, 0>(x);
+        if constexpr (J + 1 < E) piv_chain<J, E, t, 0>(x);
     };
     (step(std::integral_constant<int, T>{}), ...);
 }
 
-template <int J>
+template <int J, int E>
 __device__ __forceinline__ void piv_seq(double (&row)[CNB], double r, int lane, bool& bad) {
-    if constexpr (J < CNB) {
+    if constexpr (J < E) {
         Pivot x;
         x.lij = row[J] * r;   // lane J: sqrt(d); lanes > J: L(l, J)
         row[J] = x.lij;
         x.hh = 0.5; x.c = 1.0; x.m = 0.0; x.u = 0.0; x.rn = 1.0;
-        if constexpr (J + 1 < CNB) {
+        if constexpr (J + 1 < E) {
             const double own = row[J + 1] - x.lij * x.lij;
             bad = bad || (lane == J + 1 && !(own > 0.0));
             x.c = __builtin_amdgcn_rsq(own);
             x.hh = 0.5 * own;
         }
-        // column J of L_pp by readlane into SGPRs (an LDS broadcast costs (31 - J) doubles per lane
+        // column J of L_pp by readlane into SGPRs (an LDS broadcast costs (E - 1 - J) doubles per lane
         // of every factoring wave on the CU's shared LDS return path: no faster, measured)
         double cb[CNB];
 #pragma unroll
-        for (int k = J + 1; k < CNB; ++k) cb[k] = readlane_d(x.lij, k);
-        constexpr int NT = (CNB - 1 - J) > 0 ? (CNB - 1 - J) : 1;
-        piv_update<J>(row, cb, x, std::make_integer_sequence<int, NT>{});
-        piv_seq<J + 1>(row, x.rn, lane, bad);
+        for (int k = J + 1; k < E; ++k) cb[k] = readlane_d(x.lij, k);
+        constexpr int NT = (E - 1 - J) > 0 ? (E - 1 - J) : 1;
+        piv_update<J, E>(row, cb, x, std::make_integer_sequence<int, NT>{});
+        piv_seq<J + 1, E>(row, x.rn, lane, bad);
     }
+}
+
+// Between the halves: every stacked row's columns 16..31 -= (its columns 0..15) (rows 16..31's
+// columns 0..15)^T, i.e. A22 -= L21 L21^T and the tile rows' share, as 4 row tiles x 4 k-steps of
+// v_mfma_f64_16x16x4 on the wave's LDS staging buffer (columns 0..15 in, the product out through
+// columns 16..31).
+__device__ __forceinline__ void cross_update(double (&row)[CNB], double (*st)[CNB + 1], int lane) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) st[lane][c] = row[c];
+    wave_sync();
+    const int lr = lane & 15, kq = lane >> 4;
+    d4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        const double bv = st[16 + lr][4 * ks + kq];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(st[16 * t + lr][4 * ks + kq], bv, acc[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) st[16 * t + kq + 4 * q][16 + lr] = acc[t][q];
+    wave_sync();
+#pragma unroll
+    for (int c = 0; c < 16; ++c) row[16 + c] -= st[lane][16 + c];
 }
 
 // Load one wave's stacked 64 x 32 panel (rows 0..31: the diagonal block of panel p; rows 32..63:
@@ -996,12 +1027,15 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int pa, int pb, int it
                                                    double* __restrict__ A, double* __restrict__ Lm,
                                                    double* __restrict__ LinvT, double* __restrict__ b,
                                                    double* __restrict__ yv, int* info, const LMCtl* ctl,
-                                                   int gate) {
+                                                   int gate, unsigned long long* tdbg, int step) {
     __shared__ double stg[4][2 * CNB][CNB + 1];   // per factoring wave: its stacked panel, row-major
     __shared__ double Pt[4][CNB][CNB + 1];        // factored tile rows: [panel A i, panel A j, panel B i, panel B j]
     __shared__ double yp[2][CNB];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & (CNB - 1);
     if (gated_off(ctl, gate)) return;
+    // diagnostics: clock64 stamps of the step's last workgroup (a tile item), thread 0
+    unsigned long long* tm = (tdbg && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) ? tdbg + 16 * step : nullptr;
+    if (tm) tm[0] = clock64();
     const int it = items[it0 + blockIdx.x];
     const int ti = it & 1023, tj = (it >> 10) & 1023, mask = (it >> 20) & 3;
     const bool diag_item = (it >> 22) & 1;
@@ -1020,6 +1054,7 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int pa, int pb, int it
     }
     double row[CNB];
     if (panel >= 0) load_stacked(A, b, n, panel, other, stg[wave], lane, row);
+    if (tm) tm[1] = clock64();
     // this wave's 16 x 16 quadrant of A(i, j) in the v_mfma_f64_16x16x4 output layout: rows
     // rb*16 + kq + 4q (q = 0..3), column cb*16 + lr
     const int rb = wave >> 1, cb = wave & 1, lr = lane & 15, kq = lane >> 4;
@@ -1035,7 +1070,11 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int pa, int pb, int it
     //      their unused upper triangle.
     if (panel >= 0) {
         bool bad = lane == 0 && !(row[0] > 0.0);
-        piv_seq<0>(row, readlane_d(rsqrt_nr(row[0]), 0), lane, bad);
+        piv_seq<0, 16>(row, readlane_d(rsqrt_nr(row[0]), 0), lane, bad);
+        cross_update(row, stg[wave], lane);
+        bad = bad || (lane == 16 && !(row[16] > 0.0));
+        piv_seq<16, CNB>(row, readlane_d(rsqrt_nr(row[16]), 16), lane, bad);
+        if (tm) tm[2] = clock64();
         if (diag_item) {
             const size_t p0 = (size_t)panel * CNB;
             if (wave == 0) {
@@ -1067,6 +1106,7 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int pa, int pb, int it
     }
     if (diag_item) return;
     __syncthreads();
+    if (tm) tm[3] = clock64();
     // ---- tile update A(i, j) -= sum over the step's panels of P_i P_j^T: one 16 x 16 quadrant per
     //      wave, v_mfma_f64_16x16x4 with K running over each panel's 32 columns
     {
@@ -1084,6 +1124,7 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int pa, int pb, int it
 #pragma unroll
         for (int q = 0; q < 4; ++q) A[(ra + 4 * q) * n + ca] = aold[q] - acc[q];
     }
+    if (tm) tm[4] = clock64();
     if (ti != tj) return;
     // ---- diagonal tile: publish the tile's rows of L for each panel and forward-substitute b_i
 #pragma unroll
@@ -1506,7 +1547,7 @@ void launch_cholesky_solve(const DevProblem& P, int gate, hipStream_t s) {
     for (int st = 0; st < P.n_steps; ++st) {
         const int* h = P.h_steps + 4 * st;
         hipLaunchKernelGGL(k_chol_step, dim3(h[3] - h[2]), dim3(256), 0, s, n, h[0], h[1], h[2], P.chol_items, P.S,
-                           P.Lm, P.LinvT, P.xsol, P.yv, P.info, P.ctl, gate);
+                           P.Lm, P.LinvT, P.xsol, P.yv, P.info, P.ctl, gate, P.tdbg_chol, st);
     }
     // back-substitution: separator positions [nl + nr, NP) first, then left [0, nl) and right
     // [nl, nl + nr) side by side

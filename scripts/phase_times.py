@@ -15,9 +15,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "amc-slam_amd"))
 
-LIN_PHASES = ["obs residual+J -> LDS", "Hpp segments", "Hpl pairs", "Hll/bl"]
-SCHUR_PHASES = ["stage Hpl + lists + Dinv", "slot map + V", "S partials (MFMA)", "-", "rhs partials"]
-SHAPE = ["nobs", "nseg", "npair", "nlm", "nsent", "nkf"]
+LIN_PHASES = ["obs residual+J1 -> LDS", "sample M/g", "Hpl = N^T G", "Hll/bl"]
+SCHUR_PHASES = ["stage Hpl + lists + LDL", "slot map + W", "S partials (MFMA)", "-", "rhs partials"]
+SHAPE = ["nobs", "nsmp", "npair", "nlm", "nsent", "nkf"]
 
 
 def load(path):
@@ -72,11 +72,13 @@ def main():
     report("k_linearize", lin, LIN_PHASES, shape, out)
     report("k_schur", sch, SCHUR_PHASES, shape, out)
     if chol is not None:
-        npan = int((chol[:, 0] != 0).sum())
-        c = chol[:npan]
-        out.append(f"== k_chol_step (workgroup 0 of each of {npan} panels), cycles: load / pivots / update+store")
-        for i in range(npan):
-            out.append(f"   panel {i:3d}: {c[i, 1] - c[i, 0]:7d} {c[i, 2] - c[i, 1]:7d} {c[i, 3] - c[i, 2]:7d}")
+        nst = int((chol[:, 0] != 0).sum())
+        c = chol[:nst]
+        out.append(f"== k_chol_step (last workgroup of each of {nst} steps), cycles: load / pivots / barrier / update")
+        for i in range(nst):
+            out.append(f"   step {i:3d}: {c[i, 1] - c[i, 0]:7d} {c[i, 2] - c[i, 1]:7d} {c[i, 3] - c[i, 2]:7d} "
+                       f"{c[i, 4] - c[i, 3]:7d}")
+        npan = int((bs[:, 0] != 0).sum())
         nb = npan
         b = bs[:nb + 1]
         out.append(f"== k_chol_backsolve, cycles per block: diagonal solve / barrier wait / trailing GEMV")
