@@ -171,6 +171,17 @@ struct DevProblem {
     const int* h_steps;
     int n_steps;
     int nd_left, nd_right;  // panels of the left / right blocks of the ordering (separator: the rest)
+    // dataflow factorisation (k_chol_flow): tasks, tile ids, hand-off flags, ticket counter
+    const int* cf_tasks;
+    int cf_ntasks;
+    const int* cf_tbase;
+    const int* cf_pl0;
+    const int* cf_plist;
+    int* cf_lready;
+    int* cf_dready;
+    unsigned long long* cf_head;
+    int* cf_abort;
+    int cf_steps_path;      // LBA_CHOL_STEPS: the k_chol_step sequence instead
     double* LinvT;          // [npad / CHOL_NB][CHOL_NB][CHOL_NB] inverse diagonal blocks L_bb^-T (row-major)
     double* Hpl;
     double* Hll;
@@ -210,7 +221,7 @@ void launch_prior_lin(const DevProblem& P, int sel, int gate, hipStream_t s);
 void launch_schur(const DevProblem& P, double lambda, int gate, hipStream_t s);
 enum { ASM_SCHUR = 1, ASM_FULL = 2 };
 void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hipStream_t s);
-void launch_cholesky_solve(const DevProblem& P, int gate, hipStream_t s);
+void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s);
 void launch_update(const DevProblem& P, double lambda, int sel, int gate, hipStream_t s);
 enum { FIN_NONE = -1, FIN_HOST = 0, FIN_QUEUED = 1, FIN_QUEUED_PUBLISH = 2, FIN_INITIAL = 3 };
 void launch_finalize(const DevProblem& P, unsigned long long seq, int mode, hipStream_t s);

@@ -54,6 +54,7 @@ struct lba_problem {
     std::vector<int> chol_steps;  // dense-solve schedule: (panel A, panel B, first item, end item) per step
     int s_layout = 0;             // layout last assembled into S: 0 factorisation order, 1 natural (full)
     unsigned long long fin_seq = 0;
+    unsigned cf_epoch = 0;        // launches of the dataflow factorisation (its flags hold the epoch)
     double lambda = -1.0, ni = 2.0;
     int nBad = 0;
 };
@@ -688,6 +689,46 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         D.h_steps = p->chol_steps.data();
         D.n_steps = (int)steps.size() / 4;
         D.chol_items = dupload(p, items);
+        // dataflow factorisation (k_chol_flow): one task per envelope tile, in topological order
+        // (column by column, the diagonal tile first): task j | i << 12
+        {
+            std::vector<int> tbase(NP + 1, 0), tasks;
+            for (int i = 0; i < NP; ++i) tbase[i + 1] = tbase[i] + (i - pfh[i] + 1);
+            for (int j = 0; j < NP; ++j)
+                for (int i = j; i < NP; ++i)
+                    if (pfh[i] <= j) tasks.push_back(j | (i << 12));
+            if (NP > 4095) throw ApiError{LBA_E_LIMIT, "internal: too many panels for the dataflow factorisation"};
+            D.cf_tasks = dupload(p, tasks);
+            D.cf_ntasks = (int)tasks.size();
+            D.cf_tbase = dupload(p, tbase);
+            std::vector<int> uord;   // panel update order = the order the panels complete
+            for (int k = 0; k < std::max(nl, nr); ++k) {
+                if (k < nl) uord.push_back(k);
+                if (k < nr) uord.push_back(nl + k);
+            }
+            for (int k = 0; k < ns; ++k) uord.push_back(nl + nr + k);
+            std::vector<int> rank(NP), pl0(1, 0), plist;
+            for (int q = 0; q < NP; ++q) rank[uord[q]] = q;
+            for (int tcode : tasks) {   // per task: its panels p in [pfh[j], j) in update order
+                const int j = tcode & 4095, i = (tcode >> 12) & 4095;
+                std::vector<int> ps;
+                for (int pp = pfh[j]; pp < j; ++pp) ps.push_back(pp);
+                std::sort(ps.begin(), ps.end(), [&](int x, int y) { return rank[x] < rank[y]; });
+                for (int pp : ps) plist.push_back(pp | ((pp >= pfh[i]) << 12));
+                pl0.push_back((int)plist.size());
+            }
+            D.cf_pl0 = dupload(p, pl0);
+            D.cf_plist = dupload(p, plist);
+            D.cf_lready = dalloc<int>(p, std::max(tbase[NP], 1));
+            D.cf_dready = dalloc<int>(p, std::max(NP, 1));
+            D.cf_head = dalloc<unsigned long long>(p, 1);
+            D.cf_abort = dalloc<int>(p, 1);
+            HIPCHK(hipMemset(D.cf_lready, 0, sizeof(int) * std::max(tbase[NP], 1)));
+            HIPCHK(hipMemset(D.cf_dready, 0, sizeof(int) * std::max(NP, 1)));
+            HIPCHK(hipMemset(D.cf_head, 0, sizeof(unsigned long long)));
+            HIPCHK(hipMemset(D.cf_abort, 0, sizeof(int)));
+            D.cf_steps_path = std::getenv("LBA_CHOL_STEPS") ? 1 : 0;
+        }
         D.pfirst = dupload(p, pfh);
         D.ppos = dupload(p, ppos);
         D.pnat = dupload(p, pnat);
@@ -807,7 +848,7 @@ void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs, bool s
     launch_schur(D, lambda, GATE_NONE, p->stream);   // also clears the factorisation status
     assemble_layout(p, lambda, ASM_SCHUR);
     if (evs) HIPCHK(hipEventRecord(evs[0], p->stream));
-    launch_cholesky_solve(D, GATE_NONE, p->stream);
+    launch_cholesky_solve(D, GATE_NONE, ++p->cf_epoch, p->stream);
     if (evs) HIPCHK(hipEventRecord(evs[1], p->stream));
     launch_update(D, lambda, p->cur, GATE_NONE, p->stream);
     if (evaluate) launch_gp_prep(D, nx, 0, GATE_NONE, p->stream);
@@ -898,7 +939,7 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
             }
             launch_schur(D, LAMBDA_CTL, GATE_NONE, p->stream);
             assemble_layout(p, LAMBDA_CTL, ASM_SCHUR);
-            launch_cholesky_solve(D, GATE_NONE, p->stream);
+            launch_cholesky_solve(D, GATE_NONE, ++p->cf_epoch, p->stream);
             launch_update(D, LAMBDA_CTL, SEL_CUR, GATE_TRIAL, p->stream);
             launch_gp_prep(D, SEL_NEXT, 0, GATE_NONE, p->stream);
             launch_eval(D, SEL_NEXT, GATE_NONE, ++p->fin_seq, k == n - 1 ? FIN_QUEUED_PUBLISH : FIN_QUEUED,

@@ -655,7 +655,10 @@ __global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double la
     if (gated_off(P.ctl, gate)) return;
     const double lambda = damping(P, lambda_arg);
     LBA_TMARK(P.tdbg_schur, 0);
-    if (tile == 0 && tid == 0) *P.info = 0;
+    if (tile == 0 && tid == 0) {
+        *P.info = 0;
+        if (P.cf_head) *P.cf_head = 0;   // ticket counter of this trial's k_chol_flow
+    }
     // clear the envelope tiles of S for this trial's assembly (the previous factorisation left its
     // fill-in there); k_assemble runs after this kernel
     for (int z = tile; z < P.n_ztiles; z += gridDim.x) {
@@ -1148,6 +1151,296 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int pa, int pb, int it
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Dataflow factorisation of the permuted system in ONE launch (replaces the k_chol_step sequence).
+// One task per tile of the envelope, in a topological order (column by column) pulled from a ticket
+// counter, so progress never depends on which workgroups are resident or in what order they start:
+//   tile (i, j), i > j: keeps A(i, j) and its own copy of A(j, j) in registers (the
+//     v_mfma_f64_16x16x4 output layout, one 16 x 16 quadrant per wave); for every envelope panel
+//     p < j it waits for L(j, p) (and L(i, p) where row i reaches p) and applies
+//     A(i,j) -= L(i,p) L(j,p)^T, A(j,j) -= L(j,p) L(j,p)^T; then one wave factors the stacked
+//     [A(j,j); A(i,j)] (the k_chol_step two-level pivot sequence) and L(i, j) is published.  The
+//     copies of A(j, j) see the same updates in the same order, so they are bitwise identical;
+//   panel j (i = j): the same updates of A(j, j) and b_j -= L(j,p) y_p, then [A_jj; b_j^T] -> L_jj,
+//     y_j and [A_jj; I] -> L_jj^-T on two waves, published for the diagonal tasks below it.
+// The chain from one panel to the next is one hand-off, the last update and one factorisation.
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+typedef __attribute__((address_space(1))) int gi32_t;
+
+__device__ __forceinline__ double ld_sc1(const double* p) {
+    return __longlong_as_double((long long)__hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+    __hip_atomic_store((gu64_t*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr unsigned CF_SPIN_LIMIT = 1u << 22;   // ~0.5 s of polling before giving up (never expected)
+constexpr int CF_TIMEOUT = 0x7fff0000;          // *info value of a timed-out launch
+
+struct CholFlow {
+    int n, NP, ntasks;
+    unsigned epoch;
+    const int* tasks;    // j | i << 12 | kind << 24 (kind 0: panel j, 1: off-diagonal tile (i, j))
+    const int* pfh;      // envelope of the permuted matrix (first panel of each panel row)
+    const int* tbase;    // tile id of (i, pfh[i]); tile (i, j) = tbase[i] + j - pfh[i]
+    const int* pl0;      // per task: first entry of its update list in plist ([pl0[t], pl0[t+1]))
+    const int* plist;    // p | (row i takes part) << 12, in the order every task applies panel updates
+                         // (the order panels finish: left k and right k side by side, then the separator)
+    const double* S;     // assembled system (factorisation order, lower)
+    double* Lm;
+    double* LinvT;
+    const double* b;     // right-hand side (factorisation order)
+    double* yv;
+    int* info;
+    int* lready;         // per tile: epoch once L(i, j) is published
+    int* dready;         // per panel: epoch once L_jj^-T and y_j are published
+    unsigned long long* head;   // ticket counter (zeroed by k_schur ahead of every trial)
+    int* abort_flag;
+    unsigned long long* tdbg;   // diagnostics: per panel, s_memrealtime stamps of its task
+};
+
+// thread 0 polls up to two flags for `epoch` (relaxed, agent scope); the workgroup learns the result
+__device__ __forceinline__ bool cf_wait(const CholFlow& a, const int* f1, const int* f2, int* s_ok) {
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        const int* fs[2] = {f1, f2};
+        for (int q = 0; q < 2 && ok; ++q) {
+            if (!fs[q]) continue;
+            unsigned spins = 0;
+            while ((unsigned)__hip_atomic_load((gi32_t*)fs[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.epoch) {
+                if (++spins > CF_SPIN_LIMIT ||
+                    ((spins & 255) == 0 &&
+                     (unsigned)__hip_atomic_load((gi32_t*)a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch)) {
+                    __hip_atomic_store((gi32_t*)a.abort_flag, (int)a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    *a.info = CF_TIMEOUT;
+                    ok = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        *s_ok = ok;
+    }
+    __syncthreads();
+    return *s_ok != 0;
+}
+
+// non-blocking: are both flags (null = none) at `epoch`?  (thread 0 reads, the workgroup learns it)
+__device__ __forceinline__ bool cf_test(const CholFlow& a, const int* f1, const int* f2, int* s_ok) {
+    if (threadIdx.x == 0) {
+        bool ok = true;
+        if (f1) ok = ok && (unsigned)__hip_atomic_load((gi32_t*)f1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch;
+        if (f2) ok = ok && (unsigned)__hip_atomic_load((gi32_t*)f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch;
+        *s_ok = ok ? 1 : 0;
+    }
+    __syncthreads();
+    return *s_ok != 0;
+}
+
+// a 32 x 32 tile of handed-off data into registers (4 sc1 loads per thread), and from there to LDS
+__device__ __forceinline__ void cf_fetch(const double* src, int n, double (&r)[4]) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int e = threadIdx.x + 256 * m;
+        r[m] = ld_sc1(src + (size_t)(e >> 5) * n + (e & 31));
+    }
+}
+__device__ __forceinline__ void cf_put(double (*T)[CNB + 1], const double (&r)[4]) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int e = threadIdx.x + 256 * m;
+        T[e >> 5][e & 31] = r[m];
+    }
+}
+
+// every storing wave drains its sc1 stores, then one lane publishes the flag
+__device__ __forceinline__ void cf_publish(const CholFlow& a, int* flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store((gi32_t*)flag, (int)a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// 32 x 32 tile of a row-major matrix (leading dimension n) -> LDS, sc1 loads (handed-off data)
+__device__ __forceinline__ void cf_load_tile(const double* src, int n, double (*T)[CNB + 1]) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int e = threadIdx.x + 256 * m, r = e >> 5, c = e & 31;
+        T[r][c] = ld_sc1(src + (size_t)r * n + c);
+    }
+}
+
+// acc (this wave's quadrant) += X[rows of rb] Y[rows of cb]^T, K = 32
+__device__ __forceinline__ d4 cf_mma_nt(const double (*X)[CNB + 1], const double (*Y)[CNB + 1], int rb, int cb,
+                                        int lr, int kq, d4 acc) {
+#pragma unroll
+    for (int k0 = 0; k0 < CNB; k0 += 4)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(X[rb * 16 + lr][k0 + kq], Y[cb * 16 + lr][k0 + kq], acc, 0, 0, 0);
+    return acc;
+}
+// acc += X[rows of rb] Y[:, columns of cb], K = 32
+__device__ __forceinline__ d4 cf_mma_nn(const double (*X)[CNB + 1], const double (*Y)[CNB + 1], int rb, int cb,
+                                        int lr, int kq, d4 acc) {
+#pragma unroll
+    for (int k0 = 0; k0 < CNB; k0 += 4)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(X[rb * 16 + lr][k0 + kq], Y[k0 + kq][cb * 16 + lr], acc, 0, 0, 0);
+    return acc;
+}
+
+__global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
+    __shared__ double Lt[2][CNB][CNB + 1];       // update operands L(i, p), L(j, p)
+    __shared__ double stg[2][2 * CNB][CNB + 1];  // stacked panels of the factoring waves
+    __shared__ double bs[CNB], ys[CNB];
+    __shared__ long long s_ticket;
+    __shared__ int s_ok;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int rb = wave >> 1, cb = wave & 1, lr = lane & 15, kq = lane >> 4;
+    const int n = a.n;
+    auto tile_id = [&](int i, int j) { return a.tbase[i] + j - a.pfh[i]; };
+    auto load_quad = [&](int i, int j, double (&q)[4]) {   // plain loads: S is not written in this launch
+#pragma unroll
+        for (int m = 0; m < 4; ++m) q[m] = a.S[(size_t)(i * CNB + rb * 16 + kq + 4 * m) * n + j * CNB + cb * 16 + lr];
+    };
+    auto stage_quad = [&](double (*T)[CNB + 1], int r0, const double (&q)[4]) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) T[r0 + rb * 16 + kq + 4 * m][cb * 16 + lr] = q[m];
+    };
+    auto sub_mma = [&](double (&q)[4], d4 p) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) q[m] -= p[m];
+    };
+    // one wave: two-level pivot sequence of its stacked panel in `st` (row r of lane r)
+    auto factor = [&](double (*st)[CNB + 1], bool& bad) {
+        double row[CNB];
+#pragma unroll
+        for (int c = 0; c < CNB; ++c) row[c] = st[lane][c];
+        bad = lane == 0 && !(row[0] > 0.0);
+        piv_seq<0, 16>(row, readlane_d(rsqrt_nr(row[0]), 0), lane, bad);
+        cross_update(row, st, lane);
+        bad = bad || (lane == 16 && !(row[16] > 0.0));
+        piv_seq<16, CNB>(row, readlane_d(rsqrt_nr(row[16]), 16), lane, bad);
+#pragma unroll
+        for (int c = 0; c < CNB; ++c) st[lane][c] = row[c];
+        wave_sync();
+    };
+    const d4 z4 = {0.0, 0.0, 0.0, 0.0};
+    while (true) {
+        if (tid == 0) s_ticket = (long long)atomicAdd(a.head, 1ull);
+        __syncthreads();
+        const long long t = s_ticket;
+        __syncthreads();
+        if (t >= a.ntasks) break;
+        const int code = a.tasks[t];
+        const int j = code & 4095, i = (code >> 12) & 4095;
+        const bool diag = i == j;
+        // diagnostics: stamps of panel j's task (slots 0..6) and of tile (j + 1, j) (slots 8..14)
+        unsigned long long* tm = (a.tdbg && tid == 0 && (diag || i == j + 1)) ? a.tdbg + 16 * j + (diag ? 0 : 8) : nullptr;
+        if (tm) tm[0] = __builtin_amdgcn_s_memrealtime();
+        double qd[4], qa[4];
+        load_quad(j, j, qd);
+        if (!diag) load_quad(i, j, qa);
+        if (diag && tid < CNB) bs[tid] = a.b[j * CNB + tid];
+        // ---- updates from the envelope panels p < j, software-pipelined (the next panel's tiles are
+        //      fetched into registers when already published, while this panel's products run)
+        const int pj = a.pfh[j], pi = diag ? pj : a.pfh[i];
+        double rj[4], ri[4], ry = 0.0;
+        bool have = false;
+        auto ready = [&](int p, bool block) {
+            const int* f1 = a.lready + tile_id(j, p);
+            const int* f2 = diag ? a.dready + p : (p >= pi ? a.lready + tile_id(i, p) : nullptr);
+            return block ? cf_wait(a, f1, f2, &s_ok) : cf_test(a, f1, f2, &s_ok);
+        };
+        auto fetch = [&](int p) {
+            cf_fetch(a.Lm + (size_t)(j * CNB) * n + p * CNB, n, rj);
+            if (!diag && p >= pi) cf_fetch(a.Lm + (size_t)(i * CNB) * n + p * CNB, n, ri);
+            if (diag && tid < CNB) ry = ld_sc1(a.yv + p * CNB + tid);
+        };
+        bool ok = true;
+        // the panels p in [pj, j) in update order (the same order in every task: the copies of A_jj
+        // stay bitwise identical)
+        const int q0 = a.pl0[t], q1 = a.pl0[t + 1];
+        for (int q = q0; q < q1; ++q) {
+            const int p = a.plist[q] & 4095;
+            if (!have) {
+                if (!ready(p, true)) { ok = false; break; }
+                fetch(p);
+            }
+            cf_put(Lt[0], rj);
+            if (!diag && p >= pi) cf_put(Lt[1], ri);
+            if (diag && tid < CNB) ys[tid] = ry;
+            __syncthreads();
+            have = q + 1 < q1 && ready(a.plist[q + 1] & 4095, false);
+            if (have) fetch(a.plist[q + 1] & 4095);
+            sub_mma(qd, cf_mma_nt(Lt[0], Lt[0], rb, cb, lr, kq, z4));
+            if (!diag && p >= pi) sub_mma(qa, cf_mma_nt(Lt[1], Lt[0], rb, cb, lr, kq, z4));
+            if (diag && tid < CNB) {   // b_j -= L(j, p) y_p
+                double sacc = 0.0;
+#pragma unroll 8
+                for (int c = 0; c < CNB; ++c) sacc += Lt[0][tid][c] * ys[c];
+                bs[tid] -= sacc;
+            }
+            __syncthreads();
+        }
+        if (!ok) return;
+        if (tm) tm[1] = __builtin_amdgcn_s_memrealtime();
+        const size_t p0 = (size_t)j * CNB;
+        if (!diag) {
+            // ---- [A(j,j); A(i,j)] on wave 0 -> L(i, j) (rows 32..63)
+            stage_quad(stg[0], 0, qd);
+            stage_quad(stg[0], CNB, qa);
+            __syncthreads();
+            if (tm) tm[4] = __builtin_amdgcn_s_memrealtime();
+            if (wave == 0) {
+                bool bad;
+                factor(stg[0], bad);
+                if (tm) tm[5] = __builtin_amdgcn_s_memrealtime();
+                (void)bad;   // (a non-positive pivot of A(j,j) is reported by panel j's own task)
+#pragma unroll
+                for (int m = 0; m < 16; ++m) {
+                    const int e = lane + 64 * m, r = e >> 5, c = e & 31;
+                    st_sc1(a.Lm + (size_t)(i * CNB + r) * n + p0 + c, stg[0][CNB + r][c]);
+                }
+            }
+            cf_publish(a, a.lready + tile_id(i, j));
+            if (tm) tm[6] = __builtin_amdgcn_s_memrealtime();
+            continue;
+        }
+        // ---- panel j: wave 0 [A_jj; b_j^T] -> L_jj, y_j; wave 1 [A_jj; I] -> L_jj^-T
+        stage_quad(stg[0], 0, qd);
+        stage_quad(stg[1], 0, qd);
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {   // rows 32..63: b_j^T then zeros / the identity
+            const int e = tid + 256 * m, r = e >> 5, c = e & 31;
+            stg[0][CNB + r][c] = (r == 0) ? bs[c] : 0.0;
+            stg[1][CNB + r][c] = (c == r) ? 1.0 : 0.0;
+        }
+        __syncthreads();
+        if (tm) tm[4] = __builtin_amdgcn_s_memrealtime();
+        if (wave < 2) {
+            bool bad;
+            factor(stg[wave], bad);
+            if (__ballot(bad) != 0 && wave == 0 && lane == 0) *a.info = 1 + (int)p0;
+            if (wave == 0) {   // L_jj (plain: read by the back-substitution launch only), y_j
+#pragma unroll
+                for (int m = 0; m < 16; ++m) {
+                    const int e = lane + 64 * m, r = e >> 5, c = e & 31;
+                    a.Lm[(p0 + r) * n + p0 + c] = (c <= r) ? stg[0][r][c] : 0.0;
+                }
+                if (lane < CNB) st_sc1(a.yv + p0 + lane, stg[0][CNB][lane]);
+            } else {           // L_jj^-T
+#pragma unroll
+                for (int m = 0; m < 16; ++m) {
+                    const int e = lane + 64 * m;
+                    st_sc1(a.LinvT + p0 * CNB + e, stg[1][CNB + (e >> 5)][e & 31]);
+                }
+            }
+        }
+        if (tm) tm[5] = __builtin_amdgcn_s_memrealtime();
+        cf_publish(a, a.dready + j);
+        if (tm) tm[6] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
 constexpr int CHOL_MAXN = 6144;
 constexpr int BS_GEMV = 640;                  // trailing-update threads (one prefetched column each per pass)
 constexpr int BS_THREADS = 64 + BS_GEMV;
@@ -1541,10 +1834,20 @@ void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hi
     const int n = P.n_asm + P.n_pb;
     if (n) hipLaunchKernelGGL(k_assemble, dim3(n), dim3(144 * RED_GROUPS), 0, s, P, lambda, flags, gate);
 }
-void launch_cholesky_solve(const DevProblem& P, int gate, hipStream_t s) {
+void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s) {
     const int n = P.npad;   // multiple of CHOL_NB (identity tail)
     if (n == 0) return;
-    for (int st = 0; st < P.n_steps; ++st) {
+    if (!P.cf_steps_path) {
+        CholFlow a;
+        a.n = n; a.NP = n / CHOL_NB; a.ntasks = P.cf_ntasks; a.epoch = epoch;
+        a.tasks = P.cf_tasks; a.pfh = P.pfirst; a.tbase = P.cf_tbase; a.pl0 = P.cf_pl0;
+        a.plist = P.cf_plist;
+        a.S = P.S; a.Lm = P.Lm; a.LinvT = P.LinvT; a.b = P.xsol; a.yv = P.yv; a.info = P.info;
+        a.lready = P.cf_lready; a.dready = P.cf_dready; a.head = P.cf_head; a.abort_flag = P.cf_abort;
+        a.tdbg = P.tdbg_chol;
+        hipLaunchKernelGGL(k_chol_flow, dim3(min(P.cf_ntasks, 512)), dim3(256), 0, s, a);
+    }
+    for (int st = 0; P.cf_steps_path && st < P.n_steps; ++st) {
         const int* h = P.h_steps + 4 * st;
         hipLaunchKernelGGL(k_chol_step, dim3(h[3] - h[2]), dim3(256), 0, s, n, h[0], h[1], h[2], P.chol_items, P.S,
                            P.Lm, P.LinvT, P.xsol, P.yv, P.info, P.ctl, gate, P.tdbg_chol, st);

@@ -72,6 +72,19 @@ def main():
     report("k_linearize", lin, LIN_PHASES, shape, out)
     report("k_schur", sch, SCHUR_PHASES, shape, out)
     if chol is not None:
+        if os.environ.get("LBA_CHOL_STEPS") is None:   # k_chol_flow: s_memrealtime (100 MHz) stamps per panel
+            npan = int((chol[:, 0] != 0).sum())
+            c = chol[:npan].astype(np.int64)
+            t0 = c[:, 0].min()
+            out.append(f"== k_chol_flow panels (us from the first panel task start): start / own updates done / "
+                       f"- / - / factor start / factor end / published")
+            for j in range(npan):
+                v = [(c[j, k] - t0) / 100.0 if c[j, k] else float("nan") for k in range(7)]
+                out.append("   panel %3d: " % j + " ".join(f"{x:7.2f}" for x in v))
+                w = [(c[j, 8 + k] - t0) / 100.0 if c[j, 8 + k] else float("nan") for k in range(7)]
+                out.append("   (j+1,j)  : " + " ".join(f"{x:7.2f}" for x in w))
+            chol = None
+    if chol is not None:
         nst = int((chol[:, 0] != 0).sum())
         c = chol[:nst]
         out.append(f"== k_chol_step (last workgroup of each of {nst} steps), cycles: load / pivots / barrier / update")
