@@ -153,7 +153,7 @@ struct DevProblem {
     double qcinv[36];
     double huber_mono, huber_stereo, huber_prior;
     // work buffers
-    double* gps;            // [n_smp][GPS_STRIDE] pose samples: Rwb twb N (lba::GPSample)
+    double* gpsb[2];        // [n_smp][GPS_STRIDE] pose samples (Rwb twb N, lba::GPSample) of state buffer 0 / 1
     double* mslab;          // [n_mslots][SM_STRIDE] per (tile, sample) M / g partials, sample-sorted
     double* kfp_pose;       // [n_kf][KFP_STRIDE] Rwb twb (same prefix as a sample)
     double* hslab;          // [n_hslots][144] Hpp partial blocks, target-sorted
@@ -222,7 +222,8 @@ void launch_schur(const DevProblem& P, double lambda, int gate, hipStream_t s);
 enum { ASM_SCHUR = 1, ASM_FULL = 2 };
 void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hipStream_t s);
 void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s);
-void launch_update(const DevProblem& P, double lambda, int sel, int gate, hipStream_t s);
+// the step + trial state + the trial state's pose samples (jac: with their Jacobian factors)
+void launch_update(const DevProblem& P, double lambda, int sel, int gate, int jac, hipStream_t s);
 enum { FIN_NONE = -1, FIN_HOST = 0, FIN_QUEUED = 1, FIN_QUEUED_PUBLISH = 2, FIN_INITIAL = 3 };
 void launch_finalize(const DevProblem& P, unsigned long long seq, int mode, hipStream_t s);
 // residual evaluation of a state, then (mode != FIN_NONE) the trial summary (k_finalize)

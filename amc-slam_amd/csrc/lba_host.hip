@@ -55,6 +55,7 @@ struct lba_problem {
     int s_layout = 0;             // layout last assembled into S: 0 factorisation order, 1 natural (full)
     unsigned long long fin_seq = 0;
     unsigned cf_epoch = 0;        // launches of the dataflow factorisation (its flags hold the epoch)
+    bool gps_fresh[2] = {false, false};   // state buffer s has its pose samples with Jacobian factors
     double lambda = -1.0, ni = 2.0;
     int nBad = 0;
 };
@@ -614,7 +615,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         std::vector<double> g0((size_t)GPS_STRIDE * std::max(n_smp, 1), 0.0);
         for (int k = 0; k < n_kf; ++k)
             for (int l = 0; l < 6; ++l) g0[(size_t)(n_gps + k) * GPS_STRIDE + 12 + 6 * (12 + l) + l] = 1.0;
-        D.gps = dupload(p, g0);
+        D.gpsb[0] = dupload(p, g0);
+        D.gpsb[1] = dupload(p, g0);
     }
     D.mslab = dalloc<double>(p, (size_t)SM_STRIDE * std::max(n_mslots, 1));
     D.kfp_pose = dalloc<double>(p, (size_t)KFP_STRIDE * std::max(n_kf, 1));
@@ -766,7 +768,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     const int nchi = n_tiles + D.n_prior + D.n_vel;
     D.chi_lin = dalloc<double>(p, nchi + 1);
     D.chi_eval = dalloc<double>(p, nchi + 1);
-    D.n_upd_blocks = (n_kf + nl + 63) / 64;   // k_update: UPD_THREADS (64) per block
+    // k_update: one workgroup per GP pair, then KFs and landmarks at 64 per workgroup
+    D.n_upd_blocks = D.n_gp + (n_kf + 63) / 64 + (nl + 63) / 64;
     if (D.n_upd_blocks == 0) D.n_upd_blocks = 1;
     D.scale_part = dalloc<double>(p, D.n_upd_blocks);
     D.info = dalloc<int>(p, 1);
@@ -786,6 +789,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     HIPCHK(hipMemset(D.ctl, 0, sizeof(LMCtl)));
     p->cur = 0;
     p->has_problem = true;
+    p->gps_fresh[0] = p->gps_fresh[1] = false;
     p->linearized = false;
     return LBA_OK;
 }
@@ -793,7 +797,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
 // ------------------------------------------------------------------------------------------------
 void linearize(lba_problem* p, int write_res, bool timed = false) {
     const DevProblem& D = p->D;
-    launch_gp_prep(D, p->cur, 1, GATE_NONE, p->stream);
+    if (!p->gps_fresh[p->cur]) launch_gp_prep(D, p->cur, 1, GATE_NONE, p->stream);
+    p->gps_fresh[p->cur] = true;
     if (timed) HIPCHK(hipEventRecord(p->ev[6], p->stream));
     launch_linearize(D, p->cur, write_res, GATE_NONE, p->stream);
     if (timed) HIPCHK(hipEventRecord(p->ev[7], p->stream));
@@ -850,15 +855,16 @@ void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs, bool s
     if (evs) HIPCHK(hipEventRecord(evs[0], p->stream));
     launch_cholesky_solve(D, GATE_NONE, ++p->cf_epoch, p->stream);
     if (evs) HIPCHK(hipEventRecord(evs[1], p->stream));
-    launch_update(D, lambda, p->cur, GATE_NONE, p->stream);
-    if (evaluate) launch_gp_prep(D, nx, 0, GATE_NONE, p->stream);
+    launch_update(D, lambda, p->cur, GATE_NONE, 1, p->stream);   // (+ the trial state's pose samples)
+    p->gps_fresh[nx] = true;
     finalize_and_wait(p, sync || evs, evaluate ? nx : -1);
     if (evs) HIPCHK(hipEventRecord(evs[2], p->stream));
 }
 
 double eval_current(lba_problem* p) {
     const DevProblem& D = p->D;
-    launch_gp_prep(D, p->cur, 0, GATE_NONE, p->stream);
+    launch_gp_prep(D, p->cur, 1, GATE_NONE, p->stream);   // (the samples the linearisation then uses)
+    p->gps_fresh[p->cur] = true;
     finalize_and_wait(p, true, p->cur);
     return p->h_fin[1];
 }
@@ -928,7 +934,6 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
                 p->qev.resize(2);
                 for (auto& e : p->qev) HIPCHK(hipEventCreate(&e));
             }
-            if (issued > 0) launch_gp_prep(D, SEL_CUR, 1, GATE_LIN, p->stream);
             if (tq) HIPCHK(hipEventRecord(p->qev[2 * issued], p->stream));
             launch_linearize(D, SEL_CUR, 0, GATE_LIN, p->stream);
             if (tq) HIPCHK(hipEventRecord(p->qev[2 * issued + 1], p->stream));
@@ -940,8 +945,9 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
             launch_schur(D, LAMBDA_CTL, GATE_NONE, p->stream);
             assemble_layout(p, LAMBDA_CTL, ASM_SCHUR);
             launch_cholesky_solve(D, GATE_NONE, ++p->cf_epoch, p->stream);
-            launch_update(D, LAMBDA_CTL, SEL_CUR, GATE_TRIAL, p->stream);
-            launch_gp_prep(D, SEL_NEXT, 0, GATE_NONE, p->stream);
+            // the step, the trial state and its pose samples with their Jacobian factors: an
+            // accepted trial's relinearisation reads them (no preparation launch)
+            launch_update(D, LAMBDA_CTL, SEL_CUR, GATE_TRIAL, 1, p->stream);
             launch_eval(D, SEL_NEXT, GATE_NONE, ++p->fin_seq, k == n - 1 ? FIN_QUEUED_PUBLISH : FIN_QUEUED,
                         p->stream);
             HIPCHK(hipGetLastError());
@@ -963,6 +969,7 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
     }
     HIPCHK(hipStreamSynchronize(p->stream));
     p->cur = c.cur;
+    p->gps_fresh[0] = p->gps_fresh[1] = true;   // every state write of the queue came with its samples
     p->lambda = c.lambda;
     p->ni = c.ni;
     p->nBad = c.nbad;
@@ -1206,6 +1213,7 @@ int lba_set_state(lba_problem* p, const lba_kf* kf_in, const double* lm_xyz) {
                 o[13] = kf_in[k].time;
                 o[14] = kf_in[k].bf;
             }
+            p->gps_fresh[p->cur] = false;   // the new poses need new samples
             HIPCHK(hipMemcpyAsync(p->kst[p->cur], kst.data(), KF_STRIDE * (size_t)p->n_kf * sizeof(double),
                                   hipMemcpyHostToDevice, p->stream));
             HIPCHK(hipStreamSynchronize(p->stream));

@@ -88,10 +88,10 @@ __device__ __forceinline__ void load_cam(const double* c, CamD* d) {
 // Pose of the body at the observation time (Rwb, twb): the observation's pose sample (a GP sample for
 // GP edges, the KF pose record for EdgeMono / EdgeStereo).  Returns the stereo bf of the edge's first
 // KF vertex.
-__device__ __forceinline__ double obs_pose(const DevProblem& P, const double* kst, int o, bool gp, double* Rwb,
-                                           double* twb) {
+__device__ __forceinline__ double obs_pose(const DevProblem& P, const double* gps, const double* kst, int o, bool gp,
+                                           double* Rwb, double* twb) {
     const int ka = gp ? P.ob_kfa[o] : P.ob_kfb[o];
-    const double* S = P.gps + (size_t)P.ob_smp[o] * GPS_STRIDE;
+    const double* S = gps + (size_t)P.ob_smp[o] * GPS_STRIDE;
 #pragma unroll
     for (int i = 0; i < 9; ++i) Rwb[i] = S[i];
     twb[0] = S[9]; twb[1] = S[10]; twb[2] = S[11];
@@ -103,12 +103,12 @@ __device__ __forceinline__ double obs_pose(const DevProblem& P, const double* ks
 // pose sample: the pose / velocity Jacobian J1 N is never formed, see k_linearize) and
 // G = rho' w sum_rows J1^T Jp; returns rho(chi2).
 template <int DIM>
-__device__ __forceinline__ double lin_obs(const DevProblem& P, const double* kst, const double* lst, int o, int cam,
-                                          bool gp, double* rows, double* rw, double* G, int write_res) {
+__device__ __forceinline__ double lin_obs(const DevProblem& P, const double* gps, const double* kst, const double* lst,
+                                          int o, int cam, bool gp, double* rows, double* rw, double* G, int write_res) {
     CamD cd;
     load_cam(P.camd + (size_t)cam * CAMD_STRIDE, &cd);
     double Rwb[9], twb[3];
-    const double bf = obs_pose(P, kst, o, gp, Rwb, twb);
+    const double bf = obs_pose(P, gps, kst, o, gp, Rwb, twb);
     const double* Xw = lst + (size_t)P.ob_lm[o] * 3;
     double z[DIM];
 #pragma unroll
@@ -153,12 +153,12 @@ __device__ __forceinline__ double lin_obs(const DevProblem& P, const double* kst
 
 // Residual-only evaluation of one observation (computeError + robust chi2); returns rho(chi2).
 template <int DIM>
-__device__ __forceinline__ double eval_obs(const DevProblem& P, const double* kst, const double* lst, int o,
-                                           int cam, bool gp) {
+__device__ __forceinline__ double eval_obs(const DevProblem& P, const double* gps, const double* kst,
+                                           const double* lst, int o, int cam, bool gp) {
     CamD cd;
     load_cam(P.camd + (size_t)cam * CAMD_STRIDE, &cd);
     double Rwb[9], twb[3];
-    const double bf = obs_pose(P, kst, o, gp, Rwb, twb);
+    const double bf = obs_pose(P, gps, kst, o, gp, Rwb, twb);
     double z[DIM];
 #pragma unroll
     for (int d = 0; d < DIM; ++d) z[d] = P.ob_z[3 * (size_t)o + d];
@@ -179,126 +179,133 @@ __device__ __forceinline__ double eval_obs(const DevProblem& P, const double* ks
 // factor N (gp_sample_build) are computed with the same per-output operation order as those serial
 // functions, but spread over the wave: lane 0 the SE(3) log, then lanes 0-2 Jr^-1, Ad(exp(xi12))^-1
 // and ad(v2) side by side, one lane per 6x6 product entry, one lane per sample for its pose /
-// Jr / Ad(exp(-xi)), one lane per (sample, row, column) of N.  Trailing workgroups write the KF pose
-// records.
+// Jr / Ad(exp(-xi)), one lane per (sample, row, column) of N.  ka / kb: the two KF states (16
+// doubles each, global or LDS); gps: the sample buffer of that state.
 constexpr int PREP_THREADS = 64;
 constexpr int PREP_SCHUNK = 16;   // samples per pass (LDS staging of their Jr / Ad blocks)
-__global__ __launch_bounds__(PREP_THREADS) void k_gp_prep(DevProblem P, int sel, int jac, int gate) {
+__device__ void gp_pair_prep(const DevProblem& P, double* gps, int i, const double* ka, const double* kb, int jac) {
     __shared__ GPPair pr;
     __shared__ double AdI[36], ad2[36], vbs[6];
     __shared__ double sJr[PREP_SCHUNK][36], sRm[PREP_SCHUNK][9], stR[PREP_SCHUNK][9], sg[PREP_SCHUNK][3];
     const int tid = threadIdx.x;
-    if (gated_off(P.ctl, gate)) return;
-    const double* __restrict__ kst = P.kbuf[state_idx(P, sel)];
-    if ((int)blockIdx.x < P.n_gp) {
-        const int i = blockIdx.x;
-        const double* ka = kst + (size_t)P.gp_kfa[i] * KF_STRIDE;
-        const double* kb = kst + (size_t)P.gp_kfb[i] * KF_STRIDE;
-        if (tid == 0) {
-            const SE3 Ta = load_se3(ka), Tb = load_se3(kb);
-            pr.T1q[0] = Ta.q.x; pr.T1q[1] = Ta.q.y; pr.T1q[2] = Ta.q.z; pr.T1q[3] = Ta.q.w;
-            for (int j = 0; j < 3; ++j) pr.T1t[j] = Ta.t[j];
-            for (int j = 0; j < 6; ++j) pr.v1[j] = ka[7 + j];
-            pr.t1 = ka[13];
-            pr.t2 = kb[13];
-            const SE3 T12 = se3_mul(se3_inv(Ta), Tb);
-            se3_log(T12, pr.xi12);
-        }
-        if (tid < 6) vbs[tid] = kb[7 + tid];
-        __syncthreads();
-        if (tid == 0) {
-            right_jac_inv(pr.xi12, pr.G2a);                 // C = Jr^-1(xi12)
-        } else if (jac && tid == 1) {
-            const SE3 E = se3_exp(pr.xi12);                 // Ad(exp(xi12))^-1 = Ad(exp(xi12)^-1)
-            se3_adj(se3_inv(E), AdI);
-        } else if (jac && tid == 2) {
-            se3_ad(vbs, ad2);
-        }
-        __syncthreads();
-        if (tid < 6) {                                      // w2 = Jr^-1(xi12) v2
-            double w = 0.0;
-            for (int l = 0; l < 6; ++l) w += pr.G2a[tid * 6 + l] * vbs[l];
-            pr.w2[tid] = w;
-        }
-        if (jac && tid < 36) {                              // A1 = -C Ad^-1
-            const int r = tid / 6, c = tid % 6;
+    if (tid == 0) {
+        const SE3 Ta = load_se3(ka), Tb = load_se3(kb);
+        pr.T1q[0] = Ta.q.x; pr.T1q[1] = Ta.q.y; pr.T1q[2] = Ta.q.z; pr.T1q[3] = Ta.q.w;
+        for (int j = 0; j < 3; ++j) pr.T1t[j] = Ta.t[j];
+        for (int j = 0; j < 6; ++j) pr.v1[j] = ka[7 + j];
+        pr.t1 = ka[13];
+        pr.t2 = kb[13];
+        const SE3 T12 = se3_mul(se3_inv(Ta), Tb);
+        se3_log(T12, pr.xi12);
+    }
+    if (tid < 6) vbs[tid] = kb[7 + tid];
+    __syncthreads();
+    if (tid == 0) {
+        right_jac_inv(pr.xi12, pr.G2a);                 // C = Jr^-1(xi12)
+    } else if (jac && tid == 1) {
+        const SE3 E = se3_exp(pr.xi12);                 // Ad(exp(xi12))^-1 = Ad(exp(xi12)^-1)
+        se3_adj(se3_inv(E), AdI);
+    } else if (jac && tid == 2) {
+        se3_ad(vbs, ad2);
+    }
+    __syncthreads();
+    if (tid < 6) {                                      // w2 = Jr^-1(xi12) v2
+        double w = 0.0;
+        for (int l = 0; l < 6; ++l) w += pr.G2a[tid * 6 + l] * vbs[l];
+        pr.w2[tid] = w;
+    }
+    if (jac && tid < 36) {                              // A1 = -C Ad^-1
+        const int r = tid / 6, c = tid % 6;
+        double v = 0.0;
+        for (int l = 0; l < 6; ++l) v += pr.G2a[r * 6 + l] * AdI[l * 6 + c];
+        pr.G1a[tid] = -v;
+    }
+    __syncthreads();
+    if (jac)
+        for (int t = tid; t < 72; t += PREP_THREADS) {   // B1 = -1/2 ad(v2) A1, D = -1/2 ad(v2) C
+            const int e = t % 36, r = e / 6, c = e % 6;
+            const double* src = t < 36 ? pr.G1a : pr.G2a;
             double v = 0.0;
-            for (int l = 0; l < 6; ++l) v += pr.G2a[r * 6 + l] * AdI[l * 6 + c];
-            pr.G1a[tid] = -v;
+            for (int l = 0; l < 6; ++l) v += ad2[r * 6 + l] * src[l * 6 + c];
+            (t < 36 ? pr.G1b : pr.G2b)[e] = v * -0.5;
+        }
+    __syncthreads();
+    for (int c0 = P.gp_s0[i]; c0 < P.gp_s0[i + 1]; c0 += PREP_SCHUNK) {
+        const int ns = min(PREP_SCHUNK, P.gp_s0[i + 1] - c0);
+        if (tid < ns) {
+            GPSample* S = reinterpret_cast<GPSample*>(gps + (size_t)(c0 + tid) * GPS_STRIDE);
+            double xi[6];
+            GPScalars g;
+            gp_sample_pose(pr, P.gps_t[c0 + tid], S->Rwb, S->twb, xi, &g);
+            if (jac) {
+                double Jl[9], Q[9];                     // Jr(xi) = [Jl, Q; 0, Jl]
+                right_jac_blocks(xi, Jl, Q);
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) {
+                        sJr[tid][r * 6 + c] = Jl[r * 3 + c];
+                        sJr[tid][r * 6 + 3 + c] = Q[r * 3 + c];
+                        sJr[tid][(3 + r) * 6 + c] = 0.0;
+                        sJr[tid][(3 + r) * 6 + 3 + c] = Jl[r * 3 + c];
+                    }
+                const double mxi[6] = {-xi[0], -xi[1], -xi[2], -xi[3], -xi[4], -xi[5]};
+                const SE3 Em = se3_exp(mxi);            // Ad(exp(-xi)) = [R', t'^ R'; 0, R']
+                double Ht[9];
+                qmat(Em.q, sRm[tid]);
+                hat3(Em.t, Ht);
+                mul33(Ht, sRm[tid], stR[tid]);
+                sg[tid][0] = g.l1; sg[tid][1] = g.l2; sg[tid][2] = g.p2;
+            }
         }
         __syncthreads();
         if (jac)
-            for (int t = tid; t < 72; t += PREP_THREADS) {   // B1 = -1/2 ad(v2) A1, D = -1/2 ad(v2) C
-                const int e = t % 36, r = e / 6, c = e % 6;
-                const double* src = t < 36 ? pr.G1a : pr.G2a;
-                double v = 0.0;
-                for (int l = 0; l < 6; ++l) v += ad2[r * 6 + l] * src[l * 6 + c];
-                (t < 36 ? pr.G1b : pr.G2b)[e] = v * -0.5;
+            for (int t = tid; t < ns * 36; t += PREP_THREADS) {   // one (row, column) of each N block
+                const int sl = t / 36, r = (t % 36) / 6, c = t % 6;
+                const double l1 = sg[sl][0], l2 = sg[sl][1], p2 = sg[sl][2];
+                const double* Jr = sJr[sl];
+                double na = 0.0, nb = 0.0, nc = 0.0;
+                for (int l = 0; l < 6; ++l) {
+                    const double ma = l1 * pr.G1a[l * 6 + c] + l2 * pr.G1b[l * 6 + c];
+                    const double mc = l1 * pr.G2a[l * 6 + c] + l2 * pr.G2b[l * 6 + c];
+                    na += Jr[r * 6 + l] * ma;
+                    nb += Jr[r * 6 + l] * mc;
+                    nc += Jr[r * 6 + l] * pr.G2a[l * 6 + c];
+                }
+                double ad = 0.0;
+                if (r < 3) ad = (c < 3) ? sRm[sl][r * 3 + c] : stR[sl][r * 3 + c - 3];
+                else if (c >= 3) ad = sRm[sl][(r - 3) * 3 + c - 3];
+                double* N = gps + (size_t)(c0 + sl) * GPS_STRIDE + 12;
+                N[c * 6 + r] = na + ad;
+                N[(6 + c) * 6 + r] = p2 * Jr[r * 6 + c];
+                N[(12 + c) * 6 + r] = nb;
+                N[(18 + c) * 6 + r] = l2 * nc;
             }
         __syncthreads();
-        for (int c0 = P.gp_s0[i]; c0 < P.gp_s0[i + 1]; c0 += PREP_SCHUNK) {
-            const int ns = min(PREP_SCHUNK, P.gp_s0[i + 1] - c0);
-            if (tid < ns) {
-                GPSample* S = reinterpret_cast<GPSample*>(P.gps + (size_t)(c0 + tid) * GPS_STRIDE);
-                double xi[6];
-                GPScalars g;
-                gp_sample_pose(pr, P.gps_t[c0 + tid], S->Rwb, S->twb, xi, &g);
-                if (jac) {
-                    double Jl[9], Q[9];                     // Jr(xi) = [Jl, Q; 0, Jl]
-                    right_jac_blocks(xi, Jl, Q);
-                    for (int r = 0; r < 3; ++r)
-                        for (int c = 0; c < 3; ++c) {
-                            sJr[tid][r * 6 + c] = Jl[r * 3 + c];
-                            sJr[tid][r * 6 + 3 + c] = Q[r * 3 + c];
-                            sJr[tid][(3 + r) * 6 + c] = 0.0;
-                            sJr[tid][(3 + r) * 6 + 3 + c] = Jl[r * 3 + c];
-                        }
-                    const double mxi[6] = {-xi[0], -xi[1], -xi[2], -xi[3], -xi[4], -xi[5]};
-                    const SE3 Em = se3_exp(mxi);            // Ad(exp(-xi)) = [R', t'^ R'; 0, R']
-                    double Ht[9];
-                    qmat(Em.q, sRm[tid]);
-                    hat3(Em.t, Ht);
-                    mul33(Ht, sRm[tid], stR[tid]);
-                    sg[tid][0] = g.l1; sg[tid][1] = g.l2; sg[tid][2] = g.p2;
-                }
-            }
-            __syncthreads();
-            if (jac)
-                for (int t = tid; t < ns * 36; t += PREP_THREADS) {   // one (row, column) of each N block
-                    const int sl = t / 36, r = (t % 36) / 6, c = t % 6;
-                    const double l1 = sg[sl][0], l2 = sg[sl][1], p2 = sg[sl][2];
-                    const double* Jr = sJr[sl];
-                    double na = 0.0, nb = 0.0, nc = 0.0;
-                    for (int l = 0; l < 6; ++l) {
-                        const double ma = l1 * pr.G1a[l * 6 + c] + l2 * pr.G1b[l * 6 + c];
-                        const double mc = l1 * pr.G2a[l * 6 + c] + l2 * pr.G2b[l * 6 + c];
-                        na += Jr[r * 6 + l] * ma;
-                        nb += Jr[r * 6 + l] * mc;
-                        nc += Jr[r * 6 + l] * pr.G2a[l * 6 + c];
-                    }
-                    double ad = 0.0;
-                    if (r < 3) ad = (c < 3) ? sRm[sl][r * 3 + c] : stR[sl][r * 3 + c - 3];
-                    else if (c >= 3) ad = sRm[sl][(r - 3) * 3 + c - 3];
-                    double* N = P.gps + (size_t)(c0 + sl) * GPS_STRIDE + 12;
-                    N[c * 6 + r] = na + ad;
-                    N[(6 + c) * 6 + r] = p2 * Jr[r * 6 + c];
-                    N[(12 + c) * 6 + r] = nb;
-                    N[(18 + c) * 6 + r] = l2 * nc;
-                }
-            __syncthreads();
-        }
+    }
+}
+
+// KF k's pose record (k_depth) and the KF's pose sample (its constant N was uploaded once)
+__device__ __forceinline__ void kf_pose_record(const DevProblem& P, double* gps, int k, const double* kk) {
+    double R[9];
+    qmat(Quat{kk[0], kk[1], kk[2], kk[3]}, R);
+    double* o = P.kfp_pose + (size_t)k * KFP_STRIDE;
+    double* so = gps + (size_t)(P.n_gps + k) * GPS_STRIDE;
+    for (int j = 0; j < 9; ++j) o[j] = so[j] = R[j];
+    o[9] = so[9] = kk[4]; o[10] = so[10] = kk[5]; o[11] = so[11] = kk[6];
+}
+
+// Pose samples of the state `sel`: one workgroup per GP pair, then KF pose records.
+__global__ __launch_bounds__(PREP_THREADS) void k_gp_prep(DevProblem P, int sel, int jac, int gate) {
+    if (gated_off(P.ctl, gate)) return;
+    const int si = state_idx(P, sel);
+    const double* __restrict__ kst = P.kbuf[si];
+    double* gps = P.gpsb[si];
+    if ((int)blockIdx.x < P.n_gp) {
+        const int i = blockIdx.x;
+        gp_pair_prep(P, gps, i, kst + (size_t)P.gp_kfa[i] * KF_STRIDE, kst + (size_t)P.gp_kfb[i] * KF_STRIDE, jac);
         return;
     }
-    const int k = (blockIdx.x - P.n_gp) * PREP_THREADS + tid;
-    if (k < P.n_kf) {   // KF pose record and the KF's pose sample (its constant N was uploaded once)
-        const double* kk = kst + (size_t)k * KF_STRIDE;
-        double R[9];
-        qmat(Quat{kk[0], kk[1], kk[2], kk[3]}, R);
-        double* o = P.kfp_pose + (size_t)k * KFP_STRIDE;
-        double* so = P.gps + (size_t)(P.n_gps + k) * GPS_STRIDE;
-        for (int j = 0; j < 9; ++j) o[j] = so[j] = R[j];
-        o[9] = so[9] = kk[4]; o[10] = so[10] = kk[5]; o[11] = so[11] = kk[6];
-    }
+    const int k = (blockIdx.x - P.n_gp) * PREP_THREADS + threadIdx.x;
+    if (k < P.n_kf) kf_pose_record(P, gps, k, kst + (size_t)k * KF_STRIDE);
 }
 
 // One (tile sample, 9-output chunk) task: outputs 9 CH .. 9 CH + 8 of the sample's partial, i.e. the
@@ -352,6 +359,7 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
     const int si = state_idx(P, sel);
     const double* __restrict__ kst = P.kbuf[si];
     const double* __restrict__ lst = P.lbuf[si];
+    const double* __restrict__ gps = P.gpsb[si];
     LBA_TMARK(P.tdbg_lin, 0);
 
     // ---- stage the tile's index lists in LDS (fixed-count loops: all loads issue before the stores)
@@ -390,8 +398,9 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
         const bool gp = kind <= LBA_STEREO_GP;
         osm[tid] = P.ob_smp[o];
         double* G = Gs + tid * G_STRIDE;
-        rho0 = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? lin_obs<3>(P, kst, lst, o, cam, gp, rows, rw, G, write_res)
-                                                             : lin_obs<2>(P, kst, lst, o, cam, gp, rows, rw, G, write_res);
+        rho0 = (kind == LBA_STEREO_GP || kind == LBA_STEREO)
+                   ? lin_obs<3>(P, gps, kst, lst, o, cam, gp, rows, rw, G, write_res)
+                   : lin_obs<2>(P, gps, kst, lst, o, cam, gp, rows, rw, G, write_res);
     }
     const double tchi = block_sum<TILE_OBS>(rho0, red);   // (its barrier also publishes rows / lists)
     if (tid == 0) P.chi_lin[tile] = tchi;
@@ -421,7 +430,7 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
             const int code = prow[q];
             const int ol = code & 0xffff, side = code >> 16;
             // N stored transposed: column c of N (6 values) at 12 + 6 c
-            const double* Nc = P.gps + (size_t)osm[ol] * GPS_STRIDE + 12 + 6 * (12 * side + 4 * sb);
+            const double* Nc = gps + (size_t)osm[ol] * GPS_STRIDE + 12 + 6 * (12 * side + 4 * sb);
             const double* G = Gs + ol * G_STRIDE;
             double g[18];
 #pragma unroll
@@ -477,7 +486,8 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
 constexpr int PRI_THREADS = 256;
 constexpr int EXP_GROUPS = PRI_THREADS / SM_STRIDE;   // 9 partial sums per output
 
-__device__ void sample_expand(const DevProblem& P, int smp, double* Msh, double* Nsh, double* MN, double* part) {
+__device__ void sample_expand(const DevProblem& P, const double* gps, int smp, double* Msh, double* Nsh, double* MN,
+                              double* part) {
     const int tid = threadIdx.x;
     const int* sl = P.seg_slot + 5 * (size_t)smp;
     const int* gl = P.seg_gslot + 2 * (size_t)smp;
@@ -499,7 +509,7 @@ __device__ void sample_expand(const DevProblem& P, int smp, double* Msh, double*
         for (; k < k1; k += EXP_GROUPS) v0 += m[(size_t)k * SM_STRIDE];
         part[tid] = (v0 + v1) + (v2 + v3);
     }
-    const double* Ng = P.gps + (size_t)smp * GPS_STRIDE + 12;
+    const double* Ng = gps + (size_t)smp * GPS_STRIDE + 12;
     if (tid < 144) Nsh[tid] = Ng[tid];   // N(l, c) at Nsh[6 c + l]
     __syncthreads();
     if (tid < SM_STRIDE) {
@@ -554,7 +564,7 @@ __global__ __launch_bounds__(PRI_THREADS) void k_prior_lin(DevProblem P, int sel
     const int idx = blockIdx.x, tid = threadIdx.x;
     if (gated_off(P.ctl, gate)) return;
     if (idx >= P.n_prior + P.n_vel) {
-        sample_expand(P, idx - P.n_prior - P.n_vel, Ji, Jj, WJi, part);
+        sample_expand(P, P.gpsb[state_idx(P, sel)], idx - P.n_prior - P.n_vel, Ji, Jj, WJi, part);
         return;
     }
     const double* __restrict__ kst = P.kbuf[state_idx(P, sel)];
@@ -789,6 +799,22 @@ __global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double la
 //   S(bi, bj) = sum Hpp partials + lambda I (diagonal) - sum Schur partials   (block_solver.hpp:432-445,
 //   setLambda :573-579), only for the blocks inside the structural pattern (the rest of S is zero
 //   from the upload and never written);  b_p = sum b partials;  bS = b_p - sum Schur rhs partials.
+// sum of x[(s0 + G q) * W + e] over the slots s0, s0 + G, ... < s1: four loads in flight, combined in
+// a fixed order
+template <int G, int W>
+__device__ __forceinline__ double slot_sum(const double* __restrict__ x, int s0, int s1, int e) {
+    double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+    int s = s0;
+    for (; s + 3 * G < s1; s += 4 * G) {
+        v0 += x[(size_t)s * W + e];
+        v1 += x[(size_t)(s + G) * W + e];
+        v2 += x[(size_t)(s + 2 * G) * W + e];
+        v3 += x[(size_t)(s + 3 * G) * W + e];
+    }
+    for (; s < s1; s += G) v0 += x[(size_t)s * W + e];
+    return (v0 + v1) + (v2 + v3);
+}
+
 __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, double lambda_arg, int flags, int gate) {
     __shared__ double red[144 * RED_GROUPS];
     const int tid = threadIdx.x;
@@ -799,10 +825,8 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
         const int ub = P.asm_list[blockIdx.x];
         const int bi = P.ub_i[ub], bj = P.ub_j[ub];
         const int e = tid % 144, g = tid / 144;
-        double v = 0.0;
-        for (int s = P.hs0[ub] + g; s < P.hs0[ub + 1]; s += RED_GROUPS) v += P.hslab[(size_t)s * 144 + e];
-        if (flags & ASM_SCHUR)
-            for (int s = P.ss0[ub] + g; s < P.ss0[ub + 1]; s += RED_GROUPS) v -= P.sslab[(size_t)s * 144 + e];
+        double v = slot_sum<RED_GROUPS, 144>(P.hslab, P.hs0[ub] + g, P.hs0[ub + 1], e);
+        if (flags & ASM_SCHUR) v -= slot_sum<RED_GROUPS, 144>(P.sslab, P.ss0[ub] + g, P.ss0[ub + 1], e);
         red[tid] = v;
         __syncthreads();
         if (g == 0) {
@@ -830,10 +854,8 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
     } else {
         const int k = blockIdx.x - P.n_asm;
         const int e = tid % 12, g = tid / 12;   // 48 groups
-        double v = 0.0, w = 0.0;
-        for (int s = P.gs0[k] + g; s < P.gs0[k + 1]; s += 48) v += P.gslab[(size_t)s * 12 + e];
-        if (flags & ASM_SCHUR)
-            for (int s = P.gps0[k] + g; s < P.gps0[k + 1]; s += 48) w += P.gpslab[(size_t)s * 12 + e];
+        const double v = slot_sum<48, 12>(P.gslab, P.gs0[k] + g, P.gs0[k + 1], e);
+        const double w = (flags & ASM_SCHUR) ? slot_sum<48, 12>(P.gpslab, P.gps0[k] + g, P.gps0[k + 1], e) : 0.0;
         red[tid] = v;
         __syncthreads();
         double bpv = 0.0;
@@ -1548,8 +1570,34 @@ __global__ __launch_bounds__(BS_THREADS) void k_chol_backsolve(const double* __r
 // ------------------------------------------------------------------------------------------------
 constexpr int UPD_THREADS = 64;     // one landmark (or KF) per thread: many small blocks for latency hiding
 
-__global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lambda_arg, int sel, int gate) {
+// Trial state of KF k (pose block h, -1 if fixed): Twb <- Twb exp(dxi), v += dv (G2oTypes.cc:41-46);
+// d = the solved step, or the stale x when the factorisation failed (BlockSolver leaves x untouched,
+// g2o then applies and pops it).  One (non-inlined) function body for every caller, so every copy of
+// a state is bitwise identical.
+__device__ __attribute__((noinline)) void kf_trial_state(const DevProblem& P, const double* kc, int h, bool ok,
+                                                         double* d, double* kn) {
+    if (h >= 0) {
+        for (int j = 0; j < 12; ++j) d[j] = ok ? P.xsol[12 * h + j] : P.x[12 * h + j];
+        const SE3 T = se3_mul(load_se3(kc), se3_exp(d));
+        kn[0] = T.q.x; kn[1] = T.q.y; kn[2] = T.q.z; kn[3] = T.q.w;
+        kn[4] = T.t[0]; kn[5] = T.t[1]; kn[6] = T.t[2];
+        for (int j = 0; j < 6; ++j) kn[7 + j] = kc[7 + j] + d[6 + j];
+        for (int j = 13; j < KF_STRIDE; ++j) kn[j] = kc[j];
+    } else {
+        for (int j = 0; j < KF_STRIDE; ++j) kn[j] = kc[j];
+    }
+}
+
+// The step and the trial state (block_solver.hpp:461-482 back-substitution, sparse_optimizer.cpp:422-435
+// oplus, computeScale partials), fused with the pose samples of the trial state:
+//   workgroups [0, n_gp): one per GP pair: its two KFs' trial states (kf_trial_state), then the pair's
+//     samples with their Jacobian factors (gp_pair_prep, jac) into the trial state's sample buffer, so
+//     an accepted trial's next linearisation needs no preparation launch;
+//   then one KF per thread (trial state, KF pose sample, x, scale), then one landmark per thread
+//   (dx_l = Dinv (bl - sum Hpl^T dx_p), oplus, scale).
+__global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lambda_arg, int sel, int gate, int jac) {
     __shared__ double red[UPD_THREADS / 64];
+    __shared__ double kab[2][KF_STRIDE];
     if (gated_off(P.ctl, gate)) return;
     const double lambda = damping(P, lambda_arg);
     const int si = state_idx(P, sel);
@@ -1557,55 +1605,65 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
     const double* __restrict__ lst = P.lbuf[si];
     double* __restrict__ ko = P.kbuf[si ^ 1];
     double* __restrict__ lo = P.lbuf[si ^ 1];
-    const int i = blockIdx.x * UPD_THREADS + threadIdx.x;
+    double* gps = P.gpsb[si ^ 1];
     const bool ok = (*P.info == 0);
-    double sc = 0.0;
-    if (i < P.n_kf) {
-        const double* kc = kst + (size_t)i * KF_STRIDE;
-        double* kn = ko + (size_t)i * KF_STRIDE;
-        const int h = P.kf_hidx[i];
-        if (h >= 0) {
-            // BlockSolver leaves x untouched when the factorisation fails; g2o then applies and pops it
+    const int nkb = (P.n_kf + UPD_THREADS - 1) / UPD_THREADS;
+    if ((int)blockIdx.x < P.n_gp) {
+        const int i = blockIdx.x;
+        if (threadIdx.x < 2) {
+            const int k = threadIdx.x ? P.gp_kfb[i] : P.gp_kfa[i];
             double d[12];
-            for (int j = 0; j < 12; ++j) {
-                d[j] = ok ? P.xsol[12 * h + j] : P.x[12 * h + j];
-                if (ok) P.x[12 * h + j] = d[j];
-                sc += d[j] * (lambda * d[j] + P.bp[12 * h + j]);
-            }
-            const SE3 T = se3_mul(load_se3(kc), se3_exp(d));   // Twb <- Twb exp(dxi) (G2oTypes.cc:41-46)
-            kn[0] = T.q.x; kn[1] = T.q.y; kn[2] = T.q.z; kn[3] = T.q.w;
-            kn[4] = T.t[0]; kn[5] = T.t[1]; kn[6] = T.t[2];
-            for (int j = 0; j < 6; ++j) kn[7 + j] = kc[7 + j] + d[6 + j];
-            for (int j = 13; j < KF_STRIDE; ++j) kn[j] = kc[j];
-        } else {
-            for (int j = 0; j < KF_STRIDE; ++j) kn[j] = kc[j];
+            kf_trial_state(P, kst + (size_t)k * KF_STRIDE, P.kf_hidx[k], ok, d, kab[threadIdx.x]);
         }
-    } else if (i < P.n_kf + P.n_lm) {
-        const int l = i - P.n_kf;
-        double xl[3];
-        double* xd = P.x + P.np + 3 * (size_t)l;
-        if (ok) {
-            double c[3] = {P.bl[3 * (size_t)l], P.bl[3 * (size_t)l + 1], P.bl[3 * (size_t)l + 2]};
-            for (int p = P.lm_pair0[l]; p < P.lm_pair0[l + 1]; ++p) {
-                const double* B = P.Hpl + (size_t)p * 36;
-                const double* xp = P.xsol + 12 * (size_t)P.pair_kf[p];
-                for (int r = 0; r < 12; ++r) {
-                    c[0] -= B[r * 3] * xp[r];
-                    c[1] -= B[r * 3 + 1] * xp[r];
-                    c[2] -= B[r * 3 + 2] * xp[r];
+        __syncthreads();
+        gp_pair_prep(P, gps, i, kab[0], kab[1], jac);
+        if (threadIdx.x == 0) P.scale_part[blockIdx.x] = 0.0;
+        return;
+    }
+    double sc = 0.0;
+    if ((int)blockIdx.x < P.n_gp + nkb) {
+        const int k = (blockIdx.x - P.n_gp) * UPD_THREADS + threadIdx.x;
+        if (k < P.n_kf) {
+            const int h = P.kf_hidx[k];
+            double d[12], kn[KF_STRIDE];
+            kf_trial_state(P, kst + (size_t)k * KF_STRIDE, h, ok, d, kn);
+            double* kw = ko + (size_t)k * KF_STRIDE;
+            for (int j = 0; j < KF_STRIDE; ++j) kw[j] = kn[j];
+            kf_pose_record(P, gps, k, kn);
+            if (h >= 0)
+                for (int j = 0; j < 12; ++j) {
+                    if (ok) P.x[12 * h + j] = d[j];
+                    sc += d[j] * (lambda * d[j] + P.bp[12 * h + j]);
                 }
-            }
-            const double* D = P.Dinv + (size_t)l * 9;
-            for (int a = 0; a < 3; ++a) {
-                xl[a] = D[a * 3] * c[0] + D[a * 3 + 1] * c[1] + D[a * 3 + 2] * c[2];
-                xd[a] = xl[a];
-            }
-        } else {
-            xl[0] = xd[0]; xl[1] = xd[1]; xl[2] = xd[2];
         }
-        for (int a = 0; a < 3; ++a) {
-            lo[3 * (size_t)l + a] = lst[3 * (size_t)l + a] + xl[a];
-            sc += xl[a] * (lambda * xl[a] + P.bl[3 * (size_t)l + a]);
+    } else {
+        const int l = (blockIdx.x - P.n_gp - nkb) * UPD_THREADS + threadIdx.x;
+        if (l < P.n_lm) {
+            double xl[3];
+            double* xd = P.x + P.np + 3 * (size_t)l;
+            if (ok) {
+                double c[3] = {P.bl[3 * (size_t)l], P.bl[3 * (size_t)l + 1], P.bl[3 * (size_t)l + 2]};
+                for (int p = P.lm_pair0[l]; p < P.lm_pair0[l + 1]; ++p) {
+                    const double* B = P.Hpl + (size_t)p * 36;
+                    const double* xp = P.xsol + 12 * (size_t)P.pair_kf[p];
+                    for (int r = 0; r < 12; ++r) {
+                        c[0] -= B[r * 3] * xp[r];
+                        c[1] -= B[r * 3 + 1] * xp[r];
+                        c[2] -= B[r * 3 + 2] * xp[r];
+                    }
+                }
+                const double* D = P.Dinv + (size_t)l * 9;
+                for (int a = 0; a < 3; ++a) {
+                    xl[a] = D[a * 3] * c[0] + D[a * 3 + 1] * c[1] + D[a * 3 + 2] * c[2];
+                    xd[a] = xl[a];
+                }
+            } else {
+                xl[0] = xd[0]; xl[1] = xd[1]; xl[2] = xd[2];
+            }
+            for (int a = 0; a < 3; ++a) {
+                lo[3 * (size_t)l + a] = lst[3 * (size_t)l + a] + xl[a];
+                sc += xl[a] * (lambda * xl[a] + P.bl[3 * (size_t)l + a]);
+            }
         }
     }
     const double s = block_sum<UPD_THREADS>(sc, red);
@@ -1626,6 +1684,7 @@ __global__ __launch_bounds__(TILE_OBS) void k_eval(DevProblem P, int sel, int ga
     const int si = state_idx(P, sel);
     const double* __restrict__ kst = P.kbuf[si];
     const double* __restrict__ lst = P.lbuf[si];
+    const double* __restrict__ gps = P.gpsb[si];
     if (tile < P.n_tiles) {
         double rho0 = 0.0;
         if (tid < P.tile_nobs[tile]) {
@@ -1633,8 +1692,8 @@ __global__ __launch_bounds__(TILE_OBS) void k_eval(DevProblem P, int sel, int ga
             const int meta = P.ob_meta[o];
             const int kind = meta & 15, cam = meta >> 4;
             const bool gp = kind <= LBA_STEREO_GP;
-            rho0 = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? eval_obs<3>(P, kst, lst, o, cam, gp)
-                                                                 : eval_obs<2>(P, kst, lst, o, cam, gp);
+            rho0 = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? eval_obs<3>(P, gps, kst, lst, o, cam, gp)
+                                                                 : eval_obs<2>(P, gps, kst, lst, o, cam, gp);
         }
         const double s = block_sum<TILE_OBS>(rho0, red);
         if (tid == 0) P.chi_eval[tile] = s;
@@ -1861,8 +1920,8 @@ void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStr
     hipLaunchKernelGGL(k_chol_backsolve, dim3(nr > 0 ? 2 : 1), dim3(BS_THREADS), 0, s, P.Lm, P.LinvT, n, P.yv,
                        P.xsol, P.pfirst, P.pnat, P.tdbg_bs, P.ctl, gate, 0, nl, nl, nl + nr, 0);
 }
-void launch_update(const DevProblem& P, double lambda, int sel, int gate, hipStream_t s) {
-    hipLaunchKernelGGL(k_update, dim3(P.n_upd_blocks), dim3(UPD_THREADS), 0, s, P, lambda, sel, gate);
+void launch_update(const DevProblem& P, double lambda, int sel, int gate, int jac, hipStream_t s) {
+    hipLaunchKernelGGL(k_update, dim3(P.n_upd_blocks), dim3(UPD_THREADS), 0, s, P, lambda, sel, gate, jac);
 }
 void launch_eval(const DevProblem& P, int sel, int gate, unsigned long long seq, int mode, hipStream_t s) {
     const int nb = P.n_tiles + cdiv(P.n_prior + P.n_vel, TILE_OBS);
