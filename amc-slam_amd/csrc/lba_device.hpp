@@ -216,7 +216,9 @@ struct DevProblem {
 // gate: GATE_*; lambda: the damping, or LAMBDA_CTL
 constexpr int HLOG_CAP = 4096;
 void launch_gp_prep(const DevProblem& P, int sel, int jac, int gate, hipStream_t s);
-void launch_linearize(const DevProblem& P, int sel, int write_res, int gate, hipStream_t s);
+// e0 / e1 (optional): timing events attached to the k_linearize dispatch itself
+void launch_linearize(const DevProblem& P, int sel, int write_res, int gate, hipStream_t s, hipEvent_t e0 = nullptr,
+                      hipEvent_t e1 = nullptr);
 void launch_prior_lin(const DevProblem& P, int sel, int gate, hipStream_t s);
 void launch_schur(const DevProblem& P, double lambda, int gate, hipStream_t s);
 enum { ASM_SCHUR = 1, ASM_FULL = 2 };

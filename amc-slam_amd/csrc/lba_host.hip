@@ -799,9 +799,8 @@ void linearize(lba_problem* p, int write_res, bool timed = false) {
     const DevProblem& D = p->D;
     if (!p->gps_fresh[p->cur]) launch_gp_prep(D, p->cur, 1, GATE_NONE, p->stream);
     p->gps_fresh[p->cur] = true;
-    if (timed) HIPCHK(hipEventRecord(p->ev[6], p->stream));
-    launch_linearize(D, p->cur, write_res, GATE_NONE, p->stream);
-    if (timed) HIPCHK(hipEventRecord(p->ev[7], p->stream));
+    launch_linearize(D, p->cur, write_res, GATE_NONE, p->stream, timed ? p->ev[6] : nullptr,
+                     timed ? p->ev[7] : nullptr);
     launch_prior_lin(D, p->cur, GATE_NONE, p->stream);
     HIPCHK(hipGetLastError());
     p->linearized = true;
@@ -857,8 +856,9 @@ void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs, bool s
     if (evs) HIPCHK(hipEventRecord(evs[1], p->stream));
     launch_update(D, lambda, p->cur, GATE_NONE, 1, p->stream);   // (+ the trial state's pose samples)
     p->gps_fresh[nx] = true;
-    finalize_and_wait(p, sync || evs, evaluate ? nx : -1);
+    if (evaluate) launch_eval(D, nx, GATE_NONE, 0, FIN_NONE, p->stream);
     if (evs) HIPCHK(hipEventRecord(evs[2], p->stream));
+    finalize_and_wait(p, sync || evs);
 }
 
 double eval_current(lba_problem* p) {
@@ -927,16 +927,16 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
         const int first = issued;
         const auto te0 = std::chrono::steady_clock::now();
         for (int k = 0; k < n; ++k, ++issued) {
-            // LBA_FLAG_TIME_SWEEP: events bracket the first k_linearize launch of the call (it always
-            // relinearises); one launch per call keeps the timing overhead off the loop
-            const bool tq = tsweep && issued == 0;
-            if (tq && p->qev.size() < 2) {
-                p->qev.resize(2);
-                for (auto& e : p->qev) HIPCHK(hipEventCreate(&e));
+            // LBA_FLAG_TIME_SWEEP: events bracket every queued k_linearize launch; the trials that did
+            // relinearise are read from the controller's log afterwards
+            const bool tq = tsweep && issued < HLOG_CAP;
+            if (tq && p->qev.size() < 2 * (size_t)issued + 2) {
+                const size_t old = p->qev.size();
+                p->qev.resize(std::max<size_t>(2 * (size_t)issued + 2, 2 * old));
+                for (size_t e = old; e < p->qev.size(); ++e) HIPCHK(hipEventCreate(&p->qev[e]));
             }
-            if (tq) HIPCHK(hipEventRecord(p->qev[2 * issued], p->stream));
-            launch_linearize(D, SEL_CUR, 0, GATE_LIN, p->stream);
-            if (tq) HIPCHK(hipEventRecord(p->qev[2 * issued + 1], p->stream));
+            launch_linearize(D, SEL_CUR, 0, GATE_LIN, p->stream, tq ? p->qev[2 * issued] : nullptr,
+                             tq ? p->qev[2 * issued + 1] : nullptr);
             launch_prior_lin(D, SEL_CUR, GATE_LIN, p->stream);
             if (issued == 0 && p->cfg.lambda_init <= 0) {
                 assemble_layout(p, 0.0, ASM_FULL);
@@ -960,10 +960,11 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
         std::memcpy(&c, hc, sizeof(LMCtl));
         if (tsweep) {
             HIPCHK(hipStreamSynchronize(p->stream));
-            if (first == 0 && issued > 0 && p->h_log[0]) {   // the bracketed launch (trial 0)
-                s.ms_k_linearize += elapsed(p->qev[0], p->qev[1]);
-                s.n_k_linearize += 1;
-            }
+            for (int q = first; q < issued && q < HLOG_CAP; ++q)
+                if (p->h_log[q]) {
+                    s.ms_k_linearize += elapsed(p->qev[2 * q], p->qev[2 * q + 1]);
+                    s.n_k_linearize += 1;
+                }
         }
         if (c.done || n <= 0) break;
     }

@@ -22,6 +22,8 @@
 #include <cfloat>
 #include <utility>
 
+#include <hip/hip_ext.h>
+
 #include "lba_device.hpp"
 #include "lba_math.hpp"
 #include "../../include/amc_lba.h"
@@ -1879,8 +1881,13 @@ void launch_gp_prep(const DevProblem& P, int sel, int jac, int gate, hipStream_t
     const int nb = P.n_gp + cdiv(P.n_kf, PREP_THREADS);
     if (nb) hipLaunchKernelGGL(k_gp_prep, dim3(nb), dim3(PREP_THREADS), 0, s, P, sel, jac, gate);
 }
-void launch_linearize(const DevProblem& P, int sel, int write_res, int gate, hipStream_t s) {
-    if (P.n_tiles) hipLaunchKernelGGL(k_linearize, dim3(P.n_tiles), dim3(TILE_OBS), 0, s, P, sel, write_res, gate);
+void launch_linearize(const DevProblem& P, int sel, int write_res, int gate, hipStream_t s, hipEvent_t e0,
+                      hipEvent_t e1) {
+    if (!P.n_tiles) return;
+    if (e0)   // the events carry the dispatch's own start / end timestamps
+        hipExtLaunchKernelGGL(k_linearize, dim3(P.n_tiles), dim3(TILE_OBS), 0, s, e0, e1, 0, P, sel, write_res, gate);
+    else
+        hipLaunchKernelGGL(k_linearize, dim3(P.n_tiles), dim3(TILE_OBS), 0, s, P, sel, write_res, gate);
 }
 void launch_prior_lin(const DevProblem& P, int sel, int gate, hipStream_t s) {
     const int n = P.n_prior + P.n_vel + P.n_smp;

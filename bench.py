@@ -121,9 +121,8 @@ def main():
     else:
         win = make_config_window(args.config, seed=args.seed)
         ex = None
-    # the timed run records HIP events around k_linearize only (LBA_FLAG_TIME_SWEEP: its first launch
-    # in each optimize call, i.e. one launch per window): the roofline below is measured live, per
-    # launch, over the timed region
+    # the timed run records HIP events around every k_linearize launch (LBA_FLAG_TIME_SWEEP): the
+    # roofline below is measured live, per launch, over the timed region
     prob = amc_lba.Problem(win, device=local, early_stop=0, flags=amc_lba.abi.FLAG_TIME_SWEEP)
 
     # warmup (not timed)

@@ -48,8 +48,8 @@ extern "C" {
 
 /* lba_config.flags.  Timing inserts HIP events into the stream (each costs a few us of
  * device idle time), so both are off by default. */
-#define LBA_FLAG_TIME_SWEEP   1   /* time the residual/Jacobian sweep kernel (lba_stats.ms_k_linearize);
-                                     queued loop: its first launch of each lba_optimize call */
+#define LBA_FLAG_TIME_SWEEP   1   /* time every launch of the residual/Jacobian sweep kernel
+                                     (lba_stats.ms_k_linearize) */
 #define LBA_FLAG_TIME_PHASES  2   /* also time every phase (ms_linearize .. ms_update_eval); runs the
                                      host-driven loop */
 #define LBA_FLAG_HOST_LOOP    4   /* take every LM decision on the host, one trial at a time (default:
