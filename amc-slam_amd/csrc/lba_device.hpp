@@ -175,6 +175,8 @@ struct DevProblem {
     const int* cf_tasks;
     int cf_ntasks;
     const int* cf_tbase;
+    double* cf_linv;        // [npad][npad] L^-1 tiles (k_chol_flow)
+    int* cf_ivready;        // per lower tile i (i + 1) / 2 + j
     const int* cf_pl0;
     const int* cf_plist;
     int* cf_lready;
@@ -189,7 +191,8 @@ struct DevProblem {
     double* Dinv;
     double* S;              // [npad][npad] (factorisation order; natural order for ASM_FULL), padding: identity
     double* bp;             // [np]
-    double* xsol;           // [np] rhs -> solution
+    double* bS;             // [npad] reduced right-hand side b_p - sum Hpl Dinv bl (factorisation order)
+    double* xsol;           // [npad] solution (natural order)
     double* yv;             // [np] forward-substituted rhs
     double* x;              // [np + 3 n_lm]
     double* chi_lin;        // [n_tiles + n_prior + n_vel]

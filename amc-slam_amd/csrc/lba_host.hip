@@ -691,18 +691,12 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         D.h_steps = p->chol_steps.data();
         D.n_steps = (int)steps.size() / 4;
         D.chol_items = dupload(p, items);
-        // dataflow factorisation (k_chol_flow): one task per envelope tile, in topological order
-        // (column by column, the diagonal tile first): task j | i << 12
+        // dataflow factorisation + solve (k_chol_flow), tasks in topological order: per column c the
+        // factor tiles (c..NP-1, c) (the diagonal first), then the L^-1 tiles of row c; at the end one
+        // solution task per panel.  Task: j | i << 12 | kind << 24, with a list of panels per task.
         {
             std::vector<int> tbase(NP + 1, 0), tasks;
             for (int i = 0; i < NP; ++i) tbase[i + 1] = tbase[i] + (i - pfh[i] + 1);
-            for (int j = 0; j < NP; ++j)
-                for (int i = j; i < NP; ++i)
-                    if (pfh[i] <= j) tasks.push_back(j | (i << 12));
-            if (NP > 4095) throw ApiError{LBA_E_LIMIT, "internal: too many panels for the dataflow factorisation"};
-            D.cf_tasks = dupload(p, tasks);
-            D.cf_ntasks = (int)tasks.size();
-            D.cf_tbase = dupload(p, tbase);
             std::vector<int> uord;   // panel update order = the order the panels complete
             for (int k = 0; k < std::max(nl, nr); ++k) {
                 if (k < nl) uord.push_back(k);
@@ -711,14 +705,44 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             for (int k = 0; k < ns; ++k) uord.push_back(nl + nr + k);
             std::vector<int> rank(NP), pl0(1, 0), plist;
             for (int q = 0; q < NP; ++q) rank[uord[q]] = q;
-            for (int tcode : tasks) {   // per task: its panels p in [pfh[j], j) in update order
-                const int j = tcode & 4095, i = (tcode >> 12) & 4095;
-                std::vector<int> ps;
-                for (int pp = pfh[j]; pp < j; ++pp) ps.push_back(pp);
-                std::sort(ps.begin(), ps.end(), [&](int x, int y) { return rank[x] < rank[y]; });
-                for (int pp : ps) plist.push_back(pp | ((pp >= pfh[i]) << 12));
+            // structure of L^-1: Linv(i,j) != 0 iff some k in [max(j, pfh[i]), i) has Linv(k,j) != 0
+            std::vector<std::vector<char>> nz(NP, std::vector<char>(NP, 0));
+            for (int j = 0; j < NP; ++j) {
+                nz[j][j] = 1;
+                for (int i = j + 1; i < NP; ++i)
+                    for (int k = std::max(j, pfh[i]); k < i && !nz[i][j]; ++k) nz[i][j] = nz[k][j];
+            }
+            for (int c = 0; c < NP; ++c) {
+                for (int i = c; i < NP; ++i) {   // factor tiles of column c: panels p in update order
+                    if (pfh[i] > c) continue;
+                    tasks.push_back(c | (i << 12));
+                    std::vector<int> ps;
+                    for (int pp = pfh[c]; pp < c; ++pp) ps.push_back(pp);
+                    std::sort(ps.begin(), ps.end(), [&](int x, int y) { return rank[x] < rank[y]; });
+                    for (int pp : ps) plist.push_back(pp | ((pp >= pfh[i]) << 12));
+                    pl0.push_back((int)plist.size());
+                }
+                for (int j = 0; j < c; ++j) {    // L^-1 tiles of row c: terms k ascending
+                    if (!nz[c][j]) continue;
+                    tasks.push_back(j | (c << 12) | (1 << 24));
+                    for (int k = std::max(j, pfh[c]); k < c; ++k)
+                        if (nz[k][j]) plist.push_back(k);
+                    pl0.push_back((int)plist.size());
+                }
+            }
+            for (int j = 0; j < NP; ++j) {      // solution blocks: rows i >= j of column j of L^-1
+                tasks.push_back(j | (j << 12) | (2 << 24));
+                for (int i = j; i < NP; ++i)
+                    if (nz[i][j]) plist.push_back(i);
                 pl0.push_back((int)plist.size());
             }
+            if (NP > 4095) throw ApiError{LBA_E_LIMIT, "internal: too many panels for the dataflow factorisation"};
+            D.cf_tasks = dupload(p, tasks);
+            D.cf_ntasks = (int)tasks.size();
+            D.cf_tbase = dupload(p, tbase);
+            D.cf_linv = dalloc<double>(p, (size_t)npad * npad);
+            D.cf_ivready = dalloc<int>(p, std::max(NP * (NP + 1) / 2, 1));
+            HIPCHK(hipMemset(D.cf_ivready, 0, sizeof(int) * std::max(NP * (NP + 1) / 2, 1)));
             D.cf_pl0 = dupload(p, pl0);
             D.cf_plist = dupload(p, plist);
             D.cf_lready = dalloc<int>(p, std::max(tbase[NP], 1));
@@ -757,6 +781,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.S = dalloc<double>(p, (size_t)npad * npad + 1);
     D.bp = dalloc<double>(p, p->np + 1);
     D.xsol = dalloc<double>(p, npad + 1);
+    D.bS = dalloc<double>(p, npad + 1);
+    HIPCHK(hipMemset(D.bS, 0, sizeof(double) * (npad + 1)));
     D.yv = dalloc<double>(p, npad + 1);
     // S and L start zero (k_assemble writes the identity of the padding rows every time)
     HIPCHK(hipMemset(D.S, 0, sizeof(double) * ((size_t)npad * npad + 1)));

@@ -851,7 +851,7 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
             for (int r = P.np + tid; r < n; r += 144 * RED_GROUPS) {
                 const int rh = (flags & ASM_FULL) ? r : P.ppos[r / CHOL_NB] * CHOL_NB + r % CHOL_NB;
                 P.S[(size_t)rh * n + rh] = 1.0;
-                P.xsol[rh] = 0.0;   // (the back-substitution leaves natural-order values here)
+                P.bS[rh] = 0.0;
             }
     } else {
         const int k = blockIdx.x - P.n_asm;
@@ -873,7 +873,7 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
             for (int q = 0; q < 48; ++q) t += red[q * 12 + tid];
             const int r = 12 * k + tid;
             const int rh = (flags & ASM_FULL) ? r : P.ppos[r / CHOL_NB] * CHOL_NB + r % CHOL_NB;
-            P.xsol[rh] = bpv - t;   // bS = b_p - sum Hpl Dinv bl (factorisation order)
+            P.bS[rh] = bpv - t;   // bS = b_p - sum Hpl Dinv bl (factorisation order)
         }
     }
 }
@@ -1204,7 +1204,8 @@ constexpr int CF_TIMEOUT = 0x7fff0000;          // *info value of a timed-out la
 struct CholFlow {
     int n, NP, ntasks;
     unsigned epoch;
-    const int* tasks;    // j | i << 12 | kind << 24 (kind 0: panel j, 1: off-diagonal tile (i, j))
+    const int* tasks;    // j | i << 12 | kind << 24 (0: factor tile (i, j) (i = j: panel j), 1: L^-1 tile (i, j),
+                         // 2: solution block j)
     const int* pfh;      // envelope of the permuted matrix (first panel of each panel row)
     const int* tbase;    // tile id of (i, pfh[i]); tile (i, j) = tbase[i] + j - pfh[i]
     const int* pl0;      // per task: first entry of its update list in plist ([pl0[t], pl0[t+1]))
@@ -1221,6 +1222,12 @@ struct CholFlow {
     unsigned long long* head;   // ticket counter (zeroed by k_schur ahead of every trial)
     int* abort_flag;
     unsigned long long* tdbg;   // diagnostics: per panel, s_memrealtime stamps of its task
+    // the solve x = L^-T y without a back-substitution chain: L^-1 tiles (computed alongside the
+    // factorisation) and per output panel one GEMV
+    double* Linv;        // [npad][npad] tiles (i, j), i > j, of L^-1 (factorisation order)
+    int* ivready;        // per lower tile (tri_id): epoch once Linv(i, j) is published
+    double* xout;        // the solution, natural panel order
+    const int* pnat;     // natural panel of a position
 };
 
 // thread 0 polls up to two flags for `epoch` (relaxed, agent scope); the workgroup learns the result
@@ -1320,6 +1327,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
     const int rb = wave >> 1, cb = wave & 1, lr = lane & 15, kq = lane >> 4;
     const int n = a.n;
     auto tile_id = [&](int i, int j) { return a.tbase[i] + j - a.pfh[i]; };
+    auto tri_id = [&](int i, int j) { return i * (i + 1) / 2 + j; };
     auto load_quad = [&](int i, int j, double (&q)[4]) {   // plain loads: S is not written in this launch
 #pragma unroll
         for (int m = 0; m < 4; ++m) q[m] = a.S[(size_t)(i * CNB + rb * 16 + kq + 4 * m) * n + j * CNB + cb * 16 + lr];
@@ -1355,6 +1363,87 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
         if (t >= a.ntasks) break;
         const int code = a.tasks[t];
         const int j = code & 4095, i = (code >> 12) & 4095;
+        const int kind = code >> 24;
+        if (kind == 1) {
+            // ---------------------------------------------------- L^-1 tile (i, j), i > j:
+            // Linv(i,j) = -L_ii^-1 sum_k L(i,k) Linv(k,j) over the list's k (Linv(j,j) = LinvT_j^T)
+            const d4 z = {0.0, 0.0, 0.0, 0.0};
+            d4 acc = z;
+            bool ok = true;
+            for (int q = a.pl0[t]; q < a.pl0[t + 1]; ++q) {
+                const int k = a.plist[q] & 4095;
+                if (!cf_wait(a, a.lready + tile_id(i, k), k == j ? a.dready + j : a.ivready + tri_id(k, j), &s_ok)) {
+                    ok = false;
+                    break;
+                }
+                cf_load_tile(a.Lm + (size_t)(i * CNB) * n + k * CNB, n, Lt[0]);
+                if (k == j) {
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {   // Linv(j,j)[r][c] = LinvT_j[c][r]
+                        const int e = tid + 256 * m;
+                        Lt[1][e & 31][e >> 5] = ld_sc1(a.LinvT + (size_t)j * CNB * CNB + e);
+                    }
+                } else {
+                    cf_load_tile(a.Linv + (size_t)(k * CNB) * n + j * CNB, n, Lt[1]);
+                }
+                __syncthreads();
+                acc = cf_mma_nn(Lt[0], Lt[1], rb, cb, lr, kq, acc);
+                __syncthreads();
+            }
+            if (!ok || !cf_wait(a, a.dready + i, nullptr, &s_ok)) return;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {   // L_ii^-1 = LinvT_i^T
+                const int e = tid + 256 * m;
+                Lt[0][e & 31][e >> 5] = ld_sc1(a.LinvT + (size_t)i * CNB * CNB + e);
+                Lt[1][rb * 16 + kq + 4 * m][cb * 16 + lr] = acc[m];
+            }
+            __syncthreads();
+            const d4 v = cf_mma_nn(Lt[0], Lt[1], rb, cb, lr, kq, z);
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                st_sc1(a.Linv + (size_t)(i * CNB + rb * 16 + kq + 4 * m) * n + j * CNB + cb * 16 + lr, -v[m]);
+            cf_publish(a, a.ivready + tri_id(i, j));
+            continue;
+        }
+        if (kind == 2) {
+            // ---------------------------------------------------- x_j = sum_i Linv(i,j)^T y_i over the list's
+            // i (Linv(j,j)^T = LinvT_j), into xsol in natural panel order
+            double part = 0.0;
+            const int c = tid & 31, rq = tid >> 5;   // output c, rows 4 rq .. 4 rq + 3 of each term
+            bool ok = true;
+            for (int q = a.pl0[t]; q < a.pl0[t + 1]; ++q) {
+                const int r = a.plist[q] & 4095;
+                if (!cf_wait(a, r == j ? a.dready + j : a.ivready + tri_id(r, j), nullptr, &s_ok)) {
+                    ok = false;
+                    break;
+                }
+                if (r == j) {
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {   // Linv(j,j)[rr][cc] = LinvT_j[cc][rr]
+                        const int e = tid + 256 * m;
+                        Lt[0][e & 31][e >> 5] = ld_sc1(a.LinvT + (size_t)j * CNB * CNB + e);
+                    }
+                } else {
+                    cf_load_tile(a.Linv + (size_t)(r * CNB) * n + j * CNB, n, Lt[0]);
+                }
+                if (tid < CNB) ys[tid] = ld_sc1(a.yv + r * CNB + tid);
+                __syncthreads();
+#pragma unroll
+                for (int u = 0; u < 4; ++u) part += Lt[0][4 * rq + u][c] * ys[4 * rq + u];
+                __syncthreads();
+            }
+            if (!ok) return;
+            Lt[1][rq][c] = part;
+            __syncthreads();
+            if (tid < CNB) {
+                double x = 0.0;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x += Lt[1][u][tid];
+                a.xout[a.pnat[j] * CNB + tid] = x;
+            }
+            __syncthreads();
+            continue;
+        }
         const bool diag = i == j;
         // diagnostics: stamps of panel j's task (slots 0..6) and of tile (j + 1, j) (slots 8..14)
         unsigned long long* tm = (a.tdbg && tid == 0 && (diag || i == j + 1)) ? a.tdbg + 16 * j + (diag ? 0 : 8) : nullptr;
@@ -1908,16 +1997,19 @@ void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStr
         a.n = n; a.NP = n / CHOL_NB; a.ntasks = P.cf_ntasks; a.epoch = epoch;
         a.tasks = P.cf_tasks; a.pfh = P.pfirst; a.tbase = P.cf_tbase; a.pl0 = P.cf_pl0;
         a.plist = P.cf_plist;
-        a.S = P.S; a.Lm = P.Lm; a.LinvT = P.LinvT; a.b = P.xsol; a.yv = P.yv; a.info = P.info;
+        a.S = P.S; a.Lm = P.Lm; a.LinvT = P.LinvT; a.b = P.bS; a.yv = P.yv; a.info = P.info;
         a.lready = P.cf_lready; a.dready = P.cf_dready; a.head = P.cf_head; a.abort_flag = P.cf_abort;
         a.tdbg = P.tdbg_chol;
+        a.Linv = P.cf_linv; a.ivready = P.cf_ivready; a.xout = P.xsol; a.pnat = P.pnat;
         hipLaunchKernelGGL(k_chol_flow, dim3(min(P.cf_ntasks, 512)), dim3(256), 0, s, a);
+        return;
     }
     for (int st = 0; P.cf_steps_path && st < P.n_steps; ++st) {
         const int* h = P.h_steps + 4 * st;
         hipLaunchKernelGGL(k_chol_step, dim3(h[3] - h[2]), dim3(256), 0, s, n, h[0], h[1], h[2], P.chol_items, P.S,
-                           P.Lm, P.LinvT, P.xsol, P.yv, P.info, P.ctl, gate, P.tdbg_chol, st);
+                           P.Lm, P.LinvT, P.bS, P.yv, P.info, P.ctl, gate, P.tdbg_chol, st);
     }
+    if (!P.cf_steps_path) return;   // k_chol_flow also solved: x = L^-T y through its L^-1 tiles
     // back-substitution: separator positions [nl + nr, NP) first, then left [0, nl) and right
     // [nl, nl + nr) side by side
     const int NP = n / CHOL_NB, nl = P.nd_left, nr = P.nd_right;
