@@ -181,6 +181,9 @@ struct DevProblem {
     const int* cf_plist;
     int* cf_lready;
     int* cf_dready;
+    int* cf_fready;
+    int* cf_zready;
+    double* cf_zv;          // [NP][NP][CHOL_NB] shares Linv(i, k) b_k of the forward solve
     unsigned long long* cf_head;
     int* cf_abort;
     int cf_steps_path;      // LBA_CHOL_STEPS: the k_chol_step sequence instead

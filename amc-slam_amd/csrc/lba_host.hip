@@ -729,6 +729,10 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                         if (nz[k][j]) plist.push_back(k);
                     pl0.push_back((int)plist.size());
                 }
+                tasks.push_back(c | (c << 12) | (3 << 24));   // y_c: the nonzero tiles of row c of L^-1
+                for (int k = 0; k <= c; ++k)
+                    if (nz[c][k]) plist.push_back(k);
+                pl0.push_back((int)plist.size());
             }
             for (int j = 0; j < NP; ++j) {      // solution blocks: rows i >= j of column j of L^-1
                 tasks.push_back(j | (j << 12) | (2 << 24));
@@ -747,6 +751,11 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             D.cf_plist = dupload(p, plist);
             D.cf_lready = dalloc<int>(p, std::max(tbase[NP], 1));
             D.cf_dready = dalloc<int>(p, std::max(NP, 1));
+            D.cf_fready = dalloc<int>(p, std::max(NP, 1));
+            HIPCHK(hipMemset(D.cf_fready, 0, sizeof(int) * std::max(NP, 1)));
+            D.cf_zready = dalloc<int>(p, std::max(NP, 1));
+            HIPCHK(hipMemset(D.cf_zready, 0, sizeof(int) * std::max(NP, 1)));
+            D.cf_zv = dalloc<double>(p, std::max((size_t)NP * NP * CHOL_NB, (size_t)1));
             D.cf_head = dalloc<unsigned long long>(p, 1);
             D.cf_abort = dalloc<int>(p, 1);
             HIPCHK(hipMemset(D.cf_lready, 0, sizeof(int) * std::max(tbase[NP], 1)));

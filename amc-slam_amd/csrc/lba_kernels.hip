@@ -184,7 +184,7 @@ __device__ __forceinline__ double eval_obs(const DevProblem& P, const double* gp
 // Jr / Ad(exp(-xi)), one lane per (sample, row, column) of N.  ka / kb: the two KF states (16
 // doubles each, global or LDS); gps: the sample buffer of that state.
 constexpr int PREP_THREADS = 64;
-constexpr int PREP_SCHUNK = 16;   // samples per pass (LDS staging of their Jr / Ad blocks)
+constexpr int PREP_SCHUNK = 21;   // samples per pass (3 lanes each; LDS staging of their Jr / Ad blocks)
 __device__ void gp_pair_prep(const DevProblem& P, double* gps, int i, const double* ka, const double* kb, int jac) {
     __shared__ GPPair pr;
     __shared__ double AdI[36], ad2[36], vbs[6];
@@ -234,28 +234,38 @@ __device__ void gp_pair_prep(const DevProblem& P, double* gps, int i, const doub
     __syncthreads();
     for (int c0 = P.gp_s0[i]; c0 < P.gp_s0[i + 1]; c0 += PREP_SCHUNK) {
         const int ns = min(PREP_SCHUNK, P.gp_s0[i + 1] - c0);
-        if (tid < ns) {
-            GPSample* S = reinterpret_cast<GPSample*>(gps + (size_t)(c0 + tid) * GPS_STRIDE);
-            double xi[6];
-            GPScalars g;
-            gp_sample_pose(pr, P.gps_t[c0 + tid], S->Rwb, S->twb, xi, &g);
-            if (jac) {
-                double Jl[9], Q[9];                     // Jr(xi) = [Jl, Q; 0, Jl]
-                right_jac_blocks(xi, Jl, Q);
-                for (int r = 0; r < 3; ++r)
-                    for (int c = 0; c < 3; ++c) {
-                        sJr[tid][r * 6 + c] = Jl[r * 3 + c];
-                        sJr[tid][r * 6 + 3 + c] = Q[r * 3 + c];
-                        sJr[tid][(3 + r) * 6 + c] = 0.0;
-                        sJr[tid][(3 + r) * 6 + 3 + c] = Jl[r * 3 + c];
-                    }
-                const double mxi[6] = {-xi[0], -xi[1], -xi[2], -xi[3], -xi[4], -xi[5]};
-                const SE3 Em = se3_exp(mxi);            // Ad(exp(-xi)) = [R', t'^ R'; 0, R']
-                double Ht[9];
-                qmat(Em.q, sRm[tid]);
-                hat3(Em.t, Ht);
-                mul33(Ht, sRm[tid], stR[tid]);
-                sg[tid][0] = g.l1; sg[tid][1] = g.l2; sg[tid][2] = g.p2;
+        // three lanes per sample, each one of the independent transcendental chains: the interpolated
+        // pose (gp_sample_pose), Jr(xi) and Ad(exp(-xi)); xi is recomputed per lane (same expression)
+        if (tid < 3 * ns) {
+            const int sl = tid / 3, role = tid - 3 * sl;
+            GPSample* S = reinterpret_cast<GPSample*>(gps + (size_t)(c0 + sl) * GPS_STRIDE);
+            if (role == 0) {
+                double xi[6];
+                GPScalars g;
+                gp_sample_pose(pr, P.gps_t[c0 + sl], S->Rwb, S->twb, xi, &g);
+            } else if (jac) {
+                const GPScalars g = gp_scalars(pr.t1, pr.t2, P.gps_t[c0 + sl]);
+                double xi[6];
+                for (int q = 0; q < 6; ++q) xi[q] = g.p2 * pr.v1[q] + g.l1 * pr.xi12[q] + g.l2 * pr.w2[q];
+                if (role == 1) {
+                    double Jl[9], Q[9];                     // Jr(xi) = [Jl, Q; 0, Jl]
+                    right_jac_blocks(xi, Jl, Q);
+                    for (int r = 0; r < 3; ++r)
+                        for (int c = 0; c < 3; ++c) {
+                            sJr[sl][r * 6 + c] = Jl[r * 3 + c];
+                            sJr[sl][r * 6 + 3 + c] = Q[r * 3 + c];
+                            sJr[sl][(3 + r) * 6 + c] = 0.0;
+                            sJr[sl][(3 + r) * 6 + 3 + c] = Jl[r * 3 + c];
+                        }
+                    sg[sl][0] = g.l1; sg[sl][1] = g.l2; sg[sl][2] = g.p2;
+                } else {
+                    const double mxi[6] = {-xi[0], -xi[1], -xi[2], -xi[3], -xi[4], -xi[5]};
+                    const SE3 Em = se3_exp(mxi);            // Ad(exp(-xi)) = [R', t'^ R'; 0, R']
+                    double Ht[9];
+                    qmat(Em.q, sRm[sl]);
+                    hat3(Em.t, Ht);
+                    mul33(Ht, sRm[sl], stR[sl]);
+                }
             }
         }
         __syncthreads();
@@ -1205,7 +1215,7 @@ struct CholFlow {
     int n, NP, ntasks;
     unsigned epoch;
     const int* tasks;    // j | i << 12 | kind << 24 (0: factor tile (i, j) (i = j: panel j), 1: L^-1 tile (i, j),
-                         // 2: solution block j)
+                         // 2: solution block x_j, 3: forward block y_i)
     const int* pfh;      // envelope of the permuted matrix (first panel of each panel row)
     const int* tbase;    // tile id of (i, pfh[i]); tile (i, j) = tbase[i] + j - pfh[i]
     const int* pl0;      // per task: first entry of its update list in plist ([pl0[t], pl0[t+1]))
@@ -1218,10 +1228,14 @@ struct CholFlow {
     double* yv;
     int* info;
     int* lready;         // per tile: epoch once L(i, j) is published
-    int* dready;         // per panel: epoch once L_jj^-T and y_j are published
+    int* fready;         // per panel: epoch once L_jj^-T is published
+    int* dready;         // per panel: epoch once y_i is published (after every Linv(i, .))
+    int* zready;         // per panel: epoch once z(i, i) = L_ii^-1 b_i is published
+    double* zv;          // [NP][NP][CNB] z(i, k) = Linv(i, k) b_k, the shares of y_i
     unsigned long long* head;   // ticket counter (zeroed by k_schur ahead of every trial)
     int* abort_flag;
     unsigned long long* tdbg;   // diagnostics: per panel, s_memrealtime stamps of its task
+    unsigned long long* tdbg2;  // diagnostics: stamps of the L^-1 tasks of the last two panel rows
     // the solve x = L^-T y without a back-substitution chain: L^-1 tiles (computed alongside the
     // factorisation) and per output panel one GEMV
     double* Linv;        // [npad][npad] tiles (i, j), i > j, of L^-1 (factorisation order)
@@ -1263,6 +1277,30 @@ __device__ __forceinline__ bool cf_test(const CholFlow& a, const int* f1, const 
         if (f1) ok = ok && (unsigned)__hip_atomic_load((gi32_t*)f1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch;
         if (f2) ok = ok && (unsigned)__hip_atomic_load((gi32_t*)f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch;
         *s_ok = ok ? 1 : 0;
+    }
+    __syncthreads();
+    return *s_ok != 0;
+}
+
+// every flag of a list at `epoch`?  (flag q polled by thread q mod 256: the waits overlap)
+template <class F>
+__device__ __forceinline__ bool cf_wait_list(const CholFlow& a, int cnt, F flag, int* s_ok) {
+    if (threadIdx.x == 0) *s_ok = 1;
+    __syncthreads();
+    for (int q = threadIdx.x; q < cnt; q += blockDim.x) {
+        const int* f = flag(q);
+        unsigned spins = 0;
+        while ((unsigned)__hip_atomic_load((gi32_t*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.epoch) {
+            if (++spins > CF_SPIN_LIMIT ||
+                ((spins & 255) == 0 &&
+                 (unsigned)__hip_atomic_load((gi32_t*)a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch)) {
+                __hip_atomic_store((gi32_t*)a.abort_flag, (int)a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                *a.info = CF_TIMEOUT;
+                *s_ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
     }
     __syncthreads();
     return *s_ok != 0;
@@ -1320,7 +1358,6 @@ __device__ __forceinline__ d4 cf_mma_nn(const double (*X)[CNB + 1], const double
 __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
     __shared__ double Lt[2][CNB][CNB + 1];       // update operands L(i, p), L(j, p)
     __shared__ double stg[2][2 * CNB][CNB + 1];  // stacked panels of the factoring waves
-    __shared__ double bs[CNB], ys[CNB];
     __shared__ long long s_ticket;
     __shared__ int s_ok;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1370,9 +1407,15 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
             const d4 z = {0.0, 0.0, 0.0, 0.0};
             d4 acc = z;
             bool ok = true;
+            unsigned long long* tv = (a.tdbg2 && tid == 0 && i >= a.NP - 2) ? a.tdbg2 + 16 * j + 4 * (i - (a.NP - 2)) : nullptr;
+            if (tv) tv[0] = __builtin_amdgcn_s_memrealtime();
+            const int zr = tid >> 3, zc = (tid & 7) * 4;   // z(i, j): row zr, columns zc .. zc + 3
+            double bj[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) bj[u] = a.b[j * CNB + zc + u];
             for (int q = a.pl0[t]; q < a.pl0[t + 1]; ++q) {
                 const int k = a.plist[q] & 4095;
-                if (!cf_wait(a, a.lready + tile_id(i, k), k == j ? a.dready + j : a.ivready + tri_id(k, j), &s_ok)) {
+                if (!cf_wait(a, a.lready + tile_id(i, k), k == j ? a.fready + j : a.ivready + tri_id(k, j), &s_ok)) {
                     ok = false;
                     break;
                 }
@@ -1390,7 +1433,9 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
                 acc = cf_mma_nn(Lt[0], Lt[1], rb, cb, lr, kq, acc);
                 __syncthreads();
             }
-            if (!ok || !cf_wait(a, a.dready + i, nullptr, &s_ok)) return;
+            if (tv) tv[1] = __builtin_amdgcn_s_memrealtime();
+            if (!ok || !cf_wait(a, a.fready + i, nullptr, &s_ok)) return;
+            if (tv) tv[2] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
             for (int m = 0; m < 4; ++m) {   // L_ii^-1 = LinvT_i^T
                 const int e = tid + 256 * m;
@@ -1399,38 +1444,53 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
             }
             __syncthreads();
             const d4 v = cf_mma_nn(Lt[0], Lt[1], rb, cb, lr, kq, z);
+            __syncthreads();   // (Lt[1] was an operand of the product)
 #pragma unroll
-            for (int m = 0; m < 4; ++m)
-                st_sc1(a.Linv + (size_t)(i * CNB + rb * 16 + kq + 4 * m) * n + j * CNB + cb * 16 + lr, -v[m]);
+            for (int m = 0; m < 4; ++m) {
+                const int rr = rb * 16 + kq + 4 * m, cc = cb * 16 + lr;
+                st_sc1(a.Linv + (size_t)(i * CNB + rr) * n + j * CNB + cc, -v[m]);
+                Lt[1][rr][cc] = -v[m];
+            }
+            __syncthreads();
+            double zs = 0.0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) zs += Lt[1][zr][zc + u] * bj[u];
+            zs += __shfl_xor(zs, 1);
+            zs += __shfl_xor(zs, 2);
+            zs += __shfl_xor(zs, 4);
+            if ((tid & 7) == 0) st_sc1(a.zv + ((size_t)i * a.NP + j) * CNB + zr, zs);
             cf_publish(a, a.ivready + tri_id(i, j));
+            if (tv) tv[3] = __builtin_amdgcn_s_memrealtime();
             continue;
         }
         if (kind == 2) {
-            // ---------------------------------------------------- x_j = sum_i Linv(i,j)^T y_i over the list's
-            // i (Linv(j,j)^T = LinvT_j), into xsol in natural panel order
-            double part = 0.0;
+            // ---------------------------------------------------- x_j = sum_r Linv(r,j)^T y_r over the list's
+            // r (Linv(j,j)^T = LinvT_j), into xsol in natural panel order.  Each term's tile is fetched as
+            // soon as it is published, ahead of y_r.
             const int c = tid & 31, rq = tid >> 5;   // output c, rows 4 rq .. 4 rq + 3 of each term
+            double part = 0.0;
             bool ok = true;
             for (int q = a.pl0[t]; q < a.pl0[t + 1]; ++q) {
                 const int r = a.plist[q] & 4095;
-                if (!cf_wait(a, r == j ? a.dready + j : a.ivready + tri_id(r, j), nullptr, &s_ok)) {
+                if (!cf_wait(a, r == j ? a.fready + j : a.ivready + tri_id(r, j), nullptr, &s_ok)) {
                     ok = false;
                     break;
                 }
-                if (r == j) {
+                double lv[4], yr[4];
 #pragma unroll
-                    for (int m = 0; m < 4; ++m) {   // Linv(j,j)[rr][cc] = LinvT_j[cc][rr]
-                        const int e = tid + 256 * m;
-                        Lt[0][e & 31][e >> 5] = ld_sc1(a.LinvT + (size_t)j * CNB * CNB + e);
-                    }
-                } else {
-                    cf_load_tile(a.Linv + (size_t)(r * CNB) * n + j * CNB, n, Lt[0]);
+                for (int u = 0; u < 4; ++u) {
+                    const int rr = 4 * rq + u;
+                    lv[u] = r == j ? ld_sc1(a.LinvT + (size_t)j * CNB * CNB + c * CNB + rr)
+                                   : ld_sc1(a.Linv + (size_t)(r * CNB + rr) * n + j * CNB + c);
                 }
-                if (tid < CNB) ys[tid] = ld_sc1(a.yv + r * CNB + tid);
-                __syncthreads();
+                if (!cf_wait(a, a.dready + r, nullptr, &s_ok)) {
+                    ok = false;
+                    break;
+                }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) part += Lt[0][4 * rq + u][c] * ys[4 * rq + u];
-                __syncthreads();
+                for (int u = 0; u < 4; ++u) yr[u] = ld_sc1(a.yv + r * CNB + 4 * rq + u);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) part += lv[u] * yr[u];
             }
             if (!ok) return;
             Lt[1][rq][c] = part;
@@ -1441,7 +1501,41 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
                 for (int u = 0; u < 8; ++u) x += Lt[1][u][tid];
                 a.xout[a.pnat[j] * CNB + tid] = x;
             }
+            if (a.tdbg && tid == 0) a.tdbg[16 * j + 15] = __builtin_amdgcn_s_memrealtime();
             __syncthreads();
+            continue;
+        }
+        if (kind == 3) {
+            // ---------------------------------------------------- y_i = sum_k z(i, k) over the list's k
+            // (z(i, k) = Linv(i, k) b_k, made by the tasks of Linv(i, k) and panel i): the forward solve
+            // without a chain through the panels
+            const int q0 = a.pl0[t], cnt = a.pl0[t + 1] - q0;
+            if (!cf_wait_list(a, cnt, [&](int q) {
+                    const int k = a.plist[q0 + q] & 4095;
+                    return k == i ? a.zready + i : a.ivready + tri_id(i, k);
+                }, &s_ok)) return;
+            const int r = tid & 31, g = tid >> 5;   // row r, terms g, g + 8, ...
+            double acc = 0.0;
+            for (int q = g; q < cnt; q += 32) {
+                double zz[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int qq = q + 8 * u;
+                    zz[u] = qq < cnt ? ld_sc1(a.zv + ((size_t)i * a.NP + (a.plist[q0 + qq] & 4095)) * CNB + r) : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc += zz[u];
+            }
+            Lt[1][g][r] = acc;
+            __syncthreads();
+            if (tid < CNB) {
+                double y = 0.0;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) y += Lt[1][u][tid];
+                st_sc1(a.yv + i * CNB + tid, y);
+            }
+            cf_publish(a, a.dready + i);
+            if (a.tdbg && tid == 0) a.tdbg[16 * i + 7] = __builtin_amdgcn_s_memrealtime();
             continue;
         }
         const bool diag = i == j;
@@ -1451,21 +1545,19 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
         double qd[4], qa[4];
         load_quad(j, j, qd);
         if (!diag) load_quad(i, j, qa);
-        if (diag && tid < CNB) bs[tid] = a.b[j * CNB + tid];
         // ---- updates from the envelope panels p < j, software-pipelined (the next panel's tiles are
         //      fetched into registers when already published, while this panel's products run)
         const int pj = a.pfh[j], pi = diag ? pj : a.pfh[i];
-        double rj[4], ri[4], ry = 0.0;
+        double rj[4], ri[4];
         bool have = false;
         auto ready = [&](int p, bool block) {
             const int* f1 = a.lready + tile_id(j, p);
-            const int* f2 = diag ? a.dready + p : (p >= pi ? a.lready + tile_id(i, p) : nullptr);
+            const int* f2 = (!diag && p >= pi) ? a.lready + tile_id(i, p) : nullptr;
             return block ? cf_wait(a, f1, f2, &s_ok) : cf_test(a, f1, f2, &s_ok);
         };
         auto fetch = [&](int p) {
             cf_fetch(a.Lm + (size_t)(j * CNB) * n + p * CNB, n, rj);
             if (!diag && p >= pi) cf_fetch(a.Lm + (size_t)(i * CNB) * n + p * CNB, n, ri);
-            if (diag && tid < CNB) ry = ld_sc1(a.yv + p * CNB + tid);
         };
         bool ok = true;
         // the panels p in [pj, j) in update order (the same order in every task: the copies of A_jj
@@ -1479,18 +1571,11 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
             }
             cf_put(Lt[0], rj);
             if (!diag && p >= pi) cf_put(Lt[1], ri);
-            if (diag && tid < CNB) ys[tid] = ry;
             __syncthreads();
             have = q + 1 < q1 && ready(a.plist[q + 1] & 4095, false);
             if (have) fetch(a.plist[q + 1] & 4095);
             sub_mma(qd, cf_mma_nt(Lt[0], Lt[0], rb, cb, lr, kq, z4));
             if (!diag && p >= pi) sub_mma(qa, cf_mma_nt(Lt[1], Lt[0], rb, cb, lr, kq, z4));
-            if (diag && tid < CNB) {   // b_j -= L(j, p) y_p
-                double sacc = 0.0;
-#pragma unroll 8
-                for (int c = 0; c < CNB; ++c) sacc += Lt[0][tid][c] * ys[c];
-                bs[tid] -= sacc;
-            }
             __syncthreads();
         }
         if (!ok) return;
@@ -1517,40 +1602,40 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
             if (tm) tm[6] = __builtin_amdgcn_s_memrealtime();
             continue;
         }
-        // ---- panel j: wave 0 [A_jj; b_j^T] -> L_jj, y_j; wave 1 [A_jj; I] -> L_jj^-T
+        // ---- panel j: [A_jj; I] -> L_jj, L_jj^-T on wave 0, published for the L^-1 tasks
         stage_quad(stg[0], 0, qd);
-        stage_quad(stg[1], 0, qd);
-        __syncthreads();
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {   // rows 32..63: b_j^T then zeros / the identity
+        for (int m = 0; m < 4; ++m) {   // rows 32..63: the identity
             const int e = tid + 256 * m, r = e >> 5, c = e & 31;
-            stg[0][CNB + r][c] = (r == 0) ? bs[c] : 0.0;
-            stg[1][CNB + r][c] = (c == r) ? 1.0 : 0.0;
+            stg[0][CNB + r][c] = (c == r) ? 1.0 : 0.0;
         }
         __syncthreads();
         if (tm) tm[4] = __builtin_amdgcn_s_memrealtime();
-        if (wave < 2) {
+        if (wave == 0) {
             bool bad;
-            factor(stg[wave], bad);
-            if (__ballot(bad) != 0 && wave == 0 && lane == 0) *a.info = 1 + (int)p0;
-            if (wave == 0) {   // L_jj (plain: read by the back-substitution launch only), y_j
+            factor(stg[0], bad);
+            if (__ballot(bad) != 0 && lane == 0) *a.info = 1 + (int)p0;
+            if (tm) tm[5] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
-                for (int m = 0; m < 16; ++m) {
-                    const int e = lane + 64 * m, r = e >> 5, c = e & 31;
-                    a.Lm[(p0 + r) * n + p0 + c] = (c <= r) ? stg[0][r][c] : 0.0;
-                }
-                if (lane < CNB) st_sc1(a.yv + p0 + lane, stg[0][CNB][lane]);
-            } else {           // L_jj^-T
-#pragma unroll
-                for (int m = 0; m < 16; ++m) {
-                    const int e = lane + 64 * m;
-                    st_sc1(a.LinvT + p0 * CNB + e, stg[1][CNB + (e >> 5)][e & 31]);
-                }
+            for (int m = 0; m < 16; ++m) {   // L_jj (plain: no reader in this launch), L_jj^-T
+                const int e = lane + 64 * m, r = e >> 5, c = e & 31;
+                a.Lm[(p0 + r) * n + p0 + c] = (c <= r) ? stg[0][r][c] : 0.0;
+                st_sc1(a.LinvT + p0 * CNB + e, stg[0][CNB + r][c]);
             }
         }
-        if (tm) tm[5] = __builtin_amdgcn_s_memrealtime();
-        cf_publish(a, a.dready + j);
+        cf_publish(a, a.fready + j);
         if (tm) tm[6] = __builtin_amdgcn_s_memrealtime();
+        {   // z(j, j) = L_jj^-1 b_j from L_jj^-T (rows 32..63 of the staged panel)
+            const int r = tid >> 3, c0 = (tid & 7) * 4;
+            double zs = 0.0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) zs += stg[0][CNB + c0 + u][r] * a.b[j * CNB + c0 + u];
+            zs += __shfl_xor(zs, 1);
+            zs += __shfl_xor(zs, 2);
+            zs += __shfl_xor(zs, 4);
+            if ((tid & 7) == 0) st_sc1(a.zv + ((size_t)j * a.NP + j) * CNB + r, zs);
+        }
+        cf_publish(a, a.zready + j);
     }
 }
 
@@ -2000,7 +2085,9 @@ void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStr
         a.S = P.S; a.Lm = P.Lm; a.LinvT = P.LinvT; a.b = P.bS; a.yv = P.yv; a.info = P.info;
         a.lready = P.cf_lready; a.dready = P.cf_dready; a.head = P.cf_head; a.abort_flag = P.cf_abort;
         a.tdbg = P.tdbg_chol;
-        a.Linv = P.cf_linv; a.ivready = P.cf_ivready; a.xout = P.xsol; a.pnat = P.pnat;
+        a.tdbg2 = P.tdbg_bs;
+        a.Linv = P.cf_linv; a.ivready = P.cf_ivready; a.xout = P.xsol; a.pnat = P.pnat; a.fready = P.cf_fready;
+        a.zready = P.cf_zready; a.zv = P.cf_zv;
         hipLaunchKernelGGL(k_chol_flow, dim3(min(P.cf_ntasks, 512)), dim3(256), 0, s, a);
         return;
     }

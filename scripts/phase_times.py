@@ -83,6 +83,15 @@ def main():
                 out.append("   panel %3d: " % j + " ".join(f"{x:7.2f}" for x in v))
                 w = [(c[j, 8 + k] - t0) / 100.0 if c[j, 8 + k] else float("nan") for k in range(7)]
                 out.append("   (j+1,j)  : " + " ".join(f"{x:7.2f}" for x in w))
+            yx = [((c[j, 7] - t0) / 100.0, (c[j, 15] - t0) / 100.0) for j in range(npan)]
+            out.append("   forward block y_j published / solution block x_j written:")
+            out.append("   " + "  ".join(f"{j}:{y:.1f}/{x:.1f}" for j, (y, x) in enumerate(yx)))
+            b2 = bs[:npan].astype(np.int64)
+            for rr in range(2):
+                out.append(f"   L^-1 tiles of row {npan - 2 + rr}: j: start / terms done / L_ii^-1 out / published")
+                for j in range(npan - 2 + rr):
+                    v = [(b2[j, 4 * rr + k] - t0) / 100.0 if b2[j, 4 * rr + k] else float("nan") for k in range(4)]
+                    out.append(f"     {j:3d}: " + " ".join(f"{x:7.2f}" for x in v))
             chol = None
     if chol is not None:
         nst = int((chol[:, 0] != 0).sum())
