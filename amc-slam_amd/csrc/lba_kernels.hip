@@ -918,35 +918,37 @@ __device__ __forceinline__ void wave_sync() {
 // compiler from sinking a rank-1 update down to its first use, which keeps O(n^2) operands live)
 __device__ __forceinline__ void pin(double& v) { asm volatile("" : "+v"(v)); }
 
-// 1/sqrt(d): hardware estimate + two Newton steps (full fp64 precision for the pivots of an SPD S)
+// 1/sqrt(d): hardware estimate (5e-8 relative) + one cubically convergent step
+// r' = r + r e (1/2 + 3/8 e), e = 1 - d r^2: 0.62 ulp worst case over 2^20 samples, against 1.08 ulp for
+// two Newton steps, at four dependent operations instead of six (scripts/micro/rsq_accuracy.hip)
 __device__ __forceinline__ double rsqrt_nr(double d) {
-    double r = __builtin_amdgcn_rsq(d);
-    r = r * (1.5 - 0.5 * d * r * r);
-    r = r * (1.5 - 0.5 * d * r * r);
-    return r;
+    const double r = __builtin_amdgcn_rsq(d);
+    const double e = fma(-(d * r), r, 1.0);
+    return fma(r * e, fma(0.375, e, 0.5), r);
 }
 
 // Panel pivot sequence over columns [J, E), generated at compile time (pivot J, update step T,
 // chain op OP) so every row[] index is a constant.  Pivot J: l = row[J] r; column J by readlane;
 // then the rank-1 update row[k] -= l cb[k] (J < k < E), with the next pivot's chain spread through it
-// in source order (the pins keep that order): d = row[J+1] - l^2 on lane J+1, rsq, two Newton steps
-// r <- r (1.5 - 0.5 d r^2), readlane of r from lane J+1 (op s after update step floor(s NF / 7)).
+// in source order (the pins keep that order): d = row[J+1] - l^2 on lane J+1, rsq, the cubic step of
+// rsqrt_nr, readlane of r from lane J+1 (op s after update step floor(s NF / 6)).
 // The panel is factored as two 16-column halves (piv_seq<0, 16>, cross_update, piv_seq<16, 32>), so
 // the pivots' readlane broadcasts cover 2 x 120 entries instead of 496; the 256 products between the
 // halves go through the matrix cores.
 struct Pivot {
-    double lij, hh, c, m, u, rn;
+    double lij, d, c, t, e, m, rn;
 };
 
 template <int J, int E, int T, int OP>
 __device__ __forceinline__ void piv_chain(Pivot& x) {
     constexpr int NF = E - 1 - J;
-    if constexpr (OP < 7) {
-        if constexpr ((OP * NF) / 7 == T) {
-            if constexpr (OP == 0 || OP == 3) { x.m = x.hh * x.c; pin(x.m); }
-            else if constexpr (OP == 1 || OP == 4) { x.u = fma(-x.c, x.m, 1.5); pin(x.u); }
-            else if constexpr (OP == 2 || OP == 5) { x.c = x.c * x.u; pin(x.c); }
-            else { x.rn = readlane_d(x.c, J + 1); pin(x.rn); }
+    if constexpr (OP < 6) {
+        if constexpr ((OP * NF) / 6 == T) {
+            if constexpr (OP == 0) { x.t = x.d * x.c; pin(x.t); }
+            else if constexpr (OP == 1) { x.e = fma(-x.t, x.c, 1.0); pin(x.e); }
+            else if constexpr (OP == 2) { x.t = fma(0.375, x.e, 0.5); x.m = x.c * x.e; pin(x.t); pin(x.m); }
+            else if constexpr (OP == 3) { x.c = fma(x.m, x.t, x.c); pin(x.c); }
+            else if constexpr (OP == 4) { x.rn = readlane_d(x.c, J + 1); pin(x.rn); }
         }
         piv_chain<J, E, T, OP + 1>(x);
     }
@@ -973,12 +975,12 @@ __device__ __forceinline__ void piv_seq(double (&row)[CNB], double r, int lane, 
         Pivot x;
         x.lij = row[J] * r;   // lane J: sqrt(d); lanes > J: L(l, J)
         row[J] = x.lij;
-        x.hh = 0.5; x.c = 1.0; x.m = 0.0; x.u = 0.0; x.rn = 1.0;
+        x.d = 1.0; x.c = 1.0; x.t = 0.0; x.e = 0.0; x.m = 0.0; x.rn = 1.0;
         if constexpr (J + 1 < E) {
             const double own = row[J + 1] - x.lij * x.lij;
             bad = bad || (lane == J + 1 && !(own > 0.0));
             x.c = __builtin_amdgcn_rsq(own);
-            x.hh = 0.5 * own;
+            x.d = own;
         }
         // column J of L_pp by readlane into SGPRs (an LDS broadcast costs (E - 1 - J) doubles per lane
         // of every factoring wave on the CU's shared LDS return path: no faster, measured)
