@@ -215,6 +215,7 @@ struct DevProblem {
     unsigned long long* tdbg_lin;     // [n_tiles][16] k_linearize
     unsigned long long* tdbg_schur;   // [n_tiles][16] k_schur
     unsigned long long* tdbg_chol;    // [npad / CHOL_NB][16] k_chol_step (workgroup 0 of each panel)
+    unsigned long long* tdbg_cf;      // [CF_TDBG_TASKS][8] k_chol_flow factor tasks: stamps, i, j
     unsigned long long* tdbg_bs;      // [npad / CHOL_NB][16] k_chol_backsolve (per block)
 };
 

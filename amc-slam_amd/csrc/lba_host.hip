@@ -99,6 +99,8 @@ void dump_phase_times(lba_problem* p) {
     std::vector<unsigned long long> ch((size_t)nblk * 16), bs((size_t)nblk * 16);
     (void)hipMemcpy(ch.data(), D.tdbg_chol, ch.size() * 8, hipMemcpyDeviceToHost);
     (void)hipMemcpy(bs.data(), D.tdbg_bs, bs.size() * 8, hipMemcpyDeviceToHost);
+    std::vector<unsigned long long> cft((size_t)4096 * 8);
+    (void)hipMemcpy(cft.data(), D.tdbg_cf, cft.size() * 8, hipMemcpyDeviceToHost);
     if (FILE* f = std::fopen(path, "wb")) {
         const int nt = D.n_tiles;
         std::fwrite(&nt, 4, 1, f);
@@ -108,6 +110,7 @@ void dump_phase_times(lba_problem* p) {
         std::fwrite(&nblk, 4, 1, f);
         std::fwrite(ch.data(), 8, ch.size(), f);
         std::fwrite(bs.data(), 8, bs.size(), f);
+        std::fwrite(cft.data(), 8, cft.size(), f);
         std::fclose(f);
     }
 }
@@ -595,6 +598,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         const int nblk = (p->np + CHOL_NB - 1) / CHOL_NB + 1;
         D.tdbg_chol = dalloc<unsigned long long>(p, (size_t)nblk * 16);
         D.tdbg_bs = dalloc<unsigned long long>(p, (size_t)nblk * 16);
+        D.tdbg_cf = dalloc<unsigned long long>(p, (size_t)4096 * 8);
+        HIPCHK(hipMemset(D.tdbg_cf, 0, (size_t)4096 * 8 * 8));
         HIPCHK(hipMemset(D.tdbg_chol, 0, (size_t)nblk * 16 * 8));
         HIPCHK(hipMemset(D.tdbg_bs, 0, (size_t)nblk * 16 * 8));
     }
@@ -704,6 +709,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             }
             for (int k = 0; k < ns; ++k) uord.push_back(nl + nr + k);
             std::vector<int> rank(NP), pl0(1, 0), plist;
+            const bool no_lookahead = std::getenv("LBA_CHOL_NO_LOOKAHEAD") != nullptr;
             for (int q = 0; q < NP; ++q) rank[uord[q]] = q;
             // structure of L^-1: Linv(i,j) != 0 iff some k in [max(j, pfh[i]), i) has Linv(k,j) != 0
             std::vector<std::vector<char>> nz(NP, std::vector<char>(NP, 0));
@@ -715,11 +721,27 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             for (int c = 0; c < NP; ++c) {
                 for (int i = c; i < NP; ++i) {   // factor tiles of column c: panels p in update order
                     if (pfh[i] > c) continue;
-                    tasks.push_back(c | (i << 12));
+                    // lookahead over k = c - 1 when tile (c, k) exists and k is the last update of A(c,c)
+                    // and A(i,c) in update order (then every copy of a tile sees the same update order)
+                    const int k = c - 1;
+                    bool la = !no_lookahead && k >= 0 && pfh[c] <= k;
+                    for (int pp = pfh[c]; la && pp < k; ++pp)
+                        if (rank[pp] > rank[k]) la = false;
                     std::vector<int> ps;
-                    for (int pp = pfh[c]; pp < c; ++pp) ps.push_back(pp);
-                    std::sort(ps.begin(), ps.end(), [&](int x, int y) { return rank[x] < rank[y]; });
-                    for (int pp : ps) plist.push_back(pp | ((pp >= pfh[i]) << 12));
+                    if (la) {
+                        tasks.push_back(c | (i << 12) | (1 << 28));
+                        for (int pp = std::min(std::min(pfh[c], pfh[i]), pfh[k]); pp < k; ++pp) ps.push_back(pp);
+                        std::sort(ps.begin(), ps.end(), [&](int x, int y) { return rank[x] < rank[y]; });
+                        for (int pp : ps) {   // only panels that update a held tile; row i only where it is used
+                            const bool fj = pp >= pfh[c], fk = pp >= pfh[k], fi = pp >= pfh[i] && (fj || fk);
+                            if (fj || fk) plist.push_back(pp | (fi << 12) | (fj << 13) | (fk << 14));
+                        }
+                    } else {
+                        tasks.push_back(c | (i << 12));
+                        for (int pp = pfh[c]; pp < c; ++pp) ps.push_back(pp);
+                        std::sort(ps.begin(), ps.end(), [&](int x, int y) { return rank[x] < rank[y]; });
+                        for (int pp : ps) plist.push_back(pp | ((pp >= pfh[i]) << 12));
+                    }
                     pl0.push_back((int)plist.size());
                 }
                 for (int j = 0; j < c; ++j) {    // L^-1 tiles of row c: terms k ascending

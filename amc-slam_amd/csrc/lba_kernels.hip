@@ -1238,6 +1238,7 @@ struct CholFlow {
     int* abort_flag;
     unsigned long long* tdbg;   // diagnostics: per panel, s_memrealtime stamps of its task
     unsigned long long* tdbg2;  // diagnostics: stamps of the L^-1 tasks of the last two panel rows
+    unsigned long long* tdbg3;  // diagnostics: per factor task (ticket < 4096): stamps, i, j
     // the solve x = L^-T y without a back-substitution chain: L^-1 tiles (computed alongside the
     // factorisation) and per output panel one GEMV
     double* Linv;        // [npad][npad] tiles (i, j), i > j, of L^-1 (factorisation order)
@@ -1246,39 +1247,46 @@ struct CholFlow {
     const int* pnat;     // natural panel of a position
 };
 
-// thread 0 polls up to two flags for `epoch` (relaxed, agent scope); the workgroup learns the result
-__device__ __forceinline__ bool cf_wait(const CholFlow& a, const int* f1, const int* f2, int* s_ok) {
-    if (threadIdx.x == 0) {
-        int ok = 1;
-        const int* fs[2] = {f1, f2};
-        for (int q = 0; q < 2 && ok; ++q) {
-            if (!fs[q]) continue;
-            unsigned spins = 0;
-            while ((unsigned)__hip_atomic_load((gi32_t*)fs[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.epoch) {
-                if (++spins > CF_SPIN_LIMIT ||
-                    ((spins & 255) == 0 &&
-                     (unsigned)__hip_atomic_load((gi32_t*)a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch)) {
+// lanes 0..2 of wave 0 poll up to three flags (null = none) for `epoch` side by side (relaxed, agent
+// scope: one round trip when they are already set, not one per flag); the workgroup learns the result
+__device__ __forceinline__ bool cf_wait(const CholFlow& a, const int* f1, const int* f2, int* s_ok,
+                                        const int* f3 = nullptr) {
+    if (threadIdx.x < 64) {
+        const int l = threadIdx.x;
+        const int* f = l == 0 ? f1 : (l == 1 ? f2 : (l == 2 ? f3 : nullptr));
+        bool done = f == nullptr;
+        bool ok = true;
+        for (unsigned spins = 0;; ++spins) {
+            if (!done) done = (unsigned)__hip_atomic_load((gi32_t*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch;
+            if (__all(done)) break;
+            if (spins > CF_SPIN_LIMIT ||
+                ((spins & 255) == 255 &&
+                 (unsigned)__hip_atomic_load((gi32_t*)a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch)) {
+                if (l == 0) {
                     __hip_atomic_store((gi32_t*)a.abort_flag, (int)a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     *a.info = CF_TIMEOUT;
-                    ok = 0;
-                    break;
                 }
-                __builtin_amdgcn_s_sleep(2);
+                ok = false;
+                break;
             }
+            __builtin_amdgcn_s_sleep(2);
         }
-        *s_ok = ok;
+        if (l == 0) *s_ok = ok ? 1 : 0;
     }
     __syncthreads();
     return *s_ok != 0;
 }
 
-// non-blocking: are both flags (null = none) at `epoch`?  (thread 0 reads, the workgroup learns it)
-__device__ __forceinline__ bool cf_test(const CholFlow& a, const int* f1, const int* f2, int* s_ok) {
-    if (threadIdx.x == 0) {
-        bool ok = true;
-        if (f1) ok = ok && (unsigned)__hip_atomic_load((gi32_t*)f1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch;
-        if (f2) ok = ok && (unsigned)__hip_atomic_load((gi32_t*)f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch;
-        *s_ok = ok ? 1 : 0;
+// non-blocking: are all flags (null = none) at `epoch`?  (lanes 0..2 read, the workgroup learns it)
+__device__ __forceinline__ bool cf_test(const CholFlow& a, const int* f1, const int* f2, int* s_ok,
+                                        const int* f3 = nullptr) {
+    if (threadIdx.x < 64) {
+        const int l = threadIdx.x;
+        const int* f = l == 0 ? f1 : (l == 1 ? f2 : (l == 2 ? f3 : nullptr));
+        const bool done = f == nullptr ||
+                          (unsigned)__hip_atomic_load((gi32_t*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch;
+        const bool all = __all(done);
+        if (l == 0) *s_ok = all ? 1 : 0;
     }
     __syncthreads();
     return *s_ok != 0;
@@ -1358,7 +1366,7 @@ __device__ __forceinline__ d4 cf_mma_nn(const double (*X)[CNB + 1], const double
 }
 
 __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
-    __shared__ double Lt[2][CNB][CNB + 1];       // update operands L(i, p), L(j, p)
+    __shared__ double Lt[3][CNB][CNB + 1];       // update operands L(j, p), L(i, p), L(k, p)
     __shared__ double stg[2][2 * CNB][CNB + 1];  // stacked panels of the factoring waves
     __shared__ long long s_ticket;
     __shared__ int s_ok;
@@ -1402,7 +1410,8 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
         if (t >= a.ntasks) break;
         const int code = a.tasks[t];
         const int j = code & 4095, i = (code >> 12) & 4095;
-        const int kind = code >> 24;
+        const int kind = (code >> 24) & 15;
+        const bool la = (code >> 28) & 1;   // factor task with lookahead over column k = j - 1
         if (kind == 1) {
             // ---------------------------------------------------- L^-1 tile (i, j), i > j:
             // Linv(i,j) = -L_ii^-1 sum_k L(i,k) Linv(k,j) over the list's k (Linv(j,j) = LinvT_j^T)
@@ -1544,42 +1553,101 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
         // diagnostics: stamps of panel j's task (slots 0..6) and of tile (j + 1, j) (slots 8..14)
         unsigned long long* tm = (a.tdbg && tid == 0 && (diag || i == j + 1)) ? a.tdbg + 16 * j + (diag ? 0 : 8) : nullptr;
         if (tm) tm[0] = __builtin_amdgcn_s_memrealtime();
+        unsigned long long* tf = (a.tdbg3 && tid == 0 && t < 4096) ? a.tdbg3 + 8 * t : nullptr;
+        if (tf) { tf[0] = __builtin_amdgcn_s_memrealtime(); tf[4] = i | (j << 12) | ((int)la << 24); }
         double qd[4], qa[4];
         load_quad(j, j, qd);
         if (!diag) load_quad(i, j, qa);
-        // ---- updates from the envelope panels p < j, software-pipelined (the next panel's tiles are
-        //      fetched into registers when already published, while this panel's products run)
-        const int pj = a.pfh[j], pi = diag ? pj : a.pfh[i];
-        double rj[4], ri[4];
+        // lookahead: the task also holds A(k,k), A(j,k), A(i,k) of the previous column k = j - 1, whose
+        // update is the last one of A(j,j) and A(i,j) in update order (the host checks); it factors
+        // column k's two tiles itself, so only L(., p <= k - 1) is waited for, one chain step earlier
+        const int k = j - 1;
+        const bool ik = la && !diag && a.pfh[i] <= k;   // tile (i, k) inside the envelope
+        double qk[4], qjk[4], qik[4];
+        if (la) {
+            load_quad(k, k, qk);
+            load_quad(j, k, qjk);
+            if (ik) load_quad(i, k, qik);
+        }
+        // ---- updates from the envelope panels p (< j, or < k with lookahead), software-pipelined (the
+        //      next panel's tiles are fetched into registers when already published, while this panel's
+        //      products run).  Entry: p | row i takes part << 12 [| row j << 13 | row k << 14 (lookahead)]
+        double rj[4], ri[4], rk[4];
         bool have = false;
-        auto ready = [&](int p, bool block) {
-            const int* f1 = a.lready + tile_id(j, p);
-            const int* f2 = (!diag && p >= pi) ? a.lready + tile_id(i, p) : nullptr;
-            return block ? cf_wait(a, f1, f2, &s_ok) : cf_test(a, f1, f2, &s_ok);
+        auto rows = [&](int e, bool& fj, bool& fi, bool& fk) {
+            fi = !diag && ((e >> 12) & 1);
+            fj = la ? ((e >> 13) & 1) : true;
+            fk = la && ((e >> 14) & 1);
         };
-        auto fetch = [&](int p) {
-            cf_fetch(a.Lm + (size_t)(j * CNB) * n + p * CNB, n, rj);
-            if (!diag && p >= pi) cf_fetch(a.Lm + (size_t)(i * CNB) * n + p * CNB, n, ri);
+        auto ready = [&](int e, bool block) {
+            const int p = e & 4095;
+            bool fj, fi, fk;
+            rows(e, fj, fi, fk);
+            const int* f1 = fj ? a.lready + tile_id(j, p) : nullptr;
+            const int* f2 = fi ? a.lready + tile_id(i, p) : nullptr;
+            const int* f3 = fk ? a.lready + tile_id(k, p) : nullptr;
+            return block ? cf_wait(a, f1, f2, &s_ok, f3) : cf_test(a, f1, f2, &s_ok, f3);
+        };
+        auto fetch = [&](int e) {
+            const int p = e & 4095;
+            bool fj, fi, fk;
+            rows(e, fj, fi, fk);
+            if (fj) cf_fetch(a.Lm + (size_t)(j * CNB) * n + p * CNB, n, rj);
+            if (fi) cf_fetch(a.Lm + (size_t)(i * CNB) * n + p * CNB, n, ri);
+            if (fk) cf_fetch(a.Lm + (size_t)(k * CNB) * n + p * CNB, n, rk);
         };
         bool ok = true;
-        // the panels p in [pj, j) in update order (the same order in every task: the copies of A_jj
-        // stay bitwise identical)
+        // the panels in update order (the same order in every task: the copies of a tile stay bitwise
+        // identical)
         const int q0 = a.pl0[t], q1 = a.pl0[t + 1];
         for (int q = q0; q < q1; ++q) {
-            const int p = a.plist[q] & 4095;
+            const int e = a.plist[q];
+            bool fj, fi, fk;
+            rows(e, fj, fi, fk);
             if (!have) {
-                if (!ready(p, true)) { ok = false; break; }
-                fetch(p);
+                if (!ready(e, true)) { ok = false; break; }
+                if (tf) { tf[3] = __builtin_amdgcn_s_memrealtime(); tf[4] = (tf[4] & 0xffffffull) | ((unsigned long long)(la) << 24) | ((unsigned long long)(e & 4095) << 32); }
+                fetch(e);
             }
-            cf_put(Lt[0], rj);
-            if (!diag && p >= pi) cf_put(Lt[1], ri);
+            if (fj) cf_put(Lt[0], rj);
+            if (fi) cf_put(Lt[1], ri);
+            if (fk) cf_put(Lt[2], rk);
             __syncthreads();
-            have = q + 1 < q1 && ready(a.plist[q + 1] & 4095, false);
-            if (have) fetch(a.plist[q + 1] & 4095);
-            sub_mma(qd, cf_mma_nt(Lt[0], Lt[0], rb, cb, lr, kq, z4));
-            if (!diag && p >= pi) sub_mma(qa, cf_mma_nt(Lt[1], Lt[0], rb, cb, lr, kq, z4));
+            have = q + 1 < q1 && ready(a.plist[q + 1], false);
+            if (have) fetch(a.plist[q + 1]);
+            if (fj) sub_mma(qd, cf_mma_nt(Lt[0], Lt[0], rb, cb, lr, kq, z4));
+            if (fi && fj) sub_mma(qa, cf_mma_nt(Lt[1], Lt[0], rb, cb, lr, kq, z4));
+            if (fk) {
+                sub_mma(qk, cf_mma_nt(Lt[2], Lt[2], rb, cb, lr, kq, z4));
+                if (fj) sub_mma(qjk, cf_mma_nt(Lt[0], Lt[2], rb, cb, lr, kq, z4));
+                if (ik && fi) sub_mma(qik, cf_mma_nt(Lt[1], Lt[2], rb, cb, lr, kq, z4));
+            }
             __syncthreads();
         }
+        if (tf) tf[5] = __builtin_amdgcn_s_memrealtime();
+        if (ok && la) {
+            // ---- column k here: [A(k,k); A(j,k)] on wave 0 and [A(k,k); A(i,k)] on wave 1 -> L(j,k), L(i,k)
+            //      (the same stacked factorisations as the tasks of column k), then the updates from k
+            stage_quad(stg[0], 0, qk);
+            stage_quad(stg[0], CNB, qjk);
+            if (ik) {
+                stage_quad(stg[1], 0, qk);
+                stage_quad(stg[1], CNB, qik);
+            }
+            __syncthreads();
+            if (wave == 0 || (wave == 1 && ik)) {
+                bool bad;
+                factor(stg[wave], bad);
+                (void)bad;   // (reported by panel k's own task)
+            }
+            __syncthreads();
+            if (tf) tf[6] = __builtin_amdgcn_s_memrealtime();
+            sub_mma(qd, cf_mma_nt(stg[0] + CNB, stg[0] + CNB, rb, cb, lr, kq, z4));
+            if (ik) sub_mma(qa, cf_mma_nt(stg[1] + CNB, stg[0] + CNB, rb, cb, lr, kq, z4));
+            __syncthreads();
+            if (tm) tm[2] = __builtin_amdgcn_s_memrealtime();
+        }
+        if (tf) tf[1] = __builtin_amdgcn_s_memrealtime();
         if (!ok) return;
         if (tm) tm[1] = __builtin_amdgcn_s_memrealtime();
         const size_t p0 = (size_t)j * CNB;
@@ -1602,6 +1670,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
             }
             cf_publish(a, a.lready + tile_id(i, j));
             if (tm) tm[6] = __builtin_amdgcn_s_memrealtime();
+            if (tf) tf[2] = __builtin_amdgcn_s_memrealtime();
             continue;
         }
         // ---- panel j: [A_jj; I] -> L_jj, L_jj^-T on wave 0, published for the L^-1 tasks
@@ -1627,6 +1696,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
         }
         cf_publish(a, a.fready + j);
         if (tm) tm[6] = __builtin_amdgcn_s_memrealtime();
+        if (tf) tf[2] = __builtin_amdgcn_s_memrealtime();
         {   // z(j, j) = L_jj^-1 b_j from L_jj^-T (rows 32..63 of the staged panel)
             const int r = tid >> 3, c0 = (tid & 7) * 4;
             double zs = 0.0;
@@ -2088,6 +2158,7 @@ void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStr
         a.lready = P.cf_lready; a.dready = P.cf_dready; a.head = P.cf_head; a.abort_flag = P.cf_abort;
         a.tdbg = P.tdbg_chol;
         a.tdbg2 = P.tdbg_bs;
+        a.tdbg3 = P.tdbg_cf;
         a.Linv = P.cf_linv; a.ivready = P.cf_ivready; a.xout = P.xsol; a.pnat = P.pnat; a.fready = P.cf_fready;
         a.zready = P.cf_zready; a.zv = P.cf_zv;
         hipLaunchKernelGGL(k_chol_flow, dim3(min(P.cf_ntasks, 512)), dim3(256), 0, s, a);

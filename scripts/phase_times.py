@@ -30,14 +30,17 @@ def load(path):
     off += nt * 16 * 8
     shape = np.frombuffer(raw[off:off + 6 * nt * 4], np.int32).reshape(6, nt)
     off += 6 * nt * 4
-    chol = bs = None
+    chol = bs = cft = None
     if len(raw) > off:
         nb = int(np.frombuffer(raw[off:off + 4], np.int32)[0])
         off += 4
         chol = np.frombuffer(raw[off:off + nb * 16 * 8], np.uint64).reshape(nb, 16).astype(np.int64)
         off += nb * 16 * 8
         bs = np.frombuffer(raw[off:off + nb * 16 * 8], np.uint64).reshape(nb, 16).astype(np.int64)
-    return nt, lin, sch, shape, chol, bs
+        off += nb * 16 * 8
+        if len(raw) >= off + 4096 * 8 * 8:
+            cft = np.frombuffer(raw[off:off + 4096 * 8 * 8], np.uint64).reshape(4096, 8).astype(np.int64)
+    return nt, lin, sch, shape, chol, bs, cft
 
 
 def report(name, stamps, phases, shape, out):
@@ -67,7 +70,7 @@ def main():
     p = Problem(win, early_stop=0)
     p.optimize(args.iters)
     p.close()
-    nt, lin, sch, shape, chol, bs = load(args.dump)
+    nt, lin, sch, shape, chol, bs, cft = load(args.dump)
     out = [f"config {args.config}: {nt} tiles"]
     report("k_linearize", lin, LIN_PHASES, shape, out)
     report("k_schur", sch, SCHUR_PHASES, shape, out)
@@ -92,6 +95,17 @@ def main():
                 for j in range(npan - 2 + rr):
                     v = [(b2[j, 4 * rr + k] - t0) / 100.0 if b2[j, 4 * rr + k] else float("nan") for k in range(4)]
                     out.append(f"     {j:3d}: " + " ".join(f"{x:7.2f}" for x in v))
+            if cft is not None:
+                out.append("   factor tasks (ticket: i j lookahead | start / last blocking wait done (panel) / loop done / "
+                           "lookahead factors done / loop+lookahead done / published)")
+                for tk in range(4096):
+                    r = cft[tk]
+                    if r[0] == 0:
+                        continue
+                    f = lambda x: (x - t0) / 100.0 if x else float("nan")
+                    ii, jj, la, pp = r[4] & 4095, (r[4] >> 12) & 4095, (r[4] >> 24) & 1, (r[4] >> 32) & 4095
+                    out.append(f"     {tk:4d}: ({ii:2d},{jj:2d}) la={la} | {f(r[0]):7.2f} {f(r[3]):7.2f} (p={pp:2d}) "
+                               f"{f(r[5]):7.2f} {f(r[6]):7.2f} {f(r[1]):7.2f} {f(r[2]):7.2f}")
             chol = None
     if chol is not None:
         nst = int((chol[:, 0] != 0).sum())
