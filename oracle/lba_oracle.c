@@ -1146,6 +1146,37 @@ int orc_solve(orc_problem* p, double lambda, double* dx) {
     return ok;
 }
 
+/* Size-independent check of a damped step (the linear system block_solver.hpp:354-486 solves):
+ * r = (H + lambda I) dx - b over the full [pose | landmark] system of the last buildSystem, with
+ * H's upper Hpp, Hpl and Hll blocks (block_solver.hpp:564-589 for the damping).  O(nnz), so the
+ * GPU step can be checked at sizes where the dense pivoted LDLT takes too long. */
+void orc_normal_residual(const orc_problem* p, double lambda, const double* dx, double* r) {
+    const int n = p->np, nlb = p->n_lm_blocks;
+    for (int i = 0; i < n + p->nl; ++i) r[i] = -p->b[i];
+    for (int i = 0; i < n; ++i) {
+        const double* Hi = p->Hpp + (size_t)i * n;
+        double acc = (Hi[i] + lambda) * dx[i];
+        for (int j = i + 1; j < n; ++j)
+            if (Hi[j] != 0.0) { acc += Hi[j] * dx[j]; r[j] += Hi[j] * dx[i]; }
+        r[i] += acc;
+    }
+    for (int l = 0; l < nlb; ++l) {
+        const double* xl = dx + n + 3 * l;
+        double* rl = r + n + 3 * l;
+        for (int d = 0; d < 3; ++d)
+            for (int e = 0; e < 3; ++e) rl[d] += (p->Hll[9 * l + 3 * d + e] + (d == e ? lambda : 0.0)) * xl[e];
+        for (int k = p->hpl_start[l]; k < p->hpl_start[l + 1]; ++k) {
+            const int i1 = p->hpl_pose[k];
+            const double* B = p->hpl_blk + 36 * k;
+            for (int a = 0; a < 12; ++a)
+                for (int d = 0; d < 3; ++d) {
+                    r[12 * i1 + a] += B[a * 3 + d] * xl[d];
+                    rl[d] += B[a * 3 + d] * dx[12 * i1 + a];
+                }
+        }
+    }
+}
+
 /* ------------------------------------------------------------------ LM */
 static void push_state(orc_problem* p) {
     memcpy(p->kf_bak, p->kf, sizeof(kf_t) * p->n_kf);

@@ -36,6 +36,8 @@ double orc_compute_errors(orc_problem* p, double* residuals, double* obs_chi2);
 int    orc_build_system(orc_problem* p, double* H_pp, double* b, double* H_ll);
 /* setLambda + BlockSolver::solve + restoreDiagonal on the last buildSystem; dx [np + nl] */
 int    orc_solve(orc_problem* p, double lambda, double* dx);
+/* r = (H + lambda I) dx - b on the last buildSystem (full pose + landmark system, O(nnz)); r [np + nl] */
+void   orc_normal_residual(const orc_problem* p, double lambda, const double* dx, double* r);
 /* Full LM: returns iterations; stats may be NULL */
 int    orc_optimize(orc_problem* p, int iters, lba_stats* stats);
 void   orc_get_state(const orc_problem* p, lba_kf* kfs, double* lm_xyz);

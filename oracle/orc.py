@@ -43,6 +43,8 @@ def lib():
         L.orc_compute_errors.argtypes = [ctypes.c_void_p, _dp, _dp]
         L.orc_build_system.argtypes = [ctypes.c_void_p, _dp, _dp, _dp]
         L.orc_solve.argtypes = [ctypes.c_void_p, ctypes.c_double, _dp]
+        L.orc_normal_residual.argtypes = [ctypes.c_void_p, ctypes.c_double, _dp, _dp]
+        L.orc_normal_residual.restype = None
         L.orc_optimize.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(LbaStats)]
         L.orc_get_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _dp]
         L.orc_depth_ok.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
@@ -110,6 +112,13 @@ class Oracle:
         dx = np.zeros(self.pose_dim + self.lm_dim)
         ok = lib().orc_solve(self.h, lam, _d(dx))
         return bool(ok), dx
+
+    def normal_residual(self, lam, dx):
+        """(H + lam I) dx - b on the last build_system (size-independent step check)."""
+        dx = np.ascontiguousarray(dx, float)
+        r = np.zeros(self.pose_dim + self.lm_dim)
+        lib().orc_normal_residual(self.h, lam, _d(dx), _d(r))
+        return r
 
     def optimize(self, iters):
         st = LbaStats()

@@ -24,6 +24,8 @@ WINDOWS = {
     "mono_only": dict(n_opt_kf=9, n_fixed=1, n_lm=400, obs_per_lm=5, n_cam=1, gp=False, seed=3),
     "two_fixed": dict(n_opt_kf=6, n_fixed=2, n_lm=300, obs_per_lm=6, n_cam=4, gp=True, seed=4),
     "global_shape": dict(n_opt_kf=11, n_fixed=1, n_lm=500, obs_per_lm=6, n_cam=4, gp=True, global_ba=True, seed=5),
+    # BundleAdjustment shape with 37 factorisation panels (deep dependent chain, banded S)
+    "global_mid": dict(n_opt_kf=99, n_fixed=1, n_lm=8000, obs_per_lm=6, n_cam=4, gp=True, global_ba=True, seed=6),
 }
 
 
@@ -133,6 +135,33 @@ def test_cfg1_full_size_lm_properties():
     kf1, lm1 = p.state()
     kf2, lm2 = p2.state()
     assert np.array_equal(lm1, lm2) and np.array_equal(kf1["t"], kf2["t"])
+
+
+def test_cfg2_global_full_size_parity():
+    """BASELINE config 2 (global BA: 500 KF / 200k landmarks / 1.2M observations, S = 5988^2).
+    Residuals, H_pp and b against the oracle at full size; the damped step through the
+    size-independent normal-equation residual (H + lambda I) dx - b (the oracle's pivoted dense
+    LDLT takes ~50 s at this size; global_mid checks dx itself); LM descent and determinism."""
+    win = make_config_window("cfg2_global_500kf")
+    o = orc.Oracle(win)
+    chi_o, res_o, _ = o.errors()
+    H_o, b_o, _ = o.build_system()
+    p = Problem(win, early_stop=0)
+    res, H, b, _ = p.linearize()
+    assert np.linalg.norm(res - res_o) / np.linalg.norm(res_o) <= 1e-8
+    assert _rel(H, H_o) < 1e-9 and _rel(b, b_o) < 1e-9
+    del H, H_o
+    lam = win.cfg["lambda_init"]
+    ok, dx = p.solve_step(lam)
+    assert ok
+    r = o.normal_residual(lam, dx)
+    assert np.abs(r).max() <= 1e-8 * np.abs(b_o).max(), np.abs(r).max() / np.abs(b_o).max()
+    n, st = p.optimize(3)
+    assert n == 3 and st.chi2_final < st.chi2_initial
+    assert abs(st.chi2_initial - chi_o) <= 1e-9 * chi_o
+    p2 = Problem(win, early_stop=0)
+    n2, st2 = p2.optimize(3)
+    assert st2.chi2_final == st.chi2_final and st2.trials == st.trials
 
 
 @pytest.mark.parametrize("early_stop", [1, 0])
