@@ -54,7 +54,8 @@ def lib():
 
 
 def exported_symbols():
-    return ["lba_abi_version", "lba_create", "lba_destroy", "lba_last_error", "lba_set_problem", "lba_optimize",
+    return ["lba_abi_version", "lba_create", "lba_destroy", "lba_last_error", "lba_set_config", "lba_set_problem",
+            "lba_optimize",
             "lba_get_state", "lba_set_state", "lba_eval", "lba_linearize", "lba_solve_step", "lba_pose_dim"]
 
 

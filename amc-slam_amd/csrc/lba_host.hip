@@ -1190,6 +1190,18 @@ void lba_destroy(lba_problem* p) {
     delete p;
 }
 
+int lba_set_config(lba_problem* p, const lba_config* cfg) {
+    if (!p || !cfg) return LBA_E_ARG;
+    if (cfg->device != p->cfg.device) {
+        p->err = "lba_set_config cannot move a problem to another device";
+        return LBA_E_ARG;
+    }
+    p->cfg = *cfg;
+    if (p->cfg.max_trials <= 0) p->cfg.max_trials = 10;
+    if (p->cfg.tau <= 0) p->cfg.tau = 1e-5;
+    return LBA_OK;
+}
+
 const char* lba_last_error(const lba_problem* p) { return p ? p->err.c_str() : "null problem"; }
 
 int lba_pose_dim(const lba_problem* p) { return p && p->has_problem ? p->np : 0; }

@@ -133,6 +133,11 @@ void        lba_destroy(lba_problem* p);
 const char* lba_last_error(const lba_problem* p);
 int         lba_abi_version(void);
 
+/* Replace the configuration (Huber deltas, lambda0, Qc, flags) of an existing problem, e.g. between
+ * LocalGPBA calls with and without bLarge (OptimizationAlgorithmLevenberg::setUserLambdaInit,
+ * RobustKernelHuber::setDelta).  Takes effect at the next lba_set_problem; the device cannot change. */
+int lba_set_config(lba_problem* p, const lba_config* cfg);
+
 /* Copy a window to the device (replaces SparseOptimizer::addVertex/addEdge +
  * initializeOptimization, sparse_optimizer.cpp:197-267).  vel_kfs lists the KFs carrying an
  * EdgeVelocity (info QcInv(2,2), Optimizer.cc:858-870). */
