@@ -46,6 +46,9 @@ constexpr int TILE_SLIST = 1024;    // Schur (pair, pair, landmark) triples per 
 constexpr int TILE_SENT = TILE_KF * (TILE_KF + 1) / 2;   // KF-pair Schur entries per tile
 
 constexpr int CHOL_NB = 32;         // Cholesky panel / tile width
+constexpr int CF_DENSE_MAX_NP = 192;   // panels up to which the L^-1-tile solve is allowed (np 6144)
+constexpr int CF_AUTO_BAND_NP = 64;    // above this many panels the substitution solve is the default
+                                       // (measured crossover ~65 panels, profiles/r01zr_solve_sweep.txt)
 constexpr int RED_GROUPS = 4;       // reduction kernels: 4 groups x 144 threads
 
 // Levenberg-Marquardt controller of a queued optimisation (lba_host.hip: optimize_queued).  The host
@@ -187,6 +190,8 @@ struct DevProblem {
     unsigned long long* cf_head;
     int* cf_abort;
     int cf_steps_path;      // LBA_CHOL_STEPS: the k_chol_step sequence instead
+    int cf_band;            // 1: solve by substitution tasks (no L^-1 tiles, large systems)
+    double* cf_xpos;        // band solve: x in factorisation order (handed off between back tasks)
     double* LinvT;          // [npad / CHOL_NB][CHOL_NB][CHOL_NB] inverse diagonal blocks L_bb^-T (row-major)
     double* Hpl;
     double* Hll;

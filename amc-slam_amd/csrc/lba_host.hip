@@ -238,7 +238,10 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         if (kf_act[k] && !kfs[k].fixed) p->kf_hidx[k] = n_pb++;
     p->n_pb = n_pb;
     p->np = 12 * n_pb;
-    if (p->np > 6144) throw ApiError{LBA_E_LIMIT, "pose system larger than 6144 (512 keyframes) not supported yet"};
+    if (p->np > 4095 * CHOL_NB)
+        throw ApiError{LBA_E_LIMIT, "pose system larger than 131040 (10920 keyframes) not supported"};
+    if ((p->cfg.flags & LBA_FLAG_DENSE_SOLVE) && p->np > CF_DENSE_MAX_NP * CHOL_NB)
+        throw ApiError{LBA_E_LIMIT, "the L^-1-tile solve is limited to pose systems of 6144"};
     const std::vector<int>& H = p->kf_hidx;
 
     // ---- device landmark order: by the span of non-fixed KFs observing them
@@ -675,6 +678,11 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         // launch schedule: steps of (panel A, panel B); work items per step: a diagonal item per panel
         // (publishes L_pp, L_pp^-T, y_p) and every trailing tile inside the envelope with the mask
         // of the step's panels that update it.  Item: i | j << 10 | mask << 20 | diag << 22.
+        // solve path: L^-1 tiles (the solve has no substitution chain, but L^-1 of a banded factor is
+        // dense: O(n^3) work) up to CF_AUTO_BAND_NP panels, substitution tasks above (or when asked)
+        const bool band = !(p->cfg.flags & LBA_FLAG_DENSE_SOLVE) &&
+                          ((p->cfg.flags & LBA_FLAG_BAND_SOLVE) || NP > CF_AUTO_BAND_NP);
+        D.cf_band = band ? 1 : 0;
         std::vector<int> steps, items;
         auto add_step = [&](int pa, int pb) {
             const int it0 = (int)items.size();
@@ -690,8 +698,10 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 }
             steps.push_back(pa); steps.push_back(pb); steps.push_back(it0); steps.push_back((int)items.size());
         };
-        for (int k = 0; k < std::max(nl, nr); ++k) add_step(k < nl ? k : -1, k < nr ? nl + k : -1);
-        for (int k = 0; k < ns; ++k) add_step(nl + nr + k, -1);
+        if (!band) {   // (the k_chol_step schedule: O(NP^3) to build, dense systems only)
+            for (int k = 0; k < std::max(nl, nr); ++k) add_step(k < nl ? k : -1, k < nr ? nl + k : -1);
+            for (int k = 0; k < ns; ++k) add_step(nl + nr + k, -1);
+        }
         p->chol_steps = steps;
         D.h_steps = p->chol_steps.data();
         D.n_steps = (int)steps.size() / 4;
@@ -712,13 +722,16 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             const bool no_lookahead = std::getenv("LBA_CHOL_NO_LOOKAHEAD") != nullptr;
             for (int q = 0; q < NP; ++q) rank[uord[q]] = q;
             // structure of L^-1: Linv(i,j) != 0 iff some k in [max(j, pfh[i]), i) has Linv(k,j) != 0
-            std::vector<std::vector<char>> nz(NP, std::vector<char>(NP, 0));
-            for (int j = 0; j < NP; ++j) {
+            std::vector<std::vector<char>> nz(band ? 0 : NP, std::vector<char>(band ? 0 : NP, 0));
+            for (int j = 0; !band && j < NP; ++j) {
                 nz[j][j] = 1;
                 for (int i = j + 1; i < NP; ++i)
                     for (int k = std::max(j, pfh[i]); k < i && !nz[i][j]; ++k) nz[i][j] = nz[k][j];
             }
-            for (int c = 0; c < NP; ++c) {
+            // band mode visits the columns in update order (left k and right k side by side), so the
+            // two halves of the nested dissection are factored and substituted concurrently
+            for (int cq = 0; cq < NP; ++cq) {
+                const int c = band ? uord[cq] : cq;
                 for (int i = c; i < NP; ++i) {   // factor tiles of column c: panels p in update order
                     if (pfh[i] > c) continue;
                     // lookahead over k = c - 1 when tile (c, k) exists and k is the last update of A(c,c)
@@ -744,6 +757,15 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     }
                     pl0.push_back((int)plist.size());
                 }
+                if (band) {   // forward substitution y_c = L_cc^-1 (b_c - sum_k L(c,k) y_k), k in update order
+                    tasks.push_back(c | (c << 12) | (4 << 24));
+                    std::vector<int> ks;
+                    for (int k = pfh[c]; k < c; ++k) ks.push_back(k);
+                    std::sort(ks.begin(), ks.end(), [&](int x, int y) { return rank[x] < rank[y]; });
+                    for (int k : ks) plist.push_back(k);
+                    pl0.push_back((int)plist.size());
+                    continue;
+                }
                 for (int j = 0; j < c; ++j) {    // L^-1 tiles of row c: terms k ascending
                     if (!nz[c][j]) continue;
                     tasks.push_back(j | (c << 12) | (1 << 24));
@@ -756,7 +778,23 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     if (nz[c][k]) plist.push_back(k);
                 pl0.push_back((int)plist.size());
             }
-            for (int j = 0; j < NP; ++j) {      // solution blocks: rows i >= j of column j of L^-1
+            if (band) {
+                // back substitution x_j = L_jj^-T (y_j - sum_i L(i,j)^T x_i) over the rows i > j of the
+                // envelope, columns in reverse update order (separator first, then left and right side
+                // by side), terms in the order their x_i complete
+                std::vector<std::vector<int>> rows_of(NP);
+                for (int i = 0; i < NP; ++i)
+                    for (int j = pfh[i]; j < i; ++j) rows_of[j].push_back(i);
+                for (int cq = NP - 1; cq >= 0; --cq) {
+                    const int j = uord[cq];
+                    tasks.push_back(j | (j << 12) | (5 << 24));
+                    std::vector<int>& is = rows_of[j];
+                    std::sort(is.begin(), is.end(), [&](int x, int y) { return rank[x] > rank[y]; });
+                    for (int i : is) plist.push_back(i);
+                    pl0.push_back((int)plist.size());
+                }
+            }
+            for (int j = 0; !band && j < NP; ++j) {      // solution blocks: rows i >= j of column j of L^-1
                 tasks.push_back(j | (j << 12) | (2 << 24));
                 for (int i = j; i < NP; ++i)
                     if (nz[i][j]) plist.push_back(i);
@@ -766,9 +804,12 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             D.cf_tasks = dupload(p, tasks);
             D.cf_ntasks = (int)tasks.size();
             D.cf_tbase = dupload(p, tbase);
-            D.cf_linv = dalloc<double>(p, (size_t)npad * npad);
-            D.cf_ivready = dalloc<int>(p, std::max(NP * (NP + 1) / 2, 1));
-            HIPCHK(hipMemset(D.cf_ivready, 0, sizeof(int) * std::max(NP * (NP + 1) / 2, 1)));
+            // band mode: no L^-1 tiles; ivready then flags the back-substituted blocks x_j
+            const size_t niv = band ? (size_t)NP + 1 : (size_t)std::max(NP * (NP + 1) / 2, 1);
+            D.cf_linv = band ? nullptr : dalloc<double>(p, (size_t)npad * npad);
+            D.cf_ivready = dalloc<int>(p, niv);
+            HIPCHK(hipMemset(D.cf_ivready, 0, sizeof(int) * niv));
+            D.cf_xpos = band ? dalloc<double>(p, npad) : nullptr;
             D.cf_pl0 = dupload(p, pl0);
             D.cf_plist = dupload(p, plist);
             D.cf_lready = dalloc<int>(p, std::max(tbase[NP], 1));
@@ -777,14 +818,14 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             HIPCHK(hipMemset(D.cf_fready, 0, sizeof(int) * std::max(NP, 1)));
             D.cf_zready = dalloc<int>(p, std::max(NP, 1));
             HIPCHK(hipMemset(D.cf_zready, 0, sizeof(int) * std::max(NP, 1)));
-            D.cf_zv = dalloc<double>(p, std::max((size_t)NP * NP * CHOL_NB, (size_t)1));
+            D.cf_zv = band ? nullptr : dalloc<double>(p, std::max((size_t)NP * NP * CHOL_NB, (size_t)1));
             D.cf_head = dalloc<unsigned long long>(p, 1);
             D.cf_abort = dalloc<int>(p, 1);
             HIPCHK(hipMemset(D.cf_lready, 0, sizeof(int) * std::max(tbase[NP], 1)));
             HIPCHK(hipMemset(D.cf_dready, 0, sizeof(int) * std::max(NP, 1)));
             HIPCHK(hipMemset(D.cf_head, 0, sizeof(unsigned long long)));
             HIPCHK(hipMemset(D.cf_abort, 0, sizeof(int)));
-            D.cf_steps_path = std::getenv("LBA_CHOL_STEPS") ? 1 : 0;
+            D.cf_steps_path = (!band && std::getenv("LBA_CHOL_STEPS")) ? 1 : 0;
         }
         D.pfirst = dupload(p, pfh);
         D.ppos = dupload(p, ppos);

@@ -1245,6 +1245,9 @@ struct CholFlow {
     int* ivready;        // per lower tile (tri_id): epoch once Linv(i, j) is published
     double* xout;        // the solution, natural panel order
     const int* pnat;     // natural panel of a position
+    // band mode (kinds 4, 5): forward / back substitution tasks instead of L^-1 tiles
+    double* xpos;        // [npad] x in factorisation order, handed off between back tasks
+    int* xready;         // per panel: epoch once x_j is published
 };
 
 // lanes 0..2 of wave 0 poll up to three flags (null = none) for `epoch` side by side (relaxed, agent
@@ -1516,6 +1519,81 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
             __syncthreads();
             continue;
         }
+        if (kind == 4) {
+            // ---------------------------------------------------- band mode, forward substitution:
+            // y_i = L_ii^-1 (b_i - sum_k L(i,k) y_k) over the list's k (update order); thread (r, g) takes
+            // row r, columns 4g .. 4g + 3 of every term
+            const int r = tid & 31, g = tid >> 5;
+            double acc = 0.0;
+            for (int q = a.pl0[t]; q < a.pl0[t + 1]; ++q) {
+                const int kk = a.plist[q] & 4095;
+                if (!cf_wait(a, a.lready + tile_id(i, kk), a.dready + kk, &s_ok)) return;
+                double lv[4], yk[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    lv[u] = ld_sc1(a.Lm + (size_t)(i * CNB + r) * n + kk * CNB + 4 * g + u);
+                    yk[u] = ld_sc1(a.yv + kk * CNB + 4 * g + u);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc += lv[u] * yk[u];
+            }
+            if (!cf_wait(a, a.fready + i, nullptr, &s_ok)) return;
+            Lt[1][g][r] = acc;
+            __syncthreads();
+            if (tid < CNB) {
+                double v = a.b[i * CNB + tid];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v -= Lt[1][u][tid];
+                Lt[0][0][tid] = v;
+            }
+            __syncthreads();
+            if (tid < CNB) {   // (L_ii^-1 v)[r] = sum_c LinvT_i[c][r] v[c]
+                double y = 0.0;
+#pragma unroll 8
+                for (int c = 0; c < CNB; ++c) y += ld_sc1(a.LinvT + (size_t)i * CNB * CNB + c * CNB + tid) * Lt[0][0][c];
+                st_sc1(a.yv + i * CNB + tid, y);
+            }
+            cf_publish(a, a.dready + i);
+            continue;
+        }
+        if (kind == 5) {
+            // ---------------------------------------------------- band mode, back substitution:
+            // x_j = L_jj^-T (y_j - sum_i L(i,j)^T x_i) over the list's rows i > j (completion order);
+            // thread (c, g) takes output c, rows 4g .. 4g + 3 of every term
+            const int c = tid & 31, g = tid >> 5;
+            double acc = 0.0;
+            for (int q = a.pl0[t]; q < a.pl0[t + 1]; ++q) {
+                const int ii = a.plist[q] & 4095;
+                if (!cf_wait(a, a.lready + tile_id(ii, j), a.xready + ii, &s_ok)) return;
+                double lv[4], xi[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    lv[u] = ld_sc1(a.Lm + (size_t)(ii * CNB + 4 * g + u) * n + j * CNB + c);
+                    xi[u] = ld_sc1(a.xpos + ii * CNB + 4 * g + u);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc += lv[u] * xi[u];
+            }
+            if (!cf_wait(a, a.fready + j, a.dready + j, &s_ok)) return;
+            Lt[1][g][c] = acc;
+            __syncthreads();
+            if (tid < CNB) {
+                double v = ld_sc1(a.yv + j * CNB + tid);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v -= Lt[1][u][tid];
+                Lt[0][0][tid] = v;
+            }
+            __syncthreads();
+            if (tid < CNB) {   // (L_jj^-T v)[c] = sum_r LinvT_j[c][r] v[r]
+                double x = 0.0;
+#pragma unroll 8
+                for (int rr = 0; rr < CNB; ++rr) x += ld_sc1(a.LinvT + (size_t)j * CNB * CNB + tid * CNB + rr) * Lt[0][0][rr];
+                st_sc1(a.xpos + j * CNB + tid, x);
+                a.xout[a.pnat[j] * CNB + tid] = x;
+            }
+            cf_publish(a, a.xready + j);
+            continue;
+        }
         if (kind == 3) {
             // ---------------------------------------------------- y_i = sum_k z(i, k) over the list's k
             // (z(i, k) = Linv(i, k) b_k, made by the tasks of Linv(i, k) and panel i): the forward solve
@@ -1697,7 +1775,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
         cf_publish(a, a.fready + j);
         if (tm) tm[6] = __builtin_amdgcn_s_memrealtime();
         if (tf) tf[2] = __builtin_amdgcn_s_memrealtime();
-        {   // z(j, j) = L_jj^-1 b_j from L_jj^-T (rows 32..63 of the staged panel)
+        if (a.zv) {   // z(j, j) = L_jj^-1 b_j from L_jj^-T (rows 32..63 of the staged panel)
             const int r = tid >> 3, c0 = (tid & 7) * 4;
             double zs = 0.0;
 #pragma unroll
@@ -2161,6 +2239,7 @@ void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStr
         a.tdbg3 = P.tdbg_cf;
         a.Linv = P.cf_linv; a.ivready = P.cf_ivready; a.xout = P.xsol; a.pnat = P.pnat; a.fready = P.cf_fready;
         a.zready = P.cf_zready; a.zv = P.cf_zv;
+        a.xpos = P.cf_xpos; a.xready = P.cf_ivready;
         hipLaunchKernelGGL(k_chol_flow, dim3(min(P.cf_ntasks, 512)), dim3(256), 0, s, a);
         return;
     }

@@ -100,6 +100,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=20250912)
+    ap.add_argument("--solve", choices=("auto", "band", "dense"), default="auto",
+                    help="reduced-system solve: L^-1 tiles (dense) or substitution (band); auto picks by size")
     args = ap.parse_args()
 
     import torch
@@ -123,7 +125,8 @@ def main():
         ex = None
     # the timed run records HIP events around every k_linearize launch (LBA_FLAG_TIME_SWEEP): the
     # roofline below is measured live, per launch, over the timed region
-    prob = amc_lba.Problem(win, device=local, early_stop=0, flags=amc_lba.abi.FLAG_TIME_SWEEP)
+    solve_flag = {"auto": 0, "band": amc_lba.abi.FLAG_BAND_SOLVE, "dense": amc_lba.abi.FLAG_DENSE_SOLVE}[args.solve]
+    prob = amc_lba.Problem(win, device=local, early_stop=0, flags=amc_lba.abi.FLAG_TIME_SWEEP | solve_flag)
 
     # warmup (not timed)
     if args.warmup > 0:
@@ -155,7 +158,7 @@ def main():
 
     if rank == 0:
         # phase breakdown from a separate, untimed run with every phase evented
-        ph = amc_lba.Problem(win, device=local, early_stop=0, flags=amc_lba.abi.FLAG_TIME_PHASES)
+        ph = amc_lba.Problem(win, device=local, early_stop=0, flags=amc_lba.abi.FLAG_TIME_PHASES | solve_flag)
         n_ph, st_ph = ph.optimize(args.window_iters)
         phase = {k: getattr(st_ph, k) / max(n_ph, 1) for k in ("ms_linearize", "ms_schur", "ms_solve", "ms_update_eval")}
         phase["trials"] = st_ph.trials / max(n_ph, 1)
@@ -183,7 +186,7 @@ def main():
             "data": "synthetic (deterministic generator, amc_lba/synth.py, seed %d)" % args.seed,
             "config": {"workload": workload, "n_kf": int(len(win.kfs)), "n_opt_kf": int((win.kfs["fixed"] == 0).sum()),
                        "n_lm": int(len(win.lm)), "n_obs": int(len(win.obs)), "n_pairs": int(win.n_pairs),
-                       "n_cam": int(len(win.cams)), "window_iters": args.window_iters,
+                       "n_cam": int(len(win.cams)), "window_iters": args.window_iters, "solve": args.solve,
                        "parallelism": f"window farm x{world}" if world > 1 else "single window"},
             "roofline": {"bound": "hbm", "kernel": "k_linearize", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,

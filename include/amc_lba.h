@@ -54,6 +54,10 @@ extern "C" {
                                      host-driven loop */
 #define LBA_FLAG_HOST_LOOP    4   /* take every LM decision on the host, one trial at a time (default:
                                      the trials are queued and decided on the device; same results) */
+#define LBA_FLAG_BAND_SOLVE   8   /* solve the reduced camera system by forward / back substitution after
+                                     the factorisation instead of through the tiles of L^-1 (default:
+                                     chosen by size; large pose systems always take this path) */
+#define LBA_FLAG_DENSE_SOLVE 16   /* force the L^-1-tile solve (pose systems up to 6144 only) */
 
 /* LM termination codes in lba_stats.result (OptimizationAlgorithm::SolverResult) */
 #define LBA_RESULT_OK         0
