@@ -49,14 +49,52 @@ def lib():
         L.lba_eval.argtypes = [vp, _dp, _dp, vp]
         L.lba_linearize.argtypes = [vp, _dp, _dp, _dp, _dp]
         L.lba_solve_step.argtypes = [vp, ctypes.c_double, _dp]
+        L.lba_set_config.argtypes = [vp, ctypes.POINTER(LbaConfig)]
+        L.lba_set_partition.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp, vp]
+        L.lba_rccl_unique_id.argtypes = [ctypes.c_char_p]
+        L.lba_set_partition_rccl.argtypes = [vp, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32]
+        L.lba_group_create.argtypes = [ctypes.POINTER(vp), ctypes.c_int32]
+        L.lba_group_destroy.argtypes = [vp]
+        L.lba_group_destroy.restype = None
+        L.lba_set_partition_group.argtypes = [vp, vp, ctypes.c_int32]
         _lib = L
     return _lib
 
 
 def exported_symbols():
     return ["lba_abi_version", "lba_create", "lba_destroy", "lba_last_error", "lba_set_config", "lba_set_problem",
-            "lba_optimize",
-            "lba_get_state", "lba_set_state", "lba_eval", "lba_linearize", "lba_solve_step", "lba_pose_dim"]
+            "lba_optimize", "lba_get_state", "lba_set_state", "lba_eval", "lba_linearize", "lba_solve_step",
+            "lba_pose_dim", "lba_set_partition", "lba_rccl_unique_id", "lba_set_partition_rccl", "lba_group_create",
+            "lba_group_destroy", "lba_set_partition_group"]
+
+
+class Group:
+    """In-process all-reduce group of `n` problems on one device (lba_group): the partitioned global
+    BA of several ranks driven from threads of one process (tests, single-GPU rehearsal)."""
+
+    def __init__(self, n):
+        self.h = ctypes.c_void_p()
+        rc = lib().lba_group_create(ctypes.byref(self.h), n)
+        if rc != 0:
+            raise LbaError(rc, "lba_group_create failed")
+        self.n = n
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().lba_group_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        self.close()
+
+
+def rccl_unique_id():
+    """128-byte RCCL unique id (one rank creates it, the caller shares it, e.g. via torch.distributed)."""
+    buf = ctypes.create_string_buffer(128)
+    rc = lib().lba_rccl_unique_id(buf)
+    if rc != 0:
+        raise LbaError(rc, "lba_rccl_unique_id failed")
+    return buf.raw
 
 
 def _d(a):
@@ -66,7 +104,10 @@ def _d(a):
 class Problem:
     """One local-BA window resident on one GPU (lba_create + lba_set_problem)."""
 
-    def __init__(self, win, cfg=None, device=0, **cfg_over):
+    def __init__(self, win, cfg=None, device=0, group=None, rank=0, rccl_id=None, nranks=1, **cfg_over):
+        """group / rank: partitioned problem in an in-process Group; rccl_id / rank / nranks: partitioned
+        across processes over RCCL.  Construction is then collective (set_problem agrees on the
+        union envelope), so the ranks' constructors must run concurrently."""
         L = lib()
         if cfg is None:
             kw = dict(win.cfg)
@@ -81,6 +122,11 @@ class Problem:
         self._keep = tuple(np.ascontiguousarray(a) for a in (win.kfs, win.lm, win.obs, win.priors, win.vel_kfs,
                                                               win.cams))
         kfs, lm, obs, pri, vel, cams = self._keep
+        self.group = group
+        if group is not None:
+            self._check(L.lba_set_partition_group(self.h, group.h, rank))
+        elif rccl_id is not None and nranks > 1:
+            self._check(L.lba_set_partition_rccl(self.h, rccl_id, rank, nranks))
         self._check(L.lba_set_problem(self.h, ptr(kfs), len(kfs), ptr(lm), len(lm), ptr(obs), len(obs), ptr(pri),
                                       len(pri), ptr(vel), len(vel), ptr(cams), len(cams)))
 

@@ -318,6 +318,8 @@ CONFIGS = {
     "cfg0_cpu_plumbing": dict(n_opt_kf=9, n_fixed=1, n_lm=2000, obs_per_lm=5, n_cam=1, gp=False, stereo_frac=0.0),
     "cfg1_local_50kf": dict(n_opt_kf=50, n_fixed=1, n_lm=20000, obs_per_lm=6, n_cam=4, gp=True),
     "cfg2_global_500kf": dict(n_opt_kf=499, n_fixed=1, n_lm=200000, obs_per_lm=6, n_cam=4, gp=True, global_ba=True),
+    # config 4: AMV-Bench-shaped full-trajectory global BA, partitioned over the GPUs (amc_lba/gba.py)
+    "cfg4_global_5k": dict(n_opt_kf=4999, n_fixed=1, n_lm=1000000, obs_per_lm=6, n_cam=4, gp=True, global_ba=True),
 }
 
 

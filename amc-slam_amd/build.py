@@ -42,7 +42,7 @@ def map_needs_build():
 def build(force=False, verbose=True):
     if force or needs_build():
         os.makedirs(os.path.dirname(LIB), exist_ok=True)
-        cmd = [HIPCC] + FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", LIB]
+        cmd = [HIPCC] + FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", LIB, "-lrccl"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)

@@ -216,6 +216,12 @@ struct DevProblem {
     double* hfin;           // host-mapped coherent [4] copy of fin + [4] sequence number (as bits)
     double* ob_chi2;        // [n_obs]
     double* ob_res;         // [n_obs][3]
+    // partitioned global BA (lba_set_partition): this rank holds a subset of the landmarks; the
+    // reduced system, b_p and the trial sums are summed over the ranks by the caller's all-reduce
+    int part_rank, part_n;  // rank / ranks (part_n 0: not partitioned)
+    double* red4;           // [4] trial sums of this rank, all-reduced before k_finalize reads them
+    double* env_buf;        // [n_env] envelope tiles of S, then bS [npad], then b_p [np] (all-reduce buffer)
+    long long n_env;
     // diagnostics (LBA_PHASE_TIMING=<file>): per-workgroup clock64() stamps at phase boundaries
     unsigned long long* tdbg_lin;     // [n_tiles][16] k_linearize
     unsigned long long* tdbg_schur;   // [n_tiles][16] k_schur
@@ -238,6 +244,9 @@ void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hi
 void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s);
 // the step + trial state + the trial state's pose samples (jac: with their Jacobian factors)
 void launch_update(const DevProblem& P, double lambda, int sel, int gate, int jac, hipStream_t s);
+// partitioned mode: this rank's trial sums into red4; envelope of S + bS + b_p into / out of env_buf
+void launch_partials(const DevProblem& P, hipStream_t s);
+void launch_env_pack(const DevProblem& P, int unpack, int gate, hipStream_t s);
 enum { FIN_NONE = -1, FIN_HOST = 0, FIN_QUEUED = 1, FIN_QUEUED_PUBLISH = 2, FIN_INITIAL = 3 };
 void launch_finalize(const DevProblem& P, unsigned long long seq, int mode, hipStream_t s);
 // residual evaluation of a state, then (mode != FIN_NONE) the trial summary (k_finalize)

@@ -6,9 +6,13 @@
 // State stays resident on the device between LM trials: the current and trial estimates are two
 // buffers, so g2o's push/pop/discardTop (sparse_optimizer.cpp:589-613) become a buffer swap.
 // The host reads back four doubles per trial (chi2 before, chi2 after, computeScale, factor status).
+#include <rccl/rccl.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <climits>
 #include <cmath>
 #include <cstdio>
@@ -58,6 +62,12 @@ struct lba_problem {
     bool gps_fresh[2] = {false, false};   // state buffer s has its pose samples with Jacobian factors
     double lambda = -1.0, ni = 2.0;
     int nBad = 0;
+    // partitioned global BA (lba_set_partition): the caller's sum all-reduce across ranks
+    int part_rank = 0, part_n = 0;
+    lba_allreduce_fn red_fn = nullptr;
+    void* red_user = nullptr;
+    ncclComm_t comm = nullptr;        // owned when set by lba_set_partition_rccl
+    void* group_slot = nullptr;       // owned (rank, group) record of lba_set_partition_group
 };
 
 namespace {
@@ -79,6 +89,12 @@ struct ApiError {
     int code;
     std::string msg;
 };
+
+// the caller's all-reduce (sum, in place, enqueued on the problem's stream)
+void preduce(lba_problem* p, double* buf, int64_t n) {
+    if (p->red_fn(buf, n, (void*)p->stream, p->red_user) != 0)
+        throw ApiError{LBA_E_HIP, "partition all-reduce failed"};
+}
 
 // LBA_PHASE_TIMING=<file>: dump the per-workgroup phase stamps of the last k_linearize / k_schur
 // launch and the tile shapes (diagnostics; scripts/phase_times.py reads it)
@@ -232,6 +248,11 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             vel.push_back(vel_kfs[i]);
             kf_act[vel_kfs[i]] = 1;
         }
+    // partitioned: every rank carries every non-fixed keyframe (activity is the union over the ranks'
+    // edges; the caller's global graph connects them all through the motion priors on rank 0)
+    if (p->part_n > 0)
+        for (int k = 0; k < n_kf; ++k)
+            if (!kfs[k].fixed) kf_act[k] = 1;
     p->kf_hidx.assign(n_kf, -1);
     int n_pb = 0;
     for (int k = 0; k < n_kf; ++k)
@@ -652,6 +673,21 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             for (int r = P * CHOL_NB; r < (P + 1) * CHOL_NB && r < p->np; ++r) f = std::min(f, 12 * fk[r / 12] / CHOL_NB);
             pfirst[P] = f;
         }
+        if (p->part_n > 0) {   // the union envelope of the ranks' systems (one all-reduce, at set-up)
+            std::vector<double> occ((size_t)NP * NP, 0.0);
+            for (int P = 0; P < NP; ++P) occ[(size_t)P * NP + pfirst[P]] = 1.0;
+            double* d = dalloc<double>(p, occ.size());
+            HIPCHK(hipMemcpy(d, occ.data(), occ.size() * sizeof(double), hipMemcpyHostToDevice));
+            preduce(p, d, (int64_t)occ.size());
+            HIPCHK(hipStreamSynchronize(p->stream));
+            HIPCHK(hipMemcpy(occ.data(), d, occ.size() * sizeof(double), hipMemcpyDeviceToHost));
+            for (int P = 0; P < NP; ++P) {
+                int f = P;
+                for (int Q = 0; Q < P; ++Q)
+                    if (occ[(size_t)P * NP + Q] != 0.0) { f = Q; break; }
+                pfirst[P] = f;
+            }
+        }
         int sa = NP, sb = NP, best = NP;
         for (int a = 1; a < NP; ++a) {
             int b = NP;
@@ -840,6 +876,13 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             if (hcnt[u] > 0 || scnt[u] > 0 || ub_i[u] == ub_j[u]) asm_list.push_back(u);
         D.ztiles = dupload(p, ztiles);
         D.n_ztiles = (int)ztiles.size();
+        D.part_rank = p->part_rank;
+        D.part_n = p->part_n;
+        if (p->part_n > 0) {
+            D.n_env = (long long)ztiles.size() * CHOL_NB * CHOL_NB + npad + p->np;
+            D.env_buf = dalloc<double>(p, (size_t)D.n_env);
+            D.red4 = dalloc<double>(p, 4);
+        }
         D.asm_list = dupload(p, asm_list);
         D.n_asm = (int)asm_list.size();
     }
@@ -922,10 +965,12 @@ void wait_seq(lba_problem* p, unsigned long long seq) {
 // instead of spinning forever.  sync: also synchronise the stream (callers that copy device
 // buffers afterwards, or read timing events).
 // eval_sel >= 0: evaluate that state buffer first (k_eval).
+void launch_fin(lba_problem* p, unsigned long long seq, int mode);
+
 void finalize_and_wait(lba_problem* p, bool sync, int eval_sel = -1) {
     const unsigned long long seq = ++p->fin_seq;
-    if (eval_sel >= 0) launch_eval(p->D, eval_sel, GATE_NONE, seq, FIN_HOST, p->stream);
-    else launch_finalize(p->D, seq, FIN_HOST, p->stream);
+    if (eval_sel >= 0) launch_eval(p->D, eval_sel, GATE_NONE, seq, FIN_NONE, p->stream);
+    launch_fin(p, seq, FIN_HOST);
     HIPCHK(hipGetLastError());
     wait_seq(p, seq);
     if (sync) HIPCHK(hipStreamSynchronize(p->stream));
@@ -941,6 +986,20 @@ void assemble_layout(lba_problem* p, double lambda, int flags, int gate = GATE_N
         HIPCHK(hipMemsetAsync(p->D.S, 0, sizeof(double) * ((size_t)p->D.npad * p->D.npad), p->stream));
     p->s_layout = want;
     launch_assemble(p->D, lambda, flags, gate, p->stream);
+    if ((flags & ASM_SCHUR) && p->part_n > 0) {   // sum the ranks' reduced systems
+        launch_env_pack(p->D, 0, gate, p->stream);
+        preduce(p, p->D.env_buf, p->D.n_env);
+        launch_env_pack(p->D, 1, gate, p->stream);
+    }
+}
+
+// k_finalize, after summing the ranks' trial sums when partitioned
+void launch_fin(lba_problem* p, unsigned long long seq, int mode) {
+    if (p->part_n > 0) {
+        launch_partials(p->D, p->stream);
+        preduce(p, p->D.red4, 4);
+    }
+    launch_finalize(p->D, seq, mode, p->stream);
 }
 
 // one damped solve + update into the trial buffers + evaluation of the trial state
@@ -1017,7 +1076,8 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
     launch_ctl_init(D, c, p->stream);
     // starting state: poses + GP samples (with the Jacobian factors the first linearisation uses), chi2
     launch_gp_prep(D, p->cur, 1, GATE_NONE, p->stream);
-    launch_eval(D, p->cur, GATE_NONE, 0, FIN_INITIAL, p->stream);
+    launch_eval(D, p->cur, GATE_NONE, 0, FIN_NONE, p->stream);
+    launch_fin(p, 0, FIN_INITIAL);
     int issued = 0;
     const LMCtl* hc = reinterpret_cast<const LMCtl*>(p->h_fin + 8);
     while (true) {
@@ -1046,8 +1106,8 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
             // the step, the trial state and its pose samples with their Jacobian factors: an
             // accepted trial's relinearisation reads them (no preparation launch)
             launch_update(D, LAMBDA_CTL, SEL_CUR, GATE_TRIAL, 1, p->stream);
-            launch_eval(D, SEL_NEXT, GATE_NONE, ++p->fin_seq, k == n - 1 ? FIN_QUEUED_PUBLISH : FIN_QUEUED,
-                        p->stream);
+            launch_eval(D, SEL_NEXT, GATE_NONE, 0, FIN_NONE, p->stream);
+            launch_fin(p, ++p->fin_seq, k == n - 1 ? FIN_QUEUED_PUBLISH : FIN_QUEUED);
             HIPCHK(hipGetLastError());
         }
         if (std::getenv("LBA_ENQ_TIMING"))
@@ -1087,6 +1147,8 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
 
 int optimize(lba_problem* p, int iters, volatile const int32_t* stop, lba_stats* st) {
     if (!p->has_problem) throw ApiError{LBA_E_ARG, "no problem set"};
+    if (p->part_n > 0 && p->cfg.lambda_init <= 0)
+        throw ApiError{LBA_E_ARG, "partitioned problems need lambda_init > 0 (computeLambdaInit is a max over ranks)"};
     lba_stats s{};
     if (p->np + 3 * p->n_lm_dev == 0) throw ApiError{LBA_E_EMPTY, "0 vertices to optimize"};
     if (!stop && iters > 0 && !(p->cfg.flags & (LBA_FLAG_TIME_PHASES | LBA_FLAG_HOST_LOOP)))
@@ -1178,6 +1240,11 @@ int map_error(lba_problem* p, const HipError& e) {
 
 // ==================================================================================================
 // C ABI
+struct GroupSlot {   // lba_set_partition_group: the user pointer of the in-process all-reduce
+    lba_group* g;
+    int rank;
+};
+
 extern "C" {
 
 int lba_abi_version(void) { return LBA_ABI_VERSION; }
@@ -1227,6 +1294,8 @@ void lba_destroy(lba_problem* p) {
         if (e) (void)hipEventDestroy(e);
     if (p->h_fin) (void)hipHostFree(p->h_fin);
     if (p->h_log) (void)hipHostFree(p->h_log);
+    if (p->comm) (void)ncclCommDestroy(p->comm);
+    delete static_cast<GroupSlot*>(p->group_slot);
     if (p->stream) (void)hipStreamDestroy(p->stream);
     delete p;
 }
@@ -1246,6 +1315,155 @@ int lba_set_config(lba_problem* p, const lba_config* cfg) {
 const char* lba_last_error(const lba_problem* p) { return p ? p->err.c_str() : "null problem"; }
 
 int lba_pose_dim(const lba_problem* p) { return p && p->has_problem ? p->np : 0; }
+
+int lba_set_partition(lba_problem* p, int32_t rank, int32_t nranks, lba_allreduce_fn fn, void* user) {
+    if (!p || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !fn)) return LBA_E_ARG;
+    if (p->has_problem) {
+        p->err = "lba_set_partition must precede lba_set_problem";
+        return LBA_E_ARG;
+    }
+    p->part_rank = rank;
+    p->part_n = nranks > 1 ? nranks : 0;
+    p->red_fn = fn;
+    p->red_user = user;
+    return LBA_OK;
+}
+
+static int rccl_allreduce(double* buf, int64_t n, void* stream, void* user) {
+    return ncclAllReduce(buf, buf, (size_t)n, ncclDouble, ncclSum, static_cast<ncclComm_t>(user),
+                         static_cast<hipStream_t>(stream)) == ncclSuccess ? 0 : -1;
+}
+
+int lba_rccl_unique_id(void* id_out) {
+    if (!id_out) return LBA_E_ARG;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return LBA_E_HIP;
+    std::memcpy(id_out, &id, sizeof(id));
+    return LBA_OK;
+}
+
+int lba_set_partition_rccl(lba_problem* p, const void* id, int32_t rank, int32_t nranks) {
+    if (!p || !id) return LBA_E_ARG;
+    if (nranks <= 1) return lba_set_partition(p, 0, 1, nullptr, nullptr);
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    if (hipSetDevice(p->cfg.device) != hipSuccess) return LBA_E_HIP;
+    ncclComm_t comm = nullptr;
+    if (ncclCommInitRank(&comm, nranks, uid, rank) != ncclSuccess) {
+        p->err = "ncclCommInitRank failed";
+        return LBA_E_HIP;
+    }
+    const int rc = lba_set_partition(p, rank, nranks, rccl_allreduce, comm);
+    if (rc != LBA_OK) {
+        ncclCommDestroy(comm);
+        return rc;
+    }
+    if (p->comm) ncclCommDestroy(p->comm);
+    p->comm = comm;
+    return LBA_OK;
+}
+
+// ---- in-process all-reduce across problems on one device (tests; lba_group)
+constexpr int GROUP_MAX = 16;
+struct GroupBufs {
+    double* b[GROUP_MAX];
+    int n;
+};
+__global__ void k_group_sum(GroupBufs g, long long count) {
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < count; e += (long long)gridDim.x * blockDim.x) {
+        double s = 0.0;
+        for (int r = 0; r < g.n; ++r) s += g.b[r][e];   // rank order: the same bits everywhere
+        for (int r = 0; r < g.n; ++r) g.b[r][e] = s;
+    }
+}
+
+}  // extern "C"
+
+struct lba_group {
+    int n = 0;
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived = 0;
+    unsigned long long gen = 0;
+    GroupBufs bufs{};
+    long long count = -1;
+    bool bad = false;
+    hipStream_t rs = nullptr;
+    hipEvent_t ev_in[GROUP_MAX] = {};
+    hipEvent_t ev_done = nullptr;
+};
+static int group_allreduce(double* buf, int64_t n, void* stream, void* user) {
+    GroupSlot* sl = static_cast<GroupSlot*>(user);
+    lba_group* g = sl->g;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    std::unique_lock<std::mutex> lk(g->m);
+    if (hipEventRecord(g->ev_in[sl->rank], st) != hipSuccess) g->bad = true;
+    g->bufs.b[sl->rank] = buf;
+    if (g->arrived == 0) g->count = n;
+    else if (g->count != n) g->bad = true;
+    const unsigned long long my = g->gen;
+    if (++g->arrived == g->n) {   // last arrival: one sum kernel after every rank's stream point
+        bool ok = !g->bad;
+        for (int r = 0; r < g->n && ok; ++r) ok = hipStreamWaitEvent(g->rs, g->ev_in[r], 0) == hipSuccess;
+        g->bufs.n = g->n;
+        if (ok && n > 0) {
+            const int blocks = (int)std::min<long long>((n + 255) / 256, 4096);
+            hipLaunchKernelGGL(k_group_sum, dim3(blocks), dim3(256), 0, g->rs, g->bufs, (long long)n);
+            ok = hipGetLastError() == hipSuccess;
+        }
+        ok = ok && hipEventRecord(g->ev_done, g->rs) == hipSuccess;
+        g->bad = !ok;
+        g->arrived = 0;
+        g->gen++;
+        g->cv.notify_all();
+    } else {
+        g->cv.wait(lk, [&] { return g->gen != my; });
+    }
+    const bool bad = g->bad;
+    // every rank's stream waits for the sum (the event is re-recorded only after all ranks arrive again)
+    if (bad || hipStreamWaitEvent(st, g->ev_done, 0) != hipSuccess) return -1;
+    return 0;
+}
+
+extern "C" {
+
+int lba_group_create(lba_group** out, int32_t nranks) {
+    if (!out || nranks < 1 || nranks > GROUP_MAX) return LBA_E_ARG;
+    lba_group* g = new lba_group();
+    g->n = nranks;
+    if (hipStreamCreateWithFlags(&g->rs, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&g->ev_done, hipEventDisableTiming) != hipSuccess) {
+        delete g;
+        return LBA_E_HIP;
+    }
+    for (int r = 0; r < nranks; ++r)
+        if (hipEventCreateWithFlags(&g->ev_in[r], hipEventDisableTiming) != hipSuccess) return LBA_E_HIP;
+    *out = g;
+    return LBA_OK;
+}
+
+void lba_group_destroy(lba_group* g) {
+    if (!g) return;
+    (void)hipStreamSynchronize(g->rs);
+    for (int r = 0; r < g->n; ++r)
+        if (g->ev_in[r]) (void)hipEventDestroy(g->ev_in[r]);
+    if (g->ev_done) (void)hipEventDestroy(g->ev_done);
+    if (g->rs) (void)hipStreamDestroy(g->rs);
+    delete g;
+}
+
+int lba_set_partition_group(lba_problem* p, lba_group* g, int32_t rank) {
+    if (!p || !g || rank < 0 || rank >= g->n) return LBA_E_ARG;
+    GroupSlot* sl = new GroupSlot{g, rank};
+    const int rc = lba_set_partition(p, rank, g->n, group_allreduce, sl);
+    if (rc != LBA_OK) {
+        delete sl;
+        return rc;
+    }
+    delete static_cast<GroupSlot*>(p->group_slot);
+    p->group_slot = sl;
+    return LBA_OK;
+}
 
 int lba_set_problem(lba_problem* p, const lba_kf* kfs, int32_t n_kf, const double* lm_xyz, int32_t n_lm,
                     const lba_obs* obs, int32_t n_obs, const lba_prior* priors, int32_t n_priors,

@@ -843,7 +843,7 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
         __syncthreads();
         if (g == 0) {
             double t = red[e] + red[144 + e] + red[288 + e] + red[432 + e];
-            if (bi == bj && e % 13 == 0) t += lambda;
+            if (bi == bj && e % 13 == 0 && P.part_rank == 0) t += lambda;   // damping: added once over the ranks
             const int i = e / 12, j = e % 12;
             const int r = 12 * bj + j, c = 12 * bi + i;   // element (row r, col c) of S, r >= c in blocks
             if (flags & ASM_FULL) {                       // natural order, both triangles
@@ -857,7 +857,7 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
                 P.S[(size_t)max(rh, ch) * n + min(rh, ch)] = t;
             }
         }
-        if (blockIdx.x == 0)   // padding rows: identity
+        if (blockIdx.x == 0 && P.part_rank == 0)   // padding rows: identity (rank 0 of a partition)
             for (int r = P.np + tid; r < n; r += 144 * RED_GROUPS) {
                 const int rh = (flags & ASM_FULL) ? r : P.ppos[r / CHOL_NB] * CHOL_NB + r % CHOL_NB;
                 P.S[(size_t)rh * n + rh] = 1.0;
@@ -1959,7 +1959,8 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
             if (h >= 0)
                 for (int j = 0; j < 12; ++j) {
                     if (ok) P.x[12 * h + j] = d[j];
-                    sc += d[j] * (lambda * d[j] + P.bp[12 * h + j]);
+                    // (partitioned: b_p is the all-reduced one, the pose part is counted by rank 0)
+                    if (P.part_rank == 0) sc += d[j] * (lambda * d[j] + P.bp[12 * h + j]);
                 }
         }
     } else {
@@ -2103,23 +2104,69 @@ __device__ void lm_decide(LMCtl& c, double chi_lin, double chi_trial, double sca
     if ((result != LBA_RESULT_OK && c.early_stop) || c.it >= c.iters) c.done = 1;
 }
 
+// chi2 of the linearisation point, chi2 of the trial state, computeScale: sums in a fixed order
+template <int NT>
+__device__ void trial_sums(const DevProblem& P, double* red, double& sa, double& sb, double& sc) {
+    const int tid = threadIdx.x;
+    const int nc = P.n_tiles + P.n_prior + P.n_vel;
+    double a = 0.0, b = 0.0, c = 0.0;
+    for (int i = tid; i < nc; i += NT) { a += P.chi_lin[i]; b += P.chi_eval[i]; }
+    for (int i = tid; i < P.n_upd_blocks; i += NT) c += P.scale_part[i];
+    sa = block_sum<NT>(a, red);
+    __syncthreads();
+    sb = block_sum<NT>(b, red);
+    __syncthreads();
+    sc = block_sum<NT>(c, red);
+}
+
+// partitioned mode: this rank's sums (and factorisation status) for the all-reduce ahead of k_finalize
+__global__ __launch_bounds__(256) void k_partials(DevProblem P) {
+    __shared__ double red[256 / 64];
+    double sa, sb, sc;
+    trial_sums<256>(P, red, sa, sb, sc);
+    if (threadIdx.x == 0) {
+        P.red4[0] = sa; P.red4[1] = sb; P.red4[2] = sc; P.red4[3] = (double)(*P.info);
+    }
+}
+
+// partitioned mode: the envelope tiles of S (k_schur zeroes exactly these, so every rank's tiles line
+// up), bS and b_p, into (unpack = 0) or back out of (unpack = 1) the all-reduce buffer
+__global__ __launch_bounds__(256) void k_env_pack(DevProblem P, int unpack, int gate) {
+    if (gated_off(P.ctl, gate)) return;
+    const int n = P.npad;
+    if ((int)blockIdx.x < P.n_ztiles) {
+        const int code = P.ztiles[blockIdx.x], i = code & 0xffff, j = code >> 16;
+        double* buf = P.env_buf + (size_t)blockIdx.x * CHOL_NB * CHOL_NB;
+        for (int e = threadIdx.x; e < CHOL_NB * CHOL_NB; e += 256) {
+            double* sp = P.S + (size_t)(i * CHOL_NB + (e >> 5)) * n + j * CHOL_NB + (e & 31);
+            if (unpack) *sp = buf[e];
+            else buf[e] = *sp;
+        }
+    } else {
+        double* buf = P.env_buf + (size_t)P.n_ztiles * CHOL_NB * CHOL_NB;
+        for (int e = (blockIdx.x - P.n_ztiles) * 256 + threadIdx.x; e < n + P.np; e += 256 * 8) {
+            double* sp = e < n ? P.bS + e : P.bp + (e - n);
+            if (unpack) *sp = buf[e];
+            else buf[e] = *sp;
+        }
+    }
+}
+
 // mode (FIN_*): host-driven trial (publish the summary); queued trial (decide, and publish the
 // controller mirror when it is the last trial of a batch); starting-state evaluation of a queue
 // (chi2 only, into the controller)
 template <int NT>
 __device__ void finalize_body(const DevProblem& P, unsigned long long seq, int mode, double* red) {
     const int tid = threadIdx.x;
-    const int nc = P.n_tiles + P.n_prior + P.n_vel;
-    double a = 0.0, b = 0.0, c = 0.0;
-    for (int i = tid; i < nc; i += NT) { a += P.chi_lin[i]; b += P.chi_eval[i]; }
-    for (int i = tid; i < P.n_upd_blocks; i += NT) c += P.scale_part[i];
-    const double sa = block_sum<NT>(a, red);
-    __syncthreads();
-    const double sb = block_sum<NT>(b, red);
-    __syncthreads();
-    const double sc = block_sum<NT>(c, red);
+    double sa, sb, sc, sinfo;
+    if (P.part_n > 0) {   // partitioned: the all-reduced sums of every rank's k_partials
+        sa = P.red4[0]; sb = P.red4[1]; sc = P.red4[2]; sinfo = P.red4[3];
+    } else {
+        trial_sums<NT>(P, red, sa, sb, sc);
+        sinfo = (double)(*P.info);
+    }
     if (tid != 0) return;
-    const double v[4] = {sa, sb, sc, (double)(*P.info)};
+    const double v[4] = {sa, sb, sc, sinfo};
     if (mode == FIN_INITIAL) {
         P.ctl->chi0 = sb;
         return;
@@ -2130,7 +2177,7 @@ __device__ void finalize_body(const DevProblem& P, unsigned long long seq, int m
         LMCtl ctl = *P.ctl;
         if (!ctl.done)
             for (int i = 0; i < 4; ++i) P.fin[i] = v[i];
-        lm_decide(ctl, sa, sb, sc, *P.info == 0, P.hlog);
+        lm_decide(ctl, sa, sb, sc, sinfo == 0.0, P.hlog);
         *P.ctl = ctl;
         if (mode != FIN_QUEUED_PUBLISH) return;
         volatile double* h = P.hfin + 8;
@@ -2265,6 +2312,12 @@ void launch_eval(const DevProblem& P, int sel, int gate, unsigned long long seq,
     const int nb = P.n_tiles + cdiv(P.n_prior + P.n_vel, TILE_OBS);
     if (nb) hipLaunchKernelGGL(k_eval, dim3(nb), dim3(TILE_OBS), 0, s, P, sel, gate);
     if (mode != FIN_NONE) launch_finalize(P, seq, mode, s);
+}
+void launch_partials(const DevProblem& P, hipStream_t s) {
+    hipLaunchKernelGGL(k_partials, dim3(1), dim3(256), 0, s, P);
+}
+void launch_env_pack(const DevProblem& P, int unpack, int gate, hipStream_t s) {
+    hipLaunchKernelGGL(k_env_pack, dim3(P.n_ztiles + 8), dim3(256), 0, s, P, unpack, gate);
 }
 void launch_finalize(const DevProblem& P, unsigned long long seq, int mode, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, P, seq, mode);

@@ -153,6 +153,27 @@ int lba_set_problem(lba_problem* p,
                     const int32_t* vel_kfs, int32_t n_vel,
                     const lba_cam* cams, int32_t n_cam);
 
+/* ---- partitioned global BA (BASELINE config 4): one problem per GPU (rank), every
+ * rank holding ALL keyframes (same array, same fixed flags), a disjoint subset of the landmarks with
+ * all of their observations, and rank 0 alone the motion-prior / velocity edges.  Per LM trial the
+ * ranks sum their reduced camera systems (the envelope of S, the reduced rhs and b_p: one
+ * all-reduce) and their trial sums (chi2 before / after, computeScale: a 4-double all-reduce); every
+ * rank then solves the same system, so the keyframe states and the LM decisions stay identical and
+ * each rank back-substitutes its own landmarks.  The all-reduce is the caller's (sum, in place, on
+ * device memory, enqueued on the given HIP stream, bitwise identical on every rank): RCCL over
+ * xGMI (lba_set_partition_rccl), an in-process group of problems on one device (lba_group, for
+ * tests), or any function.  Call before lba_set_problem; set_problem is then collective (the ranks
+ * agree on the union envelope of S), as are lba_optimize calls, which need lambda_init > 0 and the
+ * same iteration count and stop flag on every rank. */
+typedef int (*lba_allreduce_fn)(double* dev_buf, int64_t count, void* hip_stream, void* user);
+int lba_set_partition(lba_problem* p, int32_t rank, int32_t nranks, lba_allreduce_fn fn, void* user);
+int lba_rccl_unique_id(void* id_out);   /* NCCL_UNIQUE_ID_BYTES (128) bytes, on one rank, shared by the caller */
+int lba_set_partition_rccl(lba_problem* p, const void* id, int32_t rank, int32_t nranks);
+typedef struct lba_group lba_group;     /* in-process all-reduce across problems on one device */
+int  lba_group_create(lba_group** out, int32_t nranks);
+void lba_group_destroy(lba_group* g);
+int  lba_set_partition_group(lba_problem* p, lba_group* g, int32_t rank);
+
 /* Levenberg-Marquardt (OptimizationAlgorithmLevenberg::solve x iters).  stop_flag is polled
  * between iterations and trials like SparseOptimizer::terminate().  Returns iterations run
  * (>= 0) or an LBA_E_* code. */
