@@ -117,16 +117,45 @@ def main():
     from amc_lba import farm
     from amc_lba.synth import make_config_window
 
-    if world > 1:
-        win, shared = farm.make_rank_window(args.config, rank, world, seed=args.seed)
-        ex = farm.SharedExchange(win, shared, rank, world, device=torch.device("cuda", local))
-    else:
-        win = make_config_window(args.config, seed=args.seed)
-        ex = None
+    # global BA (config 4): one problem partitioned over the ranks (landmarks split, reduced system
+    # all-reduced over RCCL every LM trial); otherwise window farming (config 3) or a single window
+    gba = args.config.startswith("cfg4")
+    solve_flag = {"auto": 0, "band": amc_lba.abi.FLAG_BAND_SOLVE, "dense": amc_lba.abi.FLAG_DENSE_SOLVE}[args.solve]
     # the timed run records HIP events around every k_linearize launch (LBA_FLAG_TIME_SWEEP): the
     # roofline below is measured live, per launch, over the timed region
-    solve_flag = {"auto": 0, "band": amc_lba.abi.FLAG_BAND_SOLVE, "dense": amc_lba.abi.FLAG_DENSE_SOLVE}[args.solve]
-    prob = amc_lba.Problem(win, device=local, early_stop=0, flags=amc_lba.abi.FLAG_TIME_SWEEP | solve_flag)
+    flags = amc_lba.abi.FLAG_TIME_SWEEP | solve_flag
+    ex, full = None, None
+    t_setup = time.perf_counter()
+    # large set-ups (config 4: ~35 s of window generation, then the engine's preprocessing) report
+    # progress, so a watchdog that looks for output does not take them for a hang
+    import threading
+    setup_done = threading.Event()
+
+    def _progress():
+        while not setup_done.wait(20.0):
+            print(f"[bench rank {rank}] setting up ({time.perf_counter() - t_setup:.0f} s)", file=sys.stderr, flush=True)
+    threading.Thread(target=_progress, daemon=True).start()
+    if gba:
+        from amc_lba.gba import partition_window
+        full = make_config_window(args.config, seed=args.seed)
+        win, _ = partition_window(full, rank, world)
+        rid = None
+        if world > 1:
+            idt = torch.zeros(128, dtype=torch.uint8, device=torch.device("cuda", local))
+            if rank == 0:
+                idt.copy_(torch.frombuffer(bytearray(amc_lba.rccl_unique_id()), dtype=torch.uint8))
+            dist.broadcast(idt, 0)
+            rid = bytes(idt.cpu().numpy().tobytes())
+        prob = amc_lba.Problem(win, device=local, early_stop=0, flags=flags, rccl_id=rid, rank=rank, nranks=world)
+    else:
+        if world > 1:
+            win, shared = farm.make_rank_window(args.config, rank, world, seed=args.seed)
+            ex = farm.SharedExchange(win, shared, rank, world, device=torch.device("cuda", local))
+        else:
+            win = make_config_window(args.config, seed=args.seed)
+        prob = amc_lba.Problem(win, device=local, early_stop=0, flags=flags)
+    t_setup = time.perf_counter() - t_setup
+    setup_done.set()
 
     # warmup (not timed)
     if args.warmup > 0:
@@ -156,14 +185,19 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
-    if rank == 0:
+    phase = None
+    if world == 1:
         # phase breakdown from a separate, untimed run with every phase evented
+        prob.close()
         ph = amc_lba.Problem(win, device=local, early_stop=0, flags=amc_lba.abi.FLAG_TIME_PHASES | solve_flag)
         n_ph, st_ph = ph.optimize(args.window_iters)
         phase = {k: getattr(st_ph, k) / max(n_ph, 1) for k in ("ms_linearize", "ms_schur", "ms_solve", "ms_update_eval")}
         phase["trials"] = st_ph.trials / max(n_ph, 1)
         ph.close()
-        total_iters = done * world
+    if rank == 0:
+        # window farm: every rank runs its own window (weak scaling); global BA: one problem (strong)
+        total_iters = done if gba else done * world
+        W = full if gba else win
         value = total_iters / dt
         k_ms = ms_k / max(n_k, 1)
         B = sweep_bytes(win)
@@ -180,14 +214,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": dt * 1e3 / done,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if gba else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (deterministic generator, amc_lba/synth.py, seed %d)" % args.seed,
-            "config": {"workload": workload, "n_kf": int(len(win.kfs)), "n_opt_kf": int((win.kfs["fixed"] == 0).sum()),
-                       "n_lm": int(len(win.lm)), "n_obs": int(len(win.obs)), "n_pairs": int(win.n_pairs),
-                       "n_cam": int(len(win.cams)), "window_iters": args.window_iters, "solve": args.solve,
-                       "parallelism": f"window farm x{world}" if world > 1 else "single window"},
+            "config": {"workload": workload, "n_kf": int(len(W.kfs)), "n_opt_kf": int((W.kfs["fixed"] == 0).sum()),
+                       "n_lm": int(len(W.lm)), "n_obs": int(len(W.obs)), "n_pairs": int(W.n_pairs),
+                       "n_cam": int(len(W.cams)), "window_iters": args.window_iters, "solve": args.solve,
+                       "parallelism": (f"landmark partition x{world} (RCCL all-reduce per trial)" if gba else
+                                       f"window farm x{world}") if world > 1 else "single window",
+                       "setup_s": t_setup},
             "roofline": {"bound": "hbm", "kernel": "k_linearize", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                          "traffic": traffic, "bytes_per_launch": B, "avg_launch_ms": k_ms,
@@ -199,7 +235,9 @@ def main():
             "trials_per_step": trials / max(done, 1),
             "phases_ms_per_step": phase,
         }
-        if not args.no_cpu and world == 1:
+        if gba:   # roofline: rank 0's partition of the sweep
+            line["roofline"]["note"] = "k_linearize of rank 0's landmark partition"
+        if not args.no_cpu and world == 1 and not gba:   # (the oracle's dense LDLT of S = 60000^2 is hours)
             line["cpu_baseline"] = cpu_baseline(win, args.cpu_seconds)
             line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
         print(json.dumps(line), flush=True)
