@@ -201,6 +201,39 @@ int lba_solve_step(lba_problem* p, double lambda, double* dx);
 /* Dimension of the pose system (12 * number of non-fixed KFs). */
 int lba_pose_dim(const lba_problem* p);
 
+/* ---- tracking: Optimizer::PoseGPOptimizationFromeLastFrame (src/Optimizer.cc:369-686), SURVEY.md §8(f)3.
+ * Per frame: vertices prev (pFrame->mpPrevFrame, fixed = the `fix` argument) and cur (pFrame), the map
+ * points fixed; EdgeMonoGPOnlyPose for the asynchronous cameras (LBA_MONO_GP: the GP pose between prev
+ * and cur at the camera's time stamp), EdgeMonoOnlyPose / EdgeStereoOnlyPose for the reference camera
+ * (LBA_MONO / LBA_STEREO at cur), EdgeGaussianPrior(prev, cur) and EdgeVelocity on both.  Four rounds
+ * of optimize(10) on the level-0 edges with re-classification between them (chi2 5.991 mono, 15.6 /
+ * 9.8 / 7.815 / 7.815 stereo, x1.5 for points tracked closer than 10 m, depth test), the robust kernel
+ * dropped after round 3.  A batch of frames runs as one launch, one workgroup per frame. */
+typedef struct lba_track_obs {
+    int32_t kind;           /* LBA_MONO_GP, LBA_MONO or LBA_STEREO */
+    int32_t cam;            /* mmpKeyToCam[i]; the reference camera (n_cam - 1) for LBA_MONO / LBA_STEREO */
+    int32_t outlier;        /* in: pFrame->mvbOutlier[i] (edge level 1); out: the last round's classification */
+    int32_t close;          /* mvpMapPoints[i]->mvTrackDepth[cam] < 10 */
+    double  t;              /* pFrame->mvTimeStamps[cam] (GP kinds) */
+    double  z[3];           /* u, v (, u_right) */
+    double  w;              /* invSigma2 / unc2 */
+    double  Xw[3];          /* pMP->GetWorldPos() widened to double (fixed) */
+} lba_track_obs;
+
+typedef struct lba_track_frame {
+    lba_kf  prev;           /* VertexPoseVel(pFrame->mpPrevFrame); prev.fixed = fix.  Not written back */
+    lba_kf  cur;            /* VertexPoseVel(pFrame); out: the optimised pose and velocity (SetPose / SetVelocity) */
+    int32_t obs0, n_obs;    /* the frame's observations in the batch array */
+    int32_t n_good;         /* out: nInitialCorrespondences - nBad, the reference's return value */
+    int32_t iterations;     /* out: LM iterations over the rounds */
+} lba_track_frame;
+
+typedef struct lba_tracker lba_tracker;   /* device buffers + stream, reused across calls */
+int  lba_tracker_create(lba_tracker** out, const lba_config* cfg);   /* qc, Huber deltas, tau, device */
+void lba_tracker_destroy(lba_tracker* t);
+int  lba_track(lba_tracker* t, lba_track_frame* frames, int32_t n_frames, lba_track_obs* obs, int32_t n_obs,
+               const lba_cam* cams, int32_t n_cam);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1370,3 +1370,243 @@ void orc_gp_query_pose(const double qc[36], const double q1[4], const double t1[
     dq[0] = dT.q.x; dq[1] = dT.q.y; dq[2] = dT.q.z; dq[3] = dT.q.w;
     memcpy(dt, dT.t, sizeof(double) * 3);
 }
+
+/* ------------------------------------------------------------------ tracking-side pose optimisation
+ * Optimizer::PoseGPOptimizationFromeLastFrame (src/Optimizer.cc:369-686): two frame vertices
+ * (prev: fixed = `fix`, cur), the map points constant (EdgeMonoGPOnlyPose / EdgeMonoOnlyPose /
+ * EdgeStereoOnlyPose, src/G2oTypes.cc:162-223, include/G2oTypes.h:186-270: the reprojection edges of
+ * this file with the point columns dropped), EdgeGaussianPrior(prev, cur), EdgeVelocity on both;
+ * BlockSolverX + LinearSolverDense + Levenberg without a user lambda (:373-381).  Four rounds of
+ * initializeOptimization(0) + optimize(10) with the re-classification of :575-672 in between.
+ * Per-edge chi2 follows g2o: e->chi2() of an active edge is the error of the last computeActiveErrors
+ * (the last trial state, even a rejected one); outliers get computeError() at the current state. */
+typedef struct {
+    orc_problem* p;
+    const int* level;
+    int robust;
+    int fixprev;
+    double* ob_chi2;
+} trk_t;
+
+static int trk_dof0(const trk_t* T) { return T->fixprev ? 12 : 0; }
+
+static double trk_errors(trk_t* T) {   /* computeActiveErrors + activeRobustChi2 over level 0 */
+    orc_problem* p = T->p;
+    double chi = 0.0, rho[3];
+    for (int k = 0; k < 2; ++k) {   /* EdgeVelocity (inactive on a fixed vertex) */
+        if (p->kf[k].fixed) continue;
+        double e = p->kf[k].vel[2];
+        chi += e * (p->gp.QcInv[2 * 6 + 2] * e);
+    }
+    {
+        double err[12];
+        prior_error(p, &p->pri[0], err);
+        chi += prior_chi2(p, &p->pri[0], err);
+    }
+    for (int i = 0; i < p->n_obs; ++i) {
+        if (T->level[i]) continue;
+        const lba_obs* o = &p->obs[i];
+        double e[3];
+        obs_error(p, o, e);
+        double c = chi2_of(e, obs_dim(o->kind), o->w);
+        T->ob_chi2[i] = c;
+        if (T->robust) { huber(c, obs_delta(p, o->kind), rho); chi += rho[0]; }
+        else chi += c;
+    }
+    return chi;
+}
+
+/* buildSystem over the level-0 edges: H [24 x 24], b [24] = -J^T rho' Omega e */
+static void trk_build(trk_t* T, double* H, double* b) {
+    orc_problem* p = T->p;
+    memset(H, 0, sizeof(double) * 576);
+    memset(b, 0, sizeof(double) * 24);
+    double rho[3];
+    for (int i = 0; i < p->n_obs; ++i) {
+        if (T->level[i]) continue;
+        const lba_obs* o = &p->obs[i];
+        int dim = obs_dim(o->kind);
+        double e[3], J[81];
+        obs_error(p, o, e);
+        obs_jacobian(p, o, J);
+        double c = chi2_of(e, dim, o->w), s = o->w;
+        if (T->robust) { huber(c, obs_delta(p, o->kind), rho); s *= rho[1]; }
+        for (int r = 0; r < dim; ++r)
+            for (int a = 0; a < 24; ++a) {
+                double ja = J[r * 27 + a];
+                if (ja == 0.0) continue;
+                b[a] -= ja * s * e[r];
+                for (int c2 = 0; c2 < 24; ++c2) H[a * 24 + c2] += ja * s * J[r * 27 + c2];
+            }
+    }
+    {   /* EdgeGaussianPrior(prev, cur), info QiInv(dt) */
+        double e[12], Ji[144], Jj[144], Jf[288], Om[144], OJ[288];
+        prior_error(p, &p->pri[0], e);
+        prior_jacobian(p, &p->pri[0], Ji, Jj);
+        for (int r = 0; r < 12; ++r)
+            for (int c = 0; c < 12; ++c) { Jf[r * 24 + c] = Ji[r * 12 + c]; Jf[r * 24 + 12 + c] = Jj[r * 12 + c]; }
+        gp_qi_inv(&p->gp, p->kf[1].time - p->kf[0].time, Om);
+        mat_mul(OJ, Om, Jf, 12, 12, 24);
+        for (int a = 0; a < 24; ++a) {
+            double s = 0.0;
+            for (int r = 0; r < 12; ++r) {
+                double oe = 0.0;
+                for (int q = 0; q < 12; ++q) oe += Om[r * 12 + q] * e[q];
+                s += Jf[r * 24 + a] * oe;
+            }
+            b[a] -= s;
+            for (int c = 0; c < 24; ++c) {
+                double h = 0.0;
+                for (int r = 0; r < 12; ++r) h += Jf[r * 24 + a] * OJ[r * 24 + c];
+                H[a * 24 + c] += h;
+            }
+        }
+    }
+    for (int k = 0; k < 2; ++k) {   /* EdgeVelocity: d e / d vel_z = 1 */
+        if (p->kf[k].fixed) continue;
+        double om = p->gp.QcInv[2 * 6 + 2];
+        H[(12 * k + 8) * 24 + 12 * k + 8] += om;
+        b[12 * k + 8] -= om * p->kf[k].vel[2];
+    }
+}
+
+static int trk_lm_iteration(trk_t* T, int iteration, double* lambda, double* ni, int* nbad, int* trials) {
+    orc_problem* p = T->p;
+    const int d0 = trk_dof0(T), n = 24 - d0;
+    double H[576], b[24], A[576], x[24];
+    double currentChi = trk_errors(T), tempChi = currentChi, iniChi = currentChi;
+    trk_build(T, H, b);
+    if (iteration == 0) {   /* computeLambdaInit over the active vertices */
+        double m = 0.0;
+        for (int i = d0; i < 24; ++i) m = fmax(m, fabs(H[i * 24 + i]));
+        *lambda = p->cfg.lambda_init > 0 ? p->cfg.lambda_init : p->cfg.tau * m;
+        *ni = 2.0;
+        *nbad = 0;
+    }
+    double rho = 0.0;
+    int qmax = 0;
+    kf_t bak[2];
+    do {
+        memcpy(bak, p->kf, sizeof(bak));
+        for (int i = 0; i < n; ++i) {
+            for (int j = 0; j < n; ++j) A[i * n + j] = H[(d0 + i) * 24 + d0 + j];
+            A[i * n + i] += *lambda;
+        }
+        int ok2 = ldlt_solve_inplace(n, A, b + d0, x);
+        if (ok2) {
+            for (int k = T->fixprev ? 1 : 0; k < 2; ++k) {
+                const double* dx = x + 12 * k - d0;
+                se3 d = se3_exp(dx);
+                p->kf[k].Twb = se3_mul(&p->kf[k].Twb, &d);
+                for (int i = 0; i < 6; ++i) p->kf[k].vel[i] += dx[6 + i];
+            }
+        }
+        tempChi = trk_errors(T);
+        if (!ok2) tempChi = DBL_MAX;
+        rho = currentChi - tempChi;
+        double scale = 1e-3;
+        if (ok2)
+            for (int i = 0; i < n; ++i) scale += x[i] * (*lambda * x[i] + b[d0 + i]);
+        rho /= scale;
+        if (rho > 0 && isfinite(tempChi)) {
+            double alpha = 1. - pow((2 * rho - 1), 3);
+            alpha = fmin(alpha, 2. / 3.);
+            *lambda *= fmax(1. / 3., alpha);
+            *ni = 2;
+            currentChi = tempChi;
+        } else {
+            *lambda *= *ni;
+            *ni *= 2;
+            memcpy(p->kf, bak, sizeof(bak));
+        }
+        qmax++;
+    } while (rho < 0 && qmax < p->cfg.max_trials);
+    *trials += qmax;
+    if (qmax == p->cfg.max_trials || rho == 0) return LBA_RESULT_TERMINATE;
+    if ((iniChi - currentChi) * 1e3 < iniChi) (*nbad)++;
+    else *nbad = 0;
+    if (*nbad >= 3) return LBA_RESULT_TERMINATE;
+    return LBA_RESULT_OK;
+}
+
+static int trk_depth_ok(const orc_problem* p, int i) {   /* isDepthPositive (include/G2oTypes.h:203-206, 260-266) */
+    const lba_obs* o = &p->obs[i];
+    const cam_t* c = &p->cam[o->cam];
+    int ks[2] = {o->kf_b, is_gp(o->kind) ? o->kf_a : -1};
+    for (int s = 0; s < 2; ++s) {
+        if (ks[s] < 0) continue;
+        se3 Twc = se3_mul(&p->kf[ks[s]].Twb, &c->Tbc);
+        se3 Tcw = se3_inv(&Twc);
+        double Xc[3];
+        se3_act(&Tcw, p->lm + 3 * o->lm, Xc);
+        if (!(Xc[2] > 0)) return 0;
+    }
+    return 1;
+}
+
+int orc_track_pose(const lba_config* cfg, lba_track_frame* fr, lba_track_obs* tob, int n, const lba_cam* cams, int n_cam) {
+    lba_kf kfs[2] = {fr->prev, fr->cur};
+    kfs[1].fixed = 0;
+    double* lm = (double*)malloc(sizeof(double) * 3 * (n > 0 ? n : 1));
+    lba_obs* ob = (lba_obs*)calloc(n > 0 ? n : 1, sizeof(lba_obs));
+    int* level = (int*)malloc(sizeof(int) * (n > 0 ? n : 1));
+    double* chi2 = (double*)calloc(n > 0 ? n : 1, sizeof(double));
+    for (int i = 0; i < n; ++i) {
+        memcpy(lm + 3 * i, tob[i].Xw, sizeof(double) * 3);
+        ob[i].kind = tob[i].kind;
+        ob[i].kf_a = tob[i].kind == LBA_MONO_GP ? 0 : -1;
+        ob[i].kf_b = 1;
+        ob[i].lm = i;
+        ob[i].cam = tob[i].cam;
+        ob[i].t = tob[i].t;
+        memcpy(ob[i].z, tob[i].z, sizeof(double) * 3);
+        ob[i].w = tob[i].w;
+        level[i] = tob[i].outlier ? 1 : 0;
+    }
+    lba_prior pri = {0, 1};
+    int vel[2] = {0, 1};
+    orc_problem* p = orc_create(cfg, kfs, 2, lm, n, ob, n, &pri, 1, vel, 2, cams, n_cam);
+    trk_t T = {p, level, 1, fr->prev.fixed != 0, chi2};
+    static const float chi2Mono[4] = {5.991f, 5.991f, 5.991f, 5.991f};
+    static const float chi2Stereo[4] = {15.6f, 9.8f, 7.815f, 7.815f};
+    int nBad = 0, iters = 0, trials = 0;
+    for (int it = 0; it < 4; ++it) {
+        double lambda = 0.0, ni = 2.0;
+        int nbad_lm = 0;
+        for (int k = 0; k < 10; ++k) {   /* optimize(its[it] = 10) */
+            int r = trk_lm_iteration(&T, k, &lambda, &ni, &nbad_lm, &trials);
+            ++iters;
+            if (r != LBA_RESULT_OK && p->cfg.early_stop) break;
+        }
+        nBad = 0;
+        const float chi2close = (float)(1.5 * chi2Mono[it]);
+        for (int i = 0; i < n; ++i) {
+            if (level[i]) {   /* e->computeError() at the current state */
+                double e[3];
+                obs_error(p, &p->obs[i], e);
+                chi2[i] = chi2_of(e, obs_dim(p->obs[i].kind), p->obs[i].w);
+            }
+            const float c2 = (float)chi2[i];
+            int out;
+            if (tob[i].kind == LBA_STEREO) out = c2 > chi2Stereo[it];
+            else {
+                const int bclose = tob[i].close != 0;
+                out = (c2 > chi2Mono[it] && !bclose) || (bclose && c2 > chi2close) || !trk_depth_ok(p, i);
+            }
+            level[i] = out;
+            nBad += out;
+        }
+        if (it == 2) T.robust = 0;
+        if (n + 3 < 10) break;   /* optimizer.edges().size() < 10 */
+    }
+    for (int i = 0; i < n; ++i) tob[i].outlier = level[i];
+    const kf_t* c = &p->kf[1];
+    fr->cur.q[0] = c->Twb.q.x; fr->cur.q[1] = c->Twb.q.y; fr->cur.q[2] = c->Twb.q.z; fr->cur.q[3] = c->Twb.q.w;
+    memcpy(fr->cur.t, c->Twb.t, sizeof(double) * 3);
+    memcpy(fr->cur.vel, c->vel, sizeof(double) * 6);
+    fr->n_good = n - nBad;
+    fr->iterations = iters;
+    orc_destroy(p);
+    free(lm); free(ob); free(level); free(chi2);
+    return fr->n_good;
+}

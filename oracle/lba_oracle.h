@@ -50,6 +50,11 @@ int    orc_obs_linearize(orc_problem* p, int obs_index, double* err, double* J);
 /* prior edge: err[12], Ji[144], Jj[144] */
 int    orc_prior_linearize(orc_problem* p, int prior_index, double* err, double* Ji, double* Jj);
 
+/* Optimizer::PoseGPOptimizationFromeLastFrame on one frame (include/amc_lba.h lba_track_*): updates
+ * fr->cur, tob[].outlier, fr->n_good (returned), fr->iterations */
+int    orc_track_pose(const lba_config* cfg, lba_track_frame* fr, lba_track_obs* tob, int n,
+                      const lba_cam* cams, int n_cam);
+
 /* Lie / GP primitives for golden-vector tests */
 void   orc_se3_exp(const double xi[6], double q[4], double t[3]);
 void   orc_se3_log(const double q[4], const double t[3], double xi[6]);

@@ -209,3 +209,12 @@ def ldlt_solve(A, b):
     x = np.zeros_like(b)
     ok = lib().orc_ldlt_solve(len(b), _d(A), _d(b), _d(x))
     return bool(ok), x
+
+
+def track_pose(cfg, frame, obs, cams):
+    """orc_track_pose on one frame (a 1-element TRACK_FRAME_DTYPE array) and its observations;
+    both arrays are updated in place.  Returns n_good."""
+    L = lib()
+    L.orc_track_pose.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] + [ctypes.c_void_p, ctypes.c_int]
+    return L.orc_track_pose(ctypes.byref(cfg), ptr(frame), ptr(obs), len(obs), ptr(cams), len(cams))
+

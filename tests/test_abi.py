@@ -53,6 +53,12 @@ def test_struct_layouts_match_header(struct, dtype):
     assert _c_sizeof(struct) == dtype.itemsize
 
 
+def test_track_structs_match_header():
+    from amc_lba.track import TRACK_FRAME_DTYPE, TRACK_OBS_DTYPE
+    assert _c_sizeof("lba_track_obs") == TRACK_OBS_DTYPE.itemsize
+    assert _c_sizeof("lba_track_frame") == TRACK_FRAME_DTYPE.itemsize
+
+
 def test_ctypes_structs_match_header():
     assert _c_sizeof("lba_config") == ctypes.sizeof(abi.LbaConfig)
     assert _c_sizeof("lba_stats") == ctypes.sizeof(abi.LbaStats)
