@@ -102,11 +102,10 @@ __device__ __forceinline__ double obs_pose(const DevProblem& P, const double* gp
 
 // One observation of the linearisation (DIM compile-time so every per-row array stays in
 // registers): residual, Huber weight, the rows [J1 e Jp] into the LDS row buffer (J1 w.r.t. the
-// pose sample: the pose / velocity Jacobian J1 N is never formed, see k_linearize) and
-// G = rho' w sum_rows J1^T Jp; returns rho(chi2).
+// pose sample: the pose / velocity Jacobian J1 N is never formed, see k_linearize); returns rho(chi2).
 template <int DIM>
 __device__ __forceinline__ double lin_obs(const DevProblem& P, const double* gps, const double* kst, const double* lst,
-                                          int o, int cam, bool gp, double* rows, double* rw, double* G, int write_res) {
+                                          int o, int cam, bool gp, double* rows, double* rw, int write_res) {
     CamD cd;
     load_cam(P.camd + (size_t)cam * CAMD_STRIDE, &cd);
     double Rwb[9], twb[3];
@@ -137,15 +136,6 @@ __device__ __forceinline__ double lin_obs(const DevProblem& P, const double* gps
         for (int j = 0; j < 3; ++j) R[7 + j] = Jp[d * 3 + j];
         rw[row + d] = s;
     }
-#pragma unroll
-    for (int l = 0; l < 6; ++l)
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            double g = 0.0;
-#pragma unroll
-            for (int d = 0; d < DIM; ++d) g += J1[d * 6 + l] * Jp[d * 3 + a];
-            G[l * 3 + a] = s * g;
-        }
     P.ob_chi2[o] = chi;
     if (write_res)
 #pragma unroll
@@ -354,9 +344,9 @@ __device__ __forceinline__ void smp_task(const DevProblem& P, const double* rows
 __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, int write_res, int gate) {
     __shared__ double rows[TILE_ROWS * ROW_STRIDE];
     __shared__ double rw[TILE_ROWS];
-    __shared__ double Gs[TILE_OBS * G_STRIDE];
     __shared__ int tsm[2 * TILE_SMP];
     __shared__ int osm[TILE_OBS];
+    __shared__ int orow[TILE_OBS];   // per observation: first LDS row | rows << 16
     __shared__ int prow[TILE_PROWS];
     __shared__ int pr0[TILE_PAIRS + 1];
     __shared__ int lrow[TILE_ROWS];
@@ -409,10 +399,10 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
         const int kind = meta & 15, cam = meta >> 4;
         const bool gp = kind <= LBA_STEREO_GP;
         osm[tid] = P.ob_smp[o];
-        double* G = Gs + tid * G_STRIDE;
-        rho0 = (kind == LBA_STEREO_GP || kind == LBA_STEREO)
-                   ? lin_obs<3>(P, gps, kst, lst, o, cam, gp, rows, rw, G, write_res)
-                   : lin_obs<2>(P, gps, kst, lst, o, cam, gp, rows, rw, G, write_res);
+        const bool st = kind == LBA_STEREO_GP || kind == LBA_STEREO;
+        orow[tid] = P.ob_row[o] | ((st ? 3 : 2) << 16);
+        rho0 = st ? lin_obs<3>(P, gps, kst, lst, o, cam, gp, rows, rw, write_res)
+                  : lin_obs<2>(P, gps, kst, lst, o, cam, gp, rows, rw, write_res);
     }
     const double tchi = block_sum<TILE_OBS>(rho0, red);   // (its barrier also publishes rows / lists)
     if (tid == 0) P.chi_lin[tile] = tchi;
@@ -443,10 +433,27 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
             const int ol = code & 0xffff, side = code >> 16;
             // N stored transposed: column c of N (6 values) at 12 + 6 c
             const double* Nc = gps + (size_t)osm[ol] * GPS_STRIDE + 12 + 6 * (12 * side + 4 * sb);
-            const double* G = Gs + ol * G_STRIDE;
+            // G = rho' w sum_rows J1^T Jp of the observation, from its LDS rows (not staged: the LDS
+            // it would take halves the workgroups a CU holds)
+            const int r0 = orow[ol] & 0xffff, nrw = orow[ol] >> 16;
             double g[18];
 #pragma unroll
-            for (int u = 0; u < 18; ++u) g[u] = G[u];
+            for (int u = 0; u < 18; ++u) g[u] = 0.0;
+            for (int d = 0; d < nrw; ++d) {
+                const double* R = rows + (r0 + d) * ROW_STRIDE;
+                double jr[9];
+#pragma unroll
+                for (int u = 0; u < 6; ++u) jr[u] = R[u];
+#pragma unroll
+                for (int u = 0; u < 3; ++u) jr[6 + u] = R[7 + u];
+#pragma unroll
+                for (int l = 0; l < 6; ++l)
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) g[l * 3 + a] += jr[l] * jr[6 + a];
+            }
+            const double sw = rw[r0];
+#pragma unroll
+            for (int u = 0; u < 18; ++u) g[u] *= sw;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 double n[6];
