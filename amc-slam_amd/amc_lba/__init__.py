@@ -57,6 +57,7 @@ def lib():
         L.lba_group_destroy.argtypes = [vp]
         L.lba_group_destroy.restype = None
         L.lba_set_partition_group.argtypes = [vp, vp, ctypes.c_int32]
+        L.lba_get_cams.argtypes = [vp, vp]
         _lib = L
     return _lib
 
@@ -65,7 +66,7 @@ def exported_symbols():
     return ["lba_abi_version", "lba_create", "lba_destroy", "lba_last_error", "lba_set_config", "lba_set_problem",
             "lba_optimize", "lba_get_state", "lba_set_state", "lba_eval", "lba_linearize", "lba_solve_step",
             "lba_pose_dim", "lba_set_partition", "lba_rccl_unique_id", "lba_set_partition_rccl", "lba_group_create",
-            "lba_group_destroy", "lba_set_partition_group"]
+            "lba_group_destroy", "lba_set_partition_group", "lba_get_cams"]
 
 
 class Group:
@@ -163,6 +164,12 @@ class Problem:
         lm = np.zeros((self.n_lm, 3))
         self._check(lib().lba_get_state(self.h, ptr(kfs), _d(lm)))
         return kfs, lm
+
+    def cams(self):
+        """Camera records with the current extrinsic estimates (lba_get_cams)."""
+        c = np.zeros(len(self.win.cams), CAM_DTYPE)
+        self._check(lib().lba_get_cams(self.h, ptr(c)))
+        return c
 
     def set_state(self, kfs=None, lm=None):
         kfs = None if kfs is None else np.ascontiguousarray(kfs, dtype=KF_DTYPE)

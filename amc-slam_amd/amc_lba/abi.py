@@ -22,12 +22,13 @@ PRIOR_DTYPE = np.dtype([("kf_a", "<i4"), ("kf_b", "<i4")], align=True)
 CAM_DTYPE = np.dtype([
     ("q", "<f8", (4,)), ("t", "<f8", (3,)),
     ("fx", "<f8"), ("fy", "<f8"), ("cx", "<f8"), ("cy", "<f8"),
+    ("ext_free", "<i4"), ("pad", "<i4"), ("rbc_ini", "<f8", (4,)), ("rbc_info", "<f8", (9,)),
 ], align=True)
 
 assert KF_DTYPE.itemsize == 128
 assert OBS_DTYPE.itemsize == 64
 assert PRIOR_DTYPE.itemsize == 8
-assert CAM_DTYPE.itemsize == 88
+assert CAM_DTYPE.itemsize == 200
 
 # observation kinds (LBA_MONO_GP ... LBA_STEREO)
 MONO_GP, STEREO_GP, MONO, STEREO = 0, 1, 2, 3

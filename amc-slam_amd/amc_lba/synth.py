@@ -12,7 +12,7 @@ outliers; every stored value is rounded to float32 like the reference's float st
 EdgeGaussianPrior between consecutive optimisable KFs, EdgeMonoGPExtrinsic for cameras
 0..n-2 (vertices prev KF, KF) and EdgeMono/EdgeStereo for the reference camera.
 """
-from dataclasses import dataclass, field
+from dataclasses import dataclass, field, replace
 
 import numpy as np
 
@@ -175,6 +175,8 @@ def make_window(n_opt_kf=50, n_fixed=1, n_lm=20000, obs_per_lm=6, n_cam=4, gp=Tr
         cams[c]["q"] = q
         cams[c]["t"] = tbc[c]
         cams[c]["fx"], cams[c]["fy"], cams[c]["cx"], cams[c]["cy"] = 500.0, 500.0, 480.0, 300.0
+        cams[c]["rbc_ini"] = q                                  # MultiFrame::mRbc_ini (Frame.cc:181)
+        cams[c]["rbc_info"] = (0.2 * np.eye(3)).ravel()         # mRbc_ini_cov (Frame.cc:182)
     W, H = 960.0, 600.0
     bf = float(F32(0.12 * 500.0))
 
@@ -311,6 +313,22 @@ def make_window(n_opt_kf=50, n_fixed=1, n_lm=20000, obs_per_lm=6, n_cam=4, gp=Tr
     return Window(kfs=kfs, lm=np.ascontiguousarray(lm), obs=obs, priors=priors,
                   vel_kfs=np.ascontiguousarray(vel_kfs, dtype=np.int32), cams=cams, cfg=cfg,
                   truth_lm=truth_lm, name=name)
+
+
+def with_free_extrinsics(win, cams=None, rot_deg=0.3, trans=0.01, seed=7):
+    """The window of an extrinsic-calibration pass (LocalGPBA bExtrinsic, src/Optimizer.cc:1228-1240):
+    the asynchronous cameras' (all but the reference camera) VertexExtrinsic free, their Tbc estimates
+    perturbed by rot_deg / trans (float-rounded like MultiKeyFrame::mTbc) while the extrinsic prior keeps
+    the generating rotation as mRbc_ini."""
+    rng = np.random.default_rng(seed)
+    cam = win.cams.copy()
+    sel = range(len(cam) - 1) if cams is None else cams
+    for c in sel:
+        R = quat_to_rot(cam[c]["q"]) @ _expso3(rng.normal(0, np.deg2rad(rot_deg), 3))
+        cam[c]["q"] = _f32(rot_to_quat(R))
+        cam[c]["t"] = _f32(cam[c]["t"] + rng.normal(0, trans, 3))
+        cam[c]["ext_free"] = 1
+    return replace(win, cams=cam, name=(win.name or "window") + "_ext")
 
 
 # BASELINE.json configs (SURVEY.md §8(d) per-config instances)

@@ -27,7 +27,9 @@
 namespace lba {
 
 constexpr int KF_STRIDE = 16;
-constexpr int CAMD_STRIDE = 16;     // Rcb(9) tcb(3) fx fy cx cy
+constexpr int CAMD_STRIDE = 88;     // Rcb(9) tcb(3) fx fy cx cy, extrinsic factor Ad(Tbc) (lba::cam_record)
+constexpr int SEG_STRIDE = 8;      // seg_slot ints per slab entry (see DevProblem::seg_slot)
+constexpr int GSEG_STRIDE = 3;     // seg_gslot ints per slab entry
 constexpr int KFP_STRIDE = 12;      // Rwb(9) twb(3)
 
 // tile limits (one workgroup of TILE_OBS threads per tile)
@@ -102,7 +104,13 @@ struct DevProblem {
     const double* gps_t;    // per GP sample: observation time
     int n_gps;              // GP samples; samples n_gps .. n_gps + n_kf - 1 are the KF poses (N = [0 | I 0])
     int n_smp;              // n_gps + n_kf
-    const double* camd;     // [n_cam][CAMD_STRIDE]
+    double* camdb[2];       // [n_cam][CAMD_STRIDE] camera records of state buffer 0 / 1 (they differ only for
+                            // cameras with a free extrinsic: k_update rewrites those from the trial state)
+    const int* kf_cam;      // [n_kf] camera whose extrinsic a KF slot holds, -1 for keyframes
+    int n_kf_user;          // KF slots n_kf_user .. n_kf - 1 are the free extrinsics (pose blocks after the KFs)
+    int n_eprior;           // EdgeExtrinsicPrior edges (one per free extrinsic), slab entries after the velocity edges
+    const int* ep_kf;       // per extrinsic prior: its KF slot
+    const double* ep_data;  // per extrinsic prior: [16] R_ini^-1 quaternion (4), information (9)
     // tiles
     const int* tile_obs0;
     const int* tile_nobs;
@@ -132,9 +140,10 @@ struct DevProblem {
     const int* lm_pair0;    // [n_lm + 1] landmark -> pairs
     // partial-sum slabs are sorted by their reduction target, so every reduction below reads
     // one contiguous range (coalesced) instead of chasing a source list
-    const int* seg_slot;    // per slab entry (pose samples, motion priors, velocity edges): 5 ints
-                            //   aa, ab, bb slot in hslab (-1 = none), ab transposed flag, -
-    const int* seg_gslot;   // per slab entry: ga, gb slot in gslab (-1 = none)
+    const int* seg_slot;    // per slab entry (pose samples, motion priors, velocity edges, extrinsic priors):
+                            //   SEG_STRIDE ints: aa, ab, bb slot in hslab (-1 = none), ab transposed flag,
+                            //   ae, be, ee slot (a sample's extrinsic block e), camera of e
+    const int* seg_gslot;   // per slab entry: ga, gb, ge slot in gslab (-1 = none)
     const int* asm_list;    // upper blocks inside the structural pattern of S (diagonal + any source)
     int n_asm;
     const int* ztiles;      // tiles (i | j << 16) of the permuted envelope, zeroed before each assembly
@@ -203,8 +212,8 @@ struct DevProblem {
     double* xsol;           // [npad] solution (natural order)
     double* yv;             // [np] forward-substituted rhs
     double* x;              // [np + 3 n_lm]
-    double* chi_lin;        // [n_tiles + n_prior + n_vel]
-    double* chi_eval;       // [n_tiles + n_prior + n_vel]
+    double* chi_lin;        // [n_tiles + n_prior + n_vel + n_eprior]
+    double* chi_eval;       // [n_tiles + n_prior + n_vel + n_eprior]
     double* scale_part;     // [n_upd_blocks]
     int n_upd_blocks;
     double* kbuf[2];        // kf state buffers [n_kf][KF_STRIDE] (current / trial, see LMCtl::cur)

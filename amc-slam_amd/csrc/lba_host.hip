@@ -44,6 +44,13 @@ struct lba_problem {
     std::vector<double> lm_host;  // original landmark positions (inactive ones are returned as is)
     std::vector<int> kf_fixed;
     int n_lm_dev = 0, n_pb = 0, np = 0;
+    // free extrinsics: KF slots n_kf .. n_kf + n_ext - 1, pose blocks after the KFs' (12 wide, the second
+    // half inert); the caller's pose system has them 6 wide: pose_ext[i] = caller index of internal pose
+    // index i (-1: inert), np_ext = its dimension
+    int n_ext = 0, np_ext = 0;
+    std::vector<int> pose_ext;
+    std::vector<lba_cam> cams;
+    std::vector<int> ext_cams;
     DevProblem D{};
     double* kst[2] = {nullptr, nullptr};
     double* lst[2] = {nullptr, nullptr};
@@ -221,6 +228,15 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     }
     for (int i = 0; i < n_vel; ++i)
         if (vel_kfs[i] < 0 || vel_kfs[i] >= n_kf) throw ApiError{LBA_E_ARG, "velocity edge: bad vertex"};
+    std::vector<int> ext_cams;   // cameras with a free extrinsic, ascending (g2o vertex ids iniMPid + c + 1)
+    for (int c = 0; c < n_cam; ++c)
+        if (cams[c].ext_free) ext_cams.push_back(c);
+    if (!ext_cams.empty()) {
+        if (p->part_n > 0) throw ApiError{LBA_E_LIMIT, "free extrinsics are not supported in a partitioned problem"};
+        for (int i = 0; i < n_obs; ++i)   // EdgeStereoGP projects through the static MultiKeyFrame::mTbc
+            if (obs[i].kind == LBA_STEREO_GP && cams[obs[i].cam].ext_free)
+                throw ApiError{LBA_E_ARG, "obs " + std::to_string(i) + ": stereo GP observation of a camera with a free extrinsic"};
+    }
 
     free_all(p);
     p->n_kf = n_kf; p->n_lm = n_lm; p->n_obs = n_obs; p->n_cam = n_cam;
@@ -253,12 +269,31 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     if (p->part_n > 0)
         for (int k = 0; k < n_kf; ++k)
             if (!kfs[k].fixed) kf_act[k] = 1;
-    p->kf_hidx.assign(n_kf, -1);
+    // free extrinsics (always active: their EdgeExtrinsicPrior is not all-fixed) as KF slots after the
+    // keyframes, pose blocks after the keyframes' (g2o orders the active vertices by id)
+    const int n_ext = (int)ext_cams.size(), n_kfs = n_kf + n_ext;
+    std::vector<int> cam_slot(n_cam, -1);
+    p->kf_hidx.assign(n_kfs, -1);
     int n_pb = 0;
     for (int k = 0; k < n_kf; ++k)
         if (kf_act[k] && !kfs[k].fixed) p->kf_hidx[k] = n_pb++;
+    const int n_pb_kf = n_pb;
+    for (int e = 0; e < n_ext; ++e) {
+        cam_slot[ext_cams[e]] = n_kf + e;
+        p->kf_hidx[n_kf + e] = n_pb++;
+    }
+    p->n_ext = n_ext;
+    p->ext_cams = ext_cams;
+    p->cams.assign(cams, cams + n_cam);
     p->n_pb = n_pb;
     p->np = 12 * n_pb;
+    p->np_ext = 12 * n_pb_kf + 6 * n_ext;
+    p->pose_ext.assign(p->np, -1);
+    for (int i = 0; i < p->np; ++i)
+        if (i < 12 * n_pb_kf) p->pose_ext[i] = i;
+        else if (i % 12 < 6) p->pose_ext[i] = 12 * n_pb_kf + 6 * ((i - 12 * n_pb_kf) / 12) + i % 12;
+    // the extrinsic block an observation links (EdgeMonoGPExtrinsic's vertex 3), or -1
+    auto ext_block = [&](const lba_obs& o) { return o.kind == LBA_MONO_GP && cam_slot[o.cam] >= 0 ? p->kf_hidx[cam_slot[o.cam]] : -1; };
     if (p->np > 4095 * CHOL_NB)
         throw ApiError{LBA_E_LIMIT, "pose system larger than 131040 (10920 keyframes) not supported"};
     if ((p->cfg.flags & LBA_FLAG_DENSE_SOLVE) && p->np > CF_DENSE_MAX_NP * CHOL_NB)
@@ -315,29 +350,33 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         }
 
     // GP pose samples: distinct observation times per GP pair (one per camera time stamp in
-    // LocalGPBA), contiguous per pair
-    std::vector<int> gp_s0(gp_a.size() + 1, 0), sample_of(n_obs, -1);
+    // LocalGPBA), contiguous per pair; observations of a camera with a free extrinsic get samples of
+    // their own (key: time, camera), so a sample couples at most one extrinsic block
+    std::vector<int> gp_s0(gp_a.size() + 1, 0), sample_of(n_obs, -1), gps_cam;
     std::vector<double> gps_t;
     {
-        std::vector<std::vector<double>> ts(gp_a.size());
+        typedef std::pair<double, int> SKey;
+        auto skey = [&](const lba_obs& o) { return SKey(o.t, ext_block(o) >= 0 ? o.cam : -1); };
+        std::vector<std::vector<SKey>> ts(gp_a.size());
         for (int i = 0; i < n_obs; ++i)
-            if (is_gp(obs[i].kind)) ts[gpmap[std::make_pair(obs[i].kf_a, obs[i].kf_b)]].push_back(obs[i].t);
+            if (is_gp(obs[i].kind)) ts[gpmap[std::make_pair(obs[i].kf_a, obs[i].kf_b)]].push_back(skey(obs[i]));
+        std::vector<SKey> keys;
         for (size_t g = 0; g < ts.size(); ++g) {
             std::sort(ts[g].begin(), ts[g].end());
             ts[g].erase(std::unique(ts[g].begin(), ts[g].end()), ts[g].end());
             gp_s0[g + 1] = gp_s0[g] + (int)ts[g].size();
-            for (double t : ts[g]) gps_t.push_back(t);
+            for (const SKey& k : ts[g]) { gps_t.push_back(k.first); gps_cam.push_back(k.second); keys.push_back(k); }
         }
         for (int i = 0; i < n_obs; ++i)
             if (is_gp(obs[i].kind)) {
                 const int g = gpmap[std::make_pair(obs[i].kf_a, obs[i].kf_b)];
-                const double* b = gps_t.data() + gp_s0[g];
-                sample_of[i] = gp_s0[g] + (int)(std::lower_bound(b, b + (gp_s0[g + 1] - gp_s0[g]), obs[i].t) - b);
+                const SKey* b = keys.data() + gp_s0[g];
+                sample_of[i] = gp_s0[g] + (int)(std::lower_bound(b, b + (gp_s0[g + 1] - gp_s0[g]), skey(obs[i])) - b);
             }
     }
 
     // pose sample of every observation: its GP sample, or the KF pose record n_gps + kf_b
-    const int n_gps = (int)gps_t.size(), n_smp = n_gps + n_kf;
+    const int n_gps = (int)gps_t.size(), n_smp = n_gps + n_kfs;
     std::vector<int> smp_of(n_obs);
     for (int i = 0; i < n_obs; ++i) smp_of[i] = is_gp(obs[i].kind) ? sample_of[i] : n_gps + obs[i].kf_b;
 
@@ -350,6 +389,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             const lba_obs& o = obs[obs_of[q]];
             if (H[o.kf_b] >= 0) ks.push_back(H[o.kf_b]);
             if (is_gp(o.kind) && H[o.kf_a] >= 0) ks.push_back(H[o.kf_a]);
+            if (ext_block(o) >= 0) ks.push_back(ext_block(o));
         }
         std::sort(ks.begin(), ks.end());
         ks.erase(std::unique(ks.begin(), ks.end()), ks.end());
@@ -368,16 +408,18 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         auto smpq = [&](int q) { return smp_of[obs_of[q]]; };
         int d = 0;
         while (d < nl) {
-            int nobs = 0, rows = 0, npair = 0, nlmt = 0;
+            int nobs = 0, rows = 0, npair = 0, nlmt = 0, nent = 0;
             std::vector<int> uni, usm;
             int ncomb = 0;   // Schur triples of the tile (sum over landmarks of P (P + 1) / 2)
             int e = d;
             while (e < nl) {
-                int no = lobs0[e + 1] - lobs0[e], nr = 0;
+                int no = lobs0[e + 1] - lobs0[e], nr = 0, ne = 0;
                 std::vector<int> s2 = usm;
                 for (int q = lobs0[e]; q < lobs0[e + 1]; ++q) {
-                    nr += obs_dim(obs[obs_of[q]].kind);
+                    const lba_obs& ob = obs[obs_of[q]];
+                    nr += obs_dim(ob.kind);
                     s2.push_back(smpq(q));
+                    ne += (H[ob.kf_b] >= 0) + (is_gp(ob.kind) && H[ob.kf_a] >= 0) + (ext_block(ob) >= 0);
                 }
                 std::sort(s2.begin(), s2.end());
                 s2.erase(std::unique(s2.begin(), s2.end()), s2.end());
@@ -389,14 +431,14 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 const int ncl = npl * (npl + 1) / 2;
                 const bool fits = nobs + no <= TILE_OBS && rows + nr <= TILE_ROWS && npair + npl <= TILE_PAIRS &&
                                   nlmt + 1 <= TILE_LMS && (int)u2.size() <= TILE_KF && (int)s2.size() <= TILE_SMP &&
-                                  ncomb + ncl <= TILE_SLIST;
+                                  ncomb + ncl <= TILE_SLIST && nent + ne <= TILE_PROWS;
                 if (!fits) {
                     if (e == d)
                         throw ApiError{LBA_E_LIMIT, "landmark " + std::to_string(order[e]) +
                                                         " exceeds tile limits (obs/rows/pairs/keyframes)"};
                     break;
                 }
-                nobs += no; rows += nr; npair += npl; nlmt += 1; uni.swap(u2); usm.swap(s2); ncomb += ncl;
+                nobs += no; rows += nr; npair += npl; nlmt += 1; uni.swap(u2); usm.swap(s2); ncomb += ncl; nent += ne;
                 ++e;
             }
             t_obs0.push_back(lobs0[d]); t_nobs.push_back(nobs);
@@ -431,6 +473,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                         const lba_obs& ob = obs[obs_of[o]];
                         if (H[ob.kf_b] == k) pair_rows.push_back((o - lobs0[d]) | (1 << 16));
                         if (is_gp(ob.kind) && H[ob.kf_a] == k) pair_rows.push_back(o - lobs0[d]);
+                        if (ext_block(ob) == k) pair_rows.push_back((o - lobs0[d]) | (2 << 16));
                     }
                     pair_r0[q + 1] = (int)pair_rows.size();
                 }
@@ -500,36 +543,55 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             const int id = ublock_id(n_pb, bi, bj);
             ub_i[id] = bi; ub_j[id] = bj;
         }
-    std::vector<int> ent_a, ent_b;
+    // (a sample of a camera with a free extrinsic also couples its block e: ae, be, ee, b_e; then the
+    // extrinsic priors on their blocks as "b")
+    std::vector<int> ent_a, ent_b, ent_e, ent_cam;
     for (int sm = 0; sm < n_smp; ++sm) {
+        ent_e.push_back(-1); ent_cam.push_back(-1);
         if (mcnt[sm] == 0) { ent_a.push_back(-1); ent_b.push_back(-1); continue; }   // unobserved
         if (sm < n_gps) {
             const int g = (int)(std::upper_bound(gp_s0.begin(), gp_s0.end(), sm) - gp_s0.begin()) - 1;
             ent_a.push_back(H[gp_a[g]]); ent_b.push_back(H[gp_b[g]]);
+            if (gps_cam[sm] >= 0) { ent_e.back() = H[cam_slot[gps_cam[sm]]]; ent_cam.back() = gps_cam[sm]; }
         } else {
             ent_a.push_back(-1); ent_b.push_back(H[sm - n_gps]);
         }
     }
-    for (auto& e : pri) { ent_a.push_back(H[e.kf_a]); ent_b.push_back(H[e.kf_b]); }
-    for (int k : vel) { ent_a.push_back(-1); ent_b.push_back(H[k]); }
+    for (auto& e : pri) { ent_a.push_back(H[e.kf_a]); ent_b.push_back(H[e.kf_b]); ent_e.push_back(-1); ent_cam.push_back(-1); }
+    for (int k : vel) { ent_a.push_back(-1); ent_b.push_back(H[k]); ent_e.push_back(-1); ent_cam.push_back(-1); }
+    for (int e = 0; e < n_ext; ++e) { ent_a.push_back(-1); ent_b.push_back(H[n_kf + e]); ent_e.push_back(-1); ent_cam.push_back(-1); }
     const int n_entries = (int)ent_a.size();
     std::vector<int> hcnt(n_ublocks + 1, 0), gcnt(n_pb + 1, 0);
     for (int en = 0; en < n_entries; ++en) {
-        const int a = ent_a[en], b = ent_b[en];
+        const int a = ent_a[en], b = ent_b[en], x = ent_e[en];
         if (a >= 0) { hcnt[ublock_id(n_pb, a, a)]++; gcnt[a]++; }
         if (b >= 0) { hcnt[ublock_id(n_pb, b, b)]++; gcnt[b]++; }
         if (a >= 0 && b >= 0) hcnt[ublock_id(n_pb, std::min(a, b), std::max(a, b))]++;
+        if (x >= 0) {   // extrinsic blocks follow every KF block: (a, x), (b, x) are upper as they stand
+            hcnt[ublock_id(n_pb, x, x)]++; gcnt[x]++;
+            if (a >= 0) hcnt[ublock_id(n_pb, a, x)]++;
+            if (b >= 0) hcnt[ublock_id(n_pb, b, x)]++;
+        }
     }
     std::vector<int> hs0 = prefix(hcnt), gs0 = prefix(gcnt);
     std::vector<int> hfill(hs0), gfill(gs0);
-    std::vector<int> seg_slot(5 * (size_t)std::max(n_entries, 1), -1), seg_gslot(2 * (size_t)std::max(n_entries, 1), -1);
+    std::vector<int> seg_slot(SEG_STRIDE * (size_t)std::max(n_entries, 1), -1),
+        seg_gslot(GSEG_STRIDE * (size_t)std::max(n_entries, 1), -1);
     for (int en = 0; en < n_entries; ++en) {
-        const int a = ent_a[en], b = ent_b[en];
-        int* sl = seg_slot.data() + 5 * (size_t)en;
-        sl[3] = 0; sl[4] = 0;
-        if (a >= 0) { sl[0] = hfill[ublock_id(n_pb, a, a)]++; seg_gslot[2 * (size_t)en] = gfill[a]++; }
+        const int a = ent_a[en], b = ent_b[en], x = ent_e[en];
+        int* sl = seg_slot.data() + SEG_STRIDE * (size_t)en;
+        int* gl = seg_gslot.data() + GSEG_STRIDE * (size_t)en;
+        sl[3] = 0;
+        if (a >= 0) { sl[0] = hfill[ublock_id(n_pb, a, a)]++; gl[0] = gfill[a]++; }
         if (a >= 0 && b >= 0) { sl[1] = hfill[ublock_id(n_pb, std::min(a, b), std::max(a, b))]++; sl[3] = a > b; }
-        if (b >= 0) { sl[2] = hfill[ublock_id(n_pb, b, b)]++; seg_gslot[2 * (size_t)en + 1] = gfill[b]++; }
+        if (b >= 0) { sl[2] = hfill[ublock_id(n_pb, b, b)]++; gl[1] = gfill[b]++; }
+        if (x >= 0) {
+            if (a >= 0) sl[4] = hfill[ublock_id(n_pb, a, x)]++;
+            if (b >= 0) sl[5] = hfill[ublock_id(n_pb, b, x)]++;
+            sl[6] = hfill[ublock_id(n_pb, x, x)]++;
+            sl[7] = ent_cam[en];
+            gl[2] = gfill[x]++;
+        }
     }
     // Schur partial blocks per (tile, KF pair) and rhs partials per (tile, KF)
     std::vector<int> scnt(n_ublocks + 1, 0), gpcnt(n_pb + 1, 0);
@@ -558,22 +620,21 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         ob_z[3 * (size_t)q] = o.z[0]; ob_z[3 * (size_t)q + 1] = o.z[1]; ob_z[3 * (size_t)q + 2] = o.z[2];
         ob_w[q] = o.w;
     }
-    // cameras: Tcb = Tbc^-1 as matrix (MultiKeyFrame::mTbc[c].cast<double>() normalises)
+    // cameras: Tcb = Tbc^-1 as matrix (MultiKeyFrame::mTbc[c].cast<double>() normalises) and the
+    // extrinsic factor Ad(Tbc) (lba::cam_record)
     std::vector<double> camd(CAMD_STRIDE * (size_t)std::max(n_cam, 1), 0.0);
-    for (int c = 0; c < n_cam; ++c) {
-        Cam cm;
-        normalize_q(cams[c].q, cm.q);
-        for (int i = 0; i < 3; ++i) cm.t[i] = cams[c].t[i];
-        cm.fx = cams[c].fx; cm.fy = cams[c].fy; cm.cx = cams[c].cx; cm.cy = cams[c].cy;
-        CamD cd;
-        cam_derive(cm, &cd);
-        double* o = camd.data() + CAMD_STRIDE * c;
-        for (int i = 0; i < 9; ++i) o[i] = cd.Rcb[i];
-        o[9] = cd.tcb[0]; o[10] = cd.tcb[1]; o[11] = cd.tcb[2];
-        o[12] = cd.fx; o[13] = cd.fy; o[14] = cd.cx; o[15] = cd.cy;
-    }
-    // keyframe / landmark state
-    std::vector<double> kst(KF_STRIDE * (size_t)std::max(n_kf, 1), 0.0), lst(3 * (size_t)std::max(nl, 1), 0.0);
+    auto cam_se3 = [&](int c) {
+        SE3 T;
+        double q[4];
+        normalize_q(cams[c].q, q);
+        T.q = Quat{q[0], q[1], q[2], q[3]};
+        for (int i = 0; i < 3; ++i) T.t[i] = cams[c].t[i];
+        return T;
+    };
+    for (int c = 0; c < n_cam; ++c)
+        cam_record(cam_se3(c), cams[c].fx, cams[c].fy, cams[c].cx, cams[c].cy, camd.data() + CAMD_STRIDE * c);
+    // keyframe / landmark state (then the free extrinsics: Tbc as the pose, no velocity)
+    std::vector<double> kst(KF_STRIDE * (size_t)std::max(n_kfs, 1), 0.0), lst(3 * (size_t)std::max(nl, 1), 0.0);
     for (int k = 0; k < n_kf; ++k) {
         double* o = kst.data() + KF_STRIDE * k;
         normalize_q(kfs[k].q, o);
@@ -582,6 +643,24 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         o[13] = kfs[k].time;
         o[14] = kfs[k].bf;
     }
+    std::vector<int> kf_cam(std::max(n_kfs, 1), -1), ep_kf(std::max(n_ext, 1), 0);
+    std::vector<double> ep_data(16 * (size_t)std::max(n_ext, 1), 0.0);
+    for (int e = 0; e < n_ext; ++e) {
+        const int c = ext_cams[e];
+        const SE3 T = cam_se3(c);
+        double* o = kst.data() + KF_STRIDE * (size_t)(n_kf + e);
+        o[0] = T.q.x; o[1] = T.q.y; o[2] = T.q.z; o[3] = T.q.w;
+        for (int i = 0; i < 3; ++i) o[4 + i] = T.t[i];
+        kf_cam[n_kf + e] = c;
+        ep_kf[e] = n_kf + e;
+        // EdgeExtrinsicPrior(R): R_ = R.inverse() of the widened, normalised mRbc_ini (so3.hpp:229-231)
+        double qi[4];
+        normalize_q(cams[c].rbc_ini, qi);
+        const Quat ri = qinv(Quat{qi[0], qi[1], qi[2], qi[3]});
+        double* d = ep_data.data() + 16 * (size_t)e;
+        d[0] = ri.x; d[1] = ri.y; d[2] = ri.z; d[3] = ri.w;
+        for (int i = 0; i < 9; ++i) d[4 + i] = cams[c].rbc_info[i];
+    }
     for (int d = 0; d < nl; ++d)
         for (int i = 0; i < 3; ++i) lst[3 * (size_t)d + i] = lm_xyz[3 * (size_t)order[d] + i];
     std::vector<int> pri_a, pri_b;
@@ -589,7 +668,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
 
     // ---- device upload
     DevProblem& D = p->D;
-    D.n_kf = n_kf; D.n_lm = nl; D.n_obs = n_obs; D.n_gp = (int)gp_a.size(); D.n_pairs = n_pairs;
+    D.n_kf = n_kfs; D.n_kf_user = n_kf; D.n_eprior = n_ext; D.n_lm = nl; D.n_obs = n_obs; D.n_gp = (int)gp_a.size(); D.n_pairs = n_pairs;
     D.n_tiles = n_tiles; D.n_pb = n_pb; D.np = p->np; D.n_prior = (int)pri.size(); D.n_vel = (int)vel.size();
     D.n_cam = n_cam; D.n_entries = n_entries; D.n_sentries = n_sent; D.n_ublocks = n_ublocks;
     D.ob_meta = dupload(p, ob_meta); D.ob_kfa = dupload(p, ob_kfa); D.ob_kfb = dupload(p, ob_kfb);
@@ -600,7 +679,11 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.ob_z = dupload(p, ob_z); D.ob_w = dupload(p, ob_w);
     D.gp_s0 = dupload(p, gp_s0); D.gps_t = dupload(p, gps_t); D.n_gps = n_gps; D.n_smp = n_smp;
     D.kf_hidx = dupload(p, p->kf_hidx); D.gp_kfa = dupload(p, gp_a); D.gp_kfb = dupload(p, gp_b);
-    D.camd = dupload(p, camd);
+    D.camdb[0] = dupload(p, camd);
+    D.camdb[1] = dupload(p, camd);
+    D.kf_cam = dupload(p, kf_cam);
+    D.ep_kf = dupload(p, ep_kf);
+    D.ep_data = dupload(p, ep_data);
     D.tile_obs0 = dupload(p, t_obs0); D.tile_nobs = dupload(p, t_nobs); D.tile_lm0 = dupload(p, t_lm0);
     D.tile_nlm = dupload(p, t_nlm); D.tile_pair0 = dupload(p, t_pair0); D.tile_npair = dupload(p, t_npair);
     D.tile_smp0 = dupload(p, t_smp0); D.tile_nsmp = dupload(p, t_nsmp); D.tsm_meta = dupload(p, tsm_meta);
@@ -642,13 +725,13 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.huber_prior = p->cfg.huber_prior;
     {   // pose samples; the KF records' factor N = [0 | I 0] is constant (k_gp_prep writes their poses)
         std::vector<double> g0((size_t)GPS_STRIDE * std::max(n_smp, 1), 0.0);
-        for (int k = 0; k < n_kf; ++k)
+        for (int k = 0; k < n_kfs; ++k)
             for (int l = 0; l < 6; ++l) g0[(size_t)(n_gps + k) * GPS_STRIDE + 12 + 6 * (12 + l) + l] = 1.0;
         D.gpsb[0] = dupload(p, g0);
         D.gpsb[1] = dupload(p, g0);
     }
     D.mslab = dalloc<double>(p, (size_t)SM_STRIDE * std::max(n_mslots, 1));
-    D.kfp_pose = dalloc<double>(p, (size_t)KFP_STRIDE * std::max(n_kf, 1));
+    D.kfp_pose = dalloc<double>(p, (size_t)KFP_STRIDE * std::max(n_kfs, 1));
     D.hslab = dalloc<double>(p, (size_t)144 * std::max(n_hslots, 1));
     D.gslab = dalloc<double>(p, (size_t)12 * std::max(n_gslots, 1));
     D.sslab = dalloc<double>(p, (size_t)144 * std::max(n_sslots, 1));
@@ -688,20 +771,23 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 pfirst[P] = f;
             }
         }
-        int sa = NP, sb = NP, best = NP;
-        for (int a = 1; a < NP; ++a) {
-            int b = NP;
-            while (b > a && pfirst[b - 1] >= a) --b;   // [b, NP): rows with no entry left of a
-            if (b >= NP) continue;
-            const int len = std::max(a, NP - b) + (b - a);
+        // panels holding rows of free extrinsics (dense: they couple every keyframe) form a tail that
+        // closes the separator; the dissection splits the keyframe panels before it
+        const int NPk = std::min(NP, 12 * n_pb_kf / CHOL_NB + (n_ext ? 0 : NP));
+        int sa = NPk, sb = NPk, best = NP;
+        for (int a = 1; a < NPk; ++a) {
+            int b = NPk;
+            while (b > a && pfirst[b - 1] >= a) --b;   // [b, NPk): rows with no entry left of a
+            if (b >= NPk) continue;
+            const int len = std::max(a, NPk - b) + (b - a) + (NP - NPk);
             if (len < best) { best = len; sa = a; sb = b; }
         }
-        const int nl = sa, nr = NP - sb, ns = sb - sa;
+        const int nl = sa, nr = NPk - sb, ns = sb - sa + (NP - NPk);
         D.nd_left = nl;
         D.nd_right = nr;
         std::vector<int> ppos(NP), pnat(NP);
         for (int P = 0; P < NP; ++P)
-            ppos[P] = P < sa ? P : (P >= sb ? nl + (P - sb) : nl + nr + (P - sa));
+            ppos[P] = P >= NPk ? P : (P < sa ? P : (P >= sb ? nl + (P - sb) : nl + nr + (P - sa)));
         for (int P = 0; P < NP; ++P) pnat[ppos[P]] = P;
         // envelope of the permuted matrix (lower part, panel positions)
         std::vector<int> pfh(NP);
@@ -906,11 +992,11 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     p->s_layout = 0;
     D.x = dalloc<double>(p, p->np + 3 * (size_t)nl + 1);
     HIPCHK(hipMemset(D.x, 0, sizeof(double) * (p->np + 3 * (size_t)nl + 1)));   // BlockSolver::_x before any solve
-    const int nchi = n_tiles + D.n_prior + D.n_vel;
+    const int nchi = n_tiles + D.n_prior + D.n_vel + D.n_eprior;
     D.chi_lin = dalloc<double>(p, nchi + 1);
     D.chi_eval = dalloc<double>(p, nchi + 1);
     // k_update: one workgroup per GP pair, then KFs and landmarks at 64 per workgroup
-    D.n_upd_blocks = D.n_gp + (n_kf + 63) / 64 + (nl + 63) / 64;
+    D.n_upd_blocks = D.n_gp + (n_kfs + 63) / 64 + (nl + 63) / 64;
     if (D.n_upd_blocks == 0) D.n_upd_blocks = 1;
     D.scale_part = dalloc<double>(p, D.n_upd_blocks);
     D.info = dalloc<int>(p, 1);
@@ -1314,7 +1400,29 @@ int lba_set_config(lba_problem* p, const lba_config* cfg) {
 
 const char* lba_last_error(const lba_problem* p) { return p ? p->err.c_str() : "null problem"; }
 
-int lba_pose_dim(const lba_problem* p) { return p && p->has_problem ? p->np : 0; }
+int lba_pose_dim(const lba_problem* p) { return p && p->has_problem ? p->np_ext : 0; }
+
+int lba_get_cams(lba_problem* p, lba_cam* cams_out) {
+    if (!p || !p->has_problem || !cams_out) return LBA_E_ARG;
+    try {
+        HIPCHK(hipSetDevice(p->cfg.device));
+        for (int c = 0; c < p->n_cam; ++c) cams_out[c] = p->cams[c];
+        if (p->n_ext) {
+            std::vector<double> kx(KF_STRIDE * (size_t)p->n_ext);
+            HIPCHK(hipMemcpyAsync(kx.data(), p->kst[p->cur] + KF_STRIDE * (size_t)p->n_kf, kx.size() * sizeof(double),
+                                  hipMemcpyDeviceToHost, p->stream));
+            HIPCHK(hipStreamSynchronize(p->stream));
+            for (int e = 0; e < p->n_ext; ++e) {
+                lba_cam& o = cams_out[p->ext_cams[e]];
+                for (int i = 0; i < 4; ++i) o.q[i] = kx[KF_STRIDE * e + i];
+                for (int i = 0; i < 3; ++i) o.t[i] = kx[KF_STRIDE * e + 4 + i];
+            }
+        }
+        return LBA_OK;
+    } catch (const HipError& e) {
+        return map_error(p, e);
+    }
+}
 
 int lba_set_partition(lba_problem* p, int32_t rank, int32_t nranks, lba_allreduce_fn fn, void* user) {
     if (!p || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !fn)) return LBA_E_ARG;
@@ -1599,11 +1707,12 @@ int lba_linearize(lba_problem* p, double* residuals, double* H_pp, double* b, do
         linearize(p, residuals ? 1 : 0);
         assemble_layout(p, 0.0, ASM_FULL);
         HIPCHK(hipGetLastError());
-        const int np = p->np, nl = D.n_lm;
+        const int np = p->np, nl = D.n_lm, npx = p->np_ext;
         std::vector<double> bp(np + 1), bl(3 * (size_t)nl + 1), hll(9 * (size_t)nl + 1), res(3 * (size_t)p->n_obs + 1);
+        std::vector<double> hpp(H_pp ? (size_t)np * np + 1 : 1);
         if (H_pp && np)
-            HIPCHK(hipMemcpy2DAsync(H_pp, np * sizeof(double), D.S, D.npad * sizeof(double), np * sizeof(double), np,
-                                    hipMemcpyDeviceToHost, p->stream));
+            HIPCHK(hipMemcpy2DAsync(hpp.data(), np * sizeof(double), D.S, D.npad * sizeof(double), np * sizeof(double),
+                                    np, hipMemcpyDeviceToHost, p->stream));
         HIPCHK(hipMemcpyAsync(bp.data(), D.bp, np * sizeof(double), hipMemcpyDeviceToHost, p->stream));
         HIPCHK(hipMemcpyAsync(bl.data(), D.bl, 3 * (size_t)nl * sizeof(double), hipMemcpyDeviceToHost, p->stream));
         HIPCHK(hipMemcpyAsync(hll.data(), D.Hll, 9 * (size_t)nl * sizeof(double), hipMemcpyDeviceToHost, p->stream));
@@ -1611,13 +1720,19 @@ int lba_linearize(lba_problem* p, double* residuals, double* H_pp, double* b, do
             HIPCHK(hipMemcpyAsync(res.data(), D.ob_res, 3 * (size_t)p->n_obs * sizeof(double), hipMemcpyDeviceToHost,
                                   p->stream));
         HIPCHK(hipStreamSynchronize(p->stream));
+        const std::vector<int>& X = p->pose_ext;   // internal pose index -> caller's (extrinsics 6 wide)
+        if (H_pp)
+            for (int i = 0; i < np; ++i)
+                for (int j = 0; j < np; ++j)
+                    if (X[i] >= 0 && X[j] >= 0) H_pp[(size_t)X[i] * npx + X[j]] = hpp[(size_t)i * np + j];
         if (b) {
-            for (int i = 0; i < np; ++i) b[i] = bp[i];
+            for (int i = 0; i < np; ++i)
+                if (X[i] >= 0) b[X[i]] = bp[i];
             int r = 0;   // landmarks in g2o order: active ones, original array order
             for (int l = 0; l < p->n_lm; ++l) {
                 const int d = p->lm_dev[l];
                 if (d < 0) continue;
-                for (int i = 0; i < 3; ++i) b[np + 3 * r + i] = bl[3 * (size_t)d + i];
+                for (int i = 0; i < 3; ++i) b[npx + 3 * r + i] = bl[3 * (size_t)d + i];
                 ++r;
             }
         }
@@ -1629,7 +1744,7 @@ int lba_linearize(lba_problem* p, double* residuals, double* H_pp, double* b, do
         if (residuals)
             for (int i = 0; i < p->n_obs; ++i)
                 for (int d = 0; d < 3; ++d) residuals[3 * (size_t)i + d] = res[3 * (size_t)p->obs_dev[i] + d];
-        return np;
+        return npx;
     } catch (const HipError& e) {
         return map_error(p, e);
     }
@@ -1641,7 +1756,7 @@ int lba_solve_step(lba_problem* p, double lambda, double* dx) {
         HIPCHK(hipSetDevice(p->cfg.device));
         if (!p->linearized) linearize(p, 0);
         trial(p, lambda, false, nullptr);
-        const int np = p->np, nl = p->D.n_lm;
+        const int np = p->np, nl = p->D.n_lm, npx = p->np_ext;
         if (p->h_fin[3] != 0.0) {
             p->err = "reduced camera system not positive definite";
             return LBA_E_SOLVE;
@@ -1649,12 +1764,13 @@ int lba_solve_step(lba_problem* p, double lambda, double* dx) {
         if (dx) {
             std::vector<double> x(np + 3 * (size_t)nl + 1);
             HIPCHK(hipMemcpy(x.data(), p->D.x, (np + 3 * (size_t)nl) * sizeof(double), hipMemcpyDeviceToHost));
-            for (int i = 0; i < np; ++i) dx[i] = x[i];
+            for (int i = 0; i < np; ++i)
+                if (p->pose_ext[i] >= 0) dx[p->pose_ext[i]] = x[i];
             int r = 0;
             for (int l = 0; l < p->n_lm; ++l) {
                 const int d = p->lm_dev[l];
                 if (d < 0) continue;
-                for (int i = 0; i < 3; ++i) dx[np + 3 * r + i] = x[np + 3 * (size_t)d + i];
+                for (int i = 0; i < 3; ++i) dx[npx + 3 * r + i] = x[np + 3 * (size_t)d + i];
                 ++r;
             }
         }

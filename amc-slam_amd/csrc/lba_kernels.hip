@@ -31,6 +31,7 @@
 namespace lba {
 
 static_assert(sizeof(GPSample) == GPS_STRIDE * sizeof(double), "GPSample layout drifted");
+static_assert(CAMD_STRIDE == CAMREC_DOUBLES, "camera record layout drifted");
 
 // phase stamps for diagnostics only (buffer allocated when LBA_PHASE_TIMING is set; the uniform
 // null test costs one scalar branch otherwise)
@@ -105,9 +106,10 @@ __device__ __forceinline__ double obs_pose(const DevProblem& P, const double* gp
 // pose sample: the pose / velocity Jacobian J1 N is never formed, see k_linearize); returns rho(chi2).
 template <int DIM>
 __device__ __forceinline__ double lin_obs(const DevProblem& P, const double* gps, const double* kst, const double* lst,
-                                          int o, int cam, bool gp, double* rows, double* rw, int write_res) {
+                                          const double* camd, int o, int cam, bool gp, double* rows, double* rw,
+                                          int write_res) {
     CamD cd;
-    load_cam(P.camd + (size_t)cam * CAMD_STRIDE, &cd);
+    load_cam(camd + (size_t)cam * CAMD_STRIDE, &cd);
     double Rwb[9], twb[3];
     const double bf = obs_pose(P, gps, kst, o, gp, Rwb, twb);
     const double* Xw = lst + (size_t)P.ob_lm[o] * 3;
@@ -146,9 +148,9 @@ __device__ __forceinline__ double lin_obs(const DevProblem& P, const double* gps
 // Residual-only evaluation of one observation (computeError + robust chi2); returns rho(chi2).
 template <int DIM>
 __device__ __forceinline__ double eval_obs(const DevProblem& P, const double* gps, const double* kst,
-                                           const double* lst, int o, int cam, bool gp) {
+                                           const double* lst, const double* camd, int o, int cam, bool gp) {
     CamD cd;
-    load_cam(P.camd + (size_t)cam * CAMD_STRIDE, &cd);
+    load_cam(camd + (size_t)cam * CAMD_STRIDE, &cd);
     double Rwb[9], twb[3];
     const double bf = obs_pose(P, gps, kst, o, gp, Rwb, twb);
     double z[DIM];
@@ -346,6 +348,7 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
     __shared__ double rw[TILE_ROWS];
     __shared__ int tsm[2 * TILE_SMP];
     __shared__ int osm[TILE_OBS];
+    __shared__ int ocam[TILE_OBS];
     __shared__ int orow[TILE_OBS];   // per observation: first LDS row | rows << 16
     __shared__ int prow[TILE_PROWS];
     __shared__ int pr0[TILE_PAIRS + 1];
@@ -362,6 +365,7 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
     const double* __restrict__ kst = P.kbuf[si];
     const double* __restrict__ lst = P.lbuf[si];
     const double* __restrict__ gps = P.gpsb[si];
+    const double* __restrict__ camd = P.camdb[si];
     LBA_TMARK(P.tdbg_lin, 0);
 
     // ---- stage the tile's index lists in LDS (fixed-count loops: all loads issue before the stores)
@@ -399,10 +403,11 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
         const int kind = meta & 15, cam = meta >> 4;
         const bool gp = kind <= LBA_STEREO_GP;
         osm[tid] = P.ob_smp[o];
+        ocam[tid] = cam;
         const bool st = kind == LBA_STEREO_GP || kind == LBA_STEREO;
         orow[tid] = P.ob_row[o] | ((st ? 3 : 2) << 16);
-        rho0 = st ? lin_obs<3>(P, gps, kst, lst, o, cam, gp, rows, rw, write_res)
-                  : lin_obs<2>(P, gps, kst, lst, o, cam, gp, rows, rw, write_res);
+        rho0 = st ? lin_obs<3>(P, gps, kst, lst, camd, o, cam, gp, rows, rw, write_res)
+                  : lin_obs<2>(P, gps, kst, lst, camd, o, cam, gp, rows, rw, write_res);
     }
     const double tchi = block_sum<TILE_OBS>(rho0, red);   // (its barrier also publishes rows / lists)
     if (tid == 0) P.chi_lin[tile] = tchi;
@@ -422,7 +427,8 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
     LBA_TMARK(P.tdbg_lin, 2);
 
     // ---- phase 3: Hpl per (KF, landmark) pair: sum over its (observation, side) entries of
-    //      N_side^T G (N_side: the 6 x 12 block of the sample's factor for that KF), four Hpl rows per task
+    //      N_side^T G (N_side: the 6 x 12 block of the sample's factor for that KF, or for side 2 the
+    //      camera's extrinsic factor [Ad(Tbc) 0]), four Hpl rows per task
     for (int task = tid; task < npair * 3; task += TILE_OBS) {
         const int pl = task / 3, sb = task % 3;
         double acc[12];
@@ -432,7 +438,8 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
             const int code = prow[q];
             const int ol = code & 0xffff, side = code >> 16;
             // N stored transposed: column c of N (6 values) at 12 + 6 c
-            const double* Nc = gps + (size_t)osm[ol] * GPS_STRIDE + 12 + 6 * (12 * side + 4 * sb);
+            const double* Nc = side < 2 ? gps + (size_t)osm[ol] * GPS_STRIDE + 12 + 6 * (12 * side + 4 * sb)
+                                        : camd + (size_t)ocam[ol] * CAMD_STRIDE + 16 + 6 * (4 * sb);
             // G = rho' w sum_rows J1^T Jp of the observation, from its LDS rows (not staged: the LDS
             // it would take halves the workgroups a CU holds)
             const int r0 = orow[ol] & 0xffff, nrw = orow[ol] >> 16;
@@ -505,12 +512,15 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
 constexpr int PRI_THREADS = 256;
 constexpr int EXP_GROUPS = PRI_THREADS / SM_STRIDE;   // 9 partial sums per output
 
-__device__ void sample_expand(const DevProblem& P, const double* gps, int smp, double* Msh, double* Nsh, double* MN,
-                              double* part) {
+// A sample of a camera whose extrinsic is free also couples that extrinsic's block e: N is extended by the
+// camera's factor [Ad(Tbc) 0] (columns 24..35) and ae, be, ee, b_e follow the same way.
+__device__ void sample_expand(const DevProblem& P, const double* gps, const double* camd, int smp, double* Msh,
+                              double* Nsh, double* MN, double* part) {
     const int tid = threadIdx.x;
-    const int* sl = P.seg_slot + 5 * (size_t)smp;
-    const int* gl = P.seg_gslot + 2 * (size_t)smp;
-    if (sl[0] < 0 && sl[1] < 0 && sl[2] < 0) return;   // no optimisable KF (uniform per workgroup)
+    const int* sl = P.seg_slot + SEG_STRIDE * (size_t)smp;
+    const int* gl = P.seg_gslot + GSEG_STRIDE * (size_t)smp;
+    if (sl[0] < 0 && sl[1] < 0 && sl[2] < 0 && sl[6] < 0) return;   // no optimisable vertex (uniform per workgroup)
+    const int ncol = sl[6] >= 0 ? 36 : 24;
     // M / g: group q of the 9 sums every 9th slot of its output (4 loads in flight), then a fixed
     // combination order over the groups
     if (tid < EXP_GROUPS * SM_STRIDE) {
@@ -530,6 +540,7 @@ __device__ void sample_expand(const DevProblem& P, const double* gps, int smp, d
     }
     const double* Ng = gps + (size_t)smp * GPS_STRIDE + 12;
     if (tid < 144) Nsh[tid] = Ng[tid];   // N(l, c) at Nsh[6 c + l]
+    else if (tid < 6 * ncol) Nsh[tid] = camd[(size_t)sl[7] * CAMD_STRIDE + 16 + (tid - 144)];
     __syncthreads();
     if (tid < SM_STRIDE) {
         double v = 0.0;
@@ -543,7 +554,7 @@ __device__ void sample_expand(const DevProblem& P, const double* gps, int smp, d
         const int a = i < j ? i : j, b = i < j ? j : i;
         return Msh[a * 6 - a * (a - 1) / 2 + (b - a)];
     };
-    if (tid < 144) {   // MN(l, c) = sum_m M(l, m) N(m, c), stored MN[6 c + l]
+    if (tid < 6 * ncol) {   // MN(l, c) = sum_m M(l, m) N(m, c), stored MN[6 c + l]
         const int t = tid, c = t / 6, l = t % 6;
         double v = 0.0;
 #pragma unroll
@@ -551,11 +562,14 @@ __device__ void sample_expand(const DevProblem& P, const double* gps, int smp, d
         MN[t] = v;
     }
     __syncthreads();
-    for (int t = tid; t < 3 * 144; t += PRI_THREADS) {
+    // blocks aa, ab, bb, ae, be, ee: column offsets of their row / column vertex in N
+    constexpr unsigned char boff_i[6] = {0, 0, 12, 0, 12, 24}, boff_j[6] = {0, 12, 12, 24, 24, 24};
+    constexpr unsigned char bslot[6] = {0, 1, 2, 4, 5, 6};
+    for (int t = tid; t < (ncol == 36 ? 6 : 3) * 144; t += PRI_THREADS) {
         const int bk = t / 144, ij = t % 144, i = ij / 12, j = ij % 12;
-        const int slot = sl[bk];
+        const int slot = sl[bslot[bk]];
         if (slot < 0) continue;
-        const int ci = (bk == 2 ? 12 : 0) + i, cj = (bk == 0 ? 0 : 12) + j;
+        const int ci = boff_i[bk] + i, cj = boff_j[bk] + j;
         double v = 0.0;
 #pragma unroll
         for (int l = 0; l < 6; ++l) v += Nsh[6 * ci + l] * MN[6 * cj + l];
@@ -563,7 +577,7 @@ __device__ void sample_expand(const DevProblem& P, const double* gps, int smp, d
         if (bk == 1 && sl[3]) H[j * 12 + i] = v;
         else H[i * 12 + j] = v;
     }
-    if (tid < 24) {
+    if (tid < ncol) {
         const int side = tid / 12, i = tid % 12;
         if (gl[side] >= 0) {
             double v = 0.0;
@@ -574,22 +588,59 @@ __device__ void sample_expand(const DevProblem& P, const double* gps, int smp, d
     }
 }
 
-// Workgroups 0 .. n_prior + n_vel - 1: EdgeGaussianPrior / EdgeVelocity quadratic forms; then one
-// workgroup per pose sample (sample_expand).
+// Workgroups 0 .. n_prior + n_vel + n_eprior - 1: EdgeGaussianPrior / EdgeVelocity / EdgeExtrinsicPrior
+// quadratic forms; then one workgroup per pose sample (sample_expand).
 __global__ __launch_bounds__(PRI_THREADS) void k_prior_lin(DevProblem P, int sel, int gate) {
-    __shared__ double Ji[144], Jj[144], WJi[144], WJj[144], Om[144], e[12], We[12];
+    __shared__ double Ji[144], Jj[216], WJi[216], WJj[144], Om[144], e[12], We[12];
     __shared__ double wsh;
     __shared__ double part[EXP_GROUPS * SM_STRIDE];
     const int idx = blockIdx.x, tid = threadIdx.x;
     if (gated_off(P.ctl, gate)) return;
-    if (idx >= P.n_prior + P.n_vel) {
-        sample_expand(P, P.gpsb[state_idx(P, sel)], idx - P.n_prior - P.n_vel, Ji, Jj, WJi, part);
+    const int si = state_idx(P, sel);
+    const int npe = P.n_prior + P.n_vel + P.n_eprior;
+    if (idx >= npe) {
+        sample_expand(P, P.gpsb[si], P.camdb[si], idx - npe, Ji, Jj, WJi, part);
         return;
     }
-    const double* __restrict__ kst = P.kbuf[state_idx(P, sel)];
+    const double* __restrict__ kst = P.kbuf[si];
     const int ent = P.pri_entry0 + idx;
-    const int* sl = P.seg_slot + 5 * (size_t)ent;
-    const int* gl = P.seg_gslot + 2 * (size_t)ent;
+    const int* sl = P.seg_slot + SEG_STRIDE * (size_t)ent;
+    const int* gl = P.seg_gslot + GSEG_STRIDE * (size_t)ent;
+    if (idx >= P.n_prior + P.n_vel) {
+        // EdgeExtrinsicPrior (unary, 3-d, no robust kernel; include/G2oTypes.h:470-494): J = [0 | Jrot], so
+        // H_ee = J^T Om J and b_e = -J^T Om e live in the rotation rows / columns 3..5 of the block
+        const int q = idx - P.n_prior - P.n_vel;
+        const double* ed = P.ep_data + 16 * (size_t)q;
+        if (tid == 0) {
+            const double* kx = kst + (size_t)P.ep_kf[q] * KF_STRIDE;
+            ext_prior_error_jac(Quat{kx[0], kx[1], kx[2], kx[3]}, Quat{ed[0], ed[1], ed[2], ed[3]}, e, Ji);
+            double chi = 0.0;
+            for (int i = 0; i < 3; ++i) {
+                double s = 0.0;
+                for (int k = 0; k < 3; ++k) s += ed[4 + 3 * i + k] * e[k];
+                We[i] = s;
+                chi += e[i] * s;
+            }
+            P.chi_lin[P.n_tiles + idx] = chi;
+        }
+        __syncthreads();
+        double* H = P.hslab + (size_t)sl[2] * 144;
+        for (int t = tid; t < 144; t += PRI_THREADS) {
+            const int i = t / 12 - 3, j = t % 12 - 3;
+            double v = 0.0;
+            if (i >= 0 && i < 3 && j >= 0 && j < 3)   // (Jrot^T Om Jrot)(i, j)
+                for (int a = 0; a < 3; ++a)
+                    for (int b = 0; b < 3; ++b) v += Ji[a * 3 + i] * ed[4 + 3 * a + b] * Ji[b * 3 + j];
+            H[t] = v;
+        }
+        if (tid < 12) {
+            double v = 0.0;
+            if (tid >= 3 && tid < 6)
+                for (int a = 0; a < 3; ++a) v += Ji[a * 3 + tid - 3] * We[a];
+            P.gslab[(size_t)gl[1] * 12 + tid] = -v;
+        }
+        return;
+    }
     if (idx < P.n_prior) {
         if (tid == 0) {
             const double* ka = kst + (size_t)P.pri_a[idx] * KF_STRIDE;
@@ -1963,6 +2014,14 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
             double* kw = ko + (size_t)k * KF_STRIDE;
             for (int j = 0; j < KF_STRIDE; ++j) kw[j] = kn[j];
             kf_pose_record(P, gps, k, kn);
+            const int xc = P.kf_cam[k];
+            if (xc >= 0) {   // a free extrinsic: the trial state's camera record (Tcb, intrinsics, Ad(Tbc))
+                const double* c0 = P.camdb[si] + (size_t)xc * CAMD_STRIDE;
+                SE3 T;
+                T.q = Quat{kn[0], kn[1], kn[2], kn[3]};
+                T.t[0] = kn[4]; T.t[1] = kn[5]; T.t[2] = kn[6];
+                cam_record(T, c0[12], c0[13], c0[14], c0[15], P.camdb[si ^ 1] + (size_t)xc * CAMD_STRIDE);
+            }
             if (h >= 0)
                 for (int j = 0; j < 12; ++j) {
                     if (ok) P.x[12 * h + j] = d[j];
@@ -2019,6 +2078,7 @@ __global__ __launch_bounds__(TILE_OBS) void k_eval(DevProblem P, int sel, int ga
     const double* __restrict__ kst = P.kbuf[si];
     const double* __restrict__ lst = P.lbuf[si];
     const double* __restrict__ gps = P.gpsb[si];
+    const double* __restrict__ camd = P.camdb[si];
     if (tile < P.n_tiles) {
         double rho0 = 0.0;
         if (tid < P.tile_nobs[tile]) {
@@ -2026,8 +2086,8 @@ __global__ __launch_bounds__(TILE_OBS) void k_eval(DevProblem P, int sel, int ga
             const int meta = P.ob_meta[o];
             const int kind = meta & 15, cam = meta >> 4;
             const bool gp = kind <= LBA_STEREO_GP;
-            rho0 = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? eval_obs<3>(P, gps, kst, lst, o, cam, gp)
-                                                                 : eval_obs<2>(P, gps, kst, lst, o, cam, gp);
+            rho0 = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? eval_obs<3>(P, gps, kst, lst, camd, o, cam, gp)
+                                                                 : eval_obs<2>(P, gps, kst, lst, camd, o, cam, gp);
         }
         const double s = block_sum<TILE_OBS>(rho0, red);
         if (tid == 0) P.chi_eval[tile] = s;
@@ -2057,6 +2117,19 @@ __device__ void prior_eval(const DevProblem& P, const double* __restrict__ kst, 
         const int v = idx - P.n_prior;
         const double ev = kst[(size_t)P.vel_kf[v] * KF_STRIDE + 9];
         P.chi_eval[P.n_tiles + idx] = ev * (P.qcinv[14] * ev);
+    } else if (idx < P.n_prior + P.n_vel + P.n_eprior) {   // EdgeExtrinsicPrior: e^T Om e
+        const int q = idx - P.n_prior - P.n_vel;
+        const double* ed = P.ep_data + 16 * (size_t)q;
+        const double* kx = kst + (size_t)P.ep_kf[q] * KF_STRIDE;
+        double e[3];
+        ext_prior_error_jac(Quat{kx[0], kx[1], kx[2], kx[3]}, Quat{ed[0], ed[1], ed[2], ed[3]}, e, nullptr);
+        double chi = 0.0;
+        for (int i = 0; i < 3; ++i) {
+            double s = 0.0;
+            for (int k = 0; k < 3; ++k) s += ed[4 + 3 * i + k] * e[k];
+            chi += e[i] * s;
+        }
+        P.chi_eval[P.n_tiles + idx] = chi;
     }
 }
 
@@ -2115,7 +2188,7 @@ __device__ void lm_decide(LMCtl& c, double chi_lin, double chi_trial, double sca
 template <int NT>
 __device__ void trial_sums(const DevProblem& P, double* red, double& sa, double& sb, double& sc) {
     const int tid = threadIdx.x;
-    const int nc = P.n_tiles + P.n_prior + P.n_vel;
+    const int nc = P.n_tiles + P.n_prior + P.n_vel + P.n_eprior;
     double a = 0.0, b = 0.0, c = 0.0;
     for (int i = tid; i < nc; i += NT) { a += P.chi_lin[i]; b += P.chi_eval[i]; }
     for (int i = tid; i < P.n_upd_blocks; i += NT) c += P.scale_part[i];
@@ -2236,7 +2309,7 @@ __global__ __launch_bounds__(256) void k_depth(DevProblem P, int sel, unsigned c
     const int meta = P.ob_meta[o];
     const int kind = meta & 15, cam = meta >> 4;
     CamD cd;
-    load_cam(P.camd + (size_t)cam * CAMD_STRIDE, &cd);
+    load_cam(P.camdb[state_idx(P, sel)] + (size_t)cam * CAMD_STRIDE, &cd);
     const double* Xw = lst + (size_t)P.ob_lm[o] * 3;
     int good = 1;
     const int ks[2] = {P.ob_kfb[o], kind <= LBA_STEREO_GP ? P.ob_kfa[o] : -1};
@@ -2268,7 +2341,7 @@ void launch_linearize(const DevProblem& P, int sel, int write_res, int gate, hip
         hipLaunchKernelGGL(k_linearize, dim3(P.n_tiles), dim3(TILE_OBS), 0, s, P, sel, write_res, gate);
 }
 void launch_prior_lin(const DevProblem& P, int sel, int gate, hipStream_t s) {
-    const int n = P.n_prior + P.n_vel + P.n_smp;
+    const int n = P.n_prior + P.n_vel + P.n_eprior + P.n_smp;
     if (n) hipLaunchKernelGGL(k_prior_lin, dim3(n), dim3(PRI_THREADS), 0, s, P, sel, gate);
 }
 void launch_schur(const DevProblem& P, double lambda, int gate, hipStream_t s) {
@@ -2316,7 +2389,7 @@ void launch_update(const DevProblem& P, double lambda, int sel, int gate, int ja
     hipLaunchKernelGGL(k_update, dim3(P.n_upd_blocks), dim3(UPD_THREADS), 0, s, P, lambda, sel, gate, jac);
 }
 void launch_eval(const DevProblem& P, int sel, int gate, unsigned long long seq, int mode, hipStream_t s) {
-    const int nb = P.n_tiles + cdiv(P.n_prior + P.n_vel, TILE_OBS);
+    const int nb = P.n_tiles + cdiv(P.n_prior + P.n_vel + P.n_eprior, TILE_OBS);
     if (nb) hipLaunchKernelGGL(k_eval, dim3(nb), dim3(TILE_OBS), 0, s, P, sel, gate);
     if (mode != FIN_NONE) launch_finalize(P, seq, mode, s);
 }

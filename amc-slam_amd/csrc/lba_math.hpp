@@ -359,6 +359,45 @@ LBA_HD void cam_derive(const Cam& c, CamD* d) {
     d->fx = c.fx; d->fy = c.fy; d->cx = c.cx; d->cy = c.cy;
 }
 
+// Camera record of a state (CAMD_STRIDE doubles): Rcb(9) tcb(3) fx fy cx cy, then the Jacobian factor of
+// the camera's extrinsic vertex stored like a sample's N (column c at 16 + 6 c, 12 columns, the last six
+// zero: the extrinsic occupies a 12-wide pose block whose second half is inert).  EdgeMonoGPExtrinsic's
+// _jacobianOplus[3] = -P [-I, Xc^] (src/G2oTypes.cc:311-313) equals J1 Ad(Tbc) with J1 = P Rcb [I, -Xb^]
+// the Jacobian w.r.t. the body pose sample: Rcb (tbc - Xb) = -Xc, so P Rcb [Rbc, (tbc - Xb)^ Rbc] = P [I, -Xc^].
+constexpr int CAMREC_DOUBLES = 16 + 72;
+LBA_HD void cam_record(const SE3& Tbc, double fx, double fy, double cx, double cy, double* o) {
+    const SE3 Tcb = se3_inv(Tbc);
+    qmat(Tcb.q, o);
+    o[9] = Tcb.t[0]; o[10] = Tcb.t[1]; o[11] = Tcb.t[2];
+    o[12] = fx; o[13] = fy; o[14] = cx; o[15] = cy;
+    double A[36];
+    se3_adj(Tbc, A);
+    for (int c = 0; c < 12; ++c)
+        for (int l = 0; l < 6; ++l) o[16 + 6 * c + l] = c < 6 ? A[l * 6 + c] : 0.0;
+}
+
+// EdgeExtrinsicPrior (include/G2oTypes.h:470-494): e = log(R_ Rbc) with R_ = Rbc_ini^-1 (qinv_ini, already
+// inverted and normalised as the edge's constructor does), Jacobian w.r.t. the rotation half of the
+// extrinsic's tangent: RightJacobianSO3(e)^-1 (src/G2oTypes.cc:575-591, Eigen 3x3 inverse); the
+// translation half is zero.
+LBA_HD void inv3(const double* m, double* r);
+LBA_HD void ext_prior_error_jac(const Quat& qbc, const Quat& qinv_ini, double* e, double* Jrot) {
+    double th;
+    so3_log(qmul(qinv_ini, qbc), e, &th);
+    if (!Jrot) return;
+    const double x = e[0], y = e[1], z = e[2];
+    const double d2 = x * x + y * y + z * z, d = sqrt(d2);
+    double Jr[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    if (!(d < 1e-5)) {
+        const double W[9] = {0.0, -z, y, z, 0.0, -x, -y, x, 0.0};
+        double WW[9];
+        mul33(W, W, WW);
+        const double a = 1.0 - cos(d), b = d - sin(d), d3 = d2 * d;
+        for (int i = 0; i < 9; ++i) Jr[i] = Jr[i] - W[i] * a / d2 + WW[i] * b / d3;
+    }
+    inv3(Jr, Jrot);
+}
+
 // GP pose sample: everything an observation at time t between (KF_a, KF_b) needs.  All observations
 // of one camera of one keyframe share t, so a window has O(pairs x cameras) samples for O(obs) GP
 // observations and the interpolation + Jacobian chain is evaluated once per sample.

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define LBA_ABI_VERSION 1
+#define LBA_ABI_VERSION 2
 
 /* status codes */
 #define LBA_OK              0
@@ -40,7 +40,7 @@ extern "C" {
 #define LBA_E_LIMIT        -6   /* problem exceeds a compiled limit (see lba_last_error) */
 
 /* observation kinds (the reprojection edges of include/G2oTypes.h) */
-#define LBA_MONO_GP    0   /* EdgeMonoGPExtrinsic / EdgeMonoGP: 2-d, vertices (kf_a=prev KF, kf_b=KF, lm), cam extrinsic fixed
+#define LBA_MONO_GP    0   /* EdgeMonoGPExtrinsic / EdgeMonoGP: 2-d, vertices (kf_a=prev KF, kf_b=KF, lm, the camera extrinsic: optimised when lba_cam.ext_free)
                               (include/G2oTypes.h:292-402, src/G2oTypes.cc:225-367) */
 #define LBA_STEREO_GP  1   /* EdgeStereoGP: 3-d [u, v, u_r] (include/G2oTypes.h:404-421, src/G2oTypes.cc:369-443) */
 #define LBA_MONO       2   /* EdgeMono: 2-d, vertices (kf_b, lm) at KF time (include/G2oTypes.h:423-446, src/G2oTypes.cc:445-468) */
@@ -108,6 +108,17 @@ typedef struct lba_cam {    /* GeometricCamera (Pinhole) + MultiKeyFrame::mTbc[c
     double q[4];            /* Tbc rotation (x,y,z,w) */
     double t[3];            /* Tbc translation */
     double fx, fy, cx, cy;  /* Pinhole::mvParameters (float values widened) */
+    /* extrinsic calibration (LocalGPBA bExtrinsic, src/Optimizer.cc:982-995,1228-1240): ext_free = 1
+     * makes this camera's VertexExtrinsic (include/G2oTypes.h:83-102, T <- T exp(d)) optimisable.  Its
+     * 6 dofs follow the keyframes' in the pose system (g2o id order: iniMPid + c + 1 > every KF id);
+     * the LBA_MONO_GP observations of the camera (EdgeMonoGPExtrinsic, src/G2oTypes.cc:241-314) link it,
+     * and an EdgeExtrinsicPrior (include/G2oTypes.h:470-494) e = log(Rbc_ini^-1 Rbc), information
+     * rbc_info, is attached to it.  0: fixed, as in every call without bExtrinsic (the prior is then
+     * inactive: all its vertices are fixed). */
+    int32_t ext_free;
+    int32_t pad;
+    double  rbc_ini[4];     /* MultiFrame::mRbc_ini[c] (x,y,z,w), float values widened (Frame.cc:181) */
+    double  rbc_info[9];    /* MultiFrame::mRbc_ini_cov[c] used as the information, row-major (0.2 I, Frame.cc:182) */
 } lba_cam;
 
 typedef struct lba_stats {
@@ -198,8 +209,11 @@ int lba_linearize(lba_problem* p, double* residuals, double* H_pp, double* b, do
 /* One damped solve at lambda on the last linearisation: dx [np + 3*n_lm] (poses then
  * landmarks), BlockSolver::solve with setLambda/restoreDiagonal (block_solver.hpp:354-486). */
 int lba_solve_step(lba_problem* p, double lambda, double* dx);
-/* Dimension of the pose system (12 * number of non-fixed KFs). */
+/* Dimension of the pose system (12 * number of non-fixed KFs + 6 * number of free extrinsics). */
 int lba_pose_dim(const lba_problem* p);
+/* Current camera extrinsics (write-back of the VertexExtrinsic estimates, src/Optimizer.cc:1419-1428):
+ * the cameras passed to lba_set_problem with Tbc (q, t) replaced by the estimate for free ones. */
+int lba_get_cams(lba_problem* p, lba_cam* cams_out);
 
 /* ---- tracking: Optimizer::PoseGPOptimizationFromeLastFrame (src/Optimizer.cc:369-686), SURVEY.md §8(f)3.
  * Per frame: vertices prev (pFrame->mpPrevFrame, fixed = the `fix` argument) and cur (pFrame), the map

@@ -408,7 +408,10 @@ static se3 gp_query_pose(const gp_t* gp, const se3* pose1, const se3* pose2, con
 }
 
 /* ------------------------------------------------------------------ Pinhole (Pinhole.cpp) */
-typedef struct { se3 Tbc; double fx, fy, cx, cy; } cam_t;
+/* the camera and its VertexExtrinsic (include/G2oTypes.h:83-102): Tbc is the vertex estimate; ext_free
+ * marks it optimisable (bExtrinsic, src/Optimizer.cc:1228-1240), with its EdgeExtrinsicPrior
+ * R_ = mRbc_ini^-1 and information (include/G2oTypes.h:470-494, src/Optimizer.cc:990-993) */
+typedef struct { se3 Tbc; double fx, fy, cx, cy; int ext_free, hidx; quat Rini_inv; double info[9]; } cam_t;
 
 static void pin_project(const cam_t* c, const double* X, double* uv) {   /* :35-41 */
     uv[0] = c->fx * X[0] / X[2] + c->cx;
@@ -434,10 +437,14 @@ struct orc_problem {
     lba_prior* pri;
     int* vel;
     cam_t* cam;
-    /* index mapping (SparseOptimizer::buildIndexMapping, sparse_optimizer.cpp:166-190) */
+    se3* cam_bak;      /* extrinsic estimates, push/pop */
+    /* index mapping (SparseOptimizer::buildIndexMapping, sparse_optimizer.cpp:166-190): keyframe blocks
+     * (12 wide) then free extrinsics (6 wide, VertexExtrinsic ids iniMPid + c + 1 follow every KF id) */
+    int* poff;         /* per pose block: offset in the pose system */
+    int* pdim;         /* per pose block: 12 or 6 */
     int* kf_hidx;      /* pose block index or -1 */
     int* lm_hidx;      /* landmark block index or -1 */
-    int np, nl;        /* pose dim (12*#pose blocks), landmark dim (3*#lm blocks) */
+    int np, nl;        /* pose dim (12 * #KF blocks + 6 * #free extrinsics), landmark dim (3*#lm blocks) */
     int n_pose_blocks, n_lm_blocks;
     /* per-edge errors */
     double* obs_err;   /* [n_obs*3] */
@@ -448,7 +455,7 @@ struct orc_problem {
     double* Hll;       /* [n_lm_blocks*9] */
     int* hpl_start;    /* per landmark block: range into hpl_pose/hpl_blk */
     int* hpl_pose;     /* pose block index, ascending within a landmark */
-    double* hpl_blk;   /* 12x3 blocks */
+    double* hpl_blk;   /* 12x3 blocks (an extrinsic's block uses its first 6 rows) */
     double* b;         /* [np + nl] */
     double* x;         /* [np + nl], persistent like BlockSolver::_x */
     double* diag_bak;  /* setLambda backup */
@@ -523,12 +530,14 @@ static void obs_error(const orc_problem* p, const lba_obs* o, double* e) {
 }
 
 /* linearizeOplus of the reprojection edges (src/G2oTypes.cc:258-314,316-367,389-443,445-495).
- * J is [dim x 27]: cols 0-11 KF_a, 12-23 KF_b, 24-26 point. */
+ * J is [dim x JC]: cols 0-11 KF_a, 12-23 KF_b, 24-26 point, 27-32 the camera extrinsic
+ * (EdgeMonoGPExtrinsic's _jacobianOplus[3] = -proj_jac [-I, Skew(Xc)], src/G2oTypes.cc:310-313). */
+#define JC 33
 static void obs_jacobian(const orc_problem* p, const lba_obs* o, double* J) {
     const cam_t* c = &p->cam[o->cam];
     const double* Xw = p->lm + 3 * o->lm;
     int dim = obs_dim(o->kind);
-    memset(J, 0, sizeof(double) * dim * 27);
+    memset(J, 0, sizeof(double) * dim * JC);
     se3 Tcb = se3_inv(&c->Tbc);
     double Rcb[9], Rwb[9], Rbw[9], Xb[3], Xc[3], pj[6], proj[9];
     if (is_gp(o->kind)) {
@@ -589,24 +598,33 @@ static void obs_jacobian(const orc_problem* p, const lba_obs* o, double* J) {
         mat_mul(JPJ, JP, JinT1, 6, 12, 6);
         for (int i = 0; i < 36; ++i) JPJ[i] += AddT[i];
         mat_mul(blk, J1, JPJ, dim, 6, 6);
-        set_block(J, 27, 0, 0, blk, dim, 6);
+        set_block(J, JC, 0, 0, blk, dim, 6);
         mat_mul(J1Jr, J1, Jr_dxi, dim, 6, 6);
         mat_mul(J1JrA, J1Jr, At1, dim, 6, 12);
         mat_mul(blk, J1JrA, JinV1, dim, 12, 6);
-        set_block(J, 27, 0, 6, blk, dim, 6);
+        set_block(J, JC, 0, 6, blk, dim, 6);
         /* Jj1 = J1 Jr_dxi Pt1; _jacobianOplus[1] = [Jj1 JinT2 | Jj1 JinV2] */
         double Jj1[36];
         mat_mul(Jj1, J1Jr, Pt1, dim, 6, 12);
         mat_mul(blk, Jj1, JinT2, dim, 12, 6);
-        set_block(J, 27, 0, 12, blk, dim, 6);
+        set_block(J, JC, 0, 12, blk, dim, 6);
         mat_mul(blk, Jj1, JinV2, dim, 12, 6);
-        set_block(J, 27, 0, 18, blk, dim, 6);
+        set_block(J, JC, 0, 18, blk, dim, 6);
         /* _jacobianOplus[2] = -proj_jac Rcb Rbw */
         double PR[9], PRR[9];
         mat_mul(PR, proj, Rcb, dim, 3, 3);
         mat_mul(PRR, PR, Rbw, dim, 3, 3);
         mat_scale(PRR, -1.0, dim * 3);
-        set_block(J, 27, 0, 24, PRR, dim, 3);
+        set_block(J, JC, 0, 24, PRR, dim, 3);
+        if (o->kind == LBA_MONO_GP) {   /* SE3deriv2 = [-I, Skew(Xc)]; J_ext = -proj_jac SE3deriv2 */
+            double S2[18], SXc[9], PE[18];
+            hat3(SXc, Xc);
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) { S2[i * 6 + j] = (i == j) ? -1.0 : 0.0; S2[i * 6 + 3 + j] = SXc[i * 3 + j]; }
+            mat_mul(PE, proj, S2, dim, 3, 6);
+            mat_scale(PE, -1.0, dim * 6);
+            set_block(J, JC, 0, 27, PE, dim, 6);
+        }
     } else {
         const kf_t* f = &p->kf[o->kf_b];
         so3_matrix(&f->Twb.q, Rwb);
@@ -628,12 +646,12 @@ static void obs_jacobian(const orc_problem* p, const lba_obs* o, double* J) {
             for (int j = 0; j < 3; ++j) { S[i * 6 + j] = -Rcb[i * 3 + j]; S[i * 6 + 3 + j] = RS[i * 3 + j]; }
         mat_mul(blk, proj, S, dim, 3, 6);
         mat_scale(blk, -1.0, dim * 6);
-        set_block(J, 27, 0, 12, blk, dim, 6);   /* velocity columns stay zero */
+        set_block(J, JC, 0, 12, blk, dim, 6);   /* velocity columns stay zero */
         double PR[9], PRR[9];
         mat_mul(PR, proj, Rcb, dim, 3, 3);
         mat_mul(PRR, PR, Rbw, dim, 3, 3);
         mat_scale(PRR, -1.0, dim * 3);
-        set_block(J, 27, 0, 24, PRR, dim, 3);
+        set_block(J, JC, 0, 24, PRR, dim, 3);
     }
 }
 
@@ -679,6 +697,28 @@ static void prior_jacobian(const orc_problem* p, const lba_prior* e, double* Ji,
     set_block(Jj, 12, 6, 6, Jri, 6, 6);
 }
 
+/* EdgeExtrinsicPrior (include/G2oTypes.h:479-491): e = (R_ * T.so3()).log(); Jacobian block (0, 3) =
+ * RightJacobianSO3(e).inverse() (src/G2oTypes.cc:575-591; Eigen's 3x3 inverse), block (0, 0) zero */
+static void ext_prior_error(const cam_t* c, double* e) {
+    quat q = so3_mul(c->Rini_inv, c->Tbc.q);
+    double th;
+    so3_log_theta(&q, e, &th);
+}
+static void ext_prior_jacobian(const double* e, double* J /* 3 x 6 */) {
+    const double x = e[0], y = e[1], z = e[2];
+    const double d2 = x * x + y * y + z * z, d = sqrt(d2);
+    double Jr[9], W[9] = {0.0, -z, y, z, 0.0, -x, -y, x, 0.0}, WW[9], Ji[9];
+    mat_eye(Jr, 3);
+    if (!(d < 1e-5)) {
+        mat_mul(WW, W, W, 3, 3, 3);
+        for (int i = 0; i < 9; ++i) Jr[i] = Jr[i] - W[i] * (1.0 - cos(d)) / d2 + WW[i] * (d - sin(d)) / (d2 * d);
+    }
+    inverse3(Ji, Jr);
+    memset(J, 0, sizeof(double) * 18);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) J[i * 6 + 3 + j] = Ji[i * 3 + j];
+}
+
 /* ------------------------------------------------------------------ construction */
 orc_problem* orc_create(const lba_config* cfg, const lba_kf* kfs, int n_kf, const double* lm_xyz, int n_lm,
                         const lba_obs* obs, int n_obs, const lba_prior* priors, int n_priors,
@@ -707,10 +747,17 @@ orc_problem* orc_create(const lba_config* cfg, const lba_kf* kfs, int n_kf, cons
     p->vel = (int*)malloc(sizeof(int) * (n_vel > 0 ? n_vel : 1));
     memcpy(p->vel, vel_kfs, sizeof(int) * n_vel);
     p->cam = (cam_t*)malloc(sizeof(cam_t) * (n_cam > 0 ? n_cam : 1));
+    p->cam_bak = (se3*)malloc(sizeof(se3) * (n_cam > 0 ? n_cam : 1));
     for (int c = 0; c < n_cam; ++c) {
         p->cam[c].Tbc = mk_se3(cams[c].q, cams[c].t);
         p->cam[c].fx = cams[c].fx; p->cam[c].fy = cams[c].fy;
         p->cam[c].cx = cams[c].cx; p->cam[c].cy = cams[c].cy;
+        p->cam[c].ext_free = cams[c].ext_free != 0;
+        p->cam[c].hidx = -1;
+        /* EdgeExtrinsicPrior(mRbc_ini[c].cast<double>()): R_(R.inverse()) */
+        quat ri = {cams[c].rbc_ini[0], cams[c].rbc_ini[1], cams[c].rbc_ini[2], cams[c].rbc_ini[3]};
+        p->cam[c].Rini_inv = so3_inv(q_normalized(ri));
+        memcpy(p->cam[c].info, cams[c].rbc_info, sizeof(double) * 9);
     }
     /* active vertices: touched by at least one edge that is not all-fixed
      * (SparseOptimizer::initializeOptimization, sparse_optimizer.cpp:197-267) */
@@ -730,11 +777,20 @@ orc_problem* orc_create(const lba_config* cfg, const lba_kf* kfs, int n_kf, cons
     int np = 0, nl = 0;
     for (int i = 0; i < n_kf; ++i) p->kf_hidx[i] = (kf_act[i] && !kfs[i].fixed) ? np++ : -1;
     for (int i = 0; i < n_lm; ++i) p->lm_hidx[i] = lm_act[i] ? nl++ : -1;
+    const int npk = np;
+    for (int c = 0; c < n_cam; ++c)   /* a free extrinsic is active through its prior edge */
+        if (p->cam[c].ext_free) p->cam[c].hidx = np++;
     free(kf_act);
     free(lm_act);
     p->n_pose_blocks = np;
     p->n_lm_blocks = nl;
-    p->np = 12 * np;
+    p->poff = (int*)malloc(sizeof(int) * (np > 0 ? np : 1));
+    p->pdim = (int*)malloc(sizeof(int) * (np > 0 ? np : 1));
+    for (int h = 0; h < np; ++h) {
+        p->poff[h] = h < npk ? 12 * h : 12 * npk + 6 * (h - npk);
+        p->pdim[h] = h < npk ? 12 : 6;
+    }
+    p->np = 12 * npk + 6 * (np - npk);
     p->nl = 3 * nl;
     p->obs_err = (double*)calloc(3 * (n_obs > 0 ? n_obs : 1), sizeof(double));
     p->pri_err = (double*)calloc(12 * (n_priors > 0 ? n_priors : 1), sizeof(double));
@@ -748,9 +804,10 @@ orc_problem* orc_create(const lba_config* cfg, const lba_kf* kfs, int n_kf, cons
     for (int i = 0; i < n_obs; ++i) {
         int l = p->lm_hidx[obs[i].lm];
         int ks[2] = {obs[i].kf_b, is_gp(obs[i].kind) ? obs[i].kf_a : -1};
-        for (int s = 0; s < 2; ++s) {
-            if (ks[s] < 0) continue;
-            int h = p->kf_hidx[ks[s]];
+        for (int s = 0; s < 3; ++s) {
+            int h;
+            if (s == 2) h = obs[i].kind == LBA_MONO_GP ? p->cam[obs[i].cam].hidx : -1;
+            else h = ks[s] < 0 ? -1 : p->kf_hidx[ks[s]];
             if (h < 0) continue;
             if (!seen[(size_t)h * nl + l]) { seen[(size_t)h * nl + l] = 1; cnt_pairs[l]++; }
         }
@@ -777,7 +834,7 @@ orc_problem* orc_create(const lba_config* cfg, const lba_kf* kfs, int n_kf, cons
 void orc_destroy(orc_problem* p) {
     if (!p) return;
     free(p->kf); free(p->kf_bak); free(p->lm); free(p->lm_bak); free(p->obs); free(p->pri); free(p->vel);
-    free(p->cam); free(p->kf_hidx); free(p->lm_hidx); free(p->obs_err); free(p->pri_err); free(p->vel_err);
+    free(p->cam); free(p->cam_bak); free(p->poff); free(p->pdim); free(p->kf_hidx); free(p->lm_hidx); free(p->obs_err); free(p->pri_err); free(p->vel_err);
     free(p->Hpp); free(p->Hll); free(p->hpl_start); free(p->hpl_pose); free(p->hpl_blk); free(p->b); free(p->x);
     free(p->diag_bak);
     free(p);
@@ -821,6 +878,13 @@ static double compute_errors(orc_problem* p) {
         if (p->cfg.huber_prior > 0) { huber(c, p->cfg.huber_prior, rho); chi += rho[0]; }
         else chi += c;
     }
+    for (int c = 0; c < p->n_cam; ++c) {   /* EdgeExtrinsicPrior: active when its vertex is free */
+        if (!p->cam[c].ext_free) continue;
+        double e[3], Oe[3];
+        ext_prior_error(&p->cam[c], e);
+        mat_mul(Oe, p->cam[c].info, e, 3, 3, 1);
+        chi += e[0] * Oe[0] + e[1] * Oe[1] + e[2] * Oe[2];
+    }
     for (int i = 0; i < p->n_obs; ++i) {
         const lba_obs* o = &p->obs[i];
         double* e = p->obs_err + 3 * i;
@@ -842,15 +906,16 @@ double orc_compute_errors(orc_problem* p, double* residuals, double* obs_chi2) {
 }
 
 /* ------------------------------------------------------------------ buildSystem */
-/* add an (i,j) pose-pose block contribution into the upper triangle of dense Hpp */
-static void hpp_add(orc_problem* p, int hi, int hj, const double* blk /*12x12, rows i cols j*/) {
-    int n = p->np;
+/* add an (i,j) pose-pose block contribution (pdim[i] x pdim[j], row-major) into the upper triangle of
+ * dense Hpp */
+static void hpp_add(orc_problem* p, int hi, int hj, const double* blk) {
+    const int n = p->np, di = p->pdim[hi], dj = p->pdim[hj], oi = p->poff[hi], oj = p->poff[hj];
     if (hi <= hj) {
-        for (int r = 0; r < 12; ++r)
-            for (int c = 0; c < 12; ++c) p->Hpp[(size_t)(12 * hi + r) * n + 12 * hj + c] += blk[r * 12 + c];
+        for (int r = 0; r < di; ++r)
+            for (int c = 0; c < dj; ++c) p->Hpp[(size_t)(oi + r) * n + oj + c] += blk[r * dj + c];
     } else {   /* transposed block (hessianRowMajor) */
-        for (int r = 0; r < 12; ++r)
-            for (int c = 0; c < 12; ++c) p->Hpp[(size_t)(12 * hj + c) * n + 12 * hi + r] += blk[r * 12 + c];
+        for (int r = 0; r < di; ++r)
+            for (int c = 0; c < dj; ++c) p->Hpp[(size_t)(oj + c) * n + oi + r] += blk[r * dj + c];
     }
 }
 static double* hpl_block(orc_problem* p, int hp, int hl) {
@@ -874,8 +939,8 @@ static void build_system(orc_problem* p) {
         double om = p->gp.QcInv[2 * 6 + 2];
         double e = p->vel_err[i];
         /* J = [0_{1x6}, A], A = e_2 -> only column 8 */
-        p->b[12 * h + 8] -= om * e;
-        p->Hpp[(size_t)(12 * h + 8) * n + 12 * h + 8] += om;
+        p->b[p->poff[h] + 8] -= om * e;
+        p->Hpp[(size_t)(p->poff[h] + 8) * n + p->poff[h] + 8] += om;
     }
     for (int i = 0; i < p->n_prior; ++i) {   /* BaseBinaryEdge::constructQuadraticForm (base_binary_edge.hpp:54-120) */
         const lba_prior* e = &p->pri[i];
@@ -897,7 +962,7 @@ static void build_system(orc_problem* p) {
         if (!p->kf[e->kf_a].fixed && hi >= 0) {
             mat_tr(AT, Ji, 12, 12);
             mat_mul(g, AT, r, 12, 12, 1);
-            for (int k = 0; k < 12; ++k) p->b[12 * hi + k] += g[k];
+            for (int k = 0; k < 12; ++k) p->b[p->poff[hi] + k] += g[k];
             mat_mul(AtW, AT, W, 12, 12, 12);
             mat_mul(blk, AtW, Ji, 12, 12, 12);
             hpp_add(p, hi, hi, blk);
@@ -909,69 +974,90 @@ static void build_system(orc_problem* p) {
         if (!p->kf[e->kf_b].fixed && hj >= 0) {
             mat_tr(AT, Jj, 12, 12);
             mat_mul(g, AT, r, 12, 12, 1);
-            for (int k = 0; k < 12; ++k) p->b[12 * hj + k] += g[k];
+            for (int k = 0; k < 12; ++k) p->b[p->poff[hj] + k] += g[k];
             mat_mul(AtW, AT, W, 12, 12, 12);
             mat_mul(blk, AtW, Jj, 12, 12, 12);
             hpp_add(p, hj, hj, blk);
         }
     }
+    for (int c = 0; c < p->n_cam; ++c) {   /* EdgeExtrinsicPrior (BaseUnaryEdge, base_unary_edge.hpp:42-72) */
+        const cam_t* cm = &p->cam[c];
+        if (!cm->ext_free) continue;
+        double e[3], J[18], JT[18], JtO[18], blk[36], Oe[3], g[6];
+        ext_prior_error(cm, e);
+        ext_prior_jacobian(e, J);
+        mat_tr(JT, J, 3, 6);
+        mat_mul(JtO, JT, cm->info, 6, 3, 3);
+        mat_mul(blk, JtO, J, 6, 3, 6);
+        hpp_add(p, cm->hidx, cm->hidx, blk);
+        mat_mul(Oe, cm->info, e, 3, 3, 1);
+        mat_mul(g, JT, Oe, 6, 3, 1);
+        for (int k = 0; k < 6; ++k) p->b[p->poff[cm->hidx] + k] -= g[k];
+    }
     for (int i = 0; i < p->n_obs; ++i) {
         const lba_obs* o = &p->obs[i];
         int dim = obs_dim(o->kind);
         const double* e = p->obs_err + 3 * i;
-        double J[81];
+        double J[3 * JC];
         obs_jacobian(p, o, J);
         huber(chi2_of(e, dim, o->w), obs_delta(p, o->kind), rho);
         double s = rho[1] * o->w;                    /* robustInformation = rho' * Omega */
         double om_r[3];
         for (int d = 0; d < dim; ++d) om_r[d] = -(o->w * e[d]) * rho[1];
         int hl = p->lm_hidx[o->lm];
-        /* vertices in edge order: GP edges (KF_a, KF_b, pt), binary edges (KF_b, pt) */
-        int vk[3], vc[3], vd[3], nv = 0;
+        /* vertices in edge order: GP edges (KF_a, KF_b, pt[, extrinsic]), binary edges (KF_b, pt);
+         * vk: KF index, -1 the point, -2 - c the extrinsic of camera c */
+        int vk[4], vc[4], vd[4], nv = 0;
         if (is_gp(o->kind)) { vk[nv] = o->kf_a; vc[nv] = 0; vd[nv++] = 12; }
         vk[nv] = o->kf_b; vc[nv] = 12; vd[nv++] = 12;
         vk[nv] = -1; vc[nv] = 24; vd[nv++] = 3;
+        if (o->kind == LBA_MONO_GP) { vk[nv] = -2 - o->cam; vc[nv] = 27; vd[nv++] = 6; }
+#define VHIDX(v) ((v) >= 0 ? (p->kf[v].fixed ? -1 : p->kf_hidx[v]) : ((v) == -1 ? hl : p->cam[-2 - (v)].hidx))
         for (int a = 0; a < nv; ++a) {
-            int ha = vk[a] >= 0 ? (p->kf[vk[a]].fixed ? -1 : p->kf_hidx[vk[a]]) : hl;
+            int ha = VHIDX(vk[a]);
             if (ha < 0) continue;
             int da = vd[a];
             double AtO[36], gb[12];   /* AtO = A^T (s I) : [da x dim] */
             for (int r = 0; r < da; ++r)
-                for (int d = 0; d < dim; ++d) AtO[r * dim + d] = J[d * 27 + vc[a] + r] * s;
+                for (int d = 0; d < dim; ++d) AtO[r * dim + d] = J[d * JC + vc[a] + r] * s;
             for (int r = 0; r < da; ++r) {
                 double acc = 0.0;
-                for (int d = 0; d < dim; ++d) acc += J[d * 27 + vc[a] + r] * om_r[d];
+                for (int d = 0; d < dim; ++d) acc += J[d * JC + vc[a] + r] * om_r[d];
                 gb[r] = acc;
             }
             double blk[144];
             for (int r = 0; r < da; ++r)
                 for (int c = 0; c < da; ++c) {
                     double acc = 0.0;
-                    for (int d = 0; d < dim; ++d) acc += AtO[r * dim + d] * J[d * 27 + vc[a] + c];
+                    for (int d = 0; d < dim; ++d) acc += AtO[r * dim + d] * J[d * JC + vc[a] + c];
                     blk[r * da + c] = acc;
                 }
-            if (vk[a] >= 0) {
-                for (int r = 0; r < 12; ++r) p->b[12 * ha + r] += gb[r];
+            if (vk[a] != -1) {
+                for (int r = 0; r < da; ++r) p->b[p->poff[ha] + r] += gb[r];
                 hpp_add(p, ha, ha, blk);
             } else {
                 for (int r = 0; r < 3; ++r) p->b[p->np + 3 * ha + r] += gb[r];
                 for (int r = 0; r < 9; ++r) p->Hll[9 * ha + r] += blk[r];
             }
             for (int c2 = a + 1; c2 < nv; ++c2) {
-                int hb = vk[c2] >= 0 ? (p->kf[vk[c2]].fixed ? -1 : p->kf_hidx[vk[c2]]) : hl;
+                int hb = VHIDX(vk[c2]);
                 if (hb < 0) continue;
                 int db = vd[c2];
                 double ob[144];
                 for (int r = 0; r < da; ++r)
                     for (int c = 0; c < db; ++c) {
                         double acc = 0.0;
-                        for (int d = 0; d < dim; ++d) acc += AtO[r * dim + d] * J[d * 27 + vc[c2] + c];
+                        for (int d = 0; d < dim; ++d) acc += AtO[r * dim + d] * J[d * JC + vc[c2] + c];
                         ob[r * db + c] = acc;
                     }
-                if (vk[c2] >= 0) hpp_add(p, ha, hb, ob);
-                else {
+                if (vk[a] != -1 && vk[c2] != -1) hpp_add(p, ha, hb, ob);
+                else if (vk[c2] == -1) {   /* (pose, point): Hpl */
                     double* B = hpl_block(p, ha, hl);
-                    for (int r = 0; r < 36; ++r) B[r] += ob[r];
+                    for (int r = 0; r < da * 3; ++r) B[r] += ob[r];
+                } else {   /* (point, extrinsic): stored as the extrinsic's Hpl block (pose index first) */
+                    double* B = hpl_block(p, hb, hl);
+                    for (int r = 0; r < db; ++r)
+                        for (int c = 0; c < 3; ++c) B[r * 3 + c] += ob[c * db + r];
                 }
             }
         }
@@ -1095,18 +1181,19 @@ static int block_solve(orc_problem* p) {
         for (int k1 = p->hpl_start[l]; k1 < p->hpl_start[l + 1]; ++k1) {
             int i1 = p->hpl_pose[k1];
             const double* Bi = p->hpl_blk + 36 * k1;
+            const int d1 = p->pdim[i1], o1 = p->poff[i1];
             double BD[36], Bb[12];
-            mat_mul(BD, Bi, Di, 12, 3, 3);
-            mat_mul(Bb, Bi, db, 12, 3, 1);
-            for (int r = 0; r < 12; ++r) coeff[12 * i1 + r] += Bb[r];
+            mat_mul(BD, Bi, Di, d1, 3, 3);
+            mat_mul(Bb, Bi, db, d1, 3, 1);
+            for (int r = 0; r < d1; ++r) coeff[o1 + r] += Bb[r];
             for (int k2 = k1; k2 < p->hpl_start[l + 1]; ++k2) {
                 int i2 = p->hpl_pose[k2];
                 const double* Bj = p->hpl_blk + 36 * k2;
-                for (int r = 0; r < 12; ++r)
-                    for (int c = 0; c < 12; ++c) {
+                for (int r = 0; r < d1; ++r)
+                    for (int c = 0; c < p->pdim[i2]; ++c) {
                         double acc = 0.0;
                         for (int a = 0; a < 3; ++a) acc += BD[r * 3 + a] * Bj[c * 3 + a];
-                        S[(size_t)(12 * i1 + r) * n + 12 * i2 + c] -= acc;
+                        S[(size_t)(o1 + r) * n + p->poff[i2] + c] -= acc;
                     }
             }
         }
@@ -1127,7 +1214,7 @@ static int block_solve(orc_problem* p) {
                 const double* B = p->hpl_blk + 36 * k;
                 for (int d = 0; d < 3; ++d) {
                     double acc = 0.0;
-                    for (int r = 0; r < 12; ++r) acc += B[r * 3 + d] * (-p->x[12 * i1 + r]);
+                    for (int r = 0; r < p->pdim[i1]; ++r) acc += B[r * 3 + d] * (-p->x[p->poff[i1] + r]);
                     cl[d] += acc;
                 }
             }
@@ -1168,10 +1255,10 @@ void orc_normal_residual(const orc_problem* p, double lambda, const double* dx, 
         for (int k = p->hpl_start[l]; k < p->hpl_start[l + 1]; ++k) {
             const int i1 = p->hpl_pose[k];
             const double* B = p->hpl_blk + 36 * k;
-            for (int a = 0; a < 12; ++a)
+            for (int a = 0; a < p->pdim[i1]; ++a)
                 for (int d = 0; d < 3; ++d) {
-                    r[12 * i1 + a] += B[a * 3 + d] * xl[d];
-                    rl[d] += B[a * 3 + d] * dx[12 * i1 + a];
+                    r[p->poff[i1] + a] += B[a * 3 + d] * xl[d];
+                    rl[d] += B[a * 3 + d] * dx[p->poff[i1] + a];
                 }
         }
     }
@@ -1181,10 +1268,12 @@ void orc_normal_residual(const orc_problem* p, double lambda, const double* dx, 
 static void push_state(orc_problem* p) {
     memcpy(p->kf_bak, p->kf, sizeof(kf_t) * p->n_kf);
     memcpy(p->lm_bak, p->lm, sizeof(double) * 3 * p->n_lm);
+    for (int c = 0; c < p->n_cam; ++c) p->cam_bak[c] = p->cam[c].Tbc;
 }
 static void pop_state(orc_problem* p) {
     memcpy(p->kf, p->kf_bak, sizeof(kf_t) * p->n_kf);
     memcpy(p->lm, p->lm_bak, sizeof(double) * 3 * p->n_lm);
+    for (int c = 0; c < p->n_cam; ++c) p->cam[c].Tbc = p->cam_bak[c];
 }
 /* SparseOptimizer::update (sparse_optimizer.cpp:422-435), VertexPoseVel::oplusImpl
  * (PoseVelocity::Update src/G2oTypes.cc:41-46), VertexSBAPointXYZ::oplusImpl */
@@ -1192,9 +1281,14 @@ static void apply_update(orc_problem* p, const double* x) {
     for (int k = 0; k < p->n_kf; ++k) {
         int h = p->kf_hidx[k];
         if (h < 0) continue;
-        se3 d = se3_exp(x + 12 * h);
+        se3 d = se3_exp(x + p->poff[h]);
         p->kf[k].Twb = se3_mul(&p->kf[k].Twb, &d);
-        for (int i = 0; i < 6; ++i) p->kf[k].vel[i] += x[12 * h + 6 + i];
+        for (int i = 0; i < 6; ++i) p->kf[k].vel[i] += x[p->poff[h] + 6 + i];
+    }
+    for (int c = 0; c < p->n_cam; ++c) {   /* VertexExtrinsic::oplusImpl: T <- T exp(d) (include/G2oTypes.h:97-99) */
+        if (p->cam[c].hidx < 0) continue;
+        se3 d = se3_exp(x + p->poff[p->cam[c].hidx]);
+        p->cam[c].Tbc = se3_mul(&p->cam[c].Tbc, &d);
     }
     for (int l = 0; l < p->n_lm; ++l) {
         int h = p->lm_hidx[l];
@@ -1297,6 +1391,14 @@ void orc_get_state(const orc_problem* p, lba_kf* kfs, double* lm_xyz) {
     if (lm_xyz) memcpy(lm_xyz, p->lm, sizeof(double) * 3 * p->n_lm);
 }
 
+void orc_get_cams(const orc_problem* p, lba_cam* cams) {   /* cams holds the set-up cameras; Tbc updated */
+    for (int c = 0; c < p->n_cam; ++c) {
+        const se3* T = &p->cam[c].Tbc;
+        cams[c].q[0] = T->q.x; cams[c].q[1] = T->q.y; cams[c].q[2] = T->q.z; cams[c].q[3] = T->q.w;
+        memcpy(cams[c].t, T->t, sizeof(double) * 3);
+    }
+}
+
 /* isDepthPositive (src/G2oTypes.cc:65-81; GP edges test both KF poses, include/G2oTypes.h:305-314) */
 void orc_depth_ok(const orc_problem* p, unsigned char* ok) {
     for (int i = 0; i < p->n_obs; ++i) {
@@ -1321,7 +1423,11 @@ int orc_obs_linearize(orc_problem* p, int i, double* err, double* J) {
     double e[3];
     obs_error(p, o, e);
     if (err) memcpy(err, e, sizeof(e));
-    if (J) obs_jacobian(p, o, J);
+    if (J) {   /* the public layout keeps the 27 vertex columns (KF_a, KF_b, point) */
+        double Jf[3 * JC];
+        obs_jacobian(p, o, Jf);
+        for (int d = 0; d < obs_dim(o->kind); ++d) memcpy(J + 27 * d, Jf + JC * d, sizeof(double) * 27);
+    }
     return obs_dim(o->kind);
 }
 int orc_prior_linearize(orc_problem* p, int i, double* err, double* Ji, double* Jj) {
@@ -1426,17 +1532,17 @@ static void trk_build(trk_t* T, double* H, double* b) {
         if (T->level[i]) continue;
         const lba_obs* o = &p->obs[i];
         int dim = obs_dim(o->kind);
-        double e[3], J[81];
+        double e[3], J[3 * JC];
         obs_error(p, o, e);
         obs_jacobian(p, o, J);
         double c = chi2_of(e, dim, o->w), s = o->w;
         if (T->robust) { huber(c, obs_delta(p, o->kind), rho); s *= rho[1]; }
         for (int r = 0; r < dim; ++r)
             for (int a = 0; a < 24; ++a) {
-                double ja = J[r * 27 + a];
+                double ja = J[r * JC + a];
                 if (ja == 0.0) continue;
                 b[a] -= ja * s * e[r];
-                for (int c2 = 0; c2 < 24; ++c2) H[a * 24 + c2] += ja * s * J[r * 27 + c2];
+                for (int c2 = 0; c2 < 24; ++c2) H[a * 24 + c2] += ja * s * J[r * JC + c2];
             }
     }
     {   /* EdgeGaussianPrior(prev, cur), info QiInv(dt) */

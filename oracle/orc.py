@@ -47,6 +47,7 @@ def lib():
         L.orc_normal_residual.restype = None
         L.orc_optimize.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(LbaStats)]
         L.orc_get_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _dp]
+        L.orc_get_cams.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.orc_depth_ok.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.orc_obs_linearize.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp]
         L.orc_prior_linearize.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp, _dp]
@@ -124,6 +125,11 @@ class Oracle:
         st = LbaStats()
         n = lib().orc_optimize(self.h, iters, ctypes.byref(st))
         return n, st
+
+    def cams(self):
+        c = np.array(self.win.cams, copy=True)
+        lib().orc_get_cams(self.h, ptr(c))
+        return c
 
     def state(self):
         from amc_lba.abi import KF_DTYPE
