@@ -27,7 +27,7 @@ HEADER_DTYPE = np.dtype([
     ("qc", "<f8", (36,)), ("inv_level_sigma2", "<f4", (MAX_LEVEL,)), ("scale_factor", "<f4", (MAX_LEVEL,)),
 ], align=True)
 MCAM_DTYPE = np.dtype([("q", "<f4", (4,)), ("t", "<f4", (3,)), ("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"),
-                       ("cy", "<f4"), ("pad", "<f4")], align=True)
+                       ("cy", "<f4"), ("rbc_ini", "<f4", (4,)), ("pad", "<f4")], align=True)
 MKF_DTYPE = np.dtype([
     ("id", "<i8"), ("prev_id", "<i8"), ("next_id", "<i8"), ("time", "<f8"), ("cam_time", "<f8", (MAX_CAM,)),
     ("q", "<f4", (4,)), ("t", "<f4", (3,)), ("vel", "<f4", (6,)), ("bf", "<f4"), ("bad", "<i4"), ("map_id", "<i4"),
@@ -46,7 +46,7 @@ GPOBS_DTYPE = np.dtype([("kf_id", "<i8"), ("time", "<f8"), ("cam", "<i4"), ("x",
                         ("octave", "<i4"), ("ur", "<f4"), ("pad", "<i4")], align=True)
 
 assert HEADER_DTYPE.itemsize == 464
-assert MCAM_DTYPE.itemsize == 48
+assert MCAM_DTYPE.itemsize == 64
 assert MKF_DTYPE.itemsize == 408
 assert KP_DTYPE.itemsize == 32
 assert MP_DTYPE.itemsize == 104
@@ -83,7 +83,7 @@ def _pad8(n):
 def pack(s):
     h = np.zeros(1, HEADER_DTYPE)
     h["magic"] = b"AMCSNAP"
-    h["version"] = 1
+    h["version"] = 2
     h["n_cam"] = s.n_cam
     for name, _, cnt in SECTIONS:
         if cnt != "n_cam":
@@ -307,6 +307,7 @@ def make_map(n_kf=30, n_lm=3000, obs_per_lm=6, n_cam=4, n_gp_frames=1, gp_obs_fr
     mcams = np.zeros(n_cam, MCAM_DTYPE)
     mcams["q"] = cams["q"].astype(F32)
     mcams["t"] = cams["t"].astype(F32)
+    mcams["rbc_ini"] = cams["q"].astype(F32)      # mRbc_ini = the initial mTbc rotation (Frame.cc:181)
     for f in ("fx", "fy", "cx", "cy"):
         mcams[f] = cams[f].astype(F32)
     levels = 8

@@ -59,16 +59,6 @@ int lbamap_local_gpba(lbamap* m, int64_t kf_id, volatile const int32_t* stop_fla
         m->err = "unknown keyframe id";
         return LBA_E_ARG;
     }
-    if (opt->extrinsic) {
-        // the second pass with free extrinsics (Optimizer.cc:1229-1240) needs extrinsic columns in
-        // the pose system; not built yet
-        m->err = "extrinsic calibration pass not supported";
-        if (out) {
-            std::memset(out, 0, sizeof(*out));
-            out->status = LBA_E_LIMIT;
-        }
-        return LBA_E_LIMIT;
-    }
     try {
         if (m->problem && m->device != opt->device) {
             lba_destroy(m->problem);

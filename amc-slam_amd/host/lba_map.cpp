@@ -310,6 +310,7 @@ std::unique_ptr<Map> Map::load(const void* bytes, size_t n, std::string* err) {
         cp.fx = cams[c].fx; cp.fy = cams[c].fy; cp.cx = cams[c].cx; cp.cy = cams[c].cy;
         std::memcpy(cp.Tbc.q, cams[c].q, sizeof(cp.Tbc.q));
         std::memcpy(cp.Tbc.t, cams[c].t, sizeof(cp.Tbc.t));
+        std::memcpy(cp.Rbc_ini, cams[c].rbc_ini, sizeof(cp.Rbc_ini));
         M->mCameras.push_back(cp);
     }
     for (int i = 0; i < h->n_kf; ++i) {
@@ -534,6 +535,7 @@ int64_t Map::save(void* bytes, size_t cap) const {
         std::memcpy(cams[c].q, mCameras[c].Tbc.q, sizeof(cams[c].q));
         std::memcpy(cams[c].t, mCameras[c].Tbc.t, sizeof(cams[c].t));
         cams[c].fx = mCameras[c].fx; cams[c].fy = mCameras[c].fy; cams[c].cx = mCameras[c].cx; cams[c].cy = mCameras[c].cy;
+        std::memcpy(cams[c].rbc_ini, mCameras[c].Rbc_ini, sizeof(cams[c].rbc_ini));
     }
     auto put_vec = [&](const void* src, size_t sz) { if (sz) std::memcpy(put(sz), src, sz); };
     put_vec(cams.data(), sizeof(lbamap_cam) * cams.size());

@@ -64,6 +64,7 @@ struct GPObs {
 struct CameraParams {      // Pinhole::mvParameters + MultiKeyFrame::mTbc[c]
     float fx = 0, fy = 0, cx = 0, cy = 0;
     SE3f Tbc;
+    float Rbc_ini[4] = {0, 0, 0, 1};   // MultiFrame::mRbc_ini[c] (Sophus::SO3f, x y z w), src/Frame.cc:181
     float uncertainty2() const { return 1.0f; }   // Pinhole::uncertainty2 (src/CameraModels/Pinhole.cpp:56-59)
 };
 

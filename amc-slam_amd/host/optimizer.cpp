@@ -136,7 +136,9 @@ void Optimizer::BuildLocalGPBAWindow(MultiKeyFrame* pKF, bool bLarge, LocalGPBAW
     for (int i = 0; i < N; ++i) W->vel_kfs.push_back(vtx(vpOptimizableKFs[i]));
     for (int i = N - 1; i > 0; --i) W->priors.push_back(lba_prior{vtx(vpOptimizableKFs[i]), vtx(vpOptimizableKFs[i - 1])});
 
-    // cameras: MultiKeyFrame::mTbc[c].cast<double>() + Pinhole parameters (VertexExtrinsic, fixed, :994-1006)
+    // cameras: MultiKeyFrame::mTbc[c].cast<double>() + Pinhole parameters (VertexExtrinsic, fixed, :982-995)
+    // and the EdgeExtrinsicPrior of each: mRbc_ini[c].cast<double>(), information mRbc_ini_cov = 0.2 I
+    // (src/Frame.cc:181-182); it only acts once the extrinsic is freed (bExtrinsic, :1228-1240)
     const std::vector<CameraParams>& cams = *pKF->mvpCamera;
     const int nCam = pKF->nCamera;
     for (int c = 0; c < nCam; ++c) {
@@ -145,6 +147,8 @@ void Optimizer::BuildLocalGPBAWindow(MultiKeyFrame* pKF, bool bLarge, LocalGPBAW
         std::memcpy(lc.q, T.q, sizeof(lc.q));
         std::memcpy(lc.t, T.t, sizeof(lc.t));
         lc.fx = cams[c].fx; lc.fy = cams[c].fy; lc.cx = cams[c].cx; lc.cy = cams[c].cy;
+        for (int i = 0; i < 4; ++i) lc.rbc_ini[i] = (double)cams[c].Rbc_ini[i];
+        for (int i = 0; i < 3; ++i) lc.rbc_info[4 * i] = 0.2;
         W->cams.push_back(lc);
     }
 
@@ -250,13 +254,6 @@ void Optimizer::BuildLocalGPBAWindow(MultiKeyFrame* pKF, bool bLarge, LocalGPBAW
 int Optimizer::LocalGPBA(MultiKeyFrame* pKF, Map* pMap, const lbamap_options& opt, lba_problem* problem,
                          lbamap_result* out) {
     lbamap_result res{};
-    if (opt.extrinsic) {
-        // the second pass with free extrinsics (Optimizer.cc:1229-1240) needs extrinsic columns in
-        // the pose system; not built yet
-        res.status = LBA_E_LIMIT;
-        if (out) *out = res;
-        return LBA_E_LIMIT;
-    }
     const bool bLarge = opt.large != 0;
     const unsigned long id = pKF->mnId;
     LocalGPBAWindow W;
@@ -280,16 +277,37 @@ int Optimizer::LocalGPBA(MultiKeyFrame* pKF, Map* pMap, const lbamap_options& op
                              (int)W.obs.size(), W.priors.data(), (int)W.priors.size(), W.vel_kfs.data(),
                              (int)W.vel_kfs.size(), W.cams.data(), (int)W.cams.size());
     lba_stats st{};
-    if (rc >= 0) rc = lba_optimize(problem, 10, nullptr, &st);
+    if (rc >= 0) rc = lba_optimize(problem, 10, nullptr, &st);   // opt_it1 = 10 (:1218)
     if (rc < 0) {
         res.status = rc;
         if (out) *out = res;
         return rc;
     }
+    const float err = (float)st.chi2_initial;
     res.iterations = st.iterations;
     res.chi2_initial = st.chi2_initial;
+    if (opt.extrinsic) {
+        // :1228-1240: free the extrinsics of the cameras with >= extrin_thresh keyframe observations, then
+        // initializeOptimization + computeActiveErrors + optimize(opt_it2) from the current estimate
+        const int opt_it2 = bLarge ? 4 : 10;
+        for (int c = 0; c < pKF->nCamera - 1; ++c)
+            if (W.cam_obs[c] >= 50) W.cams[c].ext_free = 1;
+        std::vector<lba_kf> kf_now(W.kfs.size());
+        std::vector<double> lm_now(W.lm.size());
+        rc = lba_get_state(problem, kf_now.data(), lm_now.data());
+        if (rc >= 0)
+            rc = lba_set_problem(problem, kf_now.data(), (int)kf_now.size(), lm_now.data(), (int)W.mp_ids.size(),
+                                 W.obs.data(), (int)W.obs.size(), W.priors.data(), (int)W.priors.size(),
+                                 W.vel_kfs.data(), (int)W.vel_kfs.size(), W.cams.data(), (int)W.cams.size());
+        if (rc >= 0) rc = lba_optimize(problem, opt_it2, nullptr, &st);
+        if (rc < 0) {
+            res.status = rc;
+            if (out) *out = res;
+            return rc;
+        }
+        res.iterations += st.iterations;
+    }
     res.chi2_final = st.chi2_final;
-    const float err = (float)st.chi2_initial;
     const float err_end = (float)st.chi2_final;
 
     std::vector<double> chi2(W.obs.size());
@@ -376,11 +394,22 @@ int Optimizer::LocalGPBA(MultiKeyFrame* pKF, Map* pMap, const lbamap_options& op
         MapPoint* P = pMap->mp_by_id(W.mp_ids[r]);
         P->SetWorldPos(Vec3f{(float)lm_out[3 * r], (float)lm_out[3 * r + 1], (float)lm_out[3 * r + 2]});
     }
-    for (MapPoint* P : W.lLocalMapPoints) P->UpdateNormalAndDepth();   // in lLocalMapPoints order (:1420-1426)
-    // extrinsics with >= 50 observations are written back (fixed here, so only the double round trip, :1428-1436)
+    for (MapPoint* P : W.lLocalMapPoints) P->UpdateNormalAndDepth();   // in lLocalMapPoints order (:1412-1416)
+    // extrinsics of the cameras that kept >= 50 observations: mTbc[c] = v->estimate().cast<float>()
+    // (:1419-1428; a camera that was not freed round-trips its mTbc through double)
+    std::vector<lba_cam> cam_out(W.cams.size());
+    rc = lba_get_cams(problem, cam_out.data());
+    if (rc < 0) {
+        res.status = rc;
+        if (out) *out = res;
+        return rc;
+    }
     for (int c = 0; c < pKF->nCamera - 1; ++c) {
         if (W.cam_obs[c] < 50) continue;
-        pMap->mCameras[c].Tbc = SE3d::from_float(pMap->mCameras[c].Tbc).cast_float();
+        SE3d T;
+        std::memcpy(T.q, cam_out[c].q, sizeof(T.q));
+        std::memcpy(T.t, cam_out[c].t, sizeof(T.t));
+        pMap->mCameras[c].Tbc = T.cast_float();
     }
     pMap->IncreaseChangeIndex();
     (void)id;

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define LBAMAP_VERSION   1
+#define LBAMAP_VERSION   2
 #define LBAMAP_MAX_CAM   8
 #define LBAMAP_MAX_LEVEL 16
 
@@ -60,6 +60,7 @@ typedef struct lbamap_cam {     /* Sophus::SE3f MultiKeyFrame::mTbc[c] and Pinho
     float q[4];                 /* (x, y, z, w) */
     float t[3];
     float fx, fy, cx, cy;
+    float rbc_ini[4];           /* MultiFrame::mRbc_ini[c] (x, y, z, w): the extrinsic prior's rotation (Frame.cc:181) */
     float pad;
 } lbamap_cam;
 
@@ -123,7 +124,7 @@ typedef struct lbamap_gpobs {   /* GPObs (include/MapPoint.h:46-62) keyed by the
 /* Options of one LocalGPBA call (the reference's arguments plus the GPU device). */
 typedef struct lbamap_options {
     int32_t large;              /* bLarge: window of 25 KFs, lambda0 1e-2, no divergence guard */
-    int32_t extrinsic;          /* bExtrinsic: second pass with extrinsics free (not supported: LBA_E_LIMIT) */
+    int32_t extrinsic;          /* bExtrinsic: second pass with the extrinsics of well-observed cameras free (:1228-1240) */
     int32_t device;             /* HIP device */
     int32_t flags;              /* lba_config.flags */
 } lbamap_options;

@@ -341,6 +341,9 @@ def build_window(pm, kf_id, large=False):
         cams[c]["q"], cams[c]["t"] = f2d([F32(x) for x in q], [F32(x) for x in t])
         for f in ("fx", "fy", "cx", "cy"):
             cams[c][f] = float(rec[f])
+        # EdgeExtrinsicPrior(mRbc_ini[c].cast<double>()), information mRbc_ini_cov = 0.2 I (Frame.cc:181-182)
+        cams[c]["rbc_ini"] = [float(x) for x in rec["rbc_ini"]]
+        cams[c]["rbc_info"] = (0.2 * np.eye(3)).ravel()
 
     mp_sorted = sorted(local_mps, key=lambda M: M.id)
     lidx = {M.id: i for i, M in enumerate(mp_sorted)}
@@ -418,16 +421,31 @@ def build_window(pm, kf_id, large=False):
     return W
 
 
-def local_gpba(snap, kf_id, large=False, iters=10):
+def local_gpba(snap, kf_id, large=False, iters=10, extrinsic=False):
     """Full LocalGPBA on a copy of `snap` with the C oracle as the engine.  Returns
     (status, new_snapshot, info)."""
     pm = PyMap(snap.copy())
     W = build_window(pm, kf_id, large)
     o = orc.Oracle(W.win, cfg=make_config(**W.win.cfg))
     n_it, st = o.optimize(iters)
+    err = F32(st.chi2_initial)
+    chi2_initial = st.chi2_initial
+    if extrinsic:
+        # bExtrinsic (:1228-1240): cameras with >= 50 keyframe observations get a free VertexExtrinsic;
+        # initializeOptimization / computeActiveErrors / optimize(opt_it2) from the current estimate
+        kfs, lm = o.state()
+        cams = W.win.cams.copy()
+        for c in range(pm.n_cam - 1):
+            if W.cam_obs[c] >= 50:
+                cams[c]["ext_free"] = 1
+        W.win = Window(kfs=kfs, lm=lm, obs=W.win.obs, priors=W.win.priors, vel_kfs=W.win.vel_kfs, cams=cams,
+                       cfg=W.win.cfg, name=W.win.name + "_ext")
+        o = orc.Oracle(W.win, cfg=make_config(**W.win.cfg))
+        n2, st = o.optimize(4 if large else 10)
+        n_it += n2
     _, _, chi2 = o.errors()
     depth = o.depth_ok()
-    err, err_end = F32(st.chi2_initial), F32(st.chi2_final)
+    err_end = F32(st.chi2_final)
     n = pm.n_cam
     chi2_mono, chi2_stereo = F32(5.991), F32(7.815)
 
@@ -455,7 +473,7 @@ def local_gpba(snap, kf_id, large=False, iters=10):
             elif tag == TAG_MONO_GP_KF and mono_out(i, cam):
                 W.cam_obs[cam] -= 1
                 erase.append((K, M, cam))
-    info = {"window": W, "iterations": n_it, "chi2_initial": st.chi2_initial, "chi2_final": st.chi2_final,
+    info = {"window": W, "iterations": n_it, "chi2_initial": chi2_initial, "chi2_final": st.chi2_final,
             "chi2": chi2, "depth_ok": depth, "n_erased_gp": len(erase_nkf), "n_erased": len(erase)}
     if (F32(2) * err < err_end or np.isnan(err) or np.isnan(err_end)) and not large:
         return -3, snap.copy(), info
@@ -484,8 +502,9 @@ def local_gpba(snap, kf_id, large=False, iters=10):
     for M in W.local_mps:
         pm.update_normal_and_depth(M)
     snap_out = pm.to_snapshot()
-    for c in range(n - 1):   # extrinsics with >= 50 observations: SE3d -> SE3f round trip (:1428-1436)
+    est = o.cams()
+    for c in range(n - 1):   # extrinsics with >= 50 observations: mTbc = v->estimate().cast<float>() (:1419-1428)
         if W.cam_obs[c] >= 50:
-            q, t = d2f(*f2d([F32(x) for x in snap_out.cams[c]["q"]], [F32(x) for x in snap_out.cams[c]["t"]]))
+            q, t = d2f(list(est[c]["q"]), list(est[c]["t"]))
             snap_out.cams[c]["q"], snap_out.cams[c]["t"] = q, t
     return 0, snap_out, info

@@ -122,13 +122,6 @@ def test_window_mono_only_map():
     assert set(np.unique(win.obs["kind"]).tolist()) <= {olg.MONO, olg.STEREO}
 
 
-def test_extrinsic_pass_reports_unsupported(snap4):
-    m = ms.LocalGPBAMap(snap4)
-    rc, res = m.local_gpba(29, extrinsic=True)
-    assert rc == -6 and res.status == -6
-    assert "extrinsic" in m.error()
-
-
 def test_unknown_keyframe(snap4):
     m = ms.LocalGPBAMap(snap4)
     rc, _ = m.local_gpba(12345)
@@ -212,6 +205,42 @@ def test_local_gpba_matches_oracle(snap4, kf_id, large):
     assert rc2 == st2 == 0
     assert res2.n_erased + res2.n_erased_gp == info2["n_erased"] + info2["n_erased_gp"]
     _compare_after(m.save(), exp2, info2)
+
+
+def _miscalibrated(snap, rot_deg=0.3, trans=0.01, seed=3):
+    """mTbc of the asynchronous cameras drifted from mRbc_ini (what an online calibration corrects)."""
+    from amc_lba.synth import _expso3, quat_to_rot, rot_to_quat
+    rng = np.random.default_rng(seed)
+    s = snap.copy()
+    for c in range(len(s.cams) - 1):
+        R = quat_to_rot(s.cams[c]["q"].astype(float)) @ _expso3(rng.normal(0, np.deg2rad(rot_deg), 3))
+        s.cams[c]["q"] = np.float32(rot_to_quat(R))
+        s.cams[c]["t"] = s.cams[c]["t"] + np.float32(rng.normal(0, trans, 3))
+    return s
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("large", [False, True])
+def test_local_gpba_extrinsic_pass_matches_oracle(snap4, large):
+    """bExtrinsic (src/Optimizer.cc:1218-1240, 1419-1428): optimize(10), then the extrinsics of cameras
+    with >= 50 keyframe observations freed and optimize(opt_it2 = 10, or 4 with bLarge), post-pass,
+    write-back of the poses, points and (cameras that kept >= 50 observations) mTbc."""
+    snap = _miscalibrated(snap4)
+    m = ms.LocalGPBAMap(snap)
+    rc, res = m.local_gpba(29, large=large, extrinsic=True)
+    st, exp, info = olg.local_gpba(snap, 29, large, extrinsic=True)
+    assert rc == st == 0, m.error()
+    assert min(info["window"].cam_obs[:-1]) >= 50   # every asynchronous camera was freed and written back
+    assert res.iterations == info["iterations"]
+    assert abs(res.chi2_final - info["chi2_final"]) <= 1e-7 * info["chi2_final"]
+    assert res.n_erased_gp == info["n_erased_gp"] and res.n_erased == info["n_erased"]
+    got = m.save()
+    _compare_after(got, exp, info)
+    np.testing.assert_allclose(got.cams["q"], exp.cams["q"], rtol=0, atol=2e-7)
+    np.testing.assert_allclose(got.cams["t"], exp.cams["t"], rtol=0, atol=2e-6)
+    assert np.abs(got.cams["q"][:-1] - snap.cams["q"][:-1]).max() > 1e-5   # the extrinsics moved
+    np.testing.assert_array_equal(got.cams["q"][-1], snap.cams["q"][-1])
+    np.testing.assert_array_equal(got.cams["rbc_ini"], snap.cams["rbc_ini"])
 
 
 def test_local_gpba_reference_signature_symbol():
