@@ -244,10 +244,13 @@ struct DevProblem {
 constexpr int HLOG_CAP = 4096;
 void launch_gp_prep(const DevProblem& P, int sel, int jac, int gate, hipStream_t s);
 // e0 / e1 (optional): timing events attached to the k_linearize dispatch itself
+// edges: also the motion-prior / velocity / extrinsic-prior quadratic forms of launch_prior_lin, as extra
+// workgroups after the tiles (the pose samples' part then comes with launch_schur(psel, pgate))
 void launch_linearize(const DevProblem& P, int sel, int write_res, int gate, hipStream_t s, hipEvent_t e0 = nullptr,
-                      hipEvent_t e1 = nullptr);
+                      hipEvent_t e1 = nullptr, int edges = 0);
 void launch_prior_lin(const DevProblem& P, int sel, int gate, hipStream_t s);
-void launch_schur(const DevProblem& P, double lambda, int gate, hipStream_t s);
+// psel / pgate >= 0: the prior / sample reduction of launch_prior_lin(psel, pgate) in the same launch
+void launch_schur(const DevProblem& P, double lambda, int gate, hipStream_t s, int psel = 0, int pgate = -1);
 enum { ASM_SCHUR = 1, ASM_FULL = 2 };
 void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hipStream_t s);
 void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s);

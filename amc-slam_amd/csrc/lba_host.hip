@@ -1179,14 +1179,18 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
                 p->qev.resize(std::max<size_t>(2 * (size_t)issued + 2, 2 * old));
                 for (size_t e = old; e < p->qev.size(); ++e) HIPCHK(hipEventCreate(&p->qev[e]));
             }
+            // the prior / sample reduction runs inside the linearisation's launch (edge items) and
+            // k_schur's (pose samples), filling the slots their last tiles leave idle; except before
+            // computeLambdaInit, which reads H_pp before the Schur step
+            const bool lam0 = issued == 0 && p->cfg.lambda_init <= 0;
             launch_linearize(D, SEL_CUR, 0, GATE_LIN, p->stream, tq ? p->qev[2 * issued] : nullptr,
-                             tq ? p->qev[2 * issued + 1] : nullptr);
-            launch_prior_lin(D, SEL_CUR, GATE_LIN, p->stream);
-            if (issued == 0 && p->cfg.lambda_init <= 0) {
+                             tq ? p->qev[2 * issued + 1] : nullptr, lam0 ? 0 : 1);
+            if (lam0) {
+                launch_prior_lin(D, SEL_CUR, GATE_LIN, p->stream);
                 assemble_layout(p, 0.0, ASM_FULL);
                 launch_lambda_init(D, p->cfg.tau, p->stream);
             }
-            launch_schur(D, LAMBDA_CTL, GATE_NONE, p->stream);
+            launch_schur(D, LAMBDA_CTL, GATE_NONE, p->stream, SEL_CUR, lam0 ? -1 : GATE_LIN);
             assemble_layout(p, LAMBDA_CTL, ASM_SCHUR);
             launch_cholesky_solve(D, GATE_NONE, ++p->cf_epoch, p->stream);
             // the step, the trial state and its pose samples with their Jacobian factors: an

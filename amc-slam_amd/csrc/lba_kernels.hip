@@ -343,7 +343,10 @@ __device__ __forceinline__ void smp_task(const DevProblem& P, const double* rows
     for (int q = 0; q < 9; ++q) m[q] = acc[q];
 }
 
-__global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, int write_res, int gate) {
+template <int NT>
+__device__ void edge_item(const DevProblem& P, int sel, int idx, const int tid, double* shm);
+
+__global__ __launch_bounds__(TILE_OBS, 3) void k_linearize(DevProblem P, int sel, int write_res, int gate) {
     __shared__ double rows[TILE_ROWS * ROW_STRIDE];
     __shared__ double rw[TILE_ROWS];
     __shared__ int tsm[2 * TILE_SMP];
@@ -355,6 +358,11 @@ __global__ __launch_bounds__(TILE_OBS) void k_linearize(DevProblem P, int sel, i
     __shared__ int lrow[TILE_ROWS];
     __shared__ int lr0[TILE_LMS + 1];
     __shared__ double red[TILE_OBS / 64];
+    if ((int)blockIdx.x >= P.n_tiles) {   // fused motion-prior / velocity / extrinsic-prior edge items
+        if (gated_off(P.ctl, gate)) return;
+        edge_item<TILE_OBS>(P, sel, blockIdx.x - P.n_tiles, threadIdx.x, rows);
+        return;
+    }
     const int tile = blockIdx.x, tid = threadIdx.x;
     const int obs0 = P.tile_obs0[tile], nobs = P.tile_nobs[tile];
     const int ts0 = P.tile_smp0[tile], nts = P.tile_nsmp[tile];
@@ -515,8 +523,7 @@ constexpr int EXP_GROUPS = PRI_THREADS / SM_STRIDE;   // 9 partial sums per outp
 // A sample of a camera whose extrinsic is free also couples that extrinsic's block e: N is extended by the
 // camera's factor [Ad(Tbc) 0] (columns 24..35) and ae, be, ee, b_e follow the same way.
 __device__ void sample_expand(const DevProblem& P, const double* gps, const double* camd, int smp, double* Msh,
-                              double* Nsh, double* MN, double* part) {
-    const int tid = threadIdx.x;
+                              double* Nsh, double* MN, double* part, const int tid) {
     const int* sl = P.seg_slot + SEG_STRIDE * (size_t)smp;
     const int* gl = P.seg_gslot + GSEG_STRIDE * (size_t)smp;
     if (sl[0] < 0 && sl[1] < 0 && sl[2] < 0 && sl[6] < 0) return;   // no optimisable vertex (uniform per workgroup)
@@ -588,20 +595,20 @@ __device__ void sample_expand(const DevProblem& P, const double* gps, const doub
     }
 }
 
-// Workgroups 0 .. n_prior + n_vel + n_eprior - 1: EdgeGaussianPrior / EdgeVelocity / EdgeExtrinsicPrior
-// quadratic forms; then one workgroup per pose sample (sample_expand).
-__global__ __launch_bounds__(PRI_THREADS) void k_prior_lin(DevProblem P, int sel, int gate) {
-    __shared__ double Ji[144], Jj[216], WJi[216], WJj[144], Om[144], e[12], We[12];
-    __shared__ double wsh;
-    __shared__ double part[EXP_GROUPS * SM_STRIDE];
-    const int idx = blockIdx.x, tid = threadIdx.x;
-    if (gated_off(P.ctl, gate)) return;
+// Work items of the prior / sample reduction: 0 .. n_prior + n_vel + n_eprior - 1 the EdgeGaussianPrior /
+// EdgeVelocity / EdgeExtrinsicPrior quadratic forms (edge_item, NT threads), then one per pose sample
+// (sample_expand, PRI_THREADS working threads; tid >= PRI_THREADS only takes part in the barriers).  In
+// the queued loop the edge items run as extra workgroups of k_linearize and the samples as extra
+// workgroups of k_schur (they fill the slots the last tiles leave idle); k_prior_lin runs them all for
+// the host-driven paths.  shm: PRI_SHM doubles of LDS.
+constexpr int PRI_SHM = 144 + 216 + 216 + 144 + 144 + 12 + 12 + 1 + EXP_GROUPS * SM_STRIDE;
+constexpr int EDGE_SHM = 144 * 5 + 12 + 12 + 1;
+template <int NT>
+__device__ void edge_item(const DevProblem& P, int sel, int idx, const int tid, double* shm) {
+    double *Ji = shm, *Jj = Ji + 144, *WJi = Jj + 144, *WJj = WJi + 144, *Om = WJj + 144, *e = Om + 144,
+           *We = e + 12, *wshp = We + 12;
+    double& wsh = *wshp;
     const int si = state_idx(P, sel);
-    const int npe = P.n_prior + P.n_vel + P.n_eprior;
-    if (idx >= npe) {
-        sample_expand(P, P.gpsb[si], P.camdb[si], idx - npe, Ji, Jj, WJi, part);
-        return;
-    }
     const double* __restrict__ kst = P.kbuf[si];
     const int ent = P.pri_entry0 + idx;
     const int* sl = P.seg_slot + SEG_STRIDE * (size_t)ent;
@@ -625,7 +632,7 @@ __global__ __launch_bounds__(PRI_THREADS) void k_prior_lin(DevProblem P, int sel
         }
         __syncthreads();
         double* H = P.hslab + (size_t)sl[2] * 144;
-        for (int t = tid; t < 144; t += PRI_THREADS) {
+        for (int t = tid; t < 144; t += NT) {
             const int i = t / 12 - 3, j = t % 12 - 3;
             double v = 0.0;
             if (i >= 0 && i < 3 && j >= 0 && j < 3)   // (Jrot^T Om Jrot)(i, j)
@@ -660,7 +667,7 @@ __global__ __launch_bounds__(PRI_THREADS) void k_prior_lin(DevProblem P, int sel
         }
         __syncthreads();
         const double w1 = wsh;
-        for (int t = tid; t < 288; t += PRI_THREADS) {
+        for (int t = tid; t < 288; t += NT) {
             const int which = t / 144, ij = t % 144, i = ij / 12, j = ij % 12;
             const double* J = which ? Jj : Ji;
             double s = 0.0;
@@ -674,7 +681,7 @@ __global__ __launch_bounds__(PRI_THREADS) void k_prior_lin(DevProblem P, int sel
         }
         __syncthreads();
         // aa = Ji^T W Ji, ab = Ji^T W Jj, bb = Jj^T W Jj, ga/gb = -J^T W e (base_binary_edge.hpp:54-120)
-        for (int t = tid; t < 456; t += PRI_THREADS) {
+        for (int t = tid; t < 456; t += NT) {
             if (t < 432) {
                 const int bk = t / 144, ij = t % 144, i = ij / 12, j = ij % 12;
                 const int slot = sl[bk == 0 ? 0 : (bk == 1 ? 1 : 2)];
@@ -701,9 +708,20 @@ __global__ __launch_bounds__(PRI_THREADS) void k_prior_lin(DevProblem P, int sel
         const double ev = kst[(size_t)P.vel_kf[v] * KF_STRIDE + 7 + 2];
         const double q22 = P.qcinv[2 * 6 + 2];
         double* H = P.hslab + (size_t)sl[2] * 144;
-        for (int t = tid; t < 144; t += PRI_THREADS) H[t] = (t == 8 * 12 + 8) ? q22 : 0.0;
+        for (int t = tid; t < 144; t += NT) H[t] = (t == 8 * 12 + 8) ? q22 : 0.0;
         if (tid < 12) P.gslab[(size_t)gl[1] * 12 + tid] = (tid == 8) ? -q22 * ev : 0.0;
         if (tid == 0) P.chi_lin[P.n_tiles + idx] = ev * (q22 * ev);
+    }
+}
+
+__global__ __launch_bounds__(PRI_THREADS) void k_prior_lin(DevProblem P, int sel, int gate) {
+    __shared__ double shm[PRI_SHM];
+    if (gated_off(P.ctl, gate)) return;
+    const int npe = P.n_prior + P.n_vel + P.n_eprior, si = state_idx(P, sel);
+    if ((int)blockIdx.x < npe) edge_item<PRI_THREADS>(P, sel, blockIdx.x, threadIdx.x, shm);
+    else {
+        double *Msh = shm, *Nsh = Msh + 144, *MN = Nsh + 216, *part = MN + 216;
+        sample_expand(P, P.gpsb[si], P.camdb[si], blockIdx.x - npe, Msh, Nsh, MN, part, threadIdx.x);
     }
 }
 
@@ -718,7 +736,11 @@ __global__ __launch_bounds__(PRI_THREADS) void k_prior_lin(DevProblem P, int sel
 // the factorisation status for the solve that follows, and the first blocks zero the envelope of S.
 constexpr int SCHUR_THREADS = 512;
 
-__global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double lambda_arg, int gate) {
+// Workgroups n_tiles ..: the prior / sample reduction items of k_prior_lin fused into the same launch
+// (pgate >= 0; they only need k_linearize's output), so they fill the slots k_schur's last tiles leave
+// idle instead of running as a launch of their own.
+static_assert(144 + 216 + 216 + EXP_GROUPS * SM_STRIDE <= TILE_PAIRS * 36, "fused sample items reuse the Hpl staging LDS");
+__global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double lambda_arg, int gate, int psel, int pgate) {
     __shared__ double Hs[TILE_PAIRS * 36];   // Hpl, then W = Hpl L^-T
     __shared__ double Dl[TILE_LMS * 9];      // per landmark: L^-T terms l10, l21, l10 l21 - l20; D^-1 (3); u (3)
     __shared__ int slst[TILE_SLIST];
@@ -727,6 +749,13 @@ __global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double la
     __shared__ signed char pm[TILE_PAIRS];
     __shared__ int kfl[TILE_KF];
     constexpr int NT = SCHUR_THREADS, NW = NT / 64;
+    if ((int)blockIdx.x >= P.n_tiles) {   // fused pose-sample items of the prior / sample reduction
+        if (gated_off(P.ctl, pgate)) return;
+        const int si = state_idx(P, psel);
+        sample_expand(P, P.gpsb[si], P.camdb[si], blockIdx.x - P.n_tiles, Hs, Hs + 144, Hs + 360, Hs + 576,
+                      threadIdx.x < PRI_THREADS ? threadIdx.x : (1 << 20));
+        return;
+    }
     const int tile = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int pair0 = P.tile_pair0[tile], npair = P.tile_npair[tile];
     const int lm0 = P.tile_lm0[tile], nlm = P.tile_nlm[tile];
@@ -741,7 +770,7 @@ __global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double la
     }
     // clear the envelope tiles of S for this trial's assembly (the previous factorisation left its
     // fill-in there); k_assemble runs after this kernel
-    for (int z = tile; z < P.n_ztiles; z += gridDim.x) {
+    for (int z = tile; z < P.n_ztiles; z += P.n_tiles) {
         const int zi = P.ztiles[z] & 0xffff, zj = P.ztiles[z] >> 16;
         for (int t = tid; t < CHOL_NB * CHOL_NB; t += NT)
             P.S[(size_t)(zi * CHOL_NB + t / CHOL_NB) * P.npad + zj * CHOL_NB + t % CHOL_NB] = 0.0;
@@ -2333,19 +2362,26 @@ void launch_gp_prep(const DevProblem& P, int sel, int jac, int gate, hipStream_t
     if (nb) hipLaunchKernelGGL(k_gp_prep, dim3(nb), dim3(PREP_THREADS), 0, s, P, sel, jac, gate);
 }
 void launch_linearize(const DevProblem& P, int sel, int write_res, int gate, hipStream_t s, hipEvent_t e0,
-                      hipEvent_t e1) {
-    if (!P.n_tiles) return;
+                      hipEvent_t e1, int edges) {
+    const int ne = edges ? P.n_prior + P.n_vel + P.n_eprior : 0;
+    if (!P.n_tiles) {
+        if (ne) launch_prior_lin(P, sel, gate, s);
+        return;
+    }
+    const dim3 g(P.n_tiles + ne);
     if (e0)   // the events carry the dispatch's own start / end timestamps
-        hipExtLaunchKernelGGL(k_linearize, dim3(P.n_tiles), dim3(TILE_OBS), 0, s, e0, e1, 0, P, sel, write_res, gate);
+        hipExtLaunchKernelGGL(k_linearize, g, dim3(TILE_OBS), 0, s, e0, e1, 0, P, sel, write_res, gate);
     else
-        hipLaunchKernelGGL(k_linearize, dim3(P.n_tiles), dim3(TILE_OBS), 0, s, P, sel, write_res, gate);
+        hipLaunchKernelGGL(k_linearize, g, dim3(TILE_OBS), 0, s, P, sel, write_res, gate);
 }
 void launch_prior_lin(const DevProblem& P, int sel, int gate, hipStream_t s) {
     const int n = P.n_prior + P.n_vel + P.n_eprior + P.n_smp;
     if (n) hipLaunchKernelGGL(k_prior_lin, dim3(n), dim3(PRI_THREADS), 0, s, P, sel, gate);
 }
-void launch_schur(const DevProblem& P, double lambda, int gate, hipStream_t s) {
-    if (P.n_tiles) hipLaunchKernelGGL(k_schur, dim3(P.n_tiles), dim3(SCHUR_THREADS), 0, s, P, lambda, gate);
+void launch_schur(const DevProblem& P, double lambda, int gate, hipStream_t s, int psel, int pgate) {
+    const int npri = pgate >= 0 ? P.n_smp : 0;   // the pose-sample items (the edge items ran with k_linearize)
+    if (!P.n_tiles) return;   // (no observations: no sample has a partial, and launch_linearize ran k_prior_lin)
+    hipLaunchKernelGGL(k_schur, dim3(P.n_tiles + npri), dim3(SCHUR_THREADS), 0, s, P, lambda, gate, psel, pgate);
 }
 void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hipStream_t s) {
     const int n = P.n_asm + P.n_pb;
