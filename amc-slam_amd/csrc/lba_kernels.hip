@@ -35,13 +35,14 @@ static_assert(CAMD_STRIDE == CAMREC_DOUBLES, "camera record layout drifted");
 
 // phase stamps for diagnostics only (buffer allocated when LBA_PHASE_TIMING is set; the uniform
 // null test costs one scalar branch otherwise)
-#define LBA_TMARK(buf, k)                                                           \
-    do {                                                                            \
-        if (buf) {                                                                  \
-            __syncthreads();                                                        \
-            if (threadIdx.x == 0) (buf)[(size_t)blockIdx.x * 16 + (k)] = clock64(); \
-        }                                                                           \
+#define LBA_TMARKI(buf, idx, k)                                                \
+    do {                                                                        \
+        if (buf) {                                                              \
+            __syncthreads();                                                    \
+            if (threadIdx.x == 0) (buf)[(size_t)(idx) * 16 + (k)] = clock64();  \
+        }                                                                       \
     } while (0)
+#define LBA_TMARK(buf, k) LBA_TMARKI(buf, blockIdx.x, k)
 
 typedef double d4 __attribute__((ext_vector_type(4)));   // v_mfma_f64_16x16x4 accumulator
 
@@ -763,7 +764,7 @@ __global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double la
     const int sent0 = P.tile_sent0[tile], nsent = P.tile_nsent[tile];
     if (gated_off(P.ctl, gate)) return;
     const double lambda = damping(P, lambda_arg);
-    LBA_TMARK(P.tdbg_schur, 0);
+    LBA_TMARKI(P.tdbg_schur, tile, 0);
     if (tile == 0 && tid == 0) {
         *P.info = 0;
         if (P.cf_head) *P.cf_head = 0;   // ticket counter of this trial's k_chol_flow
@@ -819,7 +820,7 @@ __global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double la
         o[6] = b0 / d0; o[7] = y1 / d1; o[8] = y2 / d2;
     }
     __syncthreads();
-    LBA_TMARK(P.tdbg_schur, 1);
+    LBA_TMARKI(P.tdbg_schur, tile, 1);
     for (int t = tid; t < npair; t += NT) {
         const int m = P.pair_lm[pair0 + t] - lm0, k = P.pair_kf[pair0 + t];
         int lk = 0;
@@ -840,7 +841,7 @@ __global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double la
         h[2] = h2 - D[1] * h1 + D[2] * h0;
     }
     __syncthreads();
-    LBA_TMARK(P.tdbg_schur, 2);
+    LBA_TMARKI(P.tdbg_schur, tile, 2);
     // ---- S partials: one wave per KF pair, K = (landmark, 3), two accumulators
     {
         const int kq = lane >> 4, cl = lane & 15, cr = min(cl, 11);
@@ -874,8 +875,8 @@ __global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double la
             }
         }
     }
-    LBA_TMARK(P.tdbg_schur, 3);
-    LBA_TMARK(P.tdbg_schur, 4);
+    LBA_TMARKI(P.tdbg_schur, tile, 3);
+    LBA_TMARKI(P.tdbg_schur, tile, 4);
     // ---- rhs partials: sum over the KF's landmarks of V(m,k) bl_m (block_solver.hpp:395-401)
     for (int task = tid; task < nkf * 12; task += NT) {
         const int l = task / 12, r = task % 12;
@@ -890,7 +891,7 @@ __global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double la
         }
         P.gpslab[(size_t)P.tkf_gslot[kf0 + l] * 12 + r] = v;
     }
-    LBA_TMARK(P.tdbg_schur, 5);
+    LBA_TMARKI(P.tdbg_schur, tile, 5);
 }
 
 // Reduced camera system of one trial, straight from the target-sorted partial slabs (each
