@@ -21,6 +21,7 @@
 #include <limits>
 #include <map>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/amc_lba.h"
@@ -55,7 +56,12 @@ struct lba_problem {
     double* kst[2] = {nullptr, nullptr};
     double* lst[2] = {nullptr, nullptr};
     int cur = 0;
-    std::vector<void*> allocs;
+    // device buffers of the window, in set_problem's allocation order; the next set_problem reuses
+    // them in the same order where they are large enough (LocalGPBA windows are alike call to call),
+    // so a call pays no hipMalloc / hipFree
+    struct Alloc { void* ptr; size_t bytes; };
+    std::vector<Alloc> allocs;
+    size_t alloc_cursor = 0;
     double* h_fin = nullptr;      // host-mapped coherent [HFIN_DOUBLES]: trial summary [4], sequence
                                   // number [4], LMCtl mirror [8..] (queued optimisation)
     double* d_hfin = nullptr;     // its device address
@@ -138,10 +144,15 @@ void dump_phase_times(lba_problem* p) {
     }
 }
 
-void free_all(lba_problem* p) {
-    dump_phase_times(p);
-    for (void* a : p->allocs) (void)hipFree(a);
+void release_all(lba_problem* p) {   // (lba_destroy)
+    for (auto& a : p->allocs) (void)hipFree(a.ptr);
     p->allocs.clear();
+    p->alloc_cursor = 0;
+}
+
+void free_all(lba_problem* p) {   // the buffers stay allocated for the next window's dalloc calls
+    dump_phase_times(p);
+    p->alloc_cursor = 0;
     p->kst[0] = p->kst[1] = p->lst[0] = p->lst[1] = nullptr;
     p->D = DevProblem{};
     p->has_problem = false;
@@ -150,9 +161,23 @@ void free_all(lba_problem* p) {
 
 template <typename T>
 T* dalloc(lba_problem* p, size_t n) {
+    const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+    if (p->alloc_cursor < p->allocs.size()) {
+        auto& a = p->allocs[p->alloc_cursor];
+        if (a.bytes < bytes) {
+            (void)hipFree(a.ptr);
+            a.ptr = nullptr;
+            a.bytes = 0;
+            HIPCHK(hipMalloc(&a.ptr, bytes));
+            a.bytes = bytes;
+        }
+        ++p->alloc_cursor;
+        return static_cast<T*>(a.ptr);
+    }
     void* d = nullptr;
-    HIPCHK(hipMalloc(&d, std::max<size_t>(n, 1) * sizeof(T)));
-    p->allocs.push_back(d);
+    HIPCHK(hipMalloc(&d, bytes));
+    p->allocs.push_back({d, bytes});
+    p->alloc_cursor = p->allocs.size();
     return static_cast<T*>(d);
 }
 template <typename T>
@@ -238,6 +263,17 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 throw ApiError{LBA_E_ARG, "obs " + std::to_string(i) + ": stereo GP observation of a camera with a free extrinsic"};
     }
 
+    // LBA_SETUP_TIMING: wall time of the set-up phases on stderr (host preprocessing vs device upload)
+    const bool stime = std::getenv("LBA_SETUP_TIMING") != nullptr;
+    auto tlast = std::chrono::steady_clock::now();
+    auto mark = [&](const char* what) {
+        if (!stime) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "set_problem %-12s %8.3f ms\n", what,
+                     std::chrono::duration<double, std::milli>(now - tlast).count());
+        tlast = now;
+    };
+    if (p->stream) HIPCHK(hipStreamSynchronize(p->stream));   // (the buffers are reused below)
     free_all(p);
     p->n_kf = n_kf; p->n_lm = n_lm; p->n_obs = n_obs; p->n_cam = n_cam;
     p->lm_host.assign(lm_xyz, lm_xyz + 3 * (size_t)n_lm);
@@ -336,17 +372,20 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         for (int i = 0; i < n_obs; ++i) obs_of[fill[p->lm_dev[obs[i].lm]]++] = i;
     }
 
-    // GP (prev KF, KF) pairs
-    std::map<std::pair<int, int>, int> gpmap;
-    std::vector<int> gp_a, gp_b;
+    // GP (prev KF, KF) pairs, numbered in order of first appearance; gp_of: each GP observation's pair
+    std::unordered_map<long long, int> gpmap;
+    gpmap.reserve(2 * (size_t)n_kf + 16);
+    std::vector<int> gp_a, gp_b, gp_of(n_obs, -1);
     for (int i = 0; i < n_obs; ++i)
         if (is_gp(obs[i].kind)) {
-            auto key = std::make_pair(obs[i].kf_a, obs[i].kf_b);
-            if (!gpmap.count(key)) {
-                gpmap[key] = (int)gp_a.size();
-                gp_a.push_back(key.first);
-                gp_b.push_back(key.second);
+            const long long key = (long long)obs[i].kf_a * n_kf + obs[i].kf_b;
+            auto it = gpmap.find(key);
+            if (it == gpmap.end()) {
+                it = gpmap.emplace(key, (int)gp_a.size()).first;
+                gp_a.push_back(obs[i].kf_a);
+                gp_b.push_back(obs[i].kf_b);
             }
+            gp_of[i] = it->second;
         }
 
     // GP pose samples: distinct observation times per GP pair (one per camera time stamp in
@@ -358,8 +397,16 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         typedef std::pair<double, int> SKey;
         auto skey = [&](const lba_obs& o) { return SKey(o.t, ext_block(o) >= 0 ? o.cam : -1); };
         std::vector<std::vector<SKey>> ts(gp_a.size());
-        for (int i = 0; i < n_obs; ++i)
-            if (is_gp(obs[i].kind)) ts[gpmap[std::make_pair(obs[i].kf_a, obs[i].kf_b)]].push_back(skey(obs[i]));
+        for (int i = 0; i < n_obs; ++i)   // distinct keys per pair are few: keep them unique while short
+            if (is_gp(obs[i].kind)) {
+                std::vector<SKey>& v = ts[gp_of[i]];
+                const SKey k = skey(obs[i]);
+                bool seen = false;
+                if (v.size() <= 16)
+                    for (const SKey& x : v)
+                        if (x == k) { seen = true; break; }
+                if (!seen) v.push_back(k);
+            }
         std::vector<SKey> keys;
         for (size_t g = 0; g < ts.size(); ++g) {
             std::sort(ts[g].begin(), ts[g].end());
@@ -369,7 +416,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         }
         for (int i = 0; i < n_obs; ++i)
             if (is_gp(obs[i].kind)) {
-                const int g = gpmap[std::make_pair(obs[i].kf_a, obs[i].kf_b)];
+                const int g = gp_of[i];
                 const SKey* b = keys.data() + gp_s0[g];
                 sample_of[i] = gp_s0[g] + (int)(std::lower_bound(b, b + (gp_s0[g + 1] - gp_s0[g]), skey(obs[i])) - b);
             }
@@ -398,6 +445,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     }
     const int n_pairs = (int)pair_lm.size();
 
+    mark("order/pairs");
     // ---- tiles: consecutive landmarks under the LDS limits of k_linearize / k_schur
     std::vector<int> t_obs0, t_nobs, t_lm0, t_nlm, t_pair0, t_npair, t_smp0, t_nsmp, t_sent0, t_nsent, t_kf0, t_nkf;
     std::vector<int> tkf_list, tsm_smp, tsm_rows, sent_l1, sent_l2, sent_k1, sent_k2;
@@ -407,38 +455,54 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     {
         auto smpq = [&](int q) { return smp_of[obs_of[q]]; };
         int d = 0;
+        // the tile's sorted sample / KF sets grow by the landmark's new elements (counted first, inserted
+        // only when the landmark fits: no per-landmark copies)
+        std::vector<int> uni, usm, new_s, new_k;
+        auto fresh = [](const std::vector<int>& set, std::vector<int>& add) {   // add := sorted unique \ set
+            std::sort(add.begin(), add.end());
+            add.erase(std::unique(add.begin(), add.end()), add.end());
+            add.erase(std::remove_if(add.begin(), add.end(),
+                                     [&](int v) { return std::binary_search(set.begin(), set.end(), v); }),
+                      add.end());
+        };
+        auto merge_in = [](std::vector<int>& set, const std::vector<int>& add) {
+            const size_t n0 = set.size();
+            set.insert(set.end(), add.begin(), add.end());
+            std::inplace_merge(set.begin(), set.begin() + n0, set.end());
+        };
         while (d < nl) {
             int nobs = 0, rows = 0, npair = 0, nlmt = 0, nent = 0;
-            std::vector<int> uni, usm;
+            uni.clear();
+            usm.clear();
             int ncomb = 0;   // Schur triples of the tile (sum over landmarks of P (P + 1) / 2)
             int e = d;
             while (e < nl) {
                 int no = lobs0[e + 1] - lobs0[e], nr = 0, ne = 0;
-                std::vector<int> s2 = usm;
+                new_s.clear();
                 for (int q = lobs0[e]; q < lobs0[e + 1]; ++q) {
                     const lba_obs& ob = obs[obs_of[q]];
                     nr += obs_dim(ob.kind);
-                    s2.push_back(smpq(q));
+                    new_s.push_back(smpq(q));
                     ne += (H[ob.kf_b] >= 0) + (is_gp(ob.kind) && H[ob.kf_a] >= 0) + (ext_block(ob) >= 0);
                 }
-                std::sort(s2.begin(), s2.end());
-                s2.erase(std::unique(s2.begin(), s2.end()), s2.end());
+                fresh(usm, new_s);
                 const int npl = lm_pair0[e + 1] - lm_pair0[e];
-                std::vector<int> u2 = uni;
-                for (int k : lm_kfs[e]) u2.push_back(k);
-                std::sort(u2.begin(), u2.end());
-                u2.erase(std::unique(u2.begin(), u2.end()), u2.end());
+                new_k.assign(lm_kfs[e].begin(), lm_kfs[e].end());
+                fresh(uni, new_k);
                 const int ncl = npl * (npl + 1) / 2;
                 const bool fits = nobs + no <= TILE_OBS && rows + nr <= TILE_ROWS && npair + npl <= TILE_PAIRS &&
-                                  nlmt + 1 <= TILE_LMS && (int)u2.size() <= TILE_KF && (int)s2.size() <= TILE_SMP &&
-                                  ncomb + ncl <= TILE_SLIST && nent + ne <= TILE_PROWS;
+                                  nlmt + 1 <= TILE_LMS && (int)(uni.size() + new_k.size()) <= TILE_KF &&
+                                  (int)(usm.size() + new_s.size()) <= TILE_SMP && ncomb + ncl <= TILE_SLIST &&
+                                  nent + ne <= TILE_PROWS;
                 if (!fits) {
                     if (e == d)
                         throw ApiError{LBA_E_LIMIT, "landmark " + std::to_string(order[e]) +
                                                         " exceeds tile limits (obs/rows/pairs/keyframes)"};
                     break;
                 }
-                nobs += no; rows += nr; npair += npl; nlmt += 1; uni.swap(u2); usm.swap(s2); ncomb += ncl; nent += ne;
+                nobs += no; rows += nr; npair += npl; nlmt += 1; ncomb += ncl; nent += ne;
+                merge_in(usm, new_s);
+                merge_in(uni, new_k);
                 ++e;
             }
             t_obs0.push_back(lobs0[d]); t_nobs.push_back(nobs);
@@ -481,35 +545,43 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     for (int r = 0; r < obs_dim(obs[obs_of[o]].kind); ++r) lm_rows.push_back(ob_row[o] + r);
                 lm_r0[l + 1] = (int)lm_rows.size();
             }
-            // Schur entries: every (k1 <= k2) pose-block pair co-observed by a landmark of the tile
-            std::vector<std::pair<int, int>> kp;
-            for (int l = d; l < e; ++l)
-                for (size_t a = 0; a < lm_kfs[l].size(); ++a)
-                    for (size_t b = a; b < lm_kfs[l].size(); ++b) kp.emplace_back(lm_kfs[l][a], lm_kfs[l][b]);
-            std::sort(kp.begin(), kp.end());
-            kp.erase(std::unique(kp.begin(), kp.end()), kp.end());
-            t_sent0.push_back((int)sent_l1.size());
-            for (auto& pr : kp) {
-                sent_l1.push_back(local(pr.first)); sent_l2.push_back(local(pr.second));
-                sent_k1.push_back(pr.first); sent_k2.push_back(pr.second);
-            }
-            t_nsent.push_back((int)kp.size());
-            // per entry: the tile's landmarks coupling its two KFs, as packed
-            // (tile-local pair of k1) | (tile-local pair of k2) << 8 | (tile-local landmark) << 16
+            // Schur entries: every (k1 <= k2) pose-block pair co-observed by a landmark of the tile, in
+            // (k1, k2) order, counted on a table over the tile's local KF indices; per entry the tile's
+            // landmarks coupling its two KFs (landmark order), packed as (tile-local pair of k1) |
+            // (tile-local pair of k2) << 8 | (tile-local landmark) << 16
             {
-                std::vector<std::vector<int>> lists(kp.size());
+                int ecnt[TILE_KF][TILE_KF] = {}, eid[TILE_KF][TILE_KF];
+                int lk[TILE_PAIRS];
                 for (int l = d; l < e; ++l) {
                     const std::vector<int>& ks = lm_kfs[l];
+                    for (size_t a = 0; a < ks.size(); ++a) lk[a] = local(ks[a]);
+                    for (size_t a = 0; a < ks.size(); ++a)
+                        for (size_t b = a; b < ks.size(); ++b) ecnt[lk[a]][lk[b]]++;
+                }
+                const int nu = (int)uni.size();
+                t_sent0.push_back((int)sent_l1.size());
+                int nen = 0;
+                std::vector<int> fill;
+                const int list0 = (int)sent_list.size();
+                for (int i = 0; i < nu; ++i)
+                    for (int j = i; j < nu; ++j) {
+                        if (!ecnt[i][j]) continue;
+                        eid[i][j] = nen++;
+                        sent_l1.push_back(i); sent_l2.push_back(j);
+                        sent_k1.push_back(uni[i]); sent_k2.push_back(uni[j]);
+                        fill.push_back((fill.empty() ? list0 : sent_r0.back()));
+                        sent_r0.push_back(fill.back() + ecnt[i][j]);
+                    }
+                t_nsent.push_back(nen);
+                sent_list.resize(sent_r0.back());
+                for (int l = d; l < e; ++l) {
+                    const std::vector<int>& ks = lm_kfs[l];
+                    for (size_t a = 0; a < ks.size(); ++a) lk[a] = local(ks[a]);
                     for (size_t a = 0; a < ks.size(); ++a)
                         for (size_t b = a; b < ks.size(); ++b) {
-                            const size_t en = std::lower_bound(kp.begin(), kp.end(), std::make_pair(ks[a], ks[b])) - kp.begin();
                             const int t1 = lm_pair0[l] + (int)a - lm_pair0[d], t2 = lm_pair0[l] + (int)b - lm_pair0[d];
-                            lists[en].push_back(t1 | (t2 << 8) | ((l - d) << 16));
+                            sent_list[fill[eid[lk[a]][lk[b]]]++] = t1 | (t2 << 8) | ((l - d) << 16);
                         }
-                }
-                for (auto& li : lists) {
-                    for (int v : li) sent_list.push_back(v);
-                    sent_r0.push_back((int)sent_list.size());
                 }
             }
             d = e;
@@ -518,6 +590,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     const int n_tiles = (int)t_obs0.size();
     const int n_sent = (int)sent_l1.size();
 
+    mark("tiles");
     // ---- partial-sum slots, sorted by reduction target
     // (tile, sample) M / g partials: per sample, its tiles in tile order
     std::vector<int> mcnt(n_smp + 1, 0);
@@ -666,6 +739,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     std::vector<int> pri_a, pri_b;
     for (auto& e : pri) { pri_a.push_back(e.kf_a); pri_b.push_back(e.kf_b); }
 
+    mark("slots/state");
     // ---- device upload
     DevProblem& D = p->D;
     D.n_kf = n_kfs; D.n_kf_user = n_kf; D.n_eprior = n_ext; D.n_lm = nl; D.n_obs = n_obs; D.n_gp = (int)gp_a.size(); D.n_pairs = n_pairs;
@@ -737,6 +811,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.sslab = dalloc<double>(p, (size_t)144 * std::max(n_sslots, 1));
     D.gpslab = dalloc<double>(p, (size_t)12 * std::max(n_gpslots, 1));
     const int npad = (p->np + CHOL_NB - 1) / CHOL_NB * CHOL_NB;
+    mark("upload");
     // ---- dense solve layout.  Envelope of S at panel granularity (per CHOL_NB panel of rows, the
     // first panel any of its rows has a structural non-zero in), then a one-level nested-dissection
     // ordering of the panels: [left | right | separator], where the right block's rows do not touch
@@ -1014,6 +1089,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         D.lbuf[s] = p->lst[s];
     }
     HIPCHK(hipMemset(D.ctl, 0, sizeof(LMCtl)));
+    mark("solve layout");
     p->cur = 0;
     p->has_problem = true;
     p->gps_fresh[0] = p->gps_fresh[1] = false;
@@ -1160,8 +1236,10 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
     c.early_stop = p->cfg.early_stop;
     c.result = LBA_RESULT_OK;
     launch_ctl_init(D, c, p->stream);
-    // starting state: poses + GP samples (with the Jacobian factors the first linearisation uses), chi2
-    launch_gp_prep(D, p->cur, 1, GATE_NONE, p->stream);
+    // starting state: poses + GP samples (with the Jacobian factors the first linearisation uses; a
+    // previous queue left them for both state buffers), chi2
+    if (!p->gps_fresh[p->cur]) launch_gp_prep(D, p->cur, 1, GATE_NONE, p->stream);
+    p->gps_fresh[p->cur] = true;
     launch_eval(D, p->cur, GATE_NONE, 0, FIN_NONE, p->stream);
     launch_fin(p, 0, FIN_INITIAL);
     int issued = 0;
@@ -1378,6 +1456,7 @@ void lba_destroy(lba_problem* p) {
     (void)hipSetDevice(p->cfg.device);
     if (p->stream) (void)hipStreamSynchronize(p->stream);
     free_all(p);
+    release_all(p);
     for (auto& e : p->ev)
         if (e) (void)hipEventDestroy(e);
     for (auto& e : p->qev)

@@ -185,7 +185,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
-    phase = None
+    phase, set_problem_ms = None, None
     if world == 1:
         # phase breakdown from a separate, untimed run with every phase evented
         prob.close()
@@ -193,6 +193,15 @@ def main():
         n_ph, st_ph = ph.optimize(args.window_iters)
         phase = {k: getattr(st_ph, k) / max(n_ph, 1) for k in ("ms_linearize", "ms_schur", "ms_solve", "ms_update_eval")}
         phase["trials"] = st_ph.trials / max(n_ph, 1)
+        # one LocalGPBA call = lba_set_problem (host preprocessing of the window + host->device upload,
+        # outside the timed region above) + optimize(window_iters): time a set_problem on the engine
+        kfs, lm, obs, pri, vel, cams = ph._keep
+        L = amc_lba.lib()
+        t_sp = time.perf_counter()
+        rc = L.lba_set_problem(ph.h, amc_lba.ptr(kfs), len(kfs), amc_lba.ptr(lm), len(lm), amc_lba.ptr(obs), len(obs),
+                               amc_lba.ptr(pri), len(pri), amc_lba.ptr(vel), len(vel), amc_lba.ptr(cams), len(cams))
+        torch.cuda.synchronize()
+        set_problem_ms = (time.perf_counter() - t_sp) * 1e3 if rc == 0 else None
         ph.close()
     if rank == 0:
         # window farm: every rank runs its own window (weak scaling); global BA: one problem (strong)
@@ -235,6 +244,11 @@ def main():
             "trials_per_step": trials / max(done, 1),
             "phases_ms_per_step": phase,
         }
+        if world == 1 and not gba:   # LocalGPBA-equivalent calls (optimize(window_iters))
+            calls = {"optimize_calls_per_s": value / args.window_iters, "set_problem_ms": set_problem_ms}
+            if set_problem_ms is not None:
+                calls["calls_per_s_with_set_problem"] = 1.0 / (args.window_iters / value + set_problem_ms * 1e-3)
+            line["localgpba_calls"] = calls
         if gba:   # roofline: rank 0's partition of the sweep
             line["roofline"]["note"] = "k_linearize of rank 0's landmark partition"
         if not args.no_cpu and world == 1 and not gba:   # (the oracle's dense LDLT of S = 60000^2 is hours)
