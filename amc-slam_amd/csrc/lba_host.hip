@@ -350,12 +350,15 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             }
     }
     std::vector<int> order;
-    for (int l = 0; l < n_lm; ++l)
-        if (lm_act[l]) order.push_back(l);
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
-        if (lmin[a] != lmin[b]) return lmin[a] < lmin[b];
-        return lmax[a] < lmax[b];
-    });
+    {   // stable order by (lmin, lmax): sort (key, index) records (INT_MAX = observed by fixed KFs only)
+        std::vector<std::pair<unsigned long long, int>> rec;
+        rec.reserve(n_lm);
+        for (int l = 0; l < n_lm; ++l)
+            if (lm_act[l]) rec.emplace_back(((unsigned long long)(unsigned)lmin[l] << 32) | (unsigned)lmax[l], l);
+        std::sort(rec.begin(), rec.end());
+        order.reserve(rec.size());
+        for (const auto& r : rec) order.push_back(r.second);
+    }
     const int nl = (int)order.size();
     p->n_lm_dev = nl;
     p->lm_orig = order;
@@ -373,19 +376,22 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     }
 
     // GP (prev KF, KF) pairs, numbered in order of first appearance; gp_of: each GP observation's pair
-    std::unordered_map<long long, int> gpmap;
-    gpmap.reserve(2 * (size_t)n_kf + 16);
+    // (per KF b a short list of its pairs: (KF a, pair index); usually one, the previous keyframe)
+    std::vector<std::vector<std::pair<int, int>>> gp_by_b(n_kf);
     std::vector<int> gp_a, gp_b, gp_of(n_obs, -1);
     for (int i = 0; i < n_obs; ++i)
         if (is_gp(obs[i].kind)) {
-            const long long key = (long long)obs[i].kf_a * n_kf + obs[i].kf_b;
-            auto it = gpmap.find(key);
-            if (it == gpmap.end()) {
-                it = gpmap.emplace(key, (int)gp_a.size()).first;
+            auto& lst = gp_by_b[obs[i].kf_b];
+            int g = -1;
+            for (const auto& e : lst)
+                if (e.first == obs[i].kf_a) { g = e.second; break; }
+            if (g < 0) {
+                g = (int)gp_a.size();
+                lst.emplace_back(obs[i].kf_a, g);
                 gp_a.push_back(obs[i].kf_a);
                 gp_b.push_back(obs[i].kf_b);
             }
-            gp_of[i] = it->second;
+            gp_of[i] = g;
         }
 
     // GP pose samples: distinct observation times per GP pair (one per camera time stamp in
@@ -428,10 +434,11 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     for (int i = 0; i < n_obs; ++i) smp_of[i] = is_gp(obs[i].kind) ? sample_of[i] : n_gps + obs[i].kf_b;
 
     // (KF, landmark) pairs, per device landmark, ascending pose block
-    std::vector<int> lm_pair0(nl + 1, 0), pair_lm, pair_kf;
-    std::vector<std::vector<int>> lm_kfs(nl);
+    std::vector<int> lm_pair0(nl + 1, 0), pair_lm, pair_kf, ks;
+    pair_lm.reserve(2 * (size_t)n_obs);
+    pair_kf.reserve(2 * (size_t)n_obs);
     for (int d = 0; d < nl; ++d) {
-        std::vector<int>& ks = lm_kfs[d];
+        ks.clear();
         for (int q = lobs0[d]; q < lobs0[d + 1]; ++q) {
             const lba_obs& o = obs[obs_of[q]];
             if (H[o.kf_b] >= 0) ks.push_back(H[o.kf_b]);
@@ -444,6 +451,19 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         for (int k : ks) { pair_lm.push_back(d); pair_kf.push_back(k); }
     }
     const int n_pairs = (int)pair_lm.size();
+    // lm_kfs[d]: the landmark's pose blocks (ascending) = its pairs' blocks
+    struct Span {
+        const int* p; size_t n;
+        const int* begin() const { return p; }
+        const int* end() const { return p + n; }
+        size_t size() const { return n; }
+        int operator[](size_t i) const { return p[i]; }
+    };
+    auto lm_kfs_at = [&](int d) { return Span{pair_kf.data() + lm_pair0[d], (size_t)(lm_pair0[d + 1] - lm_pair0[d])}; };
+    struct LmKfs {
+        decltype(lm_kfs_at)& f;
+        Span operator[](int d) const { return f(d); }
+    } lm_kfs{lm_kfs_at};
 
     mark("order/pairs");
     // ---- tiles: consecutive landmarks under the LDS limits of k_linearize / k_schur
@@ -553,7 +573,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 int ecnt[TILE_KF][TILE_KF] = {}, eid[TILE_KF][TILE_KF];
                 int lk[TILE_PAIRS];
                 for (int l = d; l < e; ++l) {
-                    const std::vector<int>& ks = lm_kfs[l];
+                    const Span ks = lm_kfs[l];
                     for (size_t a = 0; a < ks.size(); ++a) lk[a] = local(ks[a]);
                     for (size_t a = 0; a < ks.size(); ++a)
                         for (size_t b = a; b < ks.size(); ++b) ecnt[lk[a]][lk[b]]++;
@@ -575,7 +595,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 t_nsent.push_back(nen);
                 sent_list.resize(sent_r0.back());
                 for (int l = d; l < e; ++l) {
-                    const std::vector<int>& ks = lm_kfs[l];
+                    const Span ks = lm_kfs[l];
                     for (size_t a = 0; a < ks.size(); ++a) lk[a] = local(ks[a]);
                     for (size_t a = 0; a < ks.size(); ++a)
                         for (size_t b = a; b < ks.size(); ++b) {
