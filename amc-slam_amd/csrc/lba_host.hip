@@ -473,7 +473,19 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     std::vector<int> pair_r0(n_pairs + 1, 0), pair_rows, lm_r0(nl + 1, 0), lm_rows;
     std::vector<int> sent_r0(1, 0), sent_list;   // Schur entry -> (pair, pair, landmark) triples
     {
-        auto smpq = [&](int q) { return smp_of[obs_of[q]]; };
+        // per observation in device order, what the tiling reads (contiguous instead of through obs_of):
+        // pose blocks of KF b / KF a / the extrinsic (-1: none or fixed), rows, pose sample
+        std::vector<int> dhb(n_obs), dha(n_obs), dhx(n_obs), ddim(n_obs), dsmp(n_obs);
+        for (int q = 0; q < n_obs; ++q) {
+            const lba_obs& ob = obs[obs_of[q]];
+            dhb[q] = H[ob.kf_b];
+            dha[q] = is_gp(ob.kind) ? H[ob.kf_a] : -1;
+            dhx[q] = ext_block(ob);
+            ddim[q] = obs_dim(ob.kind);
+            dsmp[q] = smp_of[obs_of[q]];
+        }
+        auto smpq = [&](int q) { return dsmp[q]; };
+        std::vector<unsigned long long> tob;
         int d = 0;
         // the tile's sorted sample / KF sets grow by the landmark's new elements (counted first, inserted
         // only when the landmark fits: no per-landmark copies)
@@ -485,11 +497,11 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                                      [&](int v) { return std::binary_search(set.begin(), set.end(), v); }),
                       add.end());
         };
-        auto merge_in = [](std::vector<int>& set, const std::vector<int>& add) {
-            const size_t n0 = set.size();
-            set.insert(set.end(), add.begin(), add.end());
-            std::inplace_merge(set.begin(), set.begin() + n0, set.end());
+        auto merge_in = [](std::vector<int>& set, const std::vector<int>& add) {   // (no temporary buffers)
+            for (int v : add) set.insert(std::lower_bound(set.begin(), set.end(), v), v);
         };
+        uni.reserve(TILE_KF + 8);
+        usm.reserve(TILE_SMP + 8);
         while (d < nl) {
             int nobs = 0, rows = 0, npair = 0, nlmt = 0, nent = 0;
             uni.clear();
@@ -500,10 +512,9 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 int no = lobs0[e + 1] - lobs0[e], nr = 0, ne = 0;
                 new_s.clear();
                 for (int q = lobs0[e]; q < lobs0[e + 1]; ++q) {
-                    const lba_obs& ob = obs[obs_of[q]];
-                    nr += obs_dim(ob.kind);
-                    new_s.push_back(smpq(q));
-                    ne += (H[ob.kf_b] >= 0) + (is_gp(ob.kind) && H[ob.kf_a] >= 0) + (ext_block(ob) >= 0);
+                    nr += ddim[q];
+                    new_s.push_back(dsmp[q]);
+                    ne += (dhb[q] >= 0) + (dha[q] >= 0) + (dhx[q] >= 0);
                 }
                 fresh(usm, new_s);
                 const int npl = lm_pair0[e + 1] - lm_pair0[e];
@@ -532,17 +543,18 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             for (int k : uni) tkf_list.push_back(k);
             auto local = [&](int k) { return (int)(std::lower_bound(uni.begin(), uni.end(), k) - uni.begin()); };
             // LDS rows grouped by pose sample: every sample of the tile owns one contiguous row run
-            std::vector<int> tob;
-            for (int q = lobs0[d]; q < lobs0[e]; ++q) tob.push_back(q);
-            std::stable_sort(tob.begin(), tob.end(), [&](int a, int b) { return smpq(a) < smpq(b); });
+            tob.clear();   // (sample, observation): stable by observation within a sample
+            for (int q = lobs0[d]; q < lobs0[e]; ++q) tob.push_back(((unsigned long long)(unsigned)dsmp[q] << 32) | (unsigned)q);
+            std::sort(tob.begin(), tob.end());
             t_smp0.push_back((int)tsm_smp.size());
             int row = 0;
             for (size_t i = 0; i < tob.size();) {
-                const int sm = smpq(tob[i]), r0 = row;
+                const int sm = (int)(tob[i] >> 32), r0 = row;
                 size_t j = i;
-                for (; j < tob.size() && smpq(tob[j]) == sm; ++j) {
-                    ob_row[tob[j]] = row;
-                    row += obs_dim(obs[obs_of[tob[j]]].kind);
+                for (; j < tob.size() && (int)(tob[j] >> 32) == sm; ++j) {
+                    const int q = (int)(tob[j] & 0xffffffffu);
+                    ob_row[q] = row;
+                    row += ddim[q];
                 }
                 tsm_smp.push_back(sm);
                 tsm_rows.push_back(r0 | ((row - r0) << 16));
@@ -554,15 +566,14 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 for (int q = lm_pair0[l]; q < lm_pair0[l + 1]; ++q) {
                     const int k = pair_kf[q];
                     for (int o = lobs0[l]; o < lobs0[l + 1]; ++o) {
-                        const lba_obs& ob = obs[obs_of[o]];
-                        if (H[ob.kf_b] == k) pair_rows.push_back((o - lobs0[d]) | (1 << 16));
-                        if (is_gp(ob.kind) && H[ob.kf_a] == k) pair_rows.push_back(o - lobs0[d]);
-                        if (ext_block(ob) == k) pair_rows.push_back((o - lobs0[d]) | (2 << 16));
+                        if (dhb[o] == k) pair_rows.push_back((o - lobs0[d]) | (1 << 16));
+                        if (dha[o] == k) pair_rows.push_back(o - lobs0[d]);
+                        if (dhx[o] == k) pair_rows.push_back((o - lobs0[d]) | (2 << 16));
                     }
                     pair_r0[q + 1] = (int)pair_rows.size();
                 }
                 for (int o = lobs0[l]; o < lobs0[l + 1]; ++o)
-                    for (int r = 0; r < obs_dim(obs[obs_of[o]].kind); ++r) lm_rows.push_back(ob_row[o] + r);
+                    for (int r = 0; r < ddim[o]; ++r) lm_rows.push_back(ob_row[o] + r);
                 lm_r0[l + 1] = (int)lm_rows.size();
             }
             // Schur entries: every (k1 <= k2) pose-block pair co-observed by a landmark of the tile, in
