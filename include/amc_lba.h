@@ -114,7 +114,9 @@ typedef struct lba_cam {    /* GeometricCamera (Pinhole) + MultiKeyFrame::mTbc[c
      * the LBA_MONO_GP observations of the camera (EdgeMonoGPExtrinsic, src/G2oTypes.cc:241-314) link it,
      * and an EdgeExtrinsicPrior (include/G2oTypes.h:470-494) e = log(Rbc_ini^-1 Rbc), information
      * rbc_info, is attached to it.  0: fixed, as in every call without bExtrinsic (the prior is then
-     * inactive: all its vertices are fixed). */
+     * inactive: all its vertices are fixed).  Not with a partitioned problem (LBA_E_LIMIT), and an
+     * LBA_STEREO_GP observation of such a camera is rejected (EdgeStereoGP projects through the static
+     * MultiKeyFrame::mTbc, not the vertex). */
     int32_t ext_free;
     int32_t pad;
     double  rbc_ini[4];     /* MultiFrame::mRbc_ini[c] (x,y,z,w), float values widened (Frame.cc:181) */
