@@ -487,19 +487,10 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         auto smpq = [&](int q) { return dsmp[q]; };
         std::vector<unsigned long long> tob;
         int d = 0;
-        // the tile's sorted sample / KF sets grow by the landmark's new elements (counted first, inserted
-        // only when the landmark fits: no per-landmark copies)
+        // the tile's sample / KF sets grow by the landmark's new elements, found through membership marks
+        // (1: in the tile, 2: new for the landmark being tried); uni is sorted once the tile is closed
         std::vector<int> uni, usm, new_s, new_k;
-        auto fresh = [](const std::vector<int>& set, std::vector<int>& add) {   // add := sorted unique \ set
-            std::sort(add.begin(), add.end());
-            add.erase(std::unique(add.begin(), add.end()), add.end());
-            add.erase(std::remove_if(add.begin(), add.end(),
-                                     [&](int v) { return std::binary_search(set.begin(), set.end(), v); }),
-                      add.end());
-        };
-        auto merge_in = [](std::vector<int>& set, const std::vector<int>& add) {   // (no temporary buffers)
-            for (int v : add) set.insert(std::lower_bound(set.begin(), set.end(), v), v);
-        };
+        std::vector<char> kmark((size_t)std::max(n_pb, 1), 0), smark((size_t)std::max(n_smp, 1), 0);
         uni.reserve(TILE_KF + 8);
         usm.reserve(TILE_SMP + 8);
         while (d < nl) {
@@ -511,20 +502,22 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             while (e < nl) {
                 int no = lobs0[e + 1] - lobs0[e], nr = 0, ne = 0;
                 new_s.clear();
+                new_k.clear();
                 for (int q = lobs0[e]; q < lobs0[e + 1]; ++q) {
                     nr += ddim[q];
-                    new_s.push_back(dsmp[q]);
+                    if (!smark[dsmp[q]]) { smark[dsmp[q]] = 2; new_s.push_back(dsmp[q]); }
                     ne += (dhb[q] >= 0) + (dha[q] >= 0) + (dhx[q] >= 0);
                 }
-                fresh(usm, new_s);
+                for (int k : lm_kfs[e])
+                    if (!kmark[k]) { kmark[k] = 2; new_k.push_back(k); }
                 const int npl = lm_pair0[e + 1] - lm_pair0[e];
-                new_k.assign(lm_kfs[e].begin(), lm_kfs[e].end());
-                fresh(uni, new_k);
                 const int ncl = npl * (npl + 1) / 2;
                 const bool fits = nobs + no <= TILE_OBS && rows + nr <= TILE_ROWS && npair + npl <= TILE_PAIRS &&
                                   nlmt + 1 <= TILE_LMS && (int)(uni.size() + new_k.size()) <= TILE_KF &&
                                   (int)(usm.size() + new_s.size()) <= TILE_SMP && ncomb + ncl <= TILE_SLIST &&
                                   nent + ne <= TILE_PROWS;
+                for (int v : new_s) smark[v] = fits ? 1 : 0;
+                for (int k : new_k) kmark[k] = fits ? 1 : 0;
                 if (!fits) {
                     if (e == d)
                         throw ApiError{LBA_E_LIMIT, "landmark " + std::to_string(order[e]) +
@@ -532,10 +525,13 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     break;
                 }
                 nobs += no; rows += nr; npair += npl; nlmt += 1; ncomb += ncl; nent += ne;
-                merge_in(usm, new_s);
-                merge_in(uni, new_k);
+                usm.insert(usm.end(), new_s.begin(), new_s.end());
+                uni.insert(uni.end(), new_k.begin(), new_k.end());
                 ++e;
             }
+            for (int v : usm) smark[v] = 0;
+            for (int k : uni) kmark[k] = 0;
+            std::sort(uni.begin(), uni.end());
             t_obs0.push_back(lobs0[d]); t_nobs.push_back(nobs);
             t_lm0.push_back(d); t_nlm.push_back(nlmt);
             t_pair0.push_back(lm_pair0[d]); t_npair.push_back(npair);
