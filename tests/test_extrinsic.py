@@ -156,3 +156,24 @@ def test_gpu_extrinsic_optimize_matches_oracle(name):
     assert np.array_equal(cam["q"][3], win.cams["q"][3])   # the reference camera stays fixed
     _, _, ok = p.eval()
     np.testing.assert_array_equal(ok, o.depth_ok())
+
+
+@pytest.mark.gpu
+def test_gpu_extrinsic_argument_errors():
+    """EdgeStereoGP projects through the static MultiKeyFrame::mTbc, so a stereo GP observation of a camera
+    with a free extrinsic is rejected (LBA_E_ARG); a partitioned problem does not take free extrinsics
+    (LBA_E_LIMIT)."""
+    from amc_lba import Group, LbaError, Problem
+    from amc_lba.abi import LBA_E_ARG, LBA_E_LIMIT, STEREO_GP
+    win = _ext_win(stereo_frac=0.0)
+    bad = replace(win, obs=win.obs.copy())
+    i = int(np.nonzero(bad.obs["kind"] == 0)[0][0])
+    bad.obs["kind"][i] = STEREO_GP
+    with pytest.raises(LbaError) as ei:
+        Problem(bad)
+    assert ei.value.code == LBA_E_ARG
+    g = Group(2)   # (a single rank is not partitioned; the check fails before any collective)
+    with pytest.raises(LbaError) as ei:
+        Problem(win, group=g, rank=0)
+    assert ei.value.code == LBA_E_LIMIT
+    g.close()
