@@ -47,6 +47,7 @@ def lib():
         L.lba_get_state.argtypes = [vp, vp, _dp]
         L.lba_set_state.argtypes = [vp, vp, _dp]
         L.lba_eval.argtypes = [vp, _dp, _dp, vp]
+        L.lba_trial_chi2.argtypes = [vp, _dp]
         L.lba_linearize.argtypes = [vp, _dp, _dp, _dp, _dp]
         L.lba_solve_step.argtypes = [vp, ctypes.c_double, _dp]
         L.lba_set_config.argtypes = [vp, ctypes.POINTER(LbaConfig)]
@@ -64,7 +65,7 @@ def lib():
 
 def exported_symbols():
     return ["lba_abi_version", "lba_create", "lba_destroy", "lba_last_error", "lba_set_config", "lba_set_problem",
-            "lba_optimize", "lba_get_state", "lba_set_state", "lba_eval", "lba_linearize", "lba_solve_step",
+            "lba_optimize", "lba_get_state", "lba_set_state", "lba_eval", "lba_trial_chi2", "lba_linearize", "lba_solve_step",
             "lba_pose_dim", "lba_set_partition", "lba_rccl_unique_id", "lba_set_partition_rccl", "lba_group_create",
             "lba_group_destroy", "lba_set_partition_group", "lba_get_cams"]
 
@@ -182,6 +183,13 @@ class Problem:
         ok = np.zeros(self.n_obs, np.uint8)
         self._check(lib().lba_eval(self.h, ctypes.byref(chi), _d(c2), ptr(ok)))
         return chi.value, c2, ok
+
+    def trial_chi2(self):
+        """Per-observation chi2 of the last computed errors (after optimize: its last trial state,
+        g2o's e->chi2()), nothing re-evaluated (lba_trial_chi2)."""
+        c2 = np.zeros(self.n_obs)
+        self._check(lib().lba_trial_chi2(self.h, _d(c2)))
+        return c2
 
     def linearize(self):
         np_ = self.pose_dim

@@ -68,7 +68,8 @@ class LbaStats(ctypes.Structure):
         ("ms_total", ctypes.c_double),
         ("ms_k_linearize", ctypes.c_double),
         ("n_k_linearize", ctypes.c_int32),
-        ("pad", ctypes.c_int32),
+        ("n_k_solve", ctypes.c_int32),
+        ("ms_k_solve", ctypes.c_double),
     ]
 
     def as_dict(self):

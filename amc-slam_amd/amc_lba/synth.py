@@ -151,10 +151,14 @@ class Window:
 
 
 def make_window(n_opt_kf=50, n_fixed=1, n_lm=20000, obs_per_lm=6, n_cam=4, gp=True, stereo_frac=0.5,
-                outlier_frac=0.05, seed=20250912, global_ba=False, perturb=True, t0=100.0, name=""):
+                outlier_frac=0.05, seed=20250912, global_ba=False, perturb=True, t0=100.0, name="",
+                track=None, max_track=40, band=25):
     """Build one window.  n_fixed KFs come first (oldest); global_ba=True gives the
     BundleAdjustment graph shape (priors from the first KF, Huber 21.026 on priors, lambda0
-    1e-5, src/Optimizer.cc:61-321)."""
+    1e-5, src/Optimizer.cc:61-321).  Landmarks are seen from a band of `band` KFs around their
+    anchor; track=None draws obs_per_lm +- 2 observations per landmark, track="geometric" a
+    long-tailed track length 2 + Geometric(1 / (obs_per_lm - 1)) capped at max_track (long tracks:
+    landmarks seen from more keyframes than one tile of the device path holds)."""
     rng = np.random.default_rng(seed)
     n_kf = n_fixed + n_opt_kf
     kf_t = t0 + 0.1 * np.arange(n_kf)
@@ -199,7 +203,7 @@ def make_window(n_opt_kf=50, n_fixed=1, n_lm=20000, obs_per_lm=6, n_cam=4, gp=Tr
     Xw = np.einsum("nij,nj->ni", Rwc[k0, c0], Xc0) + pwc[k0, c0]
 
     # --- visibility over a KF band around the anchor (chunked over landmarks to bound memory)
-    band = min(n_kf, 25)
+    band = min(n_kf, band)
     koff = np.arange(band) - band // 2
     kk = np.clip(k0[:, None] + koff[None, :], 0, n_kf - 1)                 # [nl, band]
     kk_valid = (k0[:, None] + koff[None, :] >= 0) & (k0[:, None] + koff[None, :] < n_kf)
@@ -226,7 +230,10 @@ def make_window(n_opt_kf=50, n_fixed=1, n_lm=20000, obs_per_lm=6, n_cam=4, gp=Tr
     score = np.where(vis, score, np.inf).reshape(nl_gen, -1)
     order = np.argsort(score, axis=1, kind="stable")
     nvalid = np.isfinite(score).sum(axis=1)
-    target = rng.integers(obs_per_lm - 2, obs_per_lm + 3, nl_gen)
+    if track == "geometric":
+        target = np.minimum(max_track, 2 + rng.geometric(1.0 / max(obs_per_lm - 1, 1), nl_gen))
+    else:
+        target = rng.integers(obs_per_lm - 2, obs_per_lm + 3, nl_gen)
     take = np.minimum(target, nvalid)
     keep = np.nonzero(take >= 2)[0][:n_lm]
     if keep.size < n_lm:

@@ -44,7 +44,7 @@ constexpr int SM_STRIDE = 27;       // per (tile, sample) partial: M = sum rho' 
                                     // row-major) and g = sum rho' w J1^T e (6)
 constexpr int TILE_SMP = 64;        // pose samples per tile (k_linearize stages their row runs)
 constexpr int TILE_PROWS = 2 * TILE_OBS;    // pair entry-list entries per tile (each obs feeds <= 2 pairs)
-constexpr int TILE_SLIST = 1024;    // Schur (pair, pair, landmark) triples per tile (k_schur stages them)
+constexpr int LS_MFMA_CAP = 320;    // S-partial MFMA steps per tile (k_lin_schur: upper 16 x 16 output tiles x K / 8)
 constexpr int TILE_SENT = TILE_KF * (TILE_KF + 1) / 2;   // KF-pair Schur entries per tile
 
 constexpr int CHOL_NB = 32;         // Cholesky panel / tile width
@@ -111,7 +111,23 @@ struct DevProblem {
     int n_eprior;           // EdgeExtrinsicPrior edges (one per free extrinsic), slab entries after the velocity edges
     const int* ep_kf;       // per extrinsic prior: its KF slot
     const double* ep_data;  // per extrinsic prior: [16] R_ini^-1 quaternion (4), information (9)
-    // tiles
+    // tiles: [0, n_stiles) regular tiles (linearised and eliminated by k_lin_schur), then
+    // [n_stiles, n_tiles) the segments of the heavy landmarks (linearised like tiles; their Hll / bl
+    // partials go to landmark slots n_lm + segment, their Hpl partials to segment pairs n_pairs ..)
+    int n_stiles;
+    // heavy landmarks (too many observations / keyframes for one tile; device indices n_lm - n_heavy ..
+    // n_lm - 1): one k_expand work item each merges the segments' partials and eliminates the landmark
+    int n_heavy;
+    const int* hv_lm;       // [n_heavy] device landmark
+    const int* hv_seg0;     // [n_heavy + 1] segments (landmark slots n_lm + s)
+    const int* hv_hp0;      // [n_heavy + 1] heavy pairs: hp = hv_hp0[h] + i is canonical pair lm_pair0[lm] + i
+    const int* hp_src0;     // [n_hpairs + 1] CSR into hp_src: the segment pairs summing into a heavy pair
+    const int* hp_src;
+    const int* hp_gslot;    // [n_hpairs] gpslab slot of the heavy pair's rhs partial
+    const int* hv_ss0;      // [n_heavy + 1] sslab slots of the landmark's KF-pair blocks (a <= b, a-major)
+    const int* hv_sslot;
+    double* Vh;             // [n_hpairs][36] V = Hpl Dinv of the heavy pairs (scratch)
+    const int* pair_lk;     // per pair of a regular tile: tile-local KF | tile-local landmark << 8
     const int* tile_obs0;
     const int* tile_nobs;
     const int* tile_lm0;
@@ -126,8 +142,6 @@ struct DevProblem {
     const int* tile_kf0;
     const int* tile_nkf;
     const int* tkf_list;    // tile KF unions (pose block indices)
-    const int* sent_r0;     // [n_sentries + 1] CSR into sent_list
-    const int* sent_list;   // per entry: landmarks coupling k1, k2: pair1 | pair2 << 8 | lm << 16 (tile-local)
     const int* sent_l1;     // per Schur entry: tile-local KF index of k1 / k2
     const int* sent_l2;
     // pairs / landmarks
@@ -225,6 +239,7 @@ struct DevProblem {
     double* hfin;           // host-mapped coherent [4] copy of fin + [4] sequence number (as bits)
     double* ob_chi2;        // [n_obs]
     double* ob_res;         // [n_obs][3]
+    unsigned char* depth_ok;   // [n_obs] isDepthPositive flags (lba_eval)
     // partitioned global BA (lba_set_partition): this rank holds a subset of the landmarks; the
     // reduced system, b_p and the trial sums are summed over the ranks by the caller's all-reduce
     int part_rank, part_n;  // rank / ranks (part_n 0: not partitioned)
@@ -246,14 +261,19 @@ void launch_gp_prep(const DevProblem& P, int sel, int jac, int gate, hipStream_t
 // e0 / e1 (optional): timing events attached to the k_linearize dispatch itself
 // edges: also the motion-prior / velocity / extrinsic-prior quadratic forms of launch_prior_lin, as extra
 // workgroups after the tiles (the pose samples' part then comes with launch_schur(psel, pgate))
-void launch_linearize(const DevProblem& P, int sel, int write_res, int gate, hipStream_t s, hipEvent_t e0 = nullptr,
-                      hipEvent_t e1 = nullptr, int edges = 0);
-void launch_prior_lin(const DevProblem& P, int sel, int gate, hipStream_t s);
-// psel / pgate >= 0: the prior / sample reduction of launch_prior_lin(psel, pgate) in the same launch
-void launch_schur(const DevProblem& P, double lambda, int gate, hipStream_t s, int psel = 0, int pgate = -1);
+// linearisation of every tile (+ with LS_SCHUR the landmark elimination into the S / rhs partials), the
+// motion-prior / velocity / extrinsic-prior quadratic forms with LS_EDGES, residuals out with LS_RES;
+// lambda: the damping (LAMBDA_CTL: the controller's); e0 / e1 (optional): events on the dispatch itself
+enum { LS_SCHUR = 1, LS_EDGES = 2, LS_RES = 4 };
+void launch_lin_schur(const DevProblem& P, int sel, int gate, double lambda, int mode, hipStream_t s,
+                      hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+// pose-sample expansion (N^T M N into the Hpp / b_p slabs) and the heavy landmarks (merge of their segments;
+// with schur also their elimination)
+void launch_expand(const DevProblem& P, int sel, int gate, double lambda, int schur, hipStream_t s);
 enum { ASM_SCHUR = 1, ASM_FULL = 2 };
 void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hipStream_t s);
-void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s);
+void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s, hipEvent_t e0 = nullptr,
+                           hipEvent_t e1 = nullptr);
 // the step + trial state + the trial state's pose samples (jac: with their Jacobian factors)
 void launch_update(const DevProblem& P, double lambda, int sel, int gate, int jac, hipStream_t s);
 // partitioned mode: this rank's trial sums into red4; envelope of S + bS + b_p into / out of env_buf

@@ -34,7 +34,7 @@ struct lba_problem {
     lba_config cfg{};
     std::string err;
     hipStream_t stream = nullptr;
-    hipEvent_t ev[8] = {};
+    hipEvent_t ev[10] = {};
     bool has_problem = false;
     bool linearized = false;
     int n_kf = 0, n_lm = 0, n_obs = 0, n_cam = 0;
@@ -80,6 +80,8 @@ struct lba_problem {
     lba_allreduce_fn red_fn = nullptr;
     void* red_user = nullptr;
     ncclComm_t comm = nullptr;        // owned when set by lba_set_partition_rccl
+    double* d_status = nullptr;       // set-up status word of the partition (part_status)
+    bool status_entered = false;      // this set_problem has reached the status all-reduce
     void* group_slot = nullptr;       // owned (rank, group) record of lba_set_partition_group
 };
 
@@ -107,6 +109,28 @@ struct ApiError {
 void preduce(lba_problem* p, double* buf, int64_t n) {
     if (p->red_fn(buf, n, (void*)p->stream, p->red_user) != 0)
         throw ApiError{LBA_E_HIP, "partition all-reduce failed"};
+}
+
+// Partitioned set-up: every rank reports the outcome of its host preprocessing in one all-reduce at a
+// fixed point ahead of the first collective, so a rank that failed (argument check, tile limits ...)
+// releases its peers instead of leaving them in a collective it never reaches: every rank then fails.
+void part_status(lba_problem* p, int failed) {
+    p->status_entered = true;
+    const double v = failed ? 1.0 : 0.0;
+    HIPCHK(hipMemcpy(p->d_status, &v, sizeof(double), hipMemcpyHostToDevice));
+    preduce(p, p->d_status, 1);
+    HIPCHK(hipStreamSynchronize(p->stream));
+    double sum = 0.0;
+    HIPCHK(hipMemcpy(&sum, p->d_status, sizeof(double), hipMemcpyDeviceToHost));
+    if (sum != 0.0 && !failed) throw ApiError{LBA_E_ARG, "another rank of the partition failed its set-up"};
+}
+// a failing set-up that has not reached the status point yet reports its failure there
+void release_peers(lba_problem* p) {
+    if (p->part_n <= 0 || p->status_entered || !p->d_status) return;
+    try {
+        part_status(p, 1);
+    } catch (...) {
+    }
 }
 
 // LBA_PHASE_TIMING=<file>: dump the per-workgroup phase stamps of the last k_linearize / k_schur
@@ -273,6 +297,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                      std::chrono::duration<double, std::milli>(now - tlast).count());
         tlast = now;
     };
+    p->status_entered = false;
     if (p->stream) HIPCHK(hipStreamSynchronize(p->stream));   // (the buffers are reused below)
     free_all(p);
     p->n_kf = n_kf; p->n_lm = n_lm; p->n_obs = n_obs; p->n_cam = n_cam;
@@ -336,45 +361,6 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         throw ApiError{LBA_E_LIMIT, "the L^-1-tile solve is limited to pose systems of 6144"};
     const std::vector<int>& H = p->kf_hidx;
 
-    // ---- device landmark order: by the span of non-fixed KFs observing them
-    std::vector<int> lmin(n_lm, INT_MAX), lmax(n_lm, INT_MAX);
-    std::vector<int> lcnt(n_lm, 0);
-    for (int i = 0; i < n_obs; ++i) {
-        const lba_obs& o = obs[i];
-        lcnt[o.lm]++;
-        int ks[2] = {H[o.kf_b], is_gp(o.kind) ? H[o.kf_a] : -1};
-        for (int k : ks)
-            if (k >= 0) {
-                lmin[o.lm] = lmin[o.lm] == INT_MAX ? k : std::min(lmin[o.lm], k);
-                lmax[o.lm] = lmax[o.lm] == INT_MAX ? k : std::max(lmax[o.lm], k);
-            }
-    }
-    std::vector<int> order;
-    {   // stable order by (lmin, lmax): sort (key, index) records (INT_MAX = observed by fixed KFs only)
-        std::vector<std::pair<unsigned long long, int>> rec;
-        rec.reserve(n_lm);
-        for (int l = 0; l < n_lm; ++l)
-            if (lm_act[l]) rec.emplace_back(((unsigned long long)(unsigned)lmin[l] << 32) | (unsigned)lmax[l], l);
-        std::sort(rec.begin(), rec.end());
-        order.reserve(rec.size());
-        for (const auto& r : rec) order.push_back(r.second);
-    }
-    const int nl = (int)order.size();
-    p->n_lm_dev = nl;
-    p->lm_orig = order;
-    p->lm_dev.assign(n_lm, -1);
-    for (int d = 0; d < nl; ++d) p->lm_dev[order[d]] = d;
-
-    // observations grouped by device landmark (stable)
-    std::vector<int> lobs0(nl + 1, 0);
-    for (int i = 0; i < n_obs; ++i) lobs0[p->lm_dev[obs[i].lm] + 1]++;
-    for (int d = 0; d < nl; ++d) lobs0[d + 1] += lobs0[d];
-    std::vector<int> obs_of(n_obs);
-    {
-        std::vector<int> fill(lobs0.begin(), lobs0.end() - 1);
-        for (int i = 0; i < n_obs; ++i) obs_of[fill[p->lm_dev[obs[i].lm]]++] = i;
-    }
-
     // GP (prev KF, KF) pairs, numbered in order of first appearance; gp_of: each GP observation's pair
     // (per KF b a short list of its pairs: (KF a, pair index); usually one, the previous keyframe)
     std::vector<std::vector<std::pair<int, int>>> gp_by_b(n_kf);
@@ -433,6 +419,89 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     std::vector<int> smp_of(n_obs);
     for (int i = 0; i < n_obs; ++i) smp_of[i] = is_gp(obs[i].kind) ? sample_of[i] : n_gps + obs[i].kf_b;
 
+    // ---- heavy landmarks: a landmark whose observations / keyframes exceed one tile of k_lin_schur (a
+    //      long track: LocalGPBA adds every observation of a local point, up to every keyframe of the
+    //      window plus GP observations from non-keyframes, src/Optimizer.cc:1050-1200) is linearised in
+    //      segment tiles and merged / eliminated by k_expand (heavy_item); heavy landmarks go last in
+    //      device order.  tile_fits: the LDS limits of one k_lin_schur workgroup, and a cap on its dense
+    //      S-partial product (12 nkf x 12 nkf over K = 3 nlm, phase 6)
+    auto mfma_steps = [](int nkf, int nlm) {
+        const int nt = (12 * nkf + 15) / 16;
+        return nt * (nt + 1) / 2 * ((3 * nlm + 7) / 8);
+    };
+    auto tile_fits = [&](int no, int nr, int npair, int nlmt, int nkf, int ns, int ne) {
+        return no <= TILE_OBS && nr <= TILE_ROWS && npair <= TILE_PAIRS && nlmt <= TILE_LMS && nkf <= TILE_KF &&
+               ns <= TILE_SMP && ne <= TILE_PROWS && mfma_steps(nkf, nlmt) <= LS_MFMA_CAP;
+    };
+    // observations by original landmark (stable)
+    std::vector<int> lo0(n_lm + 1, 0), lo_of(n_obs);
+    for (int i = 0; i < n_obs; ++i) lo0[obs[i].lm + 1]++;
+    for (int l = 0; l < n_lm; ++l) lo0[l + 1] += lo0[l];
+    {
+        std::vector<int> fill(lo0.begin(), lo0.end() - 1);
+        for (int i = 0; i < n_obs; ++i) lo_of[fill[obs[i].lm]++] = i;
+    }
+    // per landmark: the span of non-fixed KFs observing it (device order key), heavy or not
+    std::vector<int> lmin(n_lm, INT_MAX), lmax(n_lm, INT_MAX);
+    std::vector<char> heavy(n_lm, 0);
+    {
+        std::vector<int> kl, sl;
+        for (int l = 0; l < n_lm; ++l) {
+            if (!lm_act[l]) continue;
+            kl.clear();
+            sl.clear();
+            int nr = 0, ne = 0;
+            for (int q = lo0[l]; q < lo0[l + 1]; ++q) {
+                const lba_obs& o = obs[lo_of[q]];
+                const int hb = H[o.kf_b], ha = is_gp(o.kind) ? H[o.kf_a] : -1, hx = ext_block(o);
+                for (int k : {hb, ha})
+                    if (k >= 0) {
+                        lmin[l] = lmin[l] == INT_MAX ? k : std::min(lmin[l], k);
+                        lmax[l] = lmax[l] == INT_MAX ? k : std::max(lmax[l], k);
+                    }
+                if (hb >= 0) kl.push_back(hb);
+                if (ha >= 0) kl.push_back(ha);
+                if (hx >= 0) kl.push_back(hx);
+                ne += (hb >= 0) + (ha >= 0) + (hx >= 0);
+                nr += obs_dim(o.kind);
+                sl.push_back(smp_of[lo_of[q]]);
+            }
+            std::sort(kl.begin(), kl.end());
+            const int npl = (int)(std::unique(kl.begin(), kl.end()) - kl.begin());
+            std::sort(sl.begin(), sl.end());
+            const int ns = (int)(std::unique(sl.begin(), sl.end()) - sl.begin());
+            heavy[l] = !tile_fits(lo0[l + 1] - lo0[l], nr, npl, 1, npl, ns, ne);
+        }
+    }
+    std::vector<int> order;
+    int n_heavy_lm = 0;
+    {   // stable order by (heavy, lmin, lmax): sort (key, index) records (INT_MAX = observed by fixed KFs only)
+        std::vector<std::pair<unsigned long long, int>> rec;
+        rec.reserve(n_lm);
+        for (int l = 0; l < n_lm; ++l)
+            if (lm_act[l]) {
+                rec.emplace_back(((unsigned long long)heavy[l] << 62) | ((unsigned long long)(unsigned)lmin[l] << 31) |
+                                     (unsigned)lmax[l], l);
+                n_heavy_lm += heavy[l];
+            }
+        std::sort(rec.begin(), rec.end());
+        order.reserve(rec.size());
+        for (const auto& r : rec) order.push_back(r.second);
+    }
+    const int nl = (int)order.size(), n_reg = nl - n_heavy_lm;
+    p->n_lm_dev = nl;
+    p->lm_orig = order;
+    p->lm_dev.assign(n_lm, -1);
+    for (int d = 0; d < nl; ++d) p->lm_dev[order[d]] = d;
+
+    // observations grouped by device landmark (stable)
+    std::vector<int> lobs0(nl + 1, 0), obs_of(n_obs);
+    for (int d = 0; d < nl; ++d) {
+        const int l = order[d];
+        lobs0[d + 1] = lobs0[d] + (lo0[l + 1] - lo0[l]);
+        std::copy(lo_of.begin() + lo0[l], lo_of.begin() + lo0[l + 1], obs_of.begin() + lobs0[d]);
+    }
+
     // (KF, landmark) pairs, per device landmark, ascending pose block
     std::vector<int> lm_pair0(nl + 1, 0), pair_lm, pair_kf, ks;
     pair_lm.reserve(2 * (size_t)n_obs);
@@ -466,12 +535,17 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     } lm_kfs{lm_kfs_at};
 
     mark("order/pairs");
-    // ---- tiles: consecutive landmarks under the LDS limits of k_linearize / k_schur
+    // ---- tiles: consecutive regular landmarks under the limits of one k_lin_schur workgroup (tile_fits),
+    //      then the segment tiles of the heavy landmarks
     std::vector<int> t_obs0, t_nobs, t_lm0, t_nlm, t_pair0, t_npair, t_smp0, t_nsmp, t_sent0, t_nsent, t_kf0, t_nkf;
     std::vector<int> tkf_list, tsm_smp, tsm_rows, sent_l1, sent_l2, sent_k1, sent_k2;
     std::vector<int> ob_row(n_obs, 0);
     std::vector<int> pair_r0(n_pairs + 1, 0), pair_rows, lm_r0(nl + 1, 0), lm_rows;
-    std::vector<int> sent_r0(1, 0), sent_list;   // Schur entry -> (pair, pair, landmark) triples
+    std::vector<int> pair_lk(std::max(n_pairs, 1), 0);   // regular pairs: tile-local KF | tile-local landmark << 8
+    // heavy landmarks: segments (landmark slots nl + s), segment pairs (pair slots n_pairs + c) and, per
+    // canonical pair of a heavy landmark, the segment pairs that sum into it
+    std::vector<int> hv_lm, hv_seg0(1, 0), hv_hp0(1, 0), hp_src0(1, 0), hp_src;
+    int n_stiles = 0, n_seg = 0, n_segpairs = 0;
     {
         // per observation in device order, what the tiling reads (contiguous instead of through obs_of):
         // pose blocks of KF b / KF a / the extrinsic (-1: none or fixed), rows, pose sample
@@ -484,63 +558,12 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             ddim[q] = obs_dim(ob.kind);
             dsmp[q] = smp_of[obs_of[q]];
         }
-        auto smpq = [&](int q) { return dsmp[q]; };
         std::vector<unsigned long long> tob;
-        int d = 0;
-        // the tile's sample / KF sets grow by the landmark's new elements, found through membership marks
-        // (1: in the tile, 2: new for the landmark being tried); uni is sorted once the tile is closed
-        std::vector<int> uni, usm, new_s, new_k;
-        std::vector<char> kmark((size_t)std::max(n_pb, 1), 0), smark((size_t)std::max(n_smp, 1), 0);
-        uni.reserve(TILE_KF + 8);
-        usm.reserve(TILE_SMP + 8);
-        while (d < nl) {
-            int nobs = 0, rows = 0, npair = 0, nlmt = 0, nent = 0;
-            uni.clear();
-            usm.clear();
-            int ncomb = 0;   // Schur triples of the tile (sum over landmarks of P (P + 1) / 2)
-            int e = d;
-            while (e < nl) {
-                int no = lobs0[e + 1] - lobs0[e], nr = 0, ne = 0;
-                new_s.clear();
-                new_k.clear();
-                for (int q = lobs0[e]; q < lobs0[e + 1]; ++q) {
-                    nr += ddim[q];
-                    if (!smark[dsmp[q]]) { smark[dsmp[q]] = 2; new_s.push_back(dsmp[q]); }
-                    ne += (dhb[q] >= 0) + (dha[q] >= 0) + (dhx[q] >= 0);
-                }
-                for (int k : lm_kfs[e])
-                    if (!kmark[k]) { kmark[k] = 2; new_k.push_back(k); }
-                const int npl = lm_pair0[e + 1] - lm_pair0[e];
-                const int ncl = npl * (npl + 1) / 2;
-                const bool fits = nobs + no <= TILE_OBS && rows + nr <= TILE_ROWS && npair + npl <= TILE_PAIRS &&
-                                  nlmt + 1 <= TILE_LMS && (int)(uni.size() + new_k.size()) <= TILE_KF &&
-                                  (int)(usm.size() + new_s.size()) <= TILE_SMP && ncomb + ncl <= TILE_SLIST &&
-                                  nent + ne <= TILE_PROWS;
-                for (int v : new_s) smark[v] = fits ? 1 : 0;
-                for (int k : new_k) kmark[k] = fits ? 1 : 0;
-                if (!fits) {
-                    if (e == d)
-                        throw ApiError{LBA_E_LIMIT, "landmark " + std::to_string(order[e]) +
-                                                        " exceeds tile limits (obs/rows/pairs/keyframes)"};
-                    break;
-                }
-                nobs += no; rows += nr; npair += npl; nlmt += 1; ncomb += ncl; nent += ne;
-                usm.insert(usm.end(), new_s.begin(), new_s.end());
-                uni.insert(uni.end(), new_k.begin(), new_k.end());
-                ++e;
-            }
-            for (int v : usm) smark[v] = 0;
-            for (int k : uni) kmark[k] = 0;
-            std::sort(uni.begin(), uni.end());
-            t_obs0.push_back(lobs0[d]); t_nobs.push_back(nobs);
-            t_lm0.push_back(d); t_nlm.push_back(nlmt);
-            t_pair0.push_back(lm_pair0[d]); t_npair.push_back(npair);
-            t_kf0.push_back((int)tkf_list.size()); t_nkf.push_back((int)uni.size());
-            for (int k : uni) tkf_list.push_back(k);
-            auto local = [&](int k) { return (int)(std::lower_bound(uni.begin(), uni.end(), k) - uni.begin()); };
-            // LDS rows grouped by pose sample: every sample of the tile owns one contiguous row run
-            tob.clear();   // (sample, observation): stable by observation within a sample
-            for (int q = lobs0[d]; q < lobs0[e]; ++q) tob.push_back(((unsigned long long)(unsigned)dsmp[q] << 32) | (unsigned)q);
+        // LDS rows of a tile's observations [q0, q1) grouped by pose sample: every sample of the tile owns
+        // one contiguous row run (stable by observation within a sample)
+        auto emit_rows = [&](int q0, int q1) {
+            tob.clear();
+            for (int q = q0; q < q1; ++q) tob.push_back(((unsigned long long)(unsigned)dsmp[q] << 32) | (unsigned)q);
             std::sort(tob.begin(), tob.end());
             t_smp0.push_back((int)tsm_smp.size());
             int row = 0;
@@ -557,65 +580,166 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 i = j;
             }
             t_nsmp.push_back((int)tsm_smp.size() - t_smp0.back());
-            // entry lists per pair (tile-local observation | side << 16) and row lists per landmark
+        };
+        // entry list of the pair of KF block k over observations [q0, q1) (tile-local observation | side << 16)
+        auto emit_pair_rows = [&](int k, int q0, int q1, int obase) {
+            for (int o = q0; o < q1; ++o) {
+                if (dhb[o] == k) pair_rows.push_back((o - obase) | (1 << 16));
+                if (dha[o] == k) pair_rows.push_back(o - obase);
+                if (dhx[o] == k) pair_rows.push_back((o - obase) | (2 << 16));
+            }
+        };
+        int d = 0;
+        // the tile's sample / KF sets grow by the landmark's new elements, found through membership marks
+        // (1: in the tile, 2: new for the landmark being tried); uni is sorted once the tile is closed
+        std::vector<int> uni, usm, new_s, new_k;
+        std::vector<char> kmark((size_t)std::max(n_pb, 1), 0), smark((size_t)std::max(n_smp, 1), 0);
+        uni.reserve(TILE_PAIRS + 8);
+        usm.reserve(TILE_SMP + 8);
+        while (d < n_reg) {
+            int nobs = 0, rows = 0, npair = 0, nlmt = 0, nent = 0;
+            uni.clear();
+            usm.clear();
+            int e = d;
+            while (e < n_reg) {
+                int no = lobs0[e + 1] - lobs0[e], nr = 0, ne = 0;
+                new_s.clear();
+                new_k.clear();
+                for (int q = lobs0[e]; q < lobs0[e + 1]; ++q) {
+                    nr += ddim[q];
+                    if (!smark[dsmp[q]]) { smark[dsmp[q]] = 2; new_s.push_back(dsmp[q]); }
+                    ne += (dhb[q] >= 0) + (dha[q] >= 0) + (dhx[q] >= 0);
+                }
+                for (int k : lm_kfs[e])
+                    if (!kmark[k]) { kmark[k] = 2; new_k.push_back(k); }
+                const int npl = lm_pair0[e + 1] - lm_pair0[e];
+                const bool fits = tile_fits(nobs + no, rows + nr, npair + npl, nlmt + 1, (int)(uni.size() + new_k.size()),
+                                            (int)(usm.size() + new_s.size()), nent + ne);
+                for (int v : new_s) smark[v] = fits ? 1 : 0;
+                for (int k : new_k) kmark[k] = fits ? 1 : 0;
+                if (!fits) {
+                    if (e == d)   // (the heavy classification above takes every landmark a tile cannot hold)
+                        throw ApiError{LBA_E_LIMIT, "internal: landmark " + std::to_string(order[e]) + " does not fit a tile"};
+                    break;
+                }
+                nobs += no; rows += nr; npair += npl; nlmt += 1; nent += ne;
+                usm.insert(usm.end(), new_s.begin(), new_s.end());
+                uni.insert(uni.end(), new_k.begin(), new_k.end());
+                ++e;
+            }
+            for (int v : usm) smark[v] = 0;
+            for (int k : uni) kmark[k] = 0;
+            std::sort(uni.begin(), uni.end());
+            t_obs0.push_back(lobs0[d]); t_nobs.push_back(nobs);
+            t_lm0.push_back(d); t_nlm.push_back(nlmt);
+            t_pair0.push_back(lm_pair0[d]); t_npair.push_back(npair);
+            t_kf0.push_back((int)tkf_list.size()); t_nkf.push_back((int)uni.size());
+            for (int k : uni) tkf_list.push_back(k);
+            auto local = [&](int k) { return (int)(std::lower_bound(uni.begin(), uni.end(), k) - uni.begin()); };
+            emit_rows(lobs0[d], lobs0[e]);
+            // entry lists per pair, row lists per landmark, the pairs' tile-local (KF, landmark)
             for (int l = d; l < e; ++l) {
                 for (int q = lm_pair0[l]; q < lm_pair0[l + 1]; ++q) {
-                    const int k = pair_kf[q];
-                    for (int o = lobs0[l]; o < lobs0[l + 1]; ++o) {
-                        if (dhb[o] == k) pair_rows.push_back((o - lobs0[d]) | (1 << 16));
-                        if (dha[o] == k) pair_rows.push_back(o - lobs0[d]);
-                        if (dhx[o] == k) pair_rows.push_back((o - lobs0[d]) | (2 << 16));
-                    }
+                    emit_pair_rows(pair_kf[q], lobs0[l], lobs0[l + 1], lobs0[d]);
                     pair_r0[q + 1] = (int)pair_rows.size();
+                    pair_lk[q] = local(pair_kf[q]) | ((l - d) << 8);
                 }
                 for (int o = lobs0[l]; o < lobs0[l + 1]; ++o)
                     for (int r = 0; r < ddim[o]; ++r) lm_rows.push_back(ob_row[o] + r);
                 lm_r0[l + 1] = (int)lm_rows.size();
             }
             // Schur entries: every (k1 <= k2) pose-block pair co-observed by a landmark of the tile, in
-            // (k1, k2) order, counted on a table over the tile's local KF indices; per entry the tile's
-            // landmarks coupling its two KFs (landmark order), packed as (tile-local pair of k1) |
-            // (tile-local pair of k2) << 8 | (tile-local landmark) << 16
+            // (k1, k2) order (k_lin_schur writes C's blocks of exactly these KF pairs)
             {
-                int ecnt[TILE_KF][TILE_KF] = {}, eid[TILE_KF][TILE_KF];
-                int lk[TILE_PAIRS];
+                bool co[TILE_KF][TILE_KF] = {};
+                int lk[TILE_KF];
                 for (int l = d; l < e; ++l) {
                     const Span ks = lm_kfs[l];
                     for (size_t a = 0; a < ks.size(); ++a) lk[a] = local(ks[a]);
                     for (size_t a = 0; a < ks.size(); ++a)
-                        for (size_t b = a; b < ks.size(); ++b) ecnt[lk[a]][lk[b]]++;
+                        for (size_t b = a; b < ks.size(); ++b) co[lk[a]][lk[b]] = true;
                 }
                 const int nu = (int)uni.size();
                 t_sent0.push_back((int)sent_l1.size());
                 int nen = 0;
-                std::vector<int> fill;
-                const int list0 = (int)sent_list.size();
                 for (int i = 0; i < nu; ++i)
-                    for (int j = i; j < nu; ++j) {
-                        if (!ecnt[i][j]) continue;
-                        eid[i][j] = nen++;
-                        sent_l1.push_back(i); sent_l2.push_back(j);
-                        sent_k1.push_back(uni[i]); sent_k2.push_back(uni[j]);
-                        fill.push_back((fill.empty() ? list0 : sent_r0.back()));
-                        sent_r0.push_back(fill.back() + ecnt[i][j]);
-                    }
-                t_nsent.push_back(nen);
-                sent_list.resize(sent_r0.back());
-                for (int l = d; l < e; ++l) {
-                    const Span ks = lm_kfs[l];
-                    for (size_t a = 0; a < ks.size(); ++a) lk[a] = local(ks[a]);
-                    for (size_t a = 0; a < ks.size(); ++a)
-                        for (size_t b = a; b < ks.size(); ++b) {
-                            const int t1 = lm_pair0[l] + (int)a - lm_pair0[d], t2 = lm_pair0[l] + (int)b - lm_pair0[d];
-                            sent_list[fill[eid[lk[a]][lk[b]]]++] = t1 | (t2 << 8) | ((l - d) << 16);
+                    for (int j = i; j < nu; ++j)
+                        if (co[i][j]) {
+                            ++nen;
+                            sent_l1.push_back(i); sent_l2.push_back(j);
+                            sent_k1.push_back(uni[i]); sent_k2.push_back(uni[j]);
                         }
-                }
+                t_nsent.push_back(nen);
             }
             d = e;
+        }
+        n_stiles = (int)t_obs0.size();
+        // heavy landmarks: their canonical pairs and landmark slots get no rows of their own
+        for (int q = lm_pair0[n_reg]; q < n_pairs; ++q) pair_r0[q + 1] = (int)pair_rows.size();
+        for (int l = n_reg; l < nl; ++l) lm_r0[l + 1] = (int)lm_rows.size();
+        // segments: runs of a heavy landmark's observations under the limits of k_lin_schur's phases 1-4
+        // (no elimination: no KF-union or MFMA limit; a segment's pairs are its distinct pose blocks)
+        for (int l = n_reg; l < nl; ++l) {
+            hv_lm.push_back(l);
+            const int cp0 = lm_pair0[l], ncp = lm_pair0[l + 1] - cp0;
+            std::vector<std::vector<int>> src(ncp);
+            int q0 = lobs0[l];
+            while (q0 < lobs0[l + 1]) {
+                int q1 = q0, nr = 0, ne = 0;
+                usm.clear();
+                uni.clear();
+                while (q1 < lobs0[l + 1]) {
+                    const int neq = (dhb[q1] >= 0) + (dha[q1] >= 0) + (dhx[q1] >= 0);
+                    const int ns = (int)usm.size() + !smark[dsmp[q1]];
+                    int nk = (int)uni.size();
+                    for (int k : {dhb[q1], dha[q1], dhx[q1]})
+                        if (k >= 0 && !kmark[k]) { kmark[k] = 2; ++nk; }
+                    const bool fits = q1 - q0 + 1 <= TILE_OBS && nr + ddim[q1] <= TILE_ROWS && nk <= TILE_PAIRS &&
+                                      ns <= TILE_SMP && ne + neq <= TILE_PROWS;
+                    for (int k : {dhb[q1], dha[q1], dhx[q1]})
+                        if (k >= 0 && kmark[k] == 2) {
+                            kmark[k] = fits ? 1 : 0;
+                            if (fits) uni.push_back(k);
+                        }
+                    if (!fits) break;
+                    if (!smark[dsmp[q1]]) { smark[dsmp[q1]] = 1; usm.push_back(dsmp[q1]); }
+                    nr += ddim[q1];
+                    ne += neq;
+                    ++q1;
+                }
+                for (int v : usm) smark[v] = 0;
+                for (int k : uni) kmark[k] = 0;
+                std::sort(uni.begin(), uni.end());
+                const int s = n_seg++, sp0 = n_segpairs;
+                t_obs0.push_back(q0); t_nobs.push_back(q1 - q0);
+                t_lm0.push_back(nl + s); t_nlm.push_back(1);
+                t_pair0.push_back(n_pairs + sp0); t_npair.push_back((int)uni.size());
+                t_kf0.push_back((int)tkf_list.size()); t_nkf.push_back(0);
+                t_sent0.push_back((int)sent_l1.size()); t_nsent.push_back(0);
+                emit_rows(q0, q1);
+                for (size_t c = 0; c < uni.size(); ++c) {
+                    emit_pair_rows(uni[c], q0, q1, q0);
+                    pair_r0.push_back((int)pair_rows.size());
+                    const int* kb = pair_kf.data() + cp0;
+                    src[std::lower_bound(kb, kb + ncp, uni[c]) - kb].push_back(n_pairs + sp0 + (int)c);
+                }
+                n_segpairs += (int)uni.size();
+                for (int o = q0; o < q1; ++o)
+                    for (int r = 0; r < ddim[o]; ++r) lm_rows.push_back(ob_row[o] + r);
+                lm_r0.push_back((int)lm_rows.size());
+                q0 = q1;
+            }
+            hv_seg0.push_back(n_seg);
+            for (int j = 0; j < ncp; ++j) {
+                for (int v : src[j]) hp_src.push_back(v);
+                hp_src0.push_back((int)hp_src.size());
+            }
+            hv_hp0.push_back(hv_hp0.back() + ncp);
         }
     }
     const int n_tiles = (int)t_obs0.size();
     const int n_sent = (int)sent_l1.size();
+    const int n_heavy = (int)hv_lm.size();
 
     mark("tiles");
     // ---- partial-sum slots, sorted by reduction target
@@ -697,11 +821,27 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     std::vector<int> scnt(n_ublocks + 1, 0), gpcnt(n_pb + 1, 0);
     for (int s = 0; s < n_sent; ++s) scnt[ublock_id(n_pb, sent_k1[s], sent_k2[s])]++;
     for (int k : tkf_list) gpcnt[k]++;
+    for (int h = 0; h < n_heavy; ++h) {   // a heavy landmark: every pair (a <= b) of its KFs, every KF
+        const Span ks = lm_kfs[hv_lm[h]];
+        for (size_t a = 0; a < ks.size(); ++a) {
+            gpcnt[ks[a]]++;
+            for (size_t b = a; b < ks.size(); ++b) scnt[ublock_id(n_pb, ks[a], ks[b])]++;
+        }
+    }
     std::vector<int> ss0 = prefix(scnt), gps0 = prefix(gpcnt);
     std::vector<int> sfill(ss0), gpfill(gps0);
     std::vector<int> sslot(std::max(n_sent, 1)), tkf_gslot(std::max((int)tkf_list.size(), 1));
     for (int s = 0; s < n_sent; ++s) sslot[s] = sfill[ublock_id(n_pb, sent_k1[s], sent_k2[s])]++;
     for (size_t t = 0; t < tkf_list.size(); ++t) tkf_gslot[t] = gpfill[tkf_list[t]]++;
+    std::vector<int> hv_ss0(1, 0), hv_sslot, hp_gslot;   // (after the regular tiles' slots of each target)
+    for (int h = 0; h < n_heavy; ++h) {
+        const Span ks = lm_kfs[hv_lm[h]];
+        for (size_t a = 0; a < ks.size(); ++a) {
+            hp_gslot.push_back(gpfill[ks[a]]++);
+            for (size_t b = a; b < ks.size(); ++b) hv_sslot.push_back(sfill[ublock_id(n_pb, ks[a], ks[b])]++);
+        }
+        hv_ss0.push_back((int)hv_sslot.size());
+    }
     const int n_hslots = hs0[n_ublocks], n_gslots = gs0[n_pb], n_sslots = ss0[n_ublocks], n_gpslots = gps0[n_pb];
 
 
@@ -791,7 +931,12 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.ms0 = dupload(p, ms0); D.tile_sent0 = dupload(p, t_sent0);
     D.tile_nsent = dupload(p, t_nsent); D.tile_kf0 = dupload(p, t_kf0); D.tile_nkf = dupload(p, t_nkf);
     D.tkf_list = dupload(p, tkf_list);
-    D.sent_r0 = dupload(p, sent_r0); D.sent_list = dupload(p, sent_list);
+    D.n_stiles = n_stiles; D.n_heavy = n_heavy;
+    D.hv_lm = dupload(p, hv_lm); D.hv_seg0 = dupload(p, hv_seg0); D.hv_hp0 = dupload(p, hv_hp0);
+    D.hp_src0 = dupload(p, hp_src0); D.hp_src = dupload(p, hp_src); D.hp_gslot = dupload(p, hp_gslot);
+    D.hv_ss0 = dupload(p, hv_ss0); D.hv_sslot = dupload(p, hv_sslot);
+    D.Vh = dalloc<double>(p, (size_t)36 * std::max(hv_hp0.back(), 1));
+    D.pair_lk = dupload(p, pair_lk);
     D.sent_l1 = dupload(p, sent_l1); D.sent_l2 = dupload(p, sent_l2);
     D.pair_lm = dupload(p, pair_lm); D.pair_kf = dupload(p, pair_kf); D.pair_r0 = dupload(p, pair_r0);
     D.pair_rows = dupload(p, pair_rows); D.lm_r0 = dupload(p, lm_r0); D.lm_rows = dupload(p, lm_rows);
@@ -858,6 +1003,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             for (int r = P * CHOL_NB; r < (P + 1) * CHOL_NB && r < p->np; ++r) f = std::min(f, 12 * fk[r / 12] / CHOL_NB);
             pfirst[P] = f;
         }
+        if (p->part_n > 0) part_status(p, 0);   // (every rank's preprocessing succeeded, or all throw)
         if (p->part_n > 0) {   // the union envelope of the ranks' systems (one all-reduce, at set-up)
             std::vector<double> occ((size_t)NP * NP, 0.0);
             for (int P = 0; P < NP; ++P) occ[(size_t)P * NP + pfirst[P]] = 1.0;
@@ -1077,9 +1223,9 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.npad = npad;
     D.Lm = dalloc<double>(p, (size_t)npad * npad + 1);
     D.LinvT = dalloc<double>(p, (size_t)npad * CHOL_NB + 1);
-    D.Hpl = dalloc<double>(p, (size_t)36 * std::max(n_pairs, 1));
-    D.Hll = dalloc<double>(p, (size_t)9 * std::max(nl, 1));
-    D.bl = dalloc<double>(p, (size_t)3 * std::max(nl, 1));
+    D.Hpl = dalloc<double>(p, (size_t)36 * std::max(n_pairs + n_segpairs, 1));   // canonical pairs, then segment pairs
+    D.Hll = dalloc<double>(p, (size_t)9 * std::max(nl + n_seg, 1));               // landmarks, then segments
+    D.bl = dalloc<double>(p, (size_t)3 * std::max(nl + n_seg, 1));
     D.Dinv = dalloc<double>(p, (size_t)9 * std::max(nl, 1));
     D.S = dalloc<double>(p, (size_t)npad * npad + 1);
     D.bp = dalloc<double>(p, p->np + 1);
@@ -1106,6 +1252,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.fin = dalloc<double>(p, 4);
     D.ob_chi2 = dalloc<double>(p, std::max(n_obs, 1));
     D.ob_res = dalloc<double>(p, 3 * (size_t)std::max(n_obs, 1));
+    D.depth_ok = dalloc<unsigned char>(p, std::max(n_obs, 1));
     HIPCHK(hipMemset(D.info, 0, sizeof(int)));
     for (int s = 0; s < 2; ++s) {
         p->kst[s] = dalloc<double>(p, kst.size());
@@ -1125,13 +1272,14 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
 }
 
 // ------------------------------------------------------------------------------------------------
-void linearize(lba_problem* p, int write_res, bool timed = false) {
+// computeActiveErrors + buildSystem at the current state (no elimination): H_pp / b_p pieces, Hpl,
+// Hll, bl (lba_linearize, computeLambdaInit)
+void linearize(lba_problem* p, int write_res) {
     const DevProblem& D = p->D;
     if (!p->gps_fresh[p->cur]) launch_gp_prep(D, p->cur, 1, GATE_NONE, p->stream);
     p->gps_fresh[p->cur] = true;
-    launch_linearize(D, p->cur, write_res, GATE_NONE, p->stream, timed ? p->ev[6] : nullptr,
-                     timed ? p->ev[7] : nullptr);
-    launch_prior_lin(D, p->cur, GATE_NONE, p->stream);
+    launch_lin_schur(D, p->cur, GATE_NONE, 0.0, LS_EDGES | (write_res ? LS_RES : 0), p->stream);
+    launch_expand(D, p->cur, GATE_NONE, 0.0, 0, p->stream);
     HIPCHK(hipGetLastError());
     p->linearized = true;
 }
@@ -1191,20 +1339,32 @@ void launch_fin(lba_problem* p, unsigned long long seq, int mode) {
     launch_finalize(p->D, seq, mode, p->stream);
 }
 
-// one damped solve + update into the trial buffers + evaluation of the trial state
-void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs, bool sync = true) {
+// One trial: the linearisation at the current state fused with the landmark elimination (k_lin_schur),
+// the reduced camera system, its solve, the update into the trial buffers and (evaluate) the trial
+// state's errors.  Every trial linearises: after a rejected trial the state is the same, and the
+// deterministic reductions reproduce the previous linearisation bit for bit (g2o keeps it).
+// evs: phase events [5] (LBA_FLAG_TIME_PHASES); sweep: the dispatch events of k_lin_schur (ev 6, 7)
+// and k_chol_flow (ev 8, 9).
+void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs, bool sweep, bool sync = true) {
     const DevProblem& D = p->D;
     const int nx = 1 - p->cur;
-    launch_schur(D, lambda, GATE_NONE, p->stream);   // also clears the factorisation status
-    assemble_layout(p, lambda, ASM_SCHUR);
+    if (!p->gps_fresh[p->cur]) launch_gp_prep(D, p->cur, 1, GATE_NONE, p->stream);
+    p->gps_fresh[p->cur] = true;
     if (evs) HIPCHK(hipEventRecord(evs[0], p->stream));
-    launch_cholesky_solve(D, GATE_NONE, ++p->cf_epoch, p->stream);
+    launch_lin_schur(D, p->cur, GATE_NONE, lambda, LS_SCHUR | LS_EDGES, p->stream, sweep ? p->ev[6] : nullptr,
+                     sweep ? p->ev[7] : nullptr);
     if (evs) HIPCHK(hipEventRecord(evs[1], p->stream));
+    launch_expand(D, p->cur, GATE_NONE, lambda, 1, p->stream);
+    assemble_layout(p, lambda, ASM_SCHUR);
+    if (evs) HIPCHK(hipEventRecord(evs[2], p->stream));
+    launch_cholesky_solve(D, GATE_NONE, ++p->cf_epoch, p->stream, sweep ? p->ev[8] : nullptr, sweep ? p->ev[9] : nullptr);
+    if (evs) HIPCHK(hipEventRecord(evs[3], p->stream));
     launch_update(D, lambda, p->cur, GATE_NONE, 1, p->stream);   // (+ the trial state's pose samples)
     p->gps_fresh[nx] = true;
     if (evaluate) launch_eval(D, nx, GATE_NONE, 0, FIN_NONE, p->stream);
-    if (evs) HIPCHK(hipEventRecord(evs[2], p->stream));
-    finalize_and_wait(p, sync || evs);
+    if (evs) HIPCHK(hipEventRecord(evs[4], p->stream));
+    finalize_and_wait(p, sync || evs || sweep);
+    p->linearized = false;
 }
 
 double eval_current(lba_problem* p) {
@@ -1241,10 +1401,9 @@ float elapsed(hipEvent_t a, hipEvent_t b) {
 // Queued optimisation: the same iterations as the host-driven loop in optimize() below, but the LM
 // decisions are taken on the device (k_finalize / lm_decide on the LMCtl record), so the host enqueues
 // one trial per remaining iteration without waiting for any outcome, and synchronises once per batch.
-// Launches of a queued trial take their state buffer and damping from the controller; the
-// relinearisation kernels only run when the previous trial ended an iteration (a rejected trial keeps
-// the linearisation), and k_update is a no-op once the controller is done (the other kernels of such
-// a trial only touch scratch buffers).  A batch is one trial per iteration still to run, which is exact
+// Launches of a queued trial take their state buffer and damping from the controller; every trial
+// relinearises inside k_lin_schur (see trial()), and the state-touching kernels of a trial are no-ops
+// once the controller is done (the assembly and solve of such a trial only touch scratch buffers).  A batch is one trial per iteration still to run, which is exact
 // when every trial is accepted; after rejected trials the next batch covers the rest (a trial
 // completes at most one iteration and an iteration takes at most max_trials trials, so this
 // terminates).  The starting-state evaluation and computeLambdaInit run in the queue too.
@@ -1276,32 +1435,30 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
         const int first = issued;
         const auto te0 = std::chrono::steady_clock::now();
         for (int k = 0; k < n; ++k, ++issued) {
-            // LBA_FLAG_TIME_SWEEP: events bracket every queued k_linearize launch; the trials that did
-            // relinearise are read from the controller's log afterwards
+            // LBA_FLAG_TIME_SWEEP: the dispatches of k_lin_schur and k_chol_flow carry events (their own
+            // start / end timestamps); the trials that ran are read from the controller's log afterwards
             const bool tq = tsweep && issued < HLOG_CAP;
-            if (tq && p->qev.size() < 2 * (size_t)issued + 2) {
+            if (tq && p->qev.size() < 4 * (size_t)issued + 4) {
                 const size_t old = p->qev.size();
-                p->qev.resize(std::max<size_t>(2 * (size_t)issued + 2, 2 * old));
+                p->qev.resize(std::max<size_t>(4 * (size_t)issued + 4, 2 * old));
                 for (size_t e = old; e < p->qev.size(); ++e) HIPCHK(hipEventCreate(&p->qev[e]));
             }
-            // the prior / sample reduction runs inside the linearisation's launch (edge items) and
-            // k_schur's (pose samples), filling the slots their last tiles leave idle; except before
-            // computeLambdaInit, which reads H_pp before the Schur step
-            const bool lam0 = issued == 0 && p->cfg.lambda_init <= 0;
-            launch_linearize(D, SEL_CUR, 0, GATE_LIN, p->stream, tq ? p->qev[2 * issued] : nullptr,
-                             tq ? p->qev[2 * issued + 1] : nullptr, lam0 ? 0 : 1);
-            if (lam0) {
-                launch_prior_lin(D, SEL_CUR, GATE_LIN, p->stream);
+            hipEvent_t* qe = tq ? p->qev.data() + 4 * (size_t)issued : nullptr;
+            if (issued == 0 && p->cfg.lambda_init <= 0) {   // computeLambdaInit reads H_pp / Hll of the start
+                launch_lin_schur(D, SEL_CUR, GATE_TRIAL, 0.0, LS_EDGES, p->stream);
+                launch_expand(D, SEL_CUR, GATE_TRIAL, 0.0, 0, p->stream);
                 assemble_layout(p, 0.0, ASM_FULL);
                 launch_lambda_init(D, p->cfg.tau, p->stream);
             }
-            launch_schur(D, LAMBDA_CTL, GATE_NONE, p->stream, SEL_CUR, lam0 ? -1 : GATE_LIN);
+            launch_lin_schur(D, SEL_CUR, GATE_TRIAL, LAMBDA_CTL, LS_SCHUR | LS_EDGES, p->stream, qe ? qe[0] : nullptr,
+                             qe ? qe[1] : nullptr);
+            launch_expand(D, SEL_CUR, GATE_TRIAL, LAMBDA_CTL, 1, p->stream);
             assemble_layout(p, LAMBDA_CTL, ASM_SCHUR);
-            launch_cholesky_solve(D, GATE_NONE, ++p->cf_epoch, p->stream);
-            // the step, the trial state and its pose samples with their Jacobian factors: an
-            // accepted trial's relinearisation reads them (no preparation launch)
+            launch_cholesky_solve(D, GATE_NONE, ++p->cf_epoch, p->stream, qe ? qe[2] : nullptr, qe ? qe[3] : nullptr);
+            // the step, the trial state and its pose samples with their Jacobian factors: the next
+            // trial's linearisation reads them (no preparation launch)
             launch_update(D, LAMBDA_CTL, SEL_CUR, GATE_TRIAL, 1, p->stream);
-            launch_eval(D, SEL_NEXT, GATE_NONE, 0, FIN_NONE, p->stream);
+            launch_eval(D, SEL_NEXT, GATE_TRIAL, 0, FIN_NONE, p->stream);
             launch_fin(p, ++p->fin_seq, k == n - 1 ? FIN_QUEUED_PUBLISH : FIN_QUEUED);
             HIPCHK(hipGetLastError());
         }
@@ -1315,8 +1472,10 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
             HIPCHK(hipStreamSynchronize(p->stream));
             for (int q = first; q < issued && q < HLOG_CAP; ++q)
                 if (p->h_log[q]) {
-                    s.ms_k_linearize += elapsed(p->qev[2 * q], p->qev[2 * q + 1]);
+                    s.ms_k_linearize += elapsed(p->qev[4 * q], p->qev[4 * q + 1]);
                     s.n_k_linearize += 1;
+                    s.ms_k_solve += elapsed(p->qev[4 * q + 2], p->qev[4 * q + 3]);
+                    s.n_k_solve += 1;
                 }
         }
         if (c.done || n <= 0) break;
@@ -1356,10 +1515,8 @@ int optimize(lba_problem* p, int iters, volatile const int32_t* stop, lba_stats*
     const bool tsweep = tphase || (p->cfg.flags & LBA_FLAG_TIME_SWEEP) != 0;
     for (int i = 0; i < iters; ++i) {
         if (stop && *stop) { result = LBA_RESULT_STOPPED; break; }
-        if (tphase) HIPCHK(hipEventRecord(p->ev[0], p->stream));
-        linearize(p, 0, tsweep);
-        if (tphase) HIPCHK(hipEventRecord(p->ev[1], p->stream));
         if (i == 0) {
+            if (p->cfg.lambda_init <= 0) linearize(p, 0);
             p->lambda = lambda_init(p);
             p->ni = 2.0;
             p->nBad = 0;
@@ -1367,20 +1524,19 @@ int optimize(lba_problem* p, int iters, volatile const int32_t* stop, lba_stats*
         double currentChi = 0.0, iniChi = 0.0, rho = 0.0;
         int qmax = 0;
         do {
-            trial(p, p->lambda, true, tphase ? p->ev + 2 : nullptr, false);
-            if (qmax == 0) {
-                currentChi = iniChi = p->h_fin[0];
-                if (tphase) s.ms_linearize += elapsed(p->ev[0], p->ev[1]);
-                if (tsweep) {
-                    s.ms_k_linearize += elapsed(p->ev[6], p->ev[7]);
-                    s.n_k_linearize += 1;
-                }
-            }
-            if (tphase) {
-                s.ms_schur += elapsed(qmax == 0 ? p->ev[1] : p->ev[5], p->ev[2]);
+            trial(p, p->lambda, true, tphase ? p->ev : nullptr, tsweep, false);
+            if (qmax == 0) currentChi = iniChi = p->h_fin[0];
+            if (tphase) {   // (ms_linearize: the fused linearisation + elimination)
+                s.ms_linearize += elapsed(p->ev[0], p->ev[1]);
+                s.ms_schur += elapsed(p->ev[1], p->ev[2]);
                 s.ms_solve += elapsed(p->ev[2], p->ev[3]);
                 s.ms_update_eval += elapsed(p->ev[3], p->ev[4]);
-                HIPCHK(hipEventRecord(p->ev[5], p->stream));
+            }
+            if (tsweep) {
+                s.ms_k_linearize += elapsed(p->ev[6], p->ev[7]);
+                s.n_k_linearize += 1;
+                s.ms_k_solve += elapsed(p->ev[8], p->ev[9]);
+                s.n_k_solve += 1;
             }
             double tempChi = p->h_fin[1];
             last_chi = tempChi;
@@ -1490,6 +1646,7 @@ void lba_destroy(lba_problem* p) {
         if (e) (void)hipEventDestroy(e);
     if (p->h_fin) (void)hipHostFree(p->h_fin);
     if (p->h_log) (void)hipHostFree(p->h_log);
+    if (p->d_status) (void)hipFree(p->d_status);
     if (p->comm) (void)ncclCommDestroy(p->comm);
     delete static_cast<GroupSlot*>(p->group_slot);
     if (p->stream) (void)hipStreamDestroy(p->stream);
@@ -1542,6 +1699,13 @@ int lba_set_partition(lba_problem* p, int32_t rank, int32_t nranks, lba_allreduc
     }
     p->part_rank = rank;
     p->part_n = nranks > 1 ? nranks : 0;
+    if (p->part_n > 0 && !p->d_status) {
+        (void)hipSetDevice(p->cfg.device);
+        if (hipMalloc(&p->d_status, sizeof(double)) != hipSuccess) {
+            p->err = "hipMalloc of the partition status word failed";
+            return LBA_E_HIP;
+        }
+    }
     p->red_fn = fn;
     p->red_user = user;
     return LBA_OK;
@@ -1635,7 +1799,12 @@ static int group_allreduce(double* buf, int64_t n, void* stream, void* user) {
         g->gen++;
         g->cv.notify_all();
     } else {
-        g->cv.wait(lk, [&] { return g->gen != my; });
+        // bounded: a peer that never arrives (it failed outside the set-up's status point) poisons the
+        // group instead of hanging this rank
+        if (!g->cv.wait_for(lk, std::chrono::seconds(120), [&] { return g->gen != my; })) {
+            g->bad = true;
+            return -1;
+        }
     }
     const bool bad = g->bad;
     // every rank's stream waits for the sum (the event is re-recorded only after all ranks arrive again)
@@ -1692,11 +1861,14 @@ int lba_set_problem(lba_problem* p, const lba_kf* kfs, int32_t n_kf, const doubl
         return set_problem(p, kfs, n_kf, lm_xyz, n_lm, obs, n_obs, priors, n_priors, vel_kfs, n_vel, cams, n_cam);
     } catch (const ApiError& e) {
         p->err = e.msg;
+        release_peers(p);
         free_all(p);
         return e.code;
     } catch (const HipError& e) {
+        const int rc = map_error(p, e);
+        release_peers(p);
         free_all(p);
-        return map_error(p, e);
+        return rc;
     }
 }
 
@@ -1794,14 +1966,27 @@ int lba_eval(lba_problem* p, double* chi2_robust, double* obs_chi2, uint8_t* dep
             for (int i = 0; i < p->n_obs; ++i) obs_chi2[i] = c[p->obs_dev[i]];
         }
         if (depth_ok && p->n_obs) {
-            unsigned char* d = nullptr;
-            HIPCHK(hipMalloc(&d, p->n_obs));
-            launch_depth(p->D, p->cur, d, p->stream);
+            launch_depth(p->D, p->cur, p->D.depth_ok, p->stream);
             std::vector<unsigned char> h(p->n_obs);
-            HIPCHK(hipMemcpyAsync(h.data(), d, p->n_obs, hipMemcpyDeviceToHost, p->stream));
+            HIPCHK(hipMemcpyAsync(h.data(), p->D.depth_ok, p->n_obs, hipMemcpyDeviceToHost, p->stream));
             HIPCHK(hipStreamSynchronize(p->stream));
-            (void)hipFree(d);
             for (int i = 0; i < p->n_obs; ++i) depth_ok[i] = h[p->obs_dev[i]];
+        }
+        return LBA_OK;
+    } catch (const HipError& e) {
+        return map_error(p, e);
+    }
+}
+
+int lba_trial_chi2(lba_problem* p, double* obs_chi2) {
+    if (!p || !p->has_problem || !obs_chi2) return LBA_E_ARG;
+    try {
+        HIPCHK(hipSetDevice(p->cfg.device));
+        HIPCHK(hipStreamSynchronize(p->stream));
+        if (p->n_obs) {
+            std::vector<double> c(p->n_obs);
+            HIPCHK(hipMemcpy(c.data(), p->D.ob_chi2, p->n_obs * sizeof(double), hipMemcpyDeviceToHost));
+            for (int i = 0; i < p->n_obs; ++i) obs_chi2[i] = c[p->obs_dev[i]];
         }
         return LBA_OK;
     } catch (const HipError& e) {
@@ -1864,8 +2049,7 @@ int lba_solve_step(lba_problem* p, double lambda, double* dx) {
     if (!p || !p->has_problem) return LBA_E_ARG;
     try {
         HIPCHK(hipSetDevice(p->cfg.device));
-        if (!p->linearized) linearize(p, 0);
-        trial(p, lambda, false, nullptr);
+        trial(p, lambda, false, nullptr, false);
         const int np = p->np, nl = p->D.n_lm, npx = p->np_ext;
         if (p->h_fin[3] != 0.0) {
             p->err = "reduced camera system not positive definite";

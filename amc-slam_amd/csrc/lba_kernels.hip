@@ -4,13 +4,14 @@
 // maps to:
 //   k_gp_prep        per GP pair and observation time: interpolated pose + Jacobian factor, per-KF
 //                    poses                                                  (GaussianProcess.cc:23-42)
-//   k_linearize      per tile of landmarks: residual, Huber, analytic J straight into an LDS row
-//                    buffer, then deterministic on-chip reductions into Hpp/b segment partials,
-//                    Hpl blocks and Hll/bl (BlockSolver::buildSystem, block_solver.hpp:502-560;
-//                    edge quadratic forms base_multi_edge.hpp:170-222)
-//   k_prior_lin      EdgeGaussianPrior / EdgeVelocity quadratic forms (src/G2oTypes.cc:100-118)
-//   k_schur          per tile: Dinv = (Hll + lambda I)^-1, V = Hpl Dinv, g = V bl, S partials
-//                    V(k1) Hpl(k2)^T and rhs partials                   (block_solver.hpp:381-430)
+//   k_lin_schur      per tile of landmarks: residual, Huber, analytic J straight into an LDS row
+//                    buffer, deterministic on-chip reductions into pose-sample partials, Hpl blocks and
+//                    Hll/bl (BlockSolver::buildSystem, block_solver.hpp:502-560; edge quadratic forms
+//                    base_multi_edge.hpp:170-222), then in the same workgroup the landmark elimination:
+//                    Dinv = (Hll + lambda I)^-1, S partials sum Hpl Dinv Hpl^T (fp64 MFMA) and rhs
+//                    partials (block_solver.hpp:381-430); EdgeGaussianPrior / EdgeVelocity /
+//                    EdgeExtrinsicPrior quadratic forms as extra workgroups (src/G2oTypes.cc:100-118)
+//   k_expand         per pose sample N^T M N into Hpp / b_p pieces; heavy landmarks (merge + elimination)
 //   k_assemble       S = sum Hpp partials + lambda I - sum Schur partials, b_p, bS = b_p - sum g
 //                    (block_solver.hpp:432-445)
 //   k_chol_*         blocked Cholesky + forward/back substitution of S     (linear_solver_dense.h:65-113)
@@ -347,171 +348,6 @@ __device__ __forceinline__ void smp_task(const DevProblem& P, const double* rows
 template <int NT>
 __device__ void edge_item(const DevProblem& P, int sel, int idx, const int tid, double* shm);
 
-__global__ __launch_bounds__(TILE_OBS, 3) void k_linearize(DevProblem P, int sel, int write_res, int gate) {
-    __shared__ double rows[TILE_ROWS * ROW_STRIDE];
-    __shared__ double rw[TILE_ROWS];
-    __shared__ int tsm[2 * TILE_SMP];
-    __shared__ int osm[TILE_OBS];
-    __shared__ int ocam[TILE_OBS];
-    __shared__ int orow[TILE_OBS];   // per observation: first LDS row | rows << 16
-    __shared__ int prow[TILE_PROWS];
-    __shared__ int pr0[TILE_PAIRS + 1];
-    __shared__ int lrow[TILE_ROWS];
-    __shared__ int lr0[TILE_LMS + 1];
-    __shared__ double red[TILE_OBS / 64];
-    if ((int)blockIdx.x >= P.n_tiles) {   // fused motion-prior / velocity / extrinsic-prior edge items
-        if (gated_off(P.ctl, gate)) return;
-        edge_item<TILE_OBS>(P, sel, blockIdx.x - P.n_tiles, threadIdx.x, rows);
-        return;
-    }
-    const int tile = blockIdx.x, tid = threadIdx.x;
-    const int obs0 = P.tile_obs0[tile], nobs = P.tile_nobs[tile];
-    const int ts0 = P.tile_smp0[tile], nts = P.tile_nsmp[tile];
-    const int pair0 = P.tile_pair0[tile], npair = P.tile_npair[tile];
-    const int lm0 = P.tile_lm0[tile], nlm = P.tile_nlm[tile];
-    if (gated_off(P.ctl, gate)) return;
-    const int si = state_idx(P, sel);
-    const double* __restrict__ kst = P.kbuf[si];
-    const double* __restrict__ lst = P.lbuf[si];
-    const double* __restrict__ gps = P.gpsb[si];
-    const double* __restrict__ camd = P.camdb[si];
-    LBA_TMARK(P.tdbg_lin, 0);
-
-    // ---- stage the tile's index lists in LDS (fixed-count loops: all loads issue before the stores)
-    {
-        const int q0 = P.pair_r0[pair0], nq = P.pair_r0[pair0 + npair] - q0;
-        const int m0 = P.lm_r0[lm0], nm = P.lm_r0[lm0 + nlm] - m0;
-#pragma unroll
-        for (int k = 0; k < (2 * TILE_SMP + TILE_OBS - 1) / TILE_OBS; ++k) {
-            const int t = tid + k * TILE_OBS;
-            if (t < 2 * nts) tsm[t] = P.tsm_meta[2 * (size_t)ts0 + t];
-        }
-#pragma unroll
-        for (int k = 0; k < TILE_PROWS / TILE_OBS; ++k) {
-            const int t = tid + k * TILE_OBS;
-            if (t < nq) prow[t] = P.pair_rows[q0 + t];
-        }
-#pragma unroll
-        for (int k = 0; k < TILE_ROWS / TILE_OBS + 1; ++k) {
-            const int t = tid + k * TILE_OBS;
-            if (t < nm) lrow[t] = P.lm_rows[m0 + t];
-        }
-#pragma unroll
-        for (int k = 0; k < (TILE_PAIRS + TILE_OBS) / TILE_OBS; ++k) {
-            const int t = tid + k * TILE_OBS;
-            if (t <= npair) pr0[t] = P.pair_r0[pair0 + t] - q0;
-        }
-        if (tid <= nlm) lr0[tid] = P.lm_r0[lm0 + tid] - m0;
-    }
-
-    // ---- phase 1: one observation per lane: residual, robust weight, rows [J1 e Jp] and G -> LDS
-    double rho0 = 0.0;
-    if (tid < nobs) {
-        const int o = obs0 + tid;
-        const int meta = P.ob_meta[o];
-        const int kind = meta & 15, cam = meta >> 4;
-        const bool gp = kind <= LBA_STEREO_GP;
-        osm[tid] = P.ob_smp[o];
-        ocam[tid] = cam;
-        const bool st = kind == LBA_STEREO_GP || kind == LBA_STEREO;
-        orow[tid] = P.ob_row[o] | ((st ? 3 : 2) << 16);
-        rho0 = st ? lin_obs<3>(P, gps, kst, lst, camd, o, cam, gp, rows, rw, write_res)
-                  : lin_obs<2>(P, gps, kst, lst, camd, o, cam, gp, rows, rw, write_res);
-    }
-    const double tchi = block_sum<TILE_OBS>(rho0, red);   // (its barrier also publishes rows / lists)
-    if (tid == 0) P.chi_lin[tile] = tchi;
-    LBA_TMARK(P.tdbg_lin, 1);
-
-    // ---- phase 2: the tile's partial of every pose sample it observes, in the sample's 6-dim space
-    //      (J = J1 N, so sum J^T W J = N^T M N with M = sum J1^T W J1: the 24 x 24 products are formed
-    //      once per sample in k_prior_lin instead of once per row here)
-    for (int task = tid; task < nts * 3; task += TILE_OBS) {
-        const int ts = task / 3, ch = task - 3 * ts;
-        const int meta = tsm[2 * ts], mslot = tsm[2 * ts + 1];
-        const int r0 = meta & 0xffff, nr = meta >> 16;
-        if (ch == 0) smp_task<0>(P, rows, rw, r0, nr, mslot);
-        else if (ch == 1) smp_task<1>(P, rows, rw, r0, nr, mslot);
-        else smp_task<2>(P, rows, rw, r0, nr, mslot);
-    }
-    LBA_TMARK(P.tdbg_lin, 2);
-
-    // ---- phase 3: Hpl per (KF, landmark) pair: sum over its (observation, side) entries of
-    //      N_side^T G (N_side: the 6 x 12 block of the sample's factor for that KF, or for side 2 the
-    //      camera's extrinsic factor [Ad(Tbc) 0]), four Hpl rows per task
-    for (int task = tid; task < npair * 3; task += TILE_OBS) {
-        const int pl = task / 3, sb = task % 3;
-        double acc[12];
-#pragma unroll
-        for (int q = 0; q < 12; ++q) acc[q] = 0.0;
-        for (int q = pr0[pl]; q < pr0[pl + 1]; ++q) {
-            const int code = prow[q];
-            const int ol = code & 0xffff, side = code >> 16;
-            // N stored transposed: column c of N (6 values) at 12 + 6 c
-            const double* Nc = side < 2 ? gps + (size_t)osm[ol] * GPS_STRIDE + 12 + 6 * (12 * side + 4 * sb)
-                                        : camd + (size_t)ocam[ol] * CAMD_STRIDE + 16 + 6 * (4 * sb);
-            // G = rho' w sum_rows J1^T Jp of the observation, from its LDS rows (not staged: the LDS
-            // it would take halves the workgroups a CU holds)
-            const int r0 = orow[ol] & 0xffff, nrw = orow[ol] >> 16;
-            double g[18];
-#pragma unroll
-            for (int u = 0; u < 18; ++u) g[u] = 0.0;
-            for (int d = 0; d < nrw; ++d) {
-                const double* R = rows + (r0 + d) * ROW_STRIDE;
-                double jr[9];
-#pragma unroll
-                for (int u = 0; u < 6; ++u) jr[u] = R[u];
-#pragma unroll
-                for (int u = 0; u < 3; ++u) jr[6 + u] = R[7 + u];
-#pragma unroll
-                for (int l = 0; l < 6; ++l)
-#pragma unroll
-                    for (int a = 0; a < 3; ++a) g[l * 3 + a] += jr[l] * jr[6 + a];
-            }
-            const double sw = rw[r0];
-#pragma unroll
-            for (int u = 0; u < 18; ++u) g[u] *= sw;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                double n[6];
-#pragma unroll
-                for (int l = 0; l < 6; ++l) n[l] = Nc[6 * i + l];
-#pragma unroll
-                for (int a = 0; a < 3; ++a)
-                    acc[i * 3 + a] += n[0] * g[a] + n[1] * g[3 + a] + n[2] * g[6 + a] + n[3] * g[9 + a] +
-                                      n[4] * g[12 + a] + n[5] * g[15 + a];
-            }
-        }
-        double* H = P.Hpl + (size_t)(pair0 + pl) * 36 + 12 * sb;
-#pragma unroll
-        for (int q = 0; q < 12; ++q) H[q] = acc[q];
-    }
-    LBA_TMARK(P.tdbg_lin, 3);
-    // ---- phase 4: Hll / bl per landmark
-    for (int t = tid; t < nlm; t += TILE_OBS) {
-        const int l = lm0 + t;
-        double H[9], b[3];
-#pragma unroll
-        for (int q = 0; q < 9; ++q) H[q] = 0.0;
-        b[0] = b[1] = b[2] = 0.0;
-        for (int q = lr0[t]; q < lr0[t + 1]; ++q) {
-            const int r = lrow[q];
-            const double* Rr = rows + r * ROW_STRIDE;
-            const double s = rw[r];
-            const double e = Rr[6];
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                const double sa = s * Rr[7 + a];
-#pragma unroll
-                for (int c = 0; c < 3; ++c) H[a * 3 + c] += sa * Rr[7 + c];
-                b[a] -= sa * e;
-            }
-        }
-        for (int q = 0; q < 9; ++q) P.Hll[(size_t)l * 9 + q] = H[q];
-        for (int q = 0; q < 3; ++q) P.bl[(size_t)l * 3 + q] = b[q];
-    }
-    LBA_TMARK(P.tdbg_lin, 4);
-}
-
 // ------------------------------------------------------------------------------------------------
 // Pose sample s: reduce its M / g partials (fixed slot order) and expand them through the sample's
 // Jacobian factor N (6 x 24, columns [KF a pose vel | KF b pose vel]) into Hpp blocks and b_p pieces:
@@ -715,183 +551,403 @@ __device__ void edge_item(const DevProblem& P, int sel, int idx, const int tid, 
     }
 }
 
-__global__ __launch_bounds__(PRI_THREADS) void k_prior_lin(DevProblem P, int sel, int gate) {
-    __shared__ double shm[PRI_SHM];
+// ------------------------------------------------------------------------------------------------
+// Linearisation and landmark elimination of one tile, fused: one workgroup of LS_THREADS threads per
+// tile, so the tile's Hpl goes from the linearisation straight into the elimination in LDS (no second
+// launch reads it back):
+//   1. one observation per lane: residual, Huber weight, rows [J1 e Jp] -> LDS, robust chi2 partial
+//   2. per (tile sample, 9-output chunk): the sample's M / g partial -> mslab (J = J1 N, so
+//      sum J^T W J = N^T M N per sample, formed by k_expand)
+//   3. per (pair, 6-row half): Hpl(k, lm) = sum over its (observation, side) entries of N_side^T G,
+//      G = rho' w sum_rows J1^T Jp -> HBM (k_update's back-substitution) and registers
+//   4. per landmark: Hll / bl -> HBM; eliminating: Dinv = (Hll + lambda I)^-1 (Eigen's adjugate inverse,
+//      block_solver.hpp:389) -> HBM, and Hll + lambda I = L D L^T -> LDS
+//   (eliminating regular tiles only; from here on the LDS of the rows holds Hpl)
+//   5. W = Hpl L^-T in place
+//   6. S partials: over the tile's KF rows r = 12 lk + i and landmark dimensions k = 3 m + a,
+//      C = W diag(D^-1) W^T, i.e. sum_m Hpl(m,k1) Dinv_m Hpl(m,k2)^T for every KF pair at once: one
+//      16 x 16 tile of C's upper triangle per wave and pass on the matrix cores (fp64 MFMA, K = 3 nlm),
+//      the operands gathered from W through pidx[m][lk] (zero where landmark m does not see KF lk)
+//   7. rhs partials per tile KF: sum_m W(m, k) u_m, u = D^-1 L^-1 bl (= sum_m Hpl Dinv bl)
+// (1-4: BlockSolver::buildSystem, block_solver.hpp:502-560, with the edges' quadratic forms,
+// base_multi_edge.hpp:170-222; 4-7: BlockSolver::solve's Schur loop, block_solver.hpp:381-432.)
+// Workgroups after the tiles (LS_EDGES): the motion-prior / velocity / extrinsic-prior quadratic forms
+// (edge_item).  Segment tiles of heavy landmarks (tile >= n_stiles) stop after 4; k_expand merges and
+// eliminates those landmarks.  With LS_SCHUR the launch also clears the envelope of S for this trial's
+// assembly and the factorisation status.
+constexpr int LS_THREADS = 256;
+constexpr int LS_U = TILE_PAIRS * 36;   // doubles: rows + weights while linearising, then Hpl / W
+static_assert(TILE_ROWS * (ROW_STRIDE + 1) <= LS_U, "the LDS rows alias the Hpl staging");
+static_assert(EDGE_SHM <= LS_U, "edge items run in the tile LDS");
+static_assert(2 * TILE_PAIRS <= LS_THREADS && TILE_KF * TILE_KF <= LS_THREADS && TILE_SENT <= LS_THREADS &&
+                  TILE_LMS <= LS_THREADS && 2 * TILE_SMP <= LS_THREADS && TILE_PROWS <= LS_THREADS,
+              "one staging element / Hpl half / KF-pair slot per thread");
+
+__global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int sel, int gate, double lambda_arg,
+                                                             int mode) {
+    __shared__ double U[LS_U];
+    __shared__ double Dl[TILE_LMS * 9];          // per landmark: L^-T terms l10, l21, l10 l21 - l20; D^-1 (3); u (3)
+    __shared__ int tsm[2 * TILE_SMP];
+    __shared__ int osm[TILE_OBS];
+    __shared__ int ocam[TILE_OBS];
+    __shared__ int orow[TILE_OBS];               // per observation: first LDS row | rows << 16
+    __shared__ int prow[TILE_PROWS];
+    __shared__ int pr0[TILE_PAIRS + 1];
+    __shared__ int lrow[TILE_ROWS];
+    __shared__ int lr0[TILE_LMS + 1];
+    __shared__ int eslot[TILE_KF * TILE_KF];     // sslab slot of the tile's KF pair (l1 <= l2), -1: not coupled
+    __shared__ short pidx[TILE_LMS * TILE_KF];   // tile-local pair of (landmark, tile KF), -1: none
+    __shared__ unsigned char pm[TILE_PAIRS];     // tile-local landmark of a pair
+    __shared__ double red[LS_THREADS / 64];
     if (gated_off(P.ctl, gate)) return;
-    const int npe = P.n_prior + P.n_vel + P.n_eprior, si = state_idx(P, sel);
-    if ((int)blockIdx.x < npe) edge_item<PRI_THREADS>(P, sel, blockIdx.x, threadIdx.x, shm);
-    else {
-        double *Msh = shm, *Nsh = Msh + 144, *MN = Nsh + 216, *part = MN + 216;
-        sample_expand(P, P.gpsb[si], P.camdb[si], blockIdx.x - npe, Msh, Nsh, MN, part, threadIdx.x);
+    const int tid = threadIdx.x;
+    if (mode & LS_SCHUR) {
+        // this trial's assembly starts from a cleared envelope of S (the previous factorisation left its
+        // fill-in there) and a cleared factorisation status; k_assemble runs after this launch
+        if (blockIdx.x == 0 && tid == 0) {
+            *P.info = 0;
+            if (P.cf_head) *P.cf_head = 0;   // ticket counter of this trial's k_chol_flow
+        }
+        for (int z = blockIdx.x; z < P.n_ztiles; z += gridDim.x) {
+            const int zi = P.ztiles[z] & 0xffff, zj = P.ztiles[z] >> 16;
+            for (int t = tid; t < CHOL_NB * CHOL_NB; t += LS_THREADS)
+                P.S[(size_t)(zi * CHOL_NB + t / CHOL_NB) * P.npad + zj * CHOL_NB + t % CHOL_NB] = 0.0;
+        }
     }
-}
-
-// Landmark elimination for one tile of landmarks (BlockSolver::solve's Schur loop,
-// block_solver.hpp:381-430).  Per landmark, Dinv = (Hll + lambda I)^-1 (Eigen 3x3 adjugate inverse,
-// kept for the back-substitution in k_update) and, for the Schur terms, Hll + lambda I = L D L^T:
-// Dinv = L^-T D^-1 L^-1, so with W = Hpl L^-T (transformed in place in LDS, one array instead of
-// Hpl and V = Hpl Dinv) the S partial of a KF pair (k1, k2) the tile's landmarks couple is
-// sum_m W(m,k1) D_m^-1 W(m,k2)^T, one fp64-MFMA product on one wave with K running over the
-// (pair, pair, landmark) triples and D^-1 applied while loading the A operand; and the rhs partial
-// of a tile KF, sum_m V(m,k) bl_m = sum_m W(m,k) u_m with u = D^-1 L^-1 bl.  Block 0 also clears
-// the factorisation status for the solve that follows, and the first blocks zero the envelope of S.
-constexpr int SCHUR_THREADS = 512;
-
-// Workgroups n_tiles ..: the prior / sample reduction items of k_prior_lin fused into the same launch
-// (pgate >= 0; they only need k_linearize's output), so they fill the slots k_schur's last tiles leave
-// idle instead of running as a launch of their own.
-static_assert(144 + 216 + 216 + EXP_GROUPS * SM_STRIDE <= TILE_PAIRS * 36, "fused sample items reuse the Hpl staging LDS");
-__global__ __launch_bounds__(SCHUR_THREADS) void k_schur(DevProblem P, double lambda_arg, int gate, int psel, int pgate) {
-    __shared__ double Hs[TILE_PAIRS * 36];   // Hpl, then W = Hpl L^-T
-    __shared__ double Dl[TILE_LMS * 9];      // per landmark: L^-T terms l10, l21, l10 l21 - l20; D^-1 (3); u (3)
-    __shared__ int slst[TILE_SLIST];
-    __shared__ int sl0[TILE_SENT + 1];
-    __shared__ short slot[TILE_LMS * TILE_KF];
-    __shared__ signed char pm[TILE_PAIRS];
-    __shared__ int kfl[TILE_KF];
-    constexpr int NT = SCHUR_THREADS, NW = NT / 64;
-    if ((int)blockIdx.x >= P.n_tiles) {   // fused pose-sample items of the prior / sample reduction
-        if (gated_off(P.ctl, pgate)) return;
-        const int si = state_idx(P, psel);
-        sample_expand(P, P.gpsb[si], P.camdb[si], blockIdx.x - P.n_tiles, Hs, Hs + 144, Hs + 360, Hs + 576,
-                      threadIdx.x < PRI_THREADS ? threadIdx.x : (1 << 20));
+    if ((int)blockIdx.x >= P.n_tiles) {   // motion-prior / velocity / extrinsic-prior edge items
+        edge_item<LS_THREADS>(P, sel, blockIdx.x - P.n_tiles, tid, U);
         return;
     }
-    const int tile = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tile = blockIdx.x;
+    const int obs0 = P.tile_obs0[tile], nobs = P.tile_nobs[tile];
+    const int ts0 = P.tile_smp0[tile], nts = P.tile_nsmp[tile];
     const int pair0 = P.tile_pair0[tile], npair = P.tile_npair[tile];
     const int lm0 = P.tile_lm0[tile], nlm = P.tile_nlm[tile];
-    const int kf0 = P.tile_kf0[tile], nkf = P.tile_nkf[tile];
-    const int sent0 = P.tile_sent0[tile], nsent = P.tile_nsent[tile];
-    if (gated_off(P.ctl, gate)) return;
-    const double lambda = damping(P, lambda_arg);
-    LBA_TMARKI(P.tdbg_schur, tile, 0);
-    if (tile == 0 && tid == 0) {
-        *P.info = 0;
-        if (P.cf_head) *P.cf_head = 0;   // ticket counter of this trial's k_chol_flow
-    }
-    // clear the envelope tiles of S for this trial's assembly (the previous factorisation left its
-    // fill-in there); k_assemble runs after this kernel
-    for (int z = tile; z < P.n_ztiles; z += P.n_tiles) {
-        const int zi = P.ztiles[z] & 0xffff, zj = P.ztiles[z] >> 16;
-        for (int t = tid; t < CHOL_NB * CHOL_NB; t += NT)
-            P.S[(size_t)(zi * CHOL_NB + t / CHOL_NB) * P.npad + zj * CHOL_NB + t % CHOL_NB] = 0.0;
-    }
-    // ---- stage Hpl and the Schur triple lists (fixed-count loops of unconditional loads)
-    const int nh = npair * 36;
-    if (nh > 0) {
-        constexpr int NK = (TILE_PAIRS * 36 + NT - 1) / NT;
-        double hv[NK];
-#pragma unroll
-        for (int k = 0; k < NK; ++k) hv[k] = P.Hpl[(size_t)pair0 * 36 + min(tid + k * NT, nh - 1)];
-#pragma unroll
-        for (int k = 0; k < NK; ++k)
-            if (tid + k * NT < nh) Hs[tid + k * NT] = hv[k];
-    }
+    const bool elim = (mode & LS_SCHUR) && tile < P.n_stiles;
+    const int si = state_idx(P, sel);
+    const double* __restrict__ kst = P.kbuf[si];
+    const double* __restrict__ lst = P.lbuf[si];
+    const double* __restrict__ gps = P.gpsb[si];
+    const double* __restrict__ camd = P.camdb[si];
+    double* rows = U;
+    double* rw = U + TILE_ROWS * ROW_STRIDE;
+    LBA_TMARK(P.tdbg_lin, 0);
+
+    // ---- stage the tile's index lists in LDS
     {
-        const int q0 = P.sent_r0[sent0], nq = P.sent_r0[sent0 + nsent] - q0;
+        const int q0 = P.pair_r0[pair0], nq = P.pair_r0[pair0 + npair] - q0;
+        const int m0 = P.lm_r0[lm0], nm = P.lm_r0[lm0 + nlm] - m0;
+        if (tid < 2 * nts) tsm[tid] = P.tsm_meta[2 * (size_t)ts0 + tid];
+        if (tid < nq) prow[tid] = P.pair_rows[q0 + tid];
 #pragma unroll
-        for (int k = 0; k < (TILE_SLIST + NT - 1) / NT; ++k) {
-            const int t = tid + k * NT;
-            if (t < nq) slst[t] = P.sent_list[q0 + t];
+        for (int k = 0; k < (TILE_ROWS + LS_THREADS - 1) / LS_THREADS; ++k) {
+            const int t = tid + k * LS_THREADS;
+            if (t < nm) lrow[t] = P.lm_rows[m0 + t];
         }
-        if (tid <= nsent) sl0[tid] = P.sent_r0[sent0 + tid] - q0;
+        if (tid <= npair) pr0[tid] = P.pair_r0[pair0 + tid] - q0;
+        if (tid <= nlm) lr0[tid] = P.lm_r0[lm0 + tid] - m0;
+        if (elim) {
+            eslot[tid] = -1;
+            for (int t = tid; t < TILE_LMS * TILE_KF; t += LS_THREADS) pidx[t] = -1;
+        }
     }
-    for (int t = tid; t < TILE_LMS * TILE_KF; t += NT) slot[t] = -1;
-    if (tid < nkf) kfl[tid] = P.tkf_list[kf0 + tid];
-    if (tid < nlm) {
-        const int l = lm0 + tid;
-        double H[9], D[9];
+
+    // ---- phase 1: one observation per lane: residual, robust weight, rows [J1 e Jp] -> LDS
+    double rho0 = 0.0;
+    if (tid < nobs) {
+        const int o = obs0 + tid;
+        const int meta = P.ob_meta[o];
+        const int kind = meta & 15, cam = meta >> 4;
+        const bool gp = kind <= LBA_STEREO_GP;
+        osm[tid] = P.ob_smp[o];
+        ocam[tid] = cam;
+        const bool st = kind == LBA_STEREO_GP || kind == LBA_STEREO;
+        orow[tid] = P.ob_row[o] | ((st ? 3 : 2) << 16);
+        const int wr = (mode & LS_RES) ? 1 : 0;
+        rho0 = st ? lin_obs<3>(P, gps, kst, lst, camd, o, cam, gp, rows, rw, wr)
+                  : lin_obs<2>(P, gps, kst, lst, camd, o, cam, gp, rows, rw, wr);
+    }
+    const double tchi = block_sum<LS_THREADS>(rho0, red);   // (its barrier also publishes rows / lists)
+    if (tid == 0) P.chi_lin[tile] = tchi;
+    if (elim) {   // the elimination's tables (their clearing was ordered by that barrier)
+        const int sent0 = P.tile_sent0[tile], nsent = P.tile_nsent[tile];
+        if (tid < nsent) eslot[P.sent_l1[sent0 + tid] * TILE_KF + P.sent_l2[sent0 + tid]] = P.sslot[sent0 + tid];
+        if (tid < npair) {
+            const int c = P.pair_lk[pair0 + tid];
+            pidx[(c >> 8) * TILE_KF + (c & 255)] = (short)tid;
+            pm[tid] = (unsigned char)(c >> 8);
+        }
+    }
+    LBA_TMARK(P.tdbg_lin, 1);
+
+    // ---- phase 2: the tile's partial of every pose sample it observes, in the sample's 6-dim space
+    for (int task = tid; task < nts * 3; task += LS_THREADS) {
+        const int ts = task / 3, ch = task - 3 * ts;
+        const int meta = tsm[2 * ts], mslot = tsm[2 * ts + 1];
+        const int r0 = meta & 0xffff, nr = meta >> 16;
+        if (ch == 0) smp_task<0>(P, rows, rw, r0, nr, mslot);
+        else if (ch == 1) smp_task<1>(P, rows, rw, r0, nr, mslot);
+        else smp_task<2>(P, rows, rw, r0, nr, mslot);
+    }
+    LBA_TMARK(P.tdbg_lin, 2);
+
+    // ---- phase 4: Hll / bl per landmark (threads from the top; before phase 3, so no
+    //      register state of phase 3 lives across it); eliminating:
+    //      Dinv = (Hll + lambda I)^-1 (kept for k_update) and Hll + lambda I = L D L^T
+    {
+        const int t = LS_THREADS - 1 - tid;
+        if (t < nlm) {
+            const int l = lm0 + t;
+            double H[9], b[3];
 #pragma unroll
-        for (int q = 0; q < 9; ++q) H[q] = P.Hll[(size_t)l * 9 + q];
-        H[0] += lambda; H[4] += lambda; H[8] += lambda;   // setLambda on Hll (block_solver.hpp:580-587)
-        inv3(H, D);
+            for (int q = 0; q < 9; ++q) H[q] = 0.0;
+            b[0] = b[1] = b[2] = 0.0;
+            for (int q = lr0[t]; q < lr0[t + 1]; ++q) {
+                const int r = lrow[q];
+                const double* Rr = rows + r * ROW_STRIDE;
+                const double s = rw[r];
+                const double e = Rr[6];
 #pragma unroll
-        for (int q = 0; q < 9; ++q) P.Dinv[(size_t)l * 9 + q] = D[q];
-        // H = L D L^T (unit lower L)
-        const double d0 = H[0], l10 = H[3] / d0, l20 = H[6] / d0;
-        const double d1 = H[4] - l10 * l10 * d0;
-        const double l21 = (H[7] - l20 * l10 * d0) / d1;
-        const double d2 = H[8] - l20 * l20 * d0 - l21 * l21 * d1;
-        const double b0 = P.bl[(size_t)l * 3], b1 = P.bl[(size_t)l * 3 + 1], b2 = P.bl[(size_t)l * 3 + 2];
-        const double y1 = b1 - l10 * b0, y2 = b2 - l20 * b0 - l21 * y1;   // L^-1 bl
-        double* o = Dl + tid * 9;
-        o[0] = l10; o[1] = l21; o[2] = l10 * l21 - l20;
-        o[3] = 1.0 / d0; o[4] = 1.0 / d1; o[5] = 1.0 / d2;
-        o[6] = b0 / d0; o[7] = y1 / d1; o[8] = y2 / d2;
+                for (int a = 0; a < 3; ++a) {
+                    const double sa = s * Rr[7 + a];
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) H[a * 3 + c] += sa * Rr[7 + c];
+                    b[a] -= sa * e;
+                }
+            }
+            for (int q = 0; q < 9; ++q) P.Hll[(size_t)l * 9 + q] = H[q];
+            for (int q = 0; q < 3; ++q) P.bl[(size_t)l * 3 + q] = b[q];
+            if (elim) {
+                const double lambda = damping(P, lambda_arg);
+                H[0] += lambda; H[4] += lambda; H[8] += lambda;   // setLambda on Hll (block_solver.hpp:580-587)
+                double Di[9];
+                inv3(H, Di);
+#pragma unroll
+                for (int q = 0; q < 9; ++q) P.Dinv[(size_t)l * 9 + q] = Di[q];
+                // H = L D L^T (unit lower L)
+                const double d0 = H[0], l10 = H[3] / d0, l20 = H[6] / d0;
+                const double d1 = H[4] - l10 * l10 * d0;
+                const double l21 = (H[7] - l20 * l10 * d0) / d1;
+                const double d2 = H[8] - l20 * l20 * d0 - l21 * l21 * d1;
+                const double y1 = b[1] - l10 * b[0], y2 = b[2] - l20 * b[0] - l21 * y1;   // L^-1 bl
+                double* o = Dl + t * 9;
+                o[0] = l10; o[1] = l21; o[2] = l10 * l21 - l20;
+                o[3] = 1.0 / d0; o[4] = 1.0 / d1; o[5] = 1.0 / d2;
+                o[6] = b[0] / d0; o[7] = y1 / d1; o[8] = y2 / d2;
+            }
+        }
+    }
+    LBA_TMARK(P.tdbg_lin, 3);
+
+    // ---- phase 3: Hpl per (KF, landmark) pair, six rows per thread: the sum over the pair's (observation,
+    //      side) entries of N_side^T G (N_side: the 6 x 12 block of the sample's factor for that KF, or for
+    //      side 2 the camera's extrinsic factor [Ad(Tbc) 0]); kept in registers until the rows are dead
+    double hacc[18];
+#pragma unroll
+    for (int q = 0; q < 18; ++q) hacc[q] = 0.0;
+    const int pl = tid >> 1, half = tid & 1;
+    if (pl < npair) {
+        for (int q = pr0[pl]; q < pr0[pl + 1]; ++q) {
+            const int code = prow[q];
+            const int ol = code & 0xffff, side = code >> 16;
+            // N stored transposed: column c of N (6 values) at 12 + 6 c
+            const double* Nc = side < 2 ? gps + (size_t)osm[ol] * GPS_STRIDE + 12 + 6 * (12 * side + 6 * half)
+                                        : camd + (size_t)ocam[ol] * CAMD_STRIDE + 16 + 6 * (6 * half);
+            const int r0 = orow[ol] & 0xffff, nrw = orow[ol] >> 16;
+            double g[18];   // G = rho' w sum_rows J1^T Jp of the observation, from its LDS rows
+#pragma unroll
+            for (int u = 0; u < 18; ++u) g[u] = 0.0;
+            for (int d = 0; d < nrw; ++d) {
+                const double* Rr = rows + (r0 + d) * ROW_STRIDE;
+                double jr[9];
+#pragma unroll
+                for (int u = 0; u < 6; ++u) jr[u] = Rr[u];
+#pragma unroll
+                for (int u = 0; u < 3; ++u) jr[6 + u] = Rr[7 + u];
+#pragma unroll
+                for (int l = 0; l < 6; ++l)
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) g[l * 3 + a] += jr[l] * jr[6 + a];
+            }
+            const double sw = rw[r0];
+#pragma unroll
+            for (int u = 0; u < 18; ++u) g[u] *= sw;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                double n[6];
+#pragma unroll
+                for (int l = 0; l < 6; ++l) n[l] = Nc[6 * i + l];
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+                    hacc[i * 3 + a] += n[0] * g[a] + n[1] * g[3 + a] + n[2] * g[6 + a] + n[3] * g[9 + a] +
+                                       n[4] * g[12 + a] + n[5] * g[15 + a];
+            }
+        }
+        double* Hg = P.Hpl + (size_t)(pair0 + pl) * 36 + 18 * half;
+#pragma unroll
+        for (int q = 0; q < 18; ++q) Hg[q] = hacc[q];
+    }
+    LBA_TMARK(P.tdbg_lin, 4);
+
+    if (!elim) return;
+    __syncthreads();   // every read of the rows is done: their LDS takes Hpl
+    if (pl < npair) {
+        double* h = U + pl * 36 + 18 * half;
+#pragma unroll
+        for (int q = 0; q < 18; ++q) h[q] = hacc[q];
     }
     __syncthreads();
-    LBA_TMARKI(P.tdbg_schur, tile, 1);
-    for (int t = tid; t < npair; t += NT) {
-        const int m = P.pair_lm[pair0 + t] - lm0, k = P.pair_kf[pair0 + t];
-        int lk = 0;
-        for (int l = 0; l < nkf; ++l)
-            if (kfl[l] == k) lk = l;
-        slot[m * TILE_KF + lk] = (short)t;
-        pm[t] = (signed char)m;
-    }
-    __syncthreads();
-    // ---- W = Hpl L^-T in place, one (pair, row) per task:
+    LBA_TMARKI(P.tdbg_schur, tile, 0);
+    // ---- phase 5: W = Hpl L^-T in place, one (pair, row) per task:
     //      L^-1 = [1 0 0; -l10 1 0; l10 l21 - l20, -l21, 1], w_a = sum_b h_b (L^-1)(a, b)
-    for (int task = tid; task < npair * 12; task += NT) {
+    for (int task = tid; task < npair * 12; task += LS_THREADS) {
         const int t = task / 12, r = task - 12 * t;
         const double* D = Dl + pm[t] * 9;
-        double* h = Hs + t * 36 + r * 3;
+        double* h = U + t * 36 + r * 3;
         const double h0 = h[0], h1 = h[1], h2 = h[2];
         h[1] = h1 - D[0] * h0;
         h[2] = h2 - D[1] * h1 + D[2] * h0;
     }
     __syncthreads();
-    LBA_TMARKI(P.tdbg_schur, tile, 2);
-    // ---- S partials: one wave per KF pair, K = (landmark, 3), two accumulators
+    LBA_TMARKI(P.tdbg_schur, tile, 1);
+    // ---- phase 6: S partials, C = W diag(D^-1) W^T over the tile's KF rows, upper 16 x 16 tiles
+    const int nkf = P.tile_nkf[tile];
     {
-        const int kq = lane >> 4, cl = lane & 15, cr = min(cl, 11);
-        for (int e = wave; e < nsent; e += NW) {
-            const int qb = sl0[e], nk = 3 * (sl0[e + 1] - qb);
+        const int lane = tid & 63, wave = tid >> 6, kq = lane >> 4, cl = lane & 15;
+        const int nr = 12 * nkf, K = 3 * nlm;
+        const int nt = (nr + 15) >> 4, nut = nt * (nt + 1) / 2;
+        for (int u = wave; u < nut; u += LS_THREADS / 64) {
+            int tr = 0, rem = u;
+            while (rem >= nt - tr) { rem -= nt - tr; ++tr; }
+            const int tc = tr + rem;
+            const int ra = 16 * tr + cl, rb = 16 * tc + cl;
+            const int la = ra / 12, ia = ra - 12 * la, lb = rb / 12, ib = rb - 12 * lb;
+            const bool va = ra < nr, vb = rb < nr;
             d4 c0 = {0.0, 0.0, 0.0, 0.0}, c1 = c0;
-            for (int k0 = 0; k0 < nk; k0 += 8) {
+            for (int k0 = 0; k0 < K; k0 += 8) {
                 double av[2], bv[2];
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int k = k0 + 4 * h + kq;
-                    const bool ok = k < nk && cl < 12;
-                    const int kk = k < nk ? k : 0;
-                    const int mi = kk / 3, a = kk - 3 * mi;
-                    const int code = slst[qb + mi];
-                    const int t1 = code & 255, t2 = (code >> 8) & 255, m = code >> 16;
-                    const double x = Hs[t1 * 36 + cr * 3 + a] * Dl[m * 9 + 3 + a];
-                    const double y = Hs[t2 * 36 + cr * 3 + a];
-                    av[h] = ok ? x : 0.0;
-                    bv[h] = ok ? y : 0.0;
+                for (int hh = 0; hh < 2; ++hh) {
+                    const int k = k0 + 4 * hh + kq;
+                    const bool ok = k < K;
+                    const int m = ok ? k / 3 : 0, a = k - 3 * (k / 3);
+                    const int pa = (ok && va) ? pidx[m * TILE_KF + la] : -1;
+                    const int pb = (ok && vb) ? pidx[m * TILE_KF + lb] : -1;
+                    av[hh] = pa >= 0 ? U[pa * 36 + ia * 3 + a] * Dl[m * 9 + 3 + a] : 0.0;
+                    bv[hh] = pb >= 0 ? U[pb * 36 + ib * 3 + a] : 0.0;
                 }
                 c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0], bv[0], c0, 0, 0, 0);
                 c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1], bv[1], c1, 0, 0, 0);
             }
             const d4 c = c0 + c1;
-            double* o = P.sslab + (size_t)P.sslot[sent0 + e] * 144;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int i = kq + 4 * q;
-                if (i < 12 && cl < 12) o[i * 12 + cl] = c[q];
+                const int r = 16 * tr + kq + 4 * q;   // C(r, rb): row of lane group kq, column of lane cl
+                if (r < nr && vb && r <= rb) {
+                    const int l1 = r / 12, i = r - 12 * l1;
+                    const int s = eslot[l1 * TILE_KF + lb];
+                    if (s >= 0) {
+                        double* o = P.sslab + (size_t)s * 144;
+                        o[i * 12 + ib] = c[q];
+                        if (l1 == lb && i != ib) o[ib * 12 + i] = c[q];   // a diagonal block: both halves
+                    }
+                }
             }
+        }
+    }
+    LBA_TMARKI(P.tdbg_schur, tile, 2);
+    // ---- phase 7: rhs partials: sum over the KF's landmarks of V(m,k) bl_m (block_solver.hpp:395-401)
+    {
+        const int kf0 = P.tile_kf0[tile];
+        for (int task = tid; task < nkf * 12; task += LS_THREADS) {
+            const int l = task / 12, r = task % 12;
+            double v = 0.0;
+            for (int m = 0; m < nlm; ++m) {
+                const int t = pidx[m * TILE_KF + l];
+                if (t >= 0) {
+                    const double* w = U + t * 36 + r * 3;
+                    const double* uu = Dl + m * 9 + 6;
+                    v += w[0] * uu[0] + w[1] * uu[1] + w[2] * uu[2];
+                }
+            }
+            P.gpslab[(size_t)P.tkf_gslot[kf0 + l] * 12 + r] = v;
         }
     }
     LBA_TMARKI(P.tdbg_schur, tile, 3);
-    LBA_TMARKI(P.tdbg_schur, tile, 4);
-    // ---- rhs partials: sum over the KF's landmarks of V(m,k) bl_m (block_solver.hpp:395-401)
-    for (int task = tid; task < nkf * 12; task += NT) {
-        const int l = task / 12, r = task % 12;
+}
+
+// One heavy landmark (k_expand work item, PRI_THREADS threads): its segments' partials summed in a fixed
+// order into the landmark's Hll, bl and canonical Hpl blocks (what k_update and the host paths read);
+// eliminating, Dinv = (Hll + lambda I)^-1, V = Hpl Dinv, the rhs partial V bl of each of its KFs and the
+// S partial V(a) Hpl(b)^T of each pair of its KFs (block_solver.hpp:381-432: any number of KFs, like
+// g2o's Hpl columns).  shm: 21 doubles.
+__device__ void heavy_item(const DevProblem& P, int h, double lambda, int schur, double* shm) {
+    const int tid = threadIdx.x;
+    const int l = P.hv_lm[h], s0 = P.hv_seg0[h], s1 = P.hv_seg0[h + 1];
+    const int hp0 = P.hv_hp0[h], nhp = P.hv_hp0[h + 1] - hp0, cp0 = P.lm_pair0[l];
+    double* HB = shm;   // Hll (9), bl (3), Dinv (9)
+    if (tid < 12) {
         double v = 0.0;
-        for (int m = 0; m < nlm; ++m) {
-            const int t = slot[m * TILE_KF + l];
-            if (t >= 0) {
-                const double* w = Hs + t * 36 + r * 3;
-                const double* u = Dl + m * 9 + 6;
-                v += w[0] * u[0] + w[1] * u[1] + w[2] * u[2];
-            }
-        }
-        P.gpslab[(size_t)P.tkf_gslot[kf0 + l] * 12 + r] = v;
+        for (int s = s0; s < s1; ++s)
+            v += tid < 9 ? P.Hll[(size_t)(P.n_lm + s) * 9 + tid] : P.bl[(size_t)(P.n_lm + s) * 3 + tid - 9];
+        HB[tid] = v;
+        if (tid < 9) P.Hll[(size_t)l * 9 + tid] = v;
+        else P.bl[(size_t)l * 3 + tid - 9] = v;
     }
-    LBA_TMARKI(P.tdbg_schur, tile, 5);
+    for (int t = tid; t < nhp * 36; t += PRI_THREADS) {
+        const int j = t / 36, e = t - 36 * j;
+        double v = 0.0;
+        for (int q = P.hp_src0[hp0 + j]; q < P.hp_src0[hp0 + j + 1]; ++q) v += P.Hpl[(size_t)P.hp_src[q] * 36 + e];
+        P.Hpl[(size_t)(cp0 + j) * 36 + e] = v;
+    }
+    if (!schur) return;
+    __syncthreads();
+    if (tid == 0) {
+        double Hd[9];
+        for (int q = 0; q < 9; ++q) Hd[q] = HB[q];
+        Hd[0] += lambda; Hd[4] += lambda; Hd[8] += lambda;   // setLambda (block_solver.hpp:580-587)
+        inv3(Hd, HB + 12);
+        for (int q = 0; q < 9; ++q) P.Dinv[(size_t)l * 9 + q] = HB[12 + q];
+    }
+    __syncthreads();
+    const double* Di = HB + 12;
+    for (int t = tid; t < nhp * 12; t += PRI_THREADS) {   // V = Hpl Dinv and the rhs partial V bl
+        const int j = t / 12, r = t - 12 * j;
+        const double* hr = P.Hpl + (size_t)(cp0 + j) * 36 + r * 3;
+        double* vr = P.Vh + (size_t)(hp0 + j) * 36 + r * 3;
+        double g = 0.0;
+        for (int a = 0; a < 3; ++a) {
+            const double v = hr[0] * Di[a] + hr[1] * Di[3 + a] + hr[2] * Di[6 + a];
+            vr[a] = v;
+            g += v * HB[9 + a];
+        }
+        P.gpslab[(size_t)P.hp_gslot[hp0 + j] * 12 + r] = g;
+    }
+    __syncthreads();
+    const int np2 = nhp * (nhp + 1) / 2, ss0 = P.hv_ss0[h];
+    for (int t = tid; t < np2 * 144; t += PRI_THREADS) {   // the S partial of KF pair (a <= b): V(a) Hpl(b)^T
+        const int pp = t / 144, e = t - 144 * pp, i = e / 12, jj = e - 12 * i;
+        int a = 0, rem = pp;
+        while (rem >= nhp - a) { rem -= nhp - a; ++a; }
+        const double* v = P.Vh + (size_t)(hp0 + a) * 36 + i * 3;
+        const double* hb = P.Hpl + (size_t)(cp0 + a + rem) * 36 + jj * 3;
+        P.sslab[(size_t)P.hv_sslot[ss0 + pp] * 144 + e] = v[0] * hb[0] + v[1] * hb[1] + v[2] * hb[2];
+    }
+}
+
+// After k_lin_schur: workgroups [0, n_smp) expand the pose samples' M / g partials through their factors
+// N into Hpp blocks and b_p pieces (sample_expand); [n_smp, n_smp + n_heavy) the heavy landmarks
+// (heavy_item: the merge of their segments, and with schur their elimination)
+__global__ __launch_bounds__(PRI_THREADS) void k_expand(DevProblem P, int sel, int gate, double lambda_arg, int schur) {
+    __shared__ double shm[PRI_SHM];
+    if (gated_off(P.ctl, gate)) return;
+    if ((int)blockIdx.x < P.n_smp) {
+        const int si = state_idx(P, sel);
+        double *Msh = shm, *Nsh = Msh + 144, *MN = Nsh + 216, *part = MN + 216;
+        sample_expand(P, P.gpsb[si], P.camdb[si], blockIdx.x, Msh, Nsh, MN, part, threadIdx.x);
+        return;
+    }
+    heavy_item(P, blockIdx.x - P.n_smp, schur ? damping(P, lambda_arg) : 0.0, schur, shm);
 }
 
 // Reduced camera system of one trial, straight from the target-sorted partial slabs (each
@@ -2173,7 +2229,7 @@ __device__ void prior_eval(const DevProblem& P, const double* __restrict__ kst, 
 // sparse_optimizer.cpp:360-400), log whether the trial relinearised, and publish the controller.
 __device__ void lm_decide(LMCtl& c, double chi_lin, double chi_trial, double scale, bool solved, int* hlog) {
 #pragma clang fp contract(off)   // round every operation like the host loop (no fused multiply-add)
-    if (hlog) hlog[c.slot % HLOG_CAP] = (!c.done && c.need_lin) ? 1 : 0;
+    if (hlog) hlog[c.slot % HLOG_CAP] = c.done ? 0 : 1;   // whether the trial's gated kernels ran
     c.slot++;
     if (c.done) return;
     if (c.qmax == 0) c.cur_chi = c.ini_chi = chi_lin;
@@ -2362,33 +2418,25 @@ void launch_gp_prep(const DevProblem& P, int sel, int jac, int gate, hipStream_t
     const int nb = P.n_gp + cdiv(P.n_kf, PREP_THREADS);
     if (nb) hipLaunchKernelGGL(k_gp_prep, dim3(nb), dim3(PREP_THREADS), 0, s, P, sel, jac, gate);
 }
-void launch_linearize(const DevProblem& P, int sel, int write_res, int gate, hipStream_t s, hipEvent_t e0,
-                      hipEvent_t e1, int edges) {
-    const int ne = edges ? P.n_prior + P.n_vel + P.n_eprior : 0;
-    if (!P.n_tiles) {
-        if (ne) launch_prior_lin(P, sel, gate, s);
-        return;
-    }
+void launch_lin_schur(const DevProblem& P, int sel, int gate, double lambda, int mode, hipStream_t s, hipEvent_t e0,
+                      hipEvent_t e1) {
+    const int ne = (mode & LS_EDGES) ? P.n_prior + P.n_vel + P.n_eprior : 0;
     const dim3 g(P.n_tiles + ne);
+    if (g.x == 0) return;
     if (e0)   // the events carry the dispatch's own start / end timestamps
-        hipExtLaunchKernelGGL(k_linearize, g, dim3(TILE_OBS), 0, s, e0, e1, 0, P, sel, write_res, gate);
+        hipExtLaunchKernelGGL(k_lin_schur, g, dim3(LS_THREADS), 0, s, e0, e1, 0, P, sel, gate, lambda, mode);
     else
-        hipLaunchKernelGGL(k_linearize, g, dim3(TILE_OBS), 0, s, P, sel, write_res, gate);
+        hipLaunchKernelGGL(k_lin_schur, g, dim3(LS_THREADS), 0, s, P, sel, gate, lambda, mode);
 }
-void launch_prior_lin(const DevProblem& P, int sel, int gate, hipStream_t s) {
-    const int n = P.n_prior + P.n_vel + P.n_eprior + P.n_smp;
-    if (n) hipLaunchKernelGGL(k_prior_lin, dim3(n), dim3(PRI_THREADS), 0, s, P, sel, gate);
-}
-void launch_schur(const DevProblem& P, double lambda, int gate, hipStream_t s, int psel, int pgate) {
-    const int npri = pgate >= 0 ? P.n_smp : 0;   // the pose-sample items (the edge items ran with k_linearize)
-    if (!P.n_tiles) return;   // (no observations: no sample has a partial, and launch_linearize ran k_prior_lin)
-    hipLaunchKernelGGL(k_schur, dim3(P.n_tiles + npri), dim3(SCHUR_THREADS), 0, s, P, lambda, gate, psel, pgate);
+void launch_expand(const DevProblem& P, int sel, int gate, double lambda, int schur, hipStream_t s) {
+    const int n = P.n_smp + P.n_heavy;
+    if (n) hipLaunchKernelGGL(k_expand, dim3(n), dim3(PRI_THREADS), 0, s, P, sel, gate, lambda, schur);
 }
 void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hipStream_t s) {
     const int n = P.n_asm + P.n_pb;
     if (n) hipLaunchKernelGGL(k_assemble, dim3(n), dim3(144 * RED_GROUPS), 0, s, P, lambda, flags, gate);
 }
-void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s) {
+void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const int n = P.npad;   // multiple of CHOL_NB (identity tail)
     if (n == 0) return;
     if (!P.cf_steps_path) {
@@ -2404,7 +2452,10 @@ void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStr
         a.Linv = P.cf_linv; a.ivready = P.cf_ivready; a.xout = P.xsol; a.pnat = P.pnat; a.fready = P.cf_fready;
         a.zready = P.cf_zready; a.zv = P.cf_zv;
         a.xpos = P.cf_xpos; a.xready = P.cf_ivready;
-        hipLaunchKernelGGL(k_chol_flow, dim3(min(P.cf_ntasks, 512)), dim3(256), 0, s, a);
+        if (e0)
+            hipExtLaunchKernelGGL(k_chol_flow, dim3(min(P.cf_ntasks, 512)), dim3(256), 0, s, e0, e1, 0, a);
+        else
+            hipLaunchKernelGGL(k_chol_flow, dim3(min(P.cf_ntasks, 512)), dim3(256), 0, s, a);
         return;
     }
     for (int st = 0; P.cf_steps_path && st < P.n_steps; ++st) {

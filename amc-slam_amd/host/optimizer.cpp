@@ -9,13 +9,14 @@
 //  * an observation whose keyframe is marked for this BA but was never added as a vertex (a bad
 //    covisible KF, or a bad KF marked while collecting fixed KFs) is skipped;
 //  * a GP observation whose mNextKF is not a vertex is skipped.
-//  * Post-pass chi2 values come from lba_eval at the final estimate.  g2o's e->chi2() returns the
-//    error of the last computeActiveErrors, which differs only when the last LM iteration ended
-//    on ten rejected trials.
+// Post-pass: chi2 values are those of the last computed errors (lba_trial_chi2: the last trial state,
+// also when the run ended on rejected trials, like g2o's e->chi2()), the depth test runs on the final
+// estimate (isDepthPositive reads the vertices, lba_eval).
 #include "optimizer.hpp"
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <unordered_map>
 #include <unordered_set>
@@ -313,7 +314,8 @@ int Optimizer::LocalGPBA(MultiKeyFrame* pKF, Map* pMap, const lbamap_options& op
     std::vector<double> chi2(W.obs.size());
     std::vector<uint8_t> depth_ok(W.obs.size());
     if (!W.obs.empty()) {
-        rc = lba_eval(problem, nullptr, chi2.data(), depth_ok.data());
+        rc = lba_trial_chi2(problem, chi2.data());
+        if (rc >= 0) rc = lba_eval(problem, nullptr, nullptr, depth_ok.data());
         if (rc < 0) {
             res.status = rc;
             if (out) *out = res;
@@ -428,7 +430,9 @@ void Optimizer::LocalGPBA(MultiKeyFrame* pKF, bool* pbStopFlag, Map* pMap, int& 
         if (lba_create(&p, &cfg) != LBA_OK) { p = nullptr; return; }
     }
     lbamap_options opt{bLarge ? 1 : 0, bExtrinsic ? 1 : 0, 0, 0};
-    LocalGPBA(pKF, pMap, opt, p, nullptr);
+    const int rc = LocalGPBA(pKF, pMap, opt, p, nullptr);
+    if (rc < 0)   // (the reference's void LocalGPBA has no status to return; the map stays untouched)
+        std::fprintf(stderr, "LocalGPBA: local BA skipped (%d): %s\n", rc, lba_last_error(p));
 }
 
 }  // namespace amc_slam

@@ -57,10 +57,37 @@ def sweep_flops(win):
     return float(f.sum())
 
 
-def pmc_traffic(workload):
-    """HBM bytes per k_linearize launch from the committed rocprofv3 PMC summary (FETCH_SIZE
+def schur_terms(win):
+    """The landmark elimination fused into the sweep kernel (k_lin_schur): per landmark
+    with P non-fixed KF blocks, Dinv (72 B written), and the Schur complement it adds to S: one 12 x 12
+    block per pair of its KFs (a <= b), and a 12-vector of the reduced rhs per KF.  Algorithmic bytes:
+    72 B per landmark + 1152 B per distinct coupled KF pair + 96 B per KF (the reduced system's
+    pieces, written once); FLOPs: per landmark 2 x 3 x (12P)(12P + 1) / 2 (sum_m Hpl Dinv Hpl^T, upper
+    half) + 2 x 36 P (rhs) + ~60 (3 x 3 inverse / LDL^T)."""
+    o = win.obs
+    fixed = win.kfs["fixed"].astype(bool)
+    ks = np.concatenate([np.stack([o["lm"], o["kf_b"]], 1), np.stack([o["lm"], o["kf_a"]], 1)])
+    ks = ks[(ks[:, 1] >= 0)]
+    ks = ks[~fixed[ks[:, 1]]]
+    ks = np.unique(ks, axis=0)
+    lm_ids, starts, counts = np.unique(ks[:, 0], return_index=True, return_counts=True)
+    pairs = set()
+    flops = 0.0
+    for s, c in zip(starts, counts):
+        kk = ks[s:s + c, 1]
+        P = len(kk)
+        flops += 3.0 * (12 * P) * (12 * P + 1) + 72.0 * P + 60.0
+        for a in range(P):
+            for b in range(a, P):
+                pairs.add((int(kk[a]), int(kk[b])))
+    n_kf = int((~fixed).sum())
+    return 72 * len(lm_ids) + 1152 * len(pairs) + 96 * n_kf, flops
+
+
+def pmc_traffic(workload, kernel="k_lin_schur"):
+    """HBM bytes per launch of the kernel from the committed rocprofv3 PMC summary (FETCH_SIZE
     doubled per the gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md §HBM), or None."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_k_linearize_*.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc_{kernel}_*.json")))
     for f in reversed(files):
         try:
             d = json.load(open(f))
@@ -121,8 +148,8 @@ def main():
     # all-reduced over RCCL every LM trial); otherwise window farming (config 3) or a single window
     gba = args.config.startswith("cfg4")
     solve_flag = {"auto": 0, "band": amc_lba.abi.FLAG_BAND_SOLVE, "dense": amc_lba.abi.FLAG_DENSE_SOLVE}[args.solve]
-    # the timed run records HIP events around every k_linearize launch (LBA_FLAG_TIME_SWEEP): the
-    # roofline below is measured live, per launch, over the timed region
+    # the timed run records the dispatch timestamps of every k_lin_schur and k_chol_flow launch
+    # (LBA_FLAG_TIME_SWEEP): the rooflines below are measured live, per launch, over the timed region
     flags = amc_lba.abi.FLAG_TIME_SWEEP | solve_flag
     ex, full = None, None
     t_setup = time.perf_counter()
@@ -165,13 +192,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    done, ms_k, n_k, trials = 0, 0.0, 0, 0
+    done, ms_k, n_k, trials, ms_s, n_s = 0, 0.0, 0, 0, 0.0, 0
     while done < args.steps:
         it = min(args.window_iters, args.steps - done)
         n, st = prob.optimize(it)
         done += n
         ms_k += st.ms_k_linearize
         n_k += st.n_k_linearize
+        ms_s += st.ms_k_solve
+        n_s += st.n_k_solve
         trials += st.trials
         if ex is not None:
             ex.exchange(prob)           # window boundary: publish owned shared landmarks
@@ -191,7 +220,11 @@ def main():
         prob.close()
         ph = amc_lba.Problem(win, device=local, early_stop=0, flags=amc_lba.abi.FLAG_TIME_PHASES | solve_flag)
         n_ph, st_ph = ph.optimize(args.window_iters)
-        phase = {k: getattr(st_ph, k) / max(n_ph, 1) for k in ("ms_linearize", "ms_schur", "ms_solve", "ms_update_eval")}
+        # per LM iteration: k_lin_schur (linearisation + landmark elimination, every trial), k_expand +
+        # k_assemble, the reduced-system solve, k_update + k_eval
+        phase = {name: getattr(st_ph, k) / max(n_ph, 1) for name, k in
+                 (("lin_schur", "ms_linearize"), ("expand_assemble", "ms_schur"), ("solve", "ms_solve"),
+                  ("update_eval", "ms_update_eval"))}
         phase["trials"] = st_ph.trials / max(n_ph, 1)
         # one LocalGPBA call = lba_set_problem (host preprocessing of the window + host->device upload,
         # outside the timed region above) + optimize(window_iters): time a set_problem on the engine
@@ -209,8 +242,12 @@ def main():
         W = full if gba else win
         value = total_iters / dt
         k_ms = ms_k / max(n_k, 1)
-        B = sweep_bytes(win)
-        F = sweep_flops(win)
+        B_schur, F_schur = schur_terms(win)
+        B = sweep_bytes(win) + B_schur
+        F = sweep_flops(win) + F_schur
+        s_ms = ms_s / max(n_s, 1)
+        npose = 12 * int((win.kfs["fixed"] == 0).sum())
+        F_solve = npose ** 3 / 3.0 + 2.0 * npose ** 2   # dense Cholesky + two triangular solves
         achieved = B / (k_ms * 1e-3) / 1e9 if n_k else None
         workload = f"{args.config}: {win.name or args.config} synthetic window"
         traffic = pmc_traffic(args.config)
@@ -233,14 +270,21 @@ def main():
                        "parallelism": (f"landmark partition x{world} (RCCL all-reduce per trial)" if gba else
                                        f"window farm x{world}") if world > 1 else "single window",
                        "setup_s": t_setup},
-            "roofline": {"bound": "hbm", "kernel": "k_linearize", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "kernel": "k_lin_schur", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                          "traffic": traffic, "bytes_per_launch": B, "avg_launch_ms": k_ms,
                          "timed_launches": n_k},
-            "roofline_fp64": {"kernel": "k_linearize", "flops_per_launch": F,
+            "roofline_fp64": {"kernel": "k_lin_schur", "flops_per_launch": F,
                               "achieved": F / (k_ms * 1e-3) / 1e12 if n_k else None,
                               "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                               "frac": (F / (k_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS) if n_k else None},
+            "roofline_solve": {"kernel": "k_chol_flow", "bound": "mfma", "flops_per_launch": F_solve,
+                               "achieved": F_solve / (s_ms * 1e-3) / 1e12 if n_s else None,
+                               "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                               "frac": (F_solve / (s_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS) if n_s else None,
+                               "avg_launch_ms": s_ms, "timed_launches": n_s,
+                               "note": "np^3/3 + 2 np^2 of the dense reduced camera system; the dependent "
+                                       "panel chain, not the FLOPs, sets its time"},
             "trials_per_step": trials / max(done, 1),
             "phases_ms_per_step": phase,
         }
@@ -250,7 +294,7 @@ def main():
                 calls["calls_per_s_with_set_problem"] = 1.0 / (args.window_iters / value + set_problem_ms * 1e-3)
             line["localgpba_calls"] = calls
         if gba:   # roofline: rank 0's partition of the sweep
-            line["roofline"]["note"] = "k_linearize of rank 0's landmark partition"
+            line["roofline"]["note"] = "k_lin_schur of rank 0's landmark partition"
         if not args.no_cpu and world == 1 and not gba:   # (the oracle's dense LDLT of S = 60000^2 is hours)
             line["cpu_baseline"] = cpu_baseline(win, args.cpu_seconds)
             line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]

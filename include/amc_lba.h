@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define LBA_ABI_VERSION 2
+#define LBA_ABI_VERSION 3
 
 /* status codes */
 #define LBA_OK              0
@@ -131,15 +131,19 @@ typedef struct lba_stats {
     double  chi2_initial;   /* activeRobustChi2 before the first iteration */
     double  chi2_final;     /* activeRobustChi2 of the last computed errors (g2o semantics) */
     double  lambda_final;
-    double  ms_linearize;   /* device time per phase, summed (HIP events; LBA_FLAG_TIME_PHASES) */
+    double  ms_linearize;   /* device time per phase, summed (HIP events; LBA_FLAG_TIME_PHASES):
+                               ms_linearize the fused linearisation + landmark elimination of every
+                               trial, ms_schur the pose-sample expansion + assembly of S */
     double  ms_schur;
     double  ms_solve;
     double  ms_update_eval;
     double  ms_total;       /* host wall time of lba_optimize */
-    double  ms_k_linearize; /* device time of the fused residual/Jacobian/J^T W J sweep kernel, summed
+    double  ms_k_linearize; /* device time of the fused sweep kernel (residual / Jacobian / J^T W J and the
+                               landmark elimination, k_lin_schur), summed over its dispatches
                                (LBA_FLAG_TIME_SWEEP or LBA_FLAG_TIME_PHASES) */
     int32_t n_k_linearize;  /* launches of that kernel */
-    int32_t pad;
+    int32_t n_k_solve;      /* launches of the factorisation + solve kernel (k_chol_flow) */
+    double  ms_k_solve;     /* its device time, summed (same flags) */
 } lba_stats;
 
 typedef struct lba_problem lba_problem;   /* opaque: owns device buffers + stream */
@@ -177,7 +181,10 @@ int lba_set_problem(lba_problem* p,
  * xGMI (lba_set_partition_rccl), an in-process group of problems on one device (lba_group, for
  * tests), or any function.  Call before lba_set_problem; set_problem is then collective (the ranks
  * agree on the union envelope of S), as are lba_optimize calls, which need lambda_init > 0 and the
- * same iteration count and stop flag on every rank. */
+ * same iteration count and stop flag on every rank.  A set_problem that fails on one rank fails on
+ * every rank: the ranks exchange their set-up status in one all-reduce before the first collective
+ * (the others return LBA_E_ARG, "another rank of the partition failed its set-up").  An lba_group
+ * rank waits at most 120 s for its peers, then the group is poisoned (every call returns an error). */
 typedef int (*lba_allreduce_fn)(double* dev_buf, int64_t count, void* hip_stream, void* user);
 int lba_set_partition(lba_problem* p, int32_t rank, int32_t nranks, lba_allreduce_fn fn, void* user);
 int lba_rccl_unique_id(void* id_out);   /* NCCL_UNIQUE_ID_BYTES (128) bytes, on one rank, shared by the caller */
@@ -203,6 +210,10 @@ int lba_set_state(lba_problem* p, const lba_kf* kf_in, const double* lm_xyz);
  * the LocalGPBA depth test (both KF poses for GP edges, include/G2oTypes.h:305-314).
  * Any output pointer may be NULL. */
 int lba_eval(lba_problem* p, double* chi2_robust, double* obs_chi2, uint8_t* depth_ok);
+/* Per-observation chi2 of the last computed errors, without evaluating anything: after lba_optimize
+ * the errors of its last trial state, accepted or not (g2o's e->chi2() after optimize(): the
+ * _error of the last computeActiveErrors, src/Optimizer.cc:1300-1330). */
+int lba_trial_chi2(lba_problem* p, double* obs_chi2);
 
 /* Parity/debug entry points (no LM).  lba_linearize: computeActiveErrors + buildSystem at the
  * current estimate: residuals [n_obs*3] (unused components 0), H_pp dense [np*np] full

@@ -905,6 +905,12 @@ double orc_compute_errors(orc_problem* p, double* residuals, double* obs_chi2) {
     return chi;
 }
 
+/* chi2 of the stored errors (the last compute_errors: after orc_optimize its last trial state), nothing
+ * recomputed: g2o's e->chi2() after optimize() (base_edge.h:58-61) */
+void orc_last_obs_chi2(const orc_problem* p, double* obs_chi2) {
+    for (int i = 0; i < p->n_obs; ++i) obs_chi2[i] = chi2_of(p->obs_err + 3 * i, obs_dim(p->obs[i].kind), p->obs[i].w);
+}
+
 /* ------------------------------------------------------------------ buildSystem */
 /* add an (i,j) pose-pose block contribution (pdim[i] x pdim[j], row-major) into the upper triangle of
  * dense Hpp */

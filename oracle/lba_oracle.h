@@ -42,6 +42,7 @@ void   orc_normal_residual(const orc_problem* p, double lambda, const double* dx
 int    orc_optimize(orc_problem* p, int iters, lba_stats* stats);
 void   orc_get_state(const orc_problem* p, lba_kf* kfs, double* lm_xyz);
 void   orc_depth_ok(const orc_problem* p, unsigned char* ok);
+void   orc_last_obs_chi2(const orc_problem* p, double* obs_chi2);
 void   orc_get_cams(const orc_problem* p, lba_cam* cams);   /* camera extrinsics (VertexExtrinsic estimates) */
 
 /* single-edge evaluation at the current estimate: err[3], J[3*27] row-major with columns

@@ -443,7 +443,7 @@ def local_gpba(snap, kf_id, large=False, iters=10, extrinsic=False):
         o = orc.Oracle(W.win, cfg=make_config(**W.win.cfg))
         n2, st = o.optimize(4 if large else 10)
         n_it += n2
-    _, _, chi2 = o.errors()
+    chi2 = o.last_obs_chi2()   # g2o's e->chi2(): the last computeActiveErrors (last trial state)
     depth = o.depth_ok()
     err_end = F32(st.chi2_final)
     n = pm.n_cam

@@ -49,6 +49,8 @@ def lib():
         L.orc_get_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _dp]
         L.orc_get_cams.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.orc_depth_ok.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_last_obs_chi2.argtypes = [ctypes.c_void_p, _dp]
+        L.orc_last_obs_chi2.restype = None
         L.orc_obs_linearize.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp]
         L.orc_prior_linearize.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp, _dp]
         for n in ("orc_se3_exp", "orc_se3_log", "orc_so3_exp", "orc_so3_log", "orc_right_jac_pose3",
@@ -137,6 +139,12 @@ class Oracle:
         lm = np.zeros((self.n_lm, 3))
         lib().orc_get_state(self.h, ptr(kfs), _d(lm))
         return kfs, lm
+
+    def last_obs_chi2(self):
+        """chi2 of the last computed errors (after optimize: the last trial state), nothing recomputed."""
+        c2 = np.zeros(self.n_obs)
+        lib().orc_last_obs_chi2(self.h, _d(c2))
+        return c2
 
     def depth_ok(self):
         ok = np.zeros(self.n_obs, np.uint8)

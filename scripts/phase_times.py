@@ -1,4 +1,4 @@
-"""Per-phase cycle breakdown of k_linearize / k_schur (diagnostics).
+"""Per-phase cycle breakdown of k_lin_schur (linearisation phases, then elimination phases; diagnostics).
 
 Runs a window with LBA_PHASE_TIMING set (the library then records clock64() at the phase boundaries of
 every workgroup and dumps them when the problem is destroyed), then prints per-phase averages and how
@@ -15,8 +15,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "amc-slam_amd"))
 
-LIN_PHASES = ["obs residual+J1 -> LDS", "sample M/g", "Hpl = N^T G", "Hll/bl"]
-SCHUR_PHASES = ["stage Hpl + lists + LDL", "slot map + W", "S partials (MFMA)", "-", "rhs partials"]
+LIN_PHASES = ["obs residual+J1 -> LDS", "sample M/g", "Hll/bl (+Dinv, LDL)", "Hpl = N^T G"]
+SCHUR_PHASES = ["W = Hpl L^-T", "S partials (MFMA)", "rhs partials"]
 SHAPE = ["nobs", "nsmp", "npair", "nlm", "nsent", "nkf"]
 
 
@@ -44,6 +44,8 @@ def load(path):
 
 
 def report(name, stamps, phases, shape, out):
+    live = stamps[:, len(phases)] != 0   # (segment tiles of heavy landmarks have no elimination stamps)
+    stamps, shape = stamps[live], shape[:, live]
     d = np.diff(stamps[:, :len(phases) + 1], axis=1)
     tot = stamps[:, len(phases)] - stamps[:, 0]
     out.append(f"== {name}: {stamps.shape[0]} workgroups, cycles per workgroup (clock64)")
@@ -72,8 +74,8 @@ def main():
     p.close()
     nt, lin, sch, shape, chol, bs, cft = load(args.dump)
     out = [f"config {args.config}: {nt} tiles"]
-    report("k_linearize", lin, LIN_PHASES, shape, out)
-    report("k_schur", sch, SCHUR_PHASES, shape, out)
+    report("k_lin_schur (linearisation)", lin, LIN_PHASES, shape, out)
+    report("k_lin_schur (elimination)", sch, SCHUR_PHASES, shape, out)
     if chol is not None:
         if os.environ.get("LBA_CHOL_STEPS") is None:   # k_chol_flow: s_memrealtime (100 MHz) stamps per panel
             npan = int((chol[:, 0] != 0).sum())

@@ -1,6 +1,9 @@
-"""Summarise the rocprofv3 PMC passes of scripts/pmc_linearize.sh into the per-launch HBM traffic of
-k_linearize (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md §HBM).
-FETCH_SIZE / WRITE_SIZE are reported in KB by rocprofv3."""
+"""Summarise the rocprofv3 PMC passes of scripts/pmc_linearize.sh for one kernel: the per-launch HBM
+traffic (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md §HBM; rocprofv3
+reports both in KB) and, when the SQ pass ran, per-launch medians of its counters.
+
+    python scripts/pmc_summary.py <pmc dir> <out.json> [kernel]
+"""
 import csv
 import glob
 import json
@@ -8,32 +11,45 @@ import os
 import sys
 
 
-def per_dispatch(dirname, counter):
+def per_dispatch(dirname, counter, kernel):
     vals = {}
     for f in glob.glob(os.path.join(dirname, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if r.get("Counter_Name") != counter or "k_linearize" not in r.get("Kernel_Name", ""):
+            if r.get("Counter_Name") != counter or kernel not in r.get("Kernel_Name", ""):
                 continue
             key = (r.get("Agent_Id"), r.get("Dispatch_Id"))
             vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
     return list(vals.values())
 
 
+def median(v):
+    return sorted(v)[len(v) // 2] if v else None
+
+
 def main():
     src, dst = sys.argv[1], sys.argv[2]
-    fetch = per_dispatch(os.path.join(src, "FETCH_SIZE"), "FETCH_SIZE")
-    write = per_dispatch(os.path.join(src, "WRITE_SIZE"), "WRITE_SIZE")
+    kernel = sys.argv[3] if len(sys.argv) > 3 else "k_lin_schur"
+    fetch = per_dispatch(os.path.join(src, "FETCH_SIZE"), "FETCH_SIZE", kernel)
+    write = per_dispatch(os.path.join(src, "WRITE_SIZE"), "WRITE_SIZE", kernel)
     if not fetch or not write:
-        raise SystemExit("no k_linearize counter rows found")
-    f_kb = sorted(fetch)[len(fetch) // 2]
-    w_kb = sorted(write)[len(write) // 2]
+        raise SystemExit(f"no {kernel} counter rows found")
+    f_kb, w_kb = median(fetch), median(write)
     fetch_b = 2.0 * f_kb * 1024.0   # gfx950: FETCH_SIZE reports half the bytes of wide streaming reads
     write_b = w_kb * 1024.0
-    out = {"workload": "cfg1_local_50kf", "kernel": "k_linearize", "dispatches": [len(fetch), len(write)],
+    out = {"workload": "cfg1_local_50kf", "kernel": kernel, "dispatches": [len(fetch), len(write)],
            "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
            "hbm_read_bytes_per_launch": fetch_b, "hbm_write_bytes_per_launch": write_b,
            "hbm_bytes_per_launch": fetch_b + write_b,
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), FETCH_SIZE x2 (gfx950)"}
+    sq_dir = os.path.join(src, "SQ")
+    if os.path.isdir(sq_dir):
+        sq = {}
+        for c in ("SQ_WAVES", "SQ_BUSY_CYCLES", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT"):
+            v = per_dispatch(sq_dir, c, kernel)
+            sq[c] = median(v)
+        if sq.get("SQ_INSTS_LDS") and sq.get("SQ_LDS_BANK_CONFLICT") is not None:
+            sq["lds_bank_conflict_per_lds_inst"] = sq["SQ_LDS_BANK_CONFLICT"] / sq["SQ_INSTS_LDS"]
+        out["sq_per_launch_median"] = sq
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out))
 

@@ -85,3 +85,33 @@ def test_partitioned_needs_user_lambda():
     win = make_window(**WINDOWS["global_shape"])
     with pytest.raises(LbaError):
         run_partitioned(win, 2, 2, lambda_init=0.0)
+
+
+def test_one_failing_rank_releases_its_peers():
+    """A set-up that fails on one rank only (here an out-of-range observation in rank 1's partition)
+    fails on every rank instead of leaving the others in the union-envelope all-reduce: the ranks
+    exchange their set-up status first (partition status before the first collective)."""
+    from dataclasses import replace
+    from amc_lba.abi import LBA_E_ARG
+    win = make_window(**WINDOWS["global_shape"])
+    parts = [partition_window(win, r, 2)[0] for r in range(2)]
+    bad = replace(parts[1], obs=parts[1].obs.copy())
+    bad.obs["lm"][0] = len(bad.lm) + 5
+    parts[1] = bad
+    g = Group(2)
+    codes = [None, None]
+
+    def setup(r):
+        try:
+            Problem(parts[r], group=g, rank=r, early_stop=0).close()
+            codes[r] = 0
+        except LbaError as e:
+            codes[r] = e.code
+    ts = [threading.Thread(target=setup, args=(r,)) for r in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in ts), "a rank hung in the set-up"
+    g.close()
+    assert codes == [LBA_E_ARG, LBA_E_ARG]
