@@ -14,7 +14,8 @@ from .abi import (CAM_DTYPE, KF_DTYPE, OBS_DTYPE, PRIOR_DTYPE, LbaConfig, LbaSta
                   ptr)
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libamc_lba.so")
+# AMC_LBA_LIB: another build of the library (kernel experiments; scripts/exp_build.sh)
+LIB_PATH = os.environ.get("AMC_LBA_LIB") or os.path.join(PKG_DIR, "lib", "libamc_lba.so")
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _lib = None

@@ -576,7 +576,10 @@ __device__ void edge_item(const DevProblem& P, int sel, int idx, const int tid, 
 // eliminates those landmarks.  With LS_SCHUR the launch also clears the envelope of S for this trial's
 // assembly and the factorisation status.
 constexpr int LS_THREADS = 256;
-constexpr int LS_U = TILE_PAIRS * 36;   // doubles: rows + weights while linearising, then Hpl / W
+constexpr int LS_U = (TILE_PAIRS + 2) * 36;   // doubles: rows + weights while linearising, then Hpl / W
+                                              // (+ two zero pairs after the tile's last: the MFMA gathers'
+                                              // target for absent (landmark, KF) pairs)
+constexpr int DL_STRIDE = 12;   // per landmark in LDS: l10 l21 (l10 l21 - l20) 0 | D^-1 (3) 0 | u (3) 0
 static_assert(TILE_ROWS * (ROW_STRIDE + 1) <= LS_U, "the LDS rows alias the Hpl staging");
 static_assert(EDGE_SHM <= LS_U, "edge items run in the tile LDS");
 static_assert(2 * TILE_PAIRS <= LS_THREADS && TILE_KF * TILE_KF <= LS_THREADS && TILE_SENT <= LS_THREADS &&
@@ -586,7 +589,7 @@ static_assert(2 * TILE_PAIRS <= LS_THREADS && TILE_KF * TILE_KF <= LS_THREADS &&
 __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int sel, int gate, double lambda_arg,
                                                              int mode) {
     __shared__ double U[LS_U];
-    __shared__ double Dl[TILE_LMS * 9];          // per landmark: L^-T terms l10, l21, l10 l21 - l20; D^-1 (3); u (3)
+    __shared__ double Dl[TILE_LMS * DL_STRIDE];  // per landmark: L^-T terms, D^-1, u = D^-1 L^-1 bl (DL_STRIDE)
     __shared__ int tsm[2 * TILE_SMP];
     __shared__ int osm[TILE_OBS];
     __shared__ int ocam[TILE_OBS];
@@ -596,7 +599,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
     __shared__ int lrow[TILE_ROWS];
     __shared__ int lr0[TILE_LMS + 1];
     __shared__ int eslot[TILE_KF * TILE_KF];     // sslab slot of the tile's KF pair (l1 <= l2), -1: not coupled
-    __shared__ short pidx[TILE_LMS * TILE_KF];   // tile-local pair of (landmark, tile KF), -1: none
+    __shared__ __attribute__((aligned(16))) short pidx[TILE_KF * TILE_LMS];   // [tile KF][landmark]: tile-local pair, npair (a zero pair): none
     __shared__ unsigned char pm[TILE_PAIRS];     // tile-local landmark of a pair
     __shared__ double red[LS_THREADS / 64];
     if (gated_off(P.ctl, gate)) return;
@@ -648,7 +651,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
         if (tid <= nlm) lr0[tid] = P.lm_r0[lm0 + tid] - m0;
         if (elim) {
             eslot[tid] = -1;
-            for (int t = tid; t < TILE_LMS * TILE_KF; t += LS_THREADS) pidx[t] = -1;
+            for (int t = tid; t < TILE_LMS * TILE_KF; t += LS_THREADS) pidx[t] = (short)npair;
         }
     }
 
@@ -674,7 +677,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
         if (tid < nsent) eslot[P.sent_l1[sent0 + tid] * TILE_KF + P.sent_l2[sent0 + tid]] = P.sslot[sent0 + tid];
         if (tid < npair) {
             const int c = P.pair_lk[pair0 + tid];
-            pidx[(c >> 8) * TILE_KF + (c & 255)] = (short)tid;
+            pidx[(c & 255) * TILE_LMS + (c >> 8)] = (short)tid;
             pm[tid] = (unsigned char)(c >> 8);
         }
     }
@@ -730,11 +733,13 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
                 const double l21 = (H[7] - l20 * l10 * d0) / d1;
                 const double d2 = H[8] - l20 * l20 * d0 - l21 * l21 * d1;
                 const double y1 = b[1] - l10 * b[0], y2 = b[2] - l20 * b[0] - l21 * y1;   // L^-1 bl
-                double* o = Dl + t * 9;
-                o[0] = l10; o[1] = l21; o[2] = l10 * l21 - l20;
-                o[3] = 1.0 / d0; o[4] = 1.0 / d1; o[5] = 1.0 / d2;
-                o[6] = b[0] / d0; o[7] = y1 / d1; o[8] = y2 / d2;
+                double* o = Dl + t * DL_STRIDE;
+                o[0] = l10; o[1] = l21; o[2] = l10 * l21 - l20; o[3] = 0.0;
+                o[4] = 1.0 / d0; o[5] = 1.0 / d1; o[6] = 1.0 / d2; o[7] = 0.0;
+                o[8] = b[0] / d0; o[9] = y1 / d1; o[10] = y2 / d2; o[11] = 0.0;
             }
+        } else if (elim && t < ((nlm + 3) & ~3)) {   // the MFMA loop reads landmarks in fours
+            for (int q = 0; q < DL_STRIDE; ++q) Dl[t * DL_STRIDE + q] = 0.0;
         }
     }
     LBA_TMARK(P.tdbg_lin, 3);
@@ -796,13 +801,14 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
 #pragma unroll
         for (int q = 0; q < 18; ++q) h[q] = hacc[q];
     }
+    if (tid < 72) U[npair * 36 + tid] = 0.0;   // the zero pairs
     __syncthreads();
     LBA_TMARKI(P.tdbg_schur, tile, 0);
     // ---- phase 5: W = Hpl L^-T in place, one (pair, row) per task:
     //      L^-1 = [1 0 0; -l10 1 0; l10 l21 - l20, -l21, 1], w_a = sum_b h_b (L^-1)(a, b)
     for (int task = tid; task < npair * 12; task += LS_THREADS) {
         const int t = task / 12, r = task - 12 * t;
-        const double* D = Dl + pm[t] * 9;
+        const double* D = Dl + pm[t] * DL_STRIDE;
         double* h = U + t * 36 + r * 3;
         const double h0 = h[0], h1 = h[1], h2 = h[2];
         h[1] = h1 - D[0] * h0;
@@ -810,43 +816,62 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
     }
     __syncthreads();
     LBA_TMARKI(P.tdbg_schur, tile, 1);
-    // ---- phase 6: S partials, C = W diag(D^-1) W^T over the tile's KF rows, upper 16 x 16 tiles
+    // ---- phase 6: S partials, C = W diag(D^-1) W^T over the tile's KF rows, upper 16 x 16 tiles.  The
+    //      MFMA's K = 4 is one landmark (its 3 dimensions and a zero: D^-1 padded), so a step's landmark is
+    //      uniform across the wave; a lane gathers its row of W through pidx[KF][landmark], which names
+    //      a zero pair where the landmark does not see the KF: no branches, two independent MFMA chains.
     const int nkf = P.tile_nkf[tile];
     {
         const int lane = tid & 63, wave = tid >> 6, kq = lane >> 4, cl = lane & 15;
-        const int nr = 12 * nkf, K = 3 * nlm;
+        const int nr = 12 * nkf;
         const int nt = (nr + 15) >> 4, nut = nt * (nt + 1) / 2;
         for (int u = wave; u < nut; u += LS_THREADS / 64) {
             int tr = 0, rem = u;
             while (rem >= nt - tr) { rem -= nt - tr; ++tr; }
             const int tc = tr + rem;
             const int ra = 16 * tr + cl, rb = 16 * tc + cl;
-            const int la = ra / 12, ia = ra - 12 * la, lb = rb / 12, ib = rb - 12 * lb;
             const bool va = ra < nr, vb = rb < nr;
+            const int la = va ? ra / 12 : 0, lb = vb ? rb / 12 : 0;
+            const int offa = (va ? ra - 12 * la : 0) * 3 + kq, offb = (vb ? rb - 12 * lb : 0) * 3 + kq;
+            // the lane's pidx rows, four landmarks per 8-byte LDS read (rows are TILE_LMS shorts, 128 B)
+            const uint2* pra = reinterpret_cast<const uint2*>(pidx + la * TILE_LMS);
+            const uint2* prb = reinterpret_cast<const uint2*>(pidx + lb * TILE_LMS);
+            const int zp = npair * 36;
             d4 c0 = {0.0, 0.0, 0.0, 0.0}, c1 = c0;
-            for (int k0 = 0; k0 < K; k0 += 8) {
-                double av[2], bv[2];
+            for (int m0 = 0; m0 < nlm; m0 += 4) {
+                const uint2 qa = pra[m0 >> 2], qb = prb[m0 >> 2];
+                int pa[4], pb[4];
+                pa[0] = qa.x & 0xffff; pa[1] = qa.x >> 16; pa[2] = qa.y & 0xffff; pa[3] = qa.y >> 16;
+                pb[0] = qb.x & 0xffff; pb[1] = qb.x >> 16; pb[2] = qb.y & 0xffff; pb[3] = qb.y >> 16;
+                double av[4], bv[4];
 #pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    const int k = k0 + 4 * hh + kq;
-                    const bool ok = k < K;
-                    const int m = ok ? k / 3 : 0, a = k - 3 * (k / 3);
-                    const int pa = (ok && va) ? pidx[m * TILE_KF + la] : -1;
-                    const int pb = (ok && vb) ? pidx[m * TILE_KF + lb] : -1;
-                    av[hh] = pa >= 0 ? U[pa * 36 + ia * 3 + a] * Dl[m * 9 + 3 + a] : 0.0;
-                    bv[hh] = pb >= 0 ? U[pb * 36 + ib * 3 + a] : 0.0;
+                for (int j = 0; j < 4; ++j) {   // (landmarks past nlm: their pidx entries name the zero pair)
+                    const int ia = va ? pa[j] * 36 : zp, ib2 = vb ? pb[j] * 36 : zp;
+                    av[j] = U[ia + offa] * Dl[(m0 + j) * DL_STRIDE + 4 + kq];
+                    bv[j] = U[ib2 + offb];
                 }
+#ifndef LBA_EXP_NOMFMA
                 c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0], bv[0], c0, 0, 0, 0);
                 c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1], bv[1], c1, 0, 0, 0);
+                c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[2], bv[2], c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[3], bv[3], c1, 0, 0, 0);
+#else
+                c0[0] += av[0] * bv[0] + av[2] * bv[2]; c1[0] += av[1] * bv[1] + av[3] * bv[3];
+#endif
             }
             const d4 c = c0 + c1;
+            const int ib = rb - 12 * lb;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int r = 16 * tr + kq + 4 * q;   // C(r, rb): row of lane group kq, column of lane cl
                 if (r < nr && vb && r <= rb) {
                     const int l1 = r / 12, i = r - 12 * l1;
                     const int s = eslot[l1 * TILE_KF + lb];
+#ifdef LBA_EXP_NOSTORE
+                    if (s >= 0 && c[q] == 12345.678) {
+#else
                     if (s >= 0) {
+#endif
                         double* o = P.sslab + (size_t)s * 144;
                         o[i * 12 + ib] = c[q];
                         if (l1 == lb && i != ib) o[ib * 12 + i] = c[q];   // a diagonal block: both halves
@@ -856,21 +881,29 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
         }
     }
     LBA_TMARKI(P.tdbg_schur, tile, 2);
-    // ---- phase 7: rhs partials: sum over the KF's landmarks of V(m,k) bl_m (block_solver.hpp:395-401)
+    // ---- phase 7: rhs partials: sum over the KF's landmarks of V(m,k) bl_m = W(m,k) u_m
+    //      (block_solver.hpp:395-401); absent pairs read the zero pair
     {
         const int kf0 = P.tile_kf0[tile];
         for (int task = tid; task < nkf * 12; task += LS_THREADS) {
-            const int l = task / 12, r = task % 12;
-            double v = 0.0;
-            for (int m = 0; m < nlm; ++m) {
-                const int t = pidx[m * TILE_KF + l];
-                if (t >= 0) {
-                    const double* w = U + t * 36 + r * 3;
-                    const double* uu = Dl + m * 9 + 6;
-                    v += w[0] * uu[0] + w[1] * uu[1] + w[2] * uu[2];
-                }
+            const int l = task / 12, r = task - 12 * l;
+            const short* pr = pidx + l * TILE_LMS;
+            double v0 = 0.0, v1 = 0.0;
+            int m = 0;
+            for (; m + 2 <= nlm; m += 2) {
+                const double* w0 = U + pr[m] * 36 + r * 3;
+                const double* w1 = U + pr[m + 1] * 36 + r * 3;
+                const double* u0 = Dl + m * DL_STRIDE + 8;
+                const double* u1 = u0 + DL_STRIDE;
+                v0 += w0[0] * u0[0] + w0[1] * u0[1] + w0[2] * u0[2];
+                v1 += w1[0] * u1[0] + w1[1] * u1[1] + w1[2] * u1[2];
             }
-            P.gpslab[(size_t)P.tkf_gslot[kf0 + l] * 12 + r] = v;
+            if (m < nlm) {
+                const double* w0 = U + pr[m] * 36 + r * 3;
+                const double* u0 = Dl + m * DL_STRIDE + 8;
+                v0 += w0[0] * u0[0] + w0[1] * u0[1] + w0[2] * u0[2];
+            }
+            P.gpslab[(size_t)P.tkf_gslot[kf0 + l] * 12 + r] = v0 + v1;
         }
     }
     LBA_TMARKI(P.tdbg_schur, tile, 3);
