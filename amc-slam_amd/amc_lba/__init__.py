@@ -27,12 +27,26 @@ class LbaError(RuntimeError):
         self.code = code
 
 
+def check_fresh(which="engine"):
+    """Raise if the in-tree library is missing or was built from other sources than the ones beside it
+    (build.py's content stamp): a stale binary is never loaded silently."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_amc_lba_build", os.path.join(PKG_DIR, "build.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    why = b.stale(which)
+    if why:
+        raise RuntimeError(f"{why}: run python -c 'import __graft_entry__ as g; g.build()'")
+
+
 def lib():
-    """Load libamc_lba.so (built by __graft_entry__.build()); raises if it is missing."""
+    """Load libamc_lba.so (built by __graft_entry__.build()); raises if it is missing or stale."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} not built: run python -c 'import __graft_entry__ as g; g.build()'")
+        if not os.environ.get("AMC_LBA_LIB"):
+            check_fresh("engine")
         L = ctypes.CDLL(LIB_PATH)
         vp = ctypes.c_void_p
         L.lba_abi_version.restype = ctypes.c_int

@@ -341,6 +341,8 @@ def map_lib():
     if _lib is None:
         if not os.path.exists(MAP_LIB_PATH):
             raise RuntimeError(f"{MAP_LIB_PATH} not built: run python -c 'import __graft_entry__ as g; g.build()'")
+        from . import check_fresh
+        check_fresh("map")
         L = ctypes.CDLL(MAP_LIB_PATH)
         vp = ctypes.c_void_p
         L.lbamap_load.argtypes = [ctypes.POINTER(vp), ctypes.c_char_p, ctypes.c_size_t]
