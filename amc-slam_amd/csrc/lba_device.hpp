@@ -44,7 +44,6 @@ constexpr int SM_STRIDE = 27;       // per (tile, sample) partial: M = sum rho' 
                                     // row-major) and g = sum rho' w J1^T e (6)
 constexpr int TILE_SMP = 64;        // pose samples per tile (k_linearize stages their row runs)
 constexpr int TILE_PROWS = 2 * TILE_OBS;    // pair entry-list entries per tile (each obs feeds <= 2 pairs)
-constexpr int LS_MFMA_CAP = 320;    // S-partial MFMA steps per tile (k_lin_schur: upper 16 x 16 output tiles x K / 8)
 constexpr int TILE_SENT = TILE_KF * (TILE_KF + 1) / 2;   // KF-pair Schur entries per tile
 
 constexpr int CHOL_NB = 32;         // Cholesky panel / tile width

@@ -423,15 +423,10 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     //      long track: LocalGPBA adds every observation of a local point, up to every keyframe of the
     //      window plus GP observations from non-keyframes, src/Optimizer.cc:1050-1200) is linearised in
     //      segment tiles and merged / eliminated by k_expand (heavy_item); heavy landmarks go last in
-    //      device order.  tile_fits: the LDS limits of one k_lin_schur workgroup, and a cap on its dense
-    //      S-partial product (12 nkf x 12 nkf over K = 3 nlm, phase 6)
-    auto mfma_steps = [](int nkf, int nlm) {
-        const int nt = (12 * nkf + 15) / 16;
-        return nt * (nt + 1) / 2 * ((3 * nlm + 7) / 8);
-    };
+    //      device order.  tile_fits: the LDS limits of one k_lin_schur workgroup
     auto tile_fits = [&](int no, int nr, int npair, int nlmt, int nkf, int ns, int ne) {
         return no <= TILE_OBS && nr <= TILE_ROWS && npair <= TILE_PAIRS && nlmt <= TILE_LMS && nkf <= TILE_KF &&
-               ns <= TILE_SMP && ne <= TILE_PROWS && mfma_steps(nkf, nlmt) <= LS_MFMA_CAP;
+               ns <= TILE_SMP && ne <= TILE_PROWS;
     };
     // observations by original landmark (stable)
     std::vector<int> lo0(n_lm + 1, 0), lo_of(n_obs);

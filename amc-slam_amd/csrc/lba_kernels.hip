@@ -8,7 +8,7 @@
 //                    buffer, deterministic on-chip reductions into pose-sample partials, Hpl blocks and
 //                    Hll/bl (BlockSolver::buildSystem, block_solver.hpp:502-560; edge quadratic forms
 //                    base_multi_edge.hpp:170-222), then in the same workgroup the landmark elimination:
-//                    Dinv = (Hll + lambda I)^-1, S partials sum Hpl Dinv Hpl^T (fp64 MFMA) and rhs
+//                    Dinv = (Hll + lambda I)^-1, S partials sum Hpl Dinv Hpl^T (fp64 VALU) and rhs
 //                    partials (block_solver.hpp:381-430); EdgeGaussianPrior / EdgeVelocity /
 //                    EdgeExtrinsicPrior quadratic forms as extra workgroups (src/G2oTypes.cc:100-118)
 //   k_expand         per pose sample N^T M N into Hpp / b_p pieces; heavy landmarks (merge + elimination)
@@ -564,10 +564,8 @@ __device__ void edge_item(const DevProblem& P, int sel, int idx, const int tid, 
 //      block_solver.hpp:389) -> HBM, and Hll + lambda I = L D L^T -> LDS
 //   (eliminating regular tiles only; from here on the LDS of the rows holds Hpl)
 //   5. W = Hpl L^-T in place
-//   6. S partials: over the tile's KF rows r = 12 lk + i and landmark dimensions k = 3 m + a,
-//      C = W diag(D^-1) W^T, i.e. sum_m Hpl(m,k1) Dinv_m Hpl(m,k2)^T for every KF pair at once: one
-//      16 x 16 tile of C's upper triangle per wave and pass on the matrix cores (fp64 MFMA, K = 3 nlm),
-//      the operands gathered from W through pidx[m][lk] (zero where landmark m does not see KF lk)
+//   6. S partials: per Schur entry (KF pair k1 <= k2 of the tile) C = sum_m W(m,k1) D_m^-1 W(m,k2)^T =
+//      sum_m Hpl(m,k1) Dinv_m Hpl(m,k2)^T over the landmarks that see both (fp64 FMAs, 3 x 6 blocks)
 //   7. rhs partials per tile KF: sum_m W(m, k) u_m, u = D^-1 L^-1 bl (= sum_m Hpl Dinv bl)
 // (1-4: BlockSolver::buildSystem, block_solver.hpp:502-560, with the edges' quadratic forms,
 // base_multi_edge.hpp:170-222; 4-7: BlockSolver::solve's Schur loop, block_solver.hpp:381-432.)
@@ -577,8 +575,8 @@ __device__ void edge_item(const DevProblem& P, int sel, int idx, const int tid, 
 // assembly and the factorisation status.
 constexpr int LS_THREADS = 256;
 constexpr int LS_U = (TILE_PAIRS + 2) * 36;   // doubles: rows + weights while linearising, then Hpl / W
-                                              // (+ two zero pairs after the tile's last: the MFMA gathers'
-                                              // target for absent (landmark, KF) pairs)
+                                              // (+ two zero pairs after the tile's last: what phase 7
+                                              // reads for absent (landmark, KF) pairs)
 constexpr int DL_STRIDE = 12;   // per landmark in LDS: l10 l21 (l10 l21 - l20) 0 | D^-1 (3) 0 | u (3) 0
 static_assert(TILE_ROWS * (ROW_STRIDE + 1) <= LS_U, "the LDS rows alias the Hpl staging");
 static_assert(EDGE_SHM <= LS_U, "edge items run in the tile LDS");
@@ -598,7 +596,8 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
     __shared__ int pr0[TILE_PAIRS + 1];
     __shared__ int lrow[TILE_ROWS];
     __shared__ int lr0[TILE_LMS + 1];
-    __shared__ int eslot[TILE_KF * TILE_KF];     // sslab slot of the tile's KF pair (l1 <= l2), -1: not coupled
+    __shared__ int scode[TILE_SENT];             // Schur entry: tile-local KF l1 | l2 << 8 (l1 <= l2)
+    __shared__ int sslt[TILE_SENT];              // its sslab slot
     __shared__ __attribute__((aligned(16))) short pidx[TILE_KF * TILE_LMS];   // [tile KF][landmark]: tile-local pair, npair (a zero pair): none
     __shared__ unsigned char pm[TILE_PAIRS];     // tile-local landmark of a pair
     __shared__ double red[LS_THREADS / 64];
@@ -649,10 +648,8 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
         }
         if (tid <= npair) pr0[tid] = P.pair_r0[pair0 + tid] - q0;
         if (tid <= nlm) lr0[tid] = P.lm_r0[lm0 + tid] - m0;
-        if (elim) {
-            eslot[tid] = -1;
+        if (elim)
             for (int t = tid; t < TILE_LMS * TILE_KF; t += LS_THREADS) pidx[t] = (short)npair;
-        }
     }
 
     // ---- phase 1: one observation per lane: residual, robust weight, rows [J1 e Jp] -> LDS
@@ -672,9 +669,13 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
     }
     const double tchi = block_sum<LS_THREADS>(rho0, red);   // (its barrier also publishes rows / lists)
     if (tid == 0) P.chi_lin[tile] = tchi;
-    if (elim) {   // the elimination's tables (their clearing was ordered by that barrier)
-        const int sent0 = P.tile_sent0[tile], nsent = P.tile_nsent[tile];
-        if (tid < nsent) eslot[P.sent_l1[sent0 + tid] * TILE_KF + P.sent_l2[sent0 + tid]] = P.sslot[sent0 + tid];
+    const int nsent = elim ? P.tile_nsent[tile] : 0;
+    if (elim) {   // the elimination's tables (the clearing of pidx was ordered by that barrier)
+        const int sent0 = P.tile_sent0[tile];
+        if (tid < nsent) {
+            scode[tid] = P.sent_l1[sent0 + tid] | (P.sent_l2[sent0 + tid] << 8);
+            sslt[tid] = P.sslot[sent0 + tid];
+        }
         if (tid < npair) {
             const int c = P.pair_lk[pair0 + tid];
             pidx[(c & 255) * TILE_LMS + (c >> 8)] = (short)tid;
@@ -738,8 +739,6 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
                 o[4] = 1.0 / d0; o[5] = 1.0 / d1; o[6] = 1.0 / d2; o[7] = 0.0;
                 o[8] = b[0] / d0; o[9] = y1 / d1; o[10] = y2 / d2; o[11] = 0.0;
             }
-        } else if (elim && t < ((nlm + 3) & ~3)) {   // the MFMA loop reads landmarks in fours
-            for (int q = 0; q < DL_STRIDE; ++q) Dl[t * DL_STRIDE + q] = 0.0;
         }
     }
     LBA_TMARK(P.tdbg_lin, 3);
@@ -816,69 +815,41 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
     }
     __syncthreads();
     LBA_TMARKI(P.tdbg_schur, tile, 1);
-    // ---- phase 6: S partials, C = W diag(D^-1) W^T over the tile's KF rows, upper 16 x 16 tiles.  The
-    //      MFMA's K = 4 is one landmark (its 3 dimensions and a zero: D^-1 padded), so a step's landmark is
-    //      uniform across the wave; a lane gathers its row of W through pidx[KF][landmark], which names
-    //      a zero pair where the landmark does not see the KF: no branches, two independent MFMA chains.
+    // ---- phase 6: S partials, C(k1, k2) = sum over the tile's landmarks m of W(m,k1) D_m^-1 W(m,k2)^T
+    //      (Hpl(m,k1) Dinv_m Hpl(m,k2)^T; W(m,k) the zero pair where m does not see k), on the VALU: gfx950
+    //      retires fp64 FMAs at ~1.35x its fp64 MFMA rate (scripts/micro/f64_rates.hip) and the VALU form
+    //      needs no K padding, zero blocks or padded rows.  One task per (Schur entry, 3-row group,
+    //      6-column half) keeps its 3 x 6 block of C in registers; every lane walks the tile's landmarks in
+    //      the same order, so a wave's LDS reads of one step hit one landmark's pairs (broadcasts, few
+    //      bank conflicts) and D_m^-1 is one broadcast read
     const int nkf = P.tile_nkf[tile];
-    {
-        const int lane = tid & 63, wave = tid >> 6, kq = lane >> 4, cl = lane & 15;
-        const int nr = 12 * nkf;
-        const int nt = (nr + 15) >> 4, nut = nt * (nt + 1) / 2;
-        for (int u = wave; u < nut; u += LS_THREADS / 64) {
-            int tr = 0, rem = u;
-            while (rem >= nt - tr) { rem -= nt - tr; ++tr; }
-            const int tc = tr + rem;
-            const int ra = 16 * tr + cl, rb = 16 * tc + cl;
-            const bool va = ra < nr, vb = rb < nr;
-            const int la = va ? ra / 12 : 0, lb = vb ? rb / 12 : 0;
-            const int offa = (va ? ra - 12 * la : 0) * 3 + kq, offb = (vb ? rb - 12 * lb : 0) * 3 + kq;
-            // the lane's pidx rows, four landmarks per 8-byte LDS read (rows are TILE_LMS shorts, 128 B)
-            const uint2* pra = reinterpret_cast<const uint2*>(pidx + la * TILE_LMS);
-            const uint2* prb = reinterpret_cast<const uint2*>(pidx + lb * TILE_LMS);
-            const int zp = npair * 36;
-            d4 c0 = {0.0, 0.0, 0.0, 0.0}, c1 = c0;
-            for (int m0 = 0; m0 < nlm; m0 += 4) {
-                const uint2 qa = pra[m0 >> 2], qb = prb[m0 >> 2];
-                int pa[4], pb[4];
-                pa[0] = qa.x & 0xffff; pa[1] = qa.x >> 16; pa[2] = qa.y & 0xffff; pa[3] = qa.y >> 16;
-                pb[0] = qb.x & 0xffff; pb[1] = qb.x >> 16; pb[2] = qb.y & 0xffff; pb[3] = qb.y >> 16;
-                double av[4], bv[4];
+    for (int task = tid; task < nsent * 8; task += LS_THREADS) {
+        const int q = task >> 3, rg = (task >> 1) & 3, ch = task & 1;
+        const short* p1 = pidx + (scode[q] & 255) * TILE_LMS;
+        const short* p2 = pidx + (scode[q] >> 8) * TILE_LMS;
+        double acc[18];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {   // (landmarks past nlm: their pidx entries name the zero pair)
-                    const int ia = va ? pa[j] * 36 : zp, ib2 = vb ? pb[j] * 36 : zp;
-                    av[j] = U[ia + offa] * Dl[(m0 + j) * DL_STRIDE + 4 + kq];
-                    bv[j] = U[ib2 + offb];
-                }
-#ifndef LBA_EXP_NOMFMA
-                c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0], bv[0], c0, 0, 0, 0);
-                c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1], bv[1], c1, 0, 0, 0);
-                c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[2], bv[2], c0, 0, 0, 0);
-                c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[3], bv[3], c1, 0, 0, 0);
-#else
-                c0[0] += av[0] * bv[0] + av[2] * bv[2]; c1[0] += av[1] * bv[1] + av[3] * bv[3];
-#endif
-            }
-            const d4 c = c0 + c1;
-            const int ib = rb - 12 * lb;
+        for (int u = 0; u < 18; ++u) acc[u] = 0.0;
+        for (int m = 0; m < nlm; ++m) {
+            const double* A = U + p1[m] * 36 + rg * 9;   // rows 3 rg .. 3 rg + 2 of W(m, k1)
+            const double* B = U + p2[m] * 36 + ch * 18;  // rows 6 ch .. 6 ch + 5 of W(m, k2)
+            const double* dd = Dl + m * DL_STRIDE + 4;
+            double a[9], b[18];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int r = 16 * tr + kq + 4 * q;   // C(r, rb): row of lane group kq, column of lane cl
-                if (r < nr && vb && r <= rb) {
-                    const int l1 = r / 12, i = r - 12 * l1;
-                    const int s = eslot[l1 * TILE_KF + lb];
-#ifdef LBA_EXP_NOSTORE
-                    if (s >= 0 && c[q] == 12345.678) {
-#else
-                    if (s >= 0) {
-#endif
-                        double* o = P.sslab + (size_t)s * 144;
-                        o[i * 12 + ib] = c[q];
-                        if (l1 == lb && i != ib) o[ib * 12 + i] = c[q];   // a diagonal block: both halves
-                    }
-                }
-            }
+            for (int u = 0; u < 9; ++u) a[u] = A[u] * dd[u % 3];
+#pragma unroll
+            for (int u = 0; u < 18; ++u) b[u] = B[u];
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 6; ++j)
+                    acc[i * 6 + j] += a[i * 3] * b[j * 3] + a[i * 3 + 1] * b[j * 3 + 1] + a[i * 3 + 2] * b[j * 3 + 2];
         }
+        double* o = P.sslab + (size_t)sslt[q] * 144 + (3 * rg) * 12 + 6 * ch;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 6; ++j) o[i * 12 + j] = acc[i * 6 + j];
     }
     LBA_TMARKI(P.tdbg_schur, tile, 2);
     // ---- phase 7: rhs partials: sum over the KF's landmarks of V(m,k) bl_m = W(m,k) u_m

@@ -13,13 +13,18 @@ timeout -k 10 400 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/$TA
 rc=$?; echo "smoke rc=$rc" | tee -a "$OUT/$TAG.status"
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q -rf --timeout 600 ${PYTEST_ARGS:-} > "$OUT/$TAG.pytest_gpu.log" 2>&1
+  timeout -k 10 900 python -m pytest ${TESTS:-tests} -m gpu -q -rf --timeout 600 > "$OUT/$TAG.pytest_gpu.log" 2>&1
   rc=$?; echo "pytest rc=$rc" | tee -a "$OUT/$TAG.status"
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 fi
 timeout -k 10 600 python bench.py --steps $STEPS --warmup 5 > "$OUT/$TAG.bench.log" 2>&1
 rc=$?; echo "bench rc=$rc" | tee -a "$OUT/$TAG.status"
 [ $rc -eq 0 ] || exit $rc
+if [ "${PHASES:-0}" = "1" ]; then
+  timeout -k 10 300 python scripts/phase_times.py --out "$OUT/${TAG}_phases.txt" > "$OUT/$TAG.phases.log" 2>&1
+  rc=$?; echo "phases rc=$rc" | tee -a "$OUT/$TAG.status"
+  [ $rc -eq 0 ] || exit $rc
+fi
 if [ "${SKIP_PROF:-0}" != "1" ]; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o trace \
