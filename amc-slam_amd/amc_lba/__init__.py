@@ -74,6 +74,14 @@ def lib():
         L.lba_group_destroy.restype = None
         L.lba_set_partition_group.argtypes = [vp, vp, ctypes.c_int32]
         L.lba_get_cams.argtypes = [vp, vp]
+        _ip = ctypes.POINTER(ctypes.c_int32)
+        _lp = ctypes.POINTER(ctypes.c_int64)
+        L.lba_set_farm.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp, vp]
+        L.lba_set_farm_rccl.argtypes = [vp, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32]
+        L.lba_set_farm_group.argtypes = [vp, vp, ctypes.c_int32]
+        L.lba_farm_plan.argtypes = [vp, _lp, _ip, _lp, _ip, _ip]
+        L.lba_farm_exchange.argtypes = [vp]
+        L.lba_farm_match.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _lp, _lp, _ip, ctypes.c_int32, _ip]
         _lib = L
     return _lib
 
@@ -82,7 +90,31 @@ def exported_symbols():
     return ["lba_abi_version", "lba_create", "lba_destroy", "lba_last_error", "lba_set_config", "lba_set_problem",
             "lba_optimize", "lba_get_state", "lba_set_state", "lba_eval", "lba_trial_chi2", "lba_linearize", "lba_solve_step",
             "lba_pose_dim", "lba_set_partition", "lba_rccl_unique_id", "lba_set_partition_rccl", "lba_group_create",
-            "lba_group_destroy", "lba_set_partition_group", "lba_get_cams"]
+            "lba_group_destroy", "lba_set_partition_group", "lba_get_cams", "lba_set_farm", "lba_set_farm_rccl",
+            "lba_set_farm_group", "lba_farm_plan", "lba_farm_exchange", "lba_farm_match"]
+
+
+def _i32(a):
+    a = np.ascontiguousarray(a, dtype=np.int32)
+    return a, a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+
+
+def _i64(a):
+    a = np.ascontiguousarray(a, dtype=np.int64)
+    return a, a.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+
+
+def farm_match(rank, nranks, cap, pub_gid, gid, owner):
+    """lba_farm_match (host only): source slot owner * cap + position of every received vertex, -1 for
+    the rest; returns (src, unmatched)."""
+    pg, pgp = _i64(np.asarray(pub_gid).reshape(-1))
+    g, gp = _i64(gid)
+    o, op = _i32(owner)
+    src = np.full(len(g), -1, dtype=np.int32)
+    rc = lib().lba_farm_match(rank, nranks, cap, pgp, gp, op, len(g), src.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    if rc < 0:
+        raise LbaError(rc, "lba_farm_match failed")
+    return src, rc
 
 
 class Group:
@@ -186,6 +218,26 @@ class Problem:
         c = np.zeros(len(self.win.cams), CAM_DTYPE)
         self._check(lib().lba_get_cams(self.h, ptr(c)))
         return c
+
+    # ---- window farm (lba_set_farm_*, lba_farm_plan, lba_farm_exchange)
+    def set_farm_group(self, group, rank):
+        self._check(lib().lba_set_farm_group(self.h, group.h, rank))
+
+    def set_farm_rccl(self, rccl_id, rank, nranks):
+        self._check(lib().lba_set_farm_rccl(self.h, rccl_id, rank, nranks))
+
+    def farm_plan(self, kf_gid, kf_owner, lm_gid, lm_owner):
+        """Collective: returns (kf published, lm published, kf received, lm received, unmatched)."""
+        kg, kgp = _i64(kf_gid)
+        ko, kop = _i32(kf_owner)
+        lg, lgp = _i64(lm_gid)
+        lo, lop = _i32(lm_owner)
+        out = np.zeros(5, dtype=np.int32)
+        self._check(lib().lba_farm_plan(self.h, kgp, kop, lgp, lop, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return tuple(int(v) for v in out)
+
+    def farm_exchange(self):
+        self._check(lib().lba_farm_exchange(self.h))
 
     def set_state(self, kfs=None, lm=None):
         kfs = None if kfs is None else np.ascontiguousarray(kfs, dtype=KF_DTYPE)

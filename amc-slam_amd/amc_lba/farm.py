@@ -18,15 +18,17 @@ _MAP_CACHE = {}
 
 
 def global_map(config, world, seed, stride):
-    key = (config, world, seed, stride)
+    """config: a CONFIGS name or a make_window keyword dict (its per-window shape)."""
+    ckey = config if isinstance(config, str) else tuple(sorted(config.items()))
+    key = (ckey, world, seed, stride)
     if key not in _MAP_CACHE:
-        kw = dict(CONFIGS[config])
+        kw = dict(CONFIGS[config] if isinstance(config, str) else config)
         n_opt = kw["n_opt_kf"]
         n_total = stride * (world - 1) + n_opt + 1
         kw["n_lm"] = int(round(kw["n_lm"] * n_total / (n_opt + 1)))
         kw["n_opt_kf"] = n_total - 1
         kw["n_fixed"] = 1
-        _MAP_CACHE[key] = make_window(seed=seed, name=f"{config}-map", **kw)
+        _MAP_CACHE[key] = make_window(seed=seed, name=f"{ckey}-map" if isinstance(ckey, str) else "farm-map", **kw)
     return _MAP_CACHE[key]
 
 
@@ -64,8 +66,9 @@ def farm_layout(windows):
 
 def make_farm_windows(config, world, seed=20250912, stride=25):
     g = global_map(config, world, seed, stride)
-    n_opt = CONFIGS[config]["n_opt_kf"]
-    wins = [cut_window(g, r * stride, n_opt, name=f"{config}-w{r}") for r in range(world)]
+    n_opt = (CONFIGS[config] if isinstance(config, str) else config)["n_opt_kf"]
+    tag = config if isinstance(config, str) else "farm"
+    wins = [cut_window(g, r * stride, n_opt, name=f"{tag}-w{r}") for r in range(world)]
     return wins, farm_layout(wins)
 
 
@@ -74,61 +77,79 @@ def make_rank_window(config, rank, world, seed=20250912, stride=25):
     return wins[rank], infos[rank]
 
 
-class SharedExchange:
-    """Window-boundary exchange of shared landmark / keyframe estimates (torch.distributed)."""
+def publish_owners(info):
+    """Owner arrays in the C ABI's convention (include/amc_lba.h, lba_farm_plan): the publishing rank of
+    every shared vertex, -1 for a vertex no other window holds."""
+    kf = np.where(info.kf_shared, info.kf_owner, -1).astype(np.int32)
+    lm = np.where(info.lm_shared, info.lm_owner, -1).astype(np.int32)
+    return kf, lm
 
-    def __init__(self, win, info, rank, world, device=None, group=None):
+
+class DeviceExchange:
+    """Window-boundary exchange through the engine (lba_farm_plan / lba_farm_exchange): pack kernel,
+    all-gather over the problem's collective (RCCL or an in-process group), unpack kernel, all on the
+    problem's HIP stream; the owner -> slot tables are matched once, here."""
+
+    def __init__(self, prob, win, info):
+        self.prob = prob
+        kf_owner, lm_owner = publish_owners(info)
+        self.counts = prob.farm_plan(win.kf_gid, kf_owner, win.lm_gid, lm_owner)
+
+    def exchange(self, prob=None):
+        (prob or self.prob).farm_exchange()
+
+
+class HostExchange:
+    """The same exchange for stand-in problems on the CPU (state() / set_state() over numpy; gloo): the
+    engine's buffer layout (per rank: published keyframes q t v, then landmarks), its matching
+    (lba_farm_match, host-only C), one all_gather, vectorised pack / unpack."""
+
+    KF = 13   # FARM_KF: q (4), t (3), velocity (6)
+
+    def __init__(self, win, info, rank, world, group=None):
+        import amc_lba
         import torch
-        self.torch = torch
-        self.win, self.info, self.rank, self.world = win, info, rank, world
-        self.device = device if device is not None else torch.device("cpu")
-        self.group = group
-        self.lm_send = np.nonzero((info.lm_owner == rank) & info.lm_shared)[0]
-        self.lm_recv = np.nonzero(info.lm_owner != rank)[0]
-        self.kf_send = np.nonzero((info.kf_owner == rank) & info.kf_shared)[0]
-        self.kf_recv = np.nonzero(info.kf_owner != rank)[0]
-        self.lm_gid_to_local = {int(g): i for i, g in enumerate(win.lm_gid)}
-        self.kf_gid_to_local = {int(g): i for i, g in enumerate(win.kf_gid)}
-        self.bytes_per_exchange = 8 * (info.max_lm_owned * 4 + info.max_kf_owned * 14) * world
+        import torch.distributed as dist
+        self.torch, self.dist, self.group = torch, dist, group
+        self.rank, self.world = rank, world
+        kf_owner, lm_owner = publish_owners(info)
+        self.pub_kf = np.nonzero(kf_owner == rank)[0]
+        self.pub_lm = np.nonzero(lm_owner == rank)[0]
+        cnt = self._gather(np.array([self.pub_kf.size, self.pub_lm.size], dtype=np.float64)).reshape(world, 2)
+        self.kcap, self.lcap = int(cnt[:, 0].max()), int(cnt[:, 1].max())
+        ids = np.full(self.kcap + self.lcap, -1.0)
+        ids[: self.pub_kf.size] = win.kf_gid[self.pub_kf]
+        ids[self.kcap: self.kcap + self.pub_lm.size] = win.lm_gid[self.pub_lm]
+        ids = self._gather(ids).reshape(world, -1).astype(np.int64)
+        sk, self.unmatched_kf = amc_lba.farm_match(rank, world, self.kcap, ids[:, : self.kcap], win.kf_gid, kf_owner)
+        sl, self.unmatched_lm = amc_lba.farm_match(rank, world, self.lcap, ids[:, self.kcap:], win.lm_gid, lm_owner)
+        self.stride = self.kcap * self.KF + 3 * self.lcap
+        self.recv_kf = np.nonzero(sk >= 0)[0]
+        o, i = np.divmod(sk[self.recv_kf], max(self.kcap, 1))
+        self.src_kf = o * self.stride + i * self.KF
+        self.recv_lm = np.nonzero(sl >= 0)[0]
+        o, i = np.divmod(sl[self.recv_lm], max(self.lcap, 1))
+        self.src_lm = o * self.stride + self.kcap * self.KF + 3 * i
 
-    def _pack(self, lm, kfs):
-        torch = self.torch
-        L = np.full((self.info.max_lm_owned, 4), -1.0)
-        L[: self.lm_send.size, 0] = self.win.lm_gid[self.lm_send]
-        L[: self.lm_send.size, 1:] = lm[self.lm_send]
-        K = np.full((self.info.max_kf_owned, 14), -1.0)
-        K[: self.kf_send.size, 0] = self.win.kf_gid[self.kf_send]
-        K[: self.kf_send.size, 1:5] = kfs["q"][self.kf_send]
-        K[: self.kf_send.size, 5:8] = kfs["t"][self.kf_send]
-        K[: self.kf_send.size, 8:14] = kfs["vel"][self.kf_send]
-        buf = np.concatenate([L.ravel(), K.ravel()])
-        return torch.from_numpy(buf).to(self.device)
+    def _gather(self, a):
+        t = self.torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64))
+        out = [self.torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t, group=self.group)
+        return self.torch.cat(out).numpy()
 
     def exchange(self, prob):
-        """prob: anything with state() -> (kfs, lm) and set_state(kfs=, lm=) (amc_lba.Problem)."""
-        torch = self.torch
-        import torch.distributed as dist
+        """prob: anything with state() -> (kfs, lm) and set_state(kfs=, lm=)."""
         kfs, lm = prob.state()
-        send = self._pack(lm, kfs)
-        gathered = [torch.empty_like(send) for _ in range(self.world)]
-        dist.all_gather(gathered, send, group=self.group)
-        nL = self.info.max_lm_owned * 4
-        lm_new, kfs_new = lm.copy(), kfs.copy()
-        for r, t in enumerate(gathered):
-            if r == self.rank:
-                continue
-            a = t.cpu().numpy()
-            L = a[:nL].reshape(-1, 4)
-            K = a[nL:].reshape(-1, 14)
-            for row in L[L[:, 0] >= 0]:
-                i = self.lm_gid_to_local.get(int(row[0]))
-                if i is not None and self.info.lm_owner[i] == r:
-                    lm_new[i] = row[1:]
-            for row in K[K[:, 0] >= 0]:
-                i = self.kf_gid_to_local.get(int(row[0]))
-                if i is not None and self.info.kf_owner[i] == r:
-                    kfs_new[i]["q"] = row[1:5]
-                    kfs_new[i]["t"] = row[5:8]
-                    kfs_new[i]["vel"] = row[8:14]
+        mine = np.zeros(self.stride)
+        kst = np.concatenate([kfs["q"], kfs["t"], kfs["vel"]], axis=1)   # the engine's state-record prefix
+        mine[: self.pub_kf.size * self.KF] = kst[self.pub_kf].ravel()
+        mine[self.kcap * self.KF: self.kcap * self.KF + 3 * self.pub_lm.size] = lm[self.pub_lm].ravel()
+        buf = self._gather(mine)
+        kfs_new, lm_new = kfs.copy(), lm.copy()
+        rows = buf[self.src_kf[:, None] + np.arange(self.KF)[None, :]]
+        kfs_new["q"][self.recv_kf] = rows[:, 0:4]
+        kfs_new["t"][self.recv_kf] = rows[:, 4:7]
+        kfs_new["vel"][self.recv_kf] = rows[:, 7:13]
+        lm_new[self.recv_lm] = buf[self.src_lm[:, None] + np.arange(3)[None, :]]
         prob.set_state(kfs=kfs_new, lm=lm_new)
         return lm_new, kfs_new

@@ -286,6 +286,13 @@ void launch_ctl_init(const DevProblem& P, const LMCtl& c, hipStream_t s);
 void launch_lambda_init(const DevProblem& P, double tau, hipStream_t s);
 void launch_depth(const DevProblem& P, int sel, unsigned char* ok, hipStream_t s);
 
+// window farm: a published keyframe is its q (4), t (3) and velocity (6), the prefix of its state record
+constexpr int FARM_KF = 13;
+void launch_farm_pack(const double* kst, const double* lst, const int* pub_kf, int npk, const int* pub_lm, int npl,
+                      int kcap, double* out, hipStream_t s);
+void launch_farm_unpack(double* kst, double* lst, const int* rkf, int nrk, const int* rlm, int nrl, const double* buf,
+                        hipStream_t s);
+
 constexpr int GPS_STRIDE = 156;     // doubles in lba::GPSample (static_assert in lba_kernels.hip)
 
 }  // namespace lba

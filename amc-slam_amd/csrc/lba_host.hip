@@ -83,6 +83,18 @@ struct lba_problem {
     double* d_status = nullptr;       // set-up status word of the partition (part_status)
     bool status_entered = false;      // this set_problem has reached the status all-reduce
     void* group_slot = nullptr;       // owned (rank, group) record of lba_set_partition_group
+    // window farm (lba_set_farm*, lba_farm_plan, lba_farm_exchange): the collective and the exchange plan
+    int farm_rank = 0, farm_n = 0;
+    lba_allreduce_fn farm_fn = nullptr;   // sum all-reduce (the all-gather over zero-padded slots)
+    void* farm_user = nullptr;
+    ncclComm_t farm_comm = nullptr;       // owned, lba_set_farm_rccl: native in-place all-gather
+    void* farm_slot = nullptr;            // owned GroupSlot of lba_set_farm_group
+    bool farm_planned = false;
+    int f_stride = 0, f_kcap = 0, f_npk = 0, f_npl = 0, f_nrk = 0, f_nrl = 0;
+    double* f_buf = nullptr;              // [farm_n][f_stride]: published keyframes (kcap x FARM_KF), landmarks
+    size_t f_buf_bytes = 0;
+    int* f_idx = nullptr;                 // published KFs | published landmarks | (dst, src) KFs | (dst, src) lms
+    size_t f_idx_bytes = 0;
 };
 
 namespace {
@@ -1643,7 +1655,11 @@ void lba_destroy(lba_problem* p) {
     if (p->h_log) (void)hipHostFree(p->h_log);
     if (p->d_status) (void)hipFree(p->d_status);
     if (p->comm) (void)ncclCommDestroy(p->comm);
+    if (p->farm_comm) (void)ncclCommDestroy(p->farm_comm);
+    if (p->f_buf) (void)hipFree(p->f_buf);
+    if (p->f_idx) (void)hipFree(p->f_idx);
     delete static_cast<GroupSlot*>(p->group_slot);
+    delete static_cast<GroupSlot*>(p->farm_slot);
     if (p->stream) (void)hipStreamDestroy(p->stream);
     delete p;
 }
@@ -1847,10 +1863,246 @@ int lba_set_partition_group(lba_problem* p, lba_group* g, int32_t rank) {
     return LBA_OK;
 }
 
+// ---- window farm
+int lba_set_farm(lba_problem* p, int32_t rank, int32_t nranks, lba_allreduce_fn fn, void* user) {
+    if (!p || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !fn)) return LBA_E_ARG;
+    if (p->farm_comm) (void)ncclCommDestroy(p->farm_comm);
+    p->farm_comm = nullptr;
+    delete static_cast<GroupSlot*>(p->farm_slot);
+    p->farm_slot = nullptr;
+    p->farm_rank = rank;
+    p->farm_n = nranks;
+    p->farm_fn = fn;
+    p->farm_user = user;
+    p->farm_planned = false;
+    return LBA_OK;
+}
+
+int lba_set_farm_rccl(lba_problem* p, const void* id, int32_t rank, int32_t nranks) {
+    if (!p || !id || nranks < 1 || rank < 0 || rank >= nranks) return LBA_E_ARG;
+    if (nranks == 1) return lba_set_farm(p, 0, 1, nullptr, nullptr);
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    if (hipSetDevice(p->cfg.device) != hipSuccess) return LBA_E_HIP;
+    ncclComm_t comm = nullptr;
+    if (ncclCommInitRank(&comm, nranks, uid, rank) != ncclSuccess) {
+        p->err = "ncclCommInitRank failed (farm)";
+        return LBA_E_HIP;
+    }
+    const int rc = lba_set_farm(p, rank, nranks, rccl_allreduce, comm);
+    if (rc != LBA_OK) {
+        ncclCommDestroy(comm);
+        return rc;
+    }
+    p->farm_comm = comm;   // the exchange uses ncclAllGather on it directly
+    return LBA_OK;
+}
+
+int lba_set_farm_group(lba_problem* p, lba_group* g, int32_t rank) {
+    if (!p || !g || rank < 0 || rank >= g->n) return LBA_E_ARG;
+    GroupSlot* sl = new GroupSlot{g, rank};
+    const int rc = lba_set_farm(p, rank, g->n, group_allreduce, sl);
+    if (rc != LBA_OK) {
+        delete sl;
+        return rc;
+    }
+    p->farm_slot = sl;
+    return LBA_OK;
+}
+
+int lba_farm_match(int32_t rank, int32_t nranks, int32_t cap, const int64_t* pub_gid, const int64_t* gid,
+                   const int32_t* owner, int32_t n, int32_t* src) {
+    if (nranks < 1 || rank < 0 || rank >= nranks || cap < 0 || n < 0 || (n && (!gid || !owner || !src)) ||
+        (cap && !pub_gid))
+        return LBA_E_ARG;
+    // one hash table per owner rank (its published ids -> position), built once per plan
+    std::vector<std::unordered_map<int64_t, int>> pos(nranks);
+    for (int r = 0; r < nranks; ++r) {
+        if (r == rank) continue;
+        for (int i = 0; i < cap; ++i) {
+            const int64_t g = pub_gid[(size_t)r * cap + i];
+            if (g >= 0) pos[r].emplace(g, i);
+        }
+    }
+    int unmatched = 0;
+    for (int i = 0; i < n; ++i) {
+        src[i] = -1;
+        const int o = owner[i];
+        if (o < -1 || o >= nranks) return LBA_E_ARG;
+        if (o < 0 || o == rank) continue;
+        const auto it = pos[o].find(gid[i]);
+        if (it == pos[o].end()) ++unmatched;
+        else src[i] = o * cap + it->second;
+    }
+    return unmatched;
+}
+
+}  // extern "C"
+
+namespace {
+// all-gather of `stride` doubles per rank in place in buf (rank r's slot at buf + r stride) on the
+// problem's stream: ncclAllGather, or the caller's sum all-reduce over slots that are zero but the own
+void farm_gather(lba_problem* p, double* buf, int64_t stride) {
+    if (p->farm_n <= 1) return;
+    if (p->farm_comm) {
+        if (ncclAllGather(buf + (size_t)p->farm_rank * stride, buf, (size_t)stride, ncclDouble, p->farm_comm,
+                          p->stream) != ncclSuccess)
+            throw ApiError{LBA_E_HIP, "farm all-gather (ncclAllGather) failed"};
+    } else if (p->farm_fn(buf, stride * p->farm_n, (void*)p->stream, p->farm_user) != 0) {
+        throw ApiError{LBA_E_HIP, "farm all-gather (all-reduce) failed"};
+    }
+}
+template <typename T>
+void farm_reserve(T** ptr, size_t* have, size_t bytes) {
+    if (*have >= bytes) return;
+    if (*ptr) HIPCHK(hipFree(*ptr));
+    *ptr = nullptr;
+    *have = 0;
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(ptr), bytes));
+    *have = bytes;
+}
+}  // namespace
+
+extern "C" {
+
+int lba_farm_plan(lba_problem* p, const int64_t* kf_gid, const int32_t* kf_owner, const int64_t* lm_gid,
+                  const int32_t* lm_owner, int32_t* out_counts) {
+    if (!p || !p->has_problem || p->farm_n < 1 || (p->n_kf && (!kf_gid || !kf_owner)) ||
+        (p->n_lm && (!lm_gid || !lm_owner)))
+        return LBA_E_ARG;
+    try {
+        HIPCHK(hipSetDevice(p->cfg.device));
+        const int R = p->farm_n, me = p->farm_rank;
+        std::vector<int> pub_kf, pub_lm;
+        for (int k = 0; k < p->n_kf; ++k) {
+            if (kf_owner[k] < -1 || kf_owner[k] >= R) throw ApiError{LBA_E_ARG, "farm plan: keyframe owner out of range"};
+            if (kf_owner[k] == me) pub_kf.push_back(k);
+        }
+        for (int l = 0; l < p->n_lm; ++l) {
+            if (lm_owner[l] < -1 || lm_owner[l] >= R) throw ApiError{LBA_E_ARG, "farm plan: landmark owner out of range"};
+            if (lm_owner[l] == me && p->lm_dev[l] >= 0) pub_lm.push_back(l);   // (inactive: not on the device)
+        }
+        // 1. the ranks' published counts -> slot capacities
+        double* tmp = nullptr;
+        size_t tmp_bytes = 0;
+        struct Tmp {
+            double*& t;
+            ~Tmp() { if (t) (void)hipFree(t); }
+        } guard{tmp};
+        std::vector<double> h(2 * (size_t)R, 0.0);
+        h[2 * me] = (double)pub_kf.size();
+        h[2 * me + 1] = (double)pub_lm.size();
+        farm_reserve(&tmp, &tmp_bytes, h.size() * sizeof(double));
+        HIPCHK(hipMemcpy(tmp, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+        farm_gather(p, tmp, 2);
+        HIPCHK(hipStreamSynchronize(p->stream));
+        HIPCHK(hipMemcpy(h.data(), tmp, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+        int kcap = 0, lcap = 0;
+        for (int r = 0; r < R; ++r) {
+            kcap = std::max(kcap, (int)h[2 * r]);
+            lcap = std::max(lcap, (int)h[2 * r + 1]);
+        }
+        // 2. the published global ids (-1 padded), exchanged once; ids travel as doubles (exact below 2^53)
+        const int gs = kcap + lcap;
+        std::vector<double> g((size_t)R * gs, 0.0);
+        for (int i = 0; i < kcap; ++i) g[(size_t)me * gs + i] = i < (int)pub_kf.size() ? (double)kf_gid[pub_kf[i]] : -1.0;
+        for (int i = 0; i < lcap; ++i)
+            g[(size_t)me * gs + kcap + i] = i < (int)pub_lm.size() ? (double)lm_gid[pub_lm[i]] : -1.0;
+        farm_reserve(&tmp, &tmp_bytes, std::max<size_t>(g.size(), 1) * sizeof(double));
+        HIPCHK(hipMemcpy(tmp, g.data(), g.size() * sizeof(double), hipMemcpyHostToDevice));
+        farm_gather(p, tmp, gs);
+        HIPCHK(hipStreamSynchronize(p->stream));
+        HIPCHK(hipMemcpy(g.data(), tmp, g.size() * sizeof(double), hipMemcpyDeviceToHost));
+        std::vector<int64_t> gk((size_t)R * kcap), gl((size_t)R * lcap);
+        for (int r = 0; r < R; ++r) {
+            for (int i = 0; i < kcap; ++i) gk[(size_t)r * kcap + i] = (int64_t)g[(size_t)r * gs + i];
+            for (int i = 0; i < lcap; ++i) gl[(size_t)r * lcap + i] = (int64_t)g[(size_t)r * gs + kcap + i];
+        }
+        // 3. every received vertex's source offset in the exchange buffer
+        const int stride = kcap * FARM_KF + 3 * lcap;
+        std::vector<int> sk(p->n_kf), sl(p->n_lm);
+        const int uk = p->n_kf ? lba_farm_match(me, R, kcap, gk.data(), kf_gid, kf_owner, p->n_kf, sk.data()) : 0;
+        const int ul = p->n_lm ? lba_farm_match(me, R, lcap, gl.data(), lm_gid, lm_owner, p->n_lm, sl.data()) : 0;
+        if (uk < 0 || ul < 0) throw ApiError{LBA_E_ARG, "farm plan: matching failed"};
+        const int unmatched = uk + ul;
+        std::vector<int> idx;
+        for (int k : pub_kf) idx.push_back(k);
+        for (int l : pub_lm) idx.push_back(p->lm_dev[l]);
+        int nrk = 0, nrl = 0;
+        for (int k = 0; k < p->n_kf; ++k)
+            if (sk[k] >= 0) {
+                const int o = sk[k] / std::max(kcap, 1), i = sk[k] - o * kcap;
+                idx.push_back(k);
+                idx.push_back(o * stride + i * FARM_KF);
+                ++nrk;
+            }
+        for (int l = 0; l < p->n_lm; ++l)
+            if (sl[l] >= 0) {
+                if (p->lm_dev[l] < 0) continue;   // inactive here: nothing on the device to overwrite
+                const int o = sl[l] / std::max(lcap, 1), i = sl[l] - o * lcap;
+                idx.push_back(p->lm_dev[l]);
+                idx.push_back(o * stride + kcap * FARM_KF + 3 * i);
+                ++nrl;
+            }
+        farm_reserve(&p->f_buf, &p->f_buf_bytes, std::max<size_t>((size_t)R * stride, 1) * sizeof(double));
+        farm_reserve(&p->f_idx, &p->f_idx_bytes, std::max<size_t>(idx.size(), 1) * sizeof(int));
+        if (!idx.empty()) HIPCHK(hipMemcpy(p->f_idx, idx.data(), idx.size() * sizeof(int), hipMemcpyHostToDevice));
+        p->f_stride = stride;
+        p->f_kcap = kcap;
+        p->f_npk = (int)pub_kf.size();
+        p->f_npl = (int)pub_lm.size();
+        p->f_nrk = nrk;
+        p->f_nrl = nrl;
+        p->farm_planned = true;
+        if (out_counts) {
+            out_counts[0] = p->f_npk; out_counts[1] = p->f_npl;
+            out_counts[2] = nrk; out_counts[3] = nrl; out_counts[4] = unmatched;
+        }
+        return LBA_OK;
+    } catch (const ApiError& e) {
+        p->err = e.msg;
+        return e.code;
+    } catch (const HipError& e) {
+        return map_error(p, e);
+    }
+}
+
+int lba_farm_exchange(lba_problem* p) {
+    if (!p || !p->has_problem) return LBA_E_ARG;
+    if (!p->farm_planned) {
+        p->err = "lba_farm_exchange: no plan for this window (lba_farm_plan after lba_set_problem)";
+        return LBA_E_ARG;
+    }
+    try {
+        HIPCHK(hipSetDevice(p->cfg.device));
+        const size_t S = (size_t)p->f_stride;
+        double* mine = p->f_buf + (size_t)p->farm_rank * S;
+        if (!p->farm_comm && p->farm_n > 1)   // the sum all-gather needs every other slot zero
+            HIPCHK(hipMemsetAsync(p->f_buf, 0, (size_t)p->farm_n * S * sizeof(double), p->stream));
+        const int* ik = p->f_idx;
+        const int* il = ik + p->f_npk;
+        const int* rk = il + p->f_npl;
+        const int* rl = rk + 2 * p->f_nrk;
+        launch_farm_pack(p->kst[p->cur], p->lst[p->cur], ik, p->f_npk, il, p->f_npl, p->f_kcap, mine, p->stream);
+        farm_gather(p, p->f_buf, (int64_t)S);
+        launch_farm_unpack(p->kst[p->cur], p->lst[p->cur], rk, p->f_nrk, rl, p->f_nrl, p->f_buf, p->stream);
+        HIPCHK(hipGetLastError());
+        p->gps_fresh[p->cur] = false;   // new keyframe poses need new pose samples
+        p->linearized = false;
+        return LBA_OK;
+    } catch (const ApiError& e) {
+        p->err = e.msg;
+        return e.code;
+    } catch (const HipError& e) {
+        return map_error(p, e);
+    }
+}
+
 int lba_set_problem(lba_problem* p, const lba_kf* kfs, int32_t n_kf, const double* lm_xyz, int32_t n_lm,
                     const lba_obs* obs, int32_t n_obs, const lba_prior* priors, int32_t n_priors,
                     const int32_t* vel_kfs, int32_t n_vel, const lba_cam* cams, int32_t n_cam) {
     if (!p) return LBA_E_ARG;
+    p->farm_planned = false;   // the plan holds device indices of the previous window
     try {
         HIPCHK(hipSetDevice(p->cfg.device));
         return set_problem(p, kfs, n_kf, lm_xyz, n_lm, obs, n_obs, priors, n_priors, vel_kfs, n_vel, cams, n_cam);

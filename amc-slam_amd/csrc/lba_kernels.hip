@@ -20,6 +20,7 @@
 //   k_eval           residuals / robust chi2 of the trial state           (sparse_optimizer.cpp:61-114)
 // All cross-workgroup sums are written as per-workgroup partials and reduced in a fixed order, so
 // results are bitwise reproducible run to run (no floating-point atomics).
+#include <algorithm>
 #include <cfloat>
 #include <utility>
 
@@ -2502,6 +2503,53 @@ void launch_lambda_init(const DevProblem& P, double tau, hipStream_t s) {
 }
 void launch_depth(const DevProblem& P, int sel, unsigned char* ok, hipStream_t s) {
     if (P.n_obs) hipLaunchKernelGGL(k_depth, dim3(cdiv(P.n_obs, 256)), dim3(256), 0, s, P, sel, ok);
+}
+
+// ---- window farm (lba_farm_exchange): device-resident pack / unpack of the shared vertex estimates.
+// Pack: this rank's published keyframes (q t v: FARM_KF doubles each) and landmarks (3 each) from the
+// current state buffer into its slot of the exchange buffer; unpack: every vertex another rank owns,
+// from that rank's slot (src: offset in the buffer), a bit-exact copy of the owner's estimate.
+__global__ __launch_bounds__(256) void k_farm_pack(const double* __restrict__ kst, const double* __restrict__ lst,
+                                                   const int* __restrict__ pub_kf, int npk,
+                                                   const int* __restrict__ pub_lm, int npl, int kcap,
+                                                   double* __restrict__ out) {
+    const int nk = npk * FARM_KF, n = nk + 3 * npl;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+        if (e < nk) {
+            const int i = e / FARM_KF, c = e - FARM_KF * i;
+            out[e] = kst[(size_t)pub_kf[i] * KF_STRIDE + c];
+        } else {
+            const int j = (e - nk) / 3, c = (e - nk) - 3 * j;
+            out[(size_t)kcap * FARM_KF + 3 * j + c] = lst[(size_t)pub_lm[j] * 3 + c];
+        }
+    }
+}
+__global__ __launch_bounds__(256) void k_farm_unpack(double* __restrict__ kst, double* __restrict__ lst,
+                                                     const int* __restrict__ rkf, int nrk,
+                                                     const int* __restrict__ rlm, int nrl,
+                                                     const double* __restrict__ buf) {
+    const int nk = nrk * FARM_KF, n = nk + 3 * nrl;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+        if (e < nk) {   // rkf: (destination KF, source offset) pairs
+            const int i = e / FARM_KF, c = e - FARM_KF * i;
+            kst[(size_t)rkf[2 * i] * KF_STRIDE + c] = buf[(size_t)rkf[2 * i + 1] + c];
+        } else {
+            const int j = (e - nk) / 3, c = (e - nk) - 3 * j;
+            lst[(size_t)rlm[2 * j] * 3 + c] = buf[(size_t)rlm[2 * j + 1] + c];
+        }
+    }
+}
+void launch_farm_pack(const double* kst, const double* lst, const int* pub_kf, int npk, const int* pub_lm, int npl,
+                      int kcap, double* out, hipStream_t s) {
+    const int n = npk * FARM_KF + 3 * npl;
+    if (n) hipLaunchKernelGGL(k_farm_pack, dim3(std::min(cdiv(n, 256), 1024)), dim3(256), 0, s, kst, lst, pub_kf, npk,
+                              pub_lm, npl, kcap, out);
+}
+void launch_farm_unpack(double* kst, double* lst, const int* rkf, int nrk, const int* rlm, int nrl, const double* buf,
+                        hipStream_t s) {
+    const int n = nrk * FARM_KF + 3 * nrl;
+    if (n) hipLaunchKernelGGL(k_farm_unpack, dim3(std::min(cdiv(n, 256), 1024)), dim3(256), 0, s, kst, lst, rkf, nrk,
+                              rlm, nrl, buf);
 }
 
 }  // namespace lba

@@ -177,10 +177,18 @@ def main():
     else:
         if world > 1:
             win, shared = farm.make_rank_window(args.config, rank, world, seed=args.seed)
-            ex = farm.SharedExchange(win, shared, rank, world, device=torch.device("cuda", local))
         else:
             win = make_config_window(args.config, seed=args.seed)
         prob = amc_lba.Problem(win, device=local, early_stop=0, flags=flags)
+        if world > 1:
+            # window-boundary exchange inside the engine: its own RCCL communicator (in-place
+            # ncclAllGather on the window's stream), owner -> slot tables matched once here
+            idt = torch.zeros(128, dtype=torch.uint8, device=torch.device("cuda", local))
+            if rank == 0:
+                idt.copy_(torch.frombuffer(bytearray(amc_lba.rccl_unique_id()), dtype=torch.uint8))
+            dist.broadcast(idt, 0)
+            prob.set_farm_rccl(bytes(idt.cpu().numpy().tobytes()), rank, world)
+            ex = farm.DeviceExchange(prob, win, shared)
     t_setup = time.perf_counter() - t_setup
     setup_done.set()
 
@@ -203,7 +211,7 @@ def main():
         n_s += st.n_k_solve
         trials += st.trials
         if ex is not None:
-            ex.exchange(prob)           # window boundary: publish owned shared landmarks
+            ex.exchange()               # window boundary: publish owned shared keyframes / landmarks
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

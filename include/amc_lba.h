@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define LBA_ABI_VERSION 3
+#define LBA_ABI_VERSION 4
 
 /* status codes */
 #define LBA_OK              0
@@ -193,6 +193,36 @@ typedef struct lba_group lba_group;     /* in-process all-reduce across problems
 int  lba_group_create(lba_group** out, int32_t nranks);
 void lba_group_destroy(lba_group* g);
 int  lba_set_partition_group(lba_problem* p, lba_group* g, int32_t rank);
+
+/* ---- window farm (BASELINE config 3): one LocalGPBA window per GPU (rank), windows cut
+ * from one trajectory, so neighbours share keyframes and map points.  The reference runs one local BA at
+ * a time (LocalMapping::Run -> Optimizer::LocalGPBA, src/LocalMapping.cc:131) and every window reads and
+ * writes the shared map (src/Optimizer.cc:1380-1432); here the shared estimates are exchanged at window
+ * boundaries instead, device to device:
+ *   lba_set_farm*      the collective: RCCL over xGMI (lba_set_farm_rccl: ncclAllGather on the problem's
+ *                      stream), an in-process group on one device (lba_set_farm_group, for tests), or any
+ *                      sum all-reduce of the caller's (an all-gather as a sum over zero-padded slots);
+ *   lba_farm_plan      after lba_set_problem, collective: which vertices this rank publishes (owner ==
+ *                      rank) and, for every vertex another rank owns, where its estimate lands in the
+ *                      exchange buffer (matched by global id once; no lookups at exchange time);
+ *   lba_farm_exchange  collective, per window boundary: pack kernel -> all-gather -> unpack kernel on the
+ *                      problem's stream; the received estimates are bit-exact copies of the owners'.
+ * kf_owner / lm_owner: per vertex of this window, the rank that publishes it, or -1 for a vertex no other
+ * window shares.  Keyframe time stamps and fixed flags are not exchanged (they are the same everywhere).
+ * A vertex whose owner does not publish it (no such global id on that rank) keeps its own estimate; the
+ * counts of published, received and unmatched vertices come back in out_counts[5] (may be NULL):
+ * kf published, lm published, kf received, lm received, unmatched.  lba_set_problem drops the plan. */
+int lba_set_farm(lba_problem* p, int32_t rank, int32_t nranks, lba_allreduce_fn fn, void* user);
+int lba_set_farm_rccl(lba_problem* p, const void* id, int32_t rank, int32_t nranks);
+int lba_set_farm_group(lba_problem* p, lba_group* g, int32_t rank);
+int lba_farm_plan(lba_problem* p, const int64_t* kf_gid, const int32_t* kf_owner,
+                  const int64_t* lm_gid, const int32_t* lm_owner, int32_t* out_counts);
+int lba_farm_exchange(lba_problem* p);
+/* Host-only form of the plan's matching (no device, no collective; tests): given every rank's published
+ * global ids (pub_gid: nranks x cap, -1 padded) and this window's ids / owners, the source slot of every
+ * received vertex: src[i] = owner * cap + position, or -1 (not a received vertex, or unmatched). */
+int lba_farm_match(int32_t rank, int32_t nranks, int32_t cap, const int64_t* pub_gid,
+                   const int64_t* gid, const int32_t* owner, int32_t n, int32_t* src);
 
 /* Levenberg-Marquardt (OptimizationAlgorithmLevenberg::solve x iters).  stop_flag is polled
  * between iterations and trials like SparseOptimizer::terminate().  Returns iterations run

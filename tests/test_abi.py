@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(L, n), n
         assert re.search(rf"\bT {n}\b", exported), n
     assert set(amc_lba.exported_symbols()) <= set(declared_functions())
-    assert L.lba_abi_version() == 3
+    assert L.lba_abi_version() == 4
 
 
 def _c_sizeof(struct):

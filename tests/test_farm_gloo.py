@@ -44,7 +44,7 @@ def _worker(rank, world, port, q):
     wins, infos = farm.make_farm_windows("cfg1_local_50kf", world, seed=3, stride=25)
     win, info = wins[rank], infos[rank]
     prob = _FakeProblem(win, rank)
-    ex = farm.SharedExchange(win, info, rank, world)
+    ex = farm.HostExchange(win, info, rank, world)
     before_lm, before_kf = prob.lm.copy(), prob.kfs["t"].copy()
     ex.exchange(prob)
     q.put((rank, win.lm_gid, win.kf_gid, info.lm_owner, info.kf_owner, before_lm, before_kf, prob.lm, prob.kfs["t"]))
