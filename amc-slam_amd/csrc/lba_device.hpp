@@ -86,6 +86,8 @@ struct DevProblem {
     int n_kf, n_lm, n_obs, n_gp, n_pairs, n_tiles, n_pb, np, n_prior, n_vel, n_cam;
     int npad;               // np rounded up to CHOL_NB: leading dimension of S / Lm (identity tail)
     int n_entries, n_sentries, n_ublocks;
+    // slab and table extents (LBA_DEBUG_BOUNDS builds check every indexed write against them)
+    int n_mslots, n_hslots, n_gslots, n_sslots, n_gpslots, n_chi, n_pairs_all, n_lm_all;
     // observations (device order)
     const int* ob_meta;
     const int* ob_kfa;

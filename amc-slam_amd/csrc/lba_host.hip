@@ -989,6 +989,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.gslab = dalloc<double>(p, (size_t)12 * std::max(n_gslots, 1));
     D.sslab = dalloc<double>(p, (size_t)144 * std::max(n_sslots, 1));
     D.gpslab = dalloc<double>(p, (size_t)12 * std::max(n_gpslots, 1));
+    D.n_mslots = n_mslots; D.n_hslots = n_hslots; D.n_gslots = n_gslots; D.n_sslots = n_sslots; D.n_gpslots = n_gpslots;
     const int npad = (p->np + CHOL_NB - 1) / CHOL_NB * CHOL_NB;
     mark("upload");
     // ---- dense solve layout.  Envelope of S at panel granularity (per CHOL_NB panel of rows, the
@@ -1232,6 +1233,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.LinvT = dalloc<double>(p, (size_t)npad * CHOL_NB + 1);
     D.Hpl = dalloc<double>(p, (size_t)36 * std::max(n_pairs + n_segpairs, 1));   // canonical pairs, then segment pairs
     D.Hll = dalloc<double>(p, (size_t)9 * std::max(nl + n_seg, 1));               // landmarks, then segments
+    D.n_pairs_all = n_pairs + n_segpairs;
+    D.n_lm_all = nl + n_seg;
     D.bl = dalloc<double>(p, (size_t)3 * std::max(nl + n_seg, 1));
     D.Dinv = dalloc<double>(p, (size_t)9 * std::max(nl, 1));
     D.S = dalloc<double>(p, (size_t)npad * npad + 1);
@@ -1249,6 +1252,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     HIPCHK(hipMemset(D.x, 0, sizeof(double) * (p->np + 3 * (size_t)nl + 1)));   // BlockSolver::_x before any solve
     const int nchi = n_tiles + D.n_prior + D.n_vel + D.n_eprior;
     D.chi_lin = dalloc<double>(p, nchi + 1);
+    D.n_chi = nchi;
     D.chi_eval = dalloc<double>(p, nchi + 1);
     // k_update: one workgroup per GP pair, then KFs and landmarks at 64 per workgroup
     D.n_upd_blocks = D.n_gp + (n_kfs + 63) / 64 + (nl + 63) / 64;

@@ -46,6 +46,22 @@ static_assert(CAMD_STRIDE == CAMREC_DOUBLES, "camera record layout drifted");
     } while (0)
 #define LBA_TMARK(buf, k) LBA_TMARKI(buf, blockIdx.x, k)
 
+// LBA_DEBUG_BOUNDS builds (scripts/exp_build.sh dbg -DLBA_DEBUG_BOUNDS, loaded with AMC_LBA_LIB): every
+// indexed slab / table write of the sweep, the edge items and the expansion is checked against the
+// extent set-up allocated; an out-of-range index is printed and its write skipped (no trap: a fault can
+// take the whole node down), and the launch's factorisation status gets LBA_DBG_INFO so the run fails.
+// Release builds compile the checks away.
+#ifdef LBA_DEBUG_BOUNDS
+constexpr int LBA_DBG_INFO = 0x7ffe0000;
+#define LBA_INB(P, i, n, what)                                                                            \
+    ((unsigned)(i) < (unsigned)(n) ? true                                                                 \
+                                   : (printf("lba bounds: %s index %d of %d (block %d thread %d)\n", what, \
+                                             (int)(i), (int)(n), (int)blockIdx.x, (int)threadIdx.x),      \
+                                      (P).info ? (void)atomicExch((P).info, LBA_DBG_INFO) : (void)0, false))
+#else
+#define LBA_INB(P, i, n, what) true
+#endif
+
 typedef double d4 __attribute__((ext_vector_type(4)));   // v_mfma_f64_16x16x4 accumulator
 
 // queued optimisation (LMCtl): the state buffer a launch works on, whether it runs, its damping
@@ -341,6 +357,7 @@ __device__ __forceinline__ void smp_task(const DevProblem& P, const double* rows
             acc[q] += (sw * x) * y;
         }
     }
+    if (!LBA_INB(P, mslot, P.n_mslots, "mslab")) return;
     double* m = P.mslab + (size_t)mslot * SM_STRIDE + 9 * CH;
 #pragma unroll
     for (int q = 0; q < 9; ++q) m[q] = acc[q];
@@ -446,6 +463,7 @@ __device__ void edge_item(const DevProblem& P, int sel, int idx, const int tid, 
     double *Ji = shm, *Jj = Ji + 144, *WJi = Jj + 144, *WJj = WJi + 144, *Om = WJj + 144, *e = Om + 144,
            *We = e + 12, *wshp = We + 12;
     double& wsh = *wshp;
+    if (!LBA_INB(P, idx, P.n_prior + P.n_vel + P.n_eprior, "edge item")) return;   // (uniform per workgroup)
     const int si = state_idx(P, sel);
     const double* __restrict__ kst = P.kbuf[si];
     const int ent = P.pri_entry0 + idx;
@@ -466,9 +484,12 @@ __device__ void edge_item(const DevProblem& P, int sel, int idx, const int tid, 
                 We[i] = s;
                 chi += e[i] * s;
             }
-            P.chi_lin[P.n_tiles + idx] = chi;
+            if (LBA_INB(P, P.n_tiles + idx, P.n_chi, "chi_lin")) P.chi_lin[P.n_tiles + idx] = chi;
         }
         __syncthreads();
+        if (!LBA_INB(P, sl[2], P.n_hslots, "hslab (extrinsic prior)") ||
+            !LBA_INB(P, gl[1], P.n_gslots, "gslab (extrinsic prior)"))
+            return;
         double* H = P.hslab + (size_t)sl[2] * 144;
         for (int t = tid; t < 144; t += NT) {
             const int i = t / 12 - 3, j = t % 12 - 3;
@@ -500,7 +521,7 @@ __device__ void edge_item(const DevProblem& P, int sel, int idx, const int tid, 
             }
             double r0 = chi, r1 = 1.0;
             if (P.huber_prior > 0) huber(chi, P.huber_prior, &r0, &r1);
-            P.chi_lin[P.n_tiles + idx] = r0;
+            if (LBA_INB(P, P.n_tiles + idx, P.n_chi, "chi_lin")) P.chi_lin[P.n_tiles + idx] = r0;
             wsh = r1;
         }
         __syncthreads();
@@ -523,7 +544,7 @@ __device__ void edge_item(const DevProblem& P, int sel, int idx, const int tid, 
             if (t < 432) {
                 const int bk = t / 144, ij = t % 144, i = ij / 12, j = ij % 12;
                 const int slot = sl[bk == 0 ? 0 : (bk == 1 ? 1 : 2)];
-                if (slot < 0) continue;
+                if (slot < 0 || !LBA_INB(P, slot, P.n_hslots, "hslab (prior)")) continue;
                 const double* A = (bk == 2) ? Jj : Ji;
                 const double* B = (bk == 0) ? WJi : WJj;
                 double s = 0.0;
@@ -533,7 +554,7 @@ __device__ void edge_item(const DevProblem& P, int sel, int idx, const int tid, 
                 else H[i * 12 + j] = s;
             } else {
                 const int side = (t - 432) / 12, i = (t - 432) % 12;
-                if (gl[side] < 0) continue;
+                if (gl[side] < 0 || !LBA_INB(P, gl[side], P.n_gslots, "gslab (prior)")) continue;
                 const double* A = side ? Jj : Ji;
                 double s = 0.0;
                 for (int k = 0; k < 12; ++k) s += A[k * 12 + i] * We[k];
@@ -545,6 +566,9 @@ __device__ void edge_item(const DevProblem& P, int sel, int idx, const int tid, 
         const int v = idx - P.n_prior;
         const double ev = kst[(size_t)P.vel_kf[v] * KF_STRIDE + 7 + 2];
         const double q22 = P.qcinv[2 * 6 + 2];
+        if (!LBA_INB(P, sl[2], P.n_hslots, "hslab (velocity)") || !LBA_INB(P, gl[1], P.n_gslots, "gslab (velocity)") ||
+            !LBA_INB(P, P.n_tiles + idx, P.n_chi, "chi_lin"))
+            return;
         double* H = P.hslab + (size_t)sl[2] * 144;
         for (int t = tid; t < 144; t += NT) H[t] = (t == 8 * 12 + 8) ? q22 : 0.0;
         if (tid < 12) P.gslab[(size_t)gl[1] * 12 + tid] = (tid == 8) ? -q22 * ev : 0.0;
@@ -720,8 +744,10 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
                     b[a] -= sa * e;
                 }
             }
-            for (int q = 0; q < 9; ++q) P.Hll[(size_t)l * 9 + q] = H[q];
-            for (int q = 0; q < 3; ++q) P.bl[(size_t)l * 3 + q] = b[q];
+            if (LBA_INB(P, l, P.n_lm_all, "Hll / bl")) {
+                for (int q = 0; q < 9; ++q) P.Hll[(size_t)l * 9 + q] = H[q];
+                for (int q = 0; q < 3; ++q) P.bl[(size_t)l * 3 + q] = b[q];
+            }
             if (elim) {
                 const double lambda = damping(P, lambda_arg);
                 H[0] += lambda; H[4] += lambda; H[8] += lambda;   // setLambda on Hll (block_solver.hpp:580-587)
@@ -788,9 +814,11 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
                                        n[4] * g[12 + a] + n[5] * g[15 + a];
             }
         }
-        double* Hg = P.Hpl + (size_t)(pair0 + pl) * 36 + 18 * half;
+        if (LBA_INB(P, pair0 + pl, P.n_pairs_all, "Hpl")) {
+            double* Hg = P.Hpl + (size_t)(pair0 + pl) * 36 + 18 * half;
 #pragma unroll
-        for (int q = 0; q < 18; ++q) Hg[q] = hacc[q];
+            for (int q = 0; q < 18; ++q) Hg[q] = hacc[q];
+        }
     }
     LBA_TMARK(P.tdbg_lin, 4);
 
@@ -846,6 +874,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
                 for (int j = 0; j < 6; ++j)
                     acc[i * 6 + j] += a[i * 3] * b[j * 3] + a[i * 3 + 1] * b[j * 3 + 1] + a[i * 3 + 2] * b[j * 3 + 2];
         }
+        if (!LBA_INB(P, sslt[q], P.n_sslots, "sslab")) continue;
         double* o = P.sslab + (size_t)sslt[q] * 144 + (3 * rg) * 12 + 6 * ch;
 #pragma unroll
         for (int i = 0; i < 3; ++i)
@@ -875,7 +904,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
                 const double* u0 = Dl + m * DL_STRIDE + 8;
                 v0 += w0[0] * u0[0] + w0[1] * u0[1] + w0[2] * u0[2];
             }
-            P.gpslab[(size_t)P.tkf_gslot[kf0 + l] * 12 + r] = v0 + v1;
+            if (LBA_INB(P, P.tkf_gslot[kf0 + l], P.n_gpslots, "gpslab")) P.gpslab[(size_t)P.tkf_gslot[kf0 + l] * 12 + r] = v0 + v1;
         }
     }
     LBA_TMARKI(P.tdbg_schur, tile, 3);
