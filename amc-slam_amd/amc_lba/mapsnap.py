@@ -336,6 +336,12 @@ class LbamapResult(ctypes.Structure):
         ("chi2_initial", ctypes.c_double), ("chi2_final", ctypes.c_double)]
 
 
+class LbamapBAResult(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("status", "n_kf", "n_fixed_kf", "n_mp", "n_priors", "n_vel")] + [
+        ("n_edges", ctypes.c_int32 * 5), ("iterations", ctypes.c_int32),
+        ("chi2_initial", ctypes.c_double), ("chi2_final", ctypes.c_double)]
+
+
 def map_lib():
     global _lib
     if _lib is None:
@@ -358,13 +364,19 @@ def map_lib():
                                         ctypes.POINTER(LbamapResult)]
         L.lbamap_build_window.argtypes = [vp, ctypes.c_int64, ctypes.POINTER(LbamapOptions),
                                           ctypes.POINTER(ctypes.c_int32)] + [vp] * 9 + [ctypes.POINTER(LbaConfig)]
+        L.lbamap_global_ba.argtypes = [vp, ctypes.c_int32, vp, ctypes.c_uint64, ctypes.POINTER(LbamapOptions),
+                                       ctypes.POINTER(LbamapBAResult)]
+        L.lbamap_kf_gba.argtypes = [vp, ctypes.c_int64, vp, vp, vp, ctypes.POINTER(ctypes.c_uint64)]
+        L.lbamap_mp_gba.argtypes = [vp, ctypes.c_int64, vp, ctypes.POINTER(ctypes.c_uint64)]
+        L.lbamap_build_ba_window.argtypes = [vp, ctypes.POINTER(ctypes.c_int32)] + [vp] * 9 + [ctypes.POINTER(LbaConfig)]
         _lib = L
     return _lib
 
 
 def exported_symbols():
     return ["lbamap_load", "lbamap_free", "lbamap_last_error", "lbamap_snapshot_size", "lbamap_save",
-            "lbamap_local_gpba", "lbamap_build_window"]
+            "lbamap_local_gpba", "lbamap_build_window", "lbamap_global_ba", "lbamap_kf_gba", "lbamap_mp_gba",
+            "lbamap_build_ba_window"]
 
 
 class LocalGPBAMap:
@@ -403,6 +415,61 @@ class LocalGPBAMap:
         res = LbamapResult()
         rc = map_lib().lbamap_local_gpba(self.h, kf_id, None, ctypes.byref(opt), ctypes.byref(res))
         return rc, res
+
+    def global_ba(self, iterations=10, loop_kf=0, device=0, flags=0, stop_flag=None):
+        """GlobalBundleAdjustemnt(map, iterations, stop, loop_kf) on the GPU; returns (rc, LbamapBAResult)."""
+        opt = LbamapOptions(0, 0, device, flags)
+        res = LbamapBAResult()
+        sf = None if stop_flag is None else ctypes.byref(stop_flag)
+        rc = map_lib().lbamap_global_ba(self.h, iterations, sf, loop_kf, ctypes.byref(opt), ctypes.byref(res))
+        return rc, res
+
+    def kf_gba(self, kf_id):
+        q, t, v = np.zeros(4, np.float32), np.zeros(3, np.float32), np.zeros(6, np.float32)
+        lk = ctypes.c_uint64()
+        rc = map_lib().lbamap_kf_gba(self.h, kf_id, ptr(q), ptr(t), ptr(v), ctypes.byref(lk))
+        if rc != 0:
+            raise RuntimeError("lbamap_kf_gba failed")
+        return q, t, v, lk.value
+
+    def mp_gba(self, mp_id):
+        p = np.zeros(3, np.float32)
+        lk = ctypes.c_uint64()
+        rc = map_lib().lbamap_mp_gba(self.h, mp_id, ptr(p), ctypes.byref(lk))
+        if rc != 0:
+            raise RuntimeError("lbamap_mp_gba failed")
+        return p, lk.value
+
+    def build_ba_window(self):
+        """The flat global-BA graph BundleAdjustment would optimise (no GPU needed).  Returns (Window,
+        kf_ids, mp_ids, obs_tag)."""
+        L = map_lib()
+        cnt = (ctypes.c_int32 * 6)()
+        rc = L.lbamap_build_ba_window(self.h, cnt, *([None] * 9), None)
+        if rc != 0:
+            raise RuntimeError(self.error())
+        return self._flat(cnt, lambda *a: L.lbamap_build_ba_window(self.h, cnt, *a), "global_ba")
+
+    def _flat(self, cnt, fill, name):
+        n_kf, n_lm, n_obs, n_pri, n_vel, n_cam = list(cnt)
+        kfs = np.zeros(n_kf, KF_DTYPE)
+        lm = np.zeros((n_lm, 3))
+        obs = np.zeros(n_obs, OBS_DTYPE)
+        pri = np.zeros(n_pri, PRIOR_DTYPE)
+        vel = np.zeros(n_vel, np.int32)
+        cams = np.zeros(n_cam, CAM_DTYPE)
+        kf_ids = np.zeros(n_kf, np.int64)
+        mp_ids = np.zeros(n_lm, np.int64)
+        tag = np.zeros(n_obs, np.int32)
+        cfg = LbaConfig()
+        rc = fill(ptr(kfs), ptr(lm), ptr(obs), ptr(pri), ptr(vel), ptr(cams), ptr(kf_ids), ptr(mp_ids), ptr(tag),
+                  ctypes.byref(cfg))
+        if rc != 0:
+            raise RuntimeError(self.error())
+        wcfg = {"huber_mono": cfg.huber_mono, "huber_stereo": cfg.huber_stereo, "huber_prior": cfg.huber_prior,
+                "lambda_init": cfg.lambda_init, "qc_diag": np.array(cfg.qc[:]).reshape(6, 6)}
+        win = Window(kfs=kfs, lm=lm, obs=obs, priors=pri, vel_kfs=vel, cams=cams, cfg=wcfg, name=name)
+        return win, kf_ids, mp_ids, tag
 
     def build_window(self, kf_id, large=False):
         """The flat window LocalGPBA would optimise (no GPU needed).  Returns (Window, kf_ids,

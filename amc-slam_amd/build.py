@@ -23,12 +23,12 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall"]
 HOST = os.path.join(HERE, "host")
 MAP_LIB = os.path.join(HERE, "lib", "libamc_lba_map.so")
-MAP_SOURCES = ["lba_map.cpp", "optimizer.cpp", "capi.cpp"]
+MAP_SOURCES = ["lba_map.cpp", "optimizer.cpp", "bundle_adjustment.cpp", "capi.cpp"]
 MAP_HEADERS = ["lba_map.hpp", "optimizer.hpp", os.path.join("..", "..", "include", "amc_lba_map.h"),
                os.path.join("..", "..", "include", "amc_lba.h"), os.path.join("..", "csrc", "lba_math.hpp")]
 CXX = os.environ.get("CXX", "g++")
 # -ffp-contract=off: the adapter's float conversions follow the reference's rounding step by step
-MAP_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra", "-ffp-contract=off"]
+MAP_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall", "-Wextra", "-ffp-contract=off"]
 
 
 def _digest(cmd_flags, files, extra=b""):

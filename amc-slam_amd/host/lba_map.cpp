@@ -253,6 +253,33 @@ long unsigned Map::KeyFramesInMap() const {
     return n;
 }
 
+std::vector<MultiKeyFrame*> Map::GetAllKeyFrames() const {
+    std::vector<MultiKeyFrame*> v;
+    for (const auto& k : mvKeyFrames)
+        if (!k->mbBad && k->mMapId == mMapId) v.push_back(k.get());
+    std::stable_sort(v.begin(), v.end(), [](const MultiKeyFrame* a, const MultiKeyFrame* b) { return a->mnId < b->mnId; });
+    return v;
+}
+
+std::vector<MapPoint*> Map::GetAllMapPoints() const {
+    std::vector<MapPoint*> v;
+    for (const auto& p : mvMapPoints)
+        if (!p->mbBad) v.push_back(p.get());
+    std::stable_sort(v.begin(), v.end(), [](const MapPoint* a, const MapPoint* b) { return a->mnId < b->mnId; });
+    return v;
+}
+
+unsigned long Map::GetInitKFid() const {
+    bool any = false;
+    unsigned long id = 0;
+    for (const auto& k : mvKeyFrames)
+        if (k->mMapId == mMapId && (!any || k->mnId < id)) {
+            id = k->mnId;
+            any = true;
+        }
+    return id;
+}
+
 MultiKeyFrame* Map::kf_by_id(int64_t id) const {
     auto it = mKFById.find(id);
     return it == mKFById.end() ? nullptr : it->second;

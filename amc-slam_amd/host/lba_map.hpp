@@ -83,6 +83,10 @@ public:
     MultiKeyFrame* mPrevKF = nullptr;
     MultiKeyFrame* mNextKF = nullptr;
     unsigned long mnBALocalForKF = 0, mnBAFixedForKF = 0;
+    // global BA results held back while a loop is being corrected (include/KeyFrame.h:365-370)
+    SE3f mTbwGBA;
+    float mVwbGBA[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long mnBAGlobalForKF = 0;
 
     std::vector<KeyPoint> mvKeysUn;
     std::vector<int> mmpKeyToCam;
@@ -124,6 +128,8 @@ class MapPoint {
 public:
     unsigned long mnId = 0;
     unsigned long mnBALocalForKF = 0;
+    Vec3f mPosGBA;                      // global BA result held back during a loop correction
+    unsigned long mnBAGlobalForKF = 0;  // (include/MapPoint.h)
     std::vector<float> mvTrackDepth;
     int nCamera = 0;
 
@@ -158,6 +164,13 @@ public:
     // Map::KeyFramesInMap / GetMaxKFid / EraseMapPoint / IncreaseChangeIndex (src/Map.cc)
     long unsigned KeyFramesInMap() const;
     unsigned long GetMaxKFid() const { return mnMaxKFid; }
+    // Map::GetAllKeyFrames / GetAllMapPoints (src/Map.cc): the map's sets, from which bad keyframes and
+    // points have been erased (here they stay owned, flagged bad); keyframes of this map only, by id
+    std::vector<MultiKeyFrame*> GetAllKeyFrames() const;
+    std::vector<MapPoint*> GetAllMapPoints() const;
+    // Map::GetInitKFid: the id of the keyframe the map was created with, i.e. its first (smallest) id
+    // (the snapshot does not carry mnInitKFid; a map's ids grow from it)
+    unsigned long GetInitKFid() const;
     void EraseMapPoint(MapPoint* pMP) { (void)pMP; }   // the point stays owned here, flagged bad
     void IncreaseChangeIndex() { ++mnBigChangeIdx; }
     std::mutex mMutexMapUpdate;

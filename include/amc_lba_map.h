@@ -140,6 +140,17 @@ typedef struct lbamap_result {
     double  chi2_initial, chi2_final;   /* err, err_end (Optimizer.cc:1221-1253) */
 } lbamap_result;
 
+/* What BundleAdjustment / GlobalBundleAdjustemnt did (src/Optimizer.cc:53-367). */
+typedef struct lbamap_ba_result {
+    int32_t status;             /* LBA_OK or an LBA_E_* code (nothing written back) */
+    int32_t n_kf, n_fixed_kf;   /* keyframe vertices; fixed: the map's initial keyframe */
+    int32_t n_mp;               /* point vertices kept (at least one keyframe observation) */
+    int32_t n_priors, n_vel;    /* EdgeGaussianPrior / EdgeVelocity */
+    int32_t n_edges[5];         /* MonoGP, StereoGP (non-keyframes), Mono, Stereo, MonoGP at keyframe times */
+    int32_t iterations;
+    double  chi2_initial, chi2_final;
+} lbamap_ba_result;
+
 typedef struct lbamap lbamap;   /* opaque: the loaded map + a reusable lba_problem */
 
 /* Load a snapshot (bytes as laid out above).  Returns LBA_OK or LBA_E_ARG. */
@@ -161,6 +172,21 @@ int lbamap_local_gpba(lbamap* m, int64_t kf_id, volatile const int32_t* stop_fla
  * with arrays of those sizes.  kf_ids / mp_ids / obs_tag (may be NULL) give the map ids of each
  * keyframe / landmark row and, per observation, the post-pass list it belongs to
  * (0 MonoGP, 1 StereoGP, 2 Mono, 3 Stereo, 4 MonoGP at KF time). */
+/* Optimizer::GlobalBundleAdjustemnt(pMap, n_iterations, stop, loop_kf) on the whole map (every keyframe
+ * and map point of it, GetAllKeyFrames / GetAllMapPoints), GPU engine on opt->device (opt->large and
+ * opt->extrinsic are ignored).  loop_kf == 0 writes poses, velocities and points back (SetPose /
+ * SetVelocity / SetWorldPos + UpdateNormalAndDepth); loop_kf != 0 stores them as the GBA results
+ * (mTbwGBA, mVwbGBA, mPosGBA, mnBAGlobalForKF), read back with lbamap_kf_gba / lbamap_mp_gba. */
+int lbamap_global_ba(lbamap* m, int32_t n_iterations, volatile const int32_t* stop_flag, uint64_t loop_kf,
+                     const lbamap_options* opt, lbamap_ba_result* out);
+int lbamap_kf_gba(const lbamap* m, int64_t kf_id, float q[4], float t[3], float vel[6], uint64_t* loop_kf);
+int lbamap_mp_gba(const lbamap* m, int64_t mp_id, float pos[3], uint64_t* loop_kf);
+/* The global BA graph as flat arrays, without optimising (parity tests), same outputs as
+ * lbamap_build_window. */
+int lbamap_build_ba_window(lbamap* m, int32_t counts[6], lba_kf* kfs, double* lm_xyz, lba_obs* obs,
+                           lba_prior* priors, int32_t* vel_kfs, lba_cam* cams, int64_t* kf_ids, int64_t* mp_ids,
+                           int32_t* obs_tag, lba_config* cfg);
+
 int lbamap_build_window(lbamap* m, int64_t kf_id, const lbamap_options* opt, int32_t counts[6],
                         lba_kf* kfs, double* lm_xyz, lba_obs* obs, lba_prior* priors, int32_t* vel_kfs,
                         lba_cam* cams, int64_t* kf_ids, int64_t* mp_ids, int32_t* obs_tag, lba_config* cfg);

@@ -154,7 +154,8 @@ def test_map_abi_exports():
     ("lbamap_header", ms.HEADER_DTYPE.itemsize), ("lbamap_cam", ms.MCAM_DTYPE.itemsize),
     ("lbamap_kf", ms.MKF_DTYPE.itemsize), ("lbamap_kp", ms.KP_DTYPE.itemsize), ("lbamap_mp", ms.MP_DTYPE.itemsize),
     ("lbamap_mpobs", ms.MPOBS_DTYPE.itemsize), ("lbamap_gpobs", ms.GPOBS_DTYPE.itemsize),
-    ("lbamap_options", ctypes.sizeof(ms.LbamapOptions)), ("lbamap_result", ctypes.sizeof(ms.LbamapResult))])
+    ("lbamap_options", ctypes.sizeof(ms.LbamapOptions)), ("lbamap_result", ctypes.sizeof(ms.LbamapResult)),
+    ("lbamap_ba_result", ctypes.sizeof(ms.LbamapBAResult))])
 def test_map_struct_layouts_match_header(struct, size):
     assert _c_sizeof(struct) == size
 
