@@ -81,6 +81,7 @@ def lib():
         L.lba_set_farm_group.argtypes = [vp, vp, ctypes.c_int32]
         L.lba_farm_plan.argtypes = [vp, _lp, _ip, _lp, _ip, _ip]
         L.lba_farm_exchange.argtypes = [vp]
+        L.lba_solver_info.argtypes = [vp, _ip]
         L.lba_farm_match.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _lp, _lp, _ip, ctypes.c_int32, _ip]
         _lib = L
     return _lib
@@ -91,7 +92,7 @@ def exported_symbols():
             "lba_optimize", "lba_get_state", "lba_set_state", "lba_eval", "lba_trial_chi2", "lba_linearize", "lba_solve_step",
             "lba_pose_dim", "lba_set_partition", "lba_rccl_unique_id", "lba_set_partition_rccl", "lba_group_create",
             "lba_group_destroy", "lba_set_partition_group", "lba_get_cams", "lba_set_farm", "lba_set_farm_rccl",
-            "lba_set_farm_group", "lba_farm_plan", "lba_farm_exchange", "lba_farm_match"]
+            "lba_set_farm_group", "lba_farm_plan", "lba_farm_exchange", "lba_farm_match", "lba_solver_info"]
 
 
 def _i32(a):
@@ -235,6 +236,12 @@ class Problem:
         out = np.zeros(5, dtype=np.int32)
         self._check(lib().lba_farm_plan(self.h, kgp, kop, lgp, lop, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
         return tuple(int(v) for v in out)
+
+    def solver_info(self):
+        """lba_solver_info: dict(tail, panels, envelope_tiles, band, chain)."""
+        out = np.zeros(5, dtype=np.int32)
+        self._check(lib().lba_solver_info(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return dict(zip(("tail", "panels", "envelope_tiles", "band", "chain"), (int(v) for v in out)))
 
     def farm_exchange(self):
         self._check(lib().lba_farm_exchange(self.h))

@@ -114,6 +114,29 @@ class _Trajectory:
         return v
 
 
+class _CircleTrajectory(_Trajectory):
+    """One lap of a circle in `period` seconds (constant yaw rate): the last keyframes come back to where
+    the first ones were, so landmarks near the start are seen again at the end (a loop closure)."""
+
+    def __init__(self, t_start, period, speed=4.0, height=1.5):
+        self.t_start, self.period, self.speed, self.h = t_start, period, speed, height
+        self.w = 2 * np.pi / period
+        self.r = speed / self.w
+
+    def yaw(self, t):
+        return self.w * (np.asarray(t) - self.t_start)
+
+    def yaw_rate(self, t):
+        return np.full(np.shape(t), self.w)
+
+    def pose(self, t):
+        t = np.asarray(t, dtype=np.float64)
+        a = self.yaw(t)
+        R = _rotz(a)
+        p = np.stack([self.r * np.sin(a), self.r * (1 - np.cos(a)), np.full(t.shape, self.h)], axis=-1)
+        return R, p
+
+
 @dataclass
 class Window:
     kfs: np.ndarray
@@ -152,17 +175,19 @@ class Window:
 
 def make_window(n_opt_kf=50, n_fixed=1, n_lm=20000, obs_per_lm=6, n_cam=4, gp=True, stereo_frac=0.5,
                 outlier_frac=0.05, seed=20250912, global_ba=False, perturb=True, t0=100.0, name="",
-                track=None, max_track=40, band=25):
+                track=None, max_track=40, band=25, loop=False):
     """Build one window.  n_fixed KFs come first (oldest); global_ba=True gives the
     BundleAdjustment graph shape (priors from the first KF, Huber 21.026 on priors, lambda0
     1e-5, src/Optimizer.cc:61-321).  Landmarks are seen from a band of `band` KFs around their
     anchor; track=None draws obs_per_lm +- 2 observations per landmark, track="geometric" a
     long-tailed track length 2 + Geometric(1 / (obs_per_lm - 1)) capped at max_track (long tracks:
-    landmarks seen from more keyframes than one tile of the device path holds)."""
+    landmarks seen from more keyframes than one tile of the device path holds).  loop=True drives one
+    lap of a circle: the keyframe band around a landmark's anchor wraps around, so the last keyframes
+    re-observe the first ones' landmarks (the long-range blocks of a loop-closure global BA)."""
     rng = np.random.default_rng(seed)
     n_kf = n_fixed + n_opt_kf
     kf_t = t0 + 0.1 * np.arange(n_kf)
-    traj = _Trajectory(kf_t[0] - 0.1, kf_t[-1] + 0.1)
+    traj = _CircleTrajectory(kf_t[0], 0.1 * n_kf) if loop else _Trajectory(kf_t[0] - 0.1, kf_t[-1] + 0.1)
 
     # --- cameras: reference camera (last) looks forward; others yawed +90, 180, -90 deg
     Rbc0 = np.array([[0.0, 0.0, 1.0], [-1.0, 0.0, 0.0], [0.0, -1.0, 0.0]])
@@ -205,8 +230,12 @@ def make_window(n_opt_kf=50, n_fixed=1, n_lm=20000, obs_per_lm=6, n_cam=4, gp=Tr
     # --- visibility over a KF band around the anchor (chunked over landmarks to bound memory)
     band = min(n_kf, band)
     koff = np.arange(band) - band // 2
-    kk = np.clip(k0[:, None] + koff[None, :], 0, n_kf - 1)                 # [nl, band]
-    kk_valid = (k0[:, None] + koff[None, :] >= 0) & (k0[:, None] + koff[None, :] < n_kf)
+    if loop:   # the band wraps around the lap
+        kk = (k0[:, None] + koff[None, :]) % n_kf
+        kk_valid = np.ones(kk.shape, bool)
+    else:
+        kk = np.clip(k0[:, None] + koff[None, :], 0, n_kf - 1)                 # [nl, band]
+        kk_valid = (k0[:, None] + koff[None, :] >= 0) & (k0[:, None] + koff[None, :] < n_kf)
     u = np.empty((nl_gen, band, n_cam))
     v = np.empty((nl_gen, band, n_cam))
     z = np.empty((nl_gen, band, n_cam))
@@ -226,7 +255,10 @@ def make_window(n_opt_kf=50, n_fixed=1, n_lm=20000, obs_per_lm=6, n_cam=4, gp=Tr
     if gp and n_cam > 1:
         # GP edges need the previous KF inside the window (src/Optimizer.cc:1112-1116)
         vis[:, :, : n_cam - 1] &= (kk > 0)[:, :, None]
-    score = np.abs(kk - k0[:, None])[:, :, None] * n_cam + rng.random(vis.shape)
+    dk = np.abs(kk - k0[:, None])
+    if loop:
+        dk = np.minimum(dk, n_kf - dk)
+    score = dk[:, :, None] * n_cam + rng.random(vis.shape)
     score = np.where(vis, score, np.inf).reshape(nl_gen, -1)
     order = np.argsort(score, axis=1, kind="stable")
     nvalid = np.isfinite(score).sum(axis=1)

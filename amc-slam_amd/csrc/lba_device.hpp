@@ -194,6 +194,10 @@ struct DevProblem {
     const int* pfirst;
     const int* ppos;
     const int* pnat;
+    // rows: natural -> factorisation order (the block ordering of the keyframes, then the panel
+    // permutation of the dissection) and back; [npad], the identity on the padding rows
+    const int* rpos;
+    const int* rnat;
     const int* chol_items;
     const int* h_steps;
     int n_steps;

@@ -56,6 +56,8 @@ struct lba_problem {
     double* kst[2] = {nullptr, nullptr};
     double* lst[2] = {nullptr, nullptr};
     int cur = 0;
+    int nd_tail = 0;              // panels of the dissection's tail separator (rows reaching back: loops)
+    int chain = 0;                // panels on the factorisation's dependent chain
     // device buffers of the window, in set_problem's allocation order; the next set_problem reuses
     // them in the same order where they are large enough (LocalGPBA windows are alike call to call),
     // so a call pays no hipMalloc / hipFree
@@ -992,15 +994,20 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.n_mslots = n_mslots; D.n_hslots = n_hslots; D.n_gslots = n_gslots; D.n_sslots = n_sslots; D.n_gpslots = n_gpslots;
     const int npad = (p->np + CHOL_NB - 1) / CHOL_NB * CHOL_NB;
     mark("upload");
-    // ---- dense solve layout.  Envelope of S at panel granularity (per CHOL_NB panel of rows, the
-    // first panel any of its rows has a structural non-zero in), then a one-level nested-dissection
-    // ordering of the panels: [left | right | separator], where the right block's rows do not touch
-    // the left block's columns.  The factorisation then eliminates left and right panels pairwise in
-    // the same launch and the separator afterwards, so the dependent chain is
-    // max(left, right) + separator panels instead of all of them.  Cholesky fill stays inside the
-    // envelope of the permuted matrix, which bounds everything the solver touches.
+    // ---- solve layout of the reduced camera system (block order, envelope, dissection, schedule)
     {
         const int NP = npad / CHOL_NB;
+        // Envelope of S at panel granularity (per CHOL_NB panel of rows, the first panel any of its rows has
+        // a structural non-zero in), then a one-level nested-dissection ordering of the panels.  The natural
+        // (time) order is cut into [A | S1 | B | S2]: the rows of B touch no column of A, S1 separates them,
+        // and S2 is a tail of rows that may reach back anywhere (the last keyframes of a loop closure
+        // re-observe the first ones' points: LoopClosing's global BA).  The factorisation order is
+        // [A | B | S1 | S2]: A and B are eliminated pairwise and concurrently, the separators afterwards,
+        // so the dependent chain is max(A, B) + S1 + S2 panels instead of all of them.  Cholesky fill stays
+        // inside the envelope of the permuted matrix, which bounds everything the solver touches.  Panels
+        // holding rows of free extrinsics (dense: they couple every keyframe) join the tail.  A partition
+        // dissects the union envelope of its ranks.
+        const int NPk = std::min(NP, 12 * n_pb_kf / CHOL_NB + (n_ext ? 0 : NP));
         std::vector<int> fk(n_pb);
         for (int b = 0; b < n_pb; ++b) fk[b] = b;   // diagonal (damping)
         for (int u = 0; u < n_ublocks; ++u)
@@ -1027,24 +1034,34 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 pfirst[P] = f;
             }
         }
-        // panels holding rows of free extrinsics (dense: they couple every keyframe) form a tail that
-        // closes the separator; the dissection splits the keyframe panels before it
-        const int NPk = std::min(NP, 12 * n_pb_kf / CHOL_NB + (n_ext ? 0 : NP));
-        int sa = NPk, sb = NPk, best = NP;
-        for (int a = 1; a < NPk; ++a) {
-            int b = NPk;
-            while (b > a && pfirst[b - 1] >= a) --b;   // [b, NPk): rows with no entry left of a
-            if (b >= NPk) continue;
-            const int len = std::max(a, NPk - b) + (b - a) + (NP - NPk);
-            if (len < best) { best = len; sa = a; sb = b; }
+        // cuts (a, b, c): A = [0, a), S1 = [a, b), B = [b, c), S2 = [c, NPk) (+ the extrinsic panels)
+        int sa = NPk, sb = NPk, sc = NPk, best = NP;
+        const bool no_tail = std::getenv("LBA_ND_NO_TAIL") != nullptr;   // (diagnostics: no S2)
+        for (int c = NPk; c >= 1 && (!no_tail || c == NPk); --c) {
+            if (NPk - c >= best) break;   // a tail this long is no shorter than the best chain
+            for (int a = 1; a < c; ++a) {
+                int b = c;
+                while (b > a && pfirst[b - 1] >= a) --b;   // [b, c): rows with no entry left of a
+                if (b >= c) continue;
+                const int len = std::max(a, c - b) + (b - a) + (NPk - c) + (NP - NPk);
+                if (len < best) { best = len; sa = a; sb = b; sc = c; }
+            }
         }
-        const int nl = sa, nr = NPk - sb, ns = sb - sa + (NP - NPk);
+        const int nl = sa, nr = sc - sb, ns = NP - nl - nr;
+        p->chain = std::min(best, NP);
+        p->nd_tail = NPk - sc;
         D.nd_left = nl;
         D.nd_right = nr;
         std::vector<int> ppos(NP), pnat(NP);
-        for (int P = 0; P < NP; ++P)
-            ppos[P] = P >= NPk ? P : (P < sa ? P : (P >= sb ? nl + (P - sb) : nl + nr + (P - sa)));
+        for (int P = 0; P < NP; ++P)   // [A | B | S1 | S2 | extrinsics]
+            ppos[P] = P >= sc ? P : (P < sa ? P : (P >= sb ? nl + (P - sb) : nl + nr + (P - sa)));
         for (int P = 0; P < NP; ++P) pnat[ppos[P]] = P;
+        // rows: natural -> factorisation order, and back
+        std::vector<int> rpos(npad), rnat(npad);
+        for (int r = 0; r < npad; ++r) {
+            rpos[r] = ppos[r / CHOL_NB] * CHOL_NB + r % CHOL_NB;
+            rnat[rpos[r]] = r;
+        }
         // envelope of the permuted matrix (lower part, panel positions)
         std::vector<int> pfh(NP);
         for (int i = 0; i < NP; ++i) pfh[i] = i;
@@ -1208,6 +1225,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         D.pfirst = dupload(p, pfh);
         D.ppos = dupload(p, ppos);
         D.pnat = dupload(p, pnat);
+        D.rpos = dupload(p, rpos);
+        D.rnat = dupload(p, rnat);
         // every trial, k_schur zeroes the tiles of S inside the permuted envelope (everything the
         // factorisation may write: structural non-zeros and fill-in) and k_assemble then writes the
         // structurally non-zero blocks; the rest of S stays zero from the upload
@@ -1868,6 +1887,16 @@ int lba_set_partition_group(lba_problem* p, lba_group* g, int32_t rank) {
 }
 
 // ---- window farm
+int lba_solver_info(const lba_problem* p, int32_t out[5]) {
+    if (!p || !out || !p->has_problem) return LBA_E_ARG;
+    out[0] = p->nd_tail;
+    out[1] = p->D.npad / CHOL_NB;
+    out[2] = p->D.n_ztiles;
+    out[3] = p->D.cf_band;
+    out[4] = p->chain;
+    return LBA_OK;
+}
+
 int lba_set_farm(lba_problem* p, int32_t rank, int32_t nranks, lba_allreduce_fn fn, void* user) {
     if (!p || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !fn)) return LBA_E_ARG;
     if (p->farm_comm) (void)ncclCommDestroy(p->farm_comm);

@@ -1030,14 +1030,13 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
             } else if (bi != bj || j >= i) {               // factorisation order, lower triangle: one
                 // write per unordered pair (the natural-lower entry; a diagonal block's partial sums
                 // are not bitwise symmetric, so writing both would race)
-                const int rh = P.ppos[r / CHOL_NB] * CHOL_NB + r % CHOL_NB;
-                const int ch = P.ppos[c / CHOL_NB] * CHOL_NB + c % CHOL_NB;
+                const int rh = P.rpos[r], ch = P.rpos[c];
                 P.S[(size_t)max(rh, ch) * n + min(rh, ch)] = t;
             }
         }
         if (blockIdx.x == 0 && P.part_rank == 0)   // padding rows: identity (rank 0 of a partition)
             for (int r = P.np + tid; r < n; r += 144 * RED_GROUPS) {
-                const int rh = (flags & ASM_FULL) ? r : P.ppos[r / CHOL_NB] * CHOL_NB + r % CHOL_NB;
+                const int rh = (flags & ASM_FULL) ? r : P.rpos[r];
                 P.S[(size_t)rh * n + rh] = 1.0;
                 P.bS[rh] = 0.0;
             }
@@ -1060,7 +1059,7 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
             double t = 0.0;
             for (int q = 0; q < 48; ++q) t += red[q * 12 + tid];
             const int r = 12 * k + tid;
-            const int rh = (flags & ASM_FULL) ? r : P.ppos[r / CHOL_NB] * CHOL_NB + r % CHOL_NB;
+            const int rh = (flags & ASM_FULL) ? r : P.rpos[r];
             P.bS[rh] = bpv - t;   // bS = b_p - sum Hpl Dinv bl (factorisation order)
         }
     }
@@ -1421,8 +1420,8 @@ struct CholFlow {
     // factorisation) and per output panel one GEMV
     double* Linv;        // [npad][npad] tiles (i, j), i > j, of L^-1 (factorisation order)
     int* ivready;        // per lower tile (tri_id): epoch once Linv(i, j) is published
-    double* xout;        // the solution, natural panel order
-    const int* pnat;     // natural panel of a position
+    double* xout;        // the solution, natural order
+    const int* rnat;     // natural row of a factorisation row
     // band mode (kinds 4, 5): forward / back substitution tasks instead of L^-1 tiles
     double* xpos;        // [npad] x in factorisation order, handed off between back tasks
     int* xready;         // per panel: epoch once x_j is published
@@ -1691,7 +1690,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
                 double x = 0.0;
 #pragma unroll
                 for (int u = 0; u < 8; ++u) x += Lt[1][u][tid];
-                a.xout[a.pnat[j] * CNB + tid] = x;
+                a.xout[a.rnat[j * CNB + tid]] = x;
             }
             if (a.tdbg && tid == 0) a.tdbg[16 * j + 15] = __builtin_amdgcn_s_memrealtime();
             __syncthreads();
@@ -1767,7 +1766,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
 #pragma unroll 8
                 for (int rr = 0; rr < CNB; ++rr) x += ld_sc1(a.LinvT + (size_t)j * CNB * CNB + tid * CNB + rr) * Lt[0][0][rr];
                 st_sc1(a.xpos + j * CNB + tid, x);
-                a.xout[a.pnat[j] * CNB + tid] = x;
+                a.xout[a.rnat[j * CNB + tid]] = x;
             }
             cf_publish(a, a.xready + j);
             continue;
@@ -1986,7 +1985,7 @@ __global__ __launch_bounds__(BS_THREADS) void k_chol_backsolve(const double* __r
                                                                double* __restrict__ yv,
                                                                double* __restrict__ out,
                                                                const int* __restrict__ pfirst,
-                                                               const int* __restrict__ pnat,
+                                                               const int* __restrict__ rnat,
                                                                unsigned long long* tdbg, const LMCtl* ctl,
                                                                int gate, int lo0, int hi0, int lo1, int hi1,
                                                                int write_y) {
@@ -2020,7 +2019,7 @@ __global__ __launch_bounds__(BS_THREADS) void k_chol_backsolve(const double* __r
                 }
                 const double xl = (s0 + s1) + (s2 + s3);
                 xb[lane] = xl;
-                out[pnat[blk] * CNB + lane] = xl;   // natural order
+                out[rnat[blk * CNB + lane]] = xl;   // natural order
             }
             if (tdbg && tid == 0) tdbg[(size_t)blk * 16 + 1] = clock64();   // diagonal block done
         } else {
@@ -2483,7 +2482,7 @@ void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStr
         a.tdbg = P.tdbg_chol;
         a.tdbg2 = P.tdbg_bs;
         a.tdbg3 = P.tdbg_cf;
-        a.Linv = P.cf_linv; a.ivready = P.cf_ivready; a.xout = P.xsol; a.pnat = P.pnat; a.fready = P.cf_fready;
+        a.Linv = P.cf_linv; a.ivready = P.cf_ivready; a.xout = P.xsol; a.rnat = P.rnat; a.fready = P.cf_fready;
         a.zready = P.cf_zready; a.zv = P.cf_zv;
         a.xpos = P.cf_xpos; a.xready = P.cf_ivready;
         if (e0)
@@ -2503,9 +2502,9 @@ void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStr
     const int NP = n / CHOL_NB, nl = P.nd_left, nr = P.nd_right;
     if (nl + nr < NP)
         hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(BS_THREADS), 0, s, P.Lm, P.LinvT, n, P.yv, P.xsol,
-                           P.pfirst, P.pnat, P.tdbg_bs, P.ctl, gate, nl + nr, NP, 0, 0, 1);
+                           P.pfirst, P.rnat, P.tdbg_bs, P.ctl, gate, nl + nr, NP, 0, 0, 1);
     hipLaunchKernelGGL(k_chol_backsolve, dim3(nr > 0 ? 2 : 1), dim3(BS_THREADS), 0, s, P.Lm, P.LinvT, n, P.yv,
-                       P.xsol, P.pfirst, P.pnat, P.tdbg_bs, P.ctl, gate, 0, nl, nl, nl + nr, 0);
+                       P.xsol, P.pfirst, P.rnat, P.tdbg_bs, P.ctl, gate, 0, nl, nl, nl + nr, 0);
 }
 void launch_update(const DevProblem& P, double lambda, int sel, int gate, int jac, hipStream_t s) {
     hipLaunchKernelGGL(k_update, dim3(P.n_upd_blocks), dim3(UPD_THREADS), 0, s, P, lambda, sel, gate, jac);

@@ -252,6 +252,12 @@ int lba_linearize(lba_problem* p, double* residuals, double* H_pp, double* b, do
 /* One damped solve at lambda on the last linearisation: dx [np + 3*n_lm] (poses then
  * landmarks), BlockSolver::solve with setLambda/restoreDiagonal (block_solver.hpp:354-486). */
 int lba_solve_step(lba_problem* p, double lambda, double* dx);
+/* How the reduced camera system is solved (after lba_set_problem): out[0] panels of the dissection's
+ * tail separator (rows that reach back to the first panels: the last keyframes of a loop closure),
+ * out[1] panels of CHOL_NB rows, out[2] tiles in the envelope of the factor, out[3] 1 for the
+ * substitution (band) solve, 0 for the L^-1-tile solve, out[4] panels on the factorisation's dependent
+ * chain (max(A, B) + both separators of the dissection [A | B | S1 | S2]). */
+int lba_solver_info(const lba_problem* p, int32_t out[5]);
 /* Dimension of the pose system (12 * number of non-fixed KFs + 6 * number of free extrinsics). */
 int lba_pose_dim(const lba_problem* p);
 /* Current camera extrinsics (write-back of the VertexExtrinsic estimates, src/Optimizer.cc:1419-1428):
