@@ -2119,7 +2119,9 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
             kf_trial_state(P, kst + (size_t)k * KF_STRIDE, P.kf_hidx[k], ok, d, kab[threadIdx.x]);
         }
         __syncthreads();
+#ifndef LBA_EXP_NO_GPPREP
         gp_pair_prep(P, gps, i, kab[0], kab[1], jac);
+#endif
         if (threadIdx.x == 0) P.scale_part[blockIdx.x] = 0.0;
         return;
     }
@@ -2155,6 +2157,9 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
             double* xd = P.x + P.np + 3 * (size_t)l;
             if (ok) {
                 double c[3] = {P.bl[3 * (size_t)l], P.bl[3 * (size_t)l + 1], P.bl[3 * (size_t)l + 2]};
+#ifdef LBA_EXP_NO_LMBACK
+                if (c[0] == 12345.5)
+#endif
                 for (int p = P.lm_pair0[l]; p < P.lm_pair0[l + 1]; ++p) {
                     const double* B = P.Hpl + (size_t)p * 36;
                     const double* xp = P.xsol + 12 * (size_t)P.pair_kf[p];
