@@ -82,6 +82,9 @@ def lib():
         L.lba_farm_plan.argtypes = [vp, _lp, _ip, _lp, _ip, _ip]
         L.lba_farm_exchange.argtypes = [vp]
         L.lba_solver_info.argtypes = [vp, _ip]
+        L.lba_setup_host_profile.argtypes = [ctypes.POINTER(LbaConfig), vp, ctypes.c_int32, vp, ctypes.c_int32, vp,
+                                             ctypes.c_int32, vp, ctypes.c_int32, vp, ctypes.c_int32, vp, ctypes.c_int32,
+                                             _dp, _ip]
         L.lba_farm_match.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _lp, _lp, _ip, ctypes.c_int32, _ip]
         _lib = L
     return _lib
@@ -92,7 +95,30 @@ def exported_symbols():
             "lba_optimize", "lba_get_state", "lba_set_state", "lba_eval", "lba_trial_chi2", "lba_linearize", "lba_solve_step",
             "lba_pose_dim", "lba_set_partition", "lba_rccl_unique_id", "lba_set_partition_rccl", "lba_group_create",
             "lba_group_destroy", "lba_set_partition_group", "lba_get_cams", "lba_set_farm", "lba_set_farm_rccl",
-            "lba_set_farm_group", "lba_farm_plan", "lba_farm_exchange", "lba_farm_match", "lba_solver_info"]
+            "lba_set_farm_group", "lba_farm_plan", "lba_farm_exchange", "lba_farm_match", "lba_solver_info",
+            "lba_setup_host_profile"]
+
+
+def setup_host_profile(win, **cfg_over):
+    """lba_setup_host_profile: the host preprocessing of lba_set_problem on the CPU (no GPU).  Returns
+    (phase ms [order/pairs, tiles, slots/state], counts [device landmarks, pose blocks, np, tiles, layout hash])."""
+    kw = dict(win.cfg)
+    kw.update(cfg_over)
+    cfg = make_config(**kw)
+    kfs = np.ascontiguousarray(win.kfs, dtype=KF_DTYPE)
+    lm = np.ascontiguousarray(win.lm, dtype=np.float64)
+    obs = np.ascontiguousarray(win.obs, dtype=OBS_DTYPE)
+    pri = np.ascontiguousarray(win.priors, dtype=PRIOR_DTYPE)
+    vel = np.ascontiguousarray(win.vel_kfs, dtype=np.int32)
+    cams = np.ascontiguousarray(win.cams, dtype=CAM_DTYPE)
+    ms = np.zeros(3)
+    cnt = np.zeros(5, dtype=np.int32)
+    rc = lib().lba_setup_host_profile(ctypes.byref(cfg), ptr(kfs), len(kfs), ptr(lm), len(lm), ptr(obs), len(obs),
+                                      ptr(pri), len(pri), ptr(vel), len(vel), ptr(cams), len(cams), _d(ms),
+                                      cnt.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    if rc != 0:
+        raise LbaError(rc, "lba_setup_host_profile failed")
+    return ms, cnt
 
 
 def _i32(a):

@@ -21,6 +21,8 @@
 #include <limits>
 #include <map>
 #include <string>
+#include <exception>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -58,6 +60,10 @@ struct lba_problem {
     int cur = 0;
     int nd_tail = 0;              // panels of the dissection's tail separator (rows reaching back: loops)
     int chain = 0;                // panels on the factorisation's dependent chain
+    bool host_only = false;       // lba_setup_host_profile: stop set_problem after the host preprocessing
+    uint32_t setup_hash = 0;      // (host_only) fingerprint of the tiling / slab layout
+    int setup_tiles = 0;
+    std::vector<double> setup_ms; // wall time of the set-up phases (order/pairs, tiles, slots/state, ...)
     // device buffers of the window, in set_problem's allocation order; the next set_problem reuses
     // them in the same order where they are large enough (LocalGPBA windows are alike call to call),
     // so a call pays no hipMalloc / hipFree
@@ -225,6 +231,38 @@ T* dupload(lba_problem* p, const std::vector<T>& v) {
     return d;
 }
 
+// f(i) for i in [0, n) on up to 8 host threads (LBA_SETUP_THREADS overrides; 1: serial).  Callers split work
+// into a fixed number of pieces, so the results never depend on the thread count.
+template <class F>
+void par_for(int n, F f) {
+    static const int nt_env = [] {
+        const char* e = std::getenv("LBA_SETUP_THREADS");
+        const int v = e ? std::atoi(e) : 0;
+        return v > 0 ? v : (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    }();
+    const int nt = std::min(n, nt_env);
+    if (nt <= 1) {
+        for (int i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::atomic<int> next{0};
+    std::exception_ptr err;
+    std::mutex m;
+    std::vector<std::thread> th;
+    th.reserve(nt);
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&] {
+            try {
+                for (int i; (i = next++) < n;) f(i);
+            } catch (...) {
+                std::lock_guard<std::mutex> g(m);
+                if (!err) err = std::current_exception();
+            }
+        });
+    for (auto& x : th) x.join();
+    if (err) std::rethrow_exception(err);
+}
+
 inline bool is_gp(int kind) { return kind == LBA_MONO_GP || kind == LBA_STEREO_GP; }
 inline int obs_dim(int kind) { return (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? 3 : 2; }
 
@@ -304,12 +342,20 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     // LBA_SETUP_TIMING: wall time of the set-up phases on stderr (host preprocessing vs device upload)
     const bool stime = std::getenv("LBA_SETUP_TIMING") != nullptr;
     auto tlast = std::chrono::steady_clock::now();
-    auto mark = [&](const char* what) {
+    p->setup_ms.clear();
+    auto tsub = tlast;
+    auto sub = [&](const char* what) {   // finer stamps inside a phase (LBA_SETUP_TIMING only)
         if (!stime) return;
         const auto now = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "set_problem %-12s %8.3f ms\n", what,
-                     std::chrono::duration<double, std::milli>(now - tlast).count());
-        tlast = now;
+        std::fprintf(stderr, "    %-22s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - tsub).count());
+        tsub = now;
+    };
+    auto mark = [&](const char* what) {
+        const auto now = std::chrono::steady_clock::now();
+        const double ms = std::chrono::duration<double, std::milli>(now - tlast).count();
+        p->setup_ms.push_back(ms);
+        if (stime) std::fprintf(stderr, "set_problem %-12s %8.3f ms\n", what, ms);
+        tlast = tsub = now;
     };
     p->status_entered = false;
     if (p->stream) HIPCHK(hipStreamSynchronize(p->stream));   // (the buffers are reused below)
@@ -375,6 +421,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         throw ApiError{LBA_E_LIMIT, "the L^-1-tile solve is limited to pose systems of 6144"};
     const std::vector<int>& H = p->kf_hidx;
 
+    sub("checks + activity");
     // GP (prev KF, KF) pairs, numbered in order of first appearance; gp_of: each GP observation's pair
     // (per KF b a short list of its pairs: (KF a, pair index); usually one, the previous keyframe)
     std::vector<std::vector<std::pair<int, int>>> gp_by_b(n_kf);
@@ -420,14 +467,17 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             gp_s0[g + 1] = gp_s0[g] + (int)ts[g].size();
             for (const SKey& k : ts[g]) { gps_t.push_back(k.first); gps_cam.push_back(k.second); keys.push_back(k); }
         }
-        for (int i = 0; i < n_obs; ++i)
-            if (is_gp(obs[i].kind)) {
-                const int g = gp_of[i];
-                const SKey* b = keys.data() + gp_s0[g];
-                sample_of[i] = gp_s0[g] + (int)(std::lower_bound(b, b + (gp_s0[g + 1] - gp_s0[g]), skey(obs[i])) - b);
-            }
+        par_for(8, [&](int piece) {
+            for (int i = (int)((long long)n_obs * piece / 8); i < (int)((long long)n_obs * (piece + 1) / 8); ++i)
+                if (is_gp(obs[i].kind)) {
+                    const int g = gp_of[i];
+                    const SKey* b = keys.data() + gp_s0[g];
+                    sample_of[i] = gp_s0[g] + (int)(std::lower_bound(b, b + (gp_s0[g + 1] - gp_s0[g]), skey(obs[i])) - b);
+                }
+        });
     }
 
+    sub("GP pairs + samples");
     // pose sample of every observation: its GP sample, or the KF pose record n_gps + kf_b
     const int n_gps = (int)gps_t.size(), n_smp = n_gps + n_kfs;
     std::vector<int> smp_of(n_obs);
@@ -453,9 +503,10 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     // per landmark: the span of non-fixed KFs observing it (device order key), heavy or not
     std::vector<int> lmin(n_lm, INT_MAX), lmax(n_lm, INT_MAX);
     std::vector<char> heavy(n_lm, 0);
-    {
+    constexpr int SETUP_PIECES = 8;   // (fixed: the results do not depend on the thread count)
+    par_for(SETUP_PIECES, [&](int piece) {
         std::vector<int> kl, sl;
-        for (int l = 0; l < n_lm; ++l) {
+        for (int l = (int)((long long)n_lm * piece / SETUP_PIECES); l < (int)((long long)n_lm * (piece + 1) / SETUP_PIECES); ++l) {
             if (!lm_act[l]) continue;
             kl.clear();
             sl.clear();
@@ -481,7 +532,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             const int ns = (int)(std::unique(sl.begin(), sl.end()) - sl.begin());
             heavy[l] = !tile_fits(lo0[l + 1] - lo0[l], nr, npl, 1, npl, ns, ne);
         }
-    }
+    });
+    sub("heavy classification");
     std::vector<int> order;
     int n_heavy_lm = 0;
     {   // stable order by (heavy, lmin, lmax): sort (key, index) records (INT_MAX = observed by fixed KFs only)
@@ -503,6 +555,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     p->lm_dev.assign(n_lm, -1);
     for (int d = 0; d < nl; ++d) p->lm_dev[order[d]] = d;
 
+    sub("landmark order");
     // observations grouped by device landmark (stable)
     std::vector<int> lobs0(nl + 1, 0), obs_of(n_obs);
     for (int d = 0; d < nl; ++d) {
@@ -511,11 +564,10 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         std::copy(lo_of.begin() + lo0[l], lo_of.begin() + lo0[l + 1], obs_of.begin() + lobs0[d]);
     }
 
+    sub("obs by landmark");
     // (KF, landmark) pairs, per device landmark, ascending pose block
-    std::vector<int> lm_pair0(nl + 1, 0), pair_lm, pair_kf, ks;
-    pair_lm.reserve(2 * (size_t)n_obs);
-    pair_kf.reserve(2 * (size_t)n_obs);
-    for (int d = 0; d < nl; ++d) {
+    std::vector<int> lm_pair0(nl + 1, 0), pair_lm, pair_kf;
+    auto lm_blocks = [&](int d, std::vector<int>& ks) {   // the landmark's pose blocks, ascending, distinct
         ks.clear();
         for (int q = lobs0[d]; q < lobs0[d + 1]; ++q) {
             const lba_obs& o = obs[obs_of[q]];
@@ -525,10 +577,25 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         }
         std::sort(ks.begin(), ks.end());
         ks.erase(std::unique(ks.begin(), ks.end()), ks.end());
-        lm_pair0[d + 1] = lm_pair0[d] + (int)ks.size();
-        for (int k : ks) { pair_lm.push_back(d); pair_kf.push_back(k); }
-    }
-    const int n_pairs = (int)pair_lm.size();
+    };
+    par_for(SETUP_PIECES, [&](int piece) {   // counts, then (after the prefix) the pairs themselves
+        std::vector<int> ks;
+        for (int d = (int)((long long)nl * piece / SETUP_PIECES); d < (int)((long long)nl * (piece + 1) / SETUP_PIECES); ++d) {
+            lm_blocks(d, ks);
+            lm_pair0[d + 1] = (int)ks.size();
+        }
+    });
+    for (int d = 0; d < nl; ++d) lm_pair0[d + 1] += lm_pair0[d];
+    const int n_pairs = lm_pair0[nl];
+    pair_lm.resize(n_pairs);
+    pair_kf.resize(n_pairs);
+    par_for(SETUP_PIECES, [&](int piece) {
+        std::vector<int> ks;
+        for (int d = (int)((long long)nl * piece / SETUP_PIECES); d < (int)((long long)nl * (piece + 1) / SETUP_PIECES); ++d) {
+            lm_blocks(d, ks);
+            for (size_t i = 0; i < ks.size(); ++i) { pair_lm[lm_pair0[d] + i] = d; pair_kf[lm_pair0[d] + i] = ks[i]; }
+        }
+    });
     // lm_kfs[d]: the landmark's pose blocks (ascending) = its pairs' blocks
     struct Span {
         const int* p; size_t n;
@@ -559,14 +626,17 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         // per observation in device order, what the tiling reads (contiguous instead of through obs_of):
         // pose blocks of KF b / KF a / the extrinsic (-1: none or fixed), rows, pose sample
         std::vector<int> dhb(n_obs), dha(n_obs), dhx(n_obs), ddim(n_obs), dsmp(n_obs);
-        for (int q = 0; q < n_obs; ++q) {
-            const lba_obs& ob = obs[obs_of[q]];
-            dhb[q] = H[ob.kf_b];
-            dha[q] = is_gp(ob.kind) ? H[ob.kf_a] : -1;
-            dhx[q] = ext_block(ob);
-            ddim[q] = obs_dim(ob.kind);
-            dsmp[q] = smp_of[obs_of[q]];
-        }
+        par_for(SETUP_PIECES, [&](int piece) {
+            for (int q = (int)((long long)n_obs * piece / SETUP_PIECES); q < (int)((long long)n_obs * (piece + 1) / SETUP_PIECES); ++q) {
+                const lba_obs& ob = obs[obs_of[q]];
+                dhb[q] = H[ob.kf_b];
+                dha[q] = is_gp(ob.kind) ? H[ob.kf_a] : -1;
+                dhx[q] = ext_block(ob);
+                ddim[q] = obs_dim(ob.kind);
+                dsmp[q] = smp_of[obs_of[q]];
+            }
+        });
+        sub("tile inputs");
         std::vector<unsigned long long> tob;
         // LDS rows of a tile's observations [q0, q1) grouped by pose sample: every sample of the tile owns
         // one contiguous row run (stable by observation within a sample)
@@ -598,96 +668,157 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 if (dhx[o] == k) pair_rows.push_back((o - obase) | (2 << 16));
             }
         };
-        int d = 0;
-        // the tile's sample / KF sets grow by the landmark's new elements, found through membership marks
-        // (1: in the tile, 2: new for the landmark being tried); uni is sorted once the tile is closed
-        std::vector<int> uni, usm, new_s, new_k;
-        std::vector<char> kmark((size_t)std::max(n_pb, 1), 0), smark((size_t)std::max(n_smp, 1), 0);
-        uni.reserve(TILE_PAIRS + 8);
-        usm.reserve(TILE_SMP + 8);
-        while (d < n_reg) {
-            int nobs = 0, rows = 0, npair = 0, nlmt = 0, nent = 0;
-            uni.clear();
-            usm.clear();
-            int e = d;
-            while (e < n_reg) {
-                int no = lobs0[e + 1] - lobs0[e], nr = 0, ne = 0;
-                new_s.clear();
-                new_k.clear();
-                for (int q = lobs0[e]; q < lobs0[e + 1]; ++q) {
-                    nr += ddim[q];
-                    if (!smark[dsmp[q]]) { smark[dsmp[q]] = 2; new_s.push_back(dsmp[q]); }
-                    ne += (dhb[q] >= 0) + (dha[q] >= 0) + (dhx[q] >= 0);
+        // regular tiles: the landmarks [0, n_reg) in SETUP_PIECES contiguous pieces, each tiled greedily on
+        // its own thread into piece-local lists (tiles never straddle a piece boundary, so the tiling is the
+        // same for any thread count), then concatenated with their offsets
+        struct TileOut {
+            std::vector<int> t_obs0, t_nobs, t_lm0, t_nlm, t_pair0, t_npair, t_smp0, t_nsmp, t_sent0, t_nsent, t_kf0,
+                t_nkf, tkf_list, tsm_smp, tsm_rows, sent_l1, sent_l2, sent_k1, sent_k2, pair_rows, lm_rows;
+        };
+        const int n_pieces = n_reg >= 256 * SETUP_PIECES ? SETUP_PIECES : 1;
+        std::vector<TileOut> outs(n_pieces);
+        par_for(n_pieces, [&](int piece) {
+            TileOut& T = outs[piece];
+            const int d_end = (int)((long long)n_reg * (piece + 1) / n_pieces);
+            int d = (int)((long long)n_reg * piece / n_pieces);
+            std::vector<unsigned long long> tob;
+            // the tile's sample / KF sets grow by the landmark's new elements, found through membership
+            // marks (1: in the tile, 2: new for the landmark being tried); uni is sorted once the tile closes
+            std::vector<int> uni, usm, new_s, new_k;
+            std::vector<char> kmark((size_t)std::max(n_pb, 1), 0), smark((size_t)std::max(n_smp, 1), 0);
+            uni.reserve(TILE_PAIRS + 8);
+            usm.reserve(TILE_SMP + 8);
+            while (d < d_end) {
+                int nobs = 0, rows = 0, npair = 0, nlmt = 0, nent = 0;
+                uni.clear();
+                usm.clear();
+                int e = d;
+                while (e < d_end) {
+                    int no = lobs0[e + 1] - lobs0[e], nr = 0, ne = 0;
+                    new_s.clear();
+                    new_k.clear();
+                    for (int q = lobs0[e]; q < lobs0[e + 1]; ++q) {
+                        nr += ddim[q];
+                        if (!smark[dsmp[q]]) { smark[dsmp[q]] = 2; new_s.push_back(dsmp[q]); }
+                        ne += (dhb[q] >= 0) + (dha[q] >= 0) + (dhx[q] >= 0);
+                    }
+                    for (int k : lm_kfs[e])
+                        if (!kmark[k]) { kmark[k] = 2; new_k.push_back(k); }
+                    const int npl = lm_pair0[e + 1] - lm_pair0[e];
+                    const bool fits = tile_fits(nobs + no, rows + nr, npair + npl, nlmt + 1,
+                                                (int)(uni.size() + new_k.size()), (int)(usm.size() + new_s.size()),
+                                                nent + ne);
+                    for (int v : new_s) smark[v] = fits ? 1 : 0;
+                    for (int k : new_k) kmark[k] = fits ? 1 : 0;
+                    if (!fits) {
+                        if (e == d)   // (the heavy classification above takes every landmark a tile cannot hold)
+                            throw ApiError{LBA_E_LIMIT, "internal: landmark " + std::to_string(order[e]) + " does not fit a tile"};
+                        break;
+                    }
+                    nobs += no; rows += nr; npair += npl; nlmt += 1; nent += ne;
+                    usm.insert(usm.end(), new_s.begin(), new_s.end());
+                    uni.insert(uni.end(), new_k.begin(), new_k.end());
+                    ++e;
                 }
-                for (int k : lm_kfs[e])
-                    if (!kmark[k]) { kmark[k] = 2; new_k.push_back(k); }
-                const int npl = lm_pair0[e + 1] - lm_pair0[e];
-                const bool fits = tile_fits(nobs + no, rows + nr, npair + npl, nlmt + 1, (int)(uni.size() + new_k.size()),
-                                            (int)(usm.size() + new_s.size()), nent + ne);
-                for (int v : new_s) smark[v] = fits ? 1 : 0;
-                for (int k : new_k) kmark[k] = fits ? 1 : 0;
-                if (!fits) {
-                    if (e == d)   // (the heavy classification above takes every landmark a tile cannot hold)
-                        throw ApiError{LBA_E_LIMIT, "internal: landmark " + std::to_string(order[e]) + " does not fit a tile"};
-                    break;
+                for (int v : usm) smark[v] = 0;
+                for (int k : uni) kmark[k] = 0;
+                std::sort(uni.begin(), uni.end());
+                T.t_obs0.push_back(lobs0[d]); T.t_nobs.push_back(nobs);
+                T.t_lm0.push_back(d); T.t_nlm.push_back(nlmt);
+                T.t_pair0.push_back(lm_pair0[d]); T.t_npair.push_back(npair);
+                T.t_kf0.push_back((int)T.tkf_list.size()); T.t_nkf.push_back((int)uni.size());
+                for (int k : uni) T.tkf_list.push_back(k);
+                auto local = [&](int k) { return (int)(std::lower_bound(uni.begin(), uni.end(), k) - uni.begin()); };
+                // LDS rows grouped by pose sample: every sample of the tile owns one contiguous row run
+                tob.clear();
+                for (int q = lobs0[d]; q < lobs0[e]; ++q)
+                    tob.push_back(((unsigned long long)(unsigned)dsmp[q] << 32) | (unsigned)q);
+                std::sort(tob.begin(), tob.end());
+                T.t_smp0.push_back((int)T.tsm_smp.size());
+                int row = 0;
+                for (size_t i = 0; i < tob.size();) {
+                    const int sm = (int)(tob[i] >> 32), r0 = row;
+                    size_t j = i;
+                    for (; j < tob.size() && (int)(tob[j] >> 32) == sm; ++j) {
+                        const int q = (int)(tob[j] & 0xffffffffu);
+                        ob_row[q] = row;
+                        row += ddim[q];
+                    }
+                    T.tsm_smp.push_back(sm);
+                    T.tsm_rows.push_back(r0 | ((row - r0) << 16));
+                    i = j;
                 }
-                nobs += no; rows += nr; npair += npl; nlmt += 1; nent += ne;
-                usm.insert(usm.end(), new_s.begin(), new_s.end());
-                uni.insert(uni.end(), new_k.begin(), new_k.end());
-                ++e;
-            }
-            for (int v : usm) smark[v] = 0;
-            for (int k : uni) kmark[k] = 0;
-            std::sort(uni.begin(), uni.end());
-            t_obs0.push_back(lobs0[d]); t_nobs.push_back(nobs);
-            t_lm0.push_back(d); t_nlm.push_back(nlmt);
-            t_pair0.push_back(lm_pair0[d]); t_npair.push_back(npair);
-            t_kf0.push_back((int)tkf_list.size()); t_nkf.push_back((int)uni.size());
-            for (int k : uni) tkf_list.push_back(k);
-            auto local = [&](int k) { return (int)(std::lower_bound(uni.begin(), uni.end(), k) - uni.begin()); };
-            emit_rows(lobs0[d], lobs0[e]);
-            // entry lists per pair, row lists per landmark, the pairs' tile-local (KF, landmark)
-            for (int l = d; l < e; ++l) {
-                for (int q = lm_pair0[l]; q < lm_pair0[l + 1]; ++q) {
-                    emit_pair_rows(pair_kf[q], lobs0[l], lobs0[l + 1], lobs0[d]);
-                    pair_r0[q + 1] = (int)pair_rows.size();
-                    pair_lk[q] = local(pair_kf[q]) | ((l - d) << 8);
-                }
-                for (int o = lobs0[l]; o < lobs0[l + 1]; ++o)
-                    for (int r = 0; r < ddim[o]; ++r) lm_rows.push_back(ob_row[o] + r);
-                lm_r0[l + 1] = (int)lm_rows.size();
-            }
-            // Schur entries: every (k1 <= k2) pose-block pair co-observed by a landmark of the tile, in
-            // (k1, k2) order (k_lin_schur writes C's blocks of exactly these KF pairs)
-            {
-                bool co[TILE_KF][TILE_KF] = {};
-                int lk[TILE_KF];
+                T.t_nsmp.push_back((int)T.tsm_smp.size() - T.t_smp0.back());
+                // entry lists per pair, row lists per landmark, the pairs' tile-local (KF, landmark);
+                // pair_r0 / lm_r0 hold piece-local offsets until the concatenation below
                 for (int l = d; l < e; ++l) {
-                    const Span ks = lm_kfs[l];
-                    for (size_t a = 0; a < ks.size(); ++a) lk[a] = local(ks[a]);
-                    for (size_t a = 0; a < ks.size(); ++a)
-                        for (size_t b = a; b < ks.size(); ++b) co[lk[a]][lk[b]] = true;
-                }
-                const int nu = (int)uni.size();
-                t_sent0.push_back((int)sent_l1.size());
-                int nen = 0;
-                for (int i = 0; i < nu; ++i)
-                    for (int j = i; j < nu; ++j)
-                        if (co[i][j]) {
-                            ++nen;
-                            sent_l1.push_back(i); sent_l2.push_back(j);
-                            sent_k1.push_back(uni[i]); sent_k2.push_back(uni[j]);
+                    for (int q = lm_pair0[l]; q < lm_pair0[l + 1]; ++q) {
+                        const int k = pair_kf[q];
+                        for (int o = lobs0[l]; o < lobs0[l + 1]; ++o) {
+                            if (dhb[o] == k) T.pair_rows.push_back((o - lobs0[d]) | (1 << 16));
+                            if (dha[o] == k) T.pair_rows.push_back(o - lobs0[d]);
+                            if (dhx[o] == k) T.pair_rows.push_back((o - lobs0[d]) | (2 << 16));
                         }
-                t_nsent.push_back(nen);
+                        pair_r0[q + 1] = (int)T.pair_rows.size();
+                        pair_lk[q] = local(k) | ((l - d) << 8);
+                    }
+                    for (int o = lobs0[l]; o < lobs0[l + 1]; ++o)
+                        for (int r = 0; r < ddim[o]; ++r) T.lm_rows.push_back(ob_row[o] + r);
+                    lm_r0[l + 1] = (int)T.lm_rows.size();
+                }
+                // Schur entries: every (k1 <= k2) pose-block pair co-observed by a landmark of the tile, in
+                // (k1, k2) order (k_lin_schur writes C's blocks of exactly these KF pairs)
+                {
+                    bool co[TILE_KF][TILE_KF] = {};
+                    int lk[TILE_KF];
+                    for (int l = d; l < e; ++l) {
+                        const Span ks = lm_kfs[l];
+                        for (size_t a = 0; a < ks.size(); ++a) lk[a] = local(ks[a]);
+                        for (size_t a = 0; a < ks.size(); ++a)
+                            for (size_t b = a; b < ks.size(); ++b) co[lk[a]][lk[b]] = true;
+                    }
+                    const int nu = (int)uni.size();
+                    T.t_sent0.push_back((int)T.sent_l1.size());
+                    int nen = 0;
+                    for (int i = 0; i < nu; ++i)
+                        for (int j = i; j < nu; ++j)
+                            if (co[i][j]) {
+                                ++nen;
+                                T.sent_l1.push_back(i); T.sent_l2.push_back(j);
+                                T.sent_k1.push_back(uni[i]); T.sent_k2.push_back(uni[j]);
+                            }
+                    T.t_nsent.push_back(nen);
+                }
+                d = e;
             }
-            d = e;
+        });
+        for (int piece = 0; piece < n_pieces; ++piece) {
+            const TileOut& T = outs[piece];
+            const int o_smp = (int)tsm_smp.size(), o_kf = (int)tkf_list.size(), o_sent = (int)sent_l1.size();
+            const int o_pr = (int)pair_rows.size(), o_lr = (int)lm_rows.size();
+            const int d0 = (int)((long long)n_reg * piece / n_pieces), d1 = (int)((long long)n_reg * (piece + 1) / n_pieces);
+            for (int q = lm_pair0[d0]; q < lm_pair0[d1]; ++q) pair_r0[q + 1] += o_pr;
+            for (int l = d0; l < d1; ++l) lm_r0[l + 1] += o_lr;
+            auto cat = [](std::vector<int>& dst, const std::vector<int>& src, int off) {
+                for (int v : src) dst.push_back(v + off);
+            };
+            cat(t_obs0, T.t_obs0, 0); cat(t_nobs, T.t_nobs, 0); cat(t_lm0, T.t_lm0, 0); cat(t_nlm, T.t_nlm, 0);
+            cat(t_pair0, T.t_pair0, 0); cat(t_npair, T.t_npair, 0); cat(t_smp0, T.t_smp0, o_smp);
+            cat(t_nsmp, T.t_nsmp, 0); cat(t_sent0, T.t_sent0, o_sent); cat(t_nsent, T.t_nsent, 0);
+            cat(t_kf0, T.t_kf0, o_kf); cat(t_nkf, T.t_nkf, 0); cat(tkf_list, T.tkf_list, 0);
+            cat(tsm_smp, T.tsm_smp, 0); cat(tsm_rows, T.tsm_rows, 0); cat(sent_l1, T.sent_l1, 0);
+            cat(sent_l2, T.sent_l2, 0); cat(sent_k1, T.sent_k1, 0); cat(sent_k2, T.sent_k2, 0);
+            cat(pair_rows, T.pair_rows, 0); cat(lm_rows, T.lm_rows, 0);
         }
         n_stiles = (int)t_obs0.size();
+        sub("regular tiles");
         // heavy landmarks: their canonical pairs and landmark slots get no rows of their own
         for (int q = lm_pair0[n_reg]; q < n_pairs; ++q) pair_r0[q + 1] = (int)pair_rows.size();
         for (int l = n_reg; l < nl; ++l) lm_r0[l + 1] = (int)lm_rows.size();
         // segments: runs of a heavy landmark's observations under the limits of k_lin_schur's phases 1-4
-        // (no elimination: no KF-union or MFMA limit; a segment's pairs are its distinct pose blocks)
+        // (no elimination: no KF-union limit; a segment's pairs are its distinct pose blocks)
+        std::vector<int> uni, usm;
+        std::vector<char> kmark((size_t)std::max(n_pb, 1), 0), smark((size_t)std::max(n_smp, 1), 0);
         for (int l = n_reg; l < nl; ++l) {
             hv_lm.push_back(l);
             const int cp0 = lm_pair0[l], ncp = lm_pair0[l + 1] - cp0;
@@ -916,6 +1047,17 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     for (auto& e : pri) { pri_a.push_back(e.kf_a); pri_b.push_back(e.kf_b); }
 
     mark("slots/state");
+    if (p->host_only) {   // (lba_setup_host_profile) a fingerprint of the tiling and the slab layout
+        uint32_t h = 2166136261u;
+        auto mix = [&](const std::vector<int>& v) {
+            for (int x : v) { h ^= (uint32_t)x; h *= 16777619u; }
+        };
+        mix(t_obs0); mix(t_lm0); mix(tsm_meta); mix(pair_rows); mix(lm_rows); mix(pair_lk); mix(sent_l1); mix(sent_l2);
+        mix(sslot); mix(tkf_gslot); mix(seg_slot); mix(ob_row);
+        p->setup_hash = h;
+        p->setup_tiles = n_tiles;
+        return LBA_OK;
+    }
     // ---- device upload
     DevProblem& D = p->D;
     D.n_kf = n_kfs; D.n_kf_user = n_kf; D.n_eprior = n_ext; D.n_lm = nl; D.n_obs = n_obs; D.n_gp = (int)gp_a.size(); D.n_pairs = n_pairs;
@@ -1887,6 +2029,33 @@ int lba_set_partition_group(lba_problem* p, lba_group* g, int32_t rank) {
 }
 
 // ---- window farm
+int lba_setup_host_profile(const lba_config* cfg, const lba_kf* kfs, int32_t n_kf, const double* lm_xyz, int32_t n_lm,
+                           const lba_obs* obs, int32_t n_obs, const lba_prior* priors, int32_t n_priors,
+                           const int32_t* vel_kfs, int32_t n_vel, const lba_cam* cams, int32_t n_cam,
+                           double phase_ms[3], int32_t counts[5]) {
+    if (!cfg) return LBA_E_ARG;
+    lba_problem p;   // no stream, no device memory: set_problem stops before its first device call
+    p.cfg = *cfg;
+    p.host_only = true;
+    try {
+        const int rc = set_problem(&p, kfs, n_kf, lm_xyz, n_lm, obs, n_obs, priors, n_priors, vel_kfs, n_vel, cams, n_cam);
+        if (rc < 0) return rc;
+    } catch (const ApiError& e) {
+        return e.code;
+    } catch (const HipError&) {
+        return LBA_E_HIP;
+    }
+    for (int i = 0; i < 3; ++i) if (phase_ms) phase_ms[i] = i < (int)p.setup_ms.size() ? p.setup_ms[i] : 0.0;
+    if (counts) {
+        counts[0] = p.n_lm_dev;
+        counts[1] = p.n_pb;
+        counts[2] = p.np;
+        counts[3] = p.setup_tiles;
+        counts[4] = (int32_t)p.setup_hash;
+    }
+    return LBA_OK;
+}
+
 int lba_solver_info(const lba_problem* p, int32_t out[5]) {
     if (!p || !out || !p->has_problem) return LBA_E_ARG;
     out[0] = p->nd_tail;

@@ -252,6 +252,14 @@ int lba_linearize(lba_problem* p, double* residuals, double* H_pp, double* b, do
 /* One damped solve at lambda on the last linearisation: dx [np + 3*n_lm] (poses then
  * landmarks), BlockSolver::solve with setLambda/restoreDiagonal (block_solver.hpp:354-486). */
 int lba_solve_step(lba_problem* p, double lambda, double* dx);
+/* Diagnostics: the host preprocessing of lba_set_problem alone (device order, pairs, tiles, slabs; no device,
+ * no GPU needed) on the given window; phase_ms: wall ms of the order/pairs, tiles and slots/state phases;
+ * counts: device landmarks, pose blocks, pose dimension, tiles, a 32-bit fingerprint of the tiling and slab
+ * layout (the same for any LBA_SETUP_THREADS).  Returns LBA_OK or the error lba_set_problem would return. */
+int lba_setup_host_profile(const lba_config* cfg, const lba_kf* kfs, int32_t n_kf, const double* lm_xyz, int32_t n_lm,
+                           const lba_obs* obs, int32_t n_obs, const lba_prior* priors, int32_t n_priors,
+                           const int32_t* vel_kfs, int32_t n_vel, const lba_cam* cams, int32_t n_cam,
+                           double phase_ms[3], int32_t counts[5]);
 /* How the reduced camera system is solved (after lba_set_problem): out[0] panels of the dissection's
  * tail separator (rows that reach back to the first panels: the last keyframes of a loop closure),
  * out[1] panels of CHOL_NB rows, out[2] tiles in the envelope of the factor, out[3] 1 for the

@@ -88,3 +88,24 @@ def test_null_arguments_rejected():
     assert L.lba_create(None, None) == abi.LBA_E_ARG
     assert L.lba_optimize(None, 1, None, None) == abi.LBA_E_ARG
     assert L.lba_get_state(None, None, None) == abi.LBA_E_ARG
+
+
+def _layout(threads):
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, 'amc-slam_amd'); import amc_lba; "
+            "from amc_lba.synth import make_config_window; "
+            "ms, c = amc_lba.setup_host_profile(make_config_window('cfg1_local_50kf')); print(*c)")
+    env = dict(os.environ, LBA_SETUP_THREADS=str(threads))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    return out.stdout.split()
+
+
+def test_set_problem_host_layout_independent_of_threads():
+    """lba_setup_host_profile (the host preprocessing of lba_set_problem, no GPU): the tiling and slab
+    layout of config 1 is the same with 1 and 8 set-up threads (fixed work pieces)."""
+    one, eight = _layout(1), _layout(8)
+    assert one == eight
+    n_lm, n_pb, np_, tiles, _ = (int(x) for x in one)
+    assert n_lm == 20000 and n_pb == 50 and np_ == 600 and 900 < tiles < 1200
