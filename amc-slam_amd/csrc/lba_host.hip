@@ -676,6 +676,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 t_nkf, tkf_list, tsm_smp, tsm_rows, sent_l1, sent_l2, sent_k1, sent_k2, pair_rows, lm_rows;
         };
         const int n_pieces = n_reg >= 256 * SETUP_PIECES ? SETUP_PIECES : 1;
+        // LBA_TILE_OBS_CAP (experiments): a smaller observation budget per regular tile than the LDS allows
+        const int obs_cap = std::getenv("LBA_TILE_OBS_CAP") ? std::max(1, std::atoi(std::getenv("LBA_TILE_OBS_CAP"))) : TILE_OBS;
         std::vector<TileOut> outs(n_pieces);
         par_for(n_pieces, [&](int piece) {
             TileOut& T = outs[piece];
@@ -707,7 +709,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     const int npl = lm_pair0[e + 1] - lm_pair0[e];
                     const bool fits = tile_fits(nobs + no, rows + nr, npair + npl, nlmt + 1,
                                                 (int)(uni.size() + new_k.size()), (int)(usm.size() + new_s.size()),
-                                                nent + ne);
+                                                nent + ne) &&
+                                      (nlmt == 0 || nobs + no <= obs_cap);
                     for (int v : new_s) smark[v] = fits ? 1 : 0;
                     for (int k : new_k) kmark[k] = fits ? 1 : 0;
                     if (!fits) {
@@ -2501,7 +2504,8 @@ int lba_solve_step(lba_problem* p, double lambda, double* dx) {
         trial(p, lambda, false, nullptr, false);
         const int np = p->np, nl = p->D.n_lm, npx = p->np_ext;
         if (p->h_fin[3] != 0.0) {
-            p->err = "reduced camera system not positive definite";
+            p->err = "reduced camera system not positive definite (factorisation status " +
+                     std::to_string((long long)p->h_fin[3]) + ")";
             return LBA_E_SOLVE;
         }
         if (dx) {

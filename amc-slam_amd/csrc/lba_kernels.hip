@@ -658,6 +658,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
     const double* __restrict__ camd = P.camdb[si];
     double* rows = U;
     double* rw = U + TILE_ROWS * ROW_STRIDE;
+    if (P.tdbg_lin && tid == 0) P.tdbg_lin[(size_t)blockIdx.x * 16 + 12] = __builtin_amdgcn_s_memrealtime();
     LBA_TMARK(P.tdbg_lin, 0);
 
     // ---- stage the tile's index lists in LDS
@@ -822,7 +823,10 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
     }
     LBA_TMARK(P.tdbg_lin, 4);
 
-    if (!elim) return;
+    if (!elim) {
+        if (P.tdbg_lin && tid == 0) P.tdbg_lin[(size_t)blockIdx.x * 16 + 13] = __builtin_amdgcn_s_memrealtime();
+        return;
+    }
     __syncthreads();   // every read of the rows is done: their LDS takes Hpl
     if (pl < npair) {
         double* h = U + pl * 36 + 18 * half;
@@ -908,6 +912,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
         }
     }
     LBA_TMARKI(P.tdbg_schur, tile, 3);
+    if (P.tdbg_lin && tid == 0) P.tdbg_lin[(size_t)blockIdx.x * 16 + 13] = __builtin_amdgcn_s_memrealtime();
 }
 
 // One heavy landmark (k_expand work item, PRI_THREADS threads): its segments' partials summed in a fixed
@@ -1131,15 +1136,43 @@ __device__ __forceinline__ void piv_chain(Pivot& x) {
     }
 }
 
+#ifndef LBA_CHOL_DPP
+#define LBA_CHOL_DPP 1
+#endif
+// lane x <- v of lane B + (x & 15): the pivot column of one 16-row half of the diagonal block copied
+// into every 16-lane row of the wave, so the rank-1 update can read entry k with the DPP64 row
+// broadcast (row_newbcast: each lane of a row takes lane k & 15 of that row)
+template <int B>
+__device__ __forceinline__ double rep16(double v, int lane) {
+    const int addr = (B + (lane & 15)) << 2;
+    const unsigned long long u = __double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_ds_bpermute(addr, (int)(unsigned)u);
+    const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(addr, (int)(unsigned)(u >> 32));
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+// acc = fma(-rep[lane of this row with index K & 15], l, acc): one v_fmac_f64 with a DPP64 operand, the same
+// rounding as fma(-l, cb[K], acc) from a readlane broadcast (two v_readlane_b32 fewer per entry)
+template <int K>
+__device__ __forceinline__ void fmac_bcast(double& acc, double rep, double l) {
+    asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc) : "v"(rep), "v"(l), "i"(K & 15));
+}
+
 template <int J, int E, int... T>
-__device__ __forceinline__ void piv_update(double (&row)[CNB], const double (&cb)[CNB], Pivot& x,
+__device__ __forceinline__ void piv_update(double (&row)[CNB], const double (&cb)[CNB], double rep, Pivot& x,
                                            std::integer_sequence<int, T...>) {
     constexpr int NF = E - 1 - J;
     auto step = [&](auto tc) {
         constexpr int t = decltype(tc)::value;
         if constexpr (t < NF) {
+#if LBA_CHOL_DPP
+            (void)cb;
+            fmac_bcast<J + 1 + t>(row[J + 1 + t], rep, x.lij);
+#else
+            (void)rep;
             row[J + 1 + t] -= x.lij * cb[J + 1 + t];
             pin(row[J + 1 + t]);
+#endif
         }
         if constexpr (J + 1 < E) piv_chain<J, E, t, 0>(x);
     };
@@ -1148,6 +1181,7 @@ __device__ __forceinline__ void piv_update(double (&row)[CNB], const double (&cb
 
 template <int J, int E>
 __device__ __forceinline__ void piv_seq(double (&row)[CNB], double r, int lane, bool& bad) {
+    static_assert(E - 16 <= J && J < E && E % 16 == 0 || J >= E, "pivot halves are 16 columns");
     if constexpr (J < E) {
         Pivot x;
         x.lij = row[J] * r;   // lane J: sqrt(d); lanes > J: L(l, J)
@@ -1159,13 +1193,19 @@ __device__ __forceinline__ void piv_seq(double (&row)[CNB], double r, int lane, 
             x.c = __builtin_amdgcn_rsq(own);
             x.d = own;
         }
+        double cb[CNB];
+        double rep = 0.0;
+#if LBA_CHOL_DPP
+        // column J of this half (rows E-16 .. E-1 of the diagonal block) into every 16-lane row
+        if constexpr (J + 1 < E) rep = rep16<E - 16>(x.lij, lane);
+#else
         // column J of L_pp by readlane into SGPRs (an LDS broadcast costs (E - 1 - J) doubles per lane
         // of every factoring wave on the CU's shared LDS return path: no faster, measured)
-        double cb[CNB];
 #pragma unroll
         for (int k = J + 1; k < E; ++k) cb[k] = readlane_d(x.lij, k);
+#endif
         constexpr int NT = (E - 1 - J) > 0 ? (E - 1 - J) : 1;
-        piv_update<J, E>(row, cb, x, std::make_integer_sequence<int, NT>{});
+        piv_update<J, E>(row, cb, rep, x, std::make_integer_sequence<int, NT>{});
         piv_seq<J + 1, E>(row, x.rn, lane, bad);
     }
 }
@@ -1914,14 +1954,19 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
             if (tm) tm[4] = __builtin_amdgcn_s_memrealtime();
             if (wave == 0) {
                 bool bad;
+                const unsigned long long c0 = tf ? clock64() : 0;
                 factor(stg[0], bad);
+                if (tf) tf[7] = clock64() - c0;
                 if (tm) tm[5] = __builtin_amdgcn_s_memrealtime();
                 (void)bad;   // (a non-positive pivot of A(j,j) is reported by panel j's own task)
+            }
+            __syncthreads();
+            // L(i, j) from the staged panel by all four waves (a quarter of the write-through bytes per
+            // wave: the drain before the flag is a quarter as long as one wave storing the tile)
 #pragma unroll
-                for (int m = 0; m < 16; ++m) {
-                    const int e = lane + 64 * m, r = e >> 5, c = e & 31;
-                    st_sc1(a.Lm + (size_t)(i * CNB + r) * n + p0 + c, stg[0][CNB + r][c]);
-                }
+            for (int m = 0; m < 4; ++m) {
+                const int e = tid + 256 * m, r = e >> 5, c = e & 31;
+                st_sc1(a.Lm + (size_t)(i * CNB + r) * n + p0 + c, stg[0][CNB + r][c]);
             }
             cf_publish(a, a.lready + tile_id(i, j));
             if (tm) tm[6] = __builtin_amdgcn_s_memrealtime();
@@ -1939,15 +1984,18 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
         if (tm) tm[4] = __builtin_amdgcn_s_memrealtime();
         if (wave == 0) {
             bool bad;
+            const unsigned long long c0 = tf ? clock64() : 0;
             factor(stg[0], bad);
+            if (tf) tf[7] = clock64() - c0;
             if (__ballot(bad) != 0 && lane == 0) *a.info = 1 + (int)p0;
             if (tm) tm[5] = __builtin_amdgcn_s_memrealtime();
+        }
+        __syncthreads();
 #pragma unroll
-            for (int m = 0; m < 16; ++m) {   // L_jj (plain: no reader in this launch), L_jj^-T
-                const int e = lane + 64 * m, r = e >> 5, c = e & 31;
-                a.Lm[(p0 + r) * n + p0 + c] = (c <= r) ? stg[0][r][c] : 0.0;
-                st_sc1(a.LinvT + p0 * CNB + e, stg[0][CNB + r][c]);
-            }
+        for (int m = 0; m < 4; ++m) {   // L_jj (plain: no reader in this launch), L_jj^-T, by all waves
+            const int e = tid + 256 * m, r = e >> 5, c = e & 31;
+            a.Lm[(p0 + r) * n + p0 + c] = (c <= r) ? stg[0][r][c] : 0.0;
+            st_sc1(a.LinvT + p0 * CNB + e, stg[0][CNB + r][c]);
         }
         cf_publish(a, a.fready + j);
         if (tm) tm[6] = __builtin_amdgcn_s_memrealtime();

@@ -58,6 +58,37 @@ def report(name, stamps, phases, shape, out):
         out.append(f"   shape {s:6s} mean {v.mean():7.1f} max {v.max():6.0f}  corr(total) {c:+.2f}")
 
 
+def timeline(lin, shape, out):
+    """Wall-clock (s_memrealtime, 100 MHz) start / end of every tile workgroup of the last launch: the span,
+    how the tiles' start times spread (dispatch rounds) and which tiles end last."""
+    st, en = lin[:, 12], lin[:, 13]
+    ok = (st > 0) & (en > 0)
+    if not ok.any():
+        return
+    st, en = st[ok], en[ok]
+    idx = np.nonzero(ok)[0]
+    t0 = st.min()
+    s_us, e_us = (st - t0) / 100.0, (en - t0) / 100.0
+    d = e_us - s_us
+    out.append(f"== k_lin_schur timeline (us, tiles of the last launch): span {e_us.max():.2f}, tile duration "
+               f"mean {d.mean():.2f} p50 {np.median(d):.2f} p95 {np.percentile(d, 95):.2f} max {d.max():.2f}")
+    for q in (0.5, 0.75, 0.9, 1.0):
+        out.append(f"   start time quantile {q:4.2f}: {np.quantile(s_us, q):7.2f}   end time quantile {q:4.2f}: {np.quantile(e_us, q):7.2f}")
+    late = np.argsort(-e_us)[:8]
+    for k in late:
+        t = idx[k]
+        out.append(f"   late tile {t:5d}: start {s_us[k]:6.2f} end {e_us[k]:6.2f} dur {d[k]:6.2f}  shape "
+                   + " ".join(f"{n}={shape[j, t]}" for j, n in enumerate(SHAPE)))
+    # a list-scheduling estimate: the measured durations on S slots, in index order vs longest first
+    for slots in (768,):
+        for name, order in (("index order", np.arange(len(d))), ("longest first", np.argsort(-d))):
+            fin = np.zeros(slots)
+            for k in order:
+                j = fin.argmin()
+                fin[j] += d[k]
+            out.append(f"   list schedule on {slots} slots, {name}: makespan {fin.max():.2f} us")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg1_local_50kf")
@@ -76,6 +107,8 @@ def main():
     out = [f"config {args.config}: {nt} tiles"]
     report("k_lin_schur (linearisation)", lin, LIN_PHASES, shape, out)
     report("k_lin_schur (elimination)", sch, SCHUR_PHASES, shape, out)
+    timeline(lin, shape, out)
+    np.savez_compressed(os.path.splitext(args.out)[0] + "_raw.npz", lin=lin, sch=sch, shape=shape)
     if chol is not None:
         if os.environ.get("LBA_CHOL_STEPS") is None:   # k_chol_flow: s_memrealtime (100 MHz) stamps per panel
             npan = int((chol[:, 0] != 0).sum())
@@ -107,7 +140,7 @@ def main():
                     f = lambda x: (x - t0) / 100.0 if x else float("nan")
                     ii, jj, la, pp = r[4] & 4095, (r[4] >> 12) & 4095, (r[4] >> 24) & 1, (r[4] >> 32) & 4095
                     out.append(f"     {tk:4d}: ({ii:2d},{jj:2d}) la={la} | {f(r[0]):7.2f} {f(r[3]):7.2f} (p={pp:2d}) "
-                               f"{f(r[5]):7.2f} {f(r[6]):7.2f} {f(r[1]):7.2f} {f(r[2]):7.2f}")
+                               f"{f(r[5]):7.2f} {f(r[6]):7.2f} {f(r[1]):7.2f} {f(r[2]):7.2f}  factor {r[7]} cycles")
             chol = None
     if chol is not None:
         nst = int((chol[:, 0] != 0).sum())
