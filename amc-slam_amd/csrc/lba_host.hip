@@ -22,6 +22,7 @@
 #include <map>
 #include <string>
 #include <exception>
+#include <functional>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -70,6 +71,11 @@ struct lba_problem {
     struct Alloc { void* ptr; size_t bytes; };
     std::vector<Alloc> allocs;
     size_t alloc_cursor = 0;
+    // pinned staging of the uploads (persistent chunks, bump-allocated per set_problem): dupload copies
+    // a host array into it and queues the host->device copy on the stream, so the DMA overlaps the rest
+    // of the preprocessing; the next set_problem reuses it after its stream synchronisation
+    std::vector<Alloc> pin_chunks;
+    size_t pin_chunk = 0, pin_off = 0;
     double* h_fin = nullptr;      // host-mapped coherent [HFIN_DOUBLES]: trial summary [4], sequence
                                   // number [4], LMCtl mirror [8..] (queued optimisation)
     double* d_hfin = nullptr;     // its device address
@@ -197,6 +203,8 @@ void release_all(lba_problem* p) {   // (lba_destroy)
 void free_all(lba_problem* p) {   // the buffers stay allocated for the next window's dalloc calls
     dump_phase_times(p);
     p->alloc_cursor = 0;
+    p->pin_chunk = 0;
+    p->pin_off = 0;
     p->kst[0] = p->kst[1] = p->lst[0] = p->lst[1] = nullptr;
     p->D = DevProblem{};
     p->has_problem = false;
@@ -224,43 +232,126 @@ T* dalloc(lba_problem* p, size_t n) {
     p->alloc_cursor = p->allocs.size();
     return static_cast<T*>(d);
 }
+// bytes of pinned staging (16-byte aligned) from the persistent chunks
+void* pin_stage(lba_problem* p, size_t bytes) {
+    bytes = (bytes + 15) & ~(size_t)15;
+    while (true) {
+        if (p->pin_chunk == p->pin_chunks.size()) {
+            lba_problem::Alloc a{nullptr, std::max<size_t>(bytes, (size_t)16 << 20)};
+            HIPCHK(hipHostMalloc(&a.ptr, a.bytes, hipHostMallocDefault));
+            p->pin_chunks.push_back(a);
+        }
+        lba_problem::Alloc& a = p->pin_chunks[p->pin_chunk];
+        if (p->pin_off + bytes <= a.bytes) {
+            void* r = static_cast<char*>(a.ptr) + p->pin_off;
+            p->pin_off += bytes;
+            return r;
+        }
+        ++p->pin_chunk;
+        p->pin_off = 0;
+    }
+}
 template <typename T>
 T* dupload(lba_problem* p, const std::vector<T>& v) {
     T* d = dalloc<T>(p, v.size());
-    if (!v.empty()) HIPCHK(hipMemcpy(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    if (!v.empty()) {
+        const size_t bytes = v.size() * sizeof(T);
+        void* st = pin_stage(p, bytes);
+        std::memcpy(st, v.data(), bytes);
+        HIPCHK(hipMemcpyAsync(d, st, bytes, hipMemcpyHostToDevice, p->stream));
+    }
     return d;
 }
 
 // f(i) for i in [0, n) on up to 8 host threads (LBA_SETUP_THREADS overrides; 1: serial).  Callers split work
-// into a fixed number of pieces, so the results never depend on the thread count.
-template <class F>
-void par_for(int n, F f) {
-    static const int nt_env = [] {
+// into a fixed number of pieces, so the results never depend on the thread count.  The workers persist
+// (a set-up makes several parallel passes; spawning threads per pass cost ~0.1 ms each); a pass that finds
+// the pool busy (another problem setting up on another thread) runs on its caller's thread alone.
+class SetupPool {
+  public:
+    static SetupPool& get() {
+        static SetupPool pool;
+        return pool;
+    }
+    int size() const { return (int)workers_.size() + 1; }
+    // false: the pool is in use (the caller runs the pass itself)
+    template <class F>
+    bool run(int n, F& f) {
+        std::unique_lock<std::mutex> busy(busy_, std::try_to_lock);
+        if (!busy.owns_lock()) return false;
+        std::function<void(int)> job = [&](int i) { f(i); };
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &job;
+            n_ = n;
+            next_.store(0);
+            active_ = (int)workers_.size();
+            err_ = nullptr;
+            ++gen_;
+        }
+        cv_.notify_all();
+        work();   // the caller takes pieces too
+        std::unique_lock<std::mutex> g(m_);
+        done_cv_.wait(g, [&] { return active_ == 0; });
+        job_ = nullptr;
+        if (err_) std::rethrow_exception(err_);
+        return true;
+    }
+
+  private:
+    SetupPool() {
         const char* e = std::getenv("LBA_SETUP_THREADS");
         const int v = e ? std::atoi(e) : 0;
-        return v > 0 ? v : (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-    }();
-    const int nt = std::min(n, nt_env);
-    if (nt <= 1) {
-        for (int i = 0; i < n; ++i) f(i);
-        return;
+        const int nt = v > 0 ? v : (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+        for (int t = 1; t < nt; ++t)
+            workers_.emplace_back([this] {
+                unsigned long long seen = 0;
+                while (true) {
+                    {
+                        std::unique_lock<std::mutex> g(m_);
+                        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+                        if (stop_) return;
+                        seen = gen_;
+                    }
+                    work();
+                    std::lock_guard<std::mutex> g(m_);
+                    if (--active_ == 0) done_cv_.notify_all();
+                }
+            });
     }
-    std::atomic<int> next{0};
-    std::exception_ptr err;
-    std::mutex m;
-    std::vector<std::thread> th;
-    th.reserve(nt);
-    for (int t = 0; t < nt; ++t)
-        th.emplace_back([&] {
-            try {
-                for (int i; (i = next++) < n;) f(i);
-            } catch (...) {
-                std::lock_guard<std::mutex> g(m);
-                if (!err) err = std::current_exception();
-            }
-        });
-    for (auto& x : th) x.join();
-    if (err) std::rethrow_exception(err);
+    ~SetupPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& w : workers_) w.join();
+    }
+    void work() {
+        try {
+            for (int i; (i = next_++) < n_;) (*job_)(i);
+        } catch (...) {
+            std::lock_guard<std::mutex> g(m_);
+            if (!err_) err_ = std::current_exception();
+            next_.store(n_);
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex busy_, m_;
+    std::condition_variable cv_, done_cv_;
+    std::function<void(int)>* job_ = nullptr;
+    int n_ = 0, active_ = 0;
+    std::atomic<int> next_{0};
+    unsigned long long gen_ = 0;
+    bool stop_ = false;
+    std::exception_ptr err_;
+};
+
+template <class F>
+void par_for(int n, F f) {
+    SetupPool& pool = SetupPool::get();
+    if (n <= 1 || pool.size() <= 1 || !pool.run(n, f))
+        for (int i = 0; i < n; ++i) f(i);
 }
 
 inline bool is_gp(int kind) { return kind == LBA_MONO_GP || kind == LBA_STEREO_GP; }
@@ -440,6 +531,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             }
             gp_of[i] = g;
         }
+    sub("  GP pair numbering");
 
     // GP pose samples: distinct observation times per GP pair (one per camera time stamp in
     // LocalGPBA), contiguous per pair; observations of a camera with a free extrinsic get samples of
@@ -449,17 +541,37 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     {
         typedef std::pair<double, int> SKey;
         auto skey = [&](const lba_obs& o) { return SKey(o.t, ext_block(o) >= 0 ? o.cam : -1); };
-        std::vector<std::vector<SKey>> ts(gp_a.size());
-        for (int i = 0; i < n_obs; ++i)   // distinct keys per pair are few: keep them unique while short
-            if (is_gp(obs[i].kind)) {
-                std::vector<SKey>& v = ts[gp_of[i]];
-                const SKey k = skey(obs[i]);
-                bool seen = false;
-                if (v.size() <= 16)
-                    for (const SKey& x : v)
-                        if (x == k) { seen = true; break; }
-                if (!seen) v.push_back(k);
-            }
+        // distinct keys per pair are few: each of 8 observation pieces keeps up to KC distinct keys per pair
+        // inline (flat arrays), more in a per-piece overflow list; then per pair the union, sorted
+        const int ng = (int)gp_a.size();
+        constexpr int KC = 16, NPC = 8;
+        std::vector<SKey> pk((size_t)NPC * std::max(ng, 1) * KC);
+        std::vector<int> pc((size_t)NPC * std::max(ng, 1), 0);
+        std::vector<std::vector<std::pair<int, SKey>>> pov(NPC);
+        par_for(NPC, [&](int piece) {
+            SKey* K = pk.data() + (size_t)piece * ng * KC;
+            int* C = pc.data() + (size_t)piece * ng;
+            for (int i = (int)((long long)n_obs * piece / NPC); i < (int)((long long)n_obs * (piece + 1) / NPC); ++i)
+                if (is_gp(obs[i].kind)) {
+                    const int g = gp_of[i];
+                    const SKey k = skey(obs[i]);
+                    SKey* v = K + (size_t)g * KC;
+                    bool seen = false;
+                    for (int c = 0; c < C[g]; ++c)
+                        if (v[c] == k) { seen = true; break; }
+                    if (seen) continue;
+                    if (C[g] < KC) v[C[g]++] = k;
+                    else pov[piece].emplace_back(g, k);
+                }
+        });
+        std::vector<std::vector<SKey>> ts(ng);
+        for (int piece = 0; piece < NPC; ++piece) {
+            const SKey* K = pk.data() + (size_t)piece * ng * KC;
+            const int* C = pc.data() + (size_t)piece * ng;
+            for (int g = 0; g < ng; ++g) ts[g].insert(ts[g].end(), K + (size_t)g * KC, K + (size_t)g * KC + C[g]);
+            for (const auto& e : pov[piece]) ts[e.first].push_back(e.second);
+        }
+        sub("  GP sample keys");
         std::vector<SKey> keys;
         for (size_t g = 0; g < ts.size(); ++g) {
             std::sort(ts[g].begin(), ts[g].end());
@@ -467,6 +579,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             gp_s0[g + 1] = gp_s0[g] + (int)ts[g].size();
             for (const SKey& k : ts[g]) { gps_t.push_back(k.first); gps_cam.push_back(k.second); keys.push_back(k); }
         }
+        sub("  GP sample sort");
         par_for(8, [&](int piece) {
             for (int i = (int)((long long)n_obs * piece / 8); i < (int)((long long)n_obs * (piece + 1) / 8); ++i)
                 if (is_gp(obs[i].kind)) {
@@ -505,12 +618,11 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     std::vector<char> heavy(n_lm, 0);
     constexpr int SETUP_PIECES = 8;   // (fixed: the results do not depend on the thread count)
     par_for(SETUP_PIECES, [&](int piece) {
-        std::vector<int> kl, sl;
+        // distinct pose blocks / samples of a landmark counted by stamping (stamp = landmark + 1)
+        std::vector<int> kst_((size_t)std::max(n_pb, 1), 0), sst_((size_t)std::max(n_gps + n_kfs, 1), 0);
         for (int l = (int)((long long)n_lm * piece / SETUP_PIECES); l < (int)((long long)n_lm * (piece + 1) / SETUP_PIECES); ++l) {
             if (!lm_act[l]) continue;
-            kl.clear();
-            sl.clear();
-            int nr = 0, ne = 0;
+            int nr = 0, ne = 0, npl = 0, ns = 0;
             for (int q = lo0[l]; q < lo0[l + 1]; ++q) {
                 const lba_obs& o = obs[lo_of[q]];
                 const int hb = H[o.kf_b], ha = is_gp(o.kind) ? H[o.kf_a] : -1, hx = ext_block(o);
@@ -519,35 +631,39 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                         lmin[l] = lmin[l] == INT_MAX ? k : std::min(lmin[l], k);
                         lmax[l] = lmax[l] == INT_MAX ? k : std::max(lmax[l], k);
                     }
-                if (hb >= 0) kl.push_back(hb);
-                if (ha >= 0) kl.push_back(ha);
-                if (hx >= 0) kl.push_back(hx);
+                for (int k : {hb, ha, hx})
+                    if (k >= 0 && kst_[k] != l + 1) { kst_[k] = l + 1; ++npl; }
                 ne += (hb >= 0) + (ha >= 0) + (hx >= 0);
                 nr += obs_dim(o.kind);
-                sl.push_back(smp_of[lo_of[q]]);
+                const int sm = smp_of[lo_of[q]];
+                if (sst_[sm] != l + 1) { sst_[sm] = l + 1; ++ns; }
             }
-            std::sort(kl.begin(), kl.end());
-            const int npl = (int)(std::unique(kl.begin(), kl.end()) - kl.begin());
-            std::sort(sl.begin(), sl.end());
-            const int ns = (int)(std::unique(sl.begin(), sl.end()) - sl.begin());
             heavy[l] = !tile_fits(lo0[l + 1] - lo0[l], nr, npl, 1, npl, ns, ne);
         }
     });
     sub("heavy classification");
     std::vector<int> order;
     int n_heavy_lm = 0;
-    {   // stable order by (heavy, lmin, lmax): sort (key, index) records (INT_MAX = observed by fixed KFs only)
-        std::vector<std::pair<unsigned long long, int>> rec;
-        rec.reserve(n_lm);
+    {   // stable order by (heavy, lmin, lmax) (INT_MAX = observed by fixed KFs only, after every block):
+        // three stable counting passes (lmax, lmin, heavy) over the active landmarks in index order
+        auto key = [&](int v) { return v == INT_MAX ? n_pb : v; };
+        std::vector<int> a, b;
+        a.reserve(n_lm);
         for (int l = 0; l < n_lm; ++l)
-            if (lm_act[l]) {
-                rec.emplace_back(((unsigned long long)heavy[l] << 62) | ((unsigned long long)(unsigned)lmin[l] << 31) |
-                                     (unsigned)lmax[l], l);
-                n_heavy_lm += heavy[l];
-            }
-        std::sort(rec.begin(), rec.end());
-        order.reserve(rec.size());
-        for (const auto& r : rec) order.push_back(r.second);
+            if (lm_act[l]) { a.push_back(l); n_heavy_lm += heavy[l]; }
+        b.resize(a.size());
+        std::vector<int> cnt((size_t)std::max(n_pb + 2, 3));
+        auto pass = [&](auto kf, int nk) {
+            std::fill(cnt.begin(), cnt.begin() + nk + 1, 0);
+            for (int l : a) cnt[kf(l) + 1]++;
+            for (int k = 0; k < nk; ++k) cnt[k + 1] += cnt[k];
+            for (int l : a) b[cnt[kf(l)]++] = l;
+            a.swap(b);
+        };
+        pass([&](int l) { return key(lmax[l]); }, n_pb + 1);
+        pass([&](int l) { return key(lmin[l]); }, n_pb + 1);
+        pass([&](int l) { return (int)heavy[l]; }, 2);
+        order.swap(a);
     }
     const int nl = (int)order.size(), n_reg = nl - n_heavy_lm;
     p->n_lm_dev = nl;
@@ -558,11 +674,13 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     sub("landmark order");
     // observations grouped by device landmark (stable)
     std::vector<int> lobs0(nl + 1, 0), obs_of(n_obs);
-    for (int d = 0; d < nl; ++d) {
-        const int l = order[d];
-        lobs0[d + 1] = lobs0[d] + (lo0[l + 1] - lo0[l]);
-        std::copy(lo_of.begin() + lo0[l], lo_of.begin() + lo0[l + 1], obs_of.begin() + lobs0[d]);
-    }
+    for (int d = 0; d < nl; ++d) lobs0[d + 1] = lobs0[d] + (lo0[order[d] + 1] - lo0[order[d]]);
+    par_for(SETUP_PIECES, [&](int piece) {
+        for (int d = (int)((long long)nl * piece / SETUP_PIECES); d < (int)((long long)nl * (piece + 1) / SETUP_PIECES); ++d) {
+            const int l = order[d];
+            std::copy(lo_of.begin() + lo0[l], lo_of.begin() + lo0[l + 1], obs_of.begin() + lobs0[d]);
+        }
+    });
 
     sub("obs by landmark");
     // (KF, landmark) pairs, per device landmark, ascending pose block
@@ -992,7 +1110,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     std::vector<int> ob_meta(n_obs), ob_kfa(n_obs), ob_kfb(n_obs), ob_smp(n_obs), ob_lm(n_obs);
     std::vector<double> ob_z(3 * (size_t)n_obs), ob_w(n_obs);
     p->obs_dev.assign(n_obs, -1);
-    for (int q = 0; q < n_obs; ++q) {
+    par_for(SETUP_PIECES, [&](int piece) {
+    for (int q = (int)((long long)n_obs * piece / SETUP_PIECES); q < (int)((long long)n_obs * (piece + 1) / SETUP_PIECES); ++q) {
         const lba_obs& o = obs[obs_of[q]];
         p->obs_dev[obs_of[q]] = q;
         ob_meta[q] = o.kind | (o.cam << 4);
@@ -1003,6 +1122,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         ob_z[3 * (size_t)q] = o.z[0]; ob_z[3 * (size_t)q + 1] = o.z[1]; ob_z[3 * (size_t)q + 2] = o.z[2];
         ob_w[q] = o.w;
     }
+    });
     // cameras: Tcb = Tbc^-1 as matrix (MultiKeyFrame::mTbc[c].cast<double>() normalises) and the
     // extrinsic factor Ad(Tbc) (lba::cam_record)
     std::vector<double> camd(CAMD_STRIDE * (size_t)std::max(n_cam, 1), 0.0);
@@ -1438,6 +1558,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         D.lbuf[s] = p->lst[s];
     }
     HIPCHK(hipMemset(D.ctl, 0, sizeof(LMCtl)));
+    HIPCHK(hipStreamSynchronize(p->stream));   // the staged uploads (dupload) have landed
     mark("solve layout");
     p->cur = 0;
     p->has_problem = true;
@@ -1819,6 +1940,8 @@ void lba_destroy(lba_problem* p) {
         if (e) (void)hipEventDestroy(e);
     for (auto& e : p->qev)
         if (e) (void)hipEventDestroy(e);
+    for (auto& a : p->pin_chunks) (void)hipHostFree(a.ptr);
+    p->pin_chunks.clear();
     if (p->h_fin) (void)hipHostFree(p->h_fin);
     if (p->h_log) (void)hipHostFree(p->h_log);
     if (p->d_status) (void)hipFree(p->d_status);

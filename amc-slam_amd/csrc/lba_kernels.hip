@@ -1181,7 +1181,7 @@ __device__ __forceinline__ void piv_update(double (&row)[CNB], const double (&cb
 
 template <int J, int E>
 __device__ __forceinline__ void piv_seq(double (&row)[CNB], double r, int lane, bool& bad) {
-    static_assert(E - 16 <= J && J < E && E % 16 == 0 || J >= E, "pivot halves are 16 columns");
+    static_assert((E - 16 <= J && J < E && E % 16 == 0) || J >= E, "pivot halves are 16 columns");
     if constexpr (J < E) {
         Pivot x;
         x.lij = row[J] * r;   // lane J: sqrt(d); lanes > J: L(l, J)
