@@ -76,6 +76,10 @@ struct lba_problem {
     // of the preprocessing; the next set_problem reuses it after its stream synchronisation
     std::vector<Alloc> pin_chunks;
     size_t pin_chunk = 0, pin_off = 0;
+    // observation-sized host scratch arrays of set_problem, kept between calls: resizing to the same
+    // length touches nothing (no allocation, page faults or zeroing per window; every element is written)
+    std::vector<int> scr_i[16];
+    std::vector<double> scr_d[2];
     double* h_fin = nullptr;      // host-mapped coherent [HFIN_DOUBLES]: trial summary [4], sequence
                                   // number [4], LMCtl mirror [8..] (queued optimisation)
     double* d_hfin = nullptr;     // its device address
@@ -257,7 +261,14 @@ T* dupload(lba_problem* p, const std::vector<T>& v) {
     if (!v.empty()) {
         const size_t bytes = v.size() * sizeof(T);
         void* st = pin_stage(p, bytes);
-        std::memcpy(st, v.data(), bytes);
+        if (bytes >= ((size_t)1 << 19)) {   // large arrays: the copy into pinned memory in 8 pieces
+            par_for(8, [&](int piece) {
+                const size_t b0 = bytes * piece / 8, b1 = bytes * (piece + 1) / 8;
+                std::memcpy(static_cast<char*>(st) + b0, reinterpret_cast<const char*>(v.data()) + b0, b1 - b0);
+            });
+        } else {
+            std::memcpy(st, v.data(), bytes);
+        }
         HIPCHK(hipMemcpyAsync(d, st, bytes, hipMemcpyHostToDevice, p->stream));
     }
     return d;
@@ -391,6 +402,16 @@ bool inverse6(const double* A, double* R) {
 inline int ublock_id(int n_pb, int bi, int bj) { return bi * n_pb - bi * (bi - 1) / 2 + (bj - bi); }
 
 // ------------------------------------------------------------------------------------------------
+// scratch array k of set_problem, n elements (contents unspecified: the caller writes every element)
+std::vector<int>& scr_int(lba_problem* p, int k, size_t n) {
+    p->scr_i[k].resize(n);
+    return p->scr_i[k];
+}
+std::vector<double>& scr_dbl(lba_problem* p, int k, size_t n) {
+    p->scr_d[k].resize(n);
+    return p->scr_d[k];
+}
+
 int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xyz, int n_lm, const lba_obs* obs,
                 int n_obs, const lba_prior* priors, int n_priors, const int32_t* vel_kfs, int n_vel,
                 const lba_cam* cams, int n_cam) {
@@ -399,7 +420,27 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     if ((n_kf && !kfs) || (n_lm && !lm_xyz) || (n_obs && !obs) || (n_priors && !priors) || (n_vel && !vel_kfs) ||
         (n_cam && !cams))
         throw ApiError{LBA_E_ARG, "null array with non-zero size"};
-    for (int i = 0; i < n_obs; ++i) {
+    // the first invalid observation (pieces in parallel; the serial pass below names it)
+    int first_bad = n_obs;
+    {
+        constexpr int VP = 8;
+        int bad_at[VP];
+        par_for(VP, [&](int piece) {
+            const int i0 = (int)((long long)n_obs * piece / VP), i1 = (int)((long long)n_obs * (piece + 1) / VP);
+            bad_at[piece] = n_obs;
+            for (int i = i0; i < i1; ++i) {
+                const lba_obs& o = obs[i];
+                bool ok = o.kind >= LBA_MONO_GP && o.kind <= LBA_STEREO && o.kf_b >= 0 && o.kf_b < n_kf && o.lm >= 0 &&
+                          o.lm < n_lm && o.cam >= 0 && o.cam < n_cam && o.cam <= 255;
+                if (ok && (o.kind == LBA_MONO_GP || o.kind == LBA_STEREO_GP))
+                    ok = o.kf_a >= 0 && o.kf_a < n_kf && o.kf_a != o.kf_b &&
+                         std::fabs(kfs[o.kf_b].time - kfs[o.kf_a].time) > 1e-6;
+                if (!ok) { bad_at[piece] = i; break; }
+            }
+        });
+        for (int piece = 0; piece < VP; ++piece) first_bad = std::min(first_bad, bad_at[piece]);
+    }
+    for (int i = first_bad; i < n_obs; ++i) {
         const lba_obs& o = obs[i];
         if (o.kind < LBA_MONO_GP || o.kind > LBA_STEREO) throw ApiError{LBA_E_ARG, "obs " + std::to_string(i) + ": bad kind"};
         if (o.kf_b < 0 || o.kf_b >= n_kf || o.lm < 0 || o.lm >= n_lm || o.cam < 0 || o.cam >= n_cam || o.cam > 255)
@@ -593,7 +634,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     sub("GP pairs + samples");
     // pose sample of every observation: its GP sample, or the KF pose record n_gps + kf_b
     const int n_gps = (int)gps_t.size(), n_smp = n_gps + n_kfs;
-    std::vector<int> smp_of(n_obs);
+    std::vector<int>& smp_of = scr_int(p, 0, n_obs);
     for (int i = 0; i < n_obs; ++i) smp_of[i] = is_gp(obs[i].kind) ? sample_of[i] : n_gps + obs[i].kf_b;
 
     // ---- heavy landmarks: a landmark whose observations / keyframes exceed one tile of k_lin_schur (a
@@ -606,7 +647,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                ns <= TILE_SMP && ne <= TILE_PROWS;
     };
     // observations by original landmark (stable)
-    std::vector<int> lo0(n_lm + 1, 0), lo_of(n_obs);
+    std::vector<int> lo0(n_lm + 1, 0);
+    std::vector<int>& lo_of = scr_int(p, 1, n_obs);
     for (int i = 0; i < n_obs; ++i) lo0[obs[i].lm + 1]++;
     for (int l = 0; l < n_lm; ++l) lo0[l + 1] += lo0[l];
     {
@@ -673,7 +715,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
 
     sub("landmark order");
     // observations grouped by device landmark (stable)
-    std::vector<int> lobs0(nl + 1, 0), obs_of(n_obs);
+    std::vector<int> lobs0(nl + 1, 0);
+    std::vector<int>& obs_of = scr_int(p, 2, n_obs);
     for (int d = 0; d < nl; ++d) lobs0[d + 1] = lobs0[d] + (lo0[order[d] + 1] - lo0[order[d]]);
     par_for(SETUP_PIECES, [&](int piece) {
         for (int d = (int)((long long)nl * piece / SETUP_PIECES); d < (int)((long long)nl * (piece + 1) / SETUP_PIECES); ++d) {
@@ -743,7 +786,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     {
         // per observation in device order, what the tiling reads (contiguous instead of through obs_of):
         // pose blocks of KF b / KF a / the extrinsic (-1: none or fixed), rows, pose sample
-        std::vector<int> dhb(n_obs), dha(n_obs), dhx(n_obs), ddim(n_obs), dsmp(n_obs);
+        std::vector<int>&dhb = scr_int(p, 3, n_obs), &dha = scr_int(p, 4, n_obs), &dhx = scr_int(p, 5, n_obs),
+                         &ddim = scr_int(p, 6, n_obs), &dsmp = scr_int(p, 7, n_obs);
         par_for(SETUP_PIECES, [&](int piece) {
             for (int q = (int)((long long)n_obs * piece / SETUP_PIECES); q < (int)((long long)n_obs * (piece + 1) / SETUP_PIECES); ++q) {
                 const lba_obs& ob = obs[obs_of[q]];
@@ -801,13 +845,26 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             TileOut& T = outs[piece];
             const int d_end = (int)((long long)n_reg * (piece + 1) / n_pieces);
             int d = (int)((long long)n_reg * piece / n_pieces);
-            std::vector<unsigned long long> tob;
             // the tile's sample / KF sets grow by the landmark's new elements, found through membership
             // marks (1: in the tile, 2: new for the landmark being tried); uni is sorted once the tile closes
             std::vector<int> uni, usm, new_s, new_k;
             std::vector<char> kmark((size_t)std::max(n_pb, 1), 0), smark((size_t)std::max(n_smp, 1), 0);
+            std::vector<int> sloc_v((size_t)std::max(n_smp, 1), 0);   // sample -> its rank in the closed tile
+            int* sloc = sloc_v.data();
+            int srows[TILE_SMP + 1];
             uni.reserve(TILE_PAIRS + 8);
             usm.reserve(TILE_SMP + 8);
+            {   // capacity for the piece's share of the outputs (no regrowth while tiling)
+                const int no_p = lobs0[d_end] - lobs0[d], np_p = lm_pair0[d_end] - lm_pair0[d];
+                const int nt_est = no_p / 64 + 8;
+                T.pair_rows.reserve((size_t)np_p * 4 + 16);
+                T.lm_rows.reserve((size_t)no_p * 3 + 16);
+                T.tsm_smp.reserve((size_t)nt_est * TILE_SMP / 2);
+                T.tsm_rows.reserve((size_t)nt_est * TILE_SMP / 2);
+                T.sent_l1.reserve((size_t)nt_est * 48); T.sent_l2.reserve((size_t)nt_est * 48);
+                T.sent_k1.reserve((size_t)nt_est * 48); T.sent_k2.reserve((size_t)nt_est * 48);
+                T.tkf_list.reserve((size_t)nt_est * TILE_KF);
+            }
             while (d < d_end) {
                 int nobs = 0, rows = 0, npair = 0, nlmt = 0, nent = 0;
                 uni.clear();
@@ -844,30 +901,32 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 for (int v : usm) smark[v] = 0;
                 for (int k : uni) kmark[k] = 0;
                 std::sort(uni.begin(), uni.end());
+                std::sort(usm.begin(), usm.end());
+                for (size_t i = 0; i < usm.size(); ++i) sloc[usm[i]] = (int)i;
                 T.t_obs0.push_back(lobs0[d]); T.t_nobs.push_back(nobs);
                 T.t_lm0.push_back(d); T.t_nlm.push_back(nlmt);
                 T.t_pair0.push_back(lm_pair0[d]); T.t_npair.push_back(npair);
                 T.t_kf0.push_back((int)T.tkf_list.size()); T.t_nkf.push_back((int)uni.size());
                 for (int k : uni) T.tkf_list.push_back(k);
                 auto local = [&](int k) { return (int)(std::lower_bound(uni.begin(), uni.end(), k) - uni.begin()); };
-                // LDS rows grouped by pose sample: every sample of the tile owns one contiguous row run
-                tob.clear();
-                for (int q = lobs0[d]; q < lobs0[e]; ++q)
-                    tob.push_back(((unsigned long long)(unsigned)dsmp[q] << 32) | (unsigned)q);
-                std::sort(tob.begin(), tob.end());
+                // LDS rows grouped by pose sample: every sample of the tile owns one contiguous row run, the
+                // samples ascending, observations ascending within a sample (a counting pass over the
+                // tile's sorted sample list)
                 T.t_smp0.push_back((int)T.tsm_smp.size());
-                int row = 0;
-                for (size_t i = 0; i < tob.size();) {
-                    const int sm = (int)(tob[i] >> 32), r0 = row;
-                    size_t j = i;
-                    for (; j < tob.size() && (int)(tob[j] >> 32) == sm; ++j) {
-                        const int q = (int)(tob[j] & 0xffffffffu);
-                        ob_row[q] = row;
-                        row += ddim[q];
+                {
+                    const int ns = (int)usm.size();
+                    std::fill(srows, srows + ns + 1, 0);
+                    for (int q = lobs0[d]; q < lobs0[e]; ++q) srows[sloc[dsmp[q]] + 1] += ddim[q];
+                    for (int i = 0; i < ns; ++i) srows[i + 1] += srows[i];
+                    for (int i = 0; i < ns; ++i) {
+                        T.tsm_smp.push_back(usm[i]);
+                        T.tsm_rows.push_back(srows[i] | ((srows[i + 1] - srows[i]) << 16));
                     }
-                    T.tsm_smp.push_back(sm);
-                    T.tsm_rows.push_back(r0 | ((row - r0) << 16));
-                    i = j;
+                    for (int q = lobs0[d]; q < lobs0[e]; ++q) {
+                        const int i = sloc[dsmp[q]];
+                        ob_row[q] = srows[i];
+                        srows[i] += ddim[q];
+                    }
                 }
                 T.t_nsmp.push_back((int)T.tsm_smp.size() - T.t_smp0.back());
                 // entry lists per pair, row lists per landmark, the pairs' tile-local (KF, landmark);
@@ -1104,11 +1163,13 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         hv_ss0.push_back((int)hv_sslot.size());
     }
     const int n_hslots = hs0[n_ublocks], n_gslots = gs0[n_pb], n_sslots = ss0[n_ublocks], n_gpslots = gps0[n_pb];
+    sub("slab slots");
 
 
     // ---- observations in device order
-    std::vector<int> ob_meta(n_obs), ob_kfa(n_obs), ob_kfb(n_obs), ob_smp(n_obs), ob_lm(n_obs);
-    std::vector<double> ob_z(3 * (size_t)n_obs), ob_w(n_obs);
+    std::vector<int>&ob_meta = scr_int(p, 8, n_obs), &ob_kfa = scr_int(p, 9, n_obs), &ob_kfb = scr_int(p, 10, n_obs),
+                     &ob_smp = scr_int(p, 11, n_obs), &ob_lm = scr_int(p, 12, n_obs);
+    std::vector<double>&ob_z = scr_dbl(p, 0, 3 * (size_t)n_obs), &ob_w = scr_dbl(p, 1, n_obs);
     p->obs_dev.assign(n_obs, -1);
     par_for(SETUP_PIECES, [&](int piece) {
     for (int q = (int)((long long)n_obs * piece / SETUP_PIECES); q < (int)((long long)n_obs * (piece + 1) / SETUP_PIECES); ++q) {
@@ -1123,6 +1184,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         ob_w[q] = o.w;
     }
     });
+    sub("device-order observations");
     // cameras: Tcb = Tbc^-1 as matrix (MultiKeyFrame::mTbc[c].cast<double>() normalises) and the
     // extrinsic factor Ad(Tbc) (lba::cam_record)
     std::vector<double> camd(CAMD_STRIDE * (size_t)std::max(n_cam, 1), 0.0);
@@ -1188,9 +1250,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.n_cam = n_cam; D.n_entries = n_entries; D.n_sentries = n_sent; D.n_ublocks = n_ublocks;
     D.ob_meta = dupload(p, ob_meta); D.ob_kfa = dupload(p, ob_kfa); D.ob_kfb = dupload(p, ob_kfb);
     D.ob_smp = dupload(p, ob_smp); D.ob_lm = dupload(p, ob_lm);
-    std::vector<int> ob_row_dev(n_obs);
-    for (int q = 0; q < n_obs; ++q) ob_row_dev[q] = ob_row[q];
-    D.ob_row = dupload(p, ob_row_dev);
+    D.ob_row = dupload(p, ob_row);
     D.ob_z = dupload(p, ob_z); D.ob_w = dupload(p, ob_w);
     D.gp_s0 = dupload(p, gp_s0); D.gps_t = dupload(p, gps_t); D.n_gps = n_gps; D.n_smp = n_smp;
     D.kf_hidx = dupload(p, p->kf_hidx); D.gp_kfa = dupload(p, gp_a); D.gp_kfb = dupload(p, gp_b);
