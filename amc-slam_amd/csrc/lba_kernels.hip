@@ -1164,7 +1164,11 @@ __device__ __forceinline__ void piv_update(double (&row)[CNB], const double (&cb
     constexpr int NF = E - 1 - J;
     auto step = [&](auto tc) {
         constexpr int t = decltype(tc)::value;
+#ifdef LBA_EXP_NO_UPDATE   // (micro-benchmark experiments only: the chain alone)
+        if constexpr (false) {
+#else
         if constexpr (t < NF) {
+#endif
 #if LBA_CHOL_DPP
             (void)cb;
             fmac_bcast<J + 1 + t>(row[J + 1 + t], rep, x.lij);

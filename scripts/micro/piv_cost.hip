@@ -58,7 +58,7 @@ __global__ __launch_bounds__(64) void k_ops(double* out, unsigned long long* cyc
 __global__ __launch_bounds__(64) void k_factor(const double* A, double* out, unsigned long long* cyc, int reps) {
     __shared__ double st[2 * lba::CNB][lba::CNB + 1];
     const int lane = threadIdx.x;
-    unsigned long long tot = 0;
+    unsigned long long tot = 0, h1 = 0, cr = 0;
     for (int rp = 0; rp < reps; ++rp) {
         for (int c = 0; c < lba::CNB; ++c) st[lane][c] = A[lane * lba::CNB + c];
         lba::wave_sync();
@@ -69,15 +69,22 @@ __global__ __launch_bounds__(64) void k_factor(const double* A, double* out, uns
         lba::pin(row[0]);
         const unsigned long long c0 = clock64();
         lba::piv_seq<0, 16>(row, lba::readlane_d(lba::rsqrt_nr(row[0]), 0), lane, bad);
+        lba::pin(row[15]);
+        const unsigned long long c1 = clock64();
         lba::cross_update(row, st, lane);
+        lba::pin(row[16]);
+        const unsigned long long c2 = clock64();
         lba::piv_seq<16, lba::CNB>(row, lba::readlane_d(lba::rsqrt_nr(row[16]), 16), lane, bad);
         lba::pin(row[31]);
-        tot += clock64() - c0;
+        const unsigned long long c3 = clock64();
+        tot += c3 - c0;
+        h1 += c1 - c0;
+        cr += c2 - c1;
 #pragma unroll
         for (int c = 0; c < lba::CNB; ++c) out[lane * lba::CNB + c] = row[c];
         if (bad) out[0] = -1.0;
     }
-    if (lane == 0) cyc[0] = tot / reps;
+    if (lane == 0) { cyc[0] = tot / reps; cyc[1] = h1 / reps; cyc[2] = cr / reps; }
 }
 }  // namespace
 
@@ -105,13 +112,20 @@ int main() {
     for (int rep = 0; rep < 3; ++rep) {
         k_factor<<<1, 64>>>(A, F, cyc, 20);
         (void)hipDeviceSynchronize();
-        (void)hipMemcpy(hc, cyc, 8, hipMemcpyDeviceToHost);
-        printf("stacked factor (DPP=%d): %llu cycles\n", LBA_CHOL_DPP, hc[0]);
+        (void)hipMemcpy(hc, cyc, 24, hipMemcpyDeviceToHost);
+        printf("stacked factor (DPP=%d%s): %llu cycles (first half %llu, cross update %llu)\n", LBA_CHOL_DPP,
+#ifdef LBA_EXP_NO_UPDATE
+               " chain only",
+#else
+               "",
+#endif
+               hc[0], hc[1], hc[2]);
     }
     double f[64 * 32];
     (void)hipMemcpy(f, F, sizeof f, hipMemcpyDeviceToHost);
     double cs = 0;
     for (int i = 0; i < 64 * 32; ++i) cs += f[i] * (1 + (i % 7));
     printf("checksum %.17g\n", cs);
+
     return 0;
 }
