@@ -19,6 +19,7 @@ import argparse
 import glob
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -98,6 +99,33 @@ def pmc_traffic(workload, kernel="k_lin_schur"):
     return None
 
 
+def cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline_omp(config, seconds, threads):
+    """The same oracle built with OpenMP (oracle/_build/liblba_oracle_omp.so: the per-edge error and
+    Jacobian passes, the landmark inverses, the Schur complement by pose-block rows and the landmark
+    back-substitution on `threads` threads, like g2o's G2O_USE_OPENMP build, block_solver.hpp:378-380,527;
+    the dense LDLT stays serial as Eigen's is; results bitwise the serial build's), timed in a child
+    process (the other library) on the same window."""
+    env = dict(os.environ, ORC_LIB=os.path.join(ROOT, "oracle", "_build", "liblba_oracle_omp.so"),
+               OMP_NUM_THREADS=str(threads), _BENCH_OMP_CHILD="1")
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--config", config, "--cpu-seconds", str(seconds)],
+                       env=env, capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return {"error": r.stderr[-300:]}
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    d.update({"cores": threads, "kind": "port", "cpu": cpu_model()})
+    return d
+
+
 def cpu_baseline(win, seconds):
     """The oracle (C restatement of the reference CPU path, single thread, like the reference's
     G2O_USE_OPENMP OFF build) on the same window: a bounded number of LM iterations."""
@@ -112,12 +140,21 @@ def cpu_baseline(win, seconds):
     t = time.perf_counter()
     n_run, _ = o2.optimize(n)
     dt = time.perf_counter() - t
-    return {"value": n_run / dt, "unit": "LM iterations/s", "cores": 1, "kind": "port",
-            "sample": f"{n_run} LM iterations of the same {win.name} window, oracle/lba_oracle.c (-O3, 1 thread), "
-                      f"{dt:.1f} s"}
+    threads = os.environ.get("OMP_NUM_THREADS") if orc.LIB.endswith("_omp.so") else "1"
+    return {"value": n_run / dt, "unit": "LM iterations/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
+            "sample": f"{n_run} LM iterations of the same {win.name} window, oracle/{os.path.basename(orc.LIB)} "
+                      f"(-O3, {threads} thread(s)), {dt:.1f} s"}
 
 
 def main():
+    if os.environ.get("_BENCH_OMP_CHILD"):   # cpu_baseline_omp's child: the oracle alone, one JSON line
+        ap = argparse.ArgumentParser()
+        ap.add_argument("--config", default="cfg1_local_50kf")
+        ap.add_argument("--cpu-seconds", type=float, default=12.0)
+        a, _ = ap.parse_known_args()
+        from amc_lba.synth import make_config_window
+        print(json.dumps(cpu_baseline(make_config_window(a.config), a.cpu_seconds)), flush=True)
+        return
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -310,6 +347,9 @@ def main():
         if not args.no_cpu and world == 1 and not gba:   # (the oracle's dense LDLT of S = 60000^2 is hours)
             line["cpu_baseline"] = cpu_baseline(win, args.cpu_seconds)
             line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
+            # secondary: the OpenMP build of the oracle on this rank's share of the host's cores
+            omp_threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+            line["cpu_baseline_omp"] = cpu_baseline_omp(args.config, args.cpu_seconds, omp_threads)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

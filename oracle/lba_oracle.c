@@ -24,6 +24,9 @@
 
 #include <float.h>
 #include <math.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <stdlib.h>
 #include <string.h>
 
@@ -448,6 +451,8 @@ struct orc_problem {
     int n_pose_blocks, n_lm_blocks;
     /* per-edge errors */
     double* obs_err;   /* [n_obs*3] */
+    double* obs_rho0;  /* [n_obs] robust chi2 of each observation (summed in order after the parallel pass) */
+    double* obs_J;     /* [n_obs*3*JC] Jacobians of the last build_system (filled in parallel, used in order) */
     double* pri_err;   /* [n_prior*12] */
     double* vel_err;   /* [n_vel] */
     /* Hessian (BlockSolver, block_solver.hpp) */
@@ -793,6 +798,8 @@ orc_problem* orc_create(const lba_config* cfg, const lba_kf* kfs, int n_kf, cons
     p->np = 12 * npk + 6 * (np - npk);
     p->nl = 3 * nl;
     p->obs_err = (double*)calloc(3 * (n_obs > 0 ? n_obs : 1), sizeof(double));
+    p->obs_rho0 = (double*)calloc(n_obs > 0 ? n_obs : 1, sizeof(double));
+    p->obs_J = (double*)calloc((size_t)3 * 33 * (n_obs > 0 ? n_obs : 1), sizeof(double));
     p->pri_err = (double*)calloc(12 * (n_priors > 0 ? n_priors : 1), sizeof(double));
     p->vel_err = (double*)calloc((n_vel > 0 ? n_vel : 1), sizeof(double));
     p->Hpp = (double*)calloc((size_t)p->np * p->np + 1, sizeof(double));
@@ -834,7 +841,7 @@ orc_problem* orc_create(const lba_config* cfg, const lba_kf* kfs, int n_kf, cons
 void orc_destroy(orc_problem* p) {
     if (!p) return;
     free(p->kf); free(p->kf_bak); free(p->lm); free(p->lm_bak); free(p->obs); free(p->pri); free(p->vel);
-    free(p->cam); free(p->cam_bak); free(p->poff); free(p->pdim); free(p->kf_hidx); free(p->lm_hidx); free(p->obs_err); free(p->pri_err); free(p->vel_err);
+    free(p->cam); free(p->cam_bak); free(p->poff); free(p->pdim); free(p->kf_hidx); free(p->lm_hidx); free(p->obs_err); free(p->obs_rho0); free(p->obs_J); free(p->pri_err); free(p->vel_err);
     free(p->Hpp); free(p->Hll); free(p->hpl_start); free(p->hpl_pose); free(p->hpl_blk); free(p->b); free(p->x);
     free(p->diag_bak);
     free(p);
@@ -885,14 +892,21 @@ static double compute_errors(orc_problem* p) {
         mat_mul(Oe, p->cam[c].info, e, 3, 3, 1);
         chi += e[0] * Oe[0] + e[1] * Oe[1] + e[2] * Oe[2];
     }
+    /* per observation in parallel (the OpenMP build, liblba_oracle_omp.so: g2o's computeActiveErrors
+     * with G2O_USE_OPENMP, sparse_optimizer.cpp:61-114), then summed in edge order (bitwise the serial
+     * build's result) */
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
     for (int i = 0; i < p->n_obs; ++i) {
         const lba_obs* o = &p->obs[i];
         double* e = p->obs_err + 3 * i;
+        double r3[3];
         obs_error(p, o, e);
-        double c = chi2_of(e, obs_dim(o->kind), o->w);
-        huber(c, obs_delta(p, o->kind), rho);
-        chi += rho[0];
+        huber(chi2_of(e, obs_dim(o->kind), o->w), obs_delta(p, o->kind), r3);
+        p->obs_rho0[i] = r3[0];
     }
+    for (int i = 0; i < p->n_obs; ++i) chi += p->obs_rho0[i];
     return chi;
 }
 
@@ -1000,12 +1014,17 @@ static void build_system(orc_problem* p) {
         mat_mul(g, JT, Oe, 6, 3, 1);
         for (int k = 0; k < 6; ++k) p->b[p->poff[cm->hidx] + k] -= g[k];
     }
+    /* the observations' Jacobians in parallel (the OpenMP build: g2o's linearizeOplus over the active
+     * edges, block_solver.hpp:378-380), then accumulated in edge order (bitwise the serial build's) */
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+    for (int i = 0; i < p->n_obs; ++i) obs_jacobian(p, &p->obs[i], p->obs_J + (size_t)3 * JC * i);
     for (int i = 0; i < p->n_obs; ++i) {
         const lba_obs* o = &p->obs[i];
         int dim = obs_dim(o->kind);
         const double* e = p->obs_err + 3 * i;
-        double J[3 * JC];
-        obs_jacobian(p, o, J);
+        const double* J = p->obs_J + (size_t)3 * JC * i;
         huber(chi2_of(e, dim, o->w), obs_delta(p, o->kind), rho);
         double s = rho[1] * o->w;                    /* robustInformation = rho' * Omega */
         double om_r[3];
@@ -1178,14 +1197,33 @@ static int block_solve(orc_problem* p) {
     double* S = (double*)malloc(sizeof(double) * ((size_t)n * n + 1));
     double* coeff = (double*)calloc(n + 1, sizeof(double));
     double* Dinv = (double*)malloc(sizeof(double) * 9 * (nlb > 0 ? nlb : 1));
+    double* dbl = (double*)malloc(sizeof(double) * 3 * (nlb > 0 ? nlb : 1));
     memcpy(S, p->Hpp, sizeof(double) * (size_t)n * n);   /* Hschur = Hpp (upper blocks used) */
+    /* (the OpenMP build: landmark inverses in parallel; the Schur complement with every pose block row
+     * owned by one thread that walks the landmarks in order, so each entry of S and coeff receives its
+     * terms in the serial order: bitwise the serial build's; block_solver.hpp:381-432,527) */
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+    for (int l = 0; l < nlb; ++l) {
+        inverse3(Dinv + 9 * l, p->Hll + 9 * l);
+        mat_mul(dbl + 3 * l, Dinv + 9 * l, p->b + n + 3 * l, 3, 3, 1);
+    }
+#ifdef _OPENMP
+#pragma omp parallel
+#endif
+    {
+#ifdef _OPENMP
+    const int nth = omp_get_num_threads(), th = omp_get_thread_num();
+#else
+    const int nth = 1, th = 0;
+#endif
     for (int l = 0; l < nlb; ++l) {
         double* Di = Dinv + 9 * l;
-        inverse3(Di, p->Hll + 9 * l);
-        double db[3];
-        mat_mul(db, Di, p->b + n + 3 * l, 3, 3, 1);
+        const double* db = dbl + 3 * l;
         for (int k1 = p->hpl_start[l]; k1 < p->hpl_start[l + 1]; ++k1) {
             int i1 = p->hpl_pose[k1];
+            if (i1 % nth != th) continue;
             const double* Bi = p->hpl_blk + 36 * k1;
             const int d1 = p->pdim[i1], o1 = p->poff[i1];
             double BD[36], Bb[12];
@@ -1204,6 +1242,7 @@ static int block_solve(orc_problem* p) {
             }
         }
     }
+    }
     mirror_upper(S, n);
     double* bs = (double*)malloc(sizeof(double) * (n + 1));
     for (int i = 0; i < n; ++i) bs[i] = p->b[i] - coeff[i];
@@ -1212,6 +1251,9 @@ static int block_solve(orc_problem* p) {
     if (ok) {
         memcpy(p->x, xp, sizeof(double) * n);
         /* landmarks: xl = Dinv (bl - Hpl^T xp) */
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
         for (int l = 0; l < nlb; ++l) {
             double cl[3];
             for (int d = 0; d < 3; ++d) cl[d] = p->b[n + 3 * l + d];
@@ -1227,7 +1269,7 @@ static int block_solve(orc_problem* p) {
             mat_mul(p->x + n + 3 * l, Dinv + 9 * l, cl, 3, 3, 1);
         }
     }
-    free(S); free(coeff); free(Dinv); free(bs); free(xp);
+    free(S); free(coeff); free(Dinv); free(dbl); free(bs); free(xp);
     return ok;
 }
 

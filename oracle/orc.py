@@ -11,7 +11,8 @@ import sys
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "_build", "liblba_oracle.so")
+# ORC_LIB: another build of the oracle (bench.py's OpenMP CPU baseline loads _build/liblba_oracle_omp.so)
+LIB = os.environ.get("ORC_LIB") or os.path.join(HERE, "_build", "liblba_oracle.so")
 sys.path.insert(0, os.path.join(os.path.dirname(HERE), "amc-slam_amd"))
 
 from amc_lba.abi import LbaStats, make_config, ptr  # noqa: E402
