@@ -2365,9 +2365,30 @@ template <int NT>
 __device__ void trial_sums(const DevProblem& P, double* red, double& sa, double& sb, double& sc) {
     const int tid = threadIdx.x;
     const int nc = P.n_tiles + P.n_prior + P.n_vel + P.n_eprior;
+    // (the loads of U strided elements are issued before their additions, out-of-range ones masked: the
+    //  same per-thread order of additions as the plain strided loop, without one round trip per element)
+    constexpr int U = 8;
     double a = 0.0, b = 0.0, c = 0.0;
-    for (int i = tid; i < nc; i += NT) { a += P.chi_lin[i]; b += P.chi_eval[i]; }
-    for (int i = tid; i < P.n_upd_blocks; i += NT) c += P.scale_part[i];
+    for (int i0 = tid; i0 < nc; i0 += U * NT) {
+        double xa[U], xb[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * NT;
+            xa[u] = i < nc ? P.chi_lin[i] : 0.0;
+            xb[u] = i < nc ? P.chi_eval[i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i0 + u * NT < nc) { a += xa[u]; b += xb[u]; }
+    }
+    for (int i0 = tid; i0 < P.n_upd_blocks; i0 += U * NT) {
+        double xc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) xc[u] = i0 + u * NT < P.n_upd_blocks ? P.scale_part[i0 + u * NT] : 0.0;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i0 + u * NT < P.n_upd_blocks) c += xc[u];
+    }
     sa = block_sum<NT>(a, red);
     __syncthreads();
     sb = block_sum<NT>(b, red);
