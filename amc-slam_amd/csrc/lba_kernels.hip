@@ -2153,7 +2153,15 @@ __device__ __attribute__((noinline)) void kf_trial_state(const DevProblem& P, co
 __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lambda_arg, int sel, int gate, int jac) {
     __shared__ double red[UPD_THREADS / 64];
     __shared__ double kab[2][KF_STRIDE];
+    // kf_trial_state's outputs in LDS (one slot per thread): the function stays one compiled body for
+    // both callers (their trial states must agree bitwise) without its output arrays living in scratch
+    __shared__ double kdl[UPD_THREADS][12], knl[UPD_THREADS][KF_STRIDE];
     if (gated_off(P.ctl, gate)) return;
+    // diagnostics (LBA_PHASE_TIMING): s_memrealtime start / end of each workgroup in slots 14 / 15 of the
+    // sweep's stamp rows (k_update runs after the sweep; n_upd_blocks <= n_tiles is checked)
+    unsigned long long* ustamp = (P.tdbg_lin && threadIdx.x == 0 && (int)blockIdx.x < P.n_tiles)
+                                     ? P.tdbg_lin + (size_t)blockIdx.x * 16 + 14 : nullptr;
+    if (ustamp) ustamp[0] = __builtin_amdgcn_s_memrealtime();
     const double lambda = damping(P, lambda_arg);
     const int si = state_idx(P, sel);
     const double* __restrict__ kst = P.kbuf[si];
@@ -2167,14 +2175,14 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
         const int i = blockIdx.x;
         if (threadIdx.x < 2) {
             const int k = threadIdx.x ? P.gp_kfb[i] : P.gp_kfa[i];
-            double d[12];
-            kf_trial_state(P, kst + (size_t)k * KF_STRIDE, P.kf_hidx[k], ok, d, kab[threadIdx.x]);
+            kf_trial_state(P, kst + (size_t)k * KF_STRIDE, P.kf_hidx[k], ok, kdl[threadIdx.x], kab[threadIdx.x]);
         }
         __syncthreads();
 #ifndef LBA_EXP_NO_GPPREP
         gp_pair_prep(P, gps, i, kab[0], kab[1], jac);
 #endif
         if (threadIdx.x == 0) P.scale_part[blockIdx.x] = 0.0;
+        if (ustamp) ustamp[1] = __builtin_amdgcn_s_memrealtime();
         return;
     }
     double sc = 0.0;
@@ -2182,7 +2190,8 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
         const int k = (blockIdx.x - P.n_gp) * UPD_THREADS + threadIdx.x;
         if (k < P.n_kf) {
             const int h = P.kf_hidx[k];
-            double d[12], kn[KF_STRIDE];
+            double* d = kdl[threadIdx.x];
+            double* kn = knl[threadIdx.x];
             kf_trial_state(P, kst + (size_t)k * KF_STRIDE, h, ok, d, kn);
             double* kw = ko + (size_t)k * KF_STRIDE;
             for (int j = 0; j < KF_STRIDE; ++j) kw[j] = kn[j];
@@ -2237,6 +2246,7 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
     }
     const double s = block_sum<UPD_THREADS>(sc, red);
     if (threadIdx.x == 0) P.scale_part[blockIdx.x] = s;
+    if (ustamp) ustamp[1] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ------------------------------------------------------------------------------------------------

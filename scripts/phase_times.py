@@ -89,6 +89,25 @@ def timeline(lin, shape, out):
             out.append(f"   list schedule on {slots} slots, {name}: makespan {fin.max():.2f} us")
 
 
+def update_timeline(lin, n_gp, n_kfb, out):
+    """k_update workgroups of the last launch (slots 14 / 15): GP-pair sample rebuilds, KF blocks,
+    landmark blocks; when each kind ends."""
+    st, en = lin[:, 14], lin[:, 15]
+    ok = (st > 0) & (en > 0)
+    if not ok.any():
+        return
+    t0 = st[ok].min()
+    idx = np.nonzero(ok)[0]
+    s_us, e_us = (st[ok] - t0) / 100.0, (en[ok] - t0) / 100.0
+    out.append(f"== k_update timeline (us): span {e_us.max():.2f}")
+    for name, sel in (("GP pairs", idx < n_gp), ("KF blocks", (idx >= n_gp) & (idx < n_gp + n_kfb)),
+                      ("landmark blocks", idx >= n_gp + n_kfb)):
+        if sel.any():
+            d = e_us[sel] - s_us[sel]
+            out.append(f"   {name:16s} n {sel.sum():5d}  start max {s_us[sel].max():6.2f}  end max {e_us[sel].max():6.2f}  "
+                       f"duration mean {d.mean():6.2f} max {d.max():6.2f}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg1_local_50kf")
@@ -108,6 +127,9 @@ def main():
     report("k_lin_schur (linearisation)", lin, LIN_PHASES, shape, out)
     report("k_lin_schur (elimination)", sch, SCHUR_PHASES, shape, out)
     timeline(lin, shape, out)
+    gp = win.obs["kind"] <= 1   # MONO_GP, STEREO_GP
+    n_gp = len(set(zip(win.obs["kf_a"][gp].tolist(), win.obs["kf_b"][gp].tolist())))
+    update_timeline(lin, n_gp, (len(win.kfs) + 63) // 64, out)
     np.savez_compressed(os.path.splitext(args.out)[0] + "_raw.npz", lin=lin, sch=sch, shape=shape)
     if chol is not None:
         if os.environ.get("LBA_CHOL_STEPS") is None:   # k_chol_flow: s_memrealtime (100 MHz) stamps per panel
