@@ -1780,35 +1780,66 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
         if (kind == 5) {
             // ---------------------------------------------------- band mode, back substitution:
             // x_j = L_jj^-T (y_j - sum_i L(i,j)^T x_i) over the list's rows i > j (completion order);
-            // thread (c, g) takes output c, rows 4g .. 4g + 3 of every term
+            // thread (c, g) takes output c, rows 4g .. 4g + 3 of every term.  Everything that is not an
+            // x_i is fetched first (L_jj^-T into LDS, y_j, the terms' L(i,j) entries into registers: the
+            // factorisation published them long before), so the chain from x_i to x_j is one hand-off,
+            // the dot products and the publication
             const int c = tid & 31, g = tid >> 5;
+            constexpr int MT = 4;   // terms held in registers (the rest are fetched behind their x_i)
+            const int q0 = a.pl0[t], nt = a.pl0[t + 1] - q0;
+            if (!cf_wait(a, a.fready + j, a.dready + j, &s_ok)) return;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {   // L_jj^-T -> Lt[0] (row c of Lt[0] = column c of L_jj^-1)
+                const int e = tid + 256 * m;
+                Lt[0][e >> 5][e & 31] = ld_sc1(a.LinvT + (size_t)j * CNB * CNB + e);
+            }
+            const double yj = tid < CNB ? ld_sc1(a.yv + j * CNB + tid) : 0.0;
+            double lv[MT][4];
+#pragma unroll
+            for (int q = 0; q < MT; ++q)
+                if (q < nt) {
+                    const int ii = a.plist[q0 + q] & 4095;
+                    if (!cf_wait(a, a.lready + tile_id(ii, j), nullptr, &s_ok)) return;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) lv[q][u] = ld_sc1(a.Lm + (size_t)(ii * CNB + 4 * g + u) * n + j * CNB + c);
+                }
             double acc = 0.0;
-            for (int q = a.pl0[t]; q < a.pl0[t + 1]; ++q) {
-                const int ii = a.plist[q] & 4095;
+#pragma unroll
+            for (int q = 0; q < MT; ++q)
+                if (q < nt) {
+                    const int ii = a.plist[q0 + q] & 4095;
+                    if (!cf_wait(a, a.xready + ii, nullptr, &s_ok)) return;
+                    double xi[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) xi[u] = ld_sc1(a.xpos + ii * CNB + 4 * g + u);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) acc += lv[q][u] * xi[u];
+                }
+            for (int q = MT; q < nt; ++q) {
+                const int ii = a.plist[q0 + q] & 4095;
                 if (!cf_wait(a, a.lready + tile_id(ii, j), a.xready + ii, &s_ok)) return;
-                double lv[4], xi[4];
+                double l4[4], xi[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    lv[u] = ld_sc1(a.Lm + (size_t)(ii * CNB + 4 * g + u) * n + j * CNB + c);
+                    l4[u] = ld_sc1(a.Lm + (size_t)(ii * CNB + 4 * g + u) * n + j * CNB + c);
                     xi[u] = ld_sc1(a.xpos + ii * CNB + 4 * g + u);
                 }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) acc += lv[u] * xi[u];
+                for (int u = 0; u < 4; ++u) acc += l4[u] * xi[u];
             }
-            if (!cf_wait(a, a.fready + j, a.dready + j, &s_ok)) return;
             Lt[1][g][c] = acc;
             __syncthreads();
             if (tid < CNB) {
-                double v = ld_sc1(a.yv + j * CNB + tid);
+                double v = yj;
 #pragma unroll
                 for (int u = 0; u < 8; ++u) v -= Lt[1][u][tid];
-                Lt[0][0][tid] = v;
+                Lt[2][0][tid] = v;
             }
             __syncthreads();
             if (tid < CNB) {   // (L_jj^-T v)[c] = sum_r LinvT_j[c][r] v[r]
                 double x = 0.0;
 #pragma unroll 8
-                for (int rr = 0; rr < CNB; ++rr) x += ld_sc1(a.LinvT + (size_t)j * CNB * CNB + tid * CNB + rr) * Lt[0][0][rr];
+                for (int rr = 0; rr < CNB; ++rr) x += Lt[0][tid][rr] * Lt[2][0][rr];
                 st_sc1(a.xpos + j * CNB + tid, x);
                 a.xout[a.rnat[j * CNB + tid]] = x;
             }
