@@ -1759,6 +1759,11 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
                 for (int u = 0; u < 4; ++u) acc += lv[u] * yk[u];
             }
             if (!cf_wait(a, a.fready + i, nullptr, &s_ok)) return;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {   // L_ii^-T -> Lt[2] in one round of loads
+                const int e = tid + 256 * m;
+                Lt[2][e >> 5][e & 31] = ld_sc1(a.LinvT + (size_t)i * CNB * CNB + e);
+            }
             Lt[1][g][r] = acc;
             __syncthreads();
             if (tid < CNB) {
@@ -1771,7 +1776,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
             if (tid < CNB) {   // (L_ii^-1 v)[r] = sum_c LinvT_i[c][r] v[c]
                 double y = 0.0;
 #pragma unroll 8
-                for (int c = 0; c < CNB; ++c) y += ld_sc1(a.LinvT + (size_t)i * CNB * CNB + c * CNB + tid) * Lt[0][0][c];
+                for (int c = 0; c < CNB; ++c) y += Lt[2][c][tid] * Lt[0][0][c];
                 st_sc1(a.yv + i * CNB + tid, y);
             }
             cf_publish(a, a.dready + i);
