@@ -196,11 +196,14 @@ __device__ __forceinline__ double eval_obs(const DevProblem& P, const double* gp
 // doubles each, global or LDS); gps: the sample buffer of that state.
 constexpr int PREP_THREADS = 64;
 constexpr int PREP_SCHUNK = 21;   // samples per pass (3 lanes each; LDS staging of their Jr / Ad blocks)
-__device__ void gp_pair_prep(const DevProblem& P, double* gps, int i, const double* ka, const double* kb, int jac) {
+__device__ void gp_pair_prep(const DevProblem& P, double* gps, int i, const double* ka, const double* kb, int jac,
+                             unsigned long long* pst = nullptr) {
     __shared__ GPPair pr;
     __shared__ double AdI[36], ad2[36], vbs[6];
     __shared__ double sJr[PREP_SCHUNK][36], sRm[PREP_SCHUNK][9], stR[PREP_SCHUNK][9], sg[PREP_SCHUNK][3];
     const int tid = threadIdx.x;
+    // (diagnostics: pst = s_memrealtime stamps after each phase, thread 0)
+#define PREP_STAMP(k) do { if (pst && tid == 0) pst[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
     if (tid == 0) {
         const SE3 Ta = load_se3(ka), Tb = load_se3(kb);
         pr.T1q[0] = Ta.q.x; pr.T1q[1] = Ta.q.y; pr.T1q[2] = Ta.q.z; pr.T1q[3] = Ta.q.w;
@@ -213,6 +216,7 @@ __device__ void gp_pair_prep(const DevProblem& P, double* gps, int i, const doub
     }
     if (tid < 6) vbs[tid] = kb[7 + tid];
     __syncthreads();
+    PREP_STAMP(0);
     if (tid == 0) {
         right_jac_inv(pr.xi12, pr.G2a);                 // C = Jr^-1(xi12)
     } else if (jac && tid == 1) {
@@ -222,6 +226,7 @@ __device__ void gp_pair_prep(const DevProblem& P, double* gps, int i, const doub
         se3_ad(vbs, ad2);
     }
     __syncthreads();
+    PREP_STAMP(1);
     if (tid < 6) {                                      // w2 = Jr^-1(xi12) v2
         double w = 0.0;
         for (int l = 0; l < 6; ++l) w += pr.G2a[tid * 6 + l] * vbs[l];
@@ -234,6 +239,7 @@ __device__ void gp_pair_prep(const DevProblem& P, double* gps, int i, const doub
         pr.G1a[tid] = -v;
     }
     __syncthreads();
+    PREP_STAMP(2);
     if (jac)
         for (int t = tid; t < 72; t += PREP_THREADS) {   // B1 = -1/2 ad(v2) A1, D = -1/2 ad(v2) C
             const int e = t % 36, r = e / 6, c = e % 6;
@@ -243,6 +249,7 @@ __device__ void gp_pair_prep(const DevProblem& P, double* gps, int i, const doub
             (t < 36 ? pr.G1b : pr.G2b)[e] = v * -0.5;
         }
     __syncthreads();
+    PREP_STAMP(3);
     for (int c0 = P.gp_s0[i]; c0 < P.gp_s0[i + 1]; c0 += PREP_SCHUNK) {
         const int ns = min(PREP_SCHUNK, P.gp_s0[i + 1] - c0);
         // three lanes per sample, each one of the independent transcendental chains: the interpolated
@@ -280,6 +287,7 @@ __device__ void gp_pair_prep(const DevProblem& P, double* gps, int i, const doub
             }
         }
         __syncthreads();
+    PREP_STAMP(4);
         if (jac)
             for (int t = tid; t < ns * 36; t += PREP_THREADS) {   // one (row, column) of each N block
                 const int sl = t / 36, r = (t % 36) / 6, c = t % 6;
@@ -303,7 +311,9 @@ __device__ void gp_pair_prep(const DevProblem& P, double* gps, int i, const doub
                 N[(18 + c) * 6 + r] = l2 * nc;
             }
         __syncthreads();
+    PREP_STAMP(5);
     }
+#undef PREP_STAMP
 }
 
 // KF k's pose record (k_depth) and the KF's pose sample (its constant N was uploaded once)
@@ -2215,7 +2225,7 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
         }
         __syncthreads();
 #ifndef LBA_EXP_NO_GPPREP
-        gp_pair_prep(P, gps, i, kab[0], kab[1], jac);
+        gp_pair_prep(P, gps, i, kab[0], kab[1], jac, ustamp ? P.tdbg_lin + (size_t)blockIdx.x * 16 + 5 : nullptr);
 #endif
         if (threadIdx.x == 0) P.scale_part[blockIdx.x] = 0.0;
         if (ustamp) ustamp[1] = __builtin_amdgcn_s_memrealtime();

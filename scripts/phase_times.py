@@ -100,6 +100,14 @@ def update_timeline(lin, n_gp, n_kfb, out):
     idx = np.nonzero(ok)[0]
     s_us, e_us = (st[ok] - t0) / 100.0, (en[ok] - t0) / 100.0
     out.append(f"== k_update timeline (us): span {e_us.max():.2f}")
+    gpi = idx[idx < n_gp]
+    if len(gpi) and (lin[gpi, 5] > 0).all():   # GP-pair rebuild phases (gp_pair_prep stamps, slots 5..10)
+        cols = [14, 5, 6, 7, 8, 9, 10, 15]
+        names = ["KF trial states + log(T12)", "Jr^-1 | exp(xi12) | ad(v2)", "w2, A1", "B1, D",
+                 "sample roles (pose | Jr | Ad)", "N blocks", "tail"]
+        d = np.diff(lin[np.ix_(gpi, cols)].astype(np.int64), axis=1) / 100.0
+        out.append("   GP-pair rebuild phases (us, mean / max): " +
+                   "; ".join(f"{nm} {d[:, k].mean():.2f} / {d[:, k].max():.2f}" for k, nm in enumerate(names)))
     for name, sel in (("GP pairs", idx < n_gp), ("KF blocks", (idx >= n_gp) & (idx < n_gp + n_kfb)),
                       ("landmark blocks", idx >= n_gp + n_kfb)):
         if sel.any():
