@@ -230,8 +230,8 @@ def main():
     setup_done.set()
 
     # warmup (not timed)
+    sinfo = prob.solver_info()   # (panels, envelope tiles, band mode: the solve's FLOP count below)
     if args.warmup > 0:
-        sinfo = prob.solver_info()   # (panels, envelope tiles, band mode: the solve's FLOP count below)
         prob.optimize(args.warmup)
     torch.cuda.synchronize()
     if world > 1:

@@ -13,7 +13,7 @@ timeout -k 10 400 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/$TA
 rc=$?; echo "smoke rc=$rc" | tee -a "$OUT/$TAG.status"
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  timeout -k 10 900 python -m pytest ${TESTS:-tests} -m gpu -q -rf --timeout 600 > "$OUT/$TAG.pytest_gpu.log" 2>&1
+  timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -q -rf --durations=40 --timeout 600 --timeout-method thread > "$OUT/$TAG.pytest_gpu.log" 2>&1
   rc=$?; echo "pytest rc=$rc" | tee -a "$OUT/$TAG.status"
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 fi

@@ -53,8 +53,12 @@ def _host_exchange(wins, infos, states):
     return out
 
 
-def test_farm_two_windows_exchange_matches_oracle():
-    wins, infos = farm.make_farm_windows(SHAPE, 2, seed=5, stride=STRIDE)
+@pytest.mark.parametrize("config,seed,stride", [(SHAPE, 5, STRIDE), ("cfg1_local_50kf", 20250912, 25)],
+                         ids=["small", "cfg1_windows"])
+def test_farm_two_windows_exchange_matches_oracle(config, seed, stride):
+    """small: 12-KF windows; cfg1_windows: BASELINE config 3's per-rank shape (two config-1 windows,
+    50 optimisable KFs each, stride 25 so neighbours share half their keyframes and landmarks)."""
+    wins, infos = farm.make_farm_windows(config, 2, seed=seed, stride=stride)
     assert all((np.diff(w.lm_gid) > 0).all() and (np.diff(w.kf_gid) > 0).all() for w in wins)
     g = Group(2)
     probs = [Problem(w, early_stop=0) for w in wins]

@@ -123,6 +123,32 @@ def test_cfg1_full_size_linearize_and_step_parity():
     assert _rel(dx[p.pose_dim:], dx_o[p.pose_dim:]) <= 1e-6
 
 
+def test_cfg1_full_size_optimize_matches_oracle():
+    """BASELINE config 1 end to end: the reference's optimize(10) loop
+    (Thirdparty/g2o/g2o/core/optimization_algorithm_levenberg.cpp:61-169, early stop disabled so
+    all ten iterations run) on the GPU against the oracle: iterations, trials, chi2, keyframe
+    poses / velocities and landmarks."""
+    win = make_config_window("cfg1_local_50kf")
+    o = orc.Oracle(win, early_stop=0)
+    n_o, st_o = o.optimize(10)
+    kf_o, lm_o = o.state()
+    p = Problem(win, early_stop=0)
+    n, st = p.optimize(10)
+    kf, lm = p.state()
+    assert n == n_o == 10
+    assert st.trials == st_o.trials
+    assert st.result == st_o.result
+    assert abs(st.chi2_initial - st_o.chi2_initial) <= 1e-9 * st_o.chi2_initial
+    assert abs(st.chi2_final - st_o.chi2_final) <= 1e-7 * st_o.chi2_final
+    assert _rel(kf["t"], kf_o["t"]) <= 1e-6
+    assert _rel(kf["vel"], kf_o["vel"]) <= 1e-6
+    q, qo = kf["q"] * np.sign(kf["q"][:, 3:4]), kf_o["q"] * np.sign(kf_o["q"][:, 3:4])
+    assert np.abs(q - qo).max() <= 1e-7
+    assert _rel(lm, lm_o) <= 1e-6
+    _, c2, ok = p.eval()
+    np.testing.assert_array_equal(ok, o.depth_ok())
+
+
 def test_cfg1_full_size_lm_properties():
     win = make_config_window("cfg1_local_50kf")
     p = Problem(win, early_stop=0)
