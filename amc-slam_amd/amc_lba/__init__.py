@@ -91,7 +91,7 @@ def lib():
 
 
 def exported_symbols():
-    return ["lba_abi_version", "lba_create", "lba_destroy", "lba_last_error", "lba_set_config", "lba_set_problem",
+    return ["lba_abi_version", "lba_live_problems", "lba_create", "lba_destroy", "lba_last_error", "lba_set_config", "lba_set_problem",
             "lba_optimize", "lba_get_state", "lba_set_state", "lba_eval", "lba_trial_chi2", "lba_linearize", "lba_solve_step",
             "lba_pose_dim", "lba_set_partition", "lba_rccl_unique_id", "lba_set_partition_rccl", "lba_group_create",
             "lba_group_destroy", "lba_set_partition_group", "lba_get_cams", "lba_set_farm", "lba_set_farm_rccl",

@@ -368,6 +368,7 @@ def map_lib():
                                        ctypes.POINTER(LbamapBAResult)]
         L.lbamap_kf_gba.argtypes = [vp, ctypes.c_int64, vp, vp, vp, ctypes.POINTER(ctypes.c_uint64)]
         L.lbamap_mp_gba.argtypes = [vp, ctypes.c_int64, vp, ctypes.POINTER(ctypes.c_uint64)]
+        L.lbamap_global_ba_thread.argtypes = [vp, ctypes.c_int32, vp, ctypes.c_uint64]
         L.lbamap_build_ba_window.argtypes = [vp, ctypes.POINTER(ctypes.c_int32)] + [vp] * 9 + [ctypes.POINTER(LbaConfig)]
         _lib = L
     return _lib
@@ -375,7 +376,7 @@ def map_lib():
 
 def exported_symbols():
     return ["lbamap_load", "lbamap_free", "lbamap_last_error", "lbamap_snapshot_size", "lbamap_save",
-            "lbamap_local_gpba", "lbamap_build_window", "lbamap_global_ba", "lbamap_kf_gba", "lbamap_mp_gba",
+            "lbamap_local_gpba", "lbamap_build_window", "lbamap_global_ba", "lbamap_global_ba_thread", "lbamap_kf_gba", "lbamap_mp_gba",
             "lbamap_build_ba_window"]
 
 
@@ -423,6 +424,11 @@ class LocalGPBAMap:
         sf = None if stop_flag is None else ctypes.byref(stop_flag)
         rc = map_lib().lbamap_global_ba(self.h, iterations, sf, loop_kf, ctypes.byref(opt), ctypes.byref(res))
         return rc, res
+
+    def global_ba_thread(self, iterations=10, loop_kf=0):
+        """The reference signature GlobalBundleAdjustemnt(pMap, it, pbStopFlag, nLoopKF) on the calling
+        thread, with the engine owned by (and freed with) that thread; returns rc."""
+        return map_lib().lbamap_global_ba_thread(self.h, iterations, None, loop_kf)
 
     def kf_gba(self, kf_id):
         q, t, v = np.zeros(4, np.float32), np.zeros(3, np.float32), np.zeros(6, np.float32)

@@ -1952,9 +1952,13 @@ struct GroupSlot {   // lba_set_partition_group: the user pointer of the in-proc
     int rank;
 };
 
+static std::atomic<int> g_live_problems{0};   // lba_live_problems: engines created and not yet destroyed
+
 extern "C" {
 
 int lba_abi_version(void) { return LBA_ABI_VERSION; }
+
+int lba_live_problems(void) { return g_live_problems.load(); }
 
 int lba_create(lba_problem** out, const lba_config* cfg) {
     if (!out || !cfg) return LBA_E_ARG;
@@ -1987,11 +1991,13 @@ int lba_create(lba_problem** out, const lba_config* cfg) {
         return LBA_E_HIP;
     }
     *out = p;
+    g_live_problems.fetch_add(1);
     return LBA_OK;
 }
 
 void lba_destroy(lba_problem* p) {
     if (!p) return;
+    g_live_problems.fetch_sub(1);
     (void)hipSetDevice(p->cfg.device);
     if (p->stream) (void)hipStreamSynchronize(p->stream);
     free_all(p);

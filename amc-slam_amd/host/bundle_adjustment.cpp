@@ -117,6 +117,8 @@ void Optimizer::BuildBundleAdjustmentWindow(const std::vector<MultiKeyFrame*>& v
     std::vector<MapPoint*> pts;
     std::vector<int> pt_of(vpMP.size(), -1);
     std::unordered_map<const MapPoint*, int> seen;
+    std::unordered_multimap<const MultiKeyFrame*, int> kf_pos;   // keyframe -> its positions in vpKFs
+    for (size_t k = 0; k < vpKFs.size(); ++k) kf_pos.emplace(vpKFs[k], (int)k);
     for (size_t i = 0; i < vpMP.size(); ++i) {
         MapPoint* pMP = vpMP[i];
         if (!pMP || seen.count(pMP)) continue;
@@ -162,14 +164,32 @@ void Optimizer::BuildBundleAdjustmentWindow(const std::vector<MultiKeyFrame*>& v
                     add(3, LBA_STEREO, -1, kb, c, pKFi->mTimeStamp, kpUn.x, kpUn.y, kp_ur, invSigma2);
             }
         }
-        for (MultiKeyFrame* pKFi : vpKFs) {   // GP observations of non-keyframes (:234-282)
-            if (pKFi->isBad() || !pKFi->mNextKF) continue;
-            if (pKFi->mnId > maxKFid || pKFi->mNextKF->mnId > maxKFid) continue;
-            const int a = vtx(pKFi), b = vtx(pKFi->mNextKF);
-            if (a < 0 || b < 0) continue;
-            auto range = observationsGP.equal_range(pKFi);
-            for (auto it = range.first; it != range.second; ++it) {
-                const GPObs& g = it->second;
+        // GP observations of non-keyframes (:234-282).  The reference walks vpKFs and takes each keyframe's
+        // equal_range of the point's multimap: O(points x keyframes).  Here the point's own GP observations
+        // are visited and ordered by (position of their keyframe in vpKFs, multimap order), which is the
+        // same edge order at O(observations log observations).
+        if (!observationsGP.empty()) {
+            struct GPEdge {
+                int pos, seq;
+                MultiKeyFrame* K;
+                const GPObs* g;
+            };
+            std::vector<GPEdge> ge;
+            int seq = 0;
+            for (auto it = observationsGP.begin(); it != observationsGP.end(); ++it, ++seq) {
+                auto pr = kf_pos.equal_range(it->first);
+                for (auto q = pr.first; q != pr.second; ++q) ge.push_back(GPEdge{q->second, seq, it->first, &it->second});
+            }
+            std::sort(ge.begin(), ge.end(), [](const GPEdge& x, const GPEdge& y) {
+                return x.pos != y.pos ? x.pos < y.pos : x.seq < y.seq;
+            });
+            for (const GPEdge& e : ge) {
+                MultiKeyFrame* pKFi = e.K;
+                if (pKFi->isBad() || !pKFi->mNextKF) continue;
+                if (pKFi->mnId > maxKFid || pKFi->mNextKF->mnId > maxKFid) continue;
+                const int a = vtx(pKFi), b = vtx(pKFi->mNextKF);
+                if (a < 0 || b < 0) continue;
+                const GPObs& g = *e.g;
                 const float invSigma2 = (*pKFi->mvInvLevelSigma2)[g.obs.octave];
                 if (g.ur >= 0)
                     add(1, LBA_STEREO_GP, a, b, g.cam, g.time, g.obs.x, g.obs.y, g.ur, invSigma2);
@@ -297,11 +317,20 @@ int Optimizer::BundleAdjustment(const std::vector<MultiKeyFrame*>& vpKFs, const 
 void Optimizer::BundleAdjustment(const std::vector<MultiKeyFrame*>& vpKFs, const std::vector<MapPoint*>& vpMP,
                                  int nIterations, bool* pbStopFlag, const unsigned long nLoopKF, const bool bRobust) {
     (void)bRobust;   // unused by the reference too
-    thread_local lba_problem* p = nullptr;   // one engine per calling thread (LoopClosing's GBA thread)
-    if (!p) {
+    // One engine per calling thread, freed when the thread exits: LoopClosing starts a new thread for
+    // every global BA (src/LoopClosing.cc:1044), and the reference's optimiser dies with the call.
+    struct ThreadEngine {
+        lba_problem* p = nullptr;
+        ~ThreadEngine() {
+            if (p) lba_destroy(p);
+        }
+    };
+    thread_local ThreadEngine engine;
+    if (!engine.p) {
         lba_config cfg{};
-        if (lba_create(&p, &cfg) != LBA_OK) { p = nullptr; return; }
+        if (lba_create(&engine.p, &cfg) != LBA_OK) { engine.p = nullptr; return; }
     }
+    lba_problem* p = engine.p;
     // g2o's setForceStopFlag(pbStopFlag): the engine polls an int32 between iterations and trials, which a
     // watcher keeps equal to *pbStopFlag while the optimisation runs
     volatile int32_t flag = 0;

@@ -125,6 +125,17 @@ int lbamap_global_ba(lbamap* m, int32_t n_iterations, volatile const int32_t* st
     }
 }
 
+int lbamap_global_ba_thread(lbamap* m, int32_t n_iterations, bool* stop, uint64_t loop_kf) {
+    if (!m || n_iterations < 0) return LBA_E_ARG;
+    try {
+        Optimizer::GlobalBundleAdjustemnt(m->map.get(), n_iterations, stop, (unsigned long)loop_kf, true);
+        return LBA_OK;
+    } catch (const std::exception& e) {
+        m->err = e.what();
+        return LBA_E_ARG;
+    }
+}
+
 int lbamap_kf_gba(const lbamap* m, int64_t kf_id, float q[4], float t[3], float vel[6], uint64_t* loop_kf) {
     if (!m) return LBA_E_ARG;
     const MultiKeyFrame* K = m->map->kf_by_id(kf_id);

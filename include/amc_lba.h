@@ -153,6 +153,10 @@ int         lba_create(lba_problem** out, const lba_config* cfg);
 void        lba_destroy(lba_problem* p);
 const char* lba_last_error(const lba_problem* p);
 int         lba_abi_version(void);
+/* Engines created by lba_create and not yet destroyed, process-wide (leak checks: the reference
+ * builds and frees its g2o optimiser on every call, src/Optimizer.cc:61-367, so a caller that runs one
+ * engine per call or per thread must see this return to its previous value). */
+int         lba_live_problems(void);
 
 /* Replace the configuration (Huber deltas, lambda0, Qc, flags) of an existing problem, e.g. between
  * LocalGPBA calls with and without bLarge (OptimizationAlgorithmLevenberg::setUserLambdaInit,

@@ -31,6 +31,7 @@
 #ifndef AMC_LBA_MAP_H
 #define AMC_LBA_MAP_H
 
+#include <stdbool.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -166,12 +167,6 @@ int64_t lbamap_save(const lbamap* m, void* bytes, size_t cap);
 int lbamap_local_gpba(lbamap* m, int64_t kf_id, volatile const int32_t* stop_flag, const lbamap_options* opt,
                       lbamap_result* out);
 
-/* The window LocalGPBA would build for kf_id, as the flat arrays of include/amc_lba.h, without
- * optimising and without touching the map (the BA flags are restored).  Two calls: first with
- * NULL arrays to get the counts in *counts = {n_kf, n_lm, n_obs, n_priors, n_vel, n_cam}, then
- * with arrays of those sizes.  kf_ids / mp_ids / obs_tag (may be NULL) give the map ids of each
- * keyframe / landmark row and, per observation, the post-pass list it belongs to
- * (0 MonoGP, 1 StereoGP, 2 Mono, 3 Stereo, 4 MonoGP at KF time). */
 /* Optimizer::GlobalBundleAdjustemnt(pMap, n_iterations, stop, loop_kf) on the whole map (every keyframe
  * and map point of it, GetAllKeyFrames / GetAllMapPoints), GPU engine on opt->device (opt->large and
  * opt->extrinsic are ignored).  loop_kf == 0 writes poses, velocities and points back (SetPose /
@@ -181,12 +176,23 @@ int lbamap_global_ba(lbamap* m, int32_t n_iterations, volatile const int32_t* st
                      const lbamap_options* opt, lbamap_ba_result* out);
 int lbamap_kf_gba(const lbamap* m, int64_t kf_id, float q[4], float t[3], float vel[6], uint64_t* loop_kf);
 int lbamap_mp_gba(const lbamap* m, int64_t mp_id, float pos[3], uint64_t* loop_kf);
+/* The reference's own entry, void Optimizer::GlobalBundleAdjustemnt(pMap, n_iterations, pbStopFlag,
+ * nLoopKF, bRobust) (src/Optimizer.cc:53-58), on the calling thread and GPU 0: its engine belongs to the
+ * calling thread and is destroyed when that thread exits (LoopClosing starts one thread per global BA,
+ * src/LoopClosing.cc:1044).  stop may be NULL.  Returns LBA_OK (the reference returns nothing). */
+int lbamap_global_ba_thread(lbamap* m, int32_t n_iterations, bool* stop, uint64_t loop_kf);
 /* The global BA graph as flat arrays, without optimising (parity tests), same outputs as
  * lbamap_build_window. */
 int lbamap_build_ba_window(lbamap* m, int32_t counts[6], lba_kf* kfs, double* lm_xyz, lba_obs* obs,
                            lba_prior* priors, int32_t* vel_kfs, lba_cam* cams, int64_t* kf_ids, int64_t* mp_ids,
                            int32_t* obs_tag, lba_config* cfg);
 
+/* The window LocalGPBA would build for kf_id, as the flat arrays of include/amc_lba.h, without
+ * optimising and without touching the map (the BA flags are restored).  Two calls: first with
+ * NULL arrays to get the counts in *counts = {n_kf, n_lm, n_obs, n_priors, n_vel, n_cam}, then
+ * with arrays of those sizes.  kf_ids / mp_ids / obs_tag (may be NULL) give the map ids of each
+ * keyframe / landmark row and, per observation, the post-pass list it belongs to
+ * (0 MonoGP, 1 StereoGP, 2 Mono, 3 Stereo, 4 MonoGP at KF time). */
 int lbamap_build_window(lbamap* m, int64_t kf_id, const lbamap_options* opt, int32_t counts[6],
                         lba_kf* kfs, double* lm_xyz, lba_obs* obs, lba_prior* priors, int32_t* vel_kfs,
                         lba_cam* cams, int64_t* kf_ids, int64_t* mp_ids, int32_t* obs_tag, lba_config* cfg);

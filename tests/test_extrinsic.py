@@ -172,8 +172,21 @@ def test_gpu_extrinsic_argument_errors():
     with pytest.raises(LbaError) as ei:
         Problem(bad)
     assert ei.value.code == LBA_E_ARG
-    g = Group(2)   # (a single rank is not partitioned; the check fails before any collective)
-    with pytest.raises(LbaError) as ei:
-        Problem(win, group=g, rank=0)
-    assert ei.value.code == LBA_E_LIMIT
+    # (a single rank is not partitioned).  A failing rank releases its peers through the set-up status
+    # all-reduce, so both ranks of the group call in (one alone would wait for its peer)
+    import threading
+    g = Group(2)
+    codes = [None, None]
+
+    def rank(r):
+        try:
+            Problem(win, group=g, rank=r)
+        except LbaError as e:
+            codes[r] = e.code
+    ts = [threading.Thread(target=rank, args=(r,)) for r in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert codes == [LBA_E_LIMIT, LBA_E_LIMIT]
     g.close()

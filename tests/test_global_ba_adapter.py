@@ -128,3 +128,33 @@ def test_global_ba_stop_flag():
     assert rc == 0 and res.iterations == 0
     got = m.save()
     np.testing.assert_allclose(got.mps["pos"][got.mps["bad"] == 0], snap.mps["pos"][snap.mps["bad"] == 0], rtol=1e-7)
+
+
+@pytest.mark.gpu
+def test_global_ba_thread_engines_are_freed():
+    """The reference signature GlobalBundleAdjustemnt(pMap, ...) runs on a thread LoopClosing starts per
+    loop closure (src/LoopClosing.cc:1044): two successive threads must leave no engine (device buffers,
+    stream, pinned staging) behind, and the second run must match the first's write-back path."""
+    import threading
+
+    import amc_lba
+    L = amc_lba.lib()
+    base = L.lba_live_problems()
+    snap = ms.make_map(**MAPS["plain"])
+    outs = []
+    for _ in range(2):
+        m = ms.LocalGPBAMap(snap)
+        rcs = []
+        t = threading.Thread(target=lambda: rcs.append(m.global_ba_thread(iterations=5)))
+        t.start()
+        t.join(timeout=300)
+        assert rcs == [0], m.error()
+        assert L.lba_live_problems() == base
+        outs.append(m.save())
+    np.testing.assert_array_equal(outs[0].kfs["t"], outs[1].kfs["t"])
+    np.testing.assert_array_equal(outs[0].mps["pos"], outs[1].mps["pos"])
+    # and the result is the engine's ordinary global BA
+    m = ms.LocalGPBAMap(snap)
+    rc, _ = m.global_ba(iterations=5)
+    assert rc == 0
+    np.testing.assert_array_equal(m.save().kfs["t"], outs[0].kfs["t"])
