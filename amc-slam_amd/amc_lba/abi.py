@@ -82,6 +82,7 @@ FLAG_TIME_PHASES = 2
 FLAG_HOST_LOOP = 4         # host-driven LM loop (default: queued trials decided on the device)
 FLAG_BAND_SOLVE = 8        # reduced system solved by substitution after the factorisation (large systems)
 FLAG_DENSE_SOLVE = 16      # force the L^-1-tile solve
+FLAG_TIME_SAMPLED = 32     # with FLAG_TIME_SWEEP (queued loop): events on every 10th trial only
 
 
 def make_config(qc_diag=(0.02, 0.02, 0.02, 0.002, 0.002, 0.002), huber_mono=None, huber_stereo=None,

@@ -218,6 +218,14 @@ struct DevProblem {
     unsigned long long* cf_head;
     int* cf_abort;
     int cf_steps_path;      // LBA_CHOL_STEPS: the k_chol_step sequence instead
+    // fused flow (unpartitioned): the expansion and the assembly run as k_chol_flow's first tasks
+    int cf_fused;
+    int* cf_cnt;            // [cf_ncnt] counters, zeroed by k_lin_schur (see CholFlow)
+    int cf_ncnt;
+    const int* cf_need;     // [cf_ncnt]
+    const int* cf_asm_item; // per assembly item: id | type << 28
+    const int* cf_asm_tgt;  // per assembly item: 4 counter indices
+    int cf_ntile;           // envelope tiles of the permuted system
     int cf_band;            // 1: solve by substitution tasks (no L^-1 tiles, large systems)
     double* cf_xpos;        // band solve: x in factorisation order (handed off between back tasks)
     double* LinvT;          // [npad / CHOL_NB][CHOL_NB][CHOL_NB] inverse diagonal blocks L_bb^-T (row-major)
@@ -277,8 +285,9 @@ void launch_lin_schur(const DevProblem& P, int sel, int gate, double lambda, int
 void launch_expand(const DevProblem& P, int sel, int gate, double lambda, int schur, hipStream_t s);
 enum { ASM_SCHUR = 1, ASM_FULL = 2 };
 void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hipStream_t s);
+// (fused flow: sel / lambda of the expansion and assembly it runs first)
 void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s, hipEvent_t e0 = nullptr,
-                           hipEvent_t e1 = nullptr);
+                           hipEvent_t e1 = nullptr, int sel = 0, double lambda = 0.0);
 // the step + trial state + the trial state's pose samples (jac: with their Jacobian factors)
 void launch_update(const DevProblem& P, double lambda, int sel, int gate, int jac, hipStream_t s);
 // partitioned mode: this rank's trial sums into red4; envelope of S + bS + b_p into / out of env_buf

@@ -1521,6 +1521,97 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 pl0.push_back((int)plist.size());
             }
             if (NP > 4095) throw ApiError{LBA_E_LIMIT, "internal: too many panels for the dataflow factorisation"};
+            // fused flow (LBA_FLOW_FUSED=1; one problem, not partitioned): the
+            // pose-sample expansions and heavy landmarks, then the assembly items (padding rows, rhs per pose
+            // block, S blocks) in the order the columns they feed are factored, ahead of the factor tasks; a
+            // counter per envelope tile / panel rhs tells the factor tasks when their operands are assembled
+            // (the assembly items address the slabs with 32-bit buffer offsets)
+            const long long slab_max = 8LL * std::max((long long)n_hslots * 144, (long long)n_sslots * 144);
+            const bool fused = p->part_n == 0 && !(!band && std::getenv("LBA_CHOL_STEPS")) &&
+                               std::getenv("LBA_FLOW_FUSED") && slab_max < (1LL << 31);
+            D.cf_fused = fused ? 1 : 0;
+            const int ntile = tbase[NP];
+            D.cf_ntile = ntile;
+            D.cf_ncnt = 1 + ntile + NP;
+            if (fused) {
+                std::vector<int> need(D.cf_ncnt, 0), aitem, atgt, prefix;
+                std::vector<int> akey;   // assembly item -> first update rank among the columns it feeds
+                need[0] = n_smp + n_heavy;
+                for (int e = 0; e < n_smp; ++e) prefix.push_back(e | (8 << 24));
+                for (int h = 0; h < n_heavy; ++h) prefix.push_back(h | (9 << 24));
+                auto tile_cnt = [&](int rh, int ch) {
+                    const int ti = std::max(rh, ch) / CHOL_NB, tj = std::min(rh, ch) / CHOL_NB;
+                    return 1 + tbase[ti] + tj - pfh[ti];
+                };
+                auto add_item = [&](int code, const std::vector<int>& tg, int key) {
+                    if (tg.size() > 4) throw ApiError{LBA_E_LIMIT, "internal: assembly item feeds more than 4 tiles"};
+                    aitem.push_back(code);
+                    for (int q = 0; q < 4; ++q) atgt.push_back(q < (int)tg.size() ? tg[q] : -1);
+                    for (int c : tg) need[c]++;
+                    akey.push_back(key);
+                };
+                auto uniq = [](std::vector<int> v) {
+                    std::sort(v.begin(), v.end());
+                    v.erase(std::unique(v.begin(), v.end()), v.end());
+                    return v;
+                };
+                auto col_rank = [&](int c) {   // counter -> update rank of the column it belongs to
+                    if (c > ntile) return rank[c - 1 - ntile];
+                    const int t = c - 1;
+                    int ti = (int)(std::upper_bound(tbase.begin(), tbase.end(), t) - tbase.begin()) - 1;
+                    return rank[pfh[ti] + (t - tbase[ti])];
+                };
+                auto key_of = [&](const std::vector<int>& tg) {
+                    int k = NP;
+                    for (int c : tg) k = std::min(k, col_rank(c));
+                    return k;
+                };
+                if (npad > p->np) {   // padding rows
+                    std::vector<int> tg;
+                    for (int r = p->np; r < npad; ++r) {
+                        tg.push_back(tile_cnt(rpos[r], rpos[r]));
+                        tg.push_back(1 + ntile + rpos[r] / CHOL_NB);
+                    }
+                    tg = uniq(tg);
+                    add_item(0, tg, -1);
+                }
+                for (int k = 0; k < n_pb; ++k) {   // rhs of pose block k
+                    std::vector<int> tg;
+                    for (int r = 12 * k; r < 12 * k + 12; ++r) tg.push_back(1 + ntile + rpos[r] / CHOL_NB);
+                    tg = uniq(tg);
+                    add_item(k | (1 << 28), tg, key_of(tg));
+                }
+                for (int u = 0; u < n_ublocks; ++u) {   // S blocks (k_assemble's asm_list)
+                    if (!(hcnt[u] > 0 || scnt[u] > 0 || ub_i[u] == ub_j[u])) continue;
+                    std::vector<int> tg;
+                    for (int e = 0; e < 144; ++e) {
+                        const int i = e / 12, j = e % 12, r = 12 * ub_j[u] + j, c = 12 * ub_i[u] + i;
+                        if (ub_i[u] != ub_j[u] || j >= i) tg.push_back(tile_cnt(rpos[r], rpos[c]));
+                    }
+                    tg = uniq(tg);
+                    add_item(u | (2 << 28), tg, key_of(tg));
+                }
+                std::vector<int> ord(aitem.size());
+                for (size_t q = 0; q < ord.size(); ++q) ord[q] = (int)q;
+                std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return akey[x] < akey[y]; });
+                std::vector<int> aitem2, atgt2;
+                for (int q : ord) {
+                    prefix.push_back((int)aitem2.size() | (10 << 24));
+                    aitem2.push_back(aitem[q]);
+                    for (int w = 0; w < 4; ++w) atgt2.push_back(atgt[4 * q + w]);
+                }
+                std::vector<int> all(prefix);
+                all.insert(all.end(), tasks.begin(), tasks.end());
+                tasks.swap(all);
+                std::vector<int> pl(prefix.size(), 0);
+                pl.insert(pl.end(), pl0.begin(), pl0.end());
+                pl0.swap(pl);
+                D.cf_need = dupload(p, need);
+                D.cf_asm_item = dupload(p, aitem2);
+                D.cf_asm_tgt = dupload(p, atgt2);
+                D.cf_cnt = dalloc<int>(p, D.cf_ncnt);
+                HIPCHK(hipMemset(D.cf_cnt, 0, sizeof(int) * D.cf_ncnt));
+            }
             D.cf_tasks = dupload(p, tasks);
             D.cf_ntasks = (int)tasks.size();
             D.cf_tbase = dupload(p, tbase);
@@ -1673,11 +1764,12 @@ void finalize_and_wait(lba_problem* p, bool sync, int eval_sel = -1) {
 // S holds either the factorisation-order lower triangle (trials) or the natural full matrix
 // (ASM_FULL: lba_linearize / lambda init); switching layouts clears it first, since each layout only
 // rewrites its own pattern
-void assemble_layout(lba_problem* p, double lambda, int flags, int gate = GATE_NONE) {
+void assemble_layout(lba_problem* p, double lambda, int flags, int gate = GATE_NONE, bool launch = true) {
     const int want = (flags & ASM_FULL) ? 1 : 0;
     if (want != p->s_layout || want == 1)
         HIPCHK(hipMemsetAsync(p->D.S, 0, sizeof(double) * ((size_t)p->D.npad * p->D.npad), p->stream));
     p->s_layout = want;
+    if (!launch) return;   // (the fused flow assembles S itself)
     launch_assemble(p->D, lambda, flags, gate, p->stream);
     if ((flags & ASM_SCHUR) && p->part_n > 0) {   // sum the ranks' reduced systems
         launch_env_pack(p->D, 0, gate, p->stream);
@@ -1710,10 +1802,13 @@ void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs, bool s
     launch_lin_schur(D, p->cur, GATE_NONE, lambda, LS_SCHUR | LS_EDGES, p->stream, sweep ? p->ev[6] : nullptr,
                      sweep ? p->ev[7] : nullptr);
     if (evs) HIPCHK(hipEventRecord(evs[1], p->stream));
-    launch_expand(D, p->cur, GATE_NONE, lambda, 1, p->stream);
-    assemble_layout(p, lambda, ASM_SCHUR);
+    // (fused flow: the expansion and the assembly are k_chol_flow's first tasks; the phase events then time
+    // them with the solve)
+    if (!D.cf_fused) launch_expand(D, p->cur, GATE_NONE, lambda, 1, p->stream);
+    assemble_layout(p, lambda, ASM_SCHUR, GATE_NONE, !D.cf_fused);
     if (evs) HIPCHK(hipEventRecord(evs[2], p->stream));
-    launch_cholesky_solve(D, GATE_NONE, ++p->cf_epoch, p->stream, sweep ? p->ev[8] : nullptr, sweep ? p->ev[9] : nullptr);
+    launch_cholesky_solve(D, GATE_NONE, ++p->cf_epoch, p->stream, sweep ? p->ev[8] : nullptr, sweep ? p->ev[9] : nullptr,
+                          p->cur, lambda);
     if (evs) HIPCHK(hipEventRecord(evs[3], p->stream));
     launch_update(D, lambda, p->cur, GATE_NONE, 1, p->stream);   // (+ the trial state's pose samples)
     p->gps_fresh[nx] = true;
@@ -1725,7 +1820,9 @@ void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs, bool s
 
 double eval_current(lba_problem* p) {
     const DevProblem& D = p->D;
-    launch_gp_prep(D, p->cur, 1, GATE_NONE, p->stream);   // (the samples the linearisation then uses)
+    // the samples the linearisation then uses (kept when the last trial's k_update made them: the queued
+    // loop then evaluates the same samples as this one)
+    if (!p->gps_fresh[p->cur]) launch_gp_prep(D, p->cur, 1, GATE_NONE, p->stream);
     p->gps_fresh[p->cur] = true;
     finalize_and_wait(p, true, p->cur);
     return p->h_fin[1];
@@ -1785,6 +1882,7 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
     launch_eval(D, p->cur, GATE_NONE, 0, FIN_NONE, p->stream);
     launch_fin(p, 0, FIN_INITIAL);
     int issued = 0;
+    std::vector<char> timed(tsweep ? HLOG_CAP : 0, 0);   // trials whose dispatches carry events
     const LMCtl* hc = reinterpret_cast<const LMCtl*>(p->h_fin + 8);
     while (true) {
         const int n = iters - c.it;
@@ -1793,7 +1891,12 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
         for (int k = 0; k < n; ++k, ++issued) {
             // LBA_FLAG_TIME_SWEEP: the dispatches of k_lin_schur and k_chol_flow carry events (their own
             // start / end timestamps); the trials that ran are read from the controller's log afterwards
-            const bool tq = tsweep && issued < HLOG_CAP;
+            // (LBA_FLAG_TIME_SAMPLED: the 6th trial of every 10 of a batch, or its first in a short batch:
+            // mid-batch trials, away from the start-up launches of an optimize call)
+            const int samp = n >= 6 ? 5 : 0;
+            const bool tq = tsweep && issued < HLOG_CAP &&
+                            (!(p->cfg.flags & LBA_FLAG_TIME_SAMPLED) || (issued - first) % 10 == samp);
+            if (tsweep && issued < HLOG_CAP) timed[issued] = tq;
             if (tq && p->qev.size() < 4 * (size_t)issued + 4) {
                 const size_t old = p->qev.size();
                 p->qev.resize(std::max<size_t>(4 * (size_t)issued + 4, 2 * old));
@@ -1808,9 +1911,10 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
             }
             launch_lin_schur(D, SEL_CUR, GATE_TRIAL, LAMBDA_CTL, LS_SCHUR | LS_EDGES, p->stream, qe ? qe[0] : nullptr,
                              qe ? qe[1] : nullptr);
-            launch_expand(D, SEL_CUR, GATE_TRIAL, LAMBDA_CTL, 1, p->stream);
-            assemble_layout(p, LAMBDA_CTL, ASM_SCHUR);
-            launch_cholesky_solve(D, GATE_NONE, ++p->cf_epoch, p->stream, qe ? qe[2] : nullptr, qe ? qe[3] : nullptr);
+            if (!D.cf_fused) launch_expand(D, SEL_CUR, GATE_TRIAL, LAMBDA_CTL, 1, p->stream);
+            assemble_layout(p, LAMBDA_CTL, ASM_SCHUR, GATE_NONE, !D.cf_fused);
+            launch_cholesky_solve(D, GATE_NONE, ++p->cf_epoch, p->stream, qe ? qe[2] : nullptr, qe ? qe[3] : nullptr,
+                                  SEL_CUR, LAMBDA_CTL);
             // the step, the trial state and its pose samples with their Jacobian factors: the next
             // trial's linearisation reads them (no preparation launch)
             launch_update(D, LAMBDA_CTL, SEL_CUR, GATE_TRIAL, 1, p->stream);
@@ -1827,7 +1931,7 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
         if (tsweep) {
             HIPCHK(hipStreamSynchronize(p->stream));
             for (int q = first; q < issued && q < HLOG_CAP; ++q)
-                if (p->h_log[q]) {
+                if (p->h_log[q] && timed[q]) {
                     s.ms_k_linearize += elapsed(p->qev[4 * q], p->qev[4 * q + 1]);
                     s.n_k_linearize += 1;
                     s.ms_k_solve += elapsed(p->qev[4 * q + 2], p->qev[4 * q + 3]);

@@ -64,6 +64,31 @@ constexpr int LBA_DBG_INFO = 0x7ffe0000;
 
 typedef double d4 __attribute__((ext_vector_type(4)));   // v_mfma_f64_16x16x4 accumulator
 
+// Hand-offs between workgroups of one launch (MI355X_MICROARCH.md, inter-workgroup visibility): the payload
+// stored write-through (sc1) and drained by every storing wave before the flag / counter, every load of it
+// an sc1 load.  stv<WT> / ldv<WT>: plain or sc1 by a template switch (the fused flow's expand and assembly
+// tasks publish; the standalone kernels do not need to).
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+typedef __attribute__((address_space(1))) int gi32_t;
+
+__device__ __forceinline__ double ld_sc1(const double* p) {
+    return __longlong_as_double((long long)__hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+    __hip_atomic_store((gu64_t*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool WT>
+__device__ __forceinline__ void stv(double* p, double v) {
+    if constexpr (WT) st_sc1(p, v);
+    else *p = v;
+}
+template <bool WT>
+__device__ __forceinline__ double ldv(const double* p) {
+    if constexpr (WT) return ld_sc1(p);
+    else return *p;
+}
+
 // queued optimisation (LMCtl): the state buffer a launch works on, whether it runs, its damping
 __device__ __forceinline__ int state_idx(const DevProblem& P, int sel) {
     return sel < SEL_CUR ? sel : (P.ctl->cur ^ (sel - SEL_CUR));
@@ -188,22 +213,26 @@ __device__ __forceinline__ double eval_obs(const DevProblem& P, const double* gp
 }
 
 // ------------------------------------------------------------------------------------------------
-// GP pose samples: one workgroup per GP pair.  The pair quantities (gp_pair_build) and the per-sample
-// factor N (gp_sample_build) are computed with the same per-output operation order as those serial
-// functions, but spread over the wave: lane 0 the SE(3) log, then lanes 0-2 Jr^-1, Ad(exp(xi12))^-1
-// and ad(v2) side by side, one lane per 6x6 product entry, one lane per sample for its pose /
-// Jr / Ad(exp(-xi)), one lane per (sample, row, column) of N.  ka / kb: the two KF states (16
-// doubles each, global or LDS); gps: the sample buffer of that state.
+// GP pose samples: one workgroup (one wave) per GP pair.  The pair quantities (gp_pair_build) and the
+// per-sample factor N (gp_sample_build) follow those serial functions' per-output operation order.  A
+// wave runs divergent branches one after the other, so every transcendental step is ONE code path for
+// every lane that takes it: lane 0 the pair chain (log(T1^-1 T2), Ad(T12^-1), Jr^-1(xi12)), then one
+// lane per sample its exp(xi) (pose, and Ad(exp(-xi)) = Ad(exp(xi)^-1)) followed by Jr(xi), then one lane
+// per (sample, row, column) of N.  ka / kb: the two KF states (16 doubles each, global or LDS); gps: the
+// sample buffer of that state.
 constexpr int PREP_THREADS = 64;
-constexpr int PREP_SCHUNK = 21;   // samples per pass (3 lanes each; LDS staging of their Jr / Ad blocks)
-__device__ void gp_pair_prep(const DevProblem& P, double* gps, int i, const double* ka, const double* kb, int jac,
-                             unsigned long long* pst = nullptr) {
+constexpr int PREP_SCHUNK = 32;   // samples per pass (one lane each; LDS staging of their Jr / Ad blocks)
+// (inlined into k_gp_prep and k_update: a noinline body, one copy for both, measured 4.5 % slower LM
+// iterations, profiles/r3e_ab_update_inline_wait.txt; the two copies may round differently in the last bit)
+__device__ __forceinline__ void gp_pair_prep(const DevProblem& P, double* gps, int i, const double* ka,
+                                             const double* kb, int jac, unsigned long long* pst = nullptr) {
     __shared__ GPPair pr;
     __shared__ double AdI[36], ad2[36], vbs[6];
-    __shared__ double sJr[PREP_SCHUNK][36], sRm[PREP_SCHUNK][9], stR[PREP_SCHUNK][9], sg[PREP_SCHUNK][3];
+    __shared__ double sJr[PREP_SCHUNK][18], sRm[PREP_SCHUNK][9], stR[PREP_SCHUNK][9], sg[PREP_SCHUNK][3];
     const int tid = threadIdx.x;
     // (diagnostics: pst = s_memrealtime stamps after each phase, thread 0)
 #define PREP_STAMP(k) do { if (pst && tid == 0) pst[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+    if (tid < 6) vbs[tid] = kb[7 + tid];
     if (tid == 0) {
         const SE3 Ta = load_se3(ka), Tb = load_se3(kb);
         pr.T1q[0] = Ta.q.x; pr.T1q[1] = Ta.q.y; pr.T1q[2] = Ta.q.z; pr.T1q[3] = Ta.q.w;
@@ -213,17 +242,10 @@ __device__ void gp_pair_prep(const DevProblem& P, double* gps, int i, const doub
         pr.t2 = kb[13];
         const SE3 T12 = se3_mul(se3_inv(Ta), Tb);
         se3_log(T12, pr.xi12);
-    }
-    if (tid < 6) vbs[tid] = kb[7 + tid];
-    __syncthreads();
-    PREP_STAMP(0);
-    if (tid == 0) {
+        if (jac) se3_adj(se3_inv(T12), AdI);         // Ad(exp(xi12))^-1 = Ad(T12^-1)
+        PREP_STAMP(0);
         right_jac_inv(pr.xi12, pr.G2a);                 // C = Jr^-1(xi12)
-    } else if (jac && tid == 1) {
-        const SE3 E = se3_exp(pr.xi12);                 // Ad(exp(xi12))^-1 = Ad(exp(xi12)^-1)
-        se3_adj(se3_inv(E), AdI);
-    } else if (jac && tid == 2) {
-        se3_ad(vbs, ad2);
+        if (jac) se3_ad(kb + 7, ad2);
     }
     __syncthreads();
     PREP_STAMP(1);
@@ -252,61 +274,51 @@ __device__ void gp_pair_prep(const DevProblem& P, double* gps, int i, const doub
     PREP_STAMP(3);
     for (int c0 = P.gp_s0[i]; c0 < P.gp_s0[i + 1]; c0 += PREP_SCHUNK) {
         const int ns = min(PREP_SCHUNK, P.gp_s0[i + 1] - c0);
-        // three lanes per sample, each one of the independent transcendental chains: the interpolated
-        // pose (gp_sample_pose), Jr(xi) and Ad(exp(-xi)); xi is recomputed per lane (same expression)
-        if (tid < 3 * ns) {
-            const int sl = tid / 3, role = tid - 3 * sl;
-            GPSample* S = reinterpret_cast<GPSample*>(gps + (size_t)(c0 + sl) * GPS_STRIDE);
-            if (role == 0) {
-                double xi[6];
-                GPScalars g;
-                gp_sample_pose(pr, P.gps_t[c0 + sl], S->Rwb, S->twb, xi, &g);
-            } else if (jac) {
-                const GPScalars g = gp_scalars(pr.t1, pr.t2, P.gps_t[c0 + sl]);
-                double xi[6];
-                for (int q = 0; q < 6; ++q) xi[q] = g.p2 * pr.v1[q] + g.l1 * pr.xi12[q] + g.l2 * pr.w2[q];
-                if (role == 1) {
-                    double Jl[9], Q[9];                     // Jr(xi) = [Jl, Q; 0, Jl]
-                    right_jac_blocks(xi, Jl, Q);
-                    for (int r = 0; r < 3; ++r)
-                        for (int c = 0; c < 3; ++c) {
-                            sJr[sl][r * 6 + c] = Jl[r * 3 + c];
-                            sJr[sl][r * 6 + 3 + c] = Q[r * 3 + c];
-                            sJr[sl][(3 + r) * 6 + c] = 0.0;
-                            sJr[sl][(3 + r) * 6 + 3 + c] = Jl[r * 3 + c];
-                        }
-                    sg[sl][0] = g.l1; sg[sl][1] = g.l2; sg[sl][2] = g.p2;
-                } else {
-                    const double mxi[6] = {-xi[0], -xi[1], -xi[2], -xi[3], -xi[4], -xi[5]};
-                    const SE3 Em = se3_exp(mxi);            // Ad(exp(-xi)) = [R', t'^ R'; 0, R']
-                    double Ht[9];
-                    qmat(Em.q, sRm[sl]);
-                    hat3(Em.t, Ht);
-                    mul33(Ht, sRm[sl], stR[sl]);
-                }
+        // one lane per sample: the interpolated pose T1 exp(xi) (gp_sample_pose), Ad(exp(xi)^-1), Jr(xi)
+        if (tid < ns) {
+            GPSample* S = reinterpret_cast<GPSample*>(gps + (size_t)(c0 + tid) * GPS_STRIDE);
+            double xi[6];
+            GPScalars g;
+            SE3 E;
+            gp_sample_pose(pr, P.gps_t[c0 + tid], S->Rwb, S->twb, xi, &g, &E);
+            if (jac) {
+                const SE3 Em = se3_inv(E);                  // Ad(exp(-xi)) = [R', t'^ R'; 0, R']
+                double Ht[9];
+                qmat(Em.q, sRm[tid]);
+                hat3(Em.t, Ht);
+                mul33(Ht, sRm[tid], stR[tid]);
+                right_jac_blocks(xi, sJr[tid], sJr[tid] + 9);   // Jr(xi) = [Jl, Q; 0, Jl]
+                sg[tid][0] = g.l1; sg[tid][1] = g.l2; sg[tid][2] = g.p2;
             }
         }
         __syncthreads();
-    PREP_STAMP(4);
+        PREP_STAMP(4);
         if (jac)
             for (int t = tid; t < ns * 36; t += PREP_THREADS) {   // one (row, column) of each N block
                 const int sl = t / 36, r = (t % 36) / 6, c = t % 6;
                 const double l1 = sg[sl][0], l2 = sg[sl][1], p2 = sg[sl][2];
-                const double* Jr = sJr[sl];
+                const double* Jl = sJr[sl];
+                const double* Qb = sJr[sl] + 9;
+                // row r of Jr(xi): [Jl(r), Q(r); 0, Jl(r - 3)]
+                auto jr = [&](int l) {
+                    if (r < 3) return l < 3 ? Jl[r * 3 + l] : Qb[r * 3 + l - 3];
+                    return l < 3 ? 0.0 : Jl[(r - 3) * 3 + l - 3];
+                };
                 double na = 0.0, nb = 0.0, nc = 0.0;
                 for (int l = 0; l < 6; ++l) {
                     const double ma = l1 * pr.G1a[l * 6 + c] + l2 * pr.G1b[l * 6 + c];
                     const double mc = l1 * pr.G2a[l * 6 + c] + l2 * pr.G2b[l * 6 + c];
-                    na += Jr[r * 6 + l] * ma;
-                    nb += Jr[r * 6 + l] * mc;
-                    nc += Jr[r * 6 + l] * pr.G2a[l * 6 + c];
+                    const double j = jr(l);
+                    na += j * ma;
+                    nb += j * mc;
+                    nc += j * pr.G2a[l * 6 + c];
                 }
                 double ad = 0.0;
                 if (r < 3) ad = (c < 3) ? sRm[sl][r * 3 + c] : stR[sl][r * 3 + c - 3];
                 else if (c >= 3) ad = sRm[sl][(r - 3) * 3 + c - 3];
                 double* N = gps + (size_t)(c0 + sl) * GPS_STRIDE + 12;
                 N[c * 6 + r] = na + ad;
-                N[(6 + c) * 6 + r] = p2 * Jr[r * 6 + c];
+                N[(6 + c) * 6 + r] = p2 * jr(c);
                 N[(12 + c) * 6 + r] = nb;
                 N[(18 + c) * 6 + r] = l2 * nc;
             }
@@ -387,6 +399,7 @@ constexpr int EXP_GROUPS = PRI_THREADS / SM_STRIDE;   // 9 partial sums per outp
 
 // A sample of a camera whose extrinsic is free also couples that extrinsic's block e: N is extended by the
 // camera's factor [Ad(Tbc) 0] (columns 24..35) and ae, be, ee, b_e follow the same way.
+template <bool WT>
 __device__ void sample_expand(const DevProblem& P, const double* gps, const double* camd, int smp, double* Msh,
                               double* Nsh, double* MN, double* part, const int tid) {
     const int* sl = P.seg_slot + SEG_STRIDE * (size_t)smp;
@@ -446,8 +459,7 @@ __device__ void sample_expand(const DevProblem& P, const double* gps, const doub
 #pragma unroll
         for (int l = 0; l < 6; ++l) v += Nsh[6 * ci + l] * MN[6 * cj + l];
         double* H = P.hslab + (size_t)slot * 144;
-        if (bk == 1 && sl[3]) H[j * 12 + i] = v;
-        else H[i * 12 + j] = v;
+        stv<WT>(H + ((bk == 1 && sl[3]) ? j * 12 + i : i * 12 + j), v);
     }
     if (tid < ncol) {
         const int side = tid / 12, i = tid % 12;
@@ -455,7 +467,7 @@ __device__ void sample_expand(const DevProblem& P, const double* gps, const doub
             double v = 0.0;
 #pragma unroll
             for (int l = 0; l < 6; ++l) v += Nsh[6 * (12 * side + i) + l] * Msh[21 + l];
-            P.gslab[(size_t)gl[side] * 12 + i] = -v;
+            stv<WT>(P.gslab + (size_t)gl[side] * 12 + i, -v);
         }
     }
 }
@@ -645,6 +657,8 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
             *P.info = 0;
             if (P.cf_head) *P.cf_head = 0;   // ticket counter of this trial's k_chol_flow
         }
+        if (P.cf_fused)   // the fused flow's expansion / assembly counters
+            for (int z = blockIdx.x * LS_THREADS + tid; z < P.cf_ncnt; z += gridDim.x * LS_THREADS) P.cf_cnt[z] = 0;
         for (int z = blockIdx.x; z < P.n_ztiles; z += gridDim.x) {
             const int zi = P.ztiles[z] & 0xffff, zj = P.ztiles[z] >> 16;
             for (int t = tid; t < CHOL_NB * CHOL_NB; t += LS_THREADS)
@@ -930,6 +944,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
 // eliminating, Dinv = (Hll + lambda I)^-1, V = Hpl Dinv, the rhs partial V bl of each of its KFs and the
 // S partial V(a) Hpl(b)^T of each pair of its KFs (block_solver.hpp:381-432: any number of KFs, like
 // g2o's Hpl columns).  shm: 21 doubles.
+template <bool WT>
 __device__ void heavy_item(const DevProblem& P, int h, double lambda, int schur, double* shm) {
     const int tid = threadIdx.x;
     const int l = P.hv_lm[h], s0 = P.hv_seg0[h], s1 = P.hv_seg0[h + 1];
@@ -970,7 +985,7 @@ __device__ void heavy_item(const DevProblem& P, int h, double lambda, int schur,
             vr[a] = v;
             g += v * HB[9 + a];
         }
-        P.gpslab[(size_t)P.hp_gslot[hp0 + j] * 12 + r] = g;
+        stv<WT>(P.gpslab + (size_t)P.hp_gslot[hp0 + j] * 12 + r, g);
     }
     __syncthreads();
     const int np2 = nhp * (nhp + 1) / 2, ss0 = P.hv_ss0[h];
@@ -980,7 +995,7 @@ __device__ void heavy_item(const DevProblem& P, int h, double lambda, int schur,
         while (rem >= nhp - a) { rem -= nhp - a; ++a; }
         const double* v = P.Vh + (size_t)(hp0 + a) * 36 + i * 3;
         const double* hb = P.Hpl + (size_t)(cp0 + a + rem) * 36 + jj * 3;
-        P.sslab[(size_t)P.hv_sslot[ss0 + pp] * 144 + e] = v[0] * hb[0] + v[1] * hb[1] + v[2] * hb[2];
+        stv<WT>(P.sslab + (size_t)P.hv_sslot[ss0 + pp] * 144 + e, v[0] * hb[0] + v[1] * hb[1] + v[2] * hb[2]);
     }
 }
 
@@ -993,10 +1008,10 @@ __global__ __launch_bounds__(PRI_THREADS) void k_expand(DevProblem P, int sel, i
     if ((int)blockIdx.x < P.n_smp) {
         const int si = state_idx(P, sel);
         double *Msh = shm, *Nsh = Msh + 144, *MN = Nsh + 216, *part = MN + 216;
-        sample_expand(P, P.gpsb[si], P.camdb[si], blockIdx.x, Msh, Nsh, MN, part, threadIdx.x);
+        sample_expand<false>(P, P.gpsb[si], P.camdb[si], blockIdx.x, Msh, Nsh, MN, part, threadIdx.x);
         return;
     }
-    heavy_item(P, blockIdx.x - P.n_smp, schur ? damping(P, lambda_arg) : 0.0, schur, shm);
+    heavy_item<false>(P, blockIdx.x - P.n_smp, schur ? damping(P, lambda_arg) : 0.0, schur, shm);
 }
 
 // Reduced camera system of one trial, straight from the target-sorted partial slabs (each
@@ -1006,17 +1021,17 @@ __global__ __launch_bounds__(PRI_THREADS) void k_expand(DevProblem P, int sel, i
 //   from the upload and never written);  b_p = sum b partials;  bS = b_p - sum Schur rhs partials.
 // sum of x[(s0 + G q) * W + e] over the slots s0, s0 + G, ... < s1: four loads in flight, combined in
 // a fixed order
-template <int G, int W>
+template <int G, int W, bool SC = false>
 __device__ __forceinline__ double slot_sum(const double* __restrict__ x, int s0, int s1, int e) {
     double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
     int s = s0;
     for (; s + 3 * G < s1; s += 4 * G) {
-        v0 += x[(size_t)s * W + e];
-        v1 += x[(size_t)(s + G) * W + e];
-        v2 += x[(size_t)(s + 2 * G) * W + e];
-        v3 += x[(size_t)(s + 3 * G) * W + e];
+        v0 += ldv<SC>(x + (size_t)s * W + e);
+        v1 += ldv<SC>(x + (size_t)(s + G) * W + e);
+        v2 += ldv<SC>(x + (size_t)(s + 2 * G) * W + e);
+        v3 += ldv<SC>(x + (size_t)(s + 3 * G) * W + e);
     }
-    for (; s < s1; s += G) v0 += x[(size_t)s * W + e];
+    for (; s < s1; s += G) v0 += ldv<SC>(x + (size_t)s * W + e);
     return (v0 + v1) + (v2 + v3);
 }
 
@@ -1077,6 +1092,91 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
             const int rh = (flags & ASM_FULL) ? r : P.rpos[r];
             P.bS[rh] = bpv - t;   // bS = b_p - sum Hpl Dinv bl (factorisation order)
         }
+    }
+}
+
+// The fused flow's assembly work items (k_chol_flow prefix tasks, 256 threads): k_assemble's sums with the
+// slabs read as 16-byte sc1 buffer loads (the expansion tasks published part of them in the same launch),
+// one 16-byte chunk of a slot per thread and the slots of a target split over phases of threads, every
+// thread's loads in flight together (a work item's latency is what the factor tasks wait for); S / bS are
+// stored write-through for the factor tasks.  The fixed phase order makes the sums deterministic.
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const double* p, long long n_doubles) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(8 * n_doubles), 0x00020000);
+}
+// sum over slots s0, s0 + G, ... < s1 of the 16-byte chunk c of W-double slots
+template <int G, int W>
+__device__ __forceinline__ void chunk_sum(__amdgpu_buffer_rsrc_t r, int s0, int s1, int c, double& x, double& y) {
+    double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0, c0 = 0.0, c1 = 0.0, d0 = 0.0, d1 = 0.0;
+    auto ld = [&](int s, double& u, double& v) {
+        const v4u q = __builtin_amdgcn_raw_buffer_load_b128(r, (s * W + 2 * c) * 8, 0, 16);
+        u += __longlong_as_double(((long long)q.y << 32) | q.x);
+        v += __longlong_as_double(((long long)q.w << 32) | q.z);
+    };
+    int s = s0;
+    for (; s + 3 * G < s1; s += 4 * G) {
+        ld(s, a0, a1);
+        ld(s + G, b0, b1);
+        ld(s + 2 * G, c0, c1);
+        ld(s + 3 * G, d0, d1);
+    }
+    for (; s < s1; s += G) ld(s, a0, a1);
+    x = (a0 + b0) + (c0 + d0);
+    y = (a1 + b1) + (c1 + d1);
+}
+__device__ void asm_block_item(const DevProblem& P, int ub, double lambda, double* red) {
+    constexpr int PH = 3;   // slot phases (3 x 72 chunk threads)
+    const int tid = threadIdx.x;
+    const int n = P.npad;
+    const int bi = P.ub_i[ub], bj = P.ub_j[ub];
+    const int c = tid % 72, q = tid / 72;
+    if (q < PH) {
+        double hx, hy, sx, sy;
+        chunk_sum<PH, 144>(slab_rsrc(P.hslab, (long long)P.n_hslots * 144), P.hs0[ub] + q, P.hs0[ub + 1], c, hx, hy);
+        chunk_sum<PH, 144>(slab_rsrc(P.sslab, (long long)P.n_sslots * 144), P.ss0[ub] + q, P.ss0[ub + 1], c, sx, sy);
+        red[q * 144 + 2 * c] = hx - sx;
+        red[q * 144 + 2 * c + 1] = hy - sy;
+    }
+    __syncthreads();
+    if (tid < 144) {
+        const int e = tid;
+        double t = red[e] + red[144 + e] + red[288 + e];
+        if (bi == bj && e % 13 == 0) t += lambda;
+        const int i = e / 12, j = e % 12;
+        const int r = 12 * bj + j, cc = 12 * bi + i;
+        if (bi != bj || j >= i) {
+            const int rh = P.rpos[r], ch = P.rpos[cc];
+            st_sc1(P.S + (size_t)max(rh, ch) * n + min(rh, ch), t);
+        }
+    }
+}
+__device__ void asm_rhs_item(const DevProblem& P, int k, double* red) {
+    constexpr int PH = 42;   // slot phases (42 x 6 chunk threads)
+    const int tid = threadIdx.x;
+    const int c = tid % 6, q = tid / 6;
+    if (q < PH) {
+        double gx, gy, px, py;
+        chunk_sum<PH, 12>(slab_rsrc(P.gslab, (long long)P.n_gslots * 12), P.gs0[k] + q, P.gs0[k + 1], c, gx, gy);
+        chunk_sum<PH, 12>(slab_rsrc(P.gpslab, (long long)P.n_gpslots * 12), P.gps0[k] + q, P.gps0[k + 1], c, px, py);
+        red[q * 12 + 2 * c] = gx;
+        red[q * 12 + 2 * c + 1] = gy;
+        red[PH * 12 + q * 12 + 2 * c] = px;
+        red[PH * 12 + q * 12 + 2 * c + 1] = py;
+    }
+    __syncthreads();
+    if (tid < 12) {
+        double bpv = 0.0, t = 0.0;
+        for (int w = 0; w < PH; ++w) bpv += red[w * 12 + tid];
+        for (int w = 0; w < PH; ++w) t += red[PH * 12 + w * 12 + tid];
+        P.bp[12 * k + tid] = bpv;
+        st_sc1(P.bS + P.rpos[12 * k + tid], bpv - t);   // bS = b_p - sum Hpl Dinv bl (factorisation order)
+    }
+}
+__device__ void asm_pad_item(const DevProblem& P) {   // padding rows: identity, zero rhs
+    for (int r = P.np + (int)threadIdx.x; r < P.npad; r += 256) {
+        const int rh = P.rpos[r];
+        st_sc1(P.S + (size_t)rh * P.npad + rh, 1.0);
+        st_sc1(P.bS + rh, 0.0);
     }
 }
 
@@ -1431,16 +1531,6 @@ __global__ __launch_bounds__(256) void k_chol_step(int n, int pa, int pb, int it
 //   panel j (i = j): the same updates of A(j, j) and b_j -= L(j,p) y_p, then [A_jj; b_j^T] -> L_jj,
 //     y_j and [A_jj; I] -> L_jj^-T on two waves, published for the diagonal tasks below it.
 // The chain from one panel to the next is one hand-off, the last update and one factorisation.
-typedef __attribute__((address_space(1))) unsigned long long gu64_t;
-typedef __attribute__((address_space(1))) int gi32_t;
-
-__device__ __forceinline__ double ld_sc1(const double* p) {
-    return __longlong_as_double((long long)__hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-    __hip_atomic_store((gu64_t*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
 constexpr unsigned CF_SPIN_LIMIT = 1u << 22;   // ~0.5 s of polling before giving up (never expected)
 constexpr int CF_TIMEOUT = 0x7fff0000;          // *info value of a timed-out launch
 
@@ -1479,7 +1569,50 @@ struct CholFlow {
     // band mode (kinds 4, 5): forward / back substitution tasks instead of L^-1 tiles
     double* xpos;        // [npad] x in factorisation order, handed off between back tasks
     int* xready;         // per panel: epoch once x_j is published
+    // fused mode (unpartitioned problems): the task list starts with the pose-sample expansions (kind 8),
+    // the heavy landmarks (kind 9) and the assembly of S / bS (kind 10), so the first panels factor while
+    // later blocks are still being assembled; counters instead of epoch flags (k_lin_schur zeroes them)
+    int fused;
+    int* cnt;            // [0] expansion tasks done, [1 + tile_id] assembly items done per envelope tile,
+                         // [1 + ntile + p] per panel rhs
+    const int* need;     // expected counts, same layout
+    const int* asm_item; // per assembly item: id | type << 28 (0: padding rows, 1: rhs of pose block id, 2: block ub)
+    const int* asm_tgt;  // per assembly item: 4 counter indices (-1: none)
+    int ntile;
+    int sel;             // state buffer of the expansion (SEL_CUR in the queued loop)
+    double lambda;       // damping (LAMBDA_CTL: the controller's)
 };
+
+// lanes 0..5 of wave 0 poll up to six counters (index < 0: none) until they reach their expected counts
+// (relaxed sc1 loads; bounded like cf_wait); the workgroup learns the result
+__device__ __forceinline__ bool cf_wait_cnt(const CholFlow& a, int c0, int c1, int c2, int c3, int c4, int c5,
+                                            int* s_ok) {
+    if (threadIdx.x < 64) {
+        const int l = threadIdx.x;
+        const int c = l == 0 ? c0 : l == 1 ? c1 : l == 2 ? c2 : l == 3 ? c3 : l == 4 ? c4 : l == 5 ? c5 : -1;
+        const int want = c >= 0 ? a.need[c] : 0;
+        bool done = c < 0;
+        bool ok = true;
+        for (unsigned spins = 0;; ++spins) {
+            if (!done) done = __hip_atomic_load((gi32_t*)(a.cnt + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want;
+            if (__all(done)) break;
+            if (spins > CF_SPIN_LIMIT ||
+                ((spins & 255) == 255 &&
+                 (unsigned)__hip_atomic_load((gi32_t*)a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch)) {
+                if (l == 0) {
+                    __hip_atomic_store((gi32_t*)a.abort_flag, (int)a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    *a.info = CF_TIMEOUT;
+                }
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (l == 0) *s_ok = ok ? 1 : 0;
+    }
+    __syncthreads();
+    return *s_ok != 0;
+}
 
 // lanes 0..2 of wave 0 poll up to three flags (null = none) for `epoch` side by side (relaxed, agent
 // scope: one round trip when they are already set, not one per flag); the workgroup learns the result
@@ -1599,7 +1732,7 @@ __device__ __forceinline__ d4 cf_mma_nn(const double (*X)[CNB + 1], const double
     return acc;
 }
 
-__global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
+__global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
     __shared__ double Lt[3][CNB][CNB + 1];       // update operands L(j, p), L(i, p), L(k, p)
     __shared__ double stg[2][2 * CNB][CNB + 1];  // stacked panels of the factoring waves
     __shared__ long long s_ticket;
@@ -1609,9 +1742,9 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
     const int n = a.n;
     auto tile_id = [&](int i, int j) { return a.tbase[i] + j - a.pfh[i]; };
     auto tri_id = [&](int i, int j) { return i * (i + 1) / 2 + j; };
-    auto load_quad = [&](int i, int j, double (&q)[4]) {   // plain loads: S is not written in this launch
+    auto load_quad = [&](int i, int j, double (&q)[4]) {   // sc1 loads: the fused assembly writes S in this launch
 #pragma unroll
-        for (int m = 0; m < 4; ++m) q[m] = a.S[(size_t)(i * CNB + rb * 16 + kq + 4 * m) * n + j * CNB + cb * 16 + lr];
+        for (int m = 0; m < 4; ++m) q[m] = ld_sc1(a.S + (size_t)(i * CNB + rb * 16 + kq + 4 * m) * n + j * CNB + cb * 16 + lr);
     };
     auto stage_quad = [&](double (*T)[CNB + 1], int r0, const double (&q)[4]) {
 #pragma unroll
@@ -1645,6 +1778,38 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
         const int code = a.tasks[t];
         const int j = code & 4095, i = (code >> 12) & 4095;
         const int kind = (code >> 24) & 15;
+        if (kind >= 8) {
+            // ---------------------------------------------------- fused prefix: expansion / assembly
+            const int pl = code & 0xffffff;
+            double* shm = &stg[0][0][0];
+            if (kind == 8 || kind == 9) {   // pose sample pl (N^T M N) / heavy landmark pl, published
+                const int si = state_idx(P, a.sel);
+                if (kind == 8) {
+                    double *Msh = shm, *Nsh = Msh + 144, *MN = Nsh + 216, *part = MN + 216;
+                    sample_expand<true>(P, P.gpsb[si], P.camdb[si], pl, Msh, Nsh, MN, part, tid);
+                } else {
+                    heavy_item<true>(P, pl, damping(P, a.lambda), 1, shm);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (tid == 0) __hip_atomic_fetch_add((gi32_t*)a.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                continue;
+            }
+            // assembly item pl, once every expansion is in; then one add per counter it feeds
+            if (!cf_wait_cnt(a, 0, -1, -1, -1, -1, -1, &s_ok)) return;
+            const int it = a.asm_item[pl], id = it & 0x0fffffff, ty = it >> 28;
+            if (ty == 0) asm_pad_item(P);
+            else if (ty == 1) asm_rhs_item(P, id, shm);
+            else asm_block_item(P, id, damping(P, a.lambda), shm);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid < 4) {
+                const int c = a.asm_tgt[4 * pl + tid];
+                if (c >= 0) __hip_atomic_fetch_add((gi32_t*)(a.cnt + c), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();   // (stg is the next task's LDS)
+            continue;
+        }
         const bool la = (code >> 28) & 1;   // factor task with lookahead over column k = j - 1
         if (kind == 1) {
             // ---------------------------------------------------- L^-1 tile (i, j), i > j:
@@ -1655,9 +1820,10 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
             unsigned long long* tv = (a.tdbg2 && tid == 0 && i >= a.NP - 2) ? a.tdbg2 + 16 * j + 4 * (i - (a.NP - 2)) : nullptr;
             if (tv) tv[0] = __builtin_amdgcn_s_memrealtime();
             const int zr = tid >> 3, zc = (tid & 7) * 4;   // z(i, j): row zr, columns zc .. zc + 3
+            if (a.fused && !cf_wait_cnt(a, 1 + a.ntile + j, -1, -1, -1, -1, -1, &s_ok)) return;
             double bj[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) bj[u] = a.b[j * CNB + zc + u];
+            for (int u = 0; u < 4; ++u) bj[u] = ld_sc1(a.b + j * CNB + zc + u);
             for (int q = a.pl0[t]; q < a.pl0[t + 1]; ++q) {
                 const int k = a.plist[q] & 4095;
                 if (!cf_wait(a, a.lready + tile_id(i, k), k == j ? a.fready + j : a.ivready + tri_id(k, j), &s_ok)) {
@@ -1769,6 +1935,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
                 for (int u = 0; u < 4; ++u) acc += lv[u] * yk[u];
             }
             if (!cf_wait(a, a.fready + i, nullptr, &s_ok)) return;
+            if (a.fused && !cf_wait_cnt(a, 1 + a.ntile + i, -1, -1, -1, -1, -1, &s_ok)) return;
 #pragma unroll
             for (int m = 0; m < 4; ++m) {   // L_ii^-T -> Lt[2] in one round of loads
                 const int e = tid + 256 * m;
@@ -1777,7 +1944,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
             Lt[1][g][r] = acc;
             __syncthreads();
             if (tid < CNB) {
-                double v = a.b[i * CNB + tid];
+                double v = ld_sc1(a.b + i * CNB + tid);
 #pragma unroll
                 for (int u = 0; u < 8; ++u) v -= Lt[1][u][tid];
                 Lt[0][0][tid] = v;
@@ -1900,6 +2067,14 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
         if (tm) tm[0] = __builtin_amdgcn_s_memrealtime();
         unsigned long long* tf = (a.tdbg3 && tid == 0 && t < 4096) ? a.tdbg3 + 8 * t : nullptr;
         if (tf) { tf[0] = __builtin_amdgcn_s_memrealtime(); tf[4] = i | (j << 12) | ((int)la << 24); }
+        if (a.fused) {   // the tiles this task loads (and panel j's rhs) are assembled
+            const int k = j - 1;
+            const bool ikw = la && !diag && a.pfh[i] <= k;
+            if (!cf_wait_cnt(a, 1 + tile_id(j, j), diag ? -1 : 1 + tile_id(i, j), la ? 1 + tile_id(k, k) : -1,
+                             la ? 1 + tile_id(j, k) : -1, ikw ? 1 + tile_id(i, k) : -1,
+                             (diag && a.zv) ? 1 + a.ntile + j : -1, &s_ok))
+                return;
+        }
         double qd[4], qa[4];
         load_quad(j, j, qd);
         if (!diag) load_quad(i, j, qa);
@@ -2054,7 +2229,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a) {
             const int r = tid >> 3, c0 = (tid & 7) * 4;
             double zs = 0.0;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) zs += stg[0][CNB + c0 + u][r] * a.b[j * CNB + c0 + u];
+            for (int u = 0; u < 4; ++u) zs += stg[0][CNB + c0 + u][r] * ld_sc1(a.b + j * CNB + c0 + u);
             zs += __shfl_xor(zs, 1);
             zs += __shfl_xor(zs, 2);
             zs += __shfl_xor(zs, 4);
@@ -2224,6 +2399,10 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
             kf_trial_state(P, kst + (size_t)k * KF_STRIDE, P.kf_hidx[k], ok, kdl[threadIdx.x], kab[threadIdx.x]);
         }
         __syncthreads();
+#ifdef LBA_EXP_PREP_TWICE   // (experiment: the stamps below then time a warm second run of the same code)
+        gp_pair_prep(P, gps, i, kab[0], kab[1], jac);
+        __syncthreads();
+#endif
 #ifndef LBA_EXP_NO_GPPREP
         gp_pair_prep(P, gps, i, kab[0], kab[1], jac, ustamp ? P.tdbg_lin + (size_t)blockIdx.x * 16 + 5 : nullptr);
 #endif
@@ -2603,11 +2782,15 @@ void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hi
     const int n = P.n_asm + P.n_pb;
     if (n) hipLaunchKernelGGL(k_assemble, dim3(n), dim3(144 * RED_GROUPS), 0, s, P, lambda, flags, gate);
 }
-void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
+                           int sel, double lambda) {
     const int n = P.npad;   // multiple of CHOL_NB (identity tail)
     if (n == 0) return;
     if (!P.cf_steps_path) {
         CholFlow a;
+        a.fused = P.cf_fused;
+        a.cnt = P.cf_cnt; a.need = P.cf_need; a.asm_item = P.cf_asm_item; a.asm_tgt = P.cf_asm_tgt;
+        a.ntile = P.cf_ntile; a.sel = sel; a.lambda = lambda;
         a.n = n; a.NP = n / CHOL_NB; a.ntasks = P.cf_ntasks; a.epoch = epoch;
         a.tasks = P.cf_tasks; a.pfh = P.pfirst; a.tbase = P.cf_tbase; a.pl0 = P.cf_pl0;
         a.plist = P.cf_plist;
@@ -2620,9 +2803,9 @@ void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStr
         a.zready = P.cf_zready; a.zv = P.cf_zv;
         a.xpos = P.cf_xpos; a.xready = P.cf_ivready;
         if (e0)
-            hipExtLaunchKernelGGL(k_chol_flow, dim3(min(P.cf_ntasks, 512)), dim3(256), 0, s, e0, e1, 0, a);
+            hipExtLaunchKernelGGL(k_chol_flow, dim3(min(P.cf_ntasks, 512)), dim3(256), 0, s, e0, e1, 0, a, P);
         else
-            hipLaunchKernelGGL(k_chol_flow, dim3(min(P.cf_ntasks, 512)), dim3(256), 0, s, a);
+            hipLaunchKernelGGL(k_chol_flow, dim3(min(P.cf_ntasks, 512)), dim3(256), 0, s, a, P);
         return;
     }
     for (int st = 0; P.cf_steps_path && st < P.n_steps; ++st) {

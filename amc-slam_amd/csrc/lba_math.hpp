@@ -330,11 +330,10 @@ LBA_HD void gp_pair_build(const SE3& Ta, const double* va, const SE3& Tb, const 
     P->t1 = ta;
     P->t2 = tb;
     if (!full) return;
-    // Ad(exp(xi12))^-1 = Ad(exp(xi12)^-1)
-    const SE3 E = se3_exp(P->xi12);
-    const SE3 Ei = se3_inv(E);
+    // Ad(exp(xi12))^-1 = Ad(exp(xi12)^-1) = Ad(T12^-1): exp(log(T12)) is T12 up to rounding, so the
+    // reference's exp + general 6x6 inverse (src/G2oTypes.cc:292) is the adjoint of the inverse pair pose
     double AdI[36], ad2[36];
-    se3_adj(Ei, AdI);
+    se3_adj(se3_inv(T12), AdI);
     matmul(P->G2a, AdI, P->G1a, 6, 6, 6);
     for (int i = 0; i < 36; ++i) P->G1a[i] = -P->G1a[i];
     se3_ad(vb, ad2);
@@ -411,10 +410,13 @@ struct GPSample {
     double N[GPS_N];   // stored transposed: N[c * 6 + l] = N(l, c), so one column is 48 contiguous bytes
 };
 
-LBA_HD void gp_sample_pose(const GPPair& P, double t, double* Rwb, double* twb, double* xi, GPScalars* g) {
+// (dT_out: exp(xi), whose inverse gives the Ad(exp(-xi)) block of N)
+LBA_HD void gp_sample_pose(const GPPair& P, double t, double* Rwb, double* twb, double* xi, GPScalars* g,
+                           SE3* dT_out = nullptr) {
     *g = gp_scalars(P.t1, P.t2, t);
     for (int i = 0; i < 6; ++i) xi[i] = g->p2 * P.v1[i] + g->l1 * P.xi12[i] + g->l2 * P.w2[i];
     const SE3 dT = se3_exp(xi);
+    if (dT_out) *dT_out = dT;
     SE3 T1;
     T1.q = Quat{P.T1q[0], P.T1q[1], P.T1q[2], P.T1q[3]};
     T1.t[0] = P.T1t[0]; T1.t[1] = P.T1t[1]; T1.t[2] = P.T1t[2];
@@ -426,7 +428,8 @@ LBA_HD void gp_sample_pose(const GPPair& P, double t, double* Rwb, double* twb, 
 LBA_HD void gp_sample_build(const GPPair& P, double t, GPSample* S) {
     double xi[6];
     GPScalars g;
-    gp_sample_pose(P, t, S->Rwb, S->twb, xi, &g);
+    SE3 E;
+    gp_sample_pose(P, t, S->Rwb, S->twb, xi, &g, &E);
     // Jr(xi) = [Jl, Q; 0, Jl] with Jl = LeftJacobianRot3(-w), Q = LeftJacobianPose3Q(-xi)
     double Jl[9], Q[9];
     right_jac_blocks(xi, Jl, Q);
@@ -438,9 +441,8 @@ LBA_HD void gp_sample_build(const GPPair& P, double t, GPSample* S) {
             Jr[(3 + i) * 6 + j] = 0.0;
             Jr[(3 + i) * 6 + 3 + j] = Jl[i * 3 + j];
         }
-    // Ad(exp(-xi)) = [R', t'^ R'; 0, R']
-    const double mxi[6] = {-xi[0], -xi[1], -xi[2], -xi[3], -xi[4], -xi[5]};
-    const SE3 Em = se3_exp(mxi);
+    // Ad(exp(-xi)) = Ad(exp(xi)^-1) = [R', t'^ R'; 0, R']
+    const SE3 Em = se3_inv(E);
     double Rm[9], Ht[9], tR[9];
     qmat(Em.q, Rm);
     hat3(Em.t, Ht);

@@ -164,6 +164,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=20250912)
+    ap.add_argument("--sweep-events", choices=("every", "sampled", "off"), default="sampled",
+                    help="HIP events around k_lin_schur / k_chol_flow dispatches in the timed run: every trial, "
+                         "every 10th trial (default: the events idle the device ~5 us each) or none")
     ap.add_argument("--solve", choices=("auto", "band", "dense"), default="auto",
                     help="reduced-system solve: L^-1 tiles (dense) or substitution (band); auto picks by size")
     args = ap.parse_args()
@@ -187,7 +190,8 @@ def main():
     solve_flag = {"auto": 0, "band": amc_lba.abi.FLAG_BAND_SOLVE, "dense": amc_lba.abi.FLAG_DENSE_SOLVE}[args.solve]
     # the timed run records the dispatch timestamps of every k_lin_schur and k_chol_flow launch
     # (LBA_FLAG_TIME_SWEEP): the rooflines below are measured live, per launch, over the timed region
-    flags = amc_lba.abi.FLAG_TIME_SWEEP | solve_flag
+    flags = solve_flag | {"every": amc_lba.abi.FLAG_TIME_SWEEP, "off": 0,
+                          "sampled": amc_lba.abi.FLAG_TIME_SWEEP | amc_lba.abi.FLAG_TIME_SAMPLED}[args.sweep_events]
     ex, full = None, None
     t_setup = time.perf_counter()
     # large set-ups (config 4: ~35 s of window generation, then the engine's preprocessing) report

@@ -58,6 +58,8 @@ extern "C" {
                                      the factorisation instead of through the tiles of L^-1 (default:
                                      chosen by size; large pose systems always take this path) */
 #define LBA_FLAG_DENSE_SOLVE 16   /* force the L^-1-tile solve (pose systems up to 6144 only) */
+#define LBA_FLAG_TIME_SAMPLED 32  /* with LBA_FLAG_TIME_SWEEP in the queued loop: events on one trial in
+                                     ten (the 6th of each ten of a batch), so their idle time costs ~1/10 */
 
 /* LM termination codes in lba_stats.result (OptimizationAlgorithm::SolverResult) */
 #define LBA_RESULT_OK         0

@@ -103,8 +103,8 @@ def update_timeline(lin, n_gp, n_kfb, out):
     gpi = idx[idx < n_gp]
     if len(gpi) and (lin[gpi, 5] > 0).all():   # GP-pair rebuild phases (gp_pair_prep stamps, slots 5..10)
         cols = [14, 5, 6, 7, 8, 9, 10, 15]
-        names = ["KF trial states + log(T12)", "Jr^-1 | exp(xi12) | ad(v2)", "w2, A1", "B1, D",
-                 "sample roles (pose | Jr | Ad)", "N blocks", "tail"]
+        names = ["KF trial states + log(T12) + Ad(T12^-1)", "Jr^-1(xi12), ad(v2)", "w2, A1", "B1, D",
+                 "sample lanes (exp, pose, Ad, Jr)", "N blocks", "tail"]
         d = np.diff(lin[np.ix_(gpi, cols)].astype(np.int64), axis=1) / 100.0
         out.append("   GP-pair rebuild phases (us, mean / max): " +
                    "; ".join(f"{nm} {d[:, k].mean():.2f} / {d[:, k].max():.2f}" for k, nm in enumerate(names)))
