@@ -91,7 +91,9 @@ LBA_HD void qmat(const Quat& q, double* R) {
     R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
     R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
 }
-LBA_HD Quat so3_exp(const double* w, double* theta_out) {
+// (sh / ch: sin and cos of the half angle theta / 2, when theta >= epsilon; one sincos for both, which
+// se3_exp reuses for its V matrix)
+LBA_HD Quat so3_exp(const double* w, double* theta_out, double* sh_out = nullptr, double* ch_out = nullptr) {
     const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
     double imag, real, th;
     if (th2 < kEps * kEps) {
@@ -102,13 +104,18 @@ LBA_HD Quat so3_exp(const double* w, double* theta_out) {
     } else {
         th = sqrt(th2);
         const double h = 0.5 * th;
-        imag = sin(h) / th;
-        real = cos(h);
+        double sh, ch;
+        sincos(h, &sh, &ch);
+        imag = sh / th;
+        real = ch;
+        if (sh_out) { *sh_out = sh; *ch_out = ch; }
     }
     *theta_out = th;
     return Quat{imag * w[0], imag * w[1], imag * w[2], real};
 }
-LBA_HD void so3_log(const Quat& q, double* w, double* theta_out) {
+// (cot_half: cot(theta / 2) = w / |v| outside the small-angle branch: theta = 2 atan(|v| / w), so
+// se3_log needs no sin / cos of the half angle)
+LBA_HD void so3_log(const Quat& q, double* w, double* theta_out, double* cot_half = nullptr) {
     const double sn = q.x * q.x + q.y * q.y + q.z * q.z;
     double f;
     if (sn < kEps * kEps) {
@@ -122,6 +129,7 @@ LBA_HD void so3_log(const Quat& q, double* w, double* theta_out) {
         else
             f = 2.0 * atan(n / q.w) / n;
         *theta_out = f * n;
+        if (cot_half) *cot_half = q.w / n;
     }
     w[0] = f * q.x; w[1] = f * q.y; w[2] = f * q.z;
 }
@@ -146,24 +154,26 @@ LBA_HD SE3 se3_inv(const SE3& a) {
 }
 LBA_HD SE3 se3_exp(const double* a) {
     SE3 r;
-    double th;
-    r.q = so3_exp(a + 3, &th);
+    double th, sh = 0.0, ch = 1.0;
+    r.q = so3_exp(a + 3, &th, &sh, &ch);
     double Om[9], Om2[9], V[9];
     hat3(a + 3, Om);
     mul33(Om, Om, Om2);
     if (th < kEps) {
         qmat(r.q, V);
     } else {
+        // 1 - cos(th) = 2 sin^2(th / 2), sin(th) = 2 sin(th / 2) cos(th / 2): the half-angle pair of
+        // so3_exp (Sophus evaluates cos(th) and sin(th) again; equal up to rounding)
         const double th2 = th * th;
-        const double c1 = (1.0 - cos(th)) / th2, c2 = (th - sin(th)) / (th2 * th);
+        const double c1 = 2.0 * sh * sh / th2, c2 = (th - 2.0 * sh * ch) / (th2 * th);
         for (int i = 0; i < 9; ++i) V[i] = ((i & 3) == 0 ? 1.0 : 0.0) + c1 * Om[i] + c2 * Om2[i];
     }
     mul33v(V, a, r.t);
     return r;
 }
 LBA_HD void se3_log(const SE3& T, double* xi) {
-    double th, w[3];
-    so3_log(T.q, w, &th);
+    double th, w[3], cot_h = 0.0;
+    so3_log(T.q, w, &th, &cot_h);
     xi[3] = w[0]; xi[4] = w[1]; xi[5] = w[2];
     double Om[9], Om2[9], Vi[9];
     hat3(w, Om);
@@ -172,8 +182,7 @@ LBA_HD void se3_log(const SE3& T, double* xi) {
     if (fabs(th) < kEps) {
         c = 1.0 / 12.0;
     } else {
-        const double h = 0.5 * th;
-        c = (1.0 - th * cos(h) / (2.0 * sin(h))) / (th * th);
+        c = (1.0 - 0.5 * th * cot_h) / (th * th);   // (1 - th cos(h) / (2 sin(h))) / th^2, h = th / 2
     }
     for (int i = 0; i < 9; ++i) Vi[i] = ((i & 3) == 0 ? 1.0 : 0.0) - 0.5 * Om[i] + c * Om2[i];
     mul33v(Vi, T.t, xi);
@@ -194,10 +203,23 @@ LBA_HD void se3_adj(const SE3& T, double* A) {
 }
 
 // ---------------------------------------------------------------- Pose3utils
+// The Pose3utils Jacobians below take sin / cos of the rotation angle th = |w| (and cot(th / 2)) from ONE
+// sincos of the half angle: sin(th) = 2 sh ch, cos(th) = 1 - 2 sh^2, cot(th / 2) = ch / sh (the reference
+// evaluates sin, cos and tan separately; the values agree up to rounding).
+struct AngleSC { double th2, th, s, c, sh, ch; };
+LBA_HD AngleSC angle_sc(const double* w) {
+    AngleSC a;
+    a.th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    a.th = sqrt(a.th2);
+    sincos(0.5 * a.th, &a.sh, &a.ch);
+    a.s = 2.0 * a.sh * a.ch;
+    a.c = 1.0 - 2.0 * a.sh * a.sh;
+    return a;
+}
 // LeftJacobianPose3Q (src/Pose3utils.cc:5-24), including the reference's small-angle branch
-LBA_HD void left_jac_q(const double* xi, double* Q) {
+LBA_HD void left_jac_q(const double* xi, const AngleSC& g, double* Q) {
     const double* om = xi + 3;
-    const double th = sqrt(om[0] * om[0] + om[1] * om[1] + om[2] * om[2]);
+    const double th = g.th;
     double X[9], Y[9], XY[9], YX[9], XYX[9], T1[9], T2[9], T3[9], T4[9];
     hat3(om, X);
     hat3(xi, Y);
@@ -206,7 +228,7 @@ LBA_HD void left_jac_q(const double* xi, double* Q) {
     mul33(X, YX, XYX);
     double a, b, c;
     if (fabs(th) > 1e-5) {
-        const double s = sin(th), co = cos(th);
+        const double s = g.s, co = g.c;
         const double t2 = th * th, t3 = t2 * th, t4 = t3 * th, t5 = t4 * th;
         a = (th - s) / t3;
         b = (1.0 - 0.5 * t2 - co) / t4;
@@ -224,16 +246,16 @@ LBA_HD void left_jac_q(const double* xi, double* Q) {
         Q[i] = 0.5 * Y[i] + a * (XY[i] + YX[i] + XYX[i]) - b * (T1[i] + T2[i] - 3.0 * XYX[i]) - c * (T3[i] + T4[i]);
 }
 // LeftJacobianRot3 (:48-59)
-LBA_HD void left_jac_rot3(const double* w, double* J) {
-    const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+LBA_HD void left_jac_rot3(const double* w, const AngleSC& g, double* J) {
+    const double th2 = g.th2;
     if (th2 <= 2.220446049250313e-16) {
         for (int i = 0; i < 9; ++i) J[i] = ((i & 3) == 0) ? 1.0 : 0.0;
         return;
     }
-    const double th = sqrt(th2);
+    const double th = g.th;
     const double d[3] = {w[0] / th, w[1] / th, w[2] / th};
-    const double s = sin(th);
-    const double c1 = s / th, c2 = 1.0 - s / th, c3 = (1.0 - cos(th)) / th;
+    const double s = g.s;
+    const double c1 = s / th, c2 = 1.0 - s / th, c3 = (2.0 * g.sh * g.sh) / th;   // (1 - cos th) / th
     double A[9];
     hat3(w, A);
     for (int i = 0; i < 3; ++i)
@@ -241,15 +263,15 @@ LBA_HD void left_jac_rot3(const double* w, double* J) {
             J[i * 3 + j] = (i == j ? c1 : 0.0) + c2 * d[i] * d[j] + c3 * (A[i * 3 + j] / th);
 }
 // LeftJacobianRot3Inv (:61-73)
-LBA_HD void left_jac_rot3_inv(const double* w, double* J) {
-    const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+LBA_HD void left_jac_rot3_inv(const double* w, const AngleSC& g, double* J) {
+    const double th2 = g.th2;
     if (th2 <= 2.220446049250313e-16) {
         for (int i = 0; i < 9; ++i) J[i] = ((i & 3) == 0) ? 1.0 : 0.0;
         return;
     }
-    const double th = sqrt(th2);
+    const double th = g.th;
     const double d[3] = {w[0] / th, w[1] / th, w[2] / th};
-    const double h = th / 2.0, hc = h * (1.0 / tan(h));
+    const double h = th / 2.0, hc = h * (g.ch / g.sh);   // h / tan(h)
     double A[9];
     hat3(w, A);
     for (int i = 0; i < 3; ++i)
@@ -259,15 +281,17 @@ LBA_HD void left_jac_rot3_inv(const double* w, double* J) {
 // Right Jacobian of SE(3) as blocks: Jr(xi) = LeftJacobianPose3(-xi) = [J, Q; 0, J]
 LBA_HD void right_jac_blocks(const double* xi, double* J, double* Q) {
     const double m[6] = {-xi[0], -xi[1], -xi[2], -xi[3], -xi[4], -xi[5]};
-    left_jac_q(m, Q);
-    left_jac_rot3(m + 3, J);
+    const AngleSC g = angle_sc(m + 3);
+    left_jac_q(m, g, Q);
+    left_jac_rot3(m + 3, g, J);
 }
 // Inverse right Jacobian: Jr^-1(xi) = LeftJacobianPose3Inv(-xi) = [Ji, -Ji Q Ji; 0, Ji] (6x6)
 LBA_HD void right_jac_inv(const double* xi, double* Jr) {
     const double m[6] = {-xi[0], -xi[1], -xi[2], -xi[3], -xi[4], -xi[5]};
     double Q[9], Ji[9], T[9], U[9];
-    left_jac_q(m, Q);
-    left_jac_rot3_inv(m + 3, Ji);
+    const AngleSC g = angle_sc(m + 3);
+    left_jac_q(m, g, Q);
+    left_jac_rot3_inv(m + 3, g, Ji);
     mul33(Ji, Q, T);
     mul33(T, Ji, U);
     for (int i = 0; i < 36; ++i) Jr[i] = 0.0;
