@@ -187,10 +187,9 @@ struct DevProblem {
     double* gslab;          // [n_gslots][12] b_p partials, target-sorted
     double* sslab;          // [n_sslots][144] Schur partial blocks, target-sorted
     double* gpslab;         // [n_gpslots][12] Schur rhs partials, target-sorted
-    double* Lm;             // [npad][npad] Cholesky factor (lower, row-major)
+    double* Lm;             // Cholesky factor, packed envelope tiles like S (lower)
     // dense solve in the factorisation (nested-dissection) order of the panels: position = ppos[natural],
-    // natural = pnat[position]; pfirst = envelope of the permuted matrix; chol_items = work items of the
-    // schedule h_steps (host memory: panel A, panel B, first item, end item per step)
+    // natural = pnat[position]; pfirst = envelope of the permuted matrix
     const int* pfirst;
     const int* ppos;
     const int* pnat;
@@ -198,12 +197,10 @@ struct DevProblem {
     // permutation of the dissection) and back; [npad], the identity on the padding rows
     const int* rpos;
     const int* rnat;
-    const int* chol_items;
-    const int* h_steps;
-    int n_steps;
     int nd_left, nd_right;  // panels of the left / right blocks of the ordering (separator: the rest)
     // dataflow factorisation (k_chol_flow): tasks, tile ids, hand-off flags, ticket counter
-    const int* cf_tasks;
+    const int* cf_tasks;    // j | kind << 24 | lookahead << 28
+    const int* cf_task_i;   // i
     int cf_ntasks;
     const int* cf_tbase;
     double* cf_linv;        // [npad][npad] L^-1 tiles (k_chol_flow)
@@ -217,7 +214,6 @@ struct DevProblem {
     double* cf_zv;          // [NP][NP][CHOL_NB] shares Linv(i, k) b_k of the forward solve
     unsigned long long* cf_head;
     int* cf_abort;
-    int cf_steps_path;      // LBA_CHOL_STEPS: the k_chol_step sequence instead
     // fused flow (unpartitioned): the expansion and the assembly run as k_chol_flow's first tasks
     int cf_fused;
     int* cf_cnt;            // [cf_ncnt] counters, zeroed by k_lin_schur (see CholFlow)
@@ -233,7 +229,10 @@ struct DevProblem {
     double* Hll;
     double* bl;
     double* Dinv;
-    double* S;              // [npad][npad] (factorisation order; natural order for ASM_FULL), padding: identity
+    double* S;              // [n_ztiles][32][32] packed envelope tiles of the reduced system in factorisation
+                            // order (tile (i, j) at (cf_tbase[i] + j - pfirst[i]) * 1024), padding: identity
+    double* Sfull;          // [np][np] natural order, both triangles (ASM_FULL: lba_linearize), allocated on use
+    double* Sdiag;          // [np] natural diagonal of H_pp (ASM_DIAG: computeLambdaInit)
     double* bp;             // [np]
     double* bS;             // [npad] reduced right-hand side b_p - sum Hpl Dinv bl (factorisation order)
     double* xsol;           // [npad] solution (natural order)
@@ -257,14 +256,14 @@ struct DevProblem {
     // reduced system, b_p and the trial sums are summed over the ranks by the caller's all-reduce
     int part_rank, part_n;  // rank / ranks (part_n 0: not partitioned)
     double* red4;           // [4] trial sums of this rank, all-reduced before k_finalize reads them
-    double* env_buf;        // [n_env] envelope tiles of S, then bS [npad], then b_p [np] (all-reduce buffer)
+    double* env_buf;        // [n_env] bS [npad], then b_p [np] (all-reduce buffer; S is all-reduced in place)
     long long n_env;
     // diagnostics (LBA_PHASE_TIMING=<file>): per-workgroup clock64() stamps at phase boundaries
     unsigned long long* tdbg_lin;     // [n_tiles][16] k_linearize
     unsigned long long* tdbg_schur;   // [n_tiles][16] k_schur
-    unsigned long long* tdbg_chol;    // [npad / CHOL_NB][16] k_chol_step (workgroup 0 of each panel)
+    unsigned long long* tdbg_chol;    // [npad / CHOL_NB][16] k_chol_flow panel tasks
     unsigned long long* tdbg_cf;      // [CF_TDBG_TASKS][8] k_chol_flow factor tasks: stamps, i, j
-    unsigned long long* tdbg_bs;      // [npad / CHOL_NB][16] k_chol_backsolve (per block)
+    unsigned long long* tdbg_bs;      // [npad / CHOL_NB][16] k_chol_flow L^-1 tasks of the last rows
 };
 
 // launchers (lba_kernels.hip).  sel: state buffer (0 / 1, or SEL_CUR / SEL_NEXT from the controller);
@@ -283,7 +282,7 @@ void launch_lin_schur(const DevProblem& P, int sel, int gate, double lambda, int
 // pose-sample expansion (N^T M N into the Hpp / b_p slabs) and the heavy landmarks (merge of their segments;
 // with schur also their elimination)
 void launch_expand(const DevProblem& P, int sel, int gate, double lambda, int schur, hipStream_t s);
-enum { ASM_SCHUR = 1, ASM_FULL = 2 };
+enum { ASM_SCHUR = 1, ASM_FULL = 2, ASM_DIAG = 4 };
 void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hipStream_t s);
 // (fused flow: sel / lambda of the expansion and assembly it runs first)
 void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s, hipEvent_t e0 = nullptr,

@@ -86,8 +86,7 @@ struct lba_problem {
     int* h_log = nullptr;         // host-mapped [HLOG_CAP]: per queued trial, 1 if it relinearised
     int* d_hlog = nullptr;
     std::vector<hipEvent_t> qev;  // queued optimisation, LBA_FLAG_TIME_SWEEP: 2 events per trial
-    std::vector<int> chol_steps;  // dense-solve schedule: (panel A, panel B, first item, end item) per step
-    int s_layout = 0;             // layout last assembled into S: 0 factorisation order, 1 natural (full)
+    size_t s_bytes = 0;           // device bytes of S + L (packed envelopes)
     unsigned long long fin_seq = 0;
     unsigned cf_epoch = 0;        // launches of the dataflow factorisation (its flags hold the epoch)
     bool gps_fresh[2] = {false, false};   // state buffer s has its pose samples with Jacobian factors
@@ -547,8 +546,6 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         else if (i % 12 < 6) p->pose_ext[i] = 12 * n_pb_kf + 6 * ((i - 12 * n_pb_kf) / 12) + i % 12;
     // the extrinsic block an observation links (EdgeMonoGPExtrinsic's vertex 3), or -1
     auto ext_block = [&](const lba_obs& o) { return o.kind == LBA_MONO_GP && cam_slot[o.cam] >= 0 ? p->kf_hidx[cam_slot[o.cam]] : -1; };
-    if (p->np > 4095 * CHOL_NB)
-        throw ApiError{LBA_E_LIMIT, "pose system larger than 131040 (10920 keyframes) not supported"};
     if ((p->cfg.flags & LBA_FLAG_DENSE_SOLVE) && p->np > CF_DENSE_MAX_NP * CHOL_NB)
         throw ApiError{LBA_E_LIMIT, "the L^-1-tile solve is limited to pose systems of 6144"};
     const std::vector<int>& H = p->kf_hidx;
@@ -1395,42 +1392,21 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 const int i = std::max(ppos[P], ppos[Q]), j = std::min(ppos[P], ppos[Q]);
                 pfh[i] = std::min(pfh[i], j);
             }
-        // launch schedule: steps of (panel A, panel B); work items per step: a diagonal item per panel
-        // (publishes L_pp, L_pp^-T, y_p) and every trailing tile inside the envelope with the mask
-        // of the step's panels that update it.  Item: i | j << 10 | mask << 20 | diag << 22.
         // solve path: L^-1 tiles (the solve has no substitution chain, but L^-1 of a banded factor is
         // dense: O(n^3) work) up to CF_AUTO_BAND_NP panels, substitution tasks above (or when asked)
         const bool band = !(p->cfg.flags & LBA_FLAG_DENSE_SOLVE) &&
                           ((p->cfg.flags & LBA_FLAG_BAND_SOLVE) || NP > CF_AUTO_BAND_NP);
         D.cf_band = band ? 1 : 0;
-        std::vector<int> steps, items;
-        auto add_step = [&](int pa, int pb) {
-            const int it0 = (int)items.size();
-            if (pa >= 0) items.push_back(pa | (pa << 10) | (1 << 20) | (1 << 22));
-            if (pb >= 0) items.push_back(pb | (pb << 10) | (2 << 20) | (1 << 22));
-            const int pmin = pa >= 0 ? pa : pb;
-            for (int i = pmin + 1; i < NP; ++i)
-                for (int j = pmin + 1; j <= i; ++j) {
-                    int mask = 0;
-                    if (pa >= 0 && j > pa && pfh[i] <= pa && pfh[j] <= pa) mask |= 1;
-                    if (pb >= 0 && j > pb && pfh[i] <= pb && pfh[j] <= pb) mask |= 2;
-                    if (mask) items.push_back(i | (j << 10) | (mask << 20));
-                }
-            steps.push_back(pa); steps.push_back(pb); steps.push_back(it0); steps.push_back((int)items.size());
-        };
-        if (!band) {   // (the k_chol_step schedule: O(NP^3) to build, dense systems only)
-            for (int k = 0; k < std::max(nl, nr); ++k) add_step(k < nl ? k : -1, k < nr ? nl + k : -1);
-            for (int k = 0; k < ns; ++k) add_step(nl + nr + k, -1);
-        }
-        p->chol_steps = steps;
-        D.h_steps = p->chol_steps.data();
-        D.n_steps = (int)steps.size() / 4;
-        D.chol_items = dupload(p, items);
         // dataflow factorisation + solve (k_chol_flow), tasks in topological order: per column c the
         // factor tiles (c..NP-1, c) (the diagonal first), then the L^-1 tiles of row c; at the end one
-        // solution task per panel.  Task: j | i << 12 | kind << 24, with a list of panels per task.
+        // solution task per panel.  Task: (j, i, kind), with a list of panels per task.
         {
-            std::vector<int> tbase(NP + 1, 0), tasks;
+            // task t: tasks[t] = j | kind << 24 | lookahead << 28, task_i[t] = i
+            std::vector<int> tbase(NP + 1, 0), tasks, task_i;
+            auto add_task = [&](int j, int i, int kind, int la) {
+                tasks.push_back(j | (kind << 24) | (la << 28));
+                task_i.push_back(i);
+            };
             for (int i = 0; i < NP; ++i) tbase[i + 1] = tbase[i] + (i - pfh[i] + 1);
             std::vector<int> uord;   // panel update order = the order the panels complete
             for (int k = 0; k < std::max(nl, nr); ++k) {
@@ -1462,23 +1438,23 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                         if (rank[pp] > rank[k]) la = false;
                     std::vector<int> ps;
                     if (la) {
-                        tasks.push_back(c | (i << 12) | (1 << 28));
+                        add_task(c, i, 0, 1);
                         for (int pp = std::min(std::min(pfh[c], pfh[i]), pfh[k]); pp < k; ++pp) ps.push_back(pp);
                         std::sort(ps.begin(), ps.end(), [&](int x, int y) { return rank[x] < rank[y]; });
                         for (int pp : ps) {   // only panels that update a held tile; row i only where it is used
                             const bool fj = pp >= pfh[c], fk = pp >= pfh[k], fi = pp >= pfh[i] && (fj || fk);
-                            if (fj || fk) plist.push_back(pp | (fi << 12) | (fj << 13) | (fk << 14));
+                            if (fj || fk) plist.push_back(pp | (fi << 24) | (fj << 25) | (fk << 26));
                         }
                     } else {
-                        tasks.push_back(c | (i << 12));
+                        add_task(c, i, 0, 0);
                         for (int pp = pfh[c]; pp < c; ++pp) ps.push_back(pp);
                         std::sort(ps.begin(), ps.end(), [&](int x, int y) { return rank[x] < rank[y]; });
-                        for (int pp : ps) plist.push_back(pp | ((pp >= pfh[i]) << 12));
+                        for (int pp : ps) plist.push_back(pp | ((pp >= pfh[i]) << 24));
                     }
                     pl0.push_back((int)plist.size());
                 }
                 if (band) {   // forward substitution y_c = L_cc^-1 (b_c - sum_k L(c,k) y_k), k in update order
-                    tasks.push_back(c | (c << 12) | (4 << 24));
+                    add_task(c, c, 4, 0);
                     std::vector<int> ks;
                     for (int k = pfh[c]; k < c; ++k) ks.push_back(k);
                     std::sort(ks.begin(), ks.end(), [&](int x, int y) { return rank[x] < rank[y]; });
@@ -1488,12 +1464,12 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 }
                 for (int j = 0; j < c; ++j) {    // L^-1 tiles of row c: terms k ascending
                     if (!nz[c][j]) continue;
-                    tasks.push_back(j | (c << 12) | (1 << 24));
+                    add_task(j, c, 1, 0);
                     for (int k = std::max(j, pfh[c]); k < c; ++k)
                         if (nz[k][j]) plist.push_back(k);
                     pl0.push_back((int)plist.size());
                 }
-                tasks.push_back(c | (c << 12) | (3 << 24));   // y_c: the nonzero tiles of row c of L^-1
+                add_task(c, c, 3, 0);   // y_c: the nonzero tiles of row c of L^-1
                 for (int k = 0; k <= c; ++k)
                     if (nz[c][k]) plist.push_back(k);
                 pl0.push_back((int)plist.size());
@@ -1507,7 +1483,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     for (int j = pfh[i]; j < i; ++j) rows_of[j].push_back(i);
                 for (int cq = NP - 1; cq >= 0; --cq) {
                     const int j = uord[cq];
-                    tasks.push_back(j | (j << 12) | (5 << 24));
+                    add_task(j, j, 5, 0);
                     std::vector<int>& is = rows_of[j];
                     std::sort(is.begin(), is.end(), [&](int x, int y) { return rank[x] > rank[y]; });
                     for (int i : is) plist.push_back(i);
@@ -1515,20 +1491,19 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 }
             }
             for (int j = 0; !band && j < NP; ++j) {      // solution blocks: rows i >= j of column j of L^-1
-                tasks.push_back(j | (j << 12) | (2 << 24));
+                add_task(j, j, 2, 0);
                 for (int i = j; i < NP; ++i)
                     if (nz[i][j]) plist.push_back(i);
                 pl0.push_back((int)plist.size());
             }
-            if (NP > 4095) throw ApiError{LBA_E_LIMIT, "internal: too many panels for the dataflow factorisation"};
+            if (NP >= (1 << 24)) throw ApiError{LBA_E_LIMIT, "internal: too many panels for the dataflow factorisation"};
             // fused flow (LBA_FLOW_FUSED=1; one problem, not partitioned): the
             // pose-sample expansions and heavy landmarks, then the assembly items (padding rows, rhs per pose
             // block, S blocks) in the order the columns they feed are factored, ahead of the factor tasks; a
             // counter per envelope tile / panel rhs tells the factor tasks when their operands are assembled
             // (the assembly items address the slabs with 32-bit buffer offsets)
             const long long slab_max = 8LL * std::max((long long)n_hslots * 144, (long long)n_sslots * 144);
-            const bool fused = p->part_n == 0 && !(!band && std::getenv("LBA_CHOL_STEPS")) &&
-                               std::getenv("LBA_FLOW_FUSED") && slab_max < (1LL << 31);
+            const bool fused = p->part_n == 0 && std::getenv("LBA_FLOW_FUSED") && slab_max < (1LL << 31);
             D.cf_fused = fused ? 1 : 0;
             const int ntile = tbase[NP];
             D.cf_ntile = ntile;
@@ -1603,6 +1578,9 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 std::vector<int> all(prefix);
                 all.insert(all.end(), tasks.begin(), tasks.end());
                 tasks.swap(all);
+                std::vector<int> alli(prefix.size(), 0);
+                alli.insert(alli.end(), task_i.begin(), task_i.end());
+                task_i.swap(alli);
                 std::vector<int> pl(prefix.size(), 0);
                 pl.insert(pl.end(), pl0.begin(), pl0.end());
                 pl0.swap(pl);
@@ -1613,6 +1591,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 HIPCHK(hipMemset(D.cf_cnt, 0, sizeof(int) * D.cf_ncnt));
             }
             D.cf_tasks = dupload(p, tasks);
+            D.cf_task_i = dupload(p, task_i);
             D.cf_ntasks = (int)tasks.size();
             D.cf_tbase = dupload(p, tbase);
             // band mode: no L^-1 tiles; ivready then flags the back-substituted blocks x_j
@@ -1636,7 +1615,6 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             HIPCHK(hipMemset(D.cf_dready, 0, sizeof(int) * std::max(NP, 1)));
             HIPCHK(hipMemset(D.cf_head, 0, sizeof(unsigned long long)));
             HIPCHK(hipMemset(D.cf_abort, 0, sizeof(int)));
-            D.cf_steps_path = (!band && std::getenv("LBA_CHOL_STEPS")) ? 1 : 0;
         }
         D.pfirst = dupload(p, pfh);
         D.ppos = dupload(p, ppos);
@@ -1656,7 +1634,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         D.part_rank = p->part_rank;
         D.part_n = p->part_n;
         if (p->part_n > 0) {
-            D.n_env = (long long)ztiles.size() * CHOL_NB * CHOL_NB + npad + p->np;
+            D.n_env = (long long)npad + p->np;   // bS, b_p (S is all-reduced in place)
             D.env_buf = dalloc<double>(p, (size_t)D.n_env);
             D.red4 = dalloc<double>(p, 4);
         }
@@ -1664,7 +1642,11 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         D.n_asm = (int)asm_list.size();
     }
     D.npad = npad;
-    D.Lm = dalloc<double>(p, (size_t)npad * npad + 1);
+    // S and L: packed envelope tiles (memory O(envelope); the natural-order dense H_pp of lba_linearize
+    // goes to Sfull, allocated on first use)
+    const size_t n_env_doubles = (size_t)D.n_ztiles * CHOL_NB * CHOL_NB;
+    p->s_bytes = 2 * n_env_doubles * sizeof(double);
+    D.Lm = dalloc<double>(p, n_env_doubles + 1);
     D.LinvT = dalloc<double>(p, (size_t)npad * CHOL_NB + 1);
     D.Hpl = dalloc<double>(p, (size_t)36 * std::max(n_pairs + n_segpairs, 1));   // canonical pairs, then segment pairs
     D.Hll = dalloc<double>(p, (size_t)9 * std::max(nl + n_seg, 1));               // landmarks, then segments
@@ -1672,17 +1654,18 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.n_lm_all = nl + n_seg;
     D.bl = dalloc<double>(p, (size_t)3 * std::max(nl + n_seg, 1));
     D.Dinv = dalloc<double>(p, (size_t)9 * std::max(nl, 1));
-    D.S = dalloc<double>(p, (size_t)npad * npad + 1);
+    D.S = dalloc<double>(p, n_env_doubles + 1);
+    D.Sfull = nullptr;
+    D.Sdiag = dalloc<double>(p, (size_t)p->np + 1);
     D.bp = dalloc<double>(p, p->np + 1);
     D.xsol = dalloc<double>(p, npad + 1);
     D.bS = dalloc<double>(p, npad + 1);
     HIPCHK(hipMemset(D.bS, 0, sizeof(double) * (npad + 1)));
     D.yv = dalloc<double>(p, npad + 1);
     // S and L start zero (k_assemble writes the identity of the padding rows every time)
-    HIPCHK(hipMemset(D.S, 0, sizeof(double) * ((size_t)npad * npad + 1)));
-    HIPCHK(hipMemset(D.Lm, 0, sizeof(double) * ((size_t)npad * npad + 1)));
+    HIPCHK(hipMemset(D.S, 0, sizeof(double) * (n_env_doubles + 1)));
+    HIPCHK(hipMemset(D.Lm, 0, sizeof(double) * (n_env_doubles + 1)));
     HIPCHK(hipMemset(D.xsol, 0, sizeof(double) * (npad + 1)));
-    p->s_layout = 0;
     D.x = dalloc<double>(p, p->np + 3 * (size_t)nl + 1);
     HIPCHK(hipMemset(D.x, 0, sizeof(double) * (p->np + 3 * (size_t)nl + 1)));   // BlockSolver::_x before any solve
     const int nchi = n_tiles + D.n_prior + D.n_vel + D.n_eprior;
@@ -1761,18 +1744,18 @@ void finalize_and_wait(lba_problem* p, bool sync, int eval_sel = -1) {
 }
 
 
-// S holds either the factorisation-order lower triangle (trials) or the natural full matrix
-// (ASM_FULL: lba_linearize / lambda init); switching layouts clears it first, since each layout only
-// rewrites its own pattern
+// k_assemble into S (ASM_SCHUR: the factorisation-order packed envelope a trial factors), Sfull (ASM_FULL:
+// the natural dense H_pp of lba_linearize) or Sdiag (ASM_DIAG: its diagonal, computeLambdaInit)
 void assemble_layout(lba_problem* p, double lambda, int flags, int gate = GATE_NONE, bool launch = true) {
-    const int want = (flags & ASM_FULL) ? 1 : 0;
-    if (want != p->s_layout || want == 1)
-        HIPCHK(hipMemsetAsync(p->D.S, 0, sizeof(double) * ((size_t)p->D.npad * p->D.npad), p->stream));
-    p->s_layout = want;
+    if (flags & ASM_FULL) {   // the dense natural-order H_pp (lba_linearize): its own buffer, made on first use
+        if (!p->D.Sfull) p->D.Sfull = dalloc<double>(p, (size_t)p->np * p->np + 1);
+        HIPCHK(hipMemsetAsync(p->D.Sfull, 0, sizeof(double) * ((size_t)p->np * p->np), p->stream));
+    }
     if (!launch) return;   // (the fused flow assembles S itself)
     launch_assemble(p->D, lambda, flags, gate, p->stream);
     if ((flags & ASM_SCHUR) && p->part_n > 0) {   // sum the ranks' reduced systems
         launch_env_pack(p->D, 0, gate, p->stream);
+        preduce(p, p->D.S, (int64_t)p->D.n_ztiles * CHOL_NB * CHOL_NB);   // the packed envelope, in place
         preduce(p, p->D.env_buf, p->D.n_env);
         launch_env_pack(p->D, 1, gate, p->stream);
     }
@@ -1831,15 +1814,14 @@ double eval_current(lba_problem* p) {
 double lambda_init(lba_problem* p) {   // computeLambdaInit (levenberg.cpp:171-185)
     if (p->cfg.lambda_init > 0) return p->cfg.lambda_init;
     const DevProblem& D = p->D;
-    assemble_layout(p, 0.0, ASM_FULL);
-    std::vector<double> S((size_t)p->np * p->np), Hll(9 * (size_t)std::max(D.n_lm, 1));
+    assemble_layout(p, 0.0, ASM_DIAG);
+    std::vector<double> Sd((size_t)p->np + 1), Hll(9 * (size_t)std::max(D.n_lm, 1));
     if (p->np)
-        HIPCHK(hipMemcpy2DAsync(S.data(), p->np * sizeof(double), D.S, D.npad * sizeof(double),
-                                p->np * sizeof(double), p->np, hipMemcpyDeviceToHost, p->stream));
+        HIPCHK(hipMemcpyAsync(Sd.data(), D.Sdiag, p->np * sizeof(double), hipMemcpyDeviceToHost, p->stream));
     HIPCHK(hipMemcpyAsync(Hll.data(), D.Hll, 9 * (size_t)D.n_lm * sizeof(double), hipMemcpyDeviceToHost, p->stream));
     HIPCHK(hipStreamSynchronize(p->stream));
     double m = 0.0;
-    for (int i = 0; i < p->np; ++i) m = std::max(m, std::fabs(S[(size_t)i * p->np + i]));
+    for (int i = 0; i < p->np; ++i) m = std::max(m, std::fabs(Sd[i]));
     for (int l = 0; l < D.n_lm; ++l)
         for (int d = 0; d < 3; ++d) m = std::max(m, std::fabs(Hll[9 * (size_t)l + 4 * d]));
     return p->cfg.tau * m;
@@ -1906,7 +1888,7 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
             if (issued == 0 && p->cfg.lambda_init <= 0) {   // computeLambdaInit reads H_pp / Hll of the start
                 launch_lin_schur(D, SEL_CUR, GATE_TRIAL, 0.0, LS_EDGES, p->stream);
                 launch_expand(D, SEL_CUR, GATE_TRIAL, 0.0, 0, p->stream);
-                assemble_layout(p, 0.0, ASM_FULL);
+                assemble_layout(p, 0.0, ASM_DIAG);
                 launch_lambda_init(D, p->cfg.tau, p->stream);
             }
             launch_lin_schur(D, SEL_CUR, GATE_TRIAL, LAMBDA_CTL, LS_SCHUR | LS_EDGES, p->stream, qe ? qe[0] : nullptr,
@@ -2352,6 +2334,13 @@ int lba_setup_host_profile(const lba_config* cfg, const lba_kf* kfs, int32_t n_k
     return LBA_OK;
 }
 
+int64_t lba_device_bytes(const lba_problem* p) {
+    if (!p) return LBA_E_ARG;
+    int64_t b = 0;
+    for (size_t k = 0; k < p->alloc_cursor && k < p->allocs.size(); ++k) b += (int64_t)p->allocs[k].bytes;
+    return b;
+}
+
 int lba_solver_info(const lba_problem* p, int32_t out[5]) {
     if (!p || !out || !p->has_problem) return LBA_E_ARG;
     out[0] = p->nd_tail;
@@ -2751,8 +2740,8 @@ int lba_linearize(lba_problem* p, double* residuals, double* H_pp, double* b, do
         std::vector<double> bp(np + 1), bl(3 * (size_t)nl + 1), hll(9 * (size_t)nl + 1), res(3 * (size_t)p->n_obs + 1);
         std::vector<double> hpp(H_pp ? (size_t)np * np + 1 : 1);
         if (H_pp && np)
-            HIPCHK(hipMemcpy2DAsync(hpp.data(), np * sizeof(double), D.S, D.npad * sizeof(double), np * sizeof(double),
-                                    np, hipMemcpyDeviceToHost, p->stream));
+            HIPCHK(hipMemcpyAsync(hpp.data(), D.Sfull, (size_t)np * np * sizeof(double), hipMemcpyDeviceToHost,
+                                  p->stream));
         HIPCHK(hipMemcpyAsync(bp.data(), D.bp, np * sizeof(double), hipMemcpyDeviceToHost, p->stream));
         HIPCHK(hipMemcpyAsync(bl.data(), D.bl, 3 * (size_t)nl * sizeof(double), hipMemcpyDeviceToHost, p->stream));
         HIPCHK(hipMemcpyAsync(hll.data(), D.Hll, 9 * (size_t)nl * sizeof(double), hipMemcpyDeviceToHost, p->stream));

@@ -100,6 +100,12 @@ __device__ __forceinline__ double damping(const DevProblem& P, double lambda) {
     return lambda < 0.0 ? P.ctl->lambda : lambda;
 }
 
+// element (r, c), r >= c, of the reduced system in factorisation order inside its packed envelope tile
+__device__ __forceinline__ size_t s_elem(const DevProblem& P, int r, int c) {
+    const int ti = r / CHOL_NB, tj = c / CHOL_NB;
+    return (size_t)(P.cf_tbase[ti] + tj - P.pfirst[ti]) * (CHOL_NB * CHOL_NB) + (r % CHOL_NB) * CHOL_NB + (c % CHOL_NB);
+}
+
 __device__ __forceinline__ SE3 load_se3(const double* k) {
     SE3 T;
     T.q = Quat{k[0], k[1], k[2], k[3]};
@@ -659,11 +665,8 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
         }
         if (P.cf_fused)   // the fused flow's expansion / assembly counters
             for (int z = blockIdx.x * LS_THREADS + tid; z < P.cf_ncnt; z += gridDim.x * LS_THREADS) P.cf_cnt[z] = 0;
-        for (int z = blockIdx.x; z < P.n_ztiles; z += gridDim.x) {
-            const int zi = P.ztiles[z] & 0xffff, zj = P.ztiles[z] >> 16;
-            for (int t = tid; t < CHOL_NB * CHOL_NB; t += LS_THREADS)
-                P.S[(size_t)(zi * CHOL_NB + t / CHOL_NB) * P.npad + zj * CHOL_NB + t % CHOL_NB] = 0.0;
-        }
+        const size_t nz = (size_t)P.n_ztiles * CHOL_NB * CHOL_NB;   // (S is the packed envelope)
+        for (size_t z = (size_t)blockIdx.x * LS_THREADS + tid; z < nz; z += (size_t)gridDim.x * LS_THREADS) P.S[z] = 0.0;
     }
     if ((int)blockIdx.x >= P.n_tiles) {   // motion-prior / velocity / extrinsic-prior edge items
         edge_item<LS_THREADS>(P, sel, blockIdx.x - P.n_tiles, tid, U);
@@ -1054,20 +1057,22 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
             if (bi == bj && e % 13 == 0 && P.part_rank == 0) t += lambda;   // damping: added once over the ranks
             const int i = e / 12, j = e % 12;
             const int r = 12 * bj + j, c = 12 * bi + i;   // element (row r, col c) of S, r >= c in blocks
-            if (flags & ASM_FULL) {                       // natural order, both triangles
-                P.S[(size_t)r * n + c] = t;
-                P.S[(size_t)c * n + r] = t;
+            if (flags & ASM_FULL) {                       // natural order, both triangles (dense np x np)
+                P.Sfull[(size_t)r * P.np + c] = t;
+                P.Sfull[(size_t)c * P.np + r] = t;
+            } else if (flags & ASM_DIAG) {                // the natural diagonal only (computeLambdaInit)
+                if (bi == bj && i == j) P.Sdiag[r] = t;
             } else if (bi != bj || j >= i) {               // factorisation order, lower triangle: one
                 // write per unordered pair (the natural-lower entry; a diagonal block's partial sums
                 // are not bitwise symmetric, so writing both would race)
                 const int rh = P.rpos[r], ch = P.rpos[c];
-                P.S[(size_t)max(rh, ch) * n + min(rh, ch)] = t;
+                P.S[s_elem(P, max(rh, ch), min(rh, ch))] = t;
             }
         }
-        if (blockIdx.x == 0 && P.part_rank == 0)   // padding rows: identity (rank 0 of a partition)
+        if ((flags & ASM_SCHUR) && blockIdx.x == 0 && P.part_rank == 0)   // padding rows: identity (rank 0)
             for (int r = P.np + tid; r < n; r += 144 * RED_GROUPS) {
-                const int rh = (flags & ASM_FULL) ? r : P.rpos[r];
-                P.S[(size_t)rh * n + rh] = 1.0;
+                const int rh = P.rpos[r];
+                P.S[s_elem(P, rh, rh)] = 1.0;
                 P.bS[rh] = 0.0;
             }
     } else {
@@ -1127,7 +1132,6 @@ __device__ __forceinline__ void chunk_sum(__amdgpu_buffer_rsrc_t r, int s0, int 
 __device__ void asm_block_item(const DevProblem& P, int ub, double lambda, double* red) {
     constexpr int PH = 3;   // slot phases (3 x 72 chunk threads)
     const int tid = threadIdx.x;
-    const int n = P.npad;
     const int bi = P.ub_i[ub], bj = P.ub_j[ub];
     const int c = tid % 72, q = tid / 72;
     if (q < PH) {
@@ -1146,7 +1150,7 @@ __device__ void asm_block_item(const DevProblem& P, int ub, double lambda, doubl
         const int r = 12 * bj + j, cc = 12 * bi + i;
         if (bi != bj || j >= i) {
             const int rh = P.rpos[r], ch = P.rpos[cc];
-            st_sc1(P.S + (size_t)max(rh, ch) * n + min(rh, ch), t);
+            st_sc1(P.S + s_elem(P, max(rh, ch), min(rh, ch)), t);
         }
     }
 }
@@ -1175,22 +1179,19 @@ __device__ void asm_rhs_item(const DevProblem& P, int k, double* red) {
 __device__ void asm_pad_item(const DevProblem& P) {   // padding rows: identity, zero rhs
     for (int r = P.np + (int)threadIdx.x; r < P.npad; r += 256) {
         const int rh = P.rpos[r];
-        st_sc1(P.S + (size_t)rh * P.npad + rh, 1.0);
+        st_sc1(P.S + s_elem(P, rh, rh), 1.0);
         st_sc1(P.bS + rh, 0.0);
     }
 }
 
 // ------------------------------------------------------------------------------------------------
-// Dense Cholesky S = L L^T of the reduced camera system in its factorisation order (panels
-// permuted [left | right | separator] by a one-level nested dissection of the band, lba_host.hip),
-// right-looking, one launch per step of up to two panels that do not update each other.  The
-// system is padded to a multiple of CNB with an identity tail, so every panel is exactly CNB wide
-// and all loops below are compile-time.  Every workgroup factors the stacked panels it needs
-// itself (one row per lane, pivots and column broadcast by readlane), which yields L_pp, the
-// panel rows of its tiles and y_p = L_pp^-1 b_p in one pass, then updates its tile, so a launch has
-// no inter-workgroup communication.  The factor goes to Lm (row-major) with the inverse diagonal
-// blocks in LinvT; the running right-hand side b is forward-substituted on the fly (y -> yv).  A
-// non-positive pivot sets *info (the LDLT !isPositive failure of linear_solver_dense.h:108-112).
+// Dense Cholesky S = L L^T of the reduced camera system in its factorisation order (panels permuted
+// by the nested dissection of lba_host.hip), as ONE dataflow launch (k_chol_flow below).  S and L are
+// stored as packed envelope tiles: tile (i, j), pfirst[i] <= j <= i, is 32 x 32 doubles row-major at
+// tile_id(i, j) * 1024 with tile_id = tbase[i] + j - pfirst[i] (memory O(envelope), not npad^2).  The
+// system is padded to a multiple of CNB with an identity tail, so every panel is exactly CNB wide and
+// the panel code below is compile-time.  A non-positive pivot sets *info (the LDLT !isPositive failure
+// of linear_solver_dense.h:108-112).
 constexpr int CNB = CHOL_NB;
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
@@ -1352,181 +1353,15 @@ __device__ __forceinline__ void cross_update(double (&row)[CNB], double (*st)[CN
     for (int c = 0; c < 16; ++c) row[16 + c] -= st[lane][16 + c];
 }
 
-// Load one wave's stacked 64 x 32 panel (rows 0..31: the diagonal block of panel p; rows 32..63:
-// the panel rows of tile `ti` (ti >= 0), b_p^T in row 32 (ti == -1), the identity (ti == -2) or zero
-// (ti == -3)) coalesced through LDS (16 lanes x 16 B per row, 4 rows per instruction), then every lane
-// takes its row.
-__device__ __forceinline__ void load_stacked(const double* __restrict__ A, const double* __restrict__ b, int n, int p,
-                                             int ti, double (*st)[CNB + 1], int lane, double (&row)[CNB]) {
-    const int cq = (lane & 15) * 2;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int rr = 4 * k + (lane >> 4), r32 = rr & (CNB - 1);
-        const double* src = A + (size_t)(p * CNB + r32) * n + p * CNB;   // always valid (diagonal rows)
-        bool use = rr < CNB;
-        if (rr >= CNB && ti >= 0) {
-            src = A + (size_t)(ti * CNB + r32) * n + p * CNB;
-            use = true;
-        } else if (rr == CNB && ti == -1) {
-            src = b + p * CNB;
-            use = true;
-        }
-        const double2 v = *reinterpret_cast<const double2*>(src + cq);
-        const double idv = (ti == -2) ? 1.0 : 0.0;
-        st[rr][cq] = use ? v.x : (cq == r32 ? idv : 0.0);
-        st[rr][cq + 1] = use ? v.y : (cq + 1 == r32 ? idv : 0.0);
-    }
-    // a wave's LDS accesses execute in order; the wave barrier keeps the compiler from moving the
-    // row reads above the staging stores
-    wave_sync();
-#pragma unroll
-    for (int c = 0; c < CNB; ++c) row[c] = st[lane][c];
-}
-
-// One step of the dense factorisation of the permuted system (factorisation order, see lba_host.hip):
-// up to two panels pa, pb (panel positions; -1 = none) that do not update each other, one work item
-// per workgroup (P.chol_items[it0 + blockIdx.x]):
-//   diagonal item of panel p: wave 0 factors [L_pp] (-> Lm), wave 1 [L_pp; b_p^T] (-> y_p), wave 2
-//     [L_pp; I] (-> L_pp^-T for the back-substitution); a non-positive pivot sets *info
-//   tile item (i, j, mask): for each panel of the mask, two waves factor the stacked panels
-//     [L_pp; rows of tile i] and [L_pp; rows of tile j] (or [L_pp; b_p^T] when i == j); then
-//     A(i, j) -= sum over the mask of P_i P_j^T, and when i == j the tile's rows of L are published
-//     and b_i -= sum P_i y_p (forward substitution)
-// so a launch has no inter-workgroup communication.  All global operands are loaded at entry.
-__global__ __launch_bounds__(256) void k_chol_step(int n, int pa, int pb, int it0, const int* __restrict__ items,
-                                                   double* __restrict__ A, double* __restrict__ Lm,
-                                                   double* __restrict__ LinvT, double* __restrict__ b,
-                                                   double* __restrict__ yv, int* info, const LMCtl* ctl,
-                                                   int gate, unsigned long long* tdbg, int step) {
-    __shared__ double stg[4][2 * CNB][CNB + 1];   // per factoring wave: its stacked panel, row-major
-    __shared__ double Pt[4][CNB][CNB + 1];        // factored tile rows: [panel A i, panel A j, panel B i, panel B j]
-    __shared__ double yp[2][CNB];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & (CNB - 1);
-    if (gated_off(ctl, gate)) return;
-    // diagnostics: clock64 stamps of the step's last workgroup (a tile item), thread 0
-    unsigned long long* tm = (tdbg && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) ? tdbg + 16 * step : nullptr;
-    if (tm) tm[0] = clock64();
-    const int it = items[it0 + blockIdx.x];
-    const int ti = it & 1023, tj = (it >> 10) & 1023, mask = (it >> 20) & 3;
-    const bool diag_item = (it >> 22) & 1;
-    // this wave's stacked panel
-    int panel = -1, other = -3;
-    if (diag_item) {
-        panel = (mask & 1) ? pa : pb;
-        if (wave < 3) other = wave == 0 ? -3 : (wave == 1 ? -1 : -2);
-        else panel = -1;
-    } else {
-        const int pw = (wave < 2) ? ((mask & 1) ? pa : -1) : ((mask & 2) ? pb : -1);
-        if (pw >= 0) {
-            panel = pw;
-            other = ((wave & 1) == 0) ? ti : (tj == ti ? -1 : tj);
-        }
-    }
-    double row[CNB];
-    if (panel >= 0) load_stacked(A, b, n, panel, other, stg[wave], lane, row);
-    if (tm) tm[1] = clock64();
-    // this wave's 16 x 16 quadrant of A(i, j) in the v_mfma_f64_16x16x4 output layout: rows
-    // rb*16 + kq + 4q (q = 0..3), column cb*16 + lr
-    const int rb = wave >> 1, cb = wave & 1, lr = lane & 15, kq = lane >> 4;
-    const size_t ra = (size_t)ti * CNB + rb * 16 + kq, ca = (size_t)tj * CNB + cb * 16 + lr;
-    double aold[4] = {0.0, 0.0, 0.0, 0.0};
-    if (!diag_item)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) aold[q] = A[(ra + 4 * q) * n + ca];
-    // ---- right-looking panel factorisation (piv_seq): the next pivot only needs lane j+1's own
-    //      d = a(j+1, j+1) - l(j+1, j)^2, so every lane runs the rsq chain on its own value in VALU
-    //      and the result is read from lane j+1, interleaved with this pivot's rank-1 update.  A
-    //      non-positive pivot turns into NaN and is flagged off the chain.  Lanes < k only touch
-    //      their unused upper triangle.
-    if (panel >= 0) {
-        bool bad = lane == 0 && !(row[0] > 0.0);
-        piv_seq<0, 16>(row, readlane_d(rsqrt_nr(row[0]), 0), lane, bad);
-        cross_update(row, stg[wave], lane);
-        bad = bad || (lane == 16 && !(row[16] > 0.0));
-        piv_seq<16, CNB>(row, readlane_d(rsqrt_nr(row[16]), 16), lane, bad);
-        if (tm) tm[2] = clock64();
-        if (diag_item) {
-            const size_t p0 = (size_t)panel * CNB;
-            if (wave == 0) {
-                if (lane < CNB)   // diagonal block of L (row-major), zero upper part
-#pragma unroll
-                    for (int c = 0; c < CNB; ++c) Lm[(p0 + lane) * n + p0 + c] = (c <= lane) ? row[c] : 0.0;
-                if (__ballot(bad) != 0 && lane == 0) *info = 1 + (int)p0;
-            } else if (wave == 1 && lane == CNB) {
-#pragma unroll
-                for (int c = 0; c < CNB; ++c) yv[p0 + c] = row[c];
-            } else if (wave == 2 && lane >= CNB) {   // row l32 of L_pp^-T
-                double* o = LinvT + p0 * CNB + (size_t)l32 * CNB;
-#pragma unroll
-                for (int c = 0; c < CNB; ++c) o[c] = row[c];
-            }
-        } else if (lane >= CNB) {
-            const int hb = (wave >> 1) * 2;   // 0: panel A, 2: panel B
-            if ((wave & 1) == 0) {
-#pragma unroll
-                for (int c = 0; c < CNB; ++c) Pt[hb][l32][c] = row[c];
-            } else if (tj != ti) {
-#pragma unroll
-                for (int c = 0; c < CNB; ++c) Pt[hb + 1][l32][c] = row[c];
-            } else if (lane == CNB) {
-#pragma unroll
-                for (int c = 0; c < CNB; ++c) yp[wave >> 1][c] = row[c];
-            }
-        }
-    }
-    if (diag_item) return;
-    __syncthreads();
-    if (tm) tm[3] = clock64();
-    // ---- tile update A(i, j) -= sum over the step's panels of P_i P_j^T: one 16 x 16 quadrant per
-    //      wave, v_mfma_f64_16x16x4 with K running over each panel's 32 columns
-    {
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (!(mask & (1 << h))) continue;
-            const double (*Pi)[CNB + 1] = Pt[2 * h];
-            const double (*Qj)[CNB + 1] = (ti == tj) ? Pt[2 * h] : Pt[2 * h + 1];
-#pragma unroll
-            for (int k0 = 0; k0 < CNB; k0 += 4)
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Pi[rb * 16 + lr][k0 + kq], Qj[cb * 16 + lr][k0 + kq], acc,
-                                                           0, 0, 0);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) A[(ra + 4 * q) * n + ca] = aold[q] - acc[q];
-    }
-    if (tm) tm[4] = clock64();
-    if (ti != tj) return;
-    // ---- diagonal tile: publish the tile's rows of L for each panel and forward-substitute b_i
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        if (!(mask & (1 << h))) continue;
-        const int pp = h ? pb : pa;
-        for (int t = tid; t < CNB * CNB; t += 256) {
-            const int i = t / CNB, c = t % CNB;
-            Lm[(size_t)(ti * CNB + i) * n + pp * CNB + c] = Pt[2 * h][i][c];
-        }
-    }
-    if (tid < CNB) {
-        double sum = 0.0;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (!(mask & (1 << h))) continue;
-#pragma unroll 8
-            for (int c = 0; c < CNB; ++c) sum += Pt[2 * h][tid][c] * yp[h][c];
-        }
-        b[ti * CNB + tid] -= sum;
-    }
-}
-
 // ------------------------------------------------------------------------------------------------
-// Dataflow factorisation of the permuted system in ONE launch (replaces the k_chol_step sequence).
+// Dataflow factorisation of the permuted system in ONE launch.
 // One task per tile of the envelope, in a topological order (column by column) pulled from a ticket
 // counter, so progress never depends on which workgroups are resident or in what order they start:
 //   tile (i, j), i > j: keeps A(i, j) and its own copy of A(j, j) in registers (the
 //     v_mfma_f64_16x16x4 output layout, one 16 x 16 quadrant per wave); for every envelope panel
 //     p < j it waits for L(j, p) (and L(i, p) where row i reaches p) and applies
 //     A(i,j) -= L(i,p) L(j,p)^T, A(j,j) -= L(j,p) L(j,p)^T; then one wave factors the stacked
-//     [A(j,j); A(i,j)] (the k_chol_step two-level pivot sequence) and L(i, j) is published.  The
+//     [A(j,j); A(i,j)] (the two-level pivot sequence above) and L(i, j) is published.  The
 //     copies of A(j, j) see the same updates in the same order, so they are bitwise identical;
 //   panel j (i = j): the same updates of A(j, j) and b_j -= L(j,p) y_p, then [A_jj; b_j^T] -> L_jj,
 //     y_j and [A_jj; I] -> L_jj^-T on two waves, published for the diagonal tasks below it.
@@ -1537,12 +1372,13 @@ constexpr int CF_TIMEOUT = 0x7fff0000;          // *info value of a timed-out la
 struct CholFlow {
     int n, NP, ntasks;
     unsigned epoch;
-    const int* tasks;    // j | i << 12 | kind << 24 (0: factor tile (i, j) (i = j: panel j), 1: L^-1 tile (i, j),
+    const int* task_i;   // per task: i
+    const int* tasks;    // j | kind << 24 | lookahead << 28 (0: factor tile (i, j) (i = j: panel j), 1: L^-1 tile (i, j),
                          // 2: solution block x_j, 3: forward block y_i)
     const int* pfh;      // envelope of the permuted matrix (first panel of each panel row)
     const int* tbase;    // tile id of (i, pfh[i]); tile (i, j) = tbase[i] + j - pfh[i]
     const int* pl0;      // per task: first entry of its update list in plist ([pl0[t], pl0[t+1]))
-    const int* plist;    // p | (row i takes part) << 12, in the order every task applies panel updates
+    const int* plist;    // p | (row i takes part) << 24, in the order every task applies panel updates
                          // (the order panels finish: left k and right k side by side, then the separator)
     const double* S;     // assembled system (factorisation order, lower)
     double* Lm;
@@ -1741,10 +1577,14 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
     const int rb = wave >> 1, cb = wave & 1, lr = lane & 15, kq = lane >> 4;
     const int n = a.n;
     auto tile_id = [&](int i, int j) { return a.tbase[i] + j - a.pfh[i]; };
+    // (a task's rows are fixed: their tile-id bases tbase[i] - pfh[i] are read once into registers, so no
+    // address on the chain waits for a table load behind a barrier)
+    auto rowbase = [&](int i) { return a.tbase[i] - a.pfh[i]; };
+    auto tile_at = [&](auto* base, int tid_) { return base + ((size_t)tid_ << 10); };
     auto tri_id = [&](int i, int j) { return i * (i + 1) / 2 + j; };
-    auto load_quad = [&](int i, int j, double (&q)[4]) {   // sc1 loads: the fused assembly writes S in this launch
+    auto load_quad = [&](int tl, double (&q)[4]) {   // tile tl of S; sc1 loads: the fused assembly writes S in this launch
 #pragma unroll
-        for (int m = 0; m < 4; ++m) q[m] = ld_sc1(a.S + (size_t)(i * CNB + rb * 16 + kq + 4 * m) * n + j * CNB + cb * 16 + lr);
+        for (int m = 0; m < 4; ++m) q[m] = ld_sc1(tile_at(a.S, tl) + (rb * 16 + kq + 4 * m) * CNB + cb * 16 + lr);
     };
     auto stage_quad = [&](double (*T)[CNB + 1], int r0, const double (&q)[4]) {
 #pragma unroll
@@ -1776,7 +1616,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
         __syncthreads();
         if (t >= a.ntasks) break;
         const int code = a.tasks[t];
-        const int j = code & 4095, i = (code >> 12) & 4095;
+        const int j = code & 0xffffff, i = a.task_i[t];
         const int kind = (code >> 24) & 15;
         if (kind >= 8) {
             // ---------------------------------------------------- fused prefix: expansion / assembly
@@ -1824,13 +1664,14 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             double bj[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) bj[u] = ld_sc1(a.b + j * CNB + zc + u);
+            const int rbi = rowbase(i);
             for (int q = a.pl0[t]; q < a.pl0[t + 1]; ++q) {
-                const int k = a.plist[q] & 4095;
-                if (!cf_wait(a, a.lready + tile_id(i, k), k == j ? a.fready + j : a.ivready + tri_id(k, j), &s_ok)) {
+                const int k = a.plist[q] & 0xffffff;
+                if (!cf_wait(a, a.lready + rbi + k, k == j ? a.fready + j : a.ivready + tri_id(k, j), &s_ok)) {
                     ok = false;
                     break;
                 }
-                cf_load_tile(a.Lm + (size_t)(i * CNB) * n + k * CNB, n, Lt[0]);
+                cf_load_tile(tile_at(a.Lm, rbi + k), CNB, Lt[0]);
                 if (k == j) {
 #pragma unroll
                     for (int m = 0; m < 4; ++m) {   // Linv(j,j)[r][c] = LinvT_j[c][r]
@@ -1882,7 +1723,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             double part = 0.0;
             bool ok = true;
             for (int q = a.pl0[t]; q < a.pl0[t + 1]; ++q) {
-                const int r = a.plist[q] & 4095;
+                const int r = a.plist[q] & 0xffffff;
                 if (!cf_wait(a, r == j ? a.fready + j : a.ivready + tri_id(r, j), nullptr, &s_ok)) {
                     ok = false;
                     break;
@@ -1922,13 +1763,14 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             // row r, columns 4g .. 4g + 3 of every term
             const int r = tid & 31, g = tid >> 5;
             double acc = 0.0;
+            const int rbi = rowbase(i);
             for (int q = a.pl0[t]; q < a.pl0[t + 1]; ++q) {
-                const int kk = a.plist[q] & 4095;
-                if (!cf_wait(a, a.lready + tile_id(i, kk), a.dready + kk, &s_ok)) return;
+                const int kk = a.plist[q] & 0xffffff;
+                if (!cf_wait(a, a.lready + rbi + kk, a.dready + kk, &s_ok)) return;
                 double lv[4], yk[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    lv[u] = ld_sc1(a.Lm + (size_t)(i * CNB + r) * n + kk * CNB + 4 * g + u);
+                    lv[u] = ld_sc1(tile_at(a.Lm, rbi + kk) + r * CNB + 4 * g + u);
                     yk[u] = ld_sc1(a.yv + kk * CNB + 4 * g + u);
                 }
 #pragma unroll
@@ -1980,16 +1822,17 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
 #pragma unroll
             for (int q = 0; q < MT; ++q)
                 if (q < nt) {
-                    const int ii = a.plist[q0 + q] & 4095;
-                    if (!cf_wait(a, a.lready + tile_id(ii, j), nullptr, &s_ok)) return;
+                    const int ii = a.plist[q0 + q] & 0xffffff;
+                    const int tl = tile_id(ii, j);
+                    if (!cf_wait(a, a.lready + tl, nullptr, &s_ok)) return;
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) lv[q][u] = ld_sc1(a.Lm + (size_t)(ii * CNB + 4 * g + u) * n + j * CNB + c);
+                    for (int u = 0; u < 4; ++u) lv[q][u] = ld_sc1(tile_at(a.Lm, tl) + (4 * g + u) * CNB + c);
                 }
             double acc = 0.0;
 #pragma unroll
             for (int q = 0; q < MT; ++q)
                 if (q < nt) {
-                    const int ii = a.plist[q0 + q] & 4095;
+                    const int ii = a.plist[q0 + q] & 0xffffff;
                     if (!cf_wait(a, a.xready + ii, nullptr, &s_ok)) return;
                     double xi[4];
 #pragma unroll
@@ -1998,12 +1841,13 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
                     for (int u = 0; u < 4; ++u) acc += lv[q][u] * xi[u];
                 }
             for (int q = MT; q < nt; ++q) {
-                const int ii = a.plist[q0 + q] & 4095;
-                if (!cf_wait(a, a.lready + tile_id(ii, j), a.xready + ii, &s_ok)) return;
+                const int ii = a.plist[q0 + q] & 0xffffff;
+                const int tl = tile_id(ii, j);
+                if (!cf_wait(a, a.lready + tl, a.xready + ii, &s_ok)) return;
                 double l4[4], xi[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    l4[u] = ld_sc1(a.Lm + (size_t)(ii * CNB + 4 * g + u) * n + j * CNB + c);
+                    l4[u] = ld_sc1(tile_at(a.Lm, tl) + (4 * g + u) * CNB + c);
                     xi[u] = ld_sc1(a.xpos + ii * CNB + 4 * g + u);
                 }
 #pragma unroll
@@ -2034,7 +1878,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             // without a chain through the panels
             const int q0 = a.pl0[t], cnt = a.pl0[t + 1] - q0;
             if (!cf_wait_list(a, cnt, [&](int q) {
-                    const int k = a.plist[q0 + q] & 4095;
+                    const int k = a.plist[q0 + q] & 0xffffff;
                     return k == i ? a.zready + i : a.ivready + tri_id(i, k);
                 }, &s_ok)) return;
             const int r = tid & 31, g = tid >> 5;   // row r, terms g, g + 8, ...
@@ -2044,7 +1888,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int qq = q + 8 * u;
-                    zz[u] = qq < cnt ? ld_sc1(a.zv + ((size_t)i * a.NP + (a.plist[q0 + qq] & 4095)) * CNB + r) : 0.0;
+                    zz[u] = qq < cnt ? ld_sc1(a.zv + ((size_t)i * a.NP + (a.plist[q0 + qq] & 0xffffff)) * CNB + r) : 0.0;
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) acc += zz[u];
@@ -2067,54 +1911,54 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
         if (tm) tm[0] = __builtin_amdgcn_s_memrealtime();
         unsigned long long* tf = (a.tdbg3 && tid == 0 && t < 4096) ? a.tdbg3 + 8 * t : nullptr;
         if (tf) { tf[0] = __builtin_amdgcn_s_memrealtime(); tf[4] = i | (j << 12) | ((int)la << 24); }
+        const int rbi = rowbase(i), rbj = rowbase(j), rbk = la ? rowbase(j - 1) : 0;
+        const bool ik_env = la && !diag && a.pfh[i] <= j - 1;   // tile (i, j - 1) inside the envelope
         if (a.fused) {   // the tiles this task loads (and panel j's rhs) are assembled
             const int k = j - 1;
-            const bool ikw = la && !diag && a.pfh[i] <= k;
-            if (!cf_wait_cnt(a, 1 + tile_id(j, j), diag ? -1 : 1 + tile_id(i, j), la ? 1 + tile_id(k, k) : -1,
-                             la ? 1 + tile_id(j, k) : -1, ikw ? 1 + tile_id(i, k) : -1,
-                             (diag && a.zv) ? 1 + a.ntile + j : -1, &s_ok))
+            if (!cf_wait_cnt(a, 1 + rbj + j, diag ? -1 : 1 + rbi + j, la ? 1 + rbk + k : -1, la ? 1 + rbj + k : -1,
+                             ik_env ? 1 + rbi + k : -1, (diag && a.zv) ? 1 + a.ntile + j : -1, &s_ok))
                 return;
         }
         double qd[4], qa[4];
-        load_quad(j, j, qd);
-        if (!diag) load_quad(i, j, qa);
+        load_quad(rbj + j, qd);
+        if (!diag) load_quad(rbi + j, qa);
         // lookahead: the task also holds A(k,k), A(j,k), A(i,k) of the previous column k = j - 1, whose
         // update is the last one of A(j,j) and A(i,j) in update order (the host checks); it factors
         // column k's two tiles itself, so only L(., p <= k - 1) is waited for, one chain step earlier
         const int k = j - 1;
-        const bool ik = la && !diag && a.pfh[i] <= k;   // tile (i, k) inside the envelope
+        const bool ik = ik_env;   // tile (i, k) inside the envelope
         double qk[4], qjk[4], qik[4];
         if (la) {
-            load_quad(k, k, qk);
-            load_quad(j, k, qjk);
-            if (ik) load_quad(i, k, qik);
+            load_quad(rbk + k, qk);
+            load_quad(rbj + k, qjk);
+            if (ik) load_quad(rbi + k, qik);
         }
         // ---- updates from the envelope panels p (< j, or < k with lookahead), software-pipelined (the
         //      next panel's tiles are fetched into registers when already published, while this panel's
-        //      products run).  Entry: p | row i takes part << 12 [| row j << 13 | row k << 14 (lookahead)]
+        //      products run).  Entry: p | row i takes part << 24 [| row j << 25 | row k << 26 (lookahead)]
         double rj[4], ri[4], rk[4];
         bool have = false;
         auto rows = [&](int e, bool& fj, bool& fi, bool& fk) {
-            fi = !diag && ((e >> 12) & 1);
-            fj = la ? ((e >> 13) & 1) : true;
-            fk = la && ((e >> 14) & 1);
+            fi = !diag && ((e >> 24) & 1);
+            fj = la ? ((e >> 25) & 1) : true;
+            fk = la && ((e >> 26) & 1);
         };
         auto ready = [&](int e, bool block) {
-            const int p = e & 4095;
+            const int p = e & 0xffffff;
             bool fj, fi, fk;
             rows(e, fj, fi, fk);
-            const int* f1 = fj ? a.lready + tile_id(j, p) : nullptr;
-            const int* f2 = fi ? a.lready + tile_id(i, p) : nullptr;
-            const int* f3 = fk ? a.lready + tile_id(k, p) : nullptr;
+            const int* f1 = fj ? a.lready + rbj + p : nullptr;
+            const int* f2 = fi ? a.lready + rbi + p : nullptr;
+            const int* f3 = fk ? a.lready + rbk + p : nullptr;
             return block ? cf_wait(a, f1, f2, &s_ok, f3) : cf_test(a, f1, f2, &s_ok, f3);
         };
         auto fetch = [&](int e) {
-            const int p = e & 4095;
+            const int p = e & 0xffffff;
             bool fj, fi, fk;
             rows(e, fj, fi, fk);
-            if (fj) cf_fetch(a.Lm + (size_t)(j * CNB) * n + p * CNB, n, rj);
-            if (fi) cf_fetch(a.Lm + (size_t)(i * CNB) * n + p * CNB, n, ri);
-            if (fk) cf_fetch(a.Lm + (size_t)(k * CNB) * n + p * CNB, n, rk);
+            if (fj) cf_fetch(tile_at(a.Lm, rbj + p), CNB, rj);
+            if (fi) cf_fetch(tile_at(a.Lm, rbi + p), CNB, ri);
+            if (fk) cf_fetch(tile_at(a.Lm, rbk + p), CNB, rk);
         };
         bool ok = true;
         // the panels in update order (the same order in every task: the copies of a tile stay bitwise
@@ -2126,7 +1970,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             rows(e, fj, fi, fk);
             if (!have) {
                 if (!ready(e, true)) { ok = false; break; }
-                if (tf) { tf[3] = __builtin_amdgcn_s_memrealtime(); tf[4] = (tf[4] & 0xffffffull) | ((unsigned long long)(la) << 24) | ((unsigned long long)(e & 4095) << 32); }
+                if (tf) { tf[3] = __builtin_amdgcn_s_memrealtime(); tf[4] = (tf[4] & 0xffffffull) | ((unsigned long long)(la) << 24) | ((unsigned long long)(e & 0xffffff) << 32); }
                 fetch(e);
             }
             if (fj) cf_put(Lt[0], rj);
@@ -2191,9 +2035,9 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
                 const int e = tid + 256 * m, r = e >> 5, c = e & 31;
-                st_sc1(a.Lm + (size_t)(i * CNB + r) * n + p0 + c, stg[0][CNB + r][c]);
+                st_sc1(tile_at(a.Lm, rbi + j) + r * CNB + c, stg[0][CNB + r][c]);
             }
-            cf_publish(a, a.lready + tile_id(i, j));
+            cf_publish(a, a.lready + rbi + j);
             if (tm) tm[6] = __builtin_amdgcn_s_memrealtime();
             if (tf) tf[2] = __builtin_amdgcn_s_memrealtime();
             continue;
@@ -2219,7 +2063,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
 #pragma unroll
         for (int m = 0; m < 4; ++m) {   // L_jj (plain: no reader in this launch), L_jj^-T, by all waves
             const int e = tid + 256 * m, r = e >> 5, c = e & 31;
-            a.Lm[(p0 + r) * n + p0 + c] = (c <= r) ? stg[0][r][c] : 0.0;
+            tile_at(a.Lm, rbj + j)[r * CNB + c] = (c <= r) ? stg[0][r][c] : 0.0;
             st_sc1(a.LinvT + p0 * CNB + e, stg[0][CNB + r][c]);
         }
         cf_publish(a, a.fready + j);
@@ -2237,110 +2081,6 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
         }
         cf_publish(a, a.zready + j);
     }
-}
-
-constexpr int CHOL_MAXN = 6144;
-constexpr int BS_GEMV = 640;                  // trailing-update threads (one prefetched column each per pass)
-constexpr int BS_THREADS = 64 + BS_GEMV;
-
-// L^T x = y over the block range [lo, hi) of this workgroup (launch arguments per blockIdx), bottom
-// block first; the nested-dissection order makes the separator range one launch and the left / right
-// ranges two independent workgroups of the next (right rows have no entries in left columns, so
-// neither updates the other).  write_y: store the updated right-hand side below lo back for them.
-// Within a range (L row-major: a column of a block row is read
-// coalesced across the threads that own consecutive columns).  Wave 0
-// applies the block's inverse diagonal (L_bb^-T from k_chol_step: a 32-wide GEMV instead of a
-// 32-step substitution chain); the other waves apply the solved block to the rows above
-// (y_k -= sum_i L(r0+i, k) x_i), with their column loads and the next block's L^-T tile (into a
-// double-buffered LDS tile) issued before the diagonal step, so load latency hides behind it.
-__global__ __launch_bounds__(BS_THREADS) void k_chol_backsolve(const double* __restrict__ Lm,
-                                                               const double* __restrict__ LinvT, int n,
-                                                               double* __restrict__ yv,
-                                                               double* __restrict__ out,
-                                                               const int* __restrict__ pfirst,
-                                                               const int* __restrict__ rnat,
-                                                               unsigned long long* tdbg, const LMCtl* ctl,
-                                                               int gate, int lo0, int hi0, int lo1, int hi1,
-                                                               int write_y) {
-    __shared__ double y[CHOL_MAXN];
-    __shared__ double Mb[2][CNB][CNB + 1];
-    __shared__ double xb[CNB];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int nblk = n / CNB;
-    const int k0 = tid - 64;
-    const int lo = blockIdx.x ? lo1 : lo0, hi = blockIdx.x ? hi1 : hi0;
-    if (gated_off(ctl, gate) || hi <= lo) return;
-    for (int t = tid; t < hi * CNB; t += BS_THREADS) y[t] = yv[t];
-    for (int t = tid; t < CNB * CNB; t += BS_THREADS)
-        Mb[(hi - 1) & 1][t / CNB][t % CNB] = LinvT[(size_t)(hi - 1) * CNB * CNB + t];
-    __syncthreads();
-    if (tdbg && tid == 0 && hi == nblk) tdbg[(size_t)nblk * 16] = clock64();
-    constexpr int MPT = (CNB * CNB + BS_GEMV - 1) / BS_GEMV;   // next-tile elements per GEMV thread
-    for (int blk = hi - 1; blk >= lo; --blk) {
-        const int r0 = blk * CNB;
-        const int c0 = pfirst[blk] * CNB;   // the block's rows of L are zero left of its envelope
-        if (tdbg && tid == 0) tdbg[(size_t)blk * 16] = clock64();
-        double pre[CNB];
-        if (tid < 64) {
-            if (lane < CNB) {
-                const double* m = Mb[blk & 1][lane];
-                double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-#pragma unroll
-                for (int i = 0; i < CNB; i += 4) {
-                    s0 += m[i] * y[r0 + i]; s1 += m[i + 1] * y[r0 + i + 1];
-                    s2 += m[i + 2] * y[r0 + i + 2]; s3 += m[i + 3] * y[r0 + i + 3];
-                }
-                const double xl = (s0 + s1) + (s2 + s3);
-                xb[lane] = xl;
-                out[rnat[blk * CNB + lane]] = xl;   // natural order
-            }
-            if (tdbg && tid == 0) tdbg[(size_t)blk * 16 + 1] = clock64();   // diagonal block done
-        } else {
-            if (k0 + c0 < r0) {   // column c0 + k0 of the block's rows of L: coalesced across the threads
-                const double* col = Lm + (size_t)r0 * n + c0 + k0;
-#pragma unroll
-                for (int i = 0; i < CNB; ++i) pre[i] = col[(size_t)i * n];
-            }
-            if (blk > lo) {   // next block's inverse diagonal tile -> the other LDS buffer
-                double mv[MPT];
-#pragma unroll
-                for (int u = 0; u < MPT; ++u) {
-                    const int t = k0 + u * BS_GEMV;
-                    mv[u] = LinvT[(size_t)(blk - 1) * CNB * CNB + (t < CNB * CNB ? t : 0)];
-                }
-#pragma unroll
-                for (int u = 0; u < MPT; ++u) {
-                    const int t = k0 + u * BS_GEMV;
-                    if (t < CNB * CNB) Mb[(blk - 1) & 1][t / CNB][t % CNB] = mv[u];
-                }
-            }
-        }
-        __syncthreads();
-        if (tdbg && tid == 0) tdbg[(size_t)blk * 16 + 2] = clock64();   // block x published
-        if (tid >= 64) {
-            if (k0 + c0 < r0) {
-                double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-#pragma unroll
-                for (int i = 0; i < CNB; i += 4) {
-                    s0 += pre[i] * xb[i]; s1 += pre[i + 1] * xb[i + 1];
-                    s2 += pre[i + 2] * xb[i + 2]; s3 += pre[i + 3] * xb[i + 3];
-                }
-                y[c0 + k0] -= (s0 + s1) + (s2 + s3);
-            }
-            for (int k = c0 + k0 + BS_GEMV; k < r0; k += BS_GEMV) {
-                double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-#pragma unroll
-                for (int i = 0; i < CNB; i += 4) {
-                    const double* u = Lm + (size_t)(r0 + i) * n + k;
-                    s0 += u[0] * xb[i]; s1 += u[n] * xb[i + 1]; s2 += u[2 * n] * xb[i + 2]; s3 += u[3 * n] * xb[i + 3];
-                }
-                y[k] -= (s0 + s1) + (s2 + s3);
-            }
-        }
-        __syncthreads();
-    }
-    if (write_y)
-        for (int t = tid; t < lo * CNB; t += BS_THREADS) yv[t] = y[t];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2641,26 +2381,16 @@ __global__ __launch_bounds__(256) void k_partials(DevProblem P) {
     }
 }
 
-// partitioned mode: the envelope tiles of S (k_schur zeroes exactly these, so every rank's tiles line
-// up), bS and b_p, into (unpack = 0) or back out of (unpack = 1) the all-reduce buffer
+// partitioned mode: bS and b_p into (unpack = 0) or back out of (unpack = 1) the all-reduce buffer (S itself,
+// the packed envelope, is all-reduced in place)
 __global__ __launch_bounds__(256) void k_env_pack(DevProblem P, int unpack, int gate) {
     if (gated_off(P.ctl, gate)) return;
     const int n = P.npad;
-    if ((int)blockIdx.x < P.n_ztiles) {
-        const int code = P.ztiles[blockIdx.x], i = code & 0xffff, j = code >> 16;
-        double* buf = P.env_buf + (size_t)blockIdx.x * CHOL_NB * CHOL_NB;
-        for (int e = threadIdx.x; e < CHOL_NB * CHOL_NB; e += 256) {
-            double* sp = P.S + (size_t)(i * CHOL_NB + (e >> 5)) * n + j * CHOL_NB + (e & 31);
-            if (unpack) *sp = buf[e];
-            else buf[e] = *sp;
-        }
-    } else {
-        double* buf = P.env_buf + (size_t)P.n_ztiles * CHOL_NB * CHOL_NB;
-        for (int e = (blockIdx.x - P.n_ztiles) * 256 + threadIdx.x; e < n + P.np; e += 256 * 8) {
-            double* sp = e < n ? P.bS + e : P.bp + (e - n);
-            if (unpack) *sp = buf[e];
-            else buf[e] = *sp;
-        }
+    double* buf = P.env_buf;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < n + P.np; e += 256 * gridDim.x) {
+        double* sp = e < n ? P.bS + e : P.bp + (e - n);
+        if (unpack) *sp = buf[e];
+        else buf[e] = *sp;
     }
 }
 
@@ -2715,13 +2445,13 @@ __global__ void k_ctl_init(DevProblem P, LMCtl c) {
 }
 
 // computeLambdaInit (optimization_algorithm_levenberg.cpp:171-185) on the device for a queued
-// optimisation: tau * max |H_ii| over the pose diagonal (S assembled in natural order with
-// lambda = 0, no Schur terms: Hpp) and the landmark diagonals.  A max is exact in any order.
+// optimisation: tau * max |H_ii| over the pose diagonal (Sdiag: ASM_DIAG with lambda = 0, no Schur terms:
+// diag Hpp) and the landmark diagonals.  A max is exact in any order.
 __global__ __launch_bounds__(1024) void k_lambda_init(DevProblem P, double tau) {
     __shared__ double red[16];
     const int tid = threadIdx.x;
     double m = 0.0;
-    for (int i = tid; i < P.np; i += 1024) m = fmax(m, fabs(P.S[(size_t)i * P.npad + i]));
+    for (int i = tid; i < P.np; i += 1024) m = fmax(m, fabs(P.Sdiag[i]));
     for (int i = tid; i < 3 * P.n_lm; i += 1024) m = fmax(m, fabs(P.Hll[9 * (size_t)(i / 3) + 4 * (i % 3)]));
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_down(m, off, 64));
@@ -2786,13 +2516,13 @@ void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStr
                            int sel, double lambda) {
     const int n = P.npad;   // multiple of CHOL_NB (identity tail)
     if (n == 0) return;
-    if (!P.cf_steps_path) {
+    {
         CholFlow a;
         a.fused = P.cf_fused;
         a.cnt = P.cf_cnt; a.need = P.cf_need; a.asm_item = P.cf_asm_item; a.asm_tgt = P.cf_asm_tgt;
         a.ntile = P.cf_ntile; a.sel = sel; a.lambda = lambda;
         a.n = n; a.NP = n / CHOL_NB; a.ntasks = P.cf_ntasks; a.epoch = epoch;
-        a.tasks = P.cf_tasks; a.pfh = P.pfirst; a.tbase = P.cf_tbase; a.pl0 = P.cf_pl0;
+        a.tasks = P.cf_tasks; a.task_i = P.cf_task_i; a.pfh = P.pfirst; a.tbase = P.cf_tbase; a.pl0 = P.cf_pl0;
         a.plist = P.cf_plist;
         a.S = P.S; a.Lm = P.Lm; a.LinvT = P.LinvT; a.b = P.bS; a.yv = P.yv; a.info = P.info;
         a.lready = P.cf_lready; a.dready = P.cf_dready; a.head = P.cf_head; a.abort_flag = P.cf_abort;
@@ -2808,20 +2538,6 @@ void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStr
             hipLaunchKernelGGL(k_chol_flow, dim3(min(P.cf_ntasks, 512)), dim3(256), 0, s, a, P);
         return;
     }
-    for (int st = 0; P.cf_steps_path && st < P.n_steps; ++st) {
-        const int* h = P.h_steps + 4 * st;
-        hipLaunchKernelGGL(k_chol_step, dim3(h[3] - h[2]), dim3(256), 0, s, n, h[0], h[1], h[2], P.chol_items, P.S,
-                           P.Lm, P.LinvT, P.bS, P.yv, P.info, P.ctl, gate, P.tdbg_chol, st);
-    }
-    if (!P.cf_steps_path) return;   // k_chol_flow also solved: x = L^-T y through its L^-1 tiles
-    // back-substitution: separator positions [nl + nr, NP) first, then left [0, nl) and right
-    // [nl, nl + nr) side by side
-    const int NP = n / CHOL_NB, nl = P.nd_left, nr = P.nd_right;
-    if (nl + nr < NP)
-        hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(BS_THREADS), 0, s, P.Lm, P.LinvT, n, P.yv, P.xsol,
-                           P.pfirst, P.rnat, P.tdbg_bs, P.ctl, gate, nl + nr, NP, 0, 0, 1);
-    hipLaunchKernelGGL(k_chol_backsolve, dim3(nr > 0 ? 2 : 1), dim3(BS_THREADS), 0, s, P.Lm, P.LinvT, n, P.yv,
-                       P.xsol, P.pfirst, P.rnat, P.tdbg_bs, P.ctl, gate, 0, nl, nl, nl + nr, 0);
 }
 void launch_update(const DevProblem& P, double lambda, int sel, int gate, int jac, hipStream_t s) {
     hipLaunchKernelGGL(k_update, dim3(P.n_upd_blocks), dim3(UPD_THREADS), 0, s, P, lambda, sel, gate, jac);
@@ -2835,7 +2551,7 @@ void launch_partials(const DevProblem& P, hipStream_t s) {
     hipLaunchKernelGGL(k_partials, dim3(1), dim3(256), 0, s, P);
 }
 void launch_env_pack(const DevProblem& P, int unpack, int gate, hipStream_t s) {
-    hipLaunchKernelGGL(k_env_pack, dim3(P.n_ztiles + 8), dim3(256), 0, s, P, unpack, gate);
+    hipLaunchKernelGGL(k_env_pack, dim3(8), dim3(256), 0, s, P, unpack, gate);
 }
 void launch_finalize(const DevProblem& P, unsigned long long seq, int mode, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, P, seq, mode);

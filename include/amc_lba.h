@@ -272,6 +272,10 @@ int lba_setup_host_profile(const lba_config* cfg, const lba_kf* kfs, int32_t n_k
  * substitution (band) solve, 0 for the L^-1-tile solve, out[4] panels on the factorisation's dependent
  * chain (max(A, B) + both separators of the dissection [A | B | S1 | S2]). */
 int lba_solver_info(const lba_problem* p, int32_t out[5]);
+/* Device memory (bytes) the problem's buffers hold: the reduced system and its factor are packed envelope
+ * tiles (O(envelope), not O(npose^2)); the dense H_pp of lba_linearize is allocated only when asked for.
+ * LBA_E_ARG (< 0) for a null problem. */
+int64_t lba_device_bytes(const lba_problem* p);
 /* Dimension of the pose system (12 * number of non-fixed KFs + 6 * number of free extrinsics). */
 int lba_pose_dim(const lba_problem* p);
 /* Current camera extrinsics (write-back of the VertexExtrinsic estimates, src/Optimizer.cc:1419-1428):
