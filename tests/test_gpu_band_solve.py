@@ -104,3 +104,26 @@ def test_large_pose_system_band_solve():
     p2 = Problem(win, early_stop=0)
     n2, st2 = p2.optimize(3)
     assert st2.chi2_final == st.chi2_final and st2.trials == st.trials
+
+
+def test_pose_system_beyond_131040():
+    """11 000 optimisable keyframes (pose system 132 000, 4125 panels: beyond the 12-bit panel codes of
+    round 2): set up, solved through the band path with packed envelope storage, LM descent and
+    bitwise determinism (the oracle's dense system would take 139 GB)."""
+    win = make_window(n_opt_kf=11000, n_fixed=1, n_lm=44000, obs_per_lm=4, n_cam=1, gp=False, stereo_frac=0.0,
+                      seed=11, global_ba=True, name="chain_11k")
+    p = Problem(win, early_stop=0)
+    assert p.pose_dim == 132000
+    info = p.solver_info()
+    assert info["panels"] > 4095 and info["band"] == 1
+    assert p.device_bytes() < 4e9, p.device_bytes()
+    n, st = p.optimize(2)
+    assert n == 2 and st.chi2_final < st.chi2_initial
+    kf, lm = p.state()
+    p.close()
+    p2 = Problem(win, early_stop=0)
+    n2, st2 = p2.optimize(2)
+    kf2, lm2 = p2.state()
+    assert st2.chi2_final == st.chi2_final and st2.trials == st.trials
+    np.testing.assert_array_equal(kf2["t"], kf["t"])
+    np.testing.assert_array_equal(lm2, lm)
