@@ -82,6 +82,7 @@ def lib():
         L.lba_farm_plan.argtypes = [vp, _lp, _ip, _lp, _ip, _ip]
         L.lba_farm_exchange.argtypes = [vp]
         L.lba_solver_info.argtypes = [vp, _ip]
+        L.lba_solver_flops.argtypes = [vp, _dp]
         L.lba_device_bytes.argtypes = [vp]
         L.lba_device_bytes.restype = ctypes.c_int64
         L.lba_setup_host_profile.argtypes = [ctypes.POINTER(LbaConfig), vp, ctypes.c_int32, vp, ctypes.c_int32, vp,
@@ -97,7 +98,7 @@ def exported_symbols():
             "lba_optimize", "lba_get_state", "lba_set_state", "lba_eval", "lba_trial_chi2", "lba_linearize", "lba_solve_step",
             "lba_pose_dim", "lba_set_partition", "lba_rccl_unique_id", "lba_set_partition_rccl", "lba_group_create",
             "lba_group_destroy", "lba_set_partition_group", "lba_get_cams", "lba_set_farm", "lba_set_farm_rccl",
-            "lba_set_farm_group", "lba_farm_plan", "lba_farm_exchange", "lba_farm_match", "lba_solver_info", "lba_device_bytes",
+            "lba_set_farm_group", "lba_farm_plan", "lba_farm_exchange", "lba_farm_match", "lba_solver_info", "lba_solver_flops", "lba_device_bytes",
             "lba_setup_host_profile"]
 
 
@@ -266,10 +267,18 @@ class Problem:
         return tuple(int(v) for v in out)
 
     def solver_info(self):
-        """lba_solver_info: dict(tail, panels, envelope_tiles, band, chain)."""
-        out = np.zeros(5, dtype=np.int32)
+        """lba_solver_info: dict(tail, panels, tiles (of L, fill-in included), band, chain, levels, s_tiles
+        (the pattern of S), fill (tiles of L that are zero in S))."""
+        out = np.zeros(8, dtype=np.int32)
         self._check(lib().lba_solver_info(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
-        return dict(zip(("tail", "panels", "envelope_tiles", "band", "chain"), (int(v) for v in out)))
+        return dict(zip(("tail", "panels", "tiles", "band", "chain", "levels", "s_tiles", "fill"),
+                        (int(v) for v in out)))
+
+    def solver_flops(self):
+        """lba_solver_flops: (factorisation, substitutions) algorithmic FLOPs of one solve."""
+        out = np.zeros(2, dtype=np.float64)
+        self._check(lib().lba_solver_flops(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
+        return float(out[0]), float(out[1])
 
     def device_bytes(self):
         """lba_device_bytes: device memory held by the problem's buffers."""

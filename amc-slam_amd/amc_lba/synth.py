@@ -183,11 +183,14 @@ def make_window(n_opt_kf=50, n_fixed=1, n_lm=20000, obs_per_lm=6, n_cam=4, gp=Tr
     long-tailed track length 2 + Geometric(1 / (obs_per_lm - 1)) capped at max_track (long tracks:
     landmarks seen from more keyframes than one tile of the device path holds).  loop=True drives one
     lap of a circle: the keyframe band around a landmark's anchor wraps around, so the last keyframes
-    re-observe the first ones' landmarks (the long-range blocks of a loop-closure global BA)."""
+    re-observe the first ones' landmarks (the long-range blocks of a loop-closure global BA); loop=k
+    drives k laps, so every place is revisited k - 1 times and a landmark is seen from the keyframes
+    near its place on every lap."""
     rng = np.random.default_rng(seed)
     n_kf = n_fixed + n_opt_kf
     kf_t = t0 + 0.1 * np.arange(n_kf)
-    traj = _CircleTrajectory(kf_t[0], 0.1 * n_kf) if loop else _Trajectory(kf_t[0] - 0.1, kf_t[-1] + 0.1)
+    laps = int(loop)
+    traj = _CircleTrajectory(kf_t[0], 0.1 * n_kf / laps) if loop else _Trajectory(kf_t[0] - 0.1, kf_t[-1] + 0.1)
 
     # --- cameras: reference camera (last) looks forward; others yawed +90, 180, -90 deg
     Rbc0 = np.array([[0.0, 0.0, 1.0], [-1.0, 0.0, 0.0], [0.0, -1.0, 0.0]])
@@ -230,12 +233,15 @@ def make_window(n_opt_kf=50, n_fixed=1, n_lm=20000, obs_per_lm=6, n_cam=4, gp=Tr
     # --- visibility over a KF band around the anchor (chunked over landmarks to bound memory)
     band = min(n_kf, band)
     koff = np.arange(band) - band // 2
-    if loop:   # the band wraps around the lap
+    if loop:   # the band wraps around the lap (and is repeated on every lap: the places revisited)
+        if laps > 1:
+            koff = (koff[None, :] + np.round(np.arange(laps) * n_kf / laps).astype(int)[:, None]).ravel()
         kk = (k0[:, None] + koff[None, :]) % n_kf
         kk_valid = np.ones(kk.shape, bool)
     else:
         kk = np.clip(k0[:, None] + koff[None, :], 0, n_kf - 1)                 # [nl, band]
         kk_valid = (k0[:, None] + koff[None, :] >= 0) & (k0[:, None] + koff[None, :] < n_kf)
+    band = kk.shape[1]
     u = np.empty((nl_gen, band, n_cam))
     v = np.empty((nl_gen, band, n_cam))
     z = np.empty((nl_gen, band, n_cam))
@@ -256,8 +262,10 @@ def make_window(n_opt_kf=50, n_fixed=1, n_lm=20000, obs_per_lm=6, n_cam=4, gp=Tr
         # GP edges need the previous KF inside the window (src/Optimizer.cc:1112-1116)
         vis[:, :, : n_cam - 1] &= (kk > 0)[:, :, None]
     dk = np.abs(kk - k0[:, None])
-    if loop:
-        dk = np.minimum(dk, n_kf - dk)
+    if loop:   # distance along the lap
+        per = n_kf / laps
+        dk = np.mod(dk, per) if laps > 1 else dk
+        dk = np.minimum(dk, (per if laps > 1 else n_kf) - dk)
     score = dk[:, :, None] * n_cam + rng.random(vis.shape)
     score = np.where(vis, score, np.inf).reshape(nl_gen, -1)
     order = np.argsort(score, axis=1, kind="stable")

@@ -161,8 +161,7 @@ struct DevProblem {
     const int* seg_gslot;   // per slab entry: ga, gb, ge slot in gslab (-1 = none)
     const int* asm_list;    // upper blocks inside the structural pattern of S (diagonal + any source)
     int n_asm;
-    const int* ztiles;      // tiles (i | j << 16) of the permuted envelope, zeroed before each assembly
-    int n_ztiles;
+    int n_ztiles;           // tiles of L (S and L are stored as these tiles), zeroed before each assembly
     const int* hs0;         // [n_ublocks + 1] hslab range per upper block
     const int* gs0;         // [n_pb + 1] gslab range per pose block
     const int* ub_i;        // per upper block: block row / col
@@ -187,26 +186,27 @@ struct DevProblem {
     double* gslab;          // [n_gslots][12] b_p partials, target-sorted
     double* sslab;          // [n_sslots][144] Schur partial blocks, target-sorted
     double* gpslab;         // [n_gpslots][12] Schur rhs partials, target-sorted
-    double* Lm;             // Cholesky factor, packed envelope tiles like S (lower)
+    double* Lm;             // Cholesky factor, the same tiles as S (lower)
     // dense solve in the factorisation (nested-dissection) order of the panels: position = ppos[natural],
     // natural = pnat[position]; pfirst = envelope of the permuted matrix
-    const int* pfirst;
     const int* ppos;
     const int* pnat;
     // rows: natural -> factorisation order (the block ordering of the keyframes, then the panel
     // permutation of the dissection) and back; [npad], the identity on the padding rows
     const int* rpos;
     const int* rnat;
-    int nd_left, nd_right;  // panels of the left / right blocks of the ordering (separator: the rest)
     // dataflow factorisation (k_chol_flow): tasks, tile ids, hand-off flags, ticket counter
     const int* cf_tasks;    // j | kind << 24 | lookahead << 28
     const int* cf_task_i;   // i
+    const int* cf_task_t;   // [5] tile ids a factor task holds: (j,j), (i,j), (k,k), (j,k), (i,k) (-1: none)
     int cf_ntasks;
-    const int* cf_tbase;
+    const int* cf_rowptr;   // tiles of L by row (factorisation order): row i's tiles cf_rowptr[i] .. [i + 1]
+    const int* cf_cols;     //   their columns, ascending (tile id = index)
     double* cf_linv;        // [npad][npad] L^-1 tiles (k_chol_flow)
     int* cf_ivready;        // per lower tile i (i + 1) / 2 + j
     const int* cf_pl0;
     const int* cf_plist;
+    const int* cf_plist_t;  // [3] tile ids per update / term entry
     int* cf_lready;
     int* cf_dready;
     int* cf_fready;
@@ -229,8 +229,8 @@ struct DevProblem {
     double* Hll;
     double* bl;
     double* Dinv;
-    double* S;              // [n_ztiles][32][32] packed envelope tiles of the reduced system in factorisation
-                            // order (tile (i, j) at (cf_tbase[i] + j - pfirst[i]) * 1024), padding: identity
+    double* S;              // [n_ztiles][32][32] the reduced system in factorisation order, stored as the tiles
+                            // of L (cf_rowptr / cf_cols: the symbolic factorisation), padding: identity
     double* Sfull;          // [np][np] natural order, both triangles (ASM_FULL: lba_linearize), allocated on use
     double* Sdiag;          // [np] natural diagonal of H_pp (ASM_DIAG: computeLambdaInit)
     double* bp;             // [np]

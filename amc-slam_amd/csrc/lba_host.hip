@@ -29,6 +29,7 @@
 
 #include "../../include/amc_lba.h"
 #include "lba_device.hpp"
+#include "lba_plan.hpp"
 #include "lba_math.hpp"
 
 using namespace lba;
@@ -61,6 +62,9 @@ struct lba_problem {
     int cur = 0;
     int nd_tail = 0;              // panels of the dissection's tail separator (rows reaching back: loops)
     int chain = 0;                // panels on the factorisation's dependent chain
+    int nd_levels = 0;            // depth of the nested dissection
+    int s_tiles = 0;              // tiles of the lower triangle of S (the pattern before fill-in)
+    double flops_factor = 0.0;    // algorithmic FLOPs of the tile factorisation (symbolic structure of L)
     bool host_only = false;       // lba_setup_host_profile: stop set_problem after the host preprocessing
     uint32_t setup_hash = 0;      // (host_only) fingerprint of the tiling / slab layout
     int setup_tiles = 0;
@@ -1316,213 +1320,222 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.n_mslots = n_mslots; D.n_hslots = n_hslots; D.n_gslots = n_gslots; D.n_sslots = n_sslots; D.n_gpslots = n_gpslots;
     const int npad = (p->np + CHOL_NB - 1) / CHOL_NB * CHOL_NB;
     mark("upload");
-    // ---- solve layout of the reduced camera system (block order, envelope, dissection, schedule)
+    // ---- solve layout of the reduced camera system: dissection order, tile structure of L, task lists
     {
         const int NP = npad / CHOL_NB;
-        // Envelope of S at panel granularity (per CHOL_NB panel of rows, the first panel any of its rows has
-        // a structural non-zero in), then a one-level nested-dissection ordering of the panels.  The natural
-        // (time) order is cut into [A | S1 | B | S2]: the rows of B touch no column of A, S1 separates them,
-        // and S2 is a tail of rows that may reach back anywhere (the last keyframes of a loop closure
-        // re-observe the first ones' points: LoopClosing's global BA).  The factorisation order is
-        // [A | B | S1 | S2]: A and B are eliminated pairwise and concurrently, the separators afterwards,
-        // so the dependent chain is max(A, B) + S1 + S2 panels instead of all of them.  Cholesky fill stays
-        // inside the envelope of the permuted matrix, which bounds everything the solver touches.  Panels
-        // holding rows of free extrinsics (dense: they couple every keyframe) join the tail.  A partition
-        // dissects the union envelope of its ranks.
+        // natural tile pattern of S at panel granularity (structural blocks, diagonal), then the nested-
+        // dissection order and the symbolic factorisation (lba_plan.hpp).  Panels holding rows of free
+        // extrinsics (dense: they couple every keyframe) are ordered last.  A partition plans the union
+        // pattern of its ranks' systems.
         const int NPk = std::min(NP, 12 * n_pb_kf / CHOL_NB + (n_ext ? 0 : NP));
-        std::vector<int> fk(n_pb);
-        for (int b = 0; b < n_pb; ++b) fk[b] = b;   // diagonal (damping)
-        for (int u = 0; u < n_ublocks; ++u)
-            if (hcnt[u] > 0 || scnt[u] > 0) fk[ub_j[u]] = std::min(fk[ub_j[u]], ub_i[u]);
-        std::vector<int> pfirst(NP);
+        std::vector<std::vector<int>> lower(NP);
+        for (int P = 0; P < NP; ++P) lower[P].push_back(P);
+        auto couple = [&](int r, int c) {   // natural rows r, c of S
+            const int P = std::max(r, c) / CHOL_NB, Q = std::min(r, c) / CHOL_NB;
+            lower[P].push_back(Q);
+        };
+        for (int u = 0; u < n_ublocks; ++u) {
+            if (!(hcnt[u] > 0 || scnt[u] > 0)) continue;
+            const int r0 = 12 * ub_j[u], c0 = 12 * ub_i[u];
+            couple(r0, c0); couple(r0 + 11, c0); couple(r0, c0 + 11); couple(r0 + 11, c0 + 11);
+        }
         for (int P = 0; P < NP; ++P) {
-            int f = P;
-            for (int r = P * CHOL_NB; r < (P + 1) * CHOL_NB && r < p->np; ++r) f = std::min(f, 12 * fk[r / 12] / CHOL_NB);
-            pfirst[P] = f;
+            std::sort(lower[P].begin(), lower[P].end());
+            lower[P].erase(std::unique(lower[P].begin(), lower[P].end()), lower[P].end());
         }
         if (p->part_n > 0) part_status(p, 0);   // (every rank's preprocessing succeeded, or all throw)
-        if (p->part_n > 0) {   // the union envelope of the ranks' systems (one all-reduce, at set-up)
+        if (p->part_n > 0) {   // the union pattern of the ranks' systems (one all-reduce, at set-up)
             std::vector<double> occ((size_t)NP * NP, 0.0);
-            for (int P = 0; P < NP; ++P) occ[(size_t)P * NP + pfirst[P]] = 1.0;
+            for (int P = 0; P < NP; ++P)
+                for (int Q : lower[P]) occ[(size_t)P * NP + Q] = 1.0;
             double* d = dalloc<double>(p, occ.size());
             HIPCHK(hipMemcpy(d, occ.data(), occ.size() * sizeof(double), hipMemcpyHostToDevice));
             preduce(p, d, (int64_t)occ.size());
             HIPCHK(hipStreamSynchronize(p->stream));
             HIPCHK(hipMemcpy(occ.data(), d, occ.size() * sizeof(double), hipMemcpyDeviceToHost));
             for (int P = 0; P < NP; ++P) {
-                int f = P;
-                for (int Q = 0; Q < P; ++Q)
-                    if (occ[(size_t)P * NP + Q] != 0.0) { f = Q; break; }
-                pfirst[P] = f;
+                lower[P].clear();
+                for (int Q = 0; Q <= P; ++Q)
+                    if (occ[(size_t)P * NP + Q] != 0.0 || Q == P) lower[P].push_back(Q);
             }
         }
-        // cuts (a, b, c): A = [0, a), S1 = [a, b), B = [b, c), S2 = [c, NPk) (+ the extrinsic panels)
-        int sa = NPk, sb = NPk, sc = NPk, best = NP;
-        const bool no_tail = std::getenv("LBA_ND_NO_TAIL") != nullptr;   // (diagnostics: no S2)
-        for (int c = NPk; c >= 1 && (!no_tail || c == NPk); --c) {
-            if (NPk - c >= best) break;   // a tail this long is no shorter than the best chain
-            for (int a = 1; a < c; ++a) {
-                int b = c;
-                while (b > a && pfirst[b - 1] >= a) --b;   // [b, c): rows with no entry left of a
-                if (b >= c) continue;
-                const int len = std::max(a, c - b) + (b - a) + (NPk - c) + (NP - NPk);
-                if (len < best) { best = len; sa = a; sb = b; sc = c; }
+        // (diagnostics: LBA_ND_LEVELS=<n> caps the dissection depth, 0 = natural order; LBA_ND_NO_TAIL;
+        // LBA_ND_METHOD=1 the interval dissection only, 2 the graph dissection only)
+        const char* lv = std::getenv("LBA_ND_LEVELS");
+        const char* nm = std::getenv("LBA_ND_METHOD");
+        const lba_plan::Plan pl = lba_plan::make_plan(NP, NPk, lower, lv ? std::atoi(lv) : 64,
+                                                      std::getenv("LBA_ND_NO_TAIL") == nullptr, 16,
+                                                      nm ? std::atoi(nm) : 0);
+        p->chain = pl.chain;
+        p->nd_tail = pl.tail;
+        p->nd_levels = pl.levels;
+        p->s_tiles = 0;
+        for (int P = 0; P < NP; ++P) p->s_tiles += (int)lower[P].size();
+        {   // per column with m tiles below the diagonal: potrf 32^3/3, m trsm 32^3, the m(m+1)/2 tile updates
+            // of the trailing matrix (syrk 32^3 on the diagonal ones, gemm 2 x 32^3 below)
+            const double b3 = (double)CHOL_NB * CHOL_NB * CHOL_NB;
+            double f = 0.0;
+            for (int j = 0; j < NP; ++j) {
+                const double m = (double)pl.colrows[j].size();
+                f += b3 / 3.0 + m * b3 + m * b3 + m * (m - 1.0) * b3;
             }
+            p->flops_factor = f;
         }
-        const int nl = sa, nr = sc - sb, ns = NP - nl - nr;
-        p->chain = std::min(best, NP);
-        p->nd_tail = NPk - sc;
-        D.nd_left = nl;
-        D.nd_right = nr;
-        std::vector<int> ppos(NP), pnat(NP);
-        for (int P = 0; P < NP; ++P)   // [A | B | S1 | S2 | extrinsics]
-            ppos[P] = P >= sc ? P : (P < sa ? P : (P >= sb ? nl + (P - sb) : nl + nr + (P - sa)));
-        for (int P = 0; P < NP; ++P) pnat[ppos[P]] = P;
+        const std::vector<int>& ppos = pl.ppos;
+        const std::vector<int>& pnat = pl.pnat;
         // rows: natural -> factorisation order, and back
         std::vector<int> rpos(npad), rnat(npad);
         for (int r = 0; r < npad; ++r) {
             rpos[r] = ppos[r / CHOL_NB] * CHOL_NB + r % CHOL_NB;
             rnat[rpos[r]] = r;
         }
-        // envelope of the permuted matrix (lower part, panel positions)
-        std::vector<int> pfh(NP);
-        for (int i = 0; i < NP; ++i) pfh[i] = i;
-        for (int P = 0; P < NP; ++P)
-            for (int Q = pfirst[P]; Q <= P; ++Q) {
-                const int i = std::max(ppos[P], ppos[Q]), j = std::min(ppos[P], ppos[Q]);
-                pfh[i] = std::min(pfh[i], j);
-            }
-        // solve path: L^-1 tiles (the solve has no substitution chain, but L^-1 of a banded factor is
-        // dense: O(n^3) work) up to CF_AUTO_BAND_NP panels, substitution tasks above (or when asked)
+        // solve path: L^-1 tiles (the solve has no substitution chain, but L^-1 is dense below the
+        // diagonal: O(n^3) work) up to CF_AUTO_BAND_NP panels, substitution tasks above (or when asked)
         const bool band = !(p->cfg.flags & LBA_FLAG_DENSE_SOLVE) &&
                           ((p->cfg.flags & LBA_FLAG_BAND_SOLVE) || NP > CF_AUTO_BAND_NP);
         D.cf_band = band ? 1 : 0;
+        const int ntile = pl.ntile();
         // dataflow factorisation + solve (k_chol_flow), tasks in topological order: per column c the
-        // factor tiles (c..NP-1, c) (the diagonal first), then the L^-1 tiles of row c; at the end one
-        // solution task per panel.  Task: (j, i, kind), with a list of panels per task.
+        // factor tiles of its rows (the diagonal first), then (L^-1 solve) the L^-1 tiles of row c; at the
+        // end one solution task per panel.  Task t: (j, i, kind) with five tile ids (task_t) and a list of
+        // update / term entries (plist) with three tile ids each (plist_t).
         {
-            // task t: tasks[t] = j | kind << 24 | lookahead << 28, task_i[t] = i
-            std::vector<int> tbase(NP + 1, 0), tasks, task_i;
-            auto add_task = [&](int j, int i, int kind, int la) {
+            std::vector<int> tasks, task_i, task_t, pl0(1, 0), plist, plist_t;
+            auto add_task = [&](int j, int i, int kind, int la, int t0, int t1, int t2, int t3, int t4) {
                 tasks.push_back(j | (kind << 24) | (la << 28));
                 task_i.push_back(i);
+                task_t.push_back(t0); task_t.push_back(t1); task_t.push_back(t2); task_t.push_back(t3);
+                task_t.push_back(t4);
             };
-            for (int i = 0; i < NP; ++i) tbase[i + 1] = tbase[i] + (i - pfh[i] + 1);
-            std::vector<int> uord;   // panel update order = the order the panels complete
-            for (int k = 0; k < std::max(nl, nr); ++k) {
-                if (k < nl) uord.push_back(k);
-                if (k < nr) uord.push_back(nl + k);
-            }
-            for (int k = 0; k < ns; ++k) uord.push_back(nl + nr + k);
-            std::vector<int> rank(NP), pl0(1, 0), plist;
+            auto add_entry = [&](int e, int t0, int t1, int t2) {
+                plist.push_back(e);
+                plist_t.push_back(t0); plist_t.push_back(t1); plist_t.push_back(t2);
+            };
+            auto end_task = [&]() { pl0.push_back((int)plist.size()); };
+            const std::vector<int>& rank = pl.rank;
             const bool no_lookahead = std::getenv("LBA_CHOL_NO_LOOKAHEAD") != nullptr;
-            for (int q = 0; q < NP; ++q) rank[uord[q]] = q;
-            // structure of L^-1: Linv(i,j) != 0 iff some k in [max(j, pfh[i]), i) has Linv(k,j) != 0
-            std::vector<std::vector<char>> nz(band ? 0 : NP, std::vector<char>(band ? 0 : NP, 0));
-            for (int j = 0; !band && j < NP; ++j) {
-                nz[j][j] = 1;
-                for (int i = j + 1; i < NP; ++i)
-                    for (int k = std::max(j, pfh[i]); k < i && !nz[i][j]; ++k) nz[i][j] = nz[k][j];
+            auto by_rank = [&](int x, int y) { return rank[x] < rank[y]; };
+            // row c's columns below the diagonal
+            auto rowcols = [&](int c) {
+                return std::vector<int>(pl.cols.begin() + pl.rowptr[c], pl.cols.begin() + pl.rowptr[c + 1] - 1);
+            };
+            // structure of L^-1 (L^-1 solve only): Linv(i,j) != 0 iff some k in [j, i) with L(i,k) != 0 has
+            // Linv(k,j) != 0
+            std::vector<std::vector<char>> nzi(band ? 0 : NP, std::vector<char>(band ? 0 : NP, 0));
+            for (int i = 0; !band && i < NP; ++i) {
+                nzi[i][i] = 1;
+                const std::vector<int> rc = rowcols(i);
+                for (int j = 0; j < i; ++j)
+                    for (int k : rc)
+                        if (k >= j && nzi[k][j]) { nzi[i][j] = 1; break; }
             }
-            // band mode visits the columns in update order (left k and right k side by side), so the
-            // two halves of the nested dissection are factored and substituted concurrently
+            // band mode visits the columns in update order (the halves of every dissection level side by
+            // side), so they are factored and substituted concurrently
             for (int cq = 0; cq < NP; ++cq) {
-                const int c = band ? uord[cq] : cq;
-                for (int i = c; i < NP; ++i) {   // factor tiles of column c: panels p in update order
-                    if (pfh[i] > c) continue;
-                    // lookahead over k = c - 1 when tile (c, k) exists and k is the last update of A(c,c)
-                    // and A(i,c) in update order (then every copy of a tile sees the same update order)
+                const int c = band ? pl.uord[cq] : cq;
+                const std::vector<int> rcc = rowcols(c);
+                std::vector<int> rows(1, c);
+                rows.insert(rows.end(), pl.colrows[c].begin(), pl.colrows[c].end());
+                for (int i : rows) {   // factor tiles of column c (the diagonal first)
+                    // lookahead over k = c - 1 when tile (c, k) exists and k is the last update of A(c, c)
+                    // in update order (then every copy of a tile sees the same update order)
                     const int k = c - 1;
-                    bool la = !no_lookahead && k >= 0 && pfh[c] <= k;
-                    for (int pp = pfh[c]; la && pp < k; ++pp)
-                        if (rank[pp] > rank[k]) la = false;
-                    std::vector<int> ps;
+                    bool la = !no_lookahead && k >= 0 && pl.nz(c, k);
+                    for (int pp : rcc)
+                        if (la && pp != k && rank[pp] > rank[k]) la = false;
+                    const int tcc = pl.tile_id(c, c), tic = i == c ? -1 : pl.tile_id(i, c);
                     if (la) {
-                        add_task(c, i, 0, 1);
-                        for (int pp = std::min(std::min(pfh[c], pfh[i]), pfh[k]); pp < k; ++pp) ps.push_back(pp);
-                        std::sort(ps.begin(), ps.end(), [&](int x, int y) { return rank[x] < rank[y]; });
-                        for (int pp : ps) {   // only panels that update a held tile; row i only where it is used
-                            const bool fj = pp >= pfh[c], fk = pp >= pfh[k], fi = pp >= pfh[i] && (fj || fk);
-                            if (fj || fk) plist.push_back(pp | (fi << 24) | (fj << 25) | (fk << 26));
+                        const int tik = pl.tile_id(i, k);
+                        add_task(c, i, 0, 1, tcc, tic, pl.tile_id(k, k), pl.tile_id(c, k), i == c ? -1 : tik);
+                        // updates of the held tiles A(c,c), A(i,c), A(k,k), A(c,k), A(i,k) from panels p < k
+                        std::vector<int> ps;
+                        for (int pp : rcc) if (pp < k) ps.push_back(pp);
+                        for (int pp : rowcols(k)) ps.push_back(pp);
+                        std::sort(ps.begin(), ps.end());
+                        ps.erase(std::unique(ps.begin(), ps.end()), ps.end());
+                        std::sort(ps.begin(), ps.end(), by_rank);
+                        for (int pp : ps) {   // only panels that update a held tile; row i only where used
+                            const int tcp = pl.tile_id(c, pp), tkp = pl.tile_id(k, pp), tip = pl.tile_id(i, pp);
+                            const bool fj = tcp >= 0, fk = tkp >= 0, fi = i != c && tip >= 0 && (fj || fk);
+                            if (fj || fk) add_entry(pp | (fi << 24) | (fj << 25) | (fk << 26), tcp, fi ? tip : -1, tkp);
                         }
                     } else {
-                        add_task(c, i, 0, 0);
-                        for (int pp = pfh[c]; pp < c; ++pp) ps.push_back(pp);
-                        std::sort(ps.begin(), ps.end(), [&](int x, int y) { return rank[x] < rank[y]; });
-                        for (int pp : ps) plist.push_back(pp | ((pp >= pfh[i]) << 24));
+                        add_task(c, i, 0, 0, tcc, tic, -1, -1, -1);
+                        std::vector<int> ps(rcc);
+                        std::sort(ps.begin(), ps.end(), by_rank);
+                        for (int pp : ps) {
+                            const int tip = i == c ? -1 : pl.tile_id(i, pp);
+                            add_entry(pp | ((tip >= 0) << 24), pl.tile_id(c, pp), tip, -1);
+                        }
                     }
-                    pl0.push_back((int)plist.size());
+                    end_task();
                 }
                 if (band) {   // forward substitution y_c = L_cc^-1 (b_c - sum_k L(c,k) y_k), k in update order
-                    add_task(c, c, 4, 0);
-                    std::vector<int> ks;
-                    for (int k = pfh[c]; k < c; ++k) ks.push_back(k);
-                    std::sort(ks.begin(), ks.end(), [&](int x, int y) { return rank[x] < rank[y]; });
-                    for (int k : ks) plist.push_back(k);
-                    pl0.push_back((int)plist.size());
+                    add_task(c, c, 4, 0, pl.tile_id(c, c), -1, -1, -1, -1);
+                    std::vector<int> ks(rcc);
+                    std::sort(ks.begin(), ks.end(), by_rank);
+                    for (int kk : ks) add_entry(kk, pl.tile_id(c, kk), -1, -1);
+                    end_task();
                     continue;
                 }
                 for (int j = 0; j < c; ++j) {    // L^-1 tiles of row c: terms k ascending
-                    if (!nz[c][j]) continue;
-                    add_task(j, c, 1, 0);
-                    for (int k = std::max(j, pfh[c]); k < c; ++k)
-                        if (nz[k][j]) plist.push_back(k);
-                    pl0.push_back((int)plist.size());
+                    if (!nzi[c][j]) continue;
+                    add_task(j, c, 1, 0, -1, -1, -1, -1, -1);
+                    for (int kk : rcc)
+                        if (kk >= j && nzi[kk][j]) add_entry(kk, pl.tile_id(c, kk), -1, -1);
+                    end_task();
                 }
-                add_task(c, c, 3, 0);   // y_c: the nonzero tiles of row c of L^-1
-                for (int k = 0; k <= c; ++k)
-                    if (nz[c][k]) plist.push_back(k);
-                pl0.push_back((int)plist.size());
+                add_task(c, c, 3, 0, -1, -1, -1, -1, -1);   // y_c: the nonzero tiles of row c of L^-1
+                for (int kk = 0; kk <= c; ++kk)
+                    if (nzi[c][kk]) add_entry(kk, -1, -1, -1);
+                end_task();
             }
             if (band) {
-                // back substitution x_j = L_jj^-T (y_j - sum_i L(i,j)^T x_i) over the rows i > j of the
-                // envelope, columns in reverse update order (separator first, then left and right side
-                // by side), terms in the order their x_i complete
-                std::vector<std::vector<int>> rows_of(NP);
-                for (int i = 0; i < NP; ++i)
-                    for (int j = pfh[i]; j < i; ++j) rows_of[j].push_back(i);
+                // back substitution x_j = L_jj^-T (y_j - sum_i L(i,j)^T x_i) over the rows i > j of column j,
+                // columns in reverse update order, terms in the order their x_i complete
                 for (int cq = NP - 1; cq >= 0; --cq) {
-                    const int j = uord[cq];
-                    add_task(j, j, 5, 0);
-                    std::vector<int>& is = rows_of[j];
+                    const int j = pl.uord[cq];
+                    add_task(j, j, 5, 0, -1, -1, -1, -1, -1);
+                    std::vector<int> is(pl.colrows[j]);
                     std::sort(is.begin(), is.end(), [&](int x, int y) { return rank[x] > rank[y]; });
-                    for (int i : is) plist.push_back(i);
-                    pl0.push_back((int)plist.size());
+                    for (int i : is) add_entry(i, pl.tile_id(i, j), -1, -1);
+                    end_task();
                 }
             }
             for (int j = 0; !band && j < NP; ++j) {      // solution blocks: rows i >= j of column j of L^-1
-                add_task(j, j, 2, 0);
+                add_task(j, j, 2, 0, -1, -1, -1, -1, -1);
                 for (int i = j; i < NP; ++i)
-                    if (nz[i][j]) plist.push_back(i);
-                pl0.push_back((int)plist.size());
+                    if (nzi[i][j]) add_entry(i, -1, -1, -1);
+                end_task();
             }
             if (NP >= (1 << 24)) throw ApiError{LBA_E_LIMIT, "internal: too many panels for the dataflow factorisation"};
-            // fused flow (LBA_FLOW_FUSED=1; one problem, not partitioned): the
-            // pose-sample expansions and heavy landmarks, then the assembly items (padding rows, rhs per pose
-            // block, S blocks) in the order the columns they feed are factored, ahead of the factor tasks; a
-            // counter per envelope tile / panel rhs tells the factor tasks when their operands are assembled
-            // (the assembly items address the slabs with 32-bit buffer offsets)
+            // fused flow (LBA_FLOW_FUSED=1; one problem, not partitioned): the pose-sample expansions and
+            // heavy landmarks, then the assembly items (padding rows, rhs per pose block, S blocks) in the
+            // order the columns they feed are factored, ahead of the factor tasks; a counter per tile of L /
+            // panel rhs tells the factor tasks when their operands are assembled (the assembly items address
+            // the slabs with 32-bit buffer offsets)
             const long long slab_max = 8LL * std::max((long long)n_hslots * 144, (long long)n_sslots * 144);
             const bool fused = p->part_n == 0 && std::getenv("LBA_FLOW_FUSED") && slab_max < (1LL << 31);
             D.cf_fused = fused ? 1 : 0;
-            const int ntile = tbase[NP];
             D.cf_ntile = ntile;
             D.cf_ncnt = 1 + ntile + NP;
             if (fused) {
                 std::vector<int> need(D.cf_ncnt, 0), aitem, atgt, prefix;
                 std::vector<int> akey;   // assembly item -> first update rank among the columns it feeds
+                std::vector<int> tile_col(ntile);
+                for (int i = 0; i < NP; ++i)
+                    for (int q = pl.rowptr[i]; q < pl.rowptr[i + 1]; ++q) tile_col[q] = pl.cols[q];
                 need[0] = n_smp + n_heavy;
                 for (int e = 0; e < n_smp; ++e) prefix.push_back(e | (8 << 24));
                 for (int h = 0; h < n_heavy; ++h) prefix.push_back(h | (9 << 24));
                 auto tile_cnt = [&](int rh, int ch) {
-                    const int ti = std::max(rh, ch) / CHOL_NB, tj = std::min(rh, ch) / CHOL_NB;
-                    return 1 + tbase[ti] + tj - pfh[ti];
+                    return 1 + pl.tile_id(std::max(rh, ch) / CHOL_NB, std::min(rh, ch) / CHOL_NB);
                 };
                 auto add_item = [&](int code, const std::vector<int>& tg, int key) {
                     if (tg.size() > 4) throw ApiError{LBA_E_LIMIT, "internal: assembly item feeds more than 4 tiles"};
                     aitem.push_back(code);
                     for (int q = 0; q < 4; ++q) atgt.push_back(q < (int)tg.size() ? tg[q] : -1);
-                    for (int c : tg) need[c]++;
+                    for (int cc : tg) need[cc]++;
                     akey.push_back(key);
                 };
                 auto uniq = [](std::vector<int> v) {
@@ -1530,16 +1543,14 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     v.erase(std::unique(v.begin(), v.end()), v.end());
                     return v;
                 };
-                auto col_rank = [&](int c) {   // counter -> update rank of the column it belongs to
-                    if (c > ntile) return rank[c - 1 - ntile];
-                    const int t = c - 1;
-                    int ti = (int)(std::upper_bound(tbase.begin(), tbase.end(), t) - tbase.begin()) - 1;
-                    return rank[pfh[ti] + (t - tbase[ti])];
+                auto col_rank = [&](int cc) {   // counter -> update rank of the column it belongs to
+                    if (cc > ntile) return rank[cc - 1 - ntile];
+                    return rank[tile_col[cc - 1]];
                 };
                 auto key_of = [&](const std::vector<int>& tg) {
-                    int k = NP;
-                    for (int c : tg) k = std::min(k, col_rank(c));
-                    return k;
+                    int kk = NP;
+                    for (int cc : tg) kk = std::min(kk, col_rank(cc));
+                    return kk;
                 };
                 if (npad > p->np) {   // padding rows
                     std::vector<int> tg;
@@ -1560,8 +1571,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     if (!(hcnt[u] > 0 || scnt[u] > 0 || ub_i[u] == ub_j[u])) continue;
                     std::vector<int> tg;
                     for (int e = 0; e < 144; ++e) {
-                        const int i = e / 12, j = e % 12, r = 12 * ub_j[u] + j, c = 12 * ub_i[u] + i;
-                        if (ub_i[u] != ub_j[u] || j >= i) tg.push_back(tile_cnt(rpos[r], rpos[c]));
+                        const int i = e / 12, j = e % 12, r = 12 * ub_j[u] + j, cc = 12 * ub_i[u] + i;
+                        if (ub_i[u] != ub_j[u] || j >= i) tg.push_back(tile_cnt(rpos[r], rpos[cc]));
                     }
                     tg = uniq(tg);
                     add_item(u | (2 << 28), tg, key_of(tg));
@@ -1575,15 +1586,11 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     aitem2.push_back(aitem[q]);
                     for (int w = 0; w < 4; ++w) atgt2.push_back(atgt[4 * q + w]);
                 }
-                std::vector<int> all(prefix);
-                all.insert(all.end(), tasks.begin(), tasks.end());
-                tasks.swap(all);
-                std::vector<int> alli(prefix.size(), 0);
-                alli.insert(alli.end(), task_i.begin(), task_i.end());
-                task_i.swap(alli);
-                std::vector<int> pl(prefix.size(), 0);
-                pl.insert(pl.end(), pl0.begin(), pl0.end());
-                pl0.swap(pl);
+                const size_t npre = prefix.size();
+                tasks.insert(tasks.begin(), prefix.begin(), prefix.end());
+                task_i.insert(task_i.begin(), npre, 0);
+                task_t.insert(task_t.begin(), 5 * npre, -1);
+                pl0.insert(pl0.begin(), npre, 0);
                 D.cf_need = dupload(p, need);
                 D.cf_asm_item = dupload(p, aitem2);
                 D.cf_asm_tgt = dupload(p, atgt2);
@@ -1592,8 +1599,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             }
             D.cf_tasks = dupload(p, tasks);
             D.cf_task_i = dupload(p, task_i);
+            D.cf_task_t = dupload(p, task_t);
             D.cf_ntasks = (int)tasks.size();
-            D.cf_tbase = dupload(p, tbase);
             // band mode: no L^-1 tiles; ivready then flags the back-substituted blocks x_j
             const size_t niv = band ? (size_t)NP + 1 : (size_t)std::max(NP * (NP + 1) / 2, 1);
             D.cf_linv = band ? nullptr : dalloc<double>(p, (size_t)npad * npad);
@@ -1602,7 +1609,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             D.cf_xpos = band ? dalloc<double>(p, npad) : nullptr;
             D.cf_pl0 = dupload(p, pl0);
             D.cf_plist = dupload(p, plist);
-            D.cf_lready = dalloc<int>(p, std::max(tbase[NP], 1));
+            D.cf_plist_t = dupload(p, plist_t);
+            D.cf_lready = dalloc<int>(p, std::max(ntile, 1));
             D.cf_dready = dalloc<int>(p, std::max(NP, 1));
             D.cf_fready = dalloc<int>(p, std::max(NP, 1));
             HIPCHK(hipMemset(D.cf_fready, 0, sizeof(int) * std::max(NP, 1)));
@@ -1611,26 +1619,23 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             D.cf_zv = band ? nullptr : dalloc<double>(p, std::max((size_t)NP * NP * CHOL_NB, (size_t)1));
             D.cf_head = dalloc<unsigned long long>(p, 1);
             D.cf_abort = dalloc<int>(p, 1);
-            HIPCHK(hipMemset(D.cf_lready, 0, sizeof(int) * std::max(tbase[NP], 1)));
+            HIPCHK(hipMemset(D.cf_lready, 0, sizeof(int) * std::max(ntile, 1)));
             HIPCHK(hipMemset(D.cf_dready, 0, sizeof(int) * std::max(NP, 1)));
             HIPCHK(hipMemset(D.cf_head, 0, sizeof(unsigned long long)));
             HIPCHK(hipMemset(D.cf_abort, 0, sizeof(int)));
         }
-        D.pfirst = dupload(p, pfh);
+        D.cf_rowptr = dupload(p, pl.rowptr);
+        D.cf_cols = dupload(p, pl.cols);
         D.ppos = dupload(p, ppos);
         D.pnat = dupload(p, pnat);
         D.rpos = dupload(p, rpos);
         D.rnat = dupload(p, rnat);
-        // every trial, k_schur zeroes the tiles of S inside the permuted envelope (everything the
-        // factorisation may write: structural non-zeros and fill-in) and k_assemble then writes the
-        // structurally non-zero blocks; the rest of S stays zero from the upload
-        std::vector<int> ztiles, asm_list;
-        for (int i = 0; i < NP; ++i)
-            for (int j = pfh[i]; j <= i; ++j) ztiles.push_back(i | (j << 16));
+        // every trial, k_lin_schur zeroes S (the tiles of L: structural non-zeros and fill-in) and k_assemble
+        // then writes the structurally non-zero blocks
+        std::vector<int> asm_list;
         for (int u = 0; u < n_ublocks; ++u)
             if (hcnt[u] > 0 || scnt[u] > 0 || ub_i[u] == ub_j[u]) asm_list.push_back(u);
-        D.ztiles = dupload(p, ztiles);
-        D.n_ztiles = (int)ztiles.size();
+        D.n_ztiles = ntile;
         D.part_rank = p->part_rank;
         D.part_n = p->part_n;
         if (p->part_n > 0) {
@@ -2341,13 +2346,23 @@ int64_t lba_device_bytes(const lba_problem* p) {
     return b;
 }
 
-int lba_solver_info(const lba_problem* p, int32_t out[5]) {
+int lba_solver_info(const lba_problem* p, int32_t out[8]) {
     if (!p || !out || !p->has_problem) return LBA_E_ARG;
     out[0] = p->nd_tail;
     out[1] = p->D.npad / CHOL_NB;
     out[2] = p->D.n_ztiles;
     out[3] = p->D.cf_band;
     out[4] = p->chain;
+    out[5] = p->nd_levels;
+    out[6] = p->s_tiles;
+    out[7] = p->D.n_ztiles - p->s_tiles;
+    return LBA_OK;
+}
+
+int lba_solver_flops(const lba_problem* p, double out[2]) {
+    if (!p || !out || !p->has_problem) return LBA_E_ARG;
+    out[0] = p->flops_factor;
+    out[1] = 2.0 * 2.0 * (double)p->D.n_ztiles * CHOL_NB * CHOL_NB;   // forward + back substitution
     return LBA_OK;
 }
 

@@ -100,10 +100,17 @@ __device__ __forceinline__ double damping(const DevProblem& P, double lambda) {
     return lambda < 0.0 ? P.ctl->lambda : lambda;
 }
 
-// element (r, c), r >= c, of the reduced system in factorisation order inside its packed envelope tile
+// element (r, c), r >= c, of the reduced system in factorisation order inside its tile of L (a structural
+// non-zero of S always has one: binary search of the row's tile columns)
 __device__ __forceinline__ size_t s_elem(const DevProblem& P, int r, int c) {
     const int ti = r / CHOL_NB, tj = c / CHOL_NB;
-    return (size_t)(P.cf_tbase[ti] + tj - P.pfirst[ti]) * (CHOL_NB * CHOL_NB) + (r % CHOL_NB) * CHOL_NB + (c % CHOL_NB);
+    int lo = P.cf_rowptr[ti], hi = P.cf_rowptr[ti + 1] - 1;
+    while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (P.cf_cols[m] < tj) lo = m + 1;
+        else hi = m;
+    }
+    return (size_t)lo * (CHOL_NB * CHOL_NB) + (r % CHOL_NB) * CHOL_NB + (c % CHOL_NB);
 }
 
 __device__ __forceinline__ SE3 load_se3(const double* k) {
@@ -665,7 +672,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
         }
         if (P.cf_fused)   // the fused flow's expansion / assembly counters
             for (int z = blockIdx.x * LS_THREADS + tid; z < P.cf_ncnt; z += gridDim.x * LS_THREADS) P.cf_cnt[z] = 0;
-        const size_t nz = (size_t)P.n_ztiles * CHOL_NB * CHOL_NB;   // (S is the packed envelope)
+        const size_t nz = (size_t)P.n_ztiles * CHOL_NB * CHOL_NB;   // (S: the tiles of L)
         for (size_t z = (size_t)blockIdx.x * LS_THREADS + tid; z < nz; z += (size_t)gridDim.x * LS_THREADS) P.S[z] = 0.0;
     }
     if ((int)blockIdx.x >= P.n_tiles) {   // motion-prior / velocity / extrinsic-prior edge items
@@ -1186,9 +1193,9 @@ __device__ void asm_pad_item(const DevProblem& P) {   // padding rows: identity,
 
 // ------------------------------------------------------------------------------------------------
 // Dense Cholesky S = L L^T of the reduced camera system in its factorisation order (panels permuted
-// by the nested dissection of lba_host.hip), as ONE dataflow launch (k_chol_flow below).  S and L are
-// stored as packed envelope tiles: tile (i, j), pfirst[i] <= j <= i, is 32 x 32 doubles row-major at
-// tile_id(i, j) * 1024 with tile_id = tbase[i] + j - pfirst[i] (memory O(envelope), not npad^2).  The
+// by the nested dissection of lba_plan.hpp), as ONE dataflow launch (k_chol_flow below).  S and L are
+// stored as the tiles of L's symbolic structure (fill-in included): tile t is 32 x 32 doubles row-major at
+// t * 1024, the host precomputes every tile id a task touches (memory O(nnz(L)), not npad^2).  The
 // system is padded to a multiple of CNB with an identity tail, so every panel is exactly CNB wide and
 // the panel code below is compile-time.  A non-positive pivot sets *info (the LDLT !isPositive failure
 // of linear_solver_dense.h:108-112).
@@ -1375,8 +1382,8 @@ struct CholFlow {
     const int* task_i;   // per task: i
     const int* tasks;    // j | kind << 24 | lookahead << 28 (0: factor tile (i, j) (i = j: panel j), 1: L^-1 tile (i, j),
                          // 2: solution block x_j, 3: forward block y_i)
-    const int* pfh;      // envelope of the permuted matrix (first panel of each panel row)
-    const int* tbase;    // tile id of (i, pfh[i]); tile (i, j) = tbase[i] + j - pfh[i]
+    const int* task_t;   // per task: 5 tile ids (factor tasks: (j,j), (i,j), (k,k), (j,k), (i,k); -1 none)
+    const int* plist_t;  // per list entry: 3 tile ids (factor: (j,p), (i,p), (k,p); L^-1 / forward: (i,k); back: (i,j))
     const int* pl0;      // per task: first entry of its update list in plist ([pl0[t], pl0[t+1]))
     const int* plist;    // p | (row i takes part) << 24, in the order every task applies panel updates
                          // (the order panels finish: left k and right k side by side, then the separator)
@@ -1576,10 +1583,8 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int rb = wave >> 1, cb = wave & 1, lr = lane & 15, kq = lane >> 4;
     const int n = a.n;
-    auto tile_id = [&](int i, int j) { return a.tbase[i] + j - a.pfh[i]; };
-    // (a task's rows are fixed: their tile-id bases tbase[i] - pfh[i] are read once into registers, so no
-    // address on the chain waits for a table load behind a barrier)
-    auto rowbase = [&](int i) { return a.tbase[i] - a.pfh[i]; };
+    // (the tile ids a task touches come precomputed with it, read into registers at the task's start or
+    // with its list entry, so no address on the chain waits for a table search)
     auto tile_at = [&](auto* base, int tid_) { return base + ((size_t)tid_ << 10); };
     auto tri_id = [&](int i, int j) { return i * (i + 1) / 2 + j; };
     auto load_quad = [&](int tl, double (&q)[4]) {   // tile tl of S; sc1 loads: the fused assembly writes S in this launch
@@ -1664,14 +1669,13 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             double bj[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) bj[u] = ld_sc1(a.b + j * CNB + zc + u);
-            const int rbi = rowbase(i);
             for (int q = a.pl0[t]; q < a.pl0[t + 1]; ++q) {
-                const int k = a.plist[q] & 0xffffff;
-                if (!cf_wait(a, a.lready + rbi + k, k == j ? a.fready + j : a.ivready + tri_id(k, j), &s_ok)) {
+                const int k = a.plist[q] & 0xffffff, tik = a.plist_t[3 * q];
+                if (!cf_wait(a, a.lready + tik, k == j ? a.fready + j : a.ivready + tri_id(k, j), &s_ok)) {
                     ok = false;
                     break;
                 }
-                cf_load_tile(tile_at(a.Lm, rbi + k), CNB, Lt[0]);
+                cf_load_tile(tile_at(a.Lm, tik), CNB, Lt[0]);
                 if (k == j) {
 #pragma unroll
                     for (int m = 0; m < 4; ++m) {   // Linv(j,j)[r][c] = LinvT_j[c][r]
@@ -1763,14 +1767,13 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             // row r, columns 4g .. 4g + 3 of every term
             const int r = tid & 31, g = tid >> 5;
             double acc = 0.0;
-            const int rbi = rowbase(i);
             for (int q = a.pl0[t]; q < a.pl0[t + 1]; ++q) {
-                const int kk = a.plist[q] & 0xffffff;
-                if (!cf_wait(a, a.lready + rbi + kk, a.dready + kk, &s_ok)) return;
+                const int kk = a.plist[q] & 0xffffff, tik = a.plist_t[3 * q];
+                if (!cf_wait(a, a.lready + tik, a.dready + kk, &s_ok)) return;
                 double lv[4], yk[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    lv[u] = ld_sc1(tile_at(a.Lm, rbi + kk) + r * CNB + 4 * g + u);
+                    lv[u] = ld_sc1(tile_at(a.Lm, tik) + r * CNB + 4 * g + u);
                     yk[u] = ld_sc1(a.yv + kk * CNB + 4 * g + u);
                 }
 #pragma unroll
@@ -1822,8 +1825,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
 #pragma unroll
             for (int q = 0; q < MT; ++q)
                 if (q < nt) {
-                    const int ii = a.plist[q0 + q] & 0xffffff;
-                    const int tl = tile_id(ii, j);
+                    const int tl = a.plist_t[3 * (q0 + q)];
                     if (!cf_wait(a, a.lready + tl, nullptr, &s_ok)) return;
 #pragma unroll
                     for (int u = 0; u < 4; ++u) lv[q][u] = ld_sc1(tile_at(a.Lm, tl) + (4 * g + u) * CNB + c);
@@ -1842,7 +1844,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
                 }
             for (int q = MT; q < nt; ++q) {
                 const int ii = a.plist[q0 + q] & 0xffffff;
-                const int tl = tile_id(ii, j);
+                const int tl = a.plist_t[3 * (q0 + q)];
                 if (!cf_wait(a, a.lready + tl, a.xready + ii, &s_ok)) return;
                 double l4[4], xi[4];
 #pragma unroll
@@ -1911,27 +1913,27 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
         if (tm) tm[0] = __builtin_amdgcn_s_memrealtime();
         unsigned long long* tf = (a.tdbg3 && tid == 0 && t < 4096) ? a.tdbg3 + 8 * t : nullptr;
         if (tf) { tf[0] = __builtin_amdgcn_s_memrealtime(); tf[4] = i | (j << 12) | ((int)la << 24); }
-        const int rbi = rowbase(i), rbj = rowbase(j), rbk = la ? rowbase(j - 1) : 0;
-        const bool ik_env = la && !diag && a.pfh[i] <= j - 1;   // tile (i, j - 1) inside the envelope
+        // the task's tiles: (j,j), (i,j), and with lookahead (k,k), (j,k), (i,k) (-1 when (i,k) is zero)
+        const int t_jj = a.task_t[5 * t], t_ij = a.task_t[5 * t + 1], t_kk = a.task_t[5 * t + 2],
+                  t_jk = a.task_t[5 * t + 3], t_ik = a.task_t[5 * t + 4];
+        const bool ik_env = la && !diag && t_ik >= 0;   // tile (i, j - 1) structurally non-zero
         if (a.fused) {   // the tiles this task loads (and panel j's rhs) are assembled
-            const int k = j - 1;
-            if (!cf_wait_cnt(a, 1 + rbj + j, diag ? -1 : 1 + rbi + j, la ? 1 + rbk + k : -1, la ? 1 + rbj + k : -1,
-                             ik_env ? 1 + rbi + k : -1, (diag && a.zv) ? 1 + a.ntile + j : -1, &s_ok))
+            if (!cf_wait_cnt(a, 1 + t_jj, diag ? -1 : 1 + t_ij, la ? 1 + t_kk : -1, la ? 1 + t_jk : -1,
+                             ik_env ? 1 + t_ik : -1, (diag && a.zv) ? 1 + a.ntile + j : -1, &s_ok))
                 return;
         }
         double qd[4], qa[4];
-        load_quad(rbj + j, qd);
-        if (!diag) load_quad(rbi + j, qa);
+        load_quad(t_jj, qd);
+        if (!diag) load_quad(t_ij, qa);
         // lookahead: the task also holds A(k,k), A(j,k), A(i,k) of the previous column k = j - 1, whose
         // update is the last one of A(j,j) and A(i,j) in update order (the host checks); it factors
         // column k's two tiles itself, so only L(., p <= k - 1) is waited for, one chain step earlier
-        const int k = j - 1;
-        const bool ik = ik_env;   // tile (i, k) inside the envelope
+        const bool ik = ik_env;   // tile (i, k) structurally non-zero
         double qk[4], qjk[4], qik[4];
         if (la) {
-            load_quad(rbk + k, qk);
-            load_quad(rbj + k, qjk);
-            if (ik) load_quad(rbi + k, qik);
+            load_quad(t_kk, qk);
+            load_quad(t_jk, qjk);
+            if (ik) load_quad(t_ik, qik);
         }
         // ---- updates from the envelope panels p (< j, or < k with lookahead), software-pipelined (the
         //      next panel's tiles are fetched into registers when already published, while this panel's
@@ -1943,22 +1945,21 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             fj = la ? ((e >> 25) & 1) : true;
             fk = la && ((e >> 26) & 1);
         };
-        auto ready = [&](int e, bool block) {
-            const int p = e & 0xffffff;
+        // list entry q: tiles (j,p), (i,p), (k,p) in plist_t
+        auto ready = [&](int q, bool block) {
             bool fj, fi, fk;
-            rows(e, fj, fi, fk);
-            const int* f1 = fj ? a.lready + rbj + p : nullptr;
-            const int* f2 = fi ? a.lready + rbi + p : nullptr;
-            const int* f3 = fk ? a.lready + rbk + p : nullptr;
+            rows(a.plist[q], fj, fi, fk);
+            const int* f1 = fj ? a.lready + a.plist_t[3 * q] : nullptr;
+            const int* f2 = fi ? a.lready + a.plist_t[3 * q + 1] : nullptr;
+            const int* f3 = fk ? a.lready + a.plist_t[3 * q + 2] : nullptr;
             return block ? cf_wait(a, f1, f2, &s_ok, f3) : cf_test(a, f1, f2, &s_ok, f3);
         };
-        auto fetch = [&](int e) {
-            const int p = e & 0xffffff;
+        auto fetch = [&](int q) {
             bool fj, fi, fk;
-            rows(e, fj, fi, fk);
-            if (fj) cf_fetch(tile_at(a.Lm, rbj + p), CNB, rj);
-            if (fi) cf_fetch(tile_at(a.Lm, rbi + p), CNB, ri);
-            if (fk) cf_fetch(tile_at(a.Lm, rbk + p), CNB, rk);
+            rows(a.plist[q], fj, fi, fk);
+            if (fj) cf_fetch(tile_at(a.Lm, a.plist_t[3 * q]), CNB, rj);
+            if (fi) cf_fetch(tile_at(a.Lm, a.plist_t[3 * q + 1]), CNB, ri);
+            if (fk) cf_fetch(tile_at(a.Lm, a.plist_t[3 * q + 2]), CNB, rk);
         };
         bool ok = true;
         // the panels in update order (the same order in every task: the copies of a tile stay bitwise
@@ -1969,16 +1970,16 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             bool fj, fi, fk;
             rows(e, fj, fi, fk);
             if (!have) {
-                if (!ready(e, true)) { ok = false; break; }
+                if (!ready(q, true)) { ok = false; break; }
                 if (tf) { tf[3] = __builtin_amdgcn_s_memrealtime(); tf[4] = (tf[4] & 0xffffffull) | ((unsigned long long)(la) << 24) | ((unsigned long long)(e & 0xffffff) << 32); }
-                fetch(e);
+                fetch(q);
             }
             if (fj) cf_put(Lt[0], rj);
             if (fi) cf_put(Lt[1], ri);
             if (fk) cf_put(Lt[2], rk);
             __syncthreads();
-            have = q + 1 < q1 && ready(a.plist[q + 1], false);
-            if (have) fetch(a.plist[q + 1]);
+            have = q + 1 < q1 && ready(q + 1, false);
+            if (have) fetch(q + 1);
             if (fj) sub_mma(qd, cf_mma_nt(Lt[0], Lt[0], rb, cb, lr, kq, z4));
             if (fi && fj) sub_mma(qa, cf_mma_nt(Lt[1], Lt[0], rb, cb, lr, kq, z4));
             if (fk) {
@@ -2035,9 +2036,9 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
                 const int e = tid + 256 * m, r = e >> 5, c = e & 31;
-                st_sc1(tile_at(a.Lm, rbi + j) + r * CNB + c, stg[0][CNB + r][c]);
+                st_sc1(tile_at(a.Lm, t_ij) + r * CNB + c, stg[0][CNB + r][c]);
             }
-            cf_publish(a, a.lready + rbi + j);
+            cf_publish(a, a.lready + t_ij);
             if (tm) tm[6] = __builtin_amdgcn_s_memrealtime();
             if (tf) tf[2] = __builtin_amdgcn_s_memrealtime();
             continue;
@@ -2063,7 +2064,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
 #pragma unroll
         for (int m = 0; m < 4; ++m) {   // L_jj (plain: no reader in this launch), L_jj^-T, by all waves
             const int e = tid + 256 * m, r = e >> 5, c = e & 31;
-            tile_at(a.Lm, rbj + j)[r * CNB + c] = (c <= r) ? stg[0][r][c] : 0.0;
+            tile_at(a.Lm, t_jj)[r * CNB + c] = (c <= r) ? stg[0][r][c] : 0.0;
             st_sc1(a.LinvT + p0 * CNB + e, stg[0][CNB + r][c]);
         }
         cf_publish(a, a.fready + j);
@@ -2522,7 +2523,8 @@ void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStr
         a.cnt = P.cf_cnt; a.need = P.cf_need; a.asm_item = P.cf_asm_item; a.asm_tgt = P.cf_asm_tgt;
         a.ntile = P.cf_ntile; a.sel = sel; a.lambda = lambda;
         a.n = n; a.NP = n / CHOL_NB; a.ntasks = P.cf_ntasks; a.epoch = epoch;
-        a.tasks = P.cf_tasks; a.task_i = P.cf_task_i; a.pfh = P.pfirst; a.tbase = P.cf_tbase; a.pl0 = P.cf_pl0;
+        a.tasks = P.cf_tasks; a.task_i = P.cf_task_i; a.task_t = P.cf_task_t; a.pl0 = P.cf_pl0;
+        a.plist_t = P.cf_plist_t;
         a.plist = P.cf_plist;
         a.S = P.S; a.Lm = P.Lm; a.LinvT = P.LinvT; a.b = P.bS; a.yv = P.yv; a.info = P.info;
         a.lready = P.cf_lready; a.dready = P.cf_dready; a.head = P.cf_head; a.abort_flag = P.cf_abort;

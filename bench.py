@@ -29,6 +29,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "amc-slam_amd"))
 
 METRIC = "local-BA iterations/sec (50 KF, 20k landmarks, 120k obs) at 1/2/4/8 MI355X"
+
+
+def metric_for(config, W, gba):
+    """BASELINE.json's metric string for its own configuration (configs[1]); the same form for the others."""
+    if config == "cfg1_local_50kf":
+        return METRIC
+    n_kf = int((W.kfs["fixed"] == 0).sum())
+    return (f"{'global' if gba else 'local'}-BA iterations/sec ({n_kf} KF, {len(W.lm) // 1000}k landmarks, "
+            f"{len(W.obs) // 1000}k obs) at 1/2/4/8 MI355X")
+
+
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6        # MI355X fp64 vector/matrix spec
 
@@ -234,7 +245,8 @@ def main():
     setup_done.set()
 
     # warmup (not timed)
-    sinfo = prob.solver_info()   # (panels, envelope tiles, band mode: the solve's FLOP count below)
+    sinfo = prob.solver_info()   # (panels, tiles, chain, dissection levels, fill: reported below)
+    sflops = prob.solver_flops()   # (the solve's algorithmic FLOPs below)
     if args.warmup > 0:
         prob.optimize(args.warmup)
     torch.cuda.synchronize()
@@ -301,24 +313,19 @@ def main():
         F = sweep_flops(win) + F_schur
         s_ms = ms_s / max(n_s, 1)
         npose = 12 * int((win.kfs["fixed"] == 0).sum())
-        if sinfo["band"]:
-            # envelope Cholesky of the dissected system: per envelope tile (i, j) the updates from the
-            # panels of its row's envelope (about half the mean row width), 2 x 32^3 each, + two band solves
-            NPn, E = sinfo["panels"], sinfo["envelope_tiles"]
-            w = E / max(NPn, 1)
-            F_solve = E * (w / 2.0) * 2.0 * 32 ** 3 + 2.0 * 2.0 * E * 32 ** 2
-            solve_note = ("envelope Cholesky of the dissected band system, E tiles of mean row width w: "
-                          "E (w/2) 2 x 32^3 + two substitutions (an estimate from lba_solver_info); the dependent "
-                          "panel chain, not the FLOPs, sets its time")
-        else:
-            F_solve = npose ** 3 / 3.0 + 2.0 * npose ** 2   # dense Cholesky + two triangular solves
-            solve_note = ("np^3/3 + 2 np^2 of the dense reduced camera system; the dependent panel chain, not "
-                          "the FLOPs, sets its time")
+        # algorithmic FLOPs of one solve from the symbolic structure of L (lba_solver_flops): the tile
+        # factorisation + the two substitutions (dense Cholesky np^3/3 when the system has no sparsity)
+        F_fac, F_sub = sflops
+        F_solve = F_fac + F_sub
+        solve_note = ("tile Cholesky of the nested-dissection-ordered reduced camera system: per column with m "
+                      "tiles below the diagonal 32^3/3 + 2 m 32^3 + m (m - 1) 32^3, plus two substitutions "
+                      "(lba_solver_flops, exact for the symbolic structure); the dependent panel chain, not the "
+                      "FLOPs, sets its time")
         achieved = B / (k_ms * 1e-3) / 1e9 if n_k else None
         workload = f"{args.config}: {win.name or args.config} synthetic window"
         traffic = pmc_traffic(args.config)
         line = {
-            "metric": METRIC,
+            "metric": metric_for(args.config, W, gba),
             "value": value,
             "unit": "LM iterations/s",
             "n_gpus": world,
@@ -348,7 +355,8 @@ def main():
                                "achieved": F_solve / (s_ms * 1e-3) / 1e12 if n_s else None,
                                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                                "frac": (F_solve / (s_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS) if n_s else None,
-                               "avg_launch_ms": s_ms, "timed_launches": n_s, "note": solve_note},
+                               "avg_launch_ms": s_ms, "timed_launches": n_s, "note": solve_note,
+                               "solver": sinfo, "flops_factor": F_fac, "flops_substitution": F_sub},
             "trials_per_step": trials / max(done, 1),
             "phases_ms_per_step": phase,
         }
@@ -361,10 +369,18 @@ def main():
             line["roofline"]["note"] = "k_lin_schur of rank 0's landmark partition"
         if not args.no_cpu and world == 1 and not gba:   # (the oracle's dense LDLT of S = 60000^2 is hours)
             line["cpu_baseline"] = cpu_baseline(win, args.cpu_seconds)
-            line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
             # secondary: the OpenMP build of the oracle on this rank's share of the host's cores
             omp_threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
             line["cpu_baseline_omp"] = cpu_baseline_omp(args.config, args.cpu_seconds, omp_threads)
+            # speed-up against the best CPU baseline measured (both are ports of g2o's algorithm, oracle/,
+            # not g2o itself: the reference's build is not available here)
+            cands = [("port, 1 thread", line["cpu_baseline"].get("value"))]
+            if line["cpu_baseline_omp"] and line["cpu_baseline_omp"].get("value"):
+                cands.append((f"port, OpenMP {line['cpu_baseline_omp'].get('cores')} threads",
+                              line["cpu_baseline_omp"]["value"]))
+            best = max((c for c in cands if c[1]), key=lambda c: c[1])
+            line["speedup_vs_cpu"] = {"value": value / best[1], "against": best[0],
+                                      "all": {k: value / v for k, v in cands if v}}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -266,12 +266,17 @@ int lba_setup_host_profile(const lba_config* cfg, const lba_kf* kfs, int32_t n_k
                            const lba_obs* obs, int32_t n_obs, const lba_prior* priors, int32_t n_priors,
                            const int32_t* vel_kfs, int32_t n_vel, const lba_cam* cams, int32_t n_cam,
                            double phase_ms[3], int32_t counts[5]);
-/* How the reduced camera system is solved (after lba_set_problem): out[0] panels of the dissection's
- * tail separator (rows that reach back to the first panels: the last keyframes of a loop closure),
- * out[1] panels of CHOL_NB rows, out[2] tiles in the envelope of the factor, out[3] 1 for the
- * substitution (band) solve, 0 for the L^-1-tile solve, out[4] panels on the factorisation's dependent
- * chain (max(A, B) + both separators of the dissection [A | B | S1 | S2]). */
-int lba_solver_info(const lba_problem* p, int32_t out[5]);
+/* How the reduced camera system is solved (after lba_set_problem), at the granularity of panels of
+ * CHOL_NB = 32 rows: out[0] panels of the loop-closure tail (rows that reach back to the first panels,
+ * ordered last), out[1] panels, out[2] stored 32 x 32 tiles of the factor L (fill-in included), out[3] 1
+ * for the substitution (band) solve, 0 for the L^-1-tile solve, out[4] panels on the factorisation's
+ * dependent chain (the depth of the elimination tree), out[5] levels of the nested dissection, out[6]
+ * tiles of the lower triangle of S (the pattern before fill-in), out[7] fill-in tiles (out[2] - out[6]). */
+int lba_solver_info(const lba_problem* p, int32_t out[8]);
+/* Algorithmic FLOPs of one solve of the reduced camera system, from the symbolic structure of L:
+ * out[0] the tile factorisation (per column with m tiles below the diagonal: potrf + m trsm + m(m+1)/2
+ * trailing tile updates), out[1] the forward and back substitutions. */
+int lba_solver_flops(const lba_problem* p, double out[2]);
 /* Device memory (bytes) the problem's buffers hold: the reduced system and its factor are packed envelope
  * tiles (O(envelope), not O(npose^2)); the dense H_pp of lba_linearize is allocated only when asked for.
  * LBA_E_ARG (< 0) for a null problem. */

@@ -31,3 +31,17 @@ def harness():
         os.makedirs(os.path.dirname(out), exist_ok=True)
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", src, "-o", out])
     return ctypes.CDLL(out)
+
+
+@pytest.fixture(scope="session")
+def plan_harness():
+    """Host build of the reduced camera system's ordering / symbolic factorisation (lba_plan.hpp)."""
+    import ctypes
+    import subprocess
+    src = os.path.join(ROOT, "tests", "native", "plan_harness.cpp")
+    out = os.path.join(ROOT, "tests", "native", "_build", "libplan_harness.so")
+    deps = [src, os.path.join(ROOT, "amc-slam_amd", "csrc", "lba_plan.hpp")]
+    if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(d) for d in deps):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", src, "-o", out])
+    return ctypes.CDLL(out)

@@ -19,7 +19,7 @@ HEADER = os.path.join(ROOT, "include", "amc_lba.h")
 def declared_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(lba_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|void|const char\*)\s+(lba_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_header_declares_the_boundary():

@@ -60,11 +60,11 @@ def test_cfg4_full_size_single_gpu(cfg4):
     # the reduced system and its factor are packed envelope tiles: device memory O(envelope) (dense
     # npad x npad storage of S and L alone would be 2 x 28.8 GB)
     info = p.solver_info()
-    env_bytes = 2 * info["envelope_tiles"] * 32 * 32 * 8
+    env_bytes = 2 * info["tiles"] * 32 * 32 * 8
     assert env_bytes < 2e9, env_bytes
     assert p.device_bytes() < 12e9, p.device_bytes()
     print(f"cfg4 device bytes {p.device_bytes() / 1e9:.2f} GB (S + L envelopes {env_bytes / 1e9:.2f} GB, "
-          f"{info['envelope_tiles']} tiles of {info['panels']} panels)")
+          f"{info['tiles']} tiles of {info['panels']} panels)")
     chi, _, _ = p.eval()
     assert abs(chi - chi_o) <= 1e-9 * chi_o
     n, st = p.optimize(2)

@@ -7,7 +7,9 @@ The rows of the last keyframes reach back to the first panel, which defeats the 
 cuts off a tail separator S2 of such rows: [A | S1 | B | S2], factored as [A | B | S1 | S2], so A and B
 stay concurrent (lba_solver_info: tail, chain).  Checked against the oracle's pivoted LDLT of the
 whole system on the L^-1-tile and the substitution (band) solves, and against the dissection without a
-tail (LBA_ND_NO_TAIL) on the same window."""
+tail (LBA_ND_NO_TAIL) on the same window.  A trajectory of three laps (every place revisited twice:
+every lap couples every other one) needs the graph dissection (lba_plan.hpp); its chain, levels and
+fill are reported by lba_solver_info."""
 import os
 
 import numpy as np
@@ -20,11 +22,20 @@ from amc_lba.synth import make_config_window, make_window
 
 pytestmark = pytest.mark.gpu
 
+LAPS3 = dict(n_opt_kf=149, n_fixed=1, n_lm=12000, obs_per_lm=6, n_cam=4, gp=True, global_ba=True, seed=7, loop=3)
 LOOP_MID = dict(n_opt_kf=99, n_fixed=1, n_lm=8000, obs_per_lm=6, n_cam=4, gp=True, global_ba=True, seed=6, loop=True)
 
 
 def _rel(a, b):
     return np.abs(a - b).max() / max(np.abs(b).max(), 1e-300)
+
+
+def _with_env(key, val, fn):
+    os.environ[key] = val
+    try:
+        return fn()
+    finally:
+        del os.environ[key]
 
 
 def _no_tail(fn):
@@ -125,3 +136,57 @@ def test_large_loop_band_solve():
     p2 = Problem(win, early_stop=0)
     n2, st2 = p2.optimize(3)
     assert st2.chi2_final == st.chi2_final and st2.trials == st.trials
+
+
+def test_three_laps_window_revisits():
+    win = make_window(**LAPS3)
+    o = win.obs
+    lap = np.minimum(o["kf_b"], 149) * 3 // 150
+    seen = np.zeros((len(win.lm), 3), bool)
+    seen[o["lm"], lap] = True
+    assert (seen.sum(1) == 3).mean() > 0.5   # most landmarks are seen on every lap
+
+
+@pytest.mark.parametrize("flags", [0, FLAG_BAND_SOLVE])
+def test_three_laps_match_oracle(flags):
+    """Two revisits of every place: the step and six LM iterations against the oracle; the graph
+    dissection's chain below half the panels (the interval dissection cannot cut the laps apart) with
+    the same step."""
+    win = make_window(**LAPS3)
+    o = orc.Oracle(win)
+    H_o, b_o, _ = o.build_system()
+    lam = win.cfg["lambda_init"]
+    ok_o, dx_o = o.solve(lam)
+    p = Problem(win, flags=flags)
+    info = p.solver_info()
+    print("three laps:", info, "flops", p.solver_flops())
+    assert info["chain"] < 0.5 * info["panels"] and info["levels"] >= 2
+    assert info["fill"] == info["tiles"] - info["s_tiles"] and info["fill"] >= 0
+    res, H, b, _ = p.linearize()
+    assert _rel(H, H_o) < 1e-9 and _rel(b, b_o) < 1e-9
+    ok, dx = p.solve_step(lam)
+    assert ok and ok_o
+    n = p.pose_dim
+    assert _rel(dx[:n], dx_o[:n]) <= 1e-6 and _rel(dx[n:], dx_o[n:]) <= 1e-6
+    r = o.normal_residual(lam, dx)
+    assert np.abs(r).max() <= 1e-8 * np.abs(b_o).max()
+
+    def interval_only():
+        q = Problem(win, flags=flags)
+        q.linearize()
+        ok2, dx2 = q.solve_step(lam)
+        assert ok2
+        return q.solver_info(), dx2
+
+    info_iv, dx_iv = _with_env("LBA_ND_METHOD", "1", interval_only)
+    assert info_iv["chain"] > info["chain"]
+    assert _rel(dx_iv, dx) <= 1e-8
+    o2 = orc.Oracle(win, early_stop=0)
+    n_o, st_o = o2.optimize(6)
+    p2 = Problem(win, early_stop=0, flags=flags)
+    n2, st = p2.optimize(6)
+    assert n2 == n_o and st.trials == st_o.trials
+    assert abs(st.chi2_final - st_o.chi2_final) <= 1e-7 * st_o.chi2_final
+    kf, lm = p2.state()
+    kf_o, lm_o = o2.state()
+    assert _rel(kf["t"], kf_o["t"]) <= 1e-6 and _rel(lm, lm_o) <= 1e-6
