@@ -82,7 +82,8 @@ def lib():
         L.lba_farm_plan.argtypes = [vp, _lp, _ip, _lp, _ip, _ip]
         L.lba_farm_exchange.argtypes = [vp]
         L.lba_solver_info.argtypes = [vp, _ip]
-        L.lba_solver_flops.argtypes = [vp, _dp]
+        if hasattr(L, "lba_solver_flops"):   # (absent from builds before it: A/B runs of older libraries)
+            L.lba_solver_flops.argtypes = [vp, _dp]
         L.lba_device_bytes.argtypes = [vp]
         L.lba_device_bytes.restype = ctypes.c_int64
         L.lba_setup_host_profile.argtypes = [ctypes.POINTER(LbaConfig), vp, ctypes.c_int32, vp, ctypes.c_int32, vp,

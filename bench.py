@@ -246,7 +246,10 @@ def main():
 
     # warmup (not timed)
     sinfo = prob.solver_info()   # (panels, tiles, chain, dissection levels, fill: reported below)
-    sflops = prob.solver_flops()   # (the solve's algorithmic FLOPs below)
+    try:
+        sflops = prob.solver_flops()   # (the solve's algorithmic FLOPs below)
+    except AttributeError:             # (an older library under A/B)
+        sflops = (float("nan"), float("nan"))
     if args.warmup > 0:
         prob.optimize(args.warmup)
     torch.cuda.synchronize()

@@ -6,3 +6,4 @@ timeout -k 10 600 python -u -m pytest -x -v -s --timeout 300 --timeout-method th
 rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|three laps|Error|assert" gpurun_out/$T.pytest.log | tail -8
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 bash scripts/ab_nd.sh $T
+
