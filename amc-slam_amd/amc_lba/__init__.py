@@ -39,6 +39,14 @@ def check_fresh(which="engine"):
         raise RuntimeError(f"{why}: run python -c 'import __graft_entry__ as g; g.build()'")
 
 
+def lib_digest(path=None):
+    """sha256 (first 16 hex digits) of the engine library file: profiles measured on one build carry it,
+    so a summary of another build is not taken for this one's."""
+    import hashlib
+    with open(path or LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def lib():
     """Load libamc_lba.so (built by __graft_entry__.build()); raises if it is missing or stale."""
     global _lib

@@ -98,16 +98,24 @@ def schur_terms(win):
 
 def pmc_traffic(workload, kernel="k_lin_schur"):
     """HBM bytes per launch of the kernel from the committed rocprofv3 PMC summary (FETCH_SIZE
-    doubled per the gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md §HBM), or None."""
+    doubled per the gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md §HBM) of THIS library build
+    (the summary's lib_sha256 must match the loaded library's digest), or (None, why)."""
+    import amc_lba
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc_{kernel}_*.json")))
+    digest = amc_lba.lib_digest()
+    stale = []
     for f in reversed(files):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
-            return float(d["hbm_bytes_per_launch"])
-    return None
+        if d.get("workload") != workload or not d.get("hbm_bytes_per_launch"):
+            continue
+        if d.get("lib_sha256") != digest:
+            stale.append(os.path.basename(f))
+            continue
+        return float(d["hbm_bytes_per_launch"]), os.path.basename(f)
+    return None, (f"no PMC summary of this library build ({digest}); stale: {stale}" if stale else "no PMC summary")
 
 
 def cpu_model():
@@ -326,7 +334,7 @@ def main():
                       "FLOPs, sets its time")
         achieved = B / (k_ms * 1e-3) / 1e9 if n_k else None
         workload = f"{args.config}: {win.name or args.config} synthetic window"
-        traffic = pmc_traffic(args.config)
+        traffic, traffic_src = pmc_traffic(args.config)
         line = {
             "metric": metric_for(args.config, W, gba),
             "value": value,
@@ -348,7 +356,8 @@ def main():
                        "setup_s": t_setup},
             "roofline": {"bound": "hbm", "kernel": "k_lin_schur", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                         "traffic": traffic, "bytes_per_launch": B, "avg_launch_ms": k_ms,
+                         "traffic": traffic, "traffic_source": traffic_src, "bytes_per_launch": B,
+                         "avg_launch_ms": k_ms,
                          "timed_launches": n_k},
             "roofline_fp64": {"kernel": "k_lin_schur", "flops_per_launch": F,
                               "achieved": F / (k_ms * 1e-3) / 1e12 if n_k else None,

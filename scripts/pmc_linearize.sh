@@ -14,7 +14,7 @@ cd /tmp && export TMPDIR=/tmp
 run_pass() {   # name, counters...
   local name=$1; shift
   timeout -s KILL 300 rocprofv3 --pmc "$@" --kernel-include-regex "$KERNEL" --output-format csv -d "$OUT/$name" -o pmc \
-      -- python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu > "$OUT/$name.log" 2>&1
+      -- python3 "$ROOT/bench.py" --config "${PMC_CONFIG:-cfg1_local_50kf}" --steps 10 --warmup 2 --no-cpu > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "pmc $name rc=$rc"
   return $rc

@@ -10,6 +10,9 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "amc-slam_amd"))
+from amc_lba import lib_digest  # noqa: E402
+
 
 def per_dispatch(dirname, counter, kernel):
     vals = {}
@@ -36,7 +39,7 @@ def main():
     f_kb, w_kb = median(fetch), median(write)
     fetch_b = 2.0 * f_kb * 1024.0   # gfx950: FETCH_SIZE reports half the bytes of wide streaming reads
     write_b = w_kb * 1024.0
-    out = {"workload": "cfg1_local_50kf", "kernel": kernel, "dispatches": [len(fetch), len(write)],
+    out = {"workload": os.environ.get("PMC_CONFIG", "cfg1_local_50kf"), "kernel": kernel, "lib_sha256": lib_digest(), "dispatches": [len(fetch), len(write)],
            "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
            "hbm_read_bytes_per_launch": fetch_b, "hbm_write_bytes_per_launch": write_b,
            "hbm_bytes_per_launch": fetch_b + write_b,
