@@ -10,7 +10,8 @@
 //   pose samples  [n_smp][GPS_STRIDE]: per GP (prev KF, KF, observation time) the interpolated pose
 //                 and the 6x24 Jacobian factor N (lba::GPSample; one per camera time stamp, not per
 //                 observation), then one per KF (its pose, N = [0 | I 0]) for EdgeMono / EdgeStereo
-//   Hpl           [n_pairs][12][3] one block per unique (non-fixed KF, landmark)
+//   Hpl           [n_hpl][12][3] one block per (non-fixed KF, heavy landmark) and per segment pair (regular
+//                 tiles keep theirs in LDS; their landmarks are back-substituted in the sample space)
 //   Hll, bl       [n_lm][9], [n_lm][3]
 //   mslab         per (tile, pose sample) partial of M = sum rho' w J1^T J1 and g = sum rho' w J1^T e
 //                 (J1 w.r.t. the sample's pose), slots sorted by sample
@@ -87,14 +88,14 @@ struct DevProblem {
     int npad;               // np rounded up to CHOL_NB: leading dimension of S / Lm (identity tail)
     int n_entries, n_sentries, n_ublocks;
     // slab and table extents (LBA_DEBUG_BOUNDS builds check every indexed write against them)
-    int n_mslots, n_hslots, n_gslots, n_sslots, n_gpslots, n_chi, n_pairs_all, n_lm_all;
+    int n_mslots, n_hslots, n_gslots, n_sslots, n_gpslots, n_chi, n_lm_all;
     // observations (device order)
     const int* ob_meta;
     const int* ob_kfa;
     const int* ob_kfb;
     const int* ob_smp;      // pose sample (lba::GPSample): GP sample, or n_gps + kf_b for EdgeMono/Stereo
     const int* ob_lm;
-    const int* ob_row;
+    const int* ob_row;      // tile-local LDS row | (regular tiles) tile-local pose sample << 16
     const double* ob_z;     // [n_obs][3]
     const double* ob_w;
     // keyframes
@@ -153,6 +154,16 @@ struct DevProblem {
     const int* lm_r0;       // CSR into lm_rows: tile-local rows
     const int* lm_rows;
     const int* lm_pair0;    // [n_lm + 1] landmark -> pairs
+    // k_update's back-substitution of the regular tiles' landmarks in the sample space (no Hpl): per tile
+    // sample its pose sample (tsm_smp), per pose sample the pose blocks of its KF a / KF b / extrinsic
+    // (-1: fixed or none) and the camera of the extrinsic factor (smp_blk, 4 ints), per device landmark its
+    // observations (lm_obs0, [n_lm + 1])
+    const int* tsm_smp;
+    const int* smp_blk;
+    const int* lm_obs0;
+    // Hpl is stored only for the heavy landmarks' pairs: pair index q lives at slot q - hpl_base
+    // (canonical heavy pairs, then the segment pairs); n_hpl slots
+    int hpl_base, n_hpl;
     // partial-sum slabs are sorted by their reduction target, so every reduction below reads
     // one contiguous range (coalesced) instead of chasing a source list
     const int* seg_slot;    // per slab entry (pose samples, motion priors, velocity edges, extrinsic priors):

@@ -925,7 +925,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     }
                     for (int q = lobs0[d]; q < lobs0[e]; ++q) {
                         const int i = sloc[dsmp[q]];
-                        ob_row[q] = srows[i];
+                        ob_row[q] = srows[i] | (i << 16);   // (+ the tile-local sample: k_update's back-substitution)
                         srows[i] += ddim[q];
                     }
                 }
@@ -944,7 +944,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                         pair_lk[q] = local(k) | ((l - d) << 8);
                     }
                     for (int o = lobs0[l]; o < lobs0[l + 1]; ++o)
-                        for (int r = 0; r < ddim[o]; ++r) T.lm_rows.push_back(ob_row[o] + r);
+                        for (int r = 0; r < ddim[o]; ++r) T.lm_rows.push_back((ob_row[o] & 0xffff) + r);
                     lm_r0[l + 1] = (int)T.lm_rows.size();
                 }
                 // Schur entries: every (k1 <= k2) pose-block pair co-observed by a landmark of the tile, in
@@ -1276,6 +1276,18 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.pair_lm = dupload(p, pair_lm); D.pair_kf = dupload(p, pair_kf); D.pair_r0 = dupload(p, pair_r0);
     D.pair_rows = dupload(p, pair_rows); D.lm_r0 = dupload(p, lm_r0); D.lm_rows = dupload(p, lm_rows);
     D.lm_pair0 = dupload(p, lm_pair0);
+    {   // k_update's sample-space back-substitution of the regular tiles' landmarks
+        std::vector<int> smp_blk(4 * (size_t)std::max(n_smp, 1), -1);
+        for (int sm = 0; sm < n_smp; ++sm) {
+            smp_blk[4 * (size_t)sm] = ent_a[sm];
+            smp_blk[4 * (size_t)sm + 1] = ent_b[sm];
+            smp_blk[4 * (size_t)sm + 2] = ent_e[sm];
+            smp_blk[4 * (size_t)sm + 3] = ent_cam[sm];
+        }
+        D.tsm_smp = dupload(p, tsm_smp);
+        D.smp_blk = dupload(p, smp_blk);
+        D.lm_obs0 = dupload(p, lobs0);
+    }
     D.hfin = p->d_hfin;
     D.hlog = p->d_hlog;
     if (std::getenv("LBA_PHASE_TIMING")) {
@@ -1653,9 +1665,11 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     p->s_bytes = 2 * n_env_doubles * sizeof(double);
     D.Lm = dalloc<double>(p, n_env_doubles + 1);
     D.LinvT = dalloc<double>(p, (size_t)npad * CHOL_NB + 1);
-    D.Hpl = dalloc<double>(p, (size_t)36 * std::max(n_pairs + n_segpairs, 1));   // canonical pairs, then segment pairs
+    // Hpl: only the heavy landmarks' canonical pairs, then the segment pairs (regular tiles keep theirs in LDS)
+    D.hpl_base = lm_pair0[n_reg];
+    D.n_hpl = n_pairs - D.hpl_base + n_segpairs;
+    D.Hpl = dalloc<double>(p, (size_t)36 * std::max(D.n_hpl, 1));
     D.Hll = dalloc<double>(p, (size_t)9 * std::max(nl + n_seg, 1));               // landmarks, then segments
-    D.n_pairs_all = n_pairs + n_segpairs;
     D.n_lm_all = nl + n_seg;
     D.bl = dalloc<double>(p, (size_t)3 * std::max(nl + n_seg, 1));
     D.Dinv = dalloc<double>(p, (size_t)9 * std::max(nl, 1));
@@ -1677,8 +1691,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.chi_lin = dalloc<double>(p, nchi + 1);
     D.n_chi = nchi;
     D.chi_eval = dalloc<double>(p, nchi + 1);
-    // k_update: one workgroup per GP pair, then KFs and landmarks at 64 per workgroup
-    D.n_upd_blocks = D.n_gp + (n_kfs + 63) / 64 + (nl + 63) / 64;
+    // k_update: one workgroup per GP pair, KFs at 64 per workgroup, one per regular tile, heavy landmarks at 64
+    D.n_upd_blocks = D.n_gp + (n_kfs + 63) / 64 + n_stiles + (n_heavy + 63) / 64;
     if (D.n_upd_blocks == 0) D.n_upd_blocks = 1;
     D.scale_part = dalloc<double>(p, D.n_upd_blocks);
     D.info = dalloc<int>(p, 1);

@@ -184,7 +184,7 @@ __device__ __forceinline__ double lin_obs(const DevProblem& P, const double* gps
     double J1[6 * DIM], Jp[3 * DIM];
     obs_j1<DIM>(Rwb, cd, Xb, Xc, bf, J1, Jp);
     const double s = r1 * w;   // robustInformation = rho' * Omega (base_edge.h:96-102), Omega = w I
-    const int row = P.ob_row[o];
+    const int row = P.ob_row[o] & 0xffff;
 #pragma unroll
     for (int d = 0; d < DIM; ++d) {
         double* R = rows + (row + d) * ROW_STRIDE;
@@ -237,11 +237,20 @@ constexpr int PREP_THREADS = 64;
 constexpr int PREP_SCHUNK = 32;   // samples per pass (one lane each; LDS staging of their Jr / Ad blocks)
 // (inlined into k_gp_prep and k_update: a noinline body, one copy for both, measured 4.5 % slower LM
 // iterations, profiles/r3e_ab_update_inline_wait.txt; the two copies may round differently in the last bit)
+// shm: PREP_SHM doubles of LDS (the caller's, so k_update's roles share one allocation)
+constexpr int PREP_PR = (sizeof(GPPair) / sizeof(double) + 1) & ~1;
+constexpr int PREP_SHM = PREP_PR + 36 + 36 + 8 + PREP_SCHUNK * (18 + 9 + 9 + 3);
 __device__ __forceinline__ void gp_pair_prep(const DevProblem& P, double* gps, int i, const double* ka,
-                                             const double* kb, int jac, unsigned long long* pst = nullptr) {
-    __shared__ GPPair pr;
-    __shared__ double AdI[36], ad2[36], vbs[6];
-    __shared__ double sJr[PREP_SCHUNK][18], sRm[PREP_SCHUNK][9], stR[PREP_SCHUNK][9], sg[PREP_SCHUNK][3];
+                                             const double* kb, int jac, double* shm,
+                                             unsigned long long* pst = nullptr) {
+    GPPair& pr = *reinterpret_cast<GPPair*>(shm);
+    double* AdI = shm + PREP_PR;
+    double* ad2 = AdI + 36;
+    double* vbs = ad2 + 36;
+    double(*sJr)[18] = reinterpret_cast<double(*)[18]>(vbs + 8);
+    double(*sRm)[9] = reinterpret_cast<double(*)[9]>(sJr + PREP_SCHUNK);
+    double(*stR)[9] = sRm + PREP_SCHUNK;
+    double(*sg)[3] = reinterpret_cast<double(*)[3]>(stR + PREP_SCHUNK);
     const int tid = threadIdx.x;
     // (diagnostics: pst = s_memrealtime stamps after each phase, thread 0)
 #define PREP_STAMP(k) do { if (pst && tid == 0) pst[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -358,8 +367,9 @@ __global__ __launch_bounds__(PREP_THREADS) void k_gp_prep(DevProblem P, int sel,
     const double* __restrict__ kst = P.kbuf[si];
     double* gps = P.gpsb[si];
     if ((int)blockIdx.x < P.n_gp) {
+        __shared__ double shm[PREP_SHM];
         const int i = blockIdx.x;
-        gp_pair_prep(P, gps, i, kst + (size_t)P.gp_kfa[i] * KF_STRIDE, kst + (size_t)P.gp_kfb[i] * KF_STRIDE, jac);
+        gp_pair_prep(P, gps, i, kst + (size_t)P.gp_kfa[i] * KF_STRIDE, kst + (size_t)P.gp_kfb[i] * KF_STRIDE, jac, shm);
         return;
     }
     const int k = (blockIdx.x - P.n_gp) * PREP_THREADS + threadIdx.x;
@@ -722,7 +732,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
         osm[tid] = P.ob_smp[o];
         ocam[tid] = cam;
         const bool st = kind == LBA_STEREO_GP || kind == LBA_STEREO;
-        orow[tid] = P.ob_row[o] | ((st ? 3 : 2) << 16);
+        orow[tid] = (P.ob_row[o] & 0xffff) | ((st ? 3 : 2) << 16);
         const int wr = (mode & LS_RES) ? 1 : 0;
         rho0 = st ? lin_obs<3>(P, gps, kst, lst, camd, o, cam, gp, rows, rw, wr)
                   : lin_obs<2>(P, gps, kst, lst, camd, o, cam, gp, rows, rw, wr);
@@ -849,8 +859,11 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
                                        n[4] * g[12 + a] + n[5] * g[15 + a];
             }
         }
-        if (LBA_INB(P, pair0 + pl, P.n_pairs_all, "Hpl")) {
-            double* Hg = P.Hpl + (size_t)(pair0 + pl) * 36 + 18 * half;
+        // only the segment tiles of heavy landmarks store their Hpl (k_expand merges them); a regular tile's
+        // Hpl lives in LDS until its elimination, and k_update back-substitutes its landmarks in the sample
+        // space without it
+        if (tile >= P.n_stiles && LBA_INB(P, pair0 + pl - P.hpl_base, P.n_hpl, "Hpl")) {
+            double* Hg = P.Hpl + (size_t)(pair0 + pl - P.hpl_base) * 36 + 18 * half;
 #pragma unroll
             for (int q = 0; q < 18; ++q) Hg[q] = hacc[q];
         }
@@ -968,11 +981,12 @@ __device__ void heavy_item(const DevProblem& P, int h, double lambda, int schur,
         if (tid < 9) P.Hll[(size_t)l * 9 + tid] = v;
         else P.bl[(size_t)l * 3 + tid - 9] = v;
     }
+    double* const Hpl = P.Hpl - (size_t)P.hpl_base * 36;   // (pair index -> Hpl slot: only heavy pairs are stored)
     for (int t = tid; t < nhp * 36; t += PRI_THREADS) {
         const int j = t / 36, e = t - 36 * j;
         double v = 0.0;
-        for (int q = P.hp_src0[hp0 + j]; q < P.hp_src0[hp0 + j + 1]; ++q) v += P.Hpl[(size_t)P.hp_src[q] * 36 + e];
-        P.Hpl[(size_t)(cp0 + j) * 36 + e] = v;
+        for (int q = P.hp_src0[hp0 + j]; q < P.hp_src0[hp0 + j + 1]; ++q) v += Hpl[(size_t)P.hp_src[q] * 36 + e];
+        Hpl[(size_t)(cp0 + j) * 36 + e] = v;
     }
     if (!schur) return;
     __syncthreads();
@@ -987,7 +1001,7 @@ __device__ void heavy_item(const DevProblem& P, int h, double lambda, int schur,
     const double* Di = HB + 12;
     for (int t = tid; t < nhp * 12; t += PRI_THREADS) {   // V = Hpl Dinv and the rhs partial V bl
         const int j = t / 12, r = t - 12 * j;
-        const double* hr = P.Hpl + (size_t)(cp0 + j) * 36 + r * 3;
+        const double* hr = Hpl + (size_t)(cp0 + j) * 36 + r * 3;
         double* vr = P.Vh + (size_t)(hp0 + j) * 36 + r * 3;
         double g = 0.0;
         for (int a = 0; a < 3; ++a) {
@@ -1004,7 +1018,7 @@ __device__ void heavy_item(const DevProblem& P, int h, double lambda, int schur,
         int a = 0, rem = pp;
         while (rem >= nhp - a) { rem -= nhp - a; ++a; }
         const double* v = P.Vh + (size_t)(hp0 + a) * 36 + i * 3;
-        const double* hb = P.Hpl + (size_t)(cp0 + a + rem) * 36 + jj * 3;
+        const double* hb = Hpl + (size_t)(cp0 + a + rem) * 36 + jj * 3;
         stv<WT>(P.sslab + (size_t)P.hv_sslot[ss0 + pp] * 144 + e, v[0] * hb[0] + v[1] * hb[1] + v[2] * hb[2]);
     }
 }
@@ -2105,19 +2119,140 @@ __device__ __attribute__((noinline)) void kf_trial_state(const DevProblem& P, co
     }
 }
 
+// One observation's share of the back-substitution, sum_k Hpl(k, l)^T x_k = sum_{o of l} G_o^T t_s(o): with
+// G_o = rho' w sum_rows J1^T Jp (the observation's part of every Hpl block it feeds, k_lin_schur phase 3) and
+// t_s = N_s x (the step of the observation's pose sample), G_o^T t = rho' w sum_rows Jp^T (J1 t).  The
+// linearisation is recomputed at the state the sweep linearised (the same inputs and code as lin_obs).
+template <int DIM>
+__device__ __forceinline__ void bs_obs(const DevProblem& P, const double* gps, const double* kst, const double* lst,
+                                       const double* camd, int o, int cam, bool gp, const double* t, double* v) {
+    CamD cd;
+    load_cam(camd + (size_t)cam * CAMD_STRIDE, &cd);
+    double Rwb[9], twb[3];
+    const double bf = obs_pose(P, gps, kst, o, gp, Rwb, twb);
+    double z[DIM];
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) z[d] = P.ob_z[3 * (size_t)o + d];
+    const double w = P.ob_w[o];
+    double Xb[3], Xc[3], e[DIM];
+    project_residual<DIM>(Rwb, twb, cd, lst + (size_t)P.ob_lm[o] * 3, z, bf, Xb, Xc, e);
+    double chi = 0.0;
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) chi += e[d] * (w * e[d]);
+    double r0, r1;
+    huber(chi, DIM == 3 ? P.huber_stereo : P.huber_mono, &r0, &r1);
+    double J1[6 * DIM], Jp[3 * DIM];
+    obs_j1<DIM>(Rwb, cd, Xb, Xc, bf, J1, Jp);
+    const double s = r1 * w;
+    v[0] = v[1] = v[2] = 0.0;
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) {
+        double u = 0.0;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) u += J1[d * 6 + j] * t[j];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) v[a] += u * Jp[d * 3 + a];
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) v[a] *= s;
+}
+
+// The landmarks of regular tile `tile` (one UPD_THREADS workgroup): dx_l = Dinv_l (b_l - sum_{o of l} G_o^T t_s(o))
+// (block_solver.hpp:461-482), oplus, computeScale partial.  Returns this thread's scale term.
+constexpr int UPD_TILE_OBS_PER_THREAD = (TILE_OBS + 63) / 64;
+constexpr int BS_SHM = TILE_SMP * 6 + TILE_OBS * 3;
+__device__ double bs_tile(const DevProblem& P, int tile, int si, bool ok, double lambda, double* lo, double* shm) {
+    double(*tsh)[6] = reinterpret_cast<double(*)[6]>(shm);                  // t_s per tile sample
+    double(*vsh)[3] = reinterpret_cast<double(*)[3]>(shm + TILE_SMP * 6);   // G_o^T t per observation
+    const int tid = threadIdx.x;
+    const int lm0 = P.tile_lm0[tile], nlm = P.tile_nlm[tile];
+    const double* __restrict__ lst = P.lbuf[si];
+    if (ok) {
+        const int ts0 = P.tile_smp0[tile], nts = P.tile_nsmp[tile];
+        const int obs0 = P.tile_obs0[tile], nobs = P.tile_nobs[tile];
+        const double* __restrict__ kst = P.kbuf[si];
+        const double* __restrict__ gps = P.gpsb[si];
+        const double* __restrict__ camd = P.camdb[si];
+        // t_s(r) = sum_c N_s(r, c) [x_a; x_b](c) (+ the extrinsic factor on x_e): N column c at 12 + 6 c
+        for (int task = tid; task < nts * 6; task += UPD_THREADS) {
+            const int ts = task / 6, r = task - 6 * ts;
+            const int sm = P.tsm_smp[ts0 + ts];
+            const int* bk = P.smp_blk + 4 * (size_t)sm;
+            const double* N = gps + (size_t)sm * GPS_STRIDE + 12 + r;
+            double acc = 0.0;
+            for (int side = 0; side < 3; ++side) {
+                const int h = bk[side];
+                if (h < 0) continue;
+                const double* x = P.xsol + 12 * (size_t)h;
+                const double* Nc = side < 2 ? N + 6 * 12 * side : camd + (size_t)bk[3] * CAMD_STRIDE + 16 + r;
+#pragma unroll
+                for (int c = 0; c < 12; ++c) acc += Nc[6 * c] * x[c];
+            }
+            tsh[ts][r] = acc;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < UPD_TILE_OBS_PER_THREAD; ++k) {
+            const int ol = tid + UPD_THREADS * k;
+            if (ol < nobs) {
+                const int o = obs0 + ol;
+                const int meta = P.ob_meta[o];
+                const int kind = meta & 15, cam = meta >> 4;
+                const bool gp = kind <= LBA_STEREO_GP;
+                const double* t = tsh[P.ob_row[o] >> 16];
+                if (kind == LBA_STEREO_GP || kind == LBA_STEREO) bs_obs<3>(P, gps, kst, lst, camd, o, cam, gp, t, vsh[ol]);
+                else bs_obs<2>(P, gps, kst, lst, camd, o, cam, gp, t, vsh[ol]);
+            }
+        }
+        __syncthreads();
+    }
+    double sc = 0.0;
+    if (tid < nlm) {
+        const int l = lm0 + tid;
+        double xl[3];
+        double* xd = P.x + P.np + 3 * (size_t)l;
+        if (ok) {
+            double c[3] = {P.bl[3 * (size_t)l], P.bl[3 * (size_t)l + 1], P.bl[3 * (size_t)l + 2]};
+            const int ob0 = P.tile_obs0[tile];
+            for (int o = P.lm_obs0[l]; o < P.lm_obs0[l + 1]; ++o) {
+                const double* v = vsh[o - ob0];
+                c[0] -= v[0]; c[1] -= v[1]; c[2] -= v[2];
+            }
+            const double* D = P.Dinv + (size_t)l * 9;
+            for (int a = 0; a < 3; ++a) {
+                xl[a] = D[a * 3] * c[0] + D[a * 3 + 1] * c[1] + D[a * 3 + 2] * c[2];
+                xd[a] = xl[a];
+            }
+        } else {
+            xl[0] = xd[0]; xl[1] = xd[1]; xl[2] = xd[2];
+        }
+        for (int a = 0; a < 3; ++a) {
+            lo[3 * (size_t)l + a] = lst[3 * (size_t)l + a] + xl[a];
+            sc += xl[a] * (lambda * xl[a] + P.bl[3 * (size_t)l + a]);
+        }
+    }
+    return sc;
+}
+
 // The step and the trial state (block_solver.hpp:461-482 back-substitution, sparse_optimizer.cpp:422-435
 // oplus, computeScale partials), fused with the pose samples of the trial state:
 //   workgroups [0, n_gp): one per GP pair: its two KFs' trial states (kf_trial_state), then the pair's
 //     samples with their Jacobian factors (gp_pair_prep, jac) into the trial state's sample buffer, so
 //     an accepted trial's next linearisation needs no preparation launch;
-//   then one KF per thread (trial state, KF pose sample, x, scale), then one landmark per thread
-//   (dx_l = Dinv (bl - sum Hpl^T dx_p), oplus, scale).
+//   then one KF per thread (trial state, KF pose sample, x, scale); then one workgroup per regular tile
+//   (bs_tile: its landmarks back-substituted in the sample space, oplus, scale); then one heavy landmark
+//   per thread (dx_l = Dinv (bl - sum Hpl^T dx_p), oplus, scale).
+// k_update's LDS, one allocation for its three roles: a GP pair (its KFs' trial-state slots, then
+// gp_pair_prep's buffers), a KF block (kf_trial_state's output slots: the function stays one compiled body
+// for both callers, their trial states must agree bitwise, without its output arrays living in scratch), a
+// tile (bs_tile).  (One allocation keeps k_update at 8 workgroups per CU, so every tile is resident at once.)
+constexpr int UPD_GP_SHM = 2 * 12 + 2 * KF_STRIDE + PREP_SHM;
+constexpr int UPD_KF_SHM = UPD_THREADS * (12 + KF_STRIDE);
+constexpr int UPD_SHM = UPD_GP_SHM > UPD_KF_SHM ? (UPD_GP_SHM > BS_SHM ? UPD_GP_SHM : BS_SHM)
+                                                : (UPD_KF_SHM > BS_SHM ? UPD_KF_SHM : BS_SHM);
 __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lambda_arg, int sel, int gate, int jac) {
     __shared__ double red[UPD_THREADS / 64];
-    __shared__ double kab[2][KF_STRIDE];
-    // kf_trial_state's outputs in LDS (one slot per thread): the function stays one compiled body for
-    // both callers (their trial states must agree bitwise) without its output arrays living in scratch
-    __shared__ double kdl[UPD_THREADS][12], knl[UPD_THREADS][KF_STRIDE];
+    __shared__ double ushm[UPD_SHM];
     if (gated_off(P.ctl, gate)) return;
     // diagnostics (LBA_PHASE_TIMING): s_memrealtime start / end of each workgroup in slots 14 / 15 of the
     // sweep's stamp rows (k_update runs after the sweep; n_upd_blocks <= n_tiles is checked)
@@ -2135,17 +2270,17 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
     const int nkb = (P.n_kf + UPD_THREADS - 1) / UPD_THREADS;
     if ((int)blockIdx.x < P.n_gp) {
         const int i = blockIdx.x;
+        double* kdl = ushm;                    // [2][12]
+        double* kab = ushm + 2 * 12;           // [2][KF_STRIDE]
         if (threadIdx.x < 2) {
             const int k = threadIdx.x ? P.gp_kfb[i] : P.gp_kfa[i];
-            kf_trial_state(P, kst + (size_t)k * KF_STRIDE, P.kf_hidx[k], ok, kdl[threadIdx.x], kab[threadIdx.x]);
+            kf_trial_state(P, kst + (size_t)k * KF_STRIDE, P.kf_hidx[k], ok, kdl + 12 * threadIdx.x,
+                           kab + KF_STRIDE * threadIdx.x);
         }
         __syncthreads();
-#ifdef LBA_EXP_PREP_TWICE   // (experiment: the stamps below then time a warm second run of the same code)
-        gp_pair_prep(P, gps, i, kab[0], kab[1], jac);
-        __syncthreads();
-#endif
 #ifndef LBA_EXP_NO_GPPREP
-        gp_pair_prep(P, gps, i, kab[0], kab[1], jac, ustamp ? P.tdbg_lin + (size_t)blockIdx.x * 16 + 5 : nullptr);
+        gp_pair_prep(P, gps, i, kab, kab + KF_STRIDE, jac, ushm + 2 * 12 + 2 * KF_STRIDE,
+                     ustamp ? P.tdbg_lin + (size_t)blockIdx.x * 16 + 5 : nullptr);
 #endif
         if (threadIdx.x == 0) P.scale_part[blockIdx.x] = 0.0;
         if (ustamp) ustamp[1] = __builtin_amdgcn_s_memrealtime();
@@ -2156,8 +2291,8 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
         const int k = (blockIdx.x - P.n_gp) * UPD_THREADS + threadIdx.x;
         if (k < P.n_kf) {
             const int h = P.kf_hidx[k];
-            double* d = kdl[threadIdx.x];
-            double* kn = knl[threadIdx.x];
+            double* d = ushm + 12 * threadIdx.x;
+            double* kn = ushm + 12 * UPD_THREADS + KF_STRIDE * threadIdx.x;
             kf_trial_state(P, kst + (size_t)k * KF_STRIDE, h, ok, d, kn);
             double* kw = ko + (size_t)k * KF_STRIDE;
             for (int j = 0; j < KF_STRIDE; ++j) kw[j] = kn[j];
@@ -2177,18 +2312,18 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
                     if (P.part_rank == 0) sc += d[j] * (lambda * d[j] + P.bp[12 * h + j]);
                 }
         }
+    } else if ((int)blockIdx.x < P.n_gp + nkb + P.n_stiles) {
+        sc = bs_tile(P, blockIdx.x - P.n_gp - nkb, si, ok, lambda, lo, ushm);
     } else {
-        const int l = (blockIdx.x - P.n_gp - nkb) * UPD_THREADS + threadIdx.x;
+        // heavy landmarks (device indices n_lm - n_heavy ..): through their merged Hpl blocks
+        const int l = P.n_lm - P.n_heavy + (blockIdx.x - P.n_gp - nkb - P.n_stiles) * UPD_THREADS + threadIdx.x;
         if (l < P.n_lm) {
             double xl[3];
             double* xd = P.x + P.np + 3 * (size_t)l;
             if (ok) {
                 double c[3] = {P.bl[3 * (size_t)l], P.bl[3 * (size_t)l + 1], P.bl[3 * (size_t)l + 2]};
-#ifdef LBA_EXP_NO_LMBACK
-                if (c[0] == 12345.5)
-#endif
                 for (int p = P.lm_pair0[l]; p < P.lm_pair0[l + 1]; ++p) {
-                    const double* B = P.Hpl + (size_t)p * 36;
+                    const double* B = P.Hpl + (size_t)(p - P.hpl_base) * 36;
                     const double* xp = P.xsol + 12 * (size_t)P.pair_kf[p];
                     for (int r = 0; r < 12; ++r) {
                         c[0] -= B[r * 3] * xp[r];
