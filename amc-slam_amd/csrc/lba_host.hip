@@ -961,8 +961,15 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     const int nu = (int)uni.size();
                     T.t_sent0.push_back((int)T.sent_l1.size());
                     int nen = 0;
+                    // the diagonal entries (every tile KF has one) first: k_lin_schur gives them 6 tasks (their
+                    // strictly lower 6 x 6 corner is never assembled), the others 8
+                    for (int i = 0; i < nu; ++i) {
+                        ++nen;
+                        T.sent_l1.push_back(i); T.sent_l2.push_back(i);
+                        T.sent_k1.push_back(uni[i]); T.sent_k2.push_back(uni[i]);
+                    }
                     for (int i = 0; i < nu; ++i)
-                        for (int j = i; j < nu; ++j)
+                        for (int j = i + 1; j < nu; ++j)
                             if (co[i][j]) {
                                 ++nen;
                                 T.sent_l1.push_back(i); T.sent_l2.push_back(j);

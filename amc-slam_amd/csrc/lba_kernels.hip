@@ -901,10 +901,22 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
     //      needs no K padding, zero blocks or padded rows.  One task per (Schur entry, 3-row group,
     //      6-column half) keeps its 3 x 6 block of C in registers; every lane walks the tile's landmarks in
     //      the same order, so a wave's LDS reads of one step hit one landmark's pairs (broadcasts, few
-    //      bank conflicts) and D_m^-1 is one broadcast read
+    //      bank conflicts) and D_m^-1 is one broadcast read.  The tile's nkf diagonal entries come first
+    //      with 6 tasks each: rows 6..11 x columns 0..5 of a diagonal block are strictly lower, never assembled
     const int nkf = P.tile_nkf[tile];
-    for (int task = tid; task < nsent * 8; task += LS_THREADS) {
-        const int q = task >> 3, rg = (task >> 1) & 3, ch = task & 1;
+    for (int task = tid; task < nsent * 8 - 2 * nkf; task += LS_THREADS) {
+        int q, rg, ch;
+        if (task < 6 * nkf) {
+            q = task / 6;
+            const int r6 = task - 6 * q;   // (rg, ch): (0,0) (0,1) (1,0) (1,1) (2,1) (3,1)
+            rg = r6 < 4 ? r6 >> 1 : r6 - 2;
+            ch = r6 < 4 ? r6 & 1 : 1;
+        } else {
+            const int t2 = task - 6 * nkf;
+            q = nkf + (t2 >> 3);
+            rg = (t2 >> 1) & 3;
+            ch = t2 & 1;
+        }
         const short* p1 = pidx + (scode[q] & 255) * TILE_LMS;
         const short* p2 = pidx + (scode[q] >> 8) * TILE_LMS;
         double acc[18];
