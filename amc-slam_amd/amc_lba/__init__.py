@@ -98,6 +98,12 @@ def lib():
                                              ctypes.c_int32, vp, ctypes.c_int32, vp, ctypes.c_int32, vp, ctypes.c_int32,
                                              _dp, _ip]
         L.lba_farm_match.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _lp, _lp, _ip, ctypes.c_int32, _ip]
+        if hasattr(L, "lba_partition_assign"):   # (absent from builds before it: A/B runs of older libraries)
+            L.lba_partition_assign.argtypes = [ctypes.POINTER(LbaConfig), vp, ctypes.c_int32, ctypes.c_int32, vp,
+                                               ctypes.c_int32, vp, ctypes.c_int32, vp, ctypes.c_int32, ctypes.c_int32,
+                                               _ip, _ip, _ip, _ip, _ip]
+            L.lba_kf_owner.argtypes = [vp, _ip]
+            L.lba_split_info.argtypes = [vp, _dp]
         _lib = L
     return _lib
 
@@ -108,7 +114,7 @@ def exported_symbols():
             "lba_pose_dim", "lba_set_partition", "lba_rccl_unique_id", "lba_set_partition_rccl", "lba_group_create",
             "lba_group_destroy", "lba_set_partition_group", "lba_get_cams", "lba_set_farm", "lba_set_farm_rccl",
             "lba_set_farm_group", "lba_farm_plan", "lba_farm_exchange", "lba_farm_match", "lba_solver_info", "lba_solver_flops", "lba_device_bytes",
-            "lba_setup_host_profile"]
+            "lba_setup_host_profile", "lba_partition_assign", "lba_kf_owner", "lba_split_info"]
 
 
 def setup_host_profile(win, **cfg_over):
@@ -131,6 +137,31 @@ def setup_host_profile(win, **cfg_over):
     if rc != 0:
         raise LbaError(rc, "lba_setup_host_profile failed")
     return ms, cnt
+
+
+def partition_assign(win, nranks, kf=False, **cfg_over):
+    """lba_partition_assign (host only): the landmark / motion-prior / velocity-edge split of `win` for the
+    distributed factorisation (LBA_FLAG_SUBTREE_SOLVE).  Returns (lm_rank, prior_rank, vel_rank, panels) with
+    panels = [panels of the system, panels in the top, columns of the largest subtree]; with kf=True also the
+    keyframes' ranks (-1: the top or fixed)."""
+    kw = dict(win.cfg)
+    kw.update(cfg_over)
+    cfg = make_config(**kw)
+    kfs = np.ascontiguousarray(win.kfs, dtype=KF_DTYPE)
+    obs = np.ascontiguousarray(win.obs, dtype=OBS_DTYPE)
+    pri = np.ascontiguousarray(win.priors, dtype=PRIOR_DTYPE)
+    vel = np.ascontiguousarray(win.vel_kfs, dtype=np.int32)
+    out = [np.zeros(max(n, 1), np.int32) for n in (len(win.lm), len(pri), len(vel))]
+    panels = np.zeros(3, np.int32)
+    kfr = np.zeros(max(len(kfs), 1), np.int32)
+    ip = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))   # noqa: E731
+    rc = lib().lba_partition_assign(ctypes.byref(cfg), ptr(kfs), len(kfs), len(win.lm), ptr(obs), len(obs), ptr(pri),
+                                    len(pri), ptr(vel), len(vel), nranks, ip(out[0]), ip(out[1]), ip(out[2]), ip(panels),
+                                    ip(kfr))
+    if rc != 0:
+        raise LbaError(rc, "lba_partition_assign failed")
+    res = (out[0][:len(win.lm)], out[1][:len(pri)], out[2][:len(vel)], panels)
+    return res + (kfr[:len(kfs)],) if kf else res
 
 
 def _i32(a):
@@ -274,6 +305,20 @@ class Problem:
         out = np.zeros(5, dtype=np.int32)
         self._check(lib().lba_farm_plan(self.h, kgp, kop, lgp, lop, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
         return tuple(int(v) for v in out)
+
+    def kf_owner(self):
+        """lba_kf_owner: per keyframe, the rank whose subtree holds it in the distributed factorisation (-1: all)."""
+        out = np.zeros(max(self.n_kf, 1), np.int32)
+        self._check(lib().lba_kf_owner(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return out[:self.n_kf]
+
+    def split_info(self):
+        """lba_split_info: dict(rank_flops, system_flops, allreduce_bytes, replicated_allreduce_bytes, own_panels,
+        top_panels)."""
+        out = np.zeros(6)
+        self._check(lib().lba_split_info(self.h, _d(out)))
+        return dict(zip(("rank_flops", "system_flops", "allreduce_bytes", "replicated_allreduce_bytes",
+                         "own_panels", "top_panels"), out.tolist()))
 
     def solver_info(self):
         """lba_solver_info: dict(tail, panels, tiles (of L, fill-in included), band, chain, levels, s_tiles

@@ -83,6 +83,7 @@ FLAG_HOST_LOOP = 4         # host-driven LM loop (default: queued trials decided
 FLAG_BAND_SOLVE = 8        # reduced system solved by substitution after the factorisation (large systems)
 FLAG_DENSE_SOLVE = 16      # force the L^-1-tile solve
 FLAG_TIME_SAMPLED = 32     # with FLAG_TIME_SWEEP (queued loop): events on every 10th trial only
+FLAG_SUBTREE_SOLVE = 64    # partitioned: distributed factorisation (window split by lba_partition_assign)
 
 
 def make_config(qc_diag=(0.02, 0.02, 0.02, 0.002, 0.002, 0.002), huber_mono=None, huber_stereo=None,

@@ -266,8 +266,26 @@ struct DevProblem {
     // partitioned global BA (lba_set_partition): this rank holds a subset of the landmarks; the
     // reduced system, b_p and the trial sums are summed over the ranks by the caller's all-reduce
     int part_rank, part_n;  // rank / ranks (part_n 0: not partitioned)
+    // natural row r of the reduced system: the rank whose subtree of the distributed factorisation holds it,
+    // -1 for rows every rank holds (the top of the split, every row when the solve is replicated); the
+    // damping, the padding identity and the computeScale terms of a row are added on its owner (rank 0 for -1)
+    const int* row_own;
+    // distributed factorisation (LBA_FLAG_SUBTREE_SOLVE): k_chol_flow runs twice per trial, the subtrees'
+    // tasks (cf_tasks ...) then, after the all-reduce of the top tiles (top_tiles) and of bS / b_p, the top's
+    // tasks and the back substitution (cf_tasks2 ...)
+    int cf_split;
+    const int* cf_tasks2;
+    const int* cf_task_i2;
+    const int* cf_task_t2;
+    const int* cf_pl02;
+    const int* cf_plist2;
+    const int* cf_plist_t2;
+    int cf_ntasks2;
+    const int* top_tiles;   // tiles of L in the top columns (packed into env_buf ahead of bS / b_p)
+    int n_top_tiles;
     double* red4;           // [4] trial sums of this rank, all-reduced before k_finalize reads them
-    double* env_buf;        // [n_env] bS [npad], then b_p [np] (all-reduce buffer; S is all-reduced in place)
+    double* env_buf;        // [n_env] (cf_split: the top tiles,) bS [npad], then b_p [np] (all-reduce buffer; replicated
+                            // solve: S is all-reduced in place)
     long long n_env;
     // diagnostics (LBA_PHASE_TIMING=<file>): per-workgroup clock64() stamps at phase boundaries
     unsigned long long* tdbg_lin;     // [n_tiles][16] k_linearize
@@ -303,6 +321,10 @@ void launch_update(const DevProblem& P, double lambda, int sel, int gate, int ja
 // partitioned mode: this rank's trial sums into red4; envelope of S + bS + b_p into / out of env_buf
 void launch_partials(const DevProblem& P, hipStream_t s);
 void launch_env_pack(const DevProblem& P, int unpack, int gate, hipStream_t s);
+// distributed factorisation: part 0 (the rank's subtrees and its contributions to the top) / part 1 (the top
+// and the back substitution) of k_chol_flow (same epoch for both)
+void launch_cholesky_part(const DevProblem& P, int part, unsigned epoch, hipStream_t s, hipEvent_t e0 = nullptr,
+                          hipEvent_t e1 = nullptr);
 enum { FIN_NONE = -1, FIN_HOST = 0, FIN_QUEUED = 1, FIN_QUEUED_PUBLISH = 2, FIN_INITIAL = 3 };
 void launch_finalize(const DevProblem& P, unsigned long long seq, int mode, hipStream_t s);
 // residual evaluation of a state, then (mode != FIN_NONE) the trial summary (k_finalize)

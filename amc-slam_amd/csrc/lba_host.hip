@@ -98,6 +98,11 @@ struct lba_problem {
     int nBad = 0;
     // partitioned global BA (lba_set_partition): the caller's sum all-reduce across ranks
     int part_rank = 0, part_n = 0;
+    std::vector<int> split_own;       // distributed factorisation: owner rank of each factorisation panel, -1 top
+    std::vector<int> ppos_h;          // natural panel -> factorisation position
+    int split_tasks[2] = {0, 0};      // tasks of its two launches on this rank
+    int split_panels[2] = {0, 0};     // panels of this rank's subtree / of the top
+    double flops_factor_rank = 0.0;   // factorisation FLOPs of this rank (its subtree + the top; all when replicated)
     lba_allreduce_fn red_fn = nullptr;
     void* red_user = nullptr;
     ncclComm_t comm = nullptr;        // owned when set by lba_set_partition_rccl
@@ -142,6 +147,16 @@ struct ApiError {
 void preduce(lba_problem* p, double* buf, int64_t n) {
     if (p->red_fn(buf, n, (void*)p->stream, p->red_user) != 0)
         throw ApiError{LBA_E_HIP, "partition all-reduce failed"};
+}
+
+// The factorisation plan of a panel pattern (lba_set_problem and lba_partition_assign must agree on it).
+// (diagnostics: LBA_ND_LEVELS=<n> caps the dissection depth, 0 = natural order; LBA_ND_NO_TAIL; LBA_ND_METHOD=1
+// the interval dissection only, 2 the graph dissection only)
+lba_plan::Plan plan_panels(int NP, int NPk, const std::vector<std::vector<int>>& lower) {
+    const char* lv = std::getenv("LBA_ND_LEVELS");
+    const char* nm = std::getenv("LBA_ND_METHOD");
+    return lba_plan::make_plan(NP, NPk, lower, lv ? std::atoi(lv) : 64, std::getenv("LBA_ND_NO_TAIL") == nullptr, 16,
+                               nm ? std::atoi(nm) : 0);
 }
 
 // Partitioned set-up: every rank reports the outcome of its host preprocessing in one all-reduce at a
@@ -1349,9 +1364,11 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         const int NPk = std::min(NP, 12 * n_pb_kf / CHOL_NB + (n_ext ? 0 : NP));
         std::vector<std::vector<int>> lower(NP);
         for (int P = 0; P < NP; ++P) lower[P].push_back(P);
+        std::vector<std::pair<int, int>> edge_panels;   // (this rank's edges' couplings: the split's check)
         auto couple = [&](int r, int c) {   // natural rows r, c of S
             const int P = std::max(r, c) / CHOL_NB, Q = std::min(r, c) / CHOL_NB;
             lower[P].push_back(Q);
+            edge_panels.emplace_back(P, Q);
         };
         for (int u = 0; u < n_ublocks; ++u) {
             if (!(hcnt[u] > 0 || scnt[u] > 0)) continue;
@@ -1378,16 +1395,43 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     if (occ[(size_t)P * NP + Q] != 0.0 || Q == P) lower[P].push_back(Q);
             }
         }
-        // (diagnostics: LBA_ND_LEVELS=<n> caps the dissection depth, 0 = natural order; LBA_ND_NO_TAIL;
-        // LBA_ND_METHOD=1 the interval dissection only, 2 the graph dissection only)
-        const char* lv = std::getenv("LBA_ND_LEVELS");
-        const char* nm = std::getenv("LBA_ND_METHOD");
-        const lba_plan::Plan pl = lba_plan::make_plan(NP, NPk, lower, lv ? std::atoi(lv) : 64,
-                                                      std::getenv("LBA_ND_NO_TAIL") == nullptr, 16,
-                                                      nm ? std::atoi(nm) : 0);
+        const lba_plan::Plan pl = plan_panels(NP, NPk, lower);
         p->chain = pl.chain;
         p->nd_tail = pl.tail;
         p->nd_levels = pl.levels;
+        // distributed factorisation (LBA_FLAG_SUBTREE_SOLVE, partitioned problems): the elimination tree cut into
+        // one subtree per rank plus the top (lba_plan::split_subtrees, the same on every rank); this rank's
+        // couplings must lie in its subtree and the top (lba_partition_assign gives such a landmark split)
+        const bool split = p->part_n > 0 && (p->cfg.flags & LBA_FLAG_SUBTREE_SOLVE);
+        const std::vector<int> own = split ? lba_plan::split_subtrees(pl, p->part_n) : std::vector<int>(NP, -1);
+        if (split) {   // (a second status point: a rank whose couplings leave its subtree releases its peers)
+            bool stray = false;
+            for (const auto& e : edge_panels) {
+                const int a = own[pl.ppos[e.first]], b = own[pl.ppos[e.second]];
+                if ((a >= 0 && a != p->part_rank) || (b >= 0 && b != p->part_rank)) stray = true;
+            }
+            part_status(p, stray ? 1 : 0);
+            if (stray)
+                throw ApiError{LBA_E_ARG, "partitioned problem: a landmark or edge of rank " +
+                                              std::to_string(p->part_rank) + " couples keyframes of another rank's "
+                                              "subtree (split the window with lba_partition_assign)"};
+        }
+        p->split_own = own;
+        p->ppos_h = pl.ppos;
+        {   // the factorisation work this rank does: its subtree's columns and the top (split), or all of them
+            const double b3 = (double)CHOL_NB * CHOL_NB * CHOL_NB;
+            double f = 0.0;
+            int n_own = 0, n_top = 0;
+            for (int j = 0; j < NP; ++j) {
+                if (own[j] >= 0 && own[j] != p->part_rank) continue;
+                (own[j] < 0 ? n_top : n_own)++;
+                const double m = (double)pl.colrows[j].size();
+                f += b3 / 3.0 + m * b3 + m * b3 + m * (m - 1.0) * b3;
+            }
+            p->flops_factor_rank = f;
+            p->split_panels[0] = split ? n_own : 0;
+            p->split_panels[1] = split ? n_top : NP;
+        }
         p->s_tiles = 0;
         for (int P = 0; P < NP; ++P) p->s_tiles += (int)lower[P].size();
         {   // per column with m tiles below the diagonal: potrf 32^3/3, m trsm 32^3, the m(m+1)/2 tile updates
@@ -1410,27 +1454,38 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         }
         // solve path: L^-1 tiles (the solve has no substitution chain, but L^-1 is dense below the
         // diagonal: O(n^3) work) up to CF_AUTO_BAND_NP panels, substitution tasks above (or when asked)
-        const bool band = !(p->cfg.flags & LBA_FLAG_DENSE_SOLVE) &&
-                          ((p->cfg.flags & LBA_FLAG_BAND_SOLVE) || NP > CF_AUTO_BAND_NP);
+        const bool band = split || (!(p->cfg.flags & LBA_FLAG_DENSE_SOLVE) &&
+                                    ((p->cfg.flags & LBA_FLAG_BAND_SOLVE) || NP > CF_AUTO_BAND_NP));
         D.cf_band = band ? 1 : 0;
         const int ntile = pl.ntile();
         // dataflow factorisation + solve (k_chol_flow), tasks in topological order: per column c the
         // factor tiles of its rows (the diagonal first), then (L^-1 solve) the L^-1 tiles of row c; at the
         // end one solution task per panel.  Task t: (j, i, kind) with five tile ids (task_t) and a list of
         // update / term entries (plist) with three tile ids each (plist_t).
+        // Distributed factorisation: list A (launch 0) holds this rank's subtree columns and its contributions to
+        // the top, list B (launch 1) the top columns (updated from top panels only: the subtrees' updates are summed
+        // into the top tiles between the launches) and the back substitution of the top and this rank's columns.
         {
-            std::vector<int> tasks, task_i, task_t, pl0(1, 0), plist, plist_t;
+            struct TaskList {
+                std::vector<int> tasks, task_i, task_t, pl0{0}, plist, plist_t;
+            } LA, LB;
+            TaskList* cur = &LA;
+            std::vector<int>&tasks = LA.tasks, &task_i = LA.task_i, &task_t = LA.task_t, &pl0 = LA.pl0, &plist = LA.plist,
+                            &plist_t = LA.plist_t;
             auto add_task = [&](int j, int i, int kind, int la, int t0, int t1, int t2, int t3, int t4) {
-                tasks.push_back(j | (kind << 24) | (la << 28));
-                task_i.push_back(i);
-                task_t.push_back(t0); task_t.push_back(t1); task_t.push_back(t2); task_t.push_back(t3);
-                task_t.push_back(t4);
+                cur->tasks.push_back(j | (kind << 24) | (la << 28));
+                cur->task_i.push_back(i);
+                cur->task_t.push_back(t0); cur->task_t.push_back(t1); cur->task_t.push_back(t2); cur->task_t.push_back(t3);
+                cur->task_t.push_back(t4);
             };
             auto add_entry = [&](int e, int t0, int t1, int t2) {
-                plist.push_back(e);
-                plist_t.push_back(t0); plist_t.push_back(t1); plist_t.push_back(t2);
+                cur->plist.push_back(e);
+                cur->plist_t.push_back(t0); cur->plist_t.push_back(t1); cur->plist_t.push_back(t2);
             };
-            auto end_task = [&]() { pl0.push_back((int)plist.size()); };
+            auto end_task = [&]() { cur->pl0.push_back((int)cur->plist.size()); };
+            // (split) the panels whose updates a column of owner o takes inside its launch: its own subtree's, or the
+            // top's for a top column
+            auto same_part = [&](int pp, int o) { return !split || own[pp] == o; };
             const std::vector<int>& rank = pl.rank;
             const bool no_lookahead = std::getenv("LBA_CHOL_NO_LOOKAHEAD") != nullptr;
             auto by_rank = [&](int x, int y) { return rank[x] < rank[y]; };
@@ -1452,14 +1507,18 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             // side), so they are factored and substituted concurrently
             for (int cq = 0; cq < NP; ++cq) {
                 const int c = band ? pl.uord[cq] : cq;
-                const std::vector<int> rcc = rowcols(c);
+                if (split && own[c] >= 0 && own[c] != p->part_rank) continue;   // another rank's subtree
+                cur = (split && own[c] < 0) ? &LB : &LA;
+                std::vector<int> rcc;
+                for (int pp : rowcols(c))
+                    if (same_part(pp, own[c])) rcc.push_back(pp);
                 std::vector<int> rows(1, c);
                 rows.insert(rows.end(), pl.colrows[c].begin(), pl.colrows[c].end());
                 for (int i : rows) {   // factor tiles of column c (the diagonal first)
                     // lookahead over k = c - 1 when tile (c, k) exists and k is the last update of A(c, c)
                     // in update order (then every copy of a tile sees the same update order)
                     const int k = c - 1;
-                    bool la = !no_lookahead && k >= 0 && pl.nz(c, k);
+                    bool la = !no_lookahead && k >= 0 && pl.nz(c, k) && same_part(k, own[c]);
                     for (int pp : rcc)
                         if (la && pp != k && rank[pp] > rank[k]) la = false;
                     const int tcc = pl.tile_id(c, c), tic = i == c ? -1 : pl.tile_id(i, c);
@@ -1469,7 +1528,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                         // updates of the held tiles A(c,c), A(i,c), A(k,k), A(c,k), A(i,k) from panels p < k
                         std::vector<int> ps;
                         for (int pp : rcc) if (pp < k) ps.push_back(pp);
-                        for (int pp : rowcols(k)) ps.push_back(pp);
+                        for (int pp : rowcols(k))
+                            if (same_part(pp, own[c])) ps.push_back(pp);
                         std::sort(ps.begin(), ps.end());
                         ps.erase(std::unique(ps.begin(), ps.end()), ps.end());
                         std::sort(ps.begin(), ps.end(), by_rank);
@@ -1509,11 +1569,41 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     if (nzi[c][kk]) add_entry(kk, -1, -1, -1);
                 end_task();
             }
+            if (split) {
+                // this rank's contributions to the top: per top tile (i, j) the sum over its subtree panels p of
+                // L(i,p) L(j,p)^T, per top panel i the sum of L(i,p) y_p (kinds 6, 7)
+                cur = &LA;
+                for (int j = 0; j < NP; ++j) {
+                    if (own[j] >= 0) continue;
+                    std::vector<int> rows(1, j);
+                    rows.insert(rows.end(), pl.colrows[j].begin(), pl.colrows[j].end());
+                    for (int i : rows) {
+                        std::vector<int> ps;
+                        for (int pp : rowcols(j))
+                            if (own[pp] == p->part_rank && pl.nz(i, pp)) ps.push_back(pp);
+                        if (ps.empty()) continue;
+                        std::sort(ps.begin(), ps.end(), by_rank);
+                        add_task(j, i, 6, 0, pl.tile_id(i, j), -1, -1, -1, -1);
+                        for (int pp : ps) add_entry(pp, pl.tile_id(j, pp), pl.tile_id(i, pp), -1);
+                        end_task();
+                    }
+                    std::vector<int> ks;
+                    for (int pp : rowcols(j))
+                        if (own[pp] == p->part_rank) ks.push_back(pp);
+                    if (ks.empty()) continue;
+                    std::sort(ks.begin(), ks.end(), by_rank);
+                    add_task(j, j, 7, 0, -1, -1, -1, -1, -1);
+                    for (int pp : ks) add_entry(pp, pl.tile_id(j, pp), -1, -1);
+                    end_task();
+                }
+                cur = &LB;
+            }
             if (band) {
                 // back substitution x_j = L_jj^-T (y_j - sum_i L(i,j)^T x_i) over the rows i > j of column j,
                 // columns in reverse update order, terms in the order their x_i complete
                 for (int cq = NP - 1; cq >= 0; --cq) {
                     const int j = pl.uord[cq];
+                    if (split && own[j] >= 0 && own[j] != p->part_rank) continue;
                     add_task(j, j, 5, 0, -1, -1, -1, -1, -1);
                     std::vector<int> is(pl.colrows[j]);
                     std::sort(is.begin(), is.end(), [&](int x, int y) { return rank[x] > rank[y]; });
@@ -1620,6 +1710,19 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             D.cf_task_i = dupload(p, task_i);
             D.cf_task_t = dupload(p, task_t);
             D.cf_ntasks = (int)tasks.size();
+            D.cf_split = split ? 1 : 0;
+            D.cf_ntasks2 = 0;
+            if (split) {
+                D.cf_tasks2 = dupload(p, LB.tasks);
+                D.cf_task_i2 = dupload(p, LB.task_i);
+                D.cf_task_t2 = dupload(p, LB.task_t);
+                D.cf_pl02 = dupload(p, LB.pl0);
+                D.cf_plist2 = dupload(p, LB.plist);
+                D.cf_plist_t2 = dupload(p, LB.plist_t);
+                D.cf_ntasks2 = (int)LB.tasks.size();
+                p->split_tasks[0] = D.cf_ntasks;
+                p->split_tasks[1] = D.cf_ntasks2;
+            }
             // band mode: no L^-1 tiles; ivready then flags the back-substituted blocks x_j
             const size_t niv = band ? (size_t)NP + 1 : (size_t)std::max(NP * (NP + 1) / 2, 1);
             D.cf_linv = band ? nullptr : dalloc<double>(p, (size_t)npad * npad);
@@ -1636,11 +1739,11 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             D.cf_zready = dalloc<int>(p, std::max(NP, 1));
             HIPCHK(hipMemset(D.cf_zready, 0, sizeof(int) * std::max(NP, 1)));
             D.cf_zv = band ? nullptr : dalloc<double>(p, std::max((size_t)NP * NP * CHOL_NB, (size_t)1));
-            D.cf_head = dalloc<unsigned long long>(p, 1);
+            D.cf_head = dalloc<unsigned long long>(p, 2);   // (ticket counters of the split's two launches)
             D.cf_abort = dalloc<int>(p, 1);
             HIPCHK(hipMemset(D.cf_lready, 0, sizeof(int) * std::max(ntile, 1)));
             HIPCHK(hipMemset(D.cf_dready, 0, sizeof(int) * std::max(NP, 1)));
-            HIPCHK(hipMemset(D.cf_head, 0, sizeof(unsigned long long)));
+            HIPCHK(hipMemset(D.cf_head, 0, 2 * sizeof(unsigned long long)));
             HIPCHK(hipMemset(D.cf_abort, 0, sizeof(int)));
         }
         D.cf_rowptr = dupload(p, pl.rowptr);
@@ -1657,8 +1760,21 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         D.n_ztiles = ntile;
         D.part_rank = p->part_rank;
         D.part_n = p->part_n;
+        {   // natural row -> the rank that adds its once-per-system terms (-1: rank 0)
+            std::vector<int> row_own(npad);
+            for (int r = 0; r < npad; ++r) row_own[r] = own[ppos[r / CHOL_NB]];
+            D.row_own = dupload(p, row_own);
+        }
+        std::vector<int> top_tiles;   // (split) the tiles of L in the top columns
+        if (split)
+            for (int i = 0; i < NP; ++i)
+                for (int q = pl.rowptr[i]; q < pl.rowptr[i + 1]; ++q)
+                    if (own[pl.cols[q]] < 0) top_tiles.push_back(q);
+        D.n_top_tiles = (int)top_tiles.size();
+        D.top_tiles = split ? dupload(p, top_tiles) : nullptr;
         if (p->part_n > 0) {
-            D.n_env = (long long)npad + p->np;   // bS, b_p (S is all-reduced in place)
+            // bS, b_p (replicated solve: S is all-reduced in place; split: the top tiles lead the buffer)
+            D.n_env = (long long)D.n_top_tiles * CHOL_NB * CHOL_NB + npad + p->np;
             D.env_buf = dalloc<double>(p, (size_t)D.n_env);
             D.red4 = dalloc<double>(p, 4);
         }
@@ -1779,12 +1895,30 @@ void assemble_layout(lba_problem* p, double lambda, int flags, int gate = GATE_N
     }
     if (!launch) return;   // (the fused flow assembles S itself)
     launch_assemble(p->D, lambda, flags, gate, p->stream);
-    if ((flags & ASM_SCHUR) && p->part_n > 0) {   // sum the ranks' reduced systems
+    if ((flags & ASM_SCHUR) && p->part_n > 0 && !p->D.cf_split) {   // sum the ranks' reduced systems
         launch_env_pack(p->D, 0, gate, p->stream);
         preduce(p, p->D.S, (int64_t)p->D.n_ztiles * CHOL_NB * CHOL_NB);   // the packed envelope, in place
         preduce(p, p->D.env_buf, p->D.n_env);
         launch_env_pack(p->D, 1, gate, p->stream);
     }
+}
+
+// The reduced system's solve: one k_chol_flow launch, or (distributed factorisation) the rank's subtrees and
+// its contributions to the top, the all-reduce of the top tiles with bS / b_p, then the top and the back
+// substitution (both launches under one epoch: the second reads the first one's published tiles).  e0 / e1:
+// events on the first / last dispatch.
+void launch_solve(lba_problem* p, hipEvent_t e0, hipEvent_t e1, int sel, double lambda) {
+    const DevProblem& D = p->D;
+    const unsigned epoch = ++p->cf_epoch;
+    if (!D.cf_split) {
+        launch_cholesky_solve(D, GATE_NONE, epoch, p->stream, e0, e1, sel, lambda);
+        return;
+    }
+    launch_cholesky_part(D, 0, epoch, p->stream, e0, nullptr);
+    launch_env_pack(D, 0, GATE_NONE, p->stream);
+    preduce(p, D.env_buf, D.n_env);
+    launch_env_pack(D, 1, GATE_NONE, p->stream);
+    launch_cholesky_part(D, 1, epoch, p->stream, nullptr, e1);
 }
 
 // k_finalize, after summing the ranks' trial sums when partitioned
@@ -1816,8 +1950,7 @@ void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs, bool s
     if (!D.cf_fused) launch_expand(D, p->cur, GATE_NONE, lambda, 1, p->stream);
     assemble_layout(p, lambda, ASM_SCHUR, GATE_NONE, !D.cf_fused);
     if (evs) HIPCHK(hipEventRecord(evs[2], p->stream));
-    launch_cholesky_solve(D, GATE_NONE, ++p->cf_epoch, p->stream, sweep ? p->ev[8] : nullptr, sweep ? p->ev[9] : nullptr,
-                          p->cur, lambda);
+    launch_solve(p, sweep ? p->ev[8] : nullptr, sweep ? p->ev[9] : nullptr, p->cur, lambda);
     if (evs) HIPCHK(hipEventRecord(evs[3], p->stream));
     launch_update(D, lambda, p->cur, GATE_NONE, 1, p->stream);   // (+ the trial state's pose samples)
     p->gps_fresh[nx] = true;
@@ -1921,8 +2054,7 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
                              qe ? qe[1] : nullptr);
             if (!D.cf_fused) launch_expand(D, SEL_CUR, GATE_TRIAL, LAMBDA_CTL, 1, p->stream);
             assemble_layout(p, LAMBDA_CTL, ASM_SCHUR, GATE_NONE, !D.cf_fused);
-            launch_cholesky_solve(D, GATE_NONE, ++p->cf_epoch, p->stream, qe ? qe[2] : nullptr, qe ? qe[3] : nullptr,
-                                  SEL_CUR, LAMBDA_CTL);
+            launch_solve(p, qe ? qe[2] : nullptr, qe ? qe[3] : nullptr, SEL_CUR, LAMBDA_CTL);
             // the step, the trial state and its pose samples with their Jacobian factors: the next
             // trial's linearisation reads them (no preparation launch)
             launch_update(D, LAMBDA_CTL, SEL_CUR, GATE_TRIAL, 1, p->stream);
@@ -2377,6 +2509,136 @@ int lba_solver_info(const lba_problem* p, int32_t out[8]) {
     out[5] = p->nd_levels;
     out[6] = p->s_tiles;
     out[7] = p->D.n_ztiles - p->s_tiles;
+    return LBA_OK;
+}
+
+int lba_partition_assign(const lba_config* cfg, const lba_kf* kfs, int32_t n_kf, int32_t n_lm, const lba_obs* obs,
+                         int32_t n_obs, const lba_prior* priors, int32_t n_priors, const int32_t* vel_kfs, int32_t n_vel,
+                         int32_t nranks, int32_t* lm_rank, int32_t* prior_rank, int32_t* vel_rank, int32_t* panels_out,
+                         int32_t* kf_rank) {
+    using namespace lba;
+    if (!cfg || n_kf < 0 || n_lm < 0 || n_obs < 0 || n_priors < 0 || n_vel < 0 || nranks < 1 || (n_kf && !kfs) ||
+        (n_obs && !obs) || (n_priors && !priors) || (n_vel && !vel_kfs) || (n_lm && !lm_rank) ||
+        (n_priors && !prior_rank) || (n_vel && !vel_rank))
+        return LBA_E_ARG;
+    try {
+        // pose blocks as a partitioned lba_set_problem numbers them: every non-fixed keyframe, in order
+        std::vector<int> H(n_kf, -1);
+        int n_pb = 0;
+        for (int k = 0; k < n_kf; ++k)
+            if (!kfs[k].fixed) H[k] = n_pb++;
+        auto kf_ok = [&](int k) { return k >= 0 && k < n_kf; };
+        for (int i = 0; i < n_obs; ++i)
+            if (!kf_ok(obs[i].kf_b) || (is_gp(obs[i].kind) && !kf_ok(obs[i].kf_a)) || obs[i].lm < 0 || obs[i].lm >= n_lm)
+                return LBA_E_ARG;
+        for (int i = 0; i < n_priors; ++i)
+            if (!kf_ok(priors[i].kf_a) || !kf_ok(priors[i].kf_b)) return LBA_E_ARG;
+        for (int i = 0; i < n_vel; ++i)
+            if (!kf_ok(vel_kfs[i])) return LBA_E_ARG;
+        const int np = 12 * n_pb, NP = (np + CHOL_NB - 1) / CHOL_NB;
+        // the pattern lba_set_problem plans: every pose block's diagonal, the blocks of every pair of a
+        // landmark's keyframes, of every motion prior
+        std::vector<std::vector<int>> blocks(n_lm);
+        for (int i = 0; i < n_obs; ++i) {
+            const lba_obs& o = obs[i];
+            if (H[o.kf_b] >= 0) blocks[o.lm].push_back(H[o.kf_b]);
+            if (is_gp(o.kind) && H[o.kf_a] >= 0) blocks[o.lm].push_back(H[o.kf_a]);
+        }
+        std::vector<std::vector<int>> lower(NP);
+        for (int P = 0; P < NP; ++P) lower[P].push_back(P);
+        auto couple_blocks = [&](int a, int b) {
+            const int bi = std::min(a, b), bj = std::max(a, b);
+            for (int dr : {0, 11})
+                for (int dc : {0, 11}) {
+                    const int r = 12 * bj + dr, c = 12 * bi + dc;
+                    lower[std::max(r, c) / CHOL_NB].push_back(std::min(r, c) / CHOL_NB);
+                }
+        };
+        for (auto& b : blocks) {
+            std::sort(b.begin(), b.end());
+            b.erase(std::unique(b.begin(), b.end()), b.end());
+            for (size_t x = 0; x < b.size(); ++x)
+                for (size_t y = x; y < b.size(); ++y) couple_blocks(b[x], b[y]);
+        }
+        for (int i = 0; i < n_priors; ++i) {
+            const int a = H[priors[i].kf_a], b = H[priors[i].kf_b];
+            if (a >= 0) couple_blocks(a, a);
+            if (b >= 0) couple_blocks(b, b);
+            if (a >= 0 && b >= 0) couple_blocks(a, b);
+        }
+        for (int i = 0; i < n_vel; ++i)
+            if (H[vel_kfs[i]] >= 0) couple_blocks(H[vel_kfs[i]], H[vel_kfs[i]]);
+        for (int P = 0; P < NP; ++P) {
+            std::sort(lower[P].begin(), lower[P].end());
+            lower[P].erase(std::unique(lower[P].begin(), lower[P].end()), lower[P].end());
+        }
+        const lba_plan::Plan pl = plan_panels(NP, NP, lower);
+        const std::vector<int> own = lba_plan::split_subtrees(pl, nranks);
+        // the rank of a set of pose blocks: the subtree its rows reach (one at most), else fallback
+        auto rank_of = [&](std::initializer_list<int> hs, const std::vector<int>* more, int fallback) {
+            int r = -1;
+            auto visit = [&](int h) {
+                if (h < 0) return;
+                for (int row : {12 * h, 12 * h + 11}) {
+                    const int o = own[pl.ppos[row / CHOL_NB]];
+                    if (o >= 0) r = o;
+                }
+            };
+            for (int h : hs) visit(h);
+            if (more)
+                for (int h : *more) visit(h);
+            return r >= 0 ? r : fallback;
+        };
+        for (int l = 0; l < n_lm; ++l) lm_rank[l] = rank_of({}, &blocks[l], l % nranks);
+        for (int i = 0; i < n_priors; ++i)
+            prior_rank[i] = rank_of({H[priors[i].kf_a], H[priors[i].kf_b]}, nullptr, i % nranks);
+        for (int i = 0; i < n_vel; ++i) vel_rank[i] = rank_of({H[vel_kfs[i]]}, nullptr, i % nranks);
+        if (kf_rank)
+            for (int k = 0; k < n_kf; ++k) kf_rank[k] = rank_of({H[k]}, nullptr, -1);
+        if (panels_out) {
+            std::vector<int> cnt(nranks, 0);
+            int ntop = 0;
+            for (int j = 0; j < NP; ++j) {
+                if (own[j] < 0) ++ntop;
+                else ++cnt[own[j]];
+            }
+            panels_out[0] = NP;
+            panels_out[1] = ntop;
+            panels_out[2] = *std::max_element(cnt.begin(), cnt.end());
+        }
+        return LBA_OK;
+    } catch (const std::exception&) {
+        return LBA_E_ARG;
+    }
+}
+
+int lba_split_info(const lba_problem* p, double out[6]) {
+    if (!p || !out || !p->has_problem) return LBA_E_ARG;
+    const double tile = (double)CHOL_NB * CHOL_NB * sizeof(double);
+    out[0] = p->flops_factor_rank;
+    out[1] = p->flops_factor;
+    // all-reduce bytes per trial: the split's (top tiles, bS, b_p) and the replicated solve's (every tile, bS, b_p)
+    const double vec = (double)(p->D.npad + p->np) * sizeof(double);
+    out[2] = p->part_n > 0 ? (p->D.cf_split ? p->D.n_top_tiles * tile + vec : p->D.n_ztiles * tile + vec) : 0.0;
+    out[3] = p->D.n_ztiles * tile + vec;
+    out[4] = p->split_panels[0];
+    out[5] = p->split_panels[1];
+    return LBA_OK;
+}
+
+int lba_kf_owner(const lba_problem* p, int32_t* owner) {
+    if (!p || !owner || !p->has_problem) return LBA_E_ARG;
+    const int n_kf = (int)p->kf_hidx.size() - p->n_ext;
+    for (int k = 0; k < n_kf; ++k) {
+        const int h = p->kf_hidx[k];
+        int r = -1;
+        if (h >= 0 && !p->split_own.empty())
+            for (int row : {12 * h, 12 * h + 11}) {
+                const int o = p->split_own[p->ppos_h[row / CHOL_NB]];
+                if (o >= 0) r = o;
+            }
+        owner[k] = r;
+    }
     return LBA_OK;
 }
 

@@ -678,7 +678,10 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
         // fill-in there) and a cleared factorisation status; k_assemble runs after this launch
         if (blockIdx.x == 0 && tid == 0) {
             *P.info = 0;
-            if (P.cf_head) *P.cf_head = 0;   // ticket counter of this trial's k_chol_flow
+            if (P.cf_head) {   // ticket counters of this trial's k_chol_flow (two launches when split)
+                P.cf_head[0] = 0;
+                P.cf_head[1] = 0;
+            }
         }
         if (P.cf_fused)   // the fused flow's expansion / assembly counters
             for (int z = blockIdx.x * LS_THREADS + tid; z < P.cf_ncnt; z += gridDim.x * LS_THREADS) P.cf_cnt[z] = 0;
@@ -1057,6 +1060,13 @@ __global__ __launch_bounds__(PRI_THREADS) void k_expand(DevProblem P, int sel, i
 //   from the upload and never written);  b_p = sum b partials;  bS = b_p - sum Schur rhs partials.
 // sum of x[(s0 + G q) * W + e] over the slots s0, s0 + G, ... < s1: four loads in flight, combined in
 // a fixed order
+// whether this rank adds the once-per-system terms of natural row r (damping, padding identity, computeScale):
+// its owner in the distributed factorisation, rank 0 for a row every rank holds
+__device__ __forceinline__ bool row_adds(const DevProblem& P, int r) {
+    const int o = P.row_own ? P.row_own[r] : -1;
+    return o == P.part_rank || (o < 0 && P.part_rank == 0);
+}
+
 template <int G, int W, bool SC = false>
 __device__ __forceinline__ double slot_sum(const double* __restrict__ x, int s0, int s1, int e) {
     double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
@@ -1087,9 +1097,9 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
         __syncthreads();
         if (g == 0) {
             double t = red[e] + red[144 + e] + red[288 + e] + red[432 + e];
-            if (bi == bj && e % 13 == 0 && P.part_rank == 0) t += lambda;   // damping: added once over the ranks
             const int i = e / 12, j = e % 12;
             const int r = 12 * bj + j, c = 12 * bi + i;   // element (row r, col c) of S, r >= c in blocks
+            if (bi == bj && e % 13 == 0 && row_adds(P, r)) t += lambda;   // damping: added once over the ranks
             if (flags & ASM_FULL) {                       // natural order, both triangles (dense np x np)
                 P.Sfull[(size_t)r * P.np + c] = t;
                 P.Sfull[(size_t)c * P.np + r] = t;
@@ -1102,8 +1112,9 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
                 P.S[s_elem(P, max(rh, ch), min(rh, ch))] = t;
             }
         }
-        if ((flags & ASM_SCHUR) && blockIdx.x == 0 && P.part_rank == 0)   // padding rows: identity (rank 0)
+        if ((flags & ASM_SCHUR) && blockIdx.x == 0)   // padding rows: identity (their owner)
             for (int r = P.np + tid; r < n; r += 144 * RED_GROUPS) {
+                if (!row_adds(P, r)) continue;
                 const int rh = P.rpos[r];
                 P.S[s_elem(P, rh, rh)] = 1.0;
                 P.bS[rh] = 0.0;
@@ -1407,7 +1418,8 @@ struct CholFlow {
     unsigned epoch;
     const int* task_i;   // per task: i
     const int* tasks;    // j | kind << 24 | lookahead << 28 (0: factor tile (i, j) (i = j: panel j), 1: L^-1 tile (i, j),
-                         // 2: solution block x_j, 3: forward block y_i)
+                         // 2: solution block x_j, 3: forward block y_i, 4 / 5: band forward / back substitution,
+                         // 6 / 7: a subtree's contribution to a top tile / top rhs block (distributed factorisation))
     const int* task_t;   // per task: 5 tile ids (factor tasks: (j,j), (i,j), (k,k), (j,k), (i,k); -1 none)
     const int* plist_t;  // per list entry: 3 tile ids (factor: (j,p), (i,p), (k,p); L^-1 / forward: (i,k); back: (i,j))
     const int* pl0;      // per task: first entry of its update list in plist ([pl0[t], pl0[t+1]))
@@ -1784,6 +1796,49 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
                 a.xout[a.rnat[j * CNB + tid]] = x;
             }
             if (a.tdbg && tid == 0) a.tdbg[16 * j + 15] = __builtin_amdgcn_s_memrealtime();
+            __syncthreads();
+            continue;
+        }
+        if (kind == 6) {
+            // ---------------------------------------------------- distributed factorisation, part 0: this rank's
+            // contribution to top tile (i, j), S(i,j) -= sum over its subtree panels p (the list) of L(i,p) L(j,p)^T
+            // (the ranks' S tiles of the top are all-reduced before part 1 factors them)
+            const int t_ij = a.task_t[5 * t];
+            d4 acc = z4;
+            for (int q = a.pl0[t]; q < a.pl0[t + 1]; ++q) {
+                const int tjp = a.plist_t[3 * q], tip = a.plist_t[3 * q + 1];
+                if (!cf_wait(a, a.lready + tjp, a.lready + tip, &s_ok)) return;
+                cf_load_tile(tile_at(a.Lm, tjp), CNB, Lt[0]);
+                cf_load_tile(tile_at(a.Lm, tip), CNB, Lt[1]);
+                __syncthreads();
+                acc = cf_mma_nt(Lt[1], Lt[0], rb, cb, lr, kq, acc);
+                __syncthreads();
+            }
+            double* Sq = const_cast<double*>(tile_at(a.S, t_ij));   // (read by the pack kernel after this launch)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) Sq[(rb * 16 + kq + 4 * m) * CNB + cb * 16 + lr] -= acc[m];
+            continue;
+        }
+        if (kind == 7) {
+            // ---------------------------------------------------- distributed factorisation, part 0: this rank's
+            // contribution to the top rhs block i, bS_i -= sum over its subtree panels p (the list) of L(i,p) y_p
+            const int r = tid & 31, g = tid >> 5;
+            double acc = 0.0;
+            for (int q = a.pl0[t]; q < a.pl0[t + 1]; ++q) {
+                const int kk = a.plist[q] & 0xffffff, tik = a.plist_t[3 * q];
+                if (!cf_wait(a, a.lready + tik, a.dready + kk, &s_ok)) return;
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    acc += ld_sc1(tile_at(a.Lm, tik) + r * CNB + 4 * g + u) * ld_sc1(a.yv + kk * CNB + 4 * g + u);
+            }
+            Lt[1][g][r] = acc;
+            __syncthreads();
+            if (tid < CNB) {
+                double v = 0.0;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v += Lt[1][u][tid];
+                const_cast<double*>(a.b)[i * CNB + tid] -= v;
+            }
             __syncthreads();
             continue;
         }
@@ -2320,8 +2375,8 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
             if (h >= 0)
                 for (int j = 0; j < 12; ++j) {
                     if (ok) P.x[12 * h + j] = d[j];
-                    // (partitioned: b_p is the all-reduced one, the pose part is counted by rank 0)
-                    if (P.part_rank == 0) sc += d[j] * (lambda * d[j] + P.bp[12 * h + j]);
+                    // (partitioned: b_p is the all-reduced one, a row's term is counted by its owner)
+                    if (row_adds(P, 12 * h + j)) sc += d[j] * (lambda * d[j] + P.bp[12 * h + j]);
                 }
         }
     } else if ((int)blockIdx.x < P.n_gp + nkb + P.n_stiles) {
@@ -2535,6 +2590,15 @@ __global__ __launch_bounds__(256) void k_env_pack(DevProblem P, int unpack, int 
     if (gated_off(P.ctl, gate)) return;
     const int n = P.npad;
     double* buf = P.env_buf;
+    // distributed factorisation: the top tiles of S first (after part 0 of k_chol_flow subtracted this rank's
+    // contributions from them)
+    const long long ntop = (long long)P.n_top_tiles * CHOL_NB * CHOL_NB;
+    for (long long e = blockIdx.x * 256 + threadIdx.x; e < ntop; e += 256LL * gridDim.x) {
+        double* sp = P.S + ((size_t)P.top_tiles[e >> 10] << 10) + (e & 1023);
+        if (unpack) *sp = buf[e];
+        else buf[e] = *sp;
+    }
+    buf += ntop;
     for (int e = blockIdx.x * 256 + threadIdx.x; e < n + P.np; e += 256 * gridDim.x) {
         double* sp = e < n ? P.bS + e : P.bp + (e - n);
         if (unpack) *sp = buf[e];
@@ -2660,33 +2724,49 @@ void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hi
     const int n = P.n_asm + P.n_pb;
     if (n) hipLaunchKernelGGL(k_assemble, dim3(n), dim3(144 * RED_GROUPS), 0, s, P, lambda, flags, gate);
 }
+static CholFlow make_flow(const DevProblem& P, unsigned epoch, int sel, double lambda) {
+    CholFlow a;
+    const int n = P.npad;   // multiple of CHOL_NB (identity tail)
+    a.fused = P.cf_fused;
+    a.cnt = P.cf_cnt; a.need = P.cf_need; a.asm_item = P.cf_asm_item; a.asm_tgt = P.cf_asm_tgt;
+    a.ntile = P.cf_ntile; a.sel = sel; a.lambda = lambda;
+    a.n = n; a.NP = n / CHOL_NB; a.ntasks = P.cf_ntasks; a.epoch = epoch;
+    a.tasks = P.cf_tasks; a.task_i = P.cf_task_i; a.task_t = P.cf_task_t; a.pl0 = P.cf_pl0;
+    a.plist_t = P.cf_plist_t;
+    a.plist = P.cf_plist;
+    a.S = P.S; a.Lm = P.Lm; a.LinvT = P.LinvT; a.b = P.bS; a.yv = P.yv; a.info = P.info;
+    a.lready = P.cf_lready; a.dready = P.cf_dready; a.head = P.cf_head; a.abort_flag = P.cf_abort;
+    a.tdbg = P.tdbg_chol;
+    a.tdbg2 = P.tdbg_bs;
+    a.tdbg3 = P.tdbg_cf;
+    a.Linv = P.cf_linv; a.ivready = P.cf_ivready; a.xout = P.xsol; a.rnat = P.rnat; a.fready = P.cf_fready;
+    a.zready = P.cf_zready; a.zv = P.cf_zv;
+    a.xpos = P.cf_xpos; a.xready = P.cf_ivready;
+    return a;
+}
+static void launch_flow(const CholFlow& a, const DevProblem& P, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    const dim3 g(min(a.ntasks, 512));
+    if (g.x == 0) return;
+    if (e0 || e1)
+        hipExtLaunchKernelGGL(k_chol_flow, g, dim3(256), 0, s, e0, e1, 0, a, P);
+    else
+        hipLaunchKernelGGL(k_chol_flow, g, dim3(256), 0, s, a, P);
+}
 void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
                            int sel, double lambda) {
-    const int n = P.npad;   // multiple of CHOL_NB (identity tail)
-    if (n == 0) return;
-    {
-        CholFlow a;
-        a.fused = P.cf_fused;
-        a.cnt = P.cf_cnt; a.need = P.cf_need; a.asm_item = P.cf_asm_item; a.asm_tgt = P.cf_asm_tgt;
-        a.ntile = P.cf_ntile; a.sel = sel; a.lambda = lambda;
-        a.n = n; a.NP = n / CHOL_NB; a.ntasks = P.cf_ntasks; a.epoch = epoch;
-        a.tasks = P.cf_tasks; a.task_i = P.cf_task_i; a.task_t = P.cf_task_t; a.pl0 = P.cf_pl0;
-        a.plist_t = P.cf_plist_t;
-        a.plist = P.cf_plist;
-        a.S = P.S; a.Lm = P.Lm; a.LinvT = P.LinvT; a.b = P.bS; a.yv = P.yv; a.info = P.info;
-        a.lready = P.cf_lready; a.dready = P.cf_dready; a.head = P.cf_head; a.abort_flag = P.cf_abort;
-        a.tdbg = P.tdbg_chol;
-        a.tdbg2 = P.tdbg_bs;
-        a.tdbg3 = P.tdbg_cf;
-        a.Linv = P.cf_linv; a.ivready = P.cf_ivready; a.xout = P.xsol; a.rnat = P.rnat; a.fready = P.cf_fready;
-        a.zready = P.cf_zready; a.zv = P.cf_zv;
-        a.xpos = P.cf_xpos; a.xready = P.cf_ivready;
-        if (e0)
-            hipExtLaunchKernelGGL(k_chol_flow, dim3(min(P.cf_ntasks, 512)), dim3(256), 0, s, e0, e1, 0, a, P);
-        else
-            hipLaunchKernelGGL(k_chol_flow, dim3(min(P.cf_ntasks, 512)), dim3(256), 0, s, a, P);
-        return;
+    (void)gate;
+    if (P.npad == 0) return;
+    launch_flow(make_flow(P, epoch, sel, lambda), P, s, e0, e1);
+}
+void launch_cholesky_part(const DevProblem& P, int part, unsigned epoch, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    if (P.npad == 0) return;
+    CholFlow a = make_flow(P, epoch, SEL_CUR, LAMBDA_CTL);
+    if (part == 1) {
+        a.tasks = P.cf_tasks2; a.task_i = P.cf_task_i2; a.task_t = P.cf_task_t2; a.pl0 = P.cf_pl02;
+        a.plist = P.cf_plist2; a.plist_t = P.cf_plist_t2; a.ntasks = P.cf_ntasks2;
+        a.head = P.cf_head + 1;
     }
+    launch_flow(a, P, s, e0, e1);
 }
 void launch_update(const DevProblem& P, double lambda, int sel, int gate, int jac, hipStream_t s) {
     hipLaunchKernelGGL(k_update, dim3(P.n_upd_blocks), dim3(UPD_THREADS), 0, s, P, lambda, sel, gate, jac);

@@ -368,4 +368,84 @@ inline Plan make_plan(int NP, int NPk, const std::vector<std::vector<int>>& lowe
     return best;
 }
 
+// The distributed factorisation of a partitioned problem (global BA over N GPUs): the
+// elimination tree of a plan cut into nranks disjoint subtrees of about equal work, each factored by one rank
+// alone, and the top columns above them (the separators the subtrees meet in), factored by every rank once the
+// subtrees' contributions are summed.  Columns of different subtrees never share a tile (coupled columns are
+// ancestor and descendant), so a landmark's columns lie in one subtree plus the top.  Greedy: from the roots,
+// repeatedly split the heaviest subtree of the frontier (its root column moves to the top), and keep the
+// frontier with the lowest makespan max(rank load) + top work under a largest-first assignment of its
+// subtrees to the ranks.  Returns own[j] (rank of column j's subtree, -1 for the top); deterministic, so
+// every rank derives the same split.
+inline std::vector<int> split_subtrees(const Plan& pl, int nranks) {
+    const int NP = pl.NP;
+    std::vector<int> own(NP, -1);
+    if (nranks <= 1 || NP == 0) {
+        std::fill(own.begin(), own.end(), nranks == 1 ? 0 : -1);
+        return own;
+    }
+    std::vector<int> parent(NP, -1);
+    std::vector<std::vector<int>> kids(NP);
+    std::vector<double> w(NP), sub(NP);
+    for (int j = 0; j < NP; ++j) {
+        const double m = (double)pl.colrows[j].size();
+        w[j] = 1.0 / 3.0 + 2.0 * m + m * (m - 1.0);   // column j's factor work in 32^3 units
+        if (!pl.colrows[j].empty()) {
+            parent[j] = pl.colrows[j].front();
+            kids[parent[j]].push_back(j);
+        }
+    }
+    for (int j = 0; j < NP; ++j) sub[j] = w[j];
+    for (int j = 0; j < NP; ++j)   // (children precede parents: parent > child)
+        if (parent[j] >= 0) sub[parent[j]] += sub[j];
+    std::vector<int> front;
+    for (int j = 0; j < NP; ++j)
+        if (parent[j] < 0) front.push_back(j);
+    double top = 0.0;
+    // largest-first assignment of the frontier subtrees to the ranks: makespan and the owners
+    auto assign = [&](const std::vector<int>& fr, std::vector<int>* who) {
+        std::vector<int> ord(fr);
+        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return sub[a] > sub[b] || (sub[a] == sub[b] && a < b); });
+        std::vector<double> load(nranks, 0.0);
+        if (who) who->assign(NP, -1);
+        for (int r : ord) {
+            const int k = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+            load[k] += sub[r];
+            if (who) (*who)[r] = k;
+        }
+        return *std::max_element(load.begin(), load.end());
+    };
+    // walk the splits (heaviest frontier subtree first) down to the leaves and keep the cheapest state
+    double best = assign(front, nullptr) + top;
+    std::vector<int> best_front = front;
+    for (int it = 0; it < NP && !front.empty(); ++it) {
+        int h = -1;
+        for (int r : front)
+            if (h < 0 || sub[r] > sub[h] || (sub[r] == sub[h] && r < h)) h = r;
+        std::vector<int> fr2;
+        for (int r : front)
+            if (r != h) fr2.push_back(r);
+        for (int c : kids[h]) fr2.push_back(c);
+        front.swap(fr2);
+        top += w[h];
+        if (front.empty()) break;
+        const double cost = assign(front, nullptr) + top;
+        if (cost < best) {
+            best = cost;
+            best_front = front;
+        }
+    }
+    front = best_front;
+    std::vector<int> who;
+    assign(front, &who);
+    // every column below a frontier root belongs to that root's rank; the rest is the top
+    std::vector<char> is_root(NP, 0);
+    for (int r : front) is_root[r] = 1;
+    for (int j = NP - 1; j >= 0; --j) {   // parents before children
+        if (is_root[j]) own[j] = who[j];
+        else if (parent[j] >= 0 && own[parent[j]] >= 0) own[j] = own[parent[j]];
+    }
+    return own;
+}
+
 }  // namespace lba_plan

@@ -60,6 +60,10 @@ extern "C" {
 #define LBA_FLAG_DENSE_SOLVE 16   /* force the L^-1-tile solve (pose systems up to 6144 only) */
 #define LBA_FLAG_TIME_SAMPLED 32  /* with LBA_FLAG_TIME_SWEEP in the queued loop: events on one trial in
                                      ten (the 6th of each ten of a batch), so their idle time costs ~1/10 */
+#define LBA_FLAG_SUBTREE_SOLVE 64 /* partitioned problems: distributed factorisation of the reduced camera
+                                     system (each rank factors its subtree of the nested dissection, the ranks
+                                     sum their contributions to the top separators, every rank factors the
+                                     top); the window must be split by lba_partition_assign */
 
 /* LM termination codes in lba_stats.result (OptimizationAlgorithm::SolverResult) */
 #define LBA_RESULT_OK         0
@@ -199,6 +203,27 @@ typedef struct lba_group lba_group;     /* in-process all-reduce across problems
 int  lba_group_create(lba_group** out, int32_t nranks);
 void lba_group_destroy(lba_group* g);
 int  lba_set_partition_group(lba_problem* p, lba_group* g, int32_t rank);
+/* The landmark / edge split of a window for LBA_FLAG_SUBTREE_SOLVE (host only, no device): the reduced camera
+ * system's nested dissection (the plan lba_set_problem makes) is cut into nranks subtrees and the top; each
+ * landmark goes to the rank whose subtree holds its keyframes (a landmark that only sees top keyframes, or
+ * fixed ones: rank = index mod nranks), each motion prior / velocity edge likewise.  Every rank then holds all
+ * keyframes, its landmarks with all their observations, and its edges (the replacement of the l mod N split of
+ * lba_set_partition, BlockSolver's Schur complement per partition, block_solver.hpp:381-445).  Outputs
+ * lm_rank[n_lm], prior_rank[n_priors], vel_rank[n_vel]; panels_out (may be NULL) [3]: panels of the system,
+ * panels in the top, columns of the largest subtree; kf_rank (may be NULL) [n_kf]: the rank whose subtree holds
+ * the keyframe (-1: the top, or fixed). */
+int lba_partition_assign(const lba_config* cfg, const lba_kf* kfs, int32_t n_kf, int32_t n_lm, const lba_obs* obs,
+                         int32_t n_obs, const lba_prior* priors, int32_t n_priors, const int32_t* vel_kfs, int32_t n_vel,
+                         int32_t nranks, int32_t* lm_rank, int32_t* prior_rank, int32_t* vel_rank, int32_t* panels_out,
+                         int32_t* kf_rank);
+/* LBA_FLAG_SUBTREE_SOLVE: per keyframe slot, the rank whose subtree holds it (-1: the top, every rank holds its
+ * state; a keyframe of another rank's subtree keeps its old state on this rank: gather it from its owner). */
+int  lba_kf_owner(const lba_problem* p, int32_t* owner);
+/* The rank's share of the factorisation: out[0] its factorisation FLOPs (its subtree's columns + the top; the
+ * whole system when the solve is replicated), out[1] the whole system's, out[2] bytes it all-reduces per LM trial
+ * for the solve (split: the top tiles + bS + b_p; replicated: every tile + bS + b_p; 0 unpartitioned), out[3]
+ * the replicated solve's bytes for comparison, out[4] panels of its subtree, out[5] panels of the top. */
+int  lba_split_info(const lba_problem* p, double out[6]);
 
 /* ---- window farm (BASELINE config 3): one LocalGPBA window per GPU (rank), windows cut
  * from one trajectory, so neighbours share keyframes and map points.  The reference runs one local BA at
