@@ -189,6 +189,8 @@ def main():
     ap.add_argument("--sweep-events", choices=("every", "sampled", "off"), default="sampled",
                     help="HIP events around k_lin_schur / k_chol_flow dispatches in the timed run: every trial, "
                          "every 10th trial (default: the events idle the device ~5 us each) or none")
+    ap.add_argument("--gba-solve", choices=("split", "replicated"), default="split",
+                    help="config 4 over N ranks: distributed factorisation (default) or the replicated solve")
     ap.add_argument("--solve", choices=("auto", "band", "dense"), default="auto",
                     help="reduced-system solve: L^-1 tiles (dense) or substitution (band); auto picks by size")
     args = ap.parse_args()
@@ -206,8 +208,10 @@ def main():
     from amc_lba import farm
     from amc_lba.synth import make_config_window
 
-    # global BA (config 4): one problem partitioned over the ranks (landmarks split, reduced system
-    # all-reduced over RCCL every LM trial); otherwise window farming (config 3) or a single window
+    # global BA (config 4): one problem partitioned over the ranks (--gba-solve split: the distributed
+    # factorisation, each rank factors its subtree of the nested dissection and the top separators' tiles are
+    # all-reduced over RCCL every LM trial; replicated: landmarks l % N, the whole reduced system all-reduced and
+    # factored by every rank); otherwise window farming (config 3) or a single window
     gba = args.config.startswith("cfg4")
     solve_flag = {"auto": 0, "band": amc_lba.abi.FLAG_BAND_SOLVE, "dense": amc_lba.abi.FLAG_DENSE_SOLVE}[args.solve]
     # the timed run records the dispatch timestamps of every k_lin_schur and k_chol_flow launch
@@ -228,7 +232,10 @@ def main():
     if gba:
         from amc_lba.gba import partition_window
         full = make_config_window(args.config, seed=args.seed)
-        win, _ = partition_window(full, rank, world)
+        split = world > 1 and args.gba_solve == "split"
+        win, _ = partition_window(full, rank, world, amc_lba.partition_assign(full, world) if split else None)
+        if split:
+            flags |= amc_lba.abi.FLAG_SUBTREE_SOLVE
         rid = None
         if world > 1:
             idt = torch.zeros(128, dtype=torch.uint8, device=torch.device("cuda", local))
@@ -355,7 +362,9 @@ def main():
             "config": {"workload": workload, "n_kf": int(len(W.kfs)), "n_opt_kf": int((W.kfs["fixed"] == 0).sum()),
                        "n_lm": int(len(W.lm)), "n_obs": int(len(W.obs)), "n_pairs": int(W.n_pairs),
                        "n_cam": int(len(W.cams)), "window_iters": args.window_iters, "solve": args.solve,
-                       "parallelism": (f"landmark partition x{world} (RCCL all-reduce per trial)" if gba else
+                       "parallelism": ((f"distributed factorisation x{world} (subtree per rank, RCCL all-reduce of the "
+                                        "top per trial)" if args.gba_solve == "split" else
+                                        f"landmark partition x{world} (RCCL all-reduce per trial)") if gba else
                                        f"window farm x{world}") if world > 1 else "single window",
                        "setup_s": t_setup},
             # the sweep's algorithmic intensity (F / B ~ 44 FLOP/B at config 1) is above the fp64 ridge point
