@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <sched.h>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -292,7 +293,9 @@ T* dupload(lba_problem* p, const std::vector<T>& v) {
     return d;
 }
 
-// f(i) for i in [0, n) on up to 8 host threads (LBA_SETUP_THREADS overrides; 1: serial).  Callers split work
+// f(i) for i in [0, n) on up to 8 host threads, at most the CPUs this process may run on (LBA_SETUP_THREADS
+// overrides; 1: serial; 16 threads measured no faster on a 16-CPU share of the GPU box, the serial parts of the
+// set-up dominate, profiles/r3ai_setup_threads.txt).  Callers split work
 // into a fixed number of pieces, so the results never depend on the thread count.  The workers persist
 // (a set-up makes several parallel passes; spawning threads per pass cost ~0.1 ms each); a pass that finds
 // the pool busy (another problem setting up on another thread) runs on its caller's thread alone.
@@ -331,7 +334,10 @@ class SetupPool {
     SetupPool() {
         const char* e = std::getenv("LBA_SETUP_THREADS");
         const int v = e ? std::atoi(e) : 0;
-        const int nt = v > 0 ? v : (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+        int avail = (int)std::thread::hardware_concurrency();
+        cpu_set_t cs;
+        if (sched_getaffinity(0, sizeof(cs), &cs) == 0) avail = std::min(avail > 0 ? avail : CPU_COUNT(&cs), CPU_COUNT(&cs));
+        const int nt = v > 0 ? v : std::max(1, std::min(8, avail));
         for (int t = 1; t < nt; ++t)
             workers_.emplace_back([this] {
                 unsigned long long seen = 0;
@@ -1563,6 +1569,17 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     for (int kk : rcc)
                         if (kk >= j && nzi[kk][j]) add_entry(kk, pl.tile_id(c, kk), -1, -1);
                     end_task();
+                }
+                if (c == NP - 1) {
+                    // the last panel: y_c = L_cc^-1 (b_c - sum_k L(c,k) y_k) as a substitution task (kind 4): every
+                    // y_k is out well before L_cc is, so y_c follows L_cc^-T at once instead of waiting for the
+                    // L^-1 tiles of the last row and their shares
+                    add_task(c, c, 4, 0, pl.tile_id(c, c), -1, -1, -1, -1);
+                    std::vector<int> ks(rcc);
+                    std::sort(ks.begin(), ks.end(), by_rank);
+                    for (int kk : ks) add_entry(kk, pl.tile_id(c, kk), -1, -1);
+                    end_task();
+                    continue;
                 }
                 add_task(c, c, 3, 0, -1, -1, -1, -1, -1);   // y_c: the nonzero tiles of row c of L^-1
                 for (int kk = 0; kk <= c; ++kk)

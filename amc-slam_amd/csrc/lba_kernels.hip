@@ -630,8 +630,8 @@ __device__ void edge_item(const DevProblem& P, int sel, int idx, const int tid, 
 //      sum J^T W J = N^T M N per sample, formed by k_expand)
 //   3. per (pair, 6-row half): Hpl(k, lm) = sum over its (observation, side) entries of N_side^T G,
 //      G = rho' w sum_rows J1^T Jp -> HBM (k_update's back-substitution) and registers
-//   4. per landmark: Hll / bl -> HBM; eliminating: Dinv = (Hll + lambda I)^-1 (Eigen's adjugate inverse,
-//      block_solver.hpp:389) -> HBM, and Hll + lambda I = L D L^T -> LDS
+//   4. per landmark: Hll / bl -> HBM; eliminating: Hll + lambda I = L D L^T -> LDS (k_update forms
+//      Dinv = (Hll + lambda I)^-1, Eigen's adjugate inverse, block_solver.hpp:389, from Hll)
 //   (eliminating regular tiles only; from here on the LDS of the rows holds Hpl)
 //   5. W = Hpl L^-T in place
 //   6. S partials: per Schur entry (KF pair k1 <= k2 of the tile) C = sum_m W(m,k1) D_m^-1 W(m,k2)^T =
@@ -769,8 +769,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
     LBA_TMARK(P.tdbg_lin, 2);
 
     // ---- phase 4: Hll / bl per landmark (threads from the top; before phase 3, so no
-    //      register state of phase 3 lives across it); eliminating:
-    //      Dinv = (Hll + lambda I)^-1 (kept for k_update) and Hll + lambda I = L D L^T
+    //      register state of phase 3 lives across it); eliminating: Hll + lambda I = L D L^T
     {
         const int t = LS_THREADS - 1 - tid;
         if (t < nlm) {
@@ -799,10 +798,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
             if (elim) {
                 const double lambda = damping(P, lambda_arg);
                 H[0] += lambda; H[4] += lambda; H[8] += lambda;   // setLambda on Hll (block_solver.hpp:580-587)
-                double Di[9];
-                inv3(H, Di);
-#pragma unroll
-                for (int q = 0; q < 9; ++q) P.Dinv[(size_t)l * 9 + q] = Di[q];
+                // (Dinv = (Hll + lambda I)^-1 for the back-substitution is formed by k_update from Hll: not stored)
                 // H = L D L^T (unit lower L)
                 const double d0 = H[0], l10 = H[3] / d0, l20 = H[6] / d0;
                 const double d1 = H[4] - l10 * l10 * d0;
@@ -2285,7 +2281,12 @@ __device__ double bs_tile(const DevProblem& P, int tile, int si, bool ok, double
                 const double* v = vsh[o - ob0];
                 c[0] -= v[0]; c[1] -= v[1]; c[2] -= v[2];
             }
-            const double* D = P.Dinv + (size_t)l * 9;
+            // Dinv = (Hll + lambda I)^-1 (Eigen's adjugate inverse, block_solver.hpp:389), the sweep's Hll and damping
+            double H[9], D[9];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) H[q] = P.Hll[(size_t)l * 9 + q];
+            H[0] += lambda; H[4] += lambda; H[8] += lambda;
+            inv3(H, D);
             for (int a = 0; a < 3; ++a) {
                 xl[a] = D[a * 3] * c[0] + D[a * 3 + 1] * c[1] + D[a * 3 + 2] * c[2];
                 xd[a] = xl[a];
