@@ -2164,21 +2164,37 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
 // ------------------------------------------------------------------------------------------------
 constexpr int UPD_THREADS = 64;     // one landmark (or KF) per thread: many small blocks for latency hiding
 
-// Trial state of KF k (pose block h, -1 if fixed): Twb <- Twb exp(dxi), v += dv (G2oTypes.cc:41-46);
-// d = the solved step, or the stale x when the factorisation failed (BlockSolver leaves x untouched,
-// g2o then applies and pops it).  One (non-inlined) function body for every caller, so every copy of
-// a state is bitwise identical.
-__device__ __attribute__((noinline)) void kf_trial_state(const DevProblem& P, const double* kc, int h, bool ok,
-                                                         double* d, double* kn) {
-    if (h >= 0) {
-        for (int j = 0; j < 12; ++j) d[j] = ok ? P.xsol[12 * h + j] : P.x[12 * h + j];
-        const SE3 T = se3_mul(load_se3(kc), se3_exp(d));
+// Trial state of a KF (state kc): Twb <- Twb exp(dxi), v += dv (G2oTypes.cc:41-46) with the step dx (12) =
+// the solved step, or the stale x when the factorisation failed (BlockSolver leaves x untouched, g2o then
+// applies and pops it); dx null: a fixed KF.  One (non-inlined) function body for every caller, so every copy
+// of a state is bitwise identical.
+__device__ __forceinline__ const double* kf_step(const DevProblem& P, int h, bool ok) {
+    return h < 0 ? nullptr : (ok ? P.xsol : P.x) + 12 * (size_t)h;
+}
+// (Every input is loaded into registers before the first store: the outputs may alias nothing, but through
+// generic pointers the compiler cannot know that, and interleaved loads and stores serialise into one memory
+// round trip per element.)
+__device__ __attribute__((noinline)) void kf_trial_state(const double* __restrict__ kc, const double* __restrict__ dx,
+                                                         double* __restrict__ d, double* __restrict__ kn) {
+    double c[KF_STRIDE];
+#pragma unroll
+    for (int j = 0; j < KF_STRIDE; ++j) c[j] = kc[j];
+    if (dx) {
+        double dl[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) dl[j] = dx[j];
+        const SE3 T = se3_mul(load_se3(c), se3_exp(dl));
+#pragma unroll
+        for (int j = 0; j < 12; ++j) d[j] = dl[j];
         kn[0] = T.q.x; kn[1] = T.q.y; kn[2] = T.q.z; kn[3] = T.q.w;
         kn[4] = T.t[0]; kn[5] = T.t[1]; kn[6] = T.t[2];
-        for (int j = 0; j < 6; ++j) kn[7 + j] = kc[7 + j] + d[6 + j];
-        for (int j = 13; j < KF_STRIDE; ++j) kn[j] = kc[j];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) kn[7 + j] = c[7 + j] + dl[6 + j];
+#pragma unroll
+        for (int j = 13; j < KF_STRIDE; ++j) kn[j] = c[j];
     } else {
-        for (int j = 0; j < KF_STRIDE; ++j) kn[j] = kc[j];
+#pragma unroll
+        for (int j = 0; j < KF_STRIDE; ++j) kn[j] = c[j];
     }
 }
 
@@ -2223,13 +2239,35 @@ __device__ __forceinline__ void bs_obs(const DevProblem& P, const double* gps, c
 // The landmarks of regular tile `tile` (one UPD_THREADS workgroup): dx_l = Dinv_l (b_l - sum_{o of l} G_o^T t_s(o))
 // (block_solver.hpp:461-482), oplus, computeScale partial.  Returns this thread's scale term.
 constexpr int UPD_TILE_OBS_PER_THREAD = (TILE_OBS + 63) / 64;
+constexpr int UPD_TILE_TASKS_PER_THREAD = (TILE_SMP * 6 + UPD_THREADS - 1) / UPD_THREADS;
 constexpr int BS_SHM = TILE_SMP * 6 + TILE_OBS * 3;
-__device__ double bs_tile(const DevProblem& P, int tile, int si, bool ok, double lambda, double* lo, double* shm) {
+// (Latency-bound: every load a thread needs is issued in a few batches, each stage's index loads for all of its
+// tasks before their data loads, and the landmark's own inputs at entry, so a tile costs a handful of memory
+// round trips instead of one chain per task.)
+__device__ double bs_tile(const DevProblem& P, int tile, int si, bool ok, double lambda, double* lo, double* shm,
+                          unsigned long long* stamp) {
     double(*tsh)[6] = reinterpret_cast<double(*)[6]>(shm);                  // t_s per tile sample
     double(*vsh)[3] = reinterpret_cast<double(*)[3]>(shm + TILE_SMP * 6);   // G_o^T t per observation
     const int tid = threadIdx.x;
     const int lm0 = P.tile_lm0[tile], nlm = P.tile_nlm[tile];
     const double* __restrict__ lst = P.lbuf[si];
+    // this thread's landmark: b_l, Hll, its state and the step of a failed factorisation, loaded up front
+    const bool has_l = tid < nlm;
+    const int l = lm0 + (has_l ? tid : 0);
+    double blv[3], Hv[9], lv[3], xold[3];
+    int lob0 = 0, lob1 = 0;
+    if (has_l) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            blv[a] = P.bl[3 * (size_t)l + a];
+            lv[a] = lst[3 * (size_t)l + a];
+            xold[a] = P.x[P.np + 3 * (size_t)l + a];
+        }
+#pragma unroll
+        for (int q = 0; q < 9; ++q) Hv[q] = P.Hll[(size_t)l * 9 + q];
+        lob0 = P.lm_obs0[l];
+        lob1 = P.lm_obs0[l + 1];
+    }
     if (ok) {
         const int ts0 = P.tile_smp0[tile], nts = P.tile_nsmp[tile];
         const int obs0 = P.tile_obs0[tile], nobs = P.tile_nobs[tile];
@@ -2237,23 +2275,42 @@ __device__ double bs_tile(const DevProblem& P, int tile, int si, bool ok, double
         const double* __restrict__ gps = P.gpsb[si];
         const double* __restrict__ camd = P.camdb[si];
         // t_s(r) = sum_c N_s(r, c) [x_a; x_b](c) (+ the extrinsic factor on x_e): N column c at 12 + 6 c
-        for (int task = tid; task < nts * 6; task += UPD_THREADS) {
-            const int ts = task / 6, r = task - 6 * ts;
-            const int sm = P.tsm_smp[ts0 + ts];
-            const int* bk = P.smp_blk + 4 * (size_t)sm;
-            const double* N = gps + (size_t)sm * GPS_STRIDE + 12 + r;
-            double acc = 0.0;
+        int sm[UPD_TILE_TASKS_PER_THREAD];
+#pragma unroll
+        for (int q = 0; q < UPD_TILE_TASKS_PER_THREAD; ++q) {
+            const int task = tid + UPD_THREADS * q;
+            sm[q] = task < nts * 6 ? P.tsm_smp[ts0 + task / 6] : -1;
+        }
+        int4 bk[UPD_TILE_TASKS_PER_THREAD];
+#pragma unroll
+        for (int q = 0; q < UPD_TILE_TASKS_PER_THREAD; ++q)
+            bk[q] = sm[q] >= 0 ? *reinterpret_cast<const int4*>(P.smp_blk + 4 * (size_t)sm[q]) : make_int4(-1, -1, -1, -1);
+        double acc[UPD_TILE_TASKS_PER_THREAD];
+#pragma unroll
+        for (int q = 0; q < UPD_TILE_TASKS_PER_THREAD; ++q) {
+            const int task = tid + UPD_THREADS * q, r = task % 6;
+            acc[q] = 0.0;
+            if (sm[q] < 0) continue;
+            const double* N = gps + (size_t)sm[q] * GPS_STRIDE + 12 + r;
+            const int hs[3] = {bk[q].x, bk[q].y, bk[q].z};
+#pragma unroll
             for (int side = 0; side < 3; ++side) {
-                const int h = bk[side];
+                const int h = hs[side];
                 if (h < 0) continue;
                 const double* x = P.xsol + 12 * (size_t)h;
-                const double* Nc = side < 2 ? N + 6 * 12 * side : camd + (size_t)bk[3] * CAMD_STRIDE + 16 + r;
+                const double* Nc = side < 2 ? N + 6 * 12 * side : camd + (size_t)bk[q].w * CAMD_STRIDE + 16 + r;
 #pragma unroll
-                for (int c = 0; c < 12; ++c) acc += Nc[6 * c] * x[c];
+                for (int c = 0; c < 12; ++c) acc[q] += Nc[6 * c] * x[c];
             }
-            tsh[ts][r] = acc;
         }
+#pragma unroll
+        for (int q = 0; q < UPD_TILE_TASKS_PER_THREAD; ++q)
+            if (sm[q] >= 0) {
+                const int task = tid + UPD_THREADS * q;
+                tsh[task / 6][task % 6] = acc[q];
+            }
         __syncthreads();
+        if (stamp) stamp[0] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
         for (int k = 0; k < UPD_TILE_OBS_PER_THREAD; ++k) {
             const int ol = tid + UPD_THREADS * k;
@@ -2268,35 +2325,33 @@ __device__ double bs_tile(const DevProblem& P, int tile, int si, bool ok, double
             }
         }
         __syncthreads();
+        if (stamp) stamp[1] = __builtin_amdgcn_s_memrealtime();
     }
     double sc = 0.0;
-    if (tid < nlm) {
-        const int l = lm0 + tid;
+    if (has_l) {
         double xl[3];
         double* xd = P.x + P.np + 3 * (size_t)l;
         if (ok) {
-            double c[3] = {P.bl[3 * (size_t)l], P.bl[3 * (size_t)l + 1], P.bl[3 * (size_t)l + 2]};
+            double c[3] = {blv[0], blv[1], blv[2]};
             const int ob0 = P.tile_obs0[tile];
-            for (int o = P.lm_obs0[l]; o < P.lm_obs0[l + 1]; ++o) {
+            for (int o = lob0; o < lob1; ++o) {
                 const double* v = vsh[o - ob0];
                 c[0] -= v[0]; c[1] -= v[1]; c[2] -= v[2];
             }
             // Dinv = (Hll + lambda I)^-1 (Eigen's adjugate inverse, block_solver.hpp:389), the sweep's Hll and damping
-            double H[9], D[9];
-#pragma unroll
-            for (int q = 0; q < 9; ++q) H[q] = P.Hll[(size_t)l * 9 + q];
-            H[0] += lambda; H[4] += lambda; H[8] += lambda;
-            inv3(H, D);
+            double D[9];
+            Hv[0] += lambda; Hv[4] += lambda; Hv[8] += lambda;
+            inv3(Hv, D);
             for (int a = 0; a < 3; ++a) {
                 xl[a] = D[a * 3] * c[0] + D[a * 3 + 1] * c[1] + D[a * 3 + 2] * c[2];
                 xd[a] = xl[a];
             }
         } else {
-            xl[0] = xd[0]; xl[1] = xd[1]; xl[2] = xd[2];
+            xl[0] = xold[0]; xl[1] = xold[1]; xl[2] = xold[2];
         }
         for (int a = 0; a < 3; ++a) {
-            lo[3 * (size_t)l + a] = lst[3 * (size_t)l + a] + xl[a];
-            sc += xl[a] * (lambda * xl[a] + P.bl[3 * (size_t)l + a]);
+            lo[3 * (size_t)l + a] = lv[a] + xl[a];
+            sc += xl[a] * (lambda * xl[a] + blv[a]);
         }
     }
     return sc;
@@ -2314,7 +2369,7 @@ __device__ double bs_tile(const DevProblem& P, int tile, int si, bool ok, double
 // gp_pair_prep's buffers), a KF block (kf_trial_state's output slots: the function stays one compiled body
 // for both callers, their trial states must agree bitwise, without its output arrays living in scratch), a
 // tile (bs_tile).  (One allocation keeps k_update at 8 workgroups per CU, so every tile is resident at once.)
-constexpr int UPD_GP_SHM = 2 * 12 + 2 * KF_STRIDE + PREP_SHM;
+constexpr int UPD_GP_SHM = 2 * 12 + 2 * KF_STRIDE + 2 * (KF_STRIDE + 12) + PREP_SHM;
 constexpr int UPD_KF_SHM = UPD_THREADS * (12 + KF_STRIDE);
 constexpr int UPD_SHM = UPD_GP_SHM > UPD_KF_SHM ? (UPD_GP_SHM > BS_SHM ? UPD_GP_SHM : BS_SHM)
                                                 : (UPD_KF_SHM > BS_SHM ? UPD_KF_SHM : BS_SHM);
@@ -2340,14 +2395,27 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
         const int i = blockIdx.x;
         double* kdl = ushm;                    // [2][12]
         double* kab = ushm + 2 * 12;           // [2][KF_STRIDE]
+        double* kin = ushm + 2 * 12 + 2 * KF_STRIDE;   // [2][KF_STRIDE + 12]: the two KFs' states and steps,
+                                                       // staged by 56 lanes in one round of loads
+        {
+            const int t = threadIdx.x, side = t >= KF_STRIDE + 12 ? 1 : 0, e = t - side * (KF_STRIDE + 12);
+            if (t < 2 * (KF_STRIDE + 12)) {
+                const int k = side ? P.gp_kfb[i] : P.gp_kfa[i];
+                const double* dx = kf_step(P, P.kf_hidx[k], ok);
+                if (e < KF_STRIDE) kin[t] = kst[(size_t)k * KF_STRIDE + e];
+                else if (dx) kin[t] = dx[e - KF_STRIDE];
+            }
+        }
+        __syncthreads();
         if (threadIdx.x < 2) {
             const int k = threadIdx.x ? P.gp_kfb[i] : P.gp_kfa[i];
-            kf_trial_state(P, kst + (size_t)k * KF_STRIDE, P.kf_hidx[k], ok, kdl + 12 * threadIdx.x,
+            double* in = kin + (KF_STRIDE + 12) * threadIdx.x;
+            kf_trial_state(in, P.kf_hidx[k] >= 0 ? in + KF_STRIDE : nullptr, kdl + 12 * threadIdx.x,
                            kab + KF_STRIDE * threadIdx.x);
         }
         __syncthreads();
 #ifndef LBA_EXP_NO_GPPREP
-        gp_pair_prep(P, gps, i, kab, kab + KF_STRIDE, jac, ushm + 2 * 12 + 2 * KF_STRIDE,
+        gp_pair_prep(P, gps, i, kab, kab + KF_STRIDE, jac, ushm + 2 * 12 + 2 * KF_STRIDE + 2 * (KF_STRIDE + 12),
                      ustamp ? P.tdbg_lin + (size_t)blockIdx.x * 16 + 5 : nullptr);
 #endif
         if (threadIdx.x == 0) P.scale_part[blockIdx.x] = 0.0;
@@ -2358,14 +2426,21 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
     if ((int)blockIdx.x < P.n_gp + nkb) {
         const int k = (blockIdx.x - P.n_gp) * UPD_THREADS + threadIdx.x;
         if (k < P.n_kf) {
-            const int h = P.kf_hidx[k];
+            const int h = P.kf_hidx[k], xc = P.kf_cam[k];
+            // this KF's b_p rows and their owners, loaded before the first store (see kf_trial_state)
+            double bph[12];
+            bool adds[12];
+#pragma unroll
+            for (int j = 0; j < 12; ++j) {
+                bph[j] = h >= 0 ? P.bp[12 * h + j] : 0.0;
+                adds[j] = h >= 0 && row_adds(P, 12 * h + j);
+            }
             double* d = ushm + 12 * threadIdx.x;
             double* kn = ushm + 12 * UPD_THREADS + KF_STRIDE * threadIdx.x;
-            kf_trial_state(P, kst + (size_t)k * KF_STRIDE, h, ok, d, kn);
+            kf_trial_state(kst + (size_t)k * KF_STRIDE, kf_step(P, h, ok), d, kn);
             double* kw = ko + (size_t)k * KF_STRIDE;
             for (int j = 0; j < KF_STRIDE; ++j) kw[j] = kn[j];
             kf_pose_record(P, gps, k, kn);
-            const int xc = P.kf_cam[k];
             if (xc >= 0) {   // a free extrinsic: the trial state's camera record (Tcb, intrinsics, Ad(Tbc))
                 const double* c0 = P.camdb[si] + (size_t)xc * CAMD_STRIDE;
                 SE3 T;
@@ -2374,14 +2449,16 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
                 cam_record(T, c0[12], c0[13], c0[14], c0[15], P.camdb[si ^ 1] + (size_t)xc * CAMD_STRIDE);
             }
             if (h >= 0)
+#pragma unroll
                 for (int j = 0; j < 12; ++j) {
                     if (ok) P.x[12 * h + j] = d[j];
                     // (partitioned: b_p is the all-reduced one, a row's term is counted by its owner)
-                    if (row_adds(P, 12 * h + j)) sc += d[j] * (lambda * d[j] + P.bp[12 * h + j]);
+                    if (adds[j]) sc += d[j] * (lambda * d[j] + bph[j]);
                 }
         }
     } else if ((int)blockIdx.x < P.n_gp + nkb + P.n_stiles) {
-        sc = bs_tile(P, blockIdx.x - P.n_gp - nkb, si, ok, lambda, lo, ushm);
+        sc = bs_tile(P, blockIdx.x - P.n_gp - nkb, si, ok, lambda, lo, ushm,
+                     ustamp ? P.tdbg_lin + (size_t)blockIdx.x * 16 + 5 : nullptr);
     } else {
         // heavy landmarks (device indices n_lm - n_heavy ..): through their merged Hpl blocks
         const int l = P.n_lm - P.n_heavy + (blockIdx.x - P.n_gp - nkb - P.n_stiles) * UPD_THREADS + threadIdx.x;

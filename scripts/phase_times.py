@@ -108,6 +108,12 @@ def update_timeline(lin, n_gp, n_kfb, out):
         d = np.diff(lin[np.ix_(gpi, cols)].astype(np.int64), axis=1) / 100.0
         out.append("   GP-pair rebuild phases (us, mean / max): " +
                    "; ".join(f"{nm} {d[:, k].mean():.2f} / {d[:, k].max():.2f}" for k, nm in enumerate(names)))
+    tli = idx[idx >= n_gp + n_kfb]
+    if len(tli) and (lin[tli, 5] > 0).all() and (lin[tli, 6] > 0).all():   # bs_tile stamps, slots 5 / 6
+        d = np.diff(lin[np.ix_(tli, [14, 5, 6, 15])].astype(np.int64), axis=1) / 100.0
+        out.append("   landmark-tile phases (us, mean / max): " +
+                   "; ".join(f"{nm} {d[:, k].mean():.2f} / {d[:, k].max():.2f}"
+                             for k, nm in enumerate(["t_s = N x", "observations G^T t", "landmarks, scale sum"])))
     for name, sel in (("GP pairs", idx < n_gp), ("KF blocks", (idx >= n_gp) & (idx < n_gp + n_kfb)),
                       ("landmark blocks", idx >= n_gp + n_kfb)):
         if sel.any():
