@@ -143,6 +143,7 @@ struct DevProblem {
     const int* tile_nsent;
     const int* tile_kf0;
     const int* tile_nkf;
+    const int* tile_perm;        // k_lin_schur workgroup -> tile (longest first)
     const int* tkf_list;    // tile KF unions (pose block indices)
     const int* sent_l1;     // per Schur entry: tile-local KF index of k1 / k2
     const int* sent_l2;

@@ -295,10 +295,14 @@ T* dupload(lba_problem* p, const std::vector<T>& v) {
 
 // f(i) for i in [0, n) on up to 8 host threads, at most the CPUs this process may run on (LBA_SETUP_THREADS
 // overrides; 1: serial; 16 threads measured no faster on a 16-CPU share of the GPU box, the serial parts of the
-// set-up dominate, profiles/r3ai_setup_threads.txt).  Callers split work
-// into a fixed number of pieces, so the results never depend on the thread count.  The workers persist
-// (a set-up makes several parallel passes; spawning threads per pass cost ~0.1 ms each); a pass that finds
-// the pool busy (another problem setting up on another thread) runs on its caller's thread alone.
+// set-up dominate, profiles/r3ai_setup_threads.txt).  Callers split work into a fixed number of pieces, so the
+// results never depend on the thread count.  The workers persist (a set-up makes a dozen parallel passes;
+// spawning threads per pass cost ~0.1 ms each) and, after a pass, poll for the next one for a while before
+// they sleep: a set-up's passes follow each other within a millisecond, and an OS wake-up of the workers per
+// pass cost more than many of the passes themselves.  Pieces are claimed from one counter that packs
+// (pass, piece), so a worker that arrives late takes no piece of a later pass for an earlier one; the caller
+// waits for the pieces to be finished, not for every worker to have looked in.  A pass that finds the pool
+// busy (another problem setting up on another thread) runs on its caller's thread alone.
 class SetupPool {
   public:
     static SetupPool& get() {
@@ -312,25 +316,26 @@ class SetupPool {
         std::unique_lock<std::mutex> busy(busy_, std::try_to_lock);
         if (!busy.owns_lock()) return false;
         std::function<void(int)> job = [&](int i) { f(i); };
+        job_ = &job;
+        n_.store(n, std::memory_order_relaxed);
+        done_.store(0, std::memory_order_relaxed);
+        err_ = nullptr;
+        const unsigned long long g = ++pass_;
         {
-            std::lock_guard<std::mutex> g(m_);
-            job_ = &job;
-            n_ = n;
-            next_.store(0);
-            active_ = (int)workers_.size();
-            err_ = nullptr;
-            ++gen_;
+            std::lock_guard<std::mutex> lk(m_);
+            claim_.store(g << 32, std::memory_order_release);   // publishes job_ / n_ with the pass number
         }
         cv_.notify_all();
-        work();   // the caller takes pieces too
-        std::unique_lock<std::mutex> g(m_);
-        done_cv_.wait(g, [&] { return active_ == 0; });
+        work(g);   // the caller takes pieces too
+        for (int spins = 0; done_.load(std::memory_order_acquire) < n; ++spins)
+            if (spins > 4096) std::this_thread::yield();
         job_ = nullptr;
         if (err_) std::rethrow_exception(err_);
         return true;
     }
 
   private:
+    static constexpr int POLL_US = 3000;   // how long an idle worker polls for the next pass before it sleeps
     SetupPool() {
         const char* e = std::getenv("LBA_SETUP_THREADS");
         const int v = e ? std::atoi(e) : 0;
@@ -342,43 +347,57 @@ class SetupPool {
             workers_.emplace_back([this] {
                 unsigned long long seen = 0;
                 while (true) {
-                    {
-                        std::unique_lock<std::mutex> g(m_);
-                        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
-                        if (stop_) return;
-                        seen = gen_;
+                    auto fresh = [&] { return stop_.load(std::memory_order_acquire) ||
+                                              (claim_.load(std::memory_order_acquire) >> 32) != seen; };
+                    const auto t0 = std::chrono::steady_clock::now();
+                    while (!fresh()) {
+                        for (int k = 0; k < 64 && !fresh(); ++k) __builtin_ia32_pause();
+                        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(POLL_US)) {
+                            std::unique_lock<std::mutex> lk(m_);
+                            cv_.wait(lk, fresh);
+                        }
                     }
-                    work();
-                    std::lock_guard<std::mutex> g(m_);
-                    if (--active_ == 0) done_cv_.notify_all();
+                    if (stop_.load(std::memory_order_acquire)) return;
+                    seen = claim_.load(std::memory_order_acquire) >> 32;
+                    work(seen);
                 }
             });
     }
     ~SetupPool() {
         {
-            std::lock_guard<std::mutex> g(m_);
-            stop_ = true;
+            std::lock_guard<std::mutex> lk(m_);
+            stop_.store(true, std::memory_order_release);
         }
         cv_.notify_all();
         for (auto& w : workers_) w.join();
     }
-    void work() {
-        try {
-            for (int i; (i = next_++) < n_;) (*job_)(i);
-        } catch (...) {
-            std::lock_guard<std::mutex> g(m_);
-            if (!err_) err_ = std::current_exception();
-            next_.store(n_);
+    // claim pieces of pass g until none is left (or the pass is over); every piece claimed is counted done
+    void work(unsigned long long g) {
+        for (;;) {
+            unsigned long long c = claim_.load(std::memory_order_acquire);
+            int i;
+            do {
+                if ((c >> 32) != g || (int)(c & 0xffffffffu) >= n_.load(std::memory_order_relaxed)) return;
+                i = (int)(c & 0xffffffffu);
+            } while (!claim_.compare_exchange_weak(c, c + 1, std::memory_order_acq_rel, std::memory_order_acquire));
+            try {
+                (*job_)(i);
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(m_);
+                if (!err_) err_ = std::current_exception();
+            }
+            done_.fetch_add(1, std::memory_order_acq_rel);
         }
     }
     std::vector<std::thread> workers_;
     std::mutex busy_, m_;
-    std::condition_variable cv_, done_cv_;
+    std::condition_variable cv_;
     std::function<void(int)>* job_ = nullptr;
-    int n_ = 0, active_ = 0;
-    std::atomic<int> next_{0};
-    unsigned long long gen_ = 0;
-    bool stop_ = false;
+    std::atomic<int> n_{0};
+    unsigned long long pass_ = 0;
+    std::atomic<unsigned long long> claim_{0};   // pass << 32 | next piece
+    std::atomic<int> done_{0};
+    std::atomic<bool> stop_{false};
     std::exception_ptr err_;
 };
 
@@ -1294,6 +1313,20 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.ms0 = dupload(p, ms0); D.tile_sent0 = dupload(p, t_sent0);
     D.tile_nsent = dupload(p, t_nsent); D.tile_kf0 = dupload(p, t_kf0); D.tile_nkf = dupload(p, t_nkf);
     D.tkf_list = dupload(p, tkf_list);
+    {   // k_lin_schur's workgroup -> tile map: longest first by a cost estimate (list scheduling: the tiles
+        // outnumber the resident workgroup slots, ~1.4x at config 1, and the costly tiles, many KFs and Schur
+        // entries, sit at the end of the landmark order, so in index order the last round of workgroups ran
+        // long after most CUs were idle).  Cost: a non-negative least-squares fit of measured tile durations
+        // on the tile shape (us ~ 0.027 npair + 0.775 nlm + 0.077 nsent + 1.807 nkf, profiles/r3aq_tile_order.txt)
+        std::vector<long long> cost(n_tiles);
+        std::vector<int> perm(n_tiles);
+        for (int t = 0; t < n_tiles; ++t) {
+            cost[t] = 27LL * t_npair[t] + 775LL * t_nlm[t] + 77LL * t_nsent[t] + 1807LL * t_nkf[t];
+            perm[t] = t;
+        }
+        std::stable_sort(perm.begin(), perm.end(), [&](int x, int y) { return cost[x] > cost[y]; });
+        D.tile_perm = dupload(p, perm);
+    }
     D.n_stiles = n_stiles; D.n_heavy = n_heavy;
     D.hv_lm = dupload(p, hv_lm); D.hv_seg0 = dupload(p, hv_seg0); D.hv_hp0 = dupload(p, hv_hp0);
     D.hp_src0 = dupload(p, hp_src0); D.hp_src = dupload(p, hp_src); D.hp_gslot = dupload(p, hp_gslot);

@@ -692,7 +692,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
         edge_item<LS_THREADS>(P, sel, blockIdx.x - P.n_tiles, tid, U);
         return;
     }
-    const int tile = blockIdx.x;
+    const int tile = P.tile_perm[blockIdx.x];
     const int obs0 = P.tile_obs0[tile], nobs = P.tile_nobs[tile];
     const int ts0 = P.tile_smp0[tile], nts = P.tile_nsmp[tile];
     const int pair0 = P.tile_pair0[tile], npair = P.tile_npair[tile];
@@ -705,8 +705,8 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
     const double* __restrict__ camd = P.camdb[si];
     double* rows = U;
     double* rw = U + TILE_ROWS * ROW_STRIDE;
-    if (P.tdbg_lin && tid == 0) P.tdbg_lin[(size_t)blockIdx.x * 16 + 12] = __builtin_amdgcn_s_memrealtime();
-    LBA_TMARK(P.tdbg_lin, 0);
+    if (P.tdbg_lin && tid == 0) P.tdbg_lin[(size_t)tile * 16 + 12] = __builtin_amdgcn_s_memrealtime();
+    LBA_TMARKI(P.tdbg_lin, tile, 0);
 
     // ---- stage the tile's index lists in LDS
     {
@@ -755,7 +755,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
             pm[tid] = (unsigned char)(c >> 8);
         }
     }
-    LBA_TMARK(P.tdbg_lin, 1);
+    LBA_TMARKI(P.tdbg_lin, tile, 1);
 
     // ---- phase 2: the tile's partial of every pose sample it observes, in the sample's 6-dim space
     for (int task = tid; task < nts * 3; task += LS_THREADS) {
@@ -766,7 +766,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
         else if (ch == 1) smp_task<1>(P, rows, rw, r0, nr, mslot);
         else smp_task<2>(P, rows, rw, r0, nr, mslot);
     }
-    LBA_TMARK(P.tdbg_lin, 2);
+    LBA_TMARKI(P.tdbg_lin, tile, 2);
 
     // ---- phase 4: Hll / bl per landmark (threads from the top; before phase 3, so no
     //      register state of phase 3 lives across it); eliminating: Hll + lambda I = L D L^T
@@ -812,7 +812,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
             }
         }
     }
-    LBA_TMARK(P.tdbg_lin, 3);
+    LBA_TMARKI(P.tdbg_lin, tile, 3);
 
     // ---- phase 3: Hpl per (KF, landmark) pair, six rows per thread: the sum over the pair's (observation,
     //      side) entries of N_side^T G (N_side: the 6 x 12 block of the sample's factor for that KF, or for
@@ -867,10 +867,10 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
             for (int q = 0; q < 18; ++q) Hg[q] = hacc[q];
         }
     }
-    LBA_TMARK(P.tdbg_lin, 4);
+    LBA_TMARKI(P.tdbg_lin, tile, 4);
 
     if (!elim) {
-        if (P.tdbg_lin && tid == 0) P.tdbg_lin[(size_t)blockIdx.x * 16 + 13] = __builtin_amdgcn_s_memrealtime();
+        if (P.tdbg_lin && tid == 0) P.tdbg_lin[(size_t)tile * 16 + 13] = __builtin_amdgcn_s_memrealtime();
         return;
     }
     __syncthreads();   // every read of the rows is done: their LDS takes Hpl
@@ -970,7 +970,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
         }
     }
     LBA_TMARKI(P.tdbg_schur, tile, 3);
-    if (P.tdbg_lin && tid == 0) P.tdbg_lin[(size_t)blockIdx.x * 16 + 13] = __builtin_amdgcn_s_memrealtime();
+    if (P.tdbg_lin && tid == 0) P.tdbg_lin[(size_t)tile * 16 + 13] = __builtin_amdgcn_s_memrealtime();
 }
 
 // One heavy landmark (k_expand work item, PRI_THREADS threads): its segments' partials summed in a fixed
