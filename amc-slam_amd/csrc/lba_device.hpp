@@ -102,6 +102,7 @@ struct DevProblem {
     const int* kf_hidx;
     const int* gp_kfa;      // per GP pair (prev KF, KF)
     const int* gp_kfb;
+    const int* gp_hab;      // per GP pair: KF a, KF b, their pose blocks (-1: fixed)
     const int* gp_s0;       // [n_gp + 1] the pair's pose samples (contiguous)
     const double* gps_t;    // per GP sample: observation time
     int n_gps;              // GP samples; samples n_gps .. n_gps + n_kf - 1 are the KF poses (N = [0 | I 0])
@@ -156,11 +157,11 @@ struct DevProblem {
     const int* lm_rows;
     const int* lm_pair0;    // [n_lm + 1] landmark -> pairs
     // k_update's back-substitution of the regular tiles' landmarks in the sample space (no Hpl): per tile
-    // sample its pose sample (tsm_smp), per pose sample the pose blocks of its KF a / KF b / extrinsic
-    // (-1: fixed or none) and the camera of the extrinsic factor (smp_blk, 4 ints), per device landmark its
+    // sample its pose sample (tsm_smp) and that sample's pose blocks of KF a / KF b / extrinsic (-1: fixed
+    // or none) and the camera of the extrinsic factor (tsm_blk, 4 ints), per device landmark its
     // observations (lm_obs0, [n_lm + 1])
     const int* tsm_smp;
-    const int* smp_blk;
+    const int* tsm_blk;
     const int* lm_obs0;
     // Hpl is stored only for the heavy landmarks' pairs: pair index q lives at slot q - hpl_base
     // (canonical heavy pairs, then the segment pairs); n_hpl slots

@@ -677,6 +677,20 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     const int n_gps = (int)gps_t.size(), n_smp = n_gps + n_kfs;
     std::vector<int>& smp_of = scr_int(p, 0, n_obs);
     for (int i = 0; i < n_obs; ++i) smp_of[i] = is_gp(obs[i].kind) ? sample_of[i] : n_gps + obs[i].kf_b;
+    // per observation (input order) what the landmark-ordered passes below read, as one 16-byte record: the pose
+    // blocks of KF b / KF a / the extrinsic (-1: none or fixed) and its pose sample << 2 | rows (those passes
+    // visit observations in landmark order: one cache line per visit instead of the observation and smp_of)
+    std::vector<int>& orec = scr_int(p, 13, 4 * (size_t)n_obs);
+    par_for(8, [&](int piece) {
+        for (int i = (int)((long long)n_obs * piece / 8); i < (int)((long long)n_obs * (piece + 1) / 8); ++i) {
+            const lba_obs& o = obs[i];
+            int* r = orec.data() + 4 * (size_t)i;
+            r[0] = H[o.kf_b];
+            r[1] = is_gp(o.kind) ? H[o.kf_a] : -1;
+            r[2] = ext_block(o);
+            r[3] = (smp_of[i] << 2) | obs_dim(o.kind);
+        }
+    });
 
     // ---- heavy landmarks: a landmark whose observations / keyframes exceed one tile of k_lin_schur (a
     //      long track: LocalGPBA adds every observation of a local point, up to every keyframe of the
@@ -707,8 +721,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             if (!lm_act[l]) continue;
             int nr = 0, ne = 0, npl = 0, ns = 0;
             for (int q = lo0[l]; q < lo0[l + 1]; ++q) {
-                const lba_obs& o = obs[lo_of[q]];
-                const int hb = H[o.kf_b], ha = is_gp(o.kind) ? H[o.kf_a] : -1, hx = ext_block(o);
+                const int* r = orec.data() + 4 * (size_t)lo_of[q];
+                const int hb = r[0], ha = r[1], hx = r[2];
                 for (int k : {hb, ha})
                     if (k >= 0) {
                         lmin[l] = lmin[l] == INT_MAX ? k : std::min(lmin[l], k);
@@ -717,8 +731,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 for (int k : {hb, ha, hx})
                     if (k >= 0 && kst_[k] != l + 1) { kst_[k] = l + 1; ++npl; }
                 ne += (hb >= 0) + (ha >= 0) + (hx >= 0);
-                nr += obs_dim(o.kind);
-                const int sm = smp_of[lo_of[q]];
+                nr += r[3] & 3;
+                const int sm = r[3] >> 2;
                 if (sst_[sm] != l + 1) { sst_[sm] = l + 1; ++ns; }
             }
             heavy[l] = !tile_fits(lo0[l + 1] - lo0[l], nr, npl, 1, npl, ns, ne);
@@ -772,10 +786,9 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     auto lm_blocks = [&](int d, std::vector<int>& ks) {   // the landmark's pose blocks, ascending, distinct
         ks.clear();
         for (int q = lobs0[d]; q < lobs0[d + 1]; ++q) {
-            const lba_obs& o = obs[obs_of[q]];
-            if (H[o.kf_b] >= 0) ks.push_back(H[o.kf_b]);
-            if (is_gp(o.kind) && H[o.kf_a] >= 0) ks.push_back(H[o.kf_a]);
-            if (ext_block(o) >= 0) ks.push_back(ext_block(o));
+            const int* r = orec.data() + 4 * (size_t)obs_of[q];
+            for (int s = 0; s < 3; ++s)
+                if (r[s] >= 0) ks.push_back(r[s]);
         }
         std::sort(ks.begin(), ks.end());
         ks.erase(std::unique(ks.begin(), ks.end()), ks.end());
@@ -831,12 +844,12 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                          &ddim = scr_int(p, 6, n_obs), &dsmp = scr_int(p, 7, n_obs);
         par_for(SETUP_PIECES, [&](int piece) {
             for (int q = (int)((long long)n_obs * piece / SETUP_PIECES); q < (int)((long long)n_obs * (piece + 1) / SETUP_PIECES); ++q) {
-                const lba_obs& ob = obs[obs_of[q]];
-                dhb[q] = H[ob.kf_b];
-                dha[q] = is_gp(ob.kind) ? H[ob.kf_a] : -1;
-                dhx[q] = ext_block(ob);
-                ddim[q] = obs_dim(ob.kind);
-                dsmp[q] = smp_of[obs_of[q]];
+                const int* r = orec.data() + 4 * (size_t)obs_of[q];
+                dhb[q] = r[0];
+                dha[q] = r[1];
+                dhx[q] = r[2];
+                ddim[q] = r[3] & 3;
+                dsmp[q] = r[3] >> 2;
             }
         });
         sub("tile inputs");
@@ -1302,6 +1315,16 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.ob_z = dupload(p, ob_z); D.ob_w = dupload(p, ob_w);
     D.gp_s0 = dupload(p, gp_s0); D.gps_t = dupload(p, gps_t); D.n_gps = n_gps; D.n_smp = n_smp;
     D.kf_hidx = dupload(p, p->kf_hidx); D.gp_kfa = dupload(p, gp_a); D.gp_kfb = dupload(p, gp_b);
+    {   // per GP pair: KF a, KF b and their pose blocks (k_update's trial states: one load, no kf_hidx hop)
+        std::vector<int> hab(4 * std::max(gp_a.size(), (size_t)1), -1);
+        for (size_t g = 0; g < gp_a.size(); ++g) {
+            hab[4 * g] = gp_a[g];
+            hab[4 * g + 1] = gp_b[g];
+            hab[4 * g + 2] = p->kf_hidx[gp_a[g]];
+            hab[4 * g + 3] = p->kf_hidx[gp_b[g]];
+        }
+        D.gp_hab = dupload(p, hab);
+    }
     D.camdb[0] = dupload(p, camd);
     D.camdb[1] = dupload(p, camd);
     D.kf_cam = dupload(p, kf_cam);
@@ -1338,15 +1361,17 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.pair_rows = dupload(p, pair_rows); D.lm_r0 = dupload(p, lm_r0); D.lm_rows = dupload(p, lm_rows);
     D.lm_pair0 = dupload(p, lm_pair0);
     {   // k_update's sample-space back-substitution of the regular tiles' landmarks
-        std::vector<int> smp_blk(4 * (size_t)std::max(n_smp, 1), -1);
-        for (int sm = 0; sm < n_smp; ++sm) {
-            smp_blk[4 * (size_t)sm] = ent_a[sm];
-            smp_blk[4 * (size_t)sm + 1] = ent_b[sm];
-            smp_blk[4 * (size_t)sm + 2] = ent_e[sm];
-            smp_blk[4 * (size_t)sm + 3] = ent_cam[sm];
+        // per tile sample (tile order, beside tsm_smp): its sample's pose blocks and extrinsic camera
+        std::vector<int> tsm_blk(4 * std::max(tsm_smp.size(), (size_t)1), -1);
+        for (size_t j = 0; j < tsm_smp.size(); ++j) {
+            const int sm = tsm_smp[j];
+            tsm_blk[4 * j] = ent_a[sm];
+            tsm_blk[4 * j + 1] = ent_b[sm];
+            tsm_blk[4 * j + 2] = ent_e[sm];
+            tsm_blk[4 * j + 3] = ent_cam[sm];
         }
         D.tsm_smp = dupload(p, tsm_smp);
-        D.smp_blk = dupload(p, smp_blk);
+        D.tsm_blk = dupload(p, tsm_blk);
         D.lm_obs0 = dupload(p, lobs0);
     }
     D.hfin = p->d_hfin;
@@ -1572,11 +1597,20 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                         std::sort(ps.begin(), ps.end());
                         ps.erase(std::unique(ps.begin(), ps.end()), ps.end());
                         std::sort(ps.begin(), ps.end(), by_rank);
+                        // column k is factored as soon as its own updates are in: bit 27 marks the last entry that
+                        // updates row k (entries after it update rows c / i only, e.g. the other half's panels in a
+                        // separator's first column); no such entry: before the first one (task bit 29)
+                        const size_t e0 = cur->plist.size();
+                        int klast = -1;
                         for (int pp : ps) {   // only panels that update a held tile; row i only where used
                             const int tcp = pl.tile_id(c, pp), tkp = pl.tile_id(k, pp), tip = pl.tile_id(i, pp);
                             const bool fj = tcp >= 0, fk = tkp >= 0, fi = i != c && tip >= 0 && (fj || fk);
+                            if (fk) klast = (int)cur->plist.size();
                             if (fj || fk) add_entry(pp | (fi << 24) | (fj << 25) | (fk << 26), tcp, fi ? tip : -1, tkp);
                         }
+                        if (klast >= 0) cur->plist[klast] |= 1 << 27;
+                        else cur->tasks.back() |= 1 << 29;
+                        (void)e0;
                     } else {
                         add_task(c, i, 0, 0, tcc, tic, -1, -1, -1);
                         std::vector<int> ps(rcc);

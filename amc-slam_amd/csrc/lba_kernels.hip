@@ -2039,6 +2039,29 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             if (fk) cf_fetch(tile_at(a.Lm, a.plist_t[3 * q + 2]), CNB, rk);
         };
         bool ok = true;
+        // lookahead: column k's two tiles are factored as soon as their own updates are in (after the list
+        // entry marked with bit 27, or before the first entry when the task's bit 29 says none updates them),
+        // so the rest of the list (updates of rows j / i only) waits while it factors; the update from k is
+        // applied last, as before (the same order of updates on every copy of a tile)
+        auto factor_k = [&]() {
+            // ---- column k here: [A(k,k); A(j,k)] on wave 0 and [A(k,k); A(i,k)] on wave 1 -> L(j,k), L(i,k)
+            //      (the same stacked factorisations as the tasks of column k), kept staged for the update
+            stage_quad(stg[0], 0, qk);
+            stage_quad(stg[0], CNB, qjk);
+            if (ik) {
+                stage_quad(stg[1], 0, qk);
+                stage_quad(stg[1], CNB, qik);
+            }
+            __syncthreads();
+            if (wave == 0 || (wave == 1 && ik)) {
+                bool bad;
+                factor(stg[wave], bad);
+                (void)bad;   // (reported by panel k's own task)
+            }
+            __syncthreads();
+            if (tf) tf[6] = __builtin_amdgcn_s_memrealtime();
+        };
+        if (la && ((code >> 29) & 1)) factor_k();
         // the panels in update order (the same order in every task: the copies of a tile stay bitwise
         // identical)
         const int q0 = a.pl0[t], q1 = a.pl0[t + 1];
@@ -2065,25 +2088,10 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
                 if (ik && fi) sub_mma(qik, cf_mma_nt(Lt[1], Lt[2], rb, cb, lr, kq, z4));
             }
             __syncthreads();
+            if (la && ((e >> 27) & 1)) factor_k();
         }
         if (tf) tf[5] = __builtin_amdgcn_s_memrealtime();
-        if (ok && la) {
-            // ---- column k here: [A(k,k); A(j,k)] on wave 0 and [A(k,k); A(i,k)] on wave 1 -> L(j,k), L(i,k)
-            //      (the same stacked factorisations as the tasks of column k), then the updates from k
-            stage_quad(stg[0], 0, qk);
-            stage_quad(stg[0], CNB, qjk);
-            if (ik) {
-                stage_quad(stg[1], 0, qk);
-                stage_quad(stg[1], CNB, qik);
-            }
-            __syncthreads();
-            if (wave == 0 || (wave == 1 && ik)) {
-                bool bad;
-                factor(stg[wave], bad);
-                (void)bad;   // (reported by panel k's own task)
-            }
-            __syncthreads();
-            if (tf) tf[6] = __builtin_amdgcn_s_memrealtime();
+        if (ok && la) {   // the update from column k (factored above)
             sub_mma(qd, cf_mma_nt(stg[0] + CNB, stg[0] + CNB, rb, cb, lr, kq, z4));
             if (ik) sub_mma(qa, cf_mma_nt(stg[1] + CNB, stg[0] + CNB, rb, cb, lr, kq, z4));
             __syncthreads();
@@ -2276,15 +2284,14 @@ __device__ double bs_tile(const DevProblem& P, int tile, int si, bool ok, double
         const double* __restrict__ camd = P.camdb[si];
         // t_s(r) = sum_c N_s(r, c) [x_a; x_b](c) (+ the extrinsic factor on x_e): N column c at 12 + 6 c
         int sm[UPD_TILE_TASKS_PER_THREAD];
+        int4 bk[UPD_TILE_TASKS_PER_THREAD];
 #pragma unroll
         for (int q = 0; q < UPD_TILE_TASKS_PER_THREAD; ++q) {
             const int task = tid + UPD_THREADS * q;
-            sm[q] = task < nts * 6 ? P.tsm_smp[ts0 + task / 6] : -1;
+            const bool in = task < nts * 6;
+            sm[q] = in ? P.tsm_smp[ts0 + task / 6] : -1;
+            bk[q] = in ? *reinterpret_cast<const int4*>(P.tsm_blk + 4 * (size_t)(ts0 + task / 6)) : make_int4(-1, -1, -1, -1);
         }
-        int4 bk[UPD_TILE_TASKS_PER_THREAD];
-#pragma unroll
-        for (int q = 0; q < UPD_TILE_TASKS_PER_THREAD; ++q)
-            bk[q] = sm[q] >= 0 ? *reinterpret_cast<const int4*>(P.smp_blk + 4 * (size_t)sm[q]) : make_int4(-1, -1, -1, -1);
         double acc[UPD_TILE_TASKS_PER_THREAD];
 #pragma unroll
         for (int q = 0; q < UPD_TILE_TASKS_PER_THREAD; ++q) {
@@ -2400,17 +2407,16 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
         {
             const int t = threadIdx.x, side = t >= KF_STRIDE + 12 ? 1 : 0, e = t - side * (KF_STRIDE + 12);
             if (t < 2 * (KF_STRIDE + 12)) {
-                const int k = side ? P.gp_kfb[i] : P.gp_kfa[i];
-                const double* dx = kf_step(P, P.kf_hidx[k], ok);
+                const int k = P.gp_hab[4 * i + side];
+                const double* dx = kf_step(P, P.gp_hab[4 * i + 2 + side], ok);
                 if (e < KF_STRIDE) kin[t] = kst[(size_t)k * KF_STRIDE + e];
                 else if (dx) kin[t] = dx[e - KF_STRIDE];
             }
         }
         __syncthreads();
         if (threadIdx.x < 2) {
-            const int k = threadIdx.x ? P.gp_kfb[i] : P.gp_kfa[i];
             double* in = kin + (KF_STRIDE + 12) * threadIdx.x;
-            kf_trial_state(in, P.kf_hidx[k] >= 0 ? in + KF_STRIDE : nullptr, kdl + 12 * threadIdx.x,
+            kf_trial_state(in, P.gp_hab[4 * i + 2 + threadIdx.x] >= 0 ? in + KF_STRIDE : nullptr, kdl + 12 * threadIdx.x,
                            kab + KF_STRIDE * threadIdx.x);
         }
         __syncthreads();
