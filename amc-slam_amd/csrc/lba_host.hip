@@ -677,20 +677,6 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     const int n_gps = (int)gps_t.size(), n_smp = n_gps + n_kfs;
     std::vector<int>& smp_of = scr_int(p, 0, n_obs);
     for (int i = 0; i < n_obs; ++i) smp_of[i] = is_gp(obs[i].kind) ? sample_of[i] : n_gps + obs[i].kf_b;
-    // per observation (input order) what the landmark-ordered passes below read, as one 16-byte record: the pose
-    // blocks of KF b / KF a / the extrinsic (-1: none or fixed) and its pose sample << 2 | rows (those passes
-    // visit observations in landmark order: one cache line per visit instead of the observation and smp_of)
-    std::vector<int>& orec = scr_int(p, 13, 4 * (size_t)n_obs);
-    par_for(8, [&](int piece) {
-        for (int i = (int)((long long)n_obs * piece / 8); i < (int)((long long)n_obs * (piece + 1) / 8); ++i) {
-            const lba_obs& o = obs[i];
-            int* r = orec.data() + 4 * (size_t)i;
-            r[0] = H[o.kf_b];
-            r[1] = is_gp(o.kind) ? H[o.kf_a] : -1;
-            r[2] = ext_block(o);
-            r[3] = (smp_of[i] << 2) | obs_dim(o.kind);
-        }
-    });
 
     // ---- heavy landmarks: a landmark whose observations / keyframes exceed one tile of k_lin_schur (a
     //      long track: LocalGPBA adds every observation of a local point, up to every keyframe of the
@@ -721,8 +707,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             if (!lm_act[l]) continue;
             int nr = 0, ne = 0, npl = 0, ns = 0;
             for (int q = lo0[l]; q < lo0[l + 1]; ++q) {
-                const int* r = orec.data() + 4 * (size_t)lo_of[q];
-                const int hb = r[0], ha = r[1], hx = r[2];
+                const lba_obs& o = obs[lo_of[q]];
+                const int hb = H[o.kf_b], ha = is_gp(o.kind) ? H[o.kf_a] : -1, hx = ext_block(o);
                 for (int k : {hb, ha})
                     if (k >= 0) {
                         lmin[l] = lmin[l] == INT_MAX ? k : std::min(lmin[l], k);
@@ -731,8 +717,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 for (int k : {hb, ha, hx})
                     if (k >= 0 && kst_[k] != l + 1) { kst_[k] = l + 1; ++npl; }
                 ne += (hb >= 0) + (ha >= 0) + (hx >= 0);
-                nr += r[3] & 3;
-                const int sm = r[3] >> 2;
+                nr += obs_dim(o.kind);
+                const int sm = smp_of[lo_of[q]];
                 if (sst_[sm] != l + 1) { sst_[sm] = l + 1; ++ns; }
             }
             heavy[l] = !tile_fits(lo0[l + 1] - lo0[l], nr, npl, 1, npl, ns, ne);
@@ -786,9 +772,10 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     auto lm_blocks = [&](int d, std::vector<int>& ks) {   // the landmark's pose blocks, ascending, distinct
         ks.clear();
         for (int q = lobs0[d]; q < lobs0[d + 1]; ++q) {
-            const int* r = orec.data() + 4 * (size_t)obs_of[q];
-            for (int s = 0; s < 3; ++s)
-                if (r[s] >= 0) ks.push_back(r[s]);
+            const lba_obs& o = obs[obs_of[q]];
+            if (H[o.kf_b] >= 0) ks.push_back(H[o.kf_b]);
+            if (is_gp(o.kind) && H[o.kf_a] >= 0) ks.push_back(H[o.kf_a]);
+            if (ext_block(o) >= 0) ks.push_back(ext_block(o));
         }
         std::sort(ks.begin(), ks.end());
         ks.erase(std::unique(ks.begin(), ks.end()), ks.end());
@@ -844,12 +831,12 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                          &ddim = scr_int(p, 6, n_obs), &dsmp = scr_int(p, 7, n_obs);
         par_for(SETUP_PIECES, [&](int piece) {
             for (int q = (int)((long long)n_obs * piece / SETUP_PIECES); q < (int)((long long)n_obs * (piece + 1) / SETUP_PIECES); ++q) {
-                const int* r = orec.data() + 4 * (size_t)obs_of[q];
-                dhb[q] = r[0];
-                dha[q] = r[1];
-                dhx[q] = r[2];
-                ddim[q] = r[3] & 3;
-                dsmp[q] = r[3] >> 2;
+                const lba_obs& ob = obs[obs_of[q]];
+                dhb[q] = H[ob.kf_b];
+                dha[q] = is_gp(ob.kind) ? H[ob.kf_a] : -1;
+                dhx[q] = ext_block(ob);
+                ddim[q] = obs_dim(ob.kind);
+                dsmp[q] = smp_of[obs_of[q]];
             }
         });
         sub("tile inputs");
@@ -1600,7 +1587,6 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                         // column k is factored as soon as its own updates are in: bit 27 marks the last entry that
                         // updates row k (entries after it update rows c / i only, e.g. the other half's panels in a
                         // separator's first column); no such entry: before the first one (task bit 29)
-                        const size_t e0 = cur->plist.size();
                         int klast = -1;
                         for (int pp : ps) {   // only panels that update a held tile; row i only where used
                             const int tcp = pl.tile_id(c, pp), tkp = pl.tile_id(k, pp), tip = pl.tile_id(i, pp);
@@ -1610,7 +1596,6 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                         }
                         if (klast >= 0) cur->plist[klast] |= 1 << 27;
                         else cur->tasks.back() |= 1 << 29;
-                        (void)e0;
                     } else {
                         add_task(c, i, 0, 0, tcc, tic, -1, -1, -1);
                         std::vector<int> ps(rcc);
