@@ -1823,9 +1823,13 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         D.rnat = dupload(p, rnat);
         // every trial, k_lin_schur zeroes S (the tiles of L: structural non-zeros and fill-in) and k_assemble
         // then writes the structurally non-zero blocks
+        // (in decreasing order of the slots a block sums: the blocks outnumber k_assemble's resident workgroups
+        // and the diagonal blocks sum the most partials, so they go first, as k_lin_schur's tiles do)
         std::vector<int> asm_list;
         for (int u = 0; u < n_ublocks; ++u)
             if (hcnt[u] > 0 || scnt[u] > 0 || ub_i[u] == ub_j[u]) asm_list.push_back(u);
+        std::stable_sort(asm_list.begin(), asm_list.end(),
+                         [&](int x, int y) { return hcnt[x] + scnt[x] > hcnt[y] + scnt[y]; });
         D.n_ztiles = ntile;
         D.part_rank = p->part_rank;
         D.part_n = p->part_n;
