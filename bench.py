@@ -313,8 +313,8 @@ def main():
         # outside the timed region above) + optimize(window_iters): time a set_problem on the engine
         kfs, lm, obs, pri, vel, cams = ph._keep
         L = amc_lba.lib()
-        sp = []   # (median of three set-ups: one sample is at the mercy of the host's scheduling)
-        for _ in range(3):
+        sp = []   # (median of seven set-ups: one sample is at the mercy of the host's scheduling)
+        for _ in range(7):
             t_sp = time.perf_counter()
             rc = L.lba_set_problem(ph.h, amc_lba.ptr(kfs), len(kfs), amc_lba.ptr(lm), len(lm), amc_lba.ptr(obs),
                                    len(obs), amc_lba.ptr(pri), len(pri), amc_lba.ptr(vel), len(vel), amc_lba.ptr(cams),
