@@ -2629,27 +2629,25 @@ __device__ void trial_sums(const DevProblem& P, double* red, double& sa, double&
     const int nc = P.n_tiles + P.n_prior + P.n_vel + P.n_eprior;
     // (the loads of U strided elements are issued before their additions, out-of-range ones masked: the
     //  same per-thread order of additions as the plain strided loop, without one round trip per element)
+    // (the three arrays' loads of one round are issued together: one memory round trip per U * NT elements of
+    //  the longer list, not one per list)
     constexpr int U = 8;
     double a = 0.0, b = 0.0, c = 0.0;
-    for (int i0 = tid; i0 < nc; i0 += U * NT) {
-        double xa[U], xb[U];
+    const int nu = P.n_upd_blocks, nmax = nc > nu ? nc : nu;
+    for (int i0 = tid; i0 < nmax; i0 += U * NT) {
+        double xa[U], xb[U], xc[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int i = i0 + u * NT;
             xa[u] = i < nc ? P.chi_lin[i] : 0.0;
             xb[u] = i < nc ? P.chi_eval[i] : 0.0;
+            xc[u] = i < nu ? P.scale_part[i] : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+        for (int u = 0; u < U; ++u) {
             if (i0 + u * NT < nc) { a += xa[u]; b += xb[u]; }
-    }
-    for (int i0 = tid; i0 < P.n_upd_blocks; i0 += U * NT) {
-        double xc[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) xc[u] = i0 + u * NT < P.n_upd_blocks ? P.scale_part[i0 + u * NT] : 0.0;
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (i0 + u * NT < P.n_upd_blocks) c += xc[u];
+            if (i0 + u * NT < nu) c += xc[u];
+        }
     }
     sa = block_sum<NT>(a, red);
     __syncthreads();
@@ -2697,11 +2695,16 @@ template <int NT>
 __device__ void finalize_body(const DevProblem& P, unsigned long long seq, int mode, double* red) {
     const int tid = threadIdx.x;
     double sa, sb, sc, sinfo;
+    // the controller and the factorisation status are loaded ahead of the sums (they do not change in this
+    // launch): the decision then waits for one round of loads, not three
+    LMCtl ctl;
+    if (tid == 0 && mode != FIN_INITIAL && mode != FIN_HOST) ctl = *P.ctl;
+    const int info = P.part_n > 0 ? 0 : *P.info;
     if (P.part_n > 0) {   // partitioned: the all-reduced sums of every rank's k_partials
         sa = P.red4[0]; sb = P.red4[1]; sc = P.red4[2]; sinfo = P.red4[3];
     } else {
         trial_sums<NT>(P, red, sa, sb, sc);
-        sinfo = (double)(*P.info);
+        sinfo = (double)info;
     }
     if (tid != 0) return;
     const double v[4] = {sa, sb, sc, sinfo};
@@ -2712,7 +2715,6 @@ __device__ void finalize_body(const DevProblem& P, unsigned long long seq, int m
     if (mode == FIN_HOST) {
         for (int i = 0; i < 4; ++i) P.fin[i] = v[i];
     } else {
-        LMCtl ctl = *P.ctl;
         if (!ctl.done)
             for (int i = 0; i < 4; ++i) P.fin[i] = v[i];
         lm_decide(ctl, sa, sb, sc, sinfo == 0.0, P.hlog);
