@@ -148,10 +148,27 @@ __device__ __forceinline__ void load_cam(const double* c, CamD* d) {
 // Pose of the body at the observation time (Rwb, twb): the observation's pose sample (a GP sample for
 // GP edges, the KF pose record for EdgeMono / EdgeStereo).  Returns the stereo bf of the edge's first
 // KF vertex.
-__device__ __forceinline__ double obs_pose(const DevProblem& P, const double* gps, const double* kst, int o, bool gp,
+// ObsIn: an observation's per-observation inputs, loaded together with its ob_meta by the caller (before the
+// branch on its kind, so they are one memory round trip, not one after the meta load and one more after that).
+struct ObsIn {
+    int kfa, kfb, smp, lm;
+    double z[3], w;
+};
+__device__ __forceinline__ ObsIn obs_in(const DevProblem& P, int o) {
+    ObsIn in;
+    in.kfa = P.ob_kfa[o];
+    in.kfb = P.ob_kfb[o];
+    in.smp = P.ob_smp[o];
+    in.lm = P.ob_lm[o];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) in.z[d] = P.ob_z[3 * (size_t)o + d];
+    in.w = P.ob_w[o];
+    return in;
+}
+__device__ __forceinline__ double obs_pose(const double* gps, const double* kst, const ObsIn& in, bool gp,
                                            double* Rwb, double* twb) {
-    const int ka = gp ? P.ob_kfa[o] : P.ob_kfb[o];
-    const double* S = gps + (size_t)P.ob_smp[o] * GPS_STRIDE;
+    const int ka = gp ? in.kfa : in.kfb;
+    const double* S = gps + (size_t)in.smp * GPS_STRIDE;
 #pragma unroll
     for (int i = 0; i < 9; ++i) Rwb[i] = S[i];
     twb[0] = S[9]; twb[1] = S[10]; twb[2] = S[11];
@@ -163,17 +180,17 @@ __device__ __forceinline__ double obs_pose(const DevProblem& P, const double* gp
 // pose sample: the pose / velocity Jacobian J1 N is never formed, see k_linearize); returns rho(chi2).
 template <int DIM>
 __device__ __forceinline__ double lin_obs(const DevProblem& P, const double* gps, const double* kst, const double* lst,
-                                          const double* camd, int o, int cam, bool gp, double* rows, double* rw,
-                                          int write_res) {
+                                          const double* camd, int o, const ObsIn& in, int cam, bool gp, double* rows,
+                                          double* rw, int write_res) {
     CamD cd;
     load_cam(camd + (size_t)cam * CAMD_STRIDE, &cd);
     double Rwb[9], twb[3];
-    const double bf = obs_pose(P, gps, kst, o, gp, Rwb, twb);
-    const double* Xw = lst + (size_t)P.ob_lm[o] * 3;
+    const double bf = obs_pose(gps, kst, in, gp, Rwb, twb);
+    const double* Xw = lst + (size_t)in.lm * 3;
     double z[DIM];
 #pragma unroll
-    for (int d = 0; d < DIM; ++d) z[d] = P.ob_z[3 * (size_t)o + d];
-    const double w = P.ob_w[o];
+    for (int d = 0; d < DIM; ++d) z[d] = in.z[d];
+    const double w = in.w;
     double Xb[3], Xc[3], e[DIM];
     project_residual<DIM>(Rwb, twb, cd, Xw, z, bf, Xb, Xc, e);
     double chi = 0.0;
@@ -205,17 +222,18 @@ __device__ __forceinline__ double lin_obs(const DevProblem& P, const double* gps
 // Residual-only evaluation of one observation (computeError + robust chi2); returns rho(chi2).
 template <int DIM>
 __device__ __forceinline__ double eval_obs(const DevProblem& P, const double* gps, const double* kst,
-                                           const double* lst, const double* camd, int o, int cam, bool gp) {
+                                           const double* lst, const double* camd, int o, const ObsIn& in, int cam,
+                                           bool gp) {
     CamD cd;
     load_cam(camd + (size_t)cam * CAMD_STRIDE, &cd);
     double Rwb[9], twb[3];
-    const double bf = obs_pose(P, gps, kst, o, gp, Rwb, twb);
+    const double bf = obs_pose(gps, kst, in, gp, Rwb, twb);
     double z[DIM];
 #pragma unroll
-    for (int d = 0; d < DIM; ++d) z[d] = P.ob_z[3 * (size_t)o + d];
-    const double w = P.ob_w[o];
+    for (int d = 0; d < DIM; ++d) z[d] = in.z[d];
+    const double w = in.w;
     double Xb[3], Xc[3], e[DIM];
-    project_residual<DIM>(Rwb, twb, cd, lst + (size_t)P.ob_lm[o] * 3, z, bf, Xb, Xc, e);
+    project_residual<DIM>(Rwb, twb, cd, lst + (size_t)in.lm * 3, z, bf, Xb, Xc, e);
     double chi = 0.0;
 #pragma unroll
     for (int d = 0; d < DIM; ++d) chi += e[d] * (w * e[d]);
@@ -729,16 +747,17 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
     double rho0 = 0.0;
     if (tid < nobs) {
         const int o = obs0 + tid;
-        const int meta = P.ob_meta[o];
+        const int meta = P.ob_meta[o], orw = P.ob_row[o];
+        const ObsIn in = obs_in(P, o);
         const int kind = meta & 15, cam = meta >> 4;
         const bool gp = kind <= LBA_STEREO_GP;
-        osm[tid] = P.ob_smp[o];
+        osm[tid] = in.smp;
         ocam[tid] = cam;
         const bool st = kind == LBA_STEREO_GP || kind == LBA_STEREO;
-        orow[tid] = (P.ob_row[o] & 0xffff) | ((st ? 3 : 2) << 16);
+        orow[tid] = (orw & 0xffff) | ((st ? 3 : 2) << 16);
         const int wr = (mode & LS_RES) ? 1 : 0;
-        rho0 = st ? lin_obs<3>(P, gps, kst, lst, camd, o, cam, gp, rows, rw, wr)
-                  : lin_obs<2>(P, gps, kst, lst, camd, o, cam, gp, rows, rw, wr);
+        rho0 = st ? lin_obs<3>(P, gps, kst, lst, camd, o, in, cam, gp, rows, rw, wr)
+                  : lin_obs<2>(P, gps, kst, lst, camd, o, in, cam, gp, rows, rw, wr);
     }
     const double tchi = block_sum<LS_THREADS>(rho0, red);   // (its barrier also publishes rows / lists)
     if (tid == 0) P.chi_lin[tile] = tchi;
@@ -2212,17 +2231,18 @@ __device__ __attribute__((noinline)) void kf_trial_state(const double* __restric
 // linearisation is recomputed at the state the sweep linearised (the same inputs and code as lin_obs).
 template <int DIM>
 __device__ __forceinline__ void bs_obs(const DevProblem& P, const double* gps, const double* kst, const double* lst,
-                                       const double* camd, int o, int cam, bool gp, const double* t, double* v) {
+                                       const double* camd, const ObsIn& in, int cam, bool gp, const double* t,
+                                       double* v) {
     CamD cd;
     load_cam(camd + (size_t)cam * CAMD_STRIDE, &cd);
     double Rwb[9], twb[3];
-    const double bf = obs_pose(P, gps, kst, o, gp, Rwb, twb);
+    const double bf = obs_pose(gps, kst, in, gp, Rwb, twb);
     double z[DIM];
 #pragma unroll
-    for (int d = 0; d < DIM; ++d) z[d] = P.ob_z[3 * (size_t)o + d];
-    const double w = P.ob_w[o];
+    for (int d = 0; d < DIM; ++d) z[d] = in.z[d];
+    const double w = in.w;
     double Xb[3], Xc[3], e[DIM];
-    project_residual<DIM>(Rwb, twb, cd, lst + (size_t)P.ob_lm[o] * 3, z, bf, Xb, Xc, e);
+    project_residual<DIM>(Rwb, twb, cd, lst + (size_t)in.lm * 3, z, bf, Xb, Xc, e);
     double chi = 0.0;
 #pragma unroll
     for (int d = 0; d < DIM; ++d) chi += e[d] * (w * e[d]);
@@ -2323,12 +2343,13 @@ __device__ double bs_tile(const DevProblem& P, int tile, int si, bool ok, double
             const int ol = tid + UPD_THREADS * k;
             if (ol < nobs) {
                 const int o = obs0 + ol;
-                const int meta = P.ob_meta[o];
+                const int meta = P.ob_meta[o], orw = P.ob_row[o];
+                const ObsIn in = obs_in(P, o);
                 const int kind = meta & 15, cam = meta >> 4;
                 const bool gp = kind <= LBA_STEREO_GP;
-                const double* t = tsh[P.ob_row[o] >> 16];
-                if (kind == LBA_STEREO_GP || kind == LBA_STEREO) bs_obs<3>(P, gps, kst, lst, camd, o, cam, gp, t, vsh[ol]);
-                else bs_obs<2>(P, gps, kst, lst, camd, o, cam, gp, t, vsh[ol]);
+                const double* t = tsh[orw >> 16];
+                if (kind == LBA_STEREO_GP || kind == LBA_STEREO) bs_obs<3>(P, gps, kst, lst, camd, in, cam, gp, t, vsh[ol]);
+                else bs_obs<2>(P, gps, kst, lst, camd, in, cam, gp, t, vsh[ol]);
             }
         }
         __syncthreads();
@@ -2522,10 +2543,11 @@ __global__ __launch_bounds__(TILE_OBS) void k_eval(DevProblem P, int sel, int ga
         if (tid < P.tile_nobs[tile]) {
             const int o = P.tile_obs0[tile] + tid;
             const int meta = P.ob_meta[o];
+            const ObsIn in = obs_in(P, o);
             const int kind = meta & 15, cam = meta >> 4;
             const bool gp = kind <= LBA_STEREO_GP;
-            rho0 = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? eval_obs<3>(P, gps, kst, lst, camd, o, cam, gp)
-                                                                 : eval_obs<2>(P, gps, kst, lst, camd, o, cam, gp);
+            rho0 = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? eval_obs<3>(P, gps, kst, lst, camd, o, in, cam, gp)
+                                                                 : eval_obs<2>(P, gps, kst, lst, camd, o, in, cam, gp);
         }
         const double s = block_sum<TILE_OBS>(rho0, red);
         if (tid == 0) P.chi_eval[tile] = s;
