@@ -272,6 +272,10 @@ __device__ __forceinline__ void gp_pair_prep(const DevProblem& P, double* gps, i
     const int tid = threadIdx.x;
     // (diagnostics: pst = s_memrealtime stamps after each phase, thread 0)
 #define PREP_STAMP(k) do { if (pst && tid == 0) pst[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+    // the pair's sample range and the first chunk's sample times, loaded before the pair chain (after it they
+    // would cost the chain one more memory round trip behind its barriers)
+    const int s0 = P.gp_s0[i], s1 = P.gp_s0[i + 1];
+    const double t_first = tid < min(PREP_SCHUNK, s1 - s0) ? P.gps_t[s0 + tid] : 0.0;
     if (tid < 6) vbs[tid] = kb[7 + tid];
     if (tid == 0) {
         const SE3 Ta = load_se3(ka), Tb = load_se3(kb);
@@ -312,15 +316,15 @@ __device__ __forceinline__ void gp_pair_prep(const DevProblem& P, double* gps, i
         }
     __syncthreads();
     PREP_STAMP(3);
-    for (int c0 = P.gp_s0[i]; c0 < P.gp_s0[i + 1]; c0 += PREP_SCHUNK) {
-        const int ns = min(PREP_SCHUNK, P.gp_s0[i + 1] - c0);
+    for (int c0 = s0; c0 < s1; c0 += PREP_SCHUNK) {
+        const int ns = min(PREP_SCHUNK, s1 - c0);
         // one lane per sample: the interpolated pose T1 exp(xi) (gp_sample_pose), Ad(exp(xi)^-1), Jr(xi)
         if (tid < ns) {
             GPSample* S = reinterpret_cast<GPSample*>(gps + (size_t)(c0 + tid) * GPS_STRIDE);
             double xi[6];
             GPScalars g;
             SE3 E;
-            gp_sample_pose(pr, P.gps_t[c0 + tid], S->Rwb, S->twb, xi, &g, &E);
+            gp_sample_pose(pr, c0 == s0 ? t_first : P.gps_t[c0 + tid], S->Rwb, S->twb, xi, &g, &E);
             if (jac) {
                 const SE3 Em = se3_inv(E);                  // Ad(exp(-xi)) = [R', t'^ R'; 0, R']
                 double Ht[9];
