@@ -409,6 +409,8 @@ __device__ __forceinline__ void smp_task(const DevProblem& P, const double* rows
     double acc[9];
 #pragma unroll
     for (int q = 0; q < 9; ++q) acc[q] = 0.0;
+    // (unrolled: the next rows' LDS reads are issued ahead of this row's FMAs; the same order of additions)
+#pragma unroll 4
     for (int r = r0; r < r0 + nr; ++r) {
         const double* R = rows + r * ROW_STRIDE;
         const double sw = rw[r];
