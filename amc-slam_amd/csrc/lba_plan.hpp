@@ -327,12 +327,19 @@ inline Plan make_plan(int NP, int NPk, const std::vector<std::vector<int>>& lowe
         // exists with the shortest chain max(A, B) + S1 + tail (a tail row may reach back anywhere)
         int c_best = NPk;
         if (tail_search && max_levels > 0) {
+            // for a cut at a, B = [b, c) is the longest top range of [0, c) whose rows all start at >= a:
+            // b = 1 + the last row r < c with pfirst[r] < a (or a), i.e. a running max over pfirst values
+            // (mv[v]: the last row below c starting at v), O(NP) per c instead of a scan per (c, a)
             int bestlen = NP + 1;
+            std::vector<int> mv(NP + 1);
             for (int c = NPk; c >= 1; --c) {
                 if (NPk - c >= bestlen) break;
+                std::fill(mv.begin(), mv.begin() + c, -1);
+                for (int r = 0; r < c; ++r) mv[pfirst[r]] = std::max(mv[pfirst[r]], r);
+                int M = -1;
                 for (int a = 1; a < c; ++a) {
-                    int b = c;
-                    while (b > a && pfirst[b - 1] >= a) --b;
+                    M = std::max(M, mv[a - 1]);
+                    const int b = M >= a ? M + 1 : a;
                     if (b >= c) continue;
                     const int len = std::max(a, c - b) + (b - a) + (NPk - c);
                     if (len < bestlen) { bestlen = len; c_best = c; }
