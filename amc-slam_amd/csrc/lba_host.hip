@@ -1334,7 +1334,9 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             cost[t] = 27LL * t_npair[t] + 775LL * t_nlm[t] + 77LL * t_nsent[t] + 1807LL * t_nkf[t];
             perm[t] = t;
         }
-        std::stable_sort(perm.begin(), perm.end(), [&](int x, int y) { return cost[x] > cost[y]; });
+        // (LBA_DISPATCH_INDEX_ORDER: index order, for the tests that check the order changes no result)
+        if (!std::getenv("LBA_DISPATCH_INDEX_ORDER"))
+            std::stable_sort(perm.begin(), perm.end(), [&](int x, int y) { return cost[x] > cost[y]; });
         D.tile_perm = dupload(p, perm);
     }
     D.n_stiles = n_stiles; D.n_heavy = n_heavy;
@@ -1828,8 +1830,9 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         std::vector<int> asm_list;
         for (int u = 0; u < n_ublocks; ++u)
             if (hcnt[u] > 0 || scnt[u] > 0 || ub_i[u] == ub_j[u]) asm_list.push_back(u);
-        std::stable_sort(asm_list.begin(), asm_list.end(),
-                         [&](int x, int y) { return hcnt[x] + scnt[x] > hcnt[y] + scnt[y]; });
+        if (!std::getenv("LBA_DISPATCH_INDEX_ORDER"))
+            std::stable_sort(asm_list.begin(), asm_list.end(),
+                             [&](int x, int y) { return hcnt[x] + scnt[x] > hcnt[y] + scnt[y]; });
         D.n_ztiles = ntile;
         D.part_rank = p->part_rank;
         D.part_n = p->part_n;
