@@ -90,6 +90,8 @@ def lib():
         L.lba_farm_plan.argtypes = [vp, _lp, _ip, _lp, _ip, _ip]
         L.lba_farm_exchange.argtypes = [vp]
         L.lba_solver_info.argtypes = [vp, _ip]
+        if hasattr(L, "lba_debug_pool_stress"):
+            L.lba_debug_pool_stress.argtypes = [ctypes.c_int32, ctypes.c_int32]
         if hasattr(L, "lba_solver_flops"):   # (absent from builds before it: A/B runs of older libraries)
             L.lba_solver_flops.argtypes = [vp, _dp]
         L.lba_device_bytes.argtypes = [vp]
@@ -114,7 +116,7 @@ def exported_symbols():
             "lba_pose_dim", "lba_set_partition", "lba_rccl_unique_id", "lba_set_partition_rccl", "lba_group_create",
             "lba_group_destroy", "lba_set_partition_group", "lba_get_cams", "lba_set_farm", "lba_set_farm_rccl",
             "lba_set_farm_group", "lba_farm_plan", "lba_farm_exchange", "lba_farm_match", "lba_solver_info", "lba_solver_flops", "lba_device_bytes",
-            "lba_setup_host_profile", "lba_partition_assign", "lba_kf_owner", "lba_split_info"]
+            "lba_setup_host_profile", "lba_debug_pool_stress", "lba_partition_assign", "lba_kf_owner", "lba_split_info"]
 
 
 def setup_host_profile(win, **cfg_over):

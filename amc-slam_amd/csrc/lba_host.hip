@@ -329,6 +329,11 @@ class SetupPool {
         work(g);   // the caller takes pieces too
         for (int spins = 0; done_.load(std::memory_order_acquire) < n; ++spins)
             if (spins > 4096) std::this_thread::yield();
+        // close the pass before any field of the next one is written: a worker that loaded this pass's
+        // last claim word (every piece taken) and was preempted before its bound check would otherwise
+        // pass that check against the next pass's larger n_ and win its CAS against the unchanged word,
+        // running a piece of the next job ahead of its publication
+        claim_.store((g << 32) | CLOSED, std::memory_order_release);
         job_ = nullptr;
         if (err_) std::rethrow_exception(err_);
         return true;
@@ -336,6 +341,7 @@ class SetupPool {
 
   private:
     static constexpr int POLL_US = 3000;   // how long an idle worker polls for the next pass before it sleeps
+    static constexpr unsigned long long CLOSED = 0x7fffffffull;   // piece word of a finished pass (>= any n)
     SetupPool() {
         const char* e = std::getenv("LBA_SETUP_THREADS");
         const int v = e ? std::atoi(e) : 0;
@@ -2279,6 +2285,28 @@ extern "C" {
 int lba_abi_version(void) { return LBA_ABI_VERSION; }
 
 int lba_live_problems(void) { return g_live_problems.load(); }
+
+int lba_debug_pool_stress(int32_t passes, int32_t max_pieces) {
+    if (passes < 0 || max_pieces < 1) return LBA_E_ARG;
+    int errors = 0;
+    std::atomic<int> in_flight{0};
+    std::vector<std::atomic<int>> runs((size_t)max_pieces);
+    for (int pass = 0; pass < passes; ++pass) {
+        // alternate short and long passes, so a pass with more pieces follows one with fewer
+        const int n = 1 + (int)(((long long)pass * 7919 + (pass & 1) * (max_pieces / 2)) % max_pieces);
+        for (int i = 0; i < n; ++i) runs[i].store(0, std::memory_order_relaxed);
+        par_for(n, [&](int i) {
+            in_flight.fetch_add(1, std::memory_order_acq_rel);
+            runs[i].fetch_add(1, std::memory_order_acq_rel);
+            for (int k = 0; k < (i * 37) % 97; ++k) __builtin_ia32_pause();
+            in_flight.fetch_sub(1, std::memory_order_acq_rel);
+        });
+        if (in_flight.load(std::memory_order_acquire) != 0) ++errors;   // a piece outlived its pass
+        for (int i = 0; i < n; ++i)
+            if (runs[i].load(std::memory_order_acquire) != 1) ++errors;   // missed or run twice
+    }
+    return errors;
+}
 
 int lba_create(lba_problem** out, const lba_config* cfg) {
     if (!out || !cfg) return LBA_E_ARG;

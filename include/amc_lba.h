@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define LBA_ABI_VERSION 4
+#define LBA_ABI_VERSION 5   /* 5: lba_solver_info writes out[8] (was out[5]) */
 
 /* status codes */
 #define LBA_OK              0
@@ -211,7 +211,9 @@ int  lba_set_partition_group(lba_problem* p, lba_group* g, int32_t rank);
  * lba_set_partition, BlockSolver's Schur complement per partition, block_solver.hpp:381-445).  Outputs
  * lm_rank[n_lm], prior_rank[n_priors], vel_rank[n_vel]; panels_out (may be NULL) [3]: panels of the system,
  * panels in the top, columns of the largest subtree; kf_rank (may be NULL) [n_kf]: the rank whose subtree holds
- * the keyframe (-1: the top, or fixed). */
+ * the keyframe (-1: the top, or fixed).  Cameras are not an input: a partitioned lba_set_problem rejects free
+ * extrinsics (lba_cam.ext_free, LBA_E_LIMIT) before it plans, so the pattern planned here (keyframe blocks only)
+ * is the one every partitioned set-up factors. */
 int lba_partition_assign(const lba_config* cfg, const lba_kf* kfs, int32_t n_kf, int32_t n_lm, const lba_obs* obs,
                          int32_t n_obs, const lba_prior* priors, int32_t n_priors, const int32_t* vel_kfs, int32_t n_vel,
                          int32_t nranks, int32_t* lm_rank, int32_t* prior_rank, int32_t* vel_rank, int32_t* panels_out,
@@ -291,6 +293,10 @@ int lba_setup_host_profile(const lba_config* cfg, const lba_kf* kfs, int32_t n_k
                            const lba_obs* obs, int32_t n_obs, const lba_prior* priors, int32_t n_priors,
                            const int32_t* vel_kfs, int32_t n_vel, const lba_cam* cams, int32_t n_cam,
                            double phase_ms[3], int32_t counts[5]);
+/* Diagnostics: `passes` back-to-back parallel passes of lba_set_problem's host thread pool, of 1..max_pieces
+ * pieces each (short and long passes alternating); returns the number of pieces that did not run exactly once
+ * in their own pass or were still running when their pass returned (0 when the pool is sound).  No device. */
+int lba_debug_pool_stress(int32_t passes, int32_t max_pieces);
 /* How the reduced camera system is solved (after lba_set_problem), at the granularity of panels of
  * CHOL_NB = 32 rows: out[0] panels of the loop-closure tail (rows that reach back to the first panels,
  * ordered last), out[1] panels, out[2] stored 32 x 32 tiles of the factor L (fill-in included), out[3] 1

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(L, n), n
         assert re.search(rf"\bT {n}\b", exported), n
     assert set(amc_lba.exported_symbols()) <= set(declared_functions())
-    assert L.lba_abi_version() == 4
+    assert L.lba_abi_version() == 5
 
 
 def _c_sizeof(struct):
@@ -109,3 +109,22 @@ def test_set_problem_host_layout_independent_of_threads():
     assert one == eight
     n_lm, n_pb, np_, tiles, _ = (int(x) for x in one)
     assert n_lm == 20000 and n_pb == 50 and np_ == 600 and 900 < tiles < 1200
+
+
+def _pool_stress(threads, passes, pieces):
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, 'amc-slam_amd'); import amc_lba; "
+            f"print(amc_lba.lib().lba_debug_pool_stress({passes}, {pieces}))")
+    env = dict(os.environ, LBA_SETUP_THREADS=str(threads))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True,
+                         cwd=ROOT)
+    return int(out.stdout.split()[-1])
+
+
+@pytest.mark.parametrize("threads", [2, 8])
+def test_setup_pool_back_to_back_passes(threads):
+    """lba_set_problem's host thread pool (SetupPool): many short passes back to back, each with a different
+    piece count (a pass with more pieces right after one with fewer is where a late worker of the old pass
+    could claim a piece of the new one): every piece runs exactly once, inside its own pass."""
+    assert _pool_stress(threads, 20000, 64) == 0
