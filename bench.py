@@ -14,6 +14,11 @@ With N > 1 every rank optimises its own window (window farming, BASELINE config 
 cut from one trajectory so neighbouring windows share keyframes and landmarks, and at every
 window boundary (each --window-iters iterations) the owners of shared landmarks publish their
 estimates with one all_gather over RCCL (xGMI).  value = iterations of all ranks / max-rank time.
+
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment launches the N rank
+processes itself (torch.distributed.run as a child process, before anything touches the GPU) and
+exits with its status; rank 0's line is the job's line.  Under a launcher, WORLD_SIZE must equal
+--gpus.  --dry-launch prints the launch (command and rank environment) and exits.
 """
 import argparse
 import glob
@@ -31,13 +36,54 @@ sys.path.insert(0, os.path.join(ROOT, "amc-slam_amd"))
 METRIC = "local-BA iterations/sec (50 KF, 20k landmarks, 120k obs) at 1/2/4/8 MI355X"
 
 
-def metric_for(config, W, gba):
-    """BASELINE.json's metric string for its own configuration (configs[1]); the same form for the others."""
+def metric_for(config, W):
+    """BASELINE.json's metric string for its own configuration (configs[1]); the same form for the others
+    (global BA for the global-BA shapes, configs[2] and configs[4])."""
     if config == "cfg1_local_50kf":
         return METRIC
+    from amc_lba.synth import CONFIGS
+    glob = bool(CONFIGS.get(config, {}).get("global_ba"))
     n_kf = int((W.kfs["fixed"] == 0).sum())
-    return (f"{'global' if gba else 'local'}-BA iterations/sec ({n_kf} KF, {len(W.lm) // 1000}k landmarks, "
+    return (f"{'global' if glob else 'local'}-BA iterations/sec ({n_kf} KF, {len(W.lm) // 1000}k landmarks, "
             f"{len(W.obs) // 1000}k obs) at 1/2/4/8 MI355X")
+
+
+def s8d_sweep_bytes(win):
+    """SURVEY.md §8(d)'s B_sweep exactly as the survey defines it: 72 B per observation + 288 B per unique
+    (KF, landmark) Hpl block + 96 B per landmark + 2 x (1152 B per KF pair + 96 B per KF).  The kernel no
+    longer writes the Hpl blocks (they stay in LDS), but this is the figure the north-star's HBM target is
+    quoted on, so it is reported as such (roofline_s8d)."""
+    n_obs = len(win.obs)
+    n_lm = len(np.unique(win.obs["lm"]))
+    n_kf = int((win.kfs["fixed"] == 0).sum())
+    return 72 * n_obs + 288 * int(win.n_pairs) + 96 * n_lm + 2 * (1152 * max(n_kf - 1, 0) + 96 * n_kf)
+
+
+def launch_ranks(args, argv):
+    """--gpus N > 1 without a launcher: run the N ranks as a child torch.distributed.run (one process per
+    GPU, RCCL over xGMI, rendezvous on 127.0.0.1) and return its exit status; None when this process is
+    the (only) rank.  Nothing here touches the GPU, so the children own the devices."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            print(f"bench.py: WORLD_SIZE={ws} but --gpus {args.gpus}", file=sys.stderr)
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    import socket
+    with socket.socket() as sk:   # a free rendezvous port
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + \
+        [a for a in argv if a != "--dry-launch"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    if args.dry_launch:
+        print(json.dumps({"launch": cmd, "nproc": args.gpus, "master_addr": "127.0.0.1", "master_port": port,
+                          "env": {"HSA_ENABLE_IPC_MODE_LEGACY": env["HSA_ENABLE_IPC_MODE_LEGACY"]}}), flush=True)
+        return 0
+    return subprocess.run(cmd, env=env).returncode
 
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
@@ -193,7 +239,16 @@ def main():
                     help="config 4 over N ranks: distributed factorisation (default) or the replicated solve")
     ap.add_argument("--solve", choices=("auto", "band", "dense"), default="auto",
                     help="reduced-system solve: L^-1 tiles (dense) or substitution (band); auto picks by size")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="with --gpus N > 1 and no launcher: print the rank launch and exit (no GPU)")
     args = ap.parse_args()
+    rc = launch_ranks(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
+    if os.environ.get("_BENCH_RANK_PROBE"):   # (tests: a launched rank reports its environment, no GPU)
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                          "HSA_ENABLE_IPC_MODE_LEGACY")}), flush=True)
+        return
 
     import torch
     import torch.distributed as dist
@@ -297,6 +352,53 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
+    # the data-path collectives, measured after the timed region (untimed): the farm's window-boundary
+    # exchange (pack, in-place ncclAllGather, unpack on the window's stream) and, for the distributed global-BA
+    # factorisation, an RCCL all-reduce of the per-trial size over the same ranks
+    comm = None
+    if world > 1 and ex is not None:
+        cnt = torch.tensor([float(ex.counts[0]), float(ex.counts[1])], device="cuda")
+        allc = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.all_gather(allc, cnt)
+        kcap = int(max(c[0].item() for c in allc))
+        lcap = int(max(c[1].item() for c in allc))
+        stride_b = (13 * kcap + 3 * lcap) * 8
+        reps = 20
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = time.perf_counter()
+        for _ in range(reps):
+            ex.exchange()
+        torch.cuda.synchronize()
+        te = torch.tensor([(time.perf_counter() - t) / reps], device="cuda")
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        comm = {"kind": "window-boundary exchange (k_farm_pack, in-place ncclAllGather, k_farm_unpack)",
+                "bytes_per_rank": stride_b, "bytes_gathered": stride_b * world,
+                "us_per_boundary": float(te.item()) * 1e6, "boundaries_timed": (done + args.window_iters - 1) //
+                args.window_iters, "published": {"kf": ex.counts[0], "lm": ex.counts[1]},
+                "received": {"kf": ex.counts[2], "lm": ex.counts[3]}}
+    elif world > 1 and gba:
+        si = prob.split_info()
+        nb = int(si["allreduce_bytes"])
+        buf = torch.ones(max(nb // 8, 1), dtype=torch.float64, device="cuda")
+        reps = 20
+        for _ in range(3):
+            dist.all_reduce(buf)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(reps):
+            dist.all_reduce(buf)
+        torch.cuda.synchronize()
+        te = torch.tensor([(time.perf_counter() - t) / reps], device="cuda")
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        comm = {"kind": ("per-trial all-reduce of the top separators' tiles + bS + b_p" if args.gba_solve == "split"
+                         else "per-trial all-reduce of every tile of S + bS + b_p"),
+                "bytes_per_trial": nb, "replicated_bytes_per_trial": int(si["replicated_allreduce_bytes"]),
+                "us_per_trial": float(te.item()) * 1e6,
+                "timing": "torch.distributed all_reduce (RCCL) of the same byte count over the same ranks, after the "
+                          "timed region",
+                "rank_flops_share": si["rank_flops"] / max(si["system_flops"], 1.0)}
+
     phase, set_problem_ms = None, None
     if world == 1:
         # phase breakdown from a separate, untimed run with every phase evented
@@ -331,6 +433,7 @@ def main():
         k_ms = ms_k / max(n_k, 1)
         B_schur, F_schur = schur_terms(win)
         B = sweep_bytes(win) + B_schur
+        B_s8d = s8d_sweep_bytes(win)
         F = sweep_flops(win) + F_schur
         s_ms = ms_s / max(n_s, 1)
         npose = 12 * int((win.kfs["fixed"] == 0).sum())
@@ -347,7 +450,7 @@ def main():
         workload = f"{args.config}: {win.name or args.config} synthetic window"
         traffic, traffic_src = pmc_traffic(args.config)
         line = {
-            "metric": metric_for(args.config, W, gba),
+            "metric": metric_for(args.config, W),
             "value": value,
             "unit": "LM iterations/s",
             "n_gpus": world,
@@ -376,6 +479,12 @@ def main():
                          "bytes_per_launch": B, "intensity_flop_per_byte": F / B,
                          "avg_launch_ms": k_ms, "timed_launches": n_k,
                          "note": "fp64 (VALU FMAs and v_mfma_f64) against the 78.6 TF fp64 peak"},
+            # SURVEY.md §8(d)'s figure, the one the north-star's >= 70 % HBM target is quoted on
+            "roofline_s8d": {"kernel": "k_lin_schur", "bound": "hbm", "bytes_per_launch": B_s8d,
+                             "achieved": B_s8d / (k_ms * 1e-3) / 1e9 if n_k else None, "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": (B_s8d / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if n_k else None,
+                             "note": "72 n_obs + 288 n_pairs + 96 n_lm + 2 (1152 n_kfpairs + 96 n_kf) over the live "
+                                     "average k_lin_schur launch"},
             "roofline_hbm": {"kernel": "k_lin_schur", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                              "bytes_per_launch": B, "traffic": traffic, "traffic_source": traffic_src},
@@ -388,6 +497,8 @@ def main():
             "trials_per_step": trials / max(done, 1),
             "phases_ms_per_step": phase,
         }
+        if comm is not None:
+            line["collective"] = comm
         if world == 1 and not gba:   # LocalGPBA-equivalent calls (optimize(window_iters))
             calls = {"optimize_calls_per_s": value / args.window_iters, "set_problem_ms": set_problem_ms}
             if set_problem_ms is not None:
