@@ -92,6 +92,7 @@ def lib():
         L.lba_solver_info.argtypes = [vp, _ip]
         if hasattr(L, "lba_debug_pool_stress"):
             L.lba_debug_pool_stress.argtypes = [ctypes.c_int32, ctypes.c_int32]
+            L.lba_debug_lie.argtypes = [ctypes.c_int32, ctypes.c_int32, _dp, _dp]
         if hasattr(L, "lba_solver_flops"):   # (absent from builds before it: A/B runs of older libraries)
             L.lba_solver_flops.argtypes = [vp, _dp]
         L.lba_device_bytes.argtypes = [vp]
@@ -116,7 +117,7 @@ def exported_symbols():
             "lba_pose_dim", "lba_set_partition", "lba_rccl_unique_id", "lba_set_partition_rccl", "lba_group_create",
             "lba_group_destroy", "lba_set_partition_group", "lba_get_cams", "lba_set_farm", "lba_set_farm_rccl",
             "lba_set_farm_group", "lba_farm_plan", "lba_farm_exchange", "lba_farm_match", "lba_solver_info", "lba_solver_flops", "lba_device_bytes",
-            "lba_setup_host_profile", "lba_debug_pool_stress", "lba_partition_assign", "lba_kf_owner", "lba_split_info"]
+            "lba_setup_host_profile", "lba_debug_pool_stress", "lba_debug_lie", "lba_partition_assign", "lba_kf_owner", "lba_split_info"]
 
 
 def setup_host_profile(win, **cfg_over):
@@ -139,6 +140,24 @@ def setup_host_profile(win, **cfg_over):
     if rc != 0:
         raise LbaError(rc, "lba_setup_host_profile failed")
     return ms, cnt
+
+
+def debug_lie(xi, q=None, t=None, device=0):
+    """lba_debug_lie: the kernels' se3 exp / log and right Jacobians (and inverse) evaluated on the GPU.  xi: (n, 6)
+    tangents, (q, t): (n, 4) / (n, 3) poses to take the log of (default: exp(xi) is not needed, identity).
+    Returns dict(q, t, log, Jr, Jr_inv)."""
+    xi = np.atleast_2d(np.asarray(xi, dtype=np.float64))
+    n = len(xi)
+    inp = np.zeros((n, 13))
+    inp[:, :6] = xi
+    inp[:, 6:10] = [0, 0, 0, 1] if q is None else np.atleast_2d(q)
+    inp[:, 10:13] = 0 if t is None else np.atleast_2d(t)
+    out = np.zeros((n, 85))
+    rc = lib().lba_debug_lie(device, n, _d(np.ascontiguousarray(inp)), _d(out))
+    if rc != 0:
+        raise LbaError(rc, "lba_debug_lie failed")
+    return {"q": out[:, 0:4], "t": out[:, 4:7], "log": out[:, 7:13], "Jr": out[:, 13:49].reshape(n, 6, 6),
+            "Jr_inv": out[:, 49:85].reshape(n, 6, 6)}
 
 
 def partition_assign(win, nranks, kf=False, **cfg_over):
@@ -362,9 +381,11 @@ class Problem:
         self._check(lib().lba_trial_chi2(self.h, _d(c2)))
         return c2
 
-    def linearize(self):
+    def linearize(self, dense=True):
+        """(residuals, H_pp dense, b, H_ll); dense=False: no H_pp (None), for pose systems whose dense H_pp
+        would not fit (config 4)."""
         np_ = self.pose_dim
-        H = np.zeros((np_, np_))
+        H = np.zeros((np_, np_)) if dense else None
         b = np.zeros(np_ + self.lm_dim)
         Hll = np.zeros((self.n_lm, 9))
         res = np.zeros((self.n_obs, 3))

@@ -175,7 +175,7 @@ class Window:
 
 def make_window(n_opt_kf=50, n_fixed=1, n_lm=20000, obs_per_lm=6, n_cam=4, gp=True, stereo_frac=0.5,
                 outlier_frac=0.05, seed=20250912, global_ba=False, perturb=True, t0=100.0, name="",
-                track=None, max_track=40, band=25, loop=False):
+                track=None, max_track=40, band=25, loop=False, straight=False):
     """Build one window.  n_fixed KFs come first (oldest); global_ba=True gives the
     BundleAdjustment graph shape (priors from the first KF, Huber 21.026 on priors, lambda0
     1e-5, src/Optimizer.cc:61-321).  Landmarks are seen from a band of `band` KFs around their
@@ -185,12 +185,16 @@ def make_window(n_opt_kf=50, n_fixed=1, n_lm=20000, obs_per_lm=6, n_cam=4, gp=Tr
     lap of a circle: the keyframe band around a landmark's anchor wraps around, so the last keyframes
     re-observe the first ones' landmarks (the long-range blocks of a loop-closure global BA); loop=k
     drives k laps, so every place is revisited k - 1 times and a landmark is seen from the keyframes
-    near its place on every lap."""
+    near its place on every lap.  straight=True drives a straight line (no yaw) and perturbs no
+    orientation or angular velocity: consecutive keyframes' relative rotations, the interpolated samples'
+    and the velocities' omega are then zero (below every small-angle threshold of Sophus and Pose3utils)
+    at the first linearisation."""
     rng = np.random.default_rng(seed)
     n_kf = n_fixed + n_opt_kf
     kf_t = t0 + 0.1 * np.arange(n_kf)
     laps = int(loop)
-    traj = _CircleTrajectory(kf_t[0], 0.1 * n_kf / laps) if loop else _Trajectory(kf_t[0] - 0.1, kf_t[-1] + 0.1)
+    traj = (_CircleTrajectory(kf_t[0], 0.1 * n_kf / laps) if loop else
+            _Trajectory(kf_t[0] - 0.1, kf_t[-1] + 0.1, A=0.0 if straight else 0.15))
 
     # --- cameras: reference camera (last) looks forward; others yawed +90, 180, -90 deg
     Rbc0 = np.array([[0.0, 0.0, 1.0], [-1.0, 0.0, 0.0], [0.0, -1.0, 0.0]])
@@ -330,9 +334,14 @@ def make_window(n_opt_kf=50, n_fixed=1, n_lm=20000, obs_per_lm=6, n_cam=4, gp=Tr
         R, p, vel = Rk[i], pk[i].copy(), vk[i].copy()
         fixed = i < n_fixed
         if perturb and not fixed:
-            R = R @ _expso3(rng.normal(0, np.deg2rad(0.5), 3))
+            dR = rng.normal(0, np.deg2rad(0.5), 3)
             p = p + rng.normal(0, 0.05, 3)
-            vel = vel + rng.normal(0, 0.1, 6)
+            dv = rng.normal(0, 0.1, 6)
+            if straight:
+                dv[3:] = 0.0
+            else:
+                R = R @ _expso3(dR)
+            vel = vel + dv
         kfs[i]["q"] = _f32(rot_to_quat(R))
         kfs[i]["t"] = _f32(p)
         kfs[i]["vel"] = _f32(vel)

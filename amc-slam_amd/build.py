@@ -17,7 +17,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "lib", "libamc_lba.so")
-SOURCES = ["lba_kernels.hip", "lba_host.hip", "lba_track.hip"]
+SOURCES = ["lba_kernels.hip", "lba_host.hip", "lba_track.hip", "lba_debug.hip"]
 HEADERS = ["lba_device.hpp", "lba_math.hpp", "lba_plan.hpp", os.path.join("..", "..", "include", "amc_lba.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall"]

@@ -297,6 +297,11 @@ int lba_setup_host_profile(const lba_config* cfg, const lba_kf* kfs, int32_t n_k
  * pieces each (short and long passes alternating); returns the number of pieces that did not run exactly once
  * in their own pass or were still running when their pass returned (0 when the pool is sound).  No device. */
 int lba_debug_pool_stress(int32_t passes, int32_t max_pieces);
+/* Diagnostics: the Lie-group primitives of the kernels (Sophus SE3 exp / log, Thirdparty/Sophus/sophus/se3.hpp:
+ * 223-252,761-781; RightJacobianPose3 / RightJacobianPose3Inv, src/Pose3utils.cc:5-46, small-angle branches
+ * included) evaluated on `device` for n records in[13 n] = {xi[6], q[4] (x,y,z,w), t[3]}: out[85 n] =
+ * {exp(xi) q[4] t[3], log(q, t)[6], Jr(xi)[36], Jr^-1(xi)[36]} (row-major). */
+int lba_debug_lie(int32_t device, int32_t n, const double* in, double* out);
 /* How the reduced camera system is solved (after lba_set_problem), at the granularity of panels of
  * CHOL_NB = 32 rows: out[0] panels of the loop-closure tail (rows that reach back to the first panels,
  * ordered last), out[1] panels, out[2] stored 32 x 32 tiles of the factor L (fill-in included), out[3] 1

@@ -27,6 +27,7 @@
 #ifdef _OPENMP
 #include <omp.h>
 #endif
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -452,11 +453,18 @@ struct orc_problem {
     /* per-edge errors */
     double* obs_err;   /* [n_obs*3] */
     double* obs_rho0;  /* [n_obs] robust chi2 of each observation (summed in order after the parallel pass) */
-    double* obs_J;     /* [n_obs*3*JC] Jacobians of the last build_system (filled in parallel, used in order) */
+    double* obs_J;     /* [JCHUNK*3*JC] Jacobians of a chunk of observations (filled in parallel, used in order) */
     double* pri_err;   /* [n_prior*12] */
     double* vel_err;   /* [n_vel] */
     /* Hessian (BlockSolver, block_solver.hpp) */
-    double* Hpp;       /* dense np x np, upper blocks valid */
+    /* Hpp as g2o's SparseBlockMatrix holds it (sparse_block_matrix.h:40-231): the upper blocks (hi <= hj) of
+     * its structural pattern (every pose block's diagonal, the pose pairs of every edge), pdim[hi] x pdim[hj]
+     * row-major in 144-double slots; block rows hpp_rowptr[hi] .. hpp_rowptr[hi + 1] - 1, columns hpp_col
+     * ascending.  O(blocks), so the normal equations of a 5000-keyframe global BA (np = 59988) fit. */
+    int* hpp_rowptr;
+    int* hpp_col;
+    double* hpp_blk;
+    int hpp_nblk;
     double* Hll;       /* [n_lm_blocks*9] */
     int* hpl_start;    /* per landmark block: range into hpl_pose/hpl_blk */
     int* hpl_pose;     /* pose block index, ascending within a landmark */
@@ -468,6 +476,11 @@ struct orc_problem {
     double lambda, ni;
     int nBad;
 };
+
+static int cmp_int(const void* a, const void* b) {
+    const int x = *(const int*)a, y = *(const int*)b;
+    return (x > y) - (x < y);
+}
 
 static se3 mk_se3(const double* q, const double* t) {
     se3 r;
@@ -538,6 +551,7 @@ static void obs_error(const orc_problem* p, const lba_obs* o, double* e) {
  * J is [dim x JC]: cols 0-11 KF_a, 12-23 KF_b, 24-26 point, 27-32 the camera extrinsic
  * (EdgeMonoGPExtrinsic's _jacobianOplus[3] = -proj_jac [-I, Skew(Xc)], src/G2oTypes.cc:310-313). */
 #define JC 33
+#define JCHUNK 65536   /* observations whose Jacobians are held at once (build_system) */
 static void obs_jacobian(const orc_problem* p, const lba_obs* o, double* J) {
     const cam_t* c = &p->cam[o->cam];
     const double* Xw = p->lm + 3 * o->lm;
@@ -799,37 +813,104 @@ orc_problem* orc_create(const lba_config* cfg, const lba_kf* kfs, int n_kf, cons
     p->nl = 3 * nl;
     p->obs_err = (double*)calloc(3 * (n_obs > 0 ? n_obs : 1), sizeof(double));
     p->obs_rho0 = (double*)calloc(n_obs > 0 ? n_obs : 1, sizeof(double));
-    p->obs_J = (double*)calloc((size_t)3 * 33 * (n_obs > 0 ? n_obs : 1), sizeof(double));
+    p->obs_J = (double*)calloc((size_t)3 * 33 * JCHUNK, sizeof(double));
     p->pri_err = (double*)calloc(12 * (n_priors > 0 ? n_priors : 1), sizeof(double));
     p->vel_err = (double*)calloc((n_vel > 0 ? n_vel : 1), sizeof(double));
-    p->Hpp = (double*)calloc((size_t)p->np * p->np + 1, sizeof(double));
     p->Hll = (double*)calloc(9 * (nl > 0 ? nl : 1), sizeof(double));
-    /* Hpl pattern: one 12x3 block per (pose block, landmark block) pair, rows ascending */
-    p->hpl_start = (int*)calloc(nl + 1, sizeof(int));
-    int* cnt_pairs = (int*)calloc(nl + 1, sizeof(int));
-    char* seen = (char*)calloc((size_t)(np > 0 ? np : 1) * (nl > 0 ? nl : 1), 1);
-    for (int i = 0; i < n_obs; ++i) {
-        int l = p->lm_hidx[obs[i].lm];
-        int ks[2] = {obs[i].kf_b, is_gp(obs[i].kind) ? obs[i].kf_a : -1};
-        for (int s = 0; s < 3; ++s) {
-            int h;
-            if (s == 2) h = obs[i].kind == LBA_MONO_GP ? p->cam[obs[i].cam].hidx : -1;
-            else h = ks[s] < 0 ? -1 : p->kf_hidx[ks[s]];
-            if (h < 0) continue;
-            if (!seen[(size_t)h * nl + l]) { seen[(size_t)h * nl + l] = 1; cnt_pairs[l]++; }
+    /* the pose vertices of every edge (hessian indices, -1 for fixed / absent), for the patterns below */
+#define OBS_POSE_VERTS(o, hs)                                                                   \
+    do {                                                                                        \
+        (hs)[0] = p->kf[(o)->kf_b].fixed ? -1 : p->kf_hidx[(o)->kf_b];                           \
+        (hs)[1] = is_gp((o)->kind) && !p->kf[(o)->kf_a].fixed ? p->kf_hidx[(o)->kf_a] : -1;       \
+        (hs)[2] = (o)->kind == LBA_MONO_GP ? p->cam[(o)->cam].hidx : -1;                         \
+    } while (0)
+    /* Hpp pattern: per block row the partner columns (candidates with duplicates, counted then filled),
+     * each row's list sorted and made unique */
+    {
+        int* cnt = (int*)calloc(np + 1, sizeof(int));
+        for (int pass = 0; pass < 2; ++pass) {
+            int* fill = pass ? (int*)calloc(np + 1, sizeof(int)) : NULL;
+            int* cand = pass ? (int*)malloc(sizeof(int) * (cnt[np] > 0 ? cnt[np] : 1)) : NULL;
+#define HPP_CAND(a, b)                                                                          \
+            do {                                                                                \
+                const int lo_ = (a) < (b) ? (a) : (b), hi_ = (a) < (b) ? (b) : (a);             \
+                if (pass) cand[cnt[lo_] + fill[lo_]++] = hi_; else cnt[lo_ + 1]++;               \
+            } while (0)
+            for (int h = 0; h < np; ++h) HPP_CAND(h, h);
+            for (int i = 0; i < n_priors; ++i) {
+                if (kfs[priors[i].kf_a].fixed && kfs[priors[i].kf_b].fixed) continue;
+                const int a = kfs[priors[i].kf_a].fixed ? -1 : p->kf_hidx[priors[i].kf_a];
+                const int b = kfs[priors[i].kf_b].fixed ? -1 : p->kf_hidx[priors[i].kf_b];
+                if (a >= 0 && b >= 0) HPP_CAND(a, b);
+            }
+            for (int i = 0; i < n_obs; ++i) {
+                int hs[3];
+                OBS_POSE_VERTS(&obs[i], hs);
+                for (int x = 0; x < 3; ++x)
+                    for (int y = x + 1; y < 3; ++y)
+                        if (hs[x] >= 0 && hs[y] >= 0) HPP_CAND(hs[x], hs[y]);
+            }
+#undef HPP_CAND
+            if (!pass) {
+                for (int h = 0; h < np; ++h) cnt[h + 1] += cnt[h];
+                continue;
+            }
+            p->hpp_rowptr = (int*)calloc(np + 1, sizeof(int));
+            int nb = 0;
+            for (int h = 0; h < np; ++h) {
+                int* r = cand + cnt[h];
+                const int m = cnt[h + 1] - cnt[h];
+                qsort(r, m, sizeof(int), cmp_int);
+                int u = 0;
+                for (int k = 0; k < m; ++k)
+                    if (u == 0 || r[u - 1] != r[k]) r[u++] = r[k];
+                nb += u;
+                p->hpp_rowptr[h + 1] = nb;
+                fill[h] = u;
+            }
+            p->hpp_nblk = nb;
+            p->hpp_col = (int*)malloc(sizeof(int) * (nb > 0 ? nb : 1));
+            for (int h = 0; h < np; ++h) memcpy(p->hpp_col + p->hpp_rowptr[h], cand + cnt[h], sizeof(int) * fill[h]);
+            p->hpp_blk = (double*)calloc((size_t)144 * (nb > 0 ? nb : 1), sizeof(double));
+            free(fill);
+            free(cand);
         }
+        free(cnt);
     }
-    for (int l = 0; l < nl; ++l) p->hpl_start[l + 1] = p->hpl_start[l] + cnt_pairs[l];
-    int npairs = p->hpl_start[nl];
-    p->hpl_pose = (int*)malloc(sizeof(int) * (npairs > 0 ? npairs : 1));
-    p->hpl_blk = (double*)calloc(36 * (size_t)(npairs > 0 ? npairs : 1), sizeof(double));
-    for (int l = 0; l < nl; ++l) {
-        int w = p->hpl_start[l];
-        for (int h = 0; h < np; ++h)
-            if (seen[(size_t)h * nl + l]) p->hpl_pose[w++] = h;
+    /* Hpl pattern: one 12x3 block per (pose block, landmark block) pair, pose blocks ascending per landmark
+     * (the observations grouped by landmark, each landmark's pose blocks sorted and made unique) */
+    p->hpl_start = (int*)calloc(nl + 1, sizeof(int));
+    {
+        int* lo_start = (int*)calloc(nl + 1, sizeof(int));
+        for (int i = 0; i < n_obs; ++i) lo_start[p->lm_hidx[obs[i].lm] + 1] += 3;
+        for (int l = 0; l < nl; ++l) lo_start[l + 1] += lo_start[l];
+        int* lfill = (int*)calloc(nl + 1, sizeof(int));
+        int* cand = (int*)malloc(sizeof(int) * (lo_start[nl] > 0 ? lo_start[nl] : 1));
+        for (int i = 0; i < n_obs; ++i) {
+            const int l = p->lm_hidx[obs[i].lm];
+            int hs[3];
+            OBS_POSE_VERTS(&obs[i], hs);
+            for (int x = 0; x < 3; ++x)
+                if (hs[x] >= 0) cand[lo_start[l] + lfill[l]++] = hs[x];
+        }
+        for (int l = 0; l < nl; ++l) {
+            int* r = cand + lo_start[l];
+            qsort(r, lfill[l], sizeof(int), cmp_int);
+            int u = 0;
+            for (int k = 0; k < lfill[l]; ++k)
+                if (u == 0 || r[u - 1] != r[k]) r[u++] = r[k];
+            lfill[l] = u;
+            p->hpl_start[l + 1] = p->hpl_start[l] + u;
+        }
+        int npairs = p->hpl_start[nl];
+        p->hpl_pose = (int*)malloc(sizeof(int) * (npairs > 0 ? npairs : 1));
+        p->hpl_blk = (double*)calloc(36 * (size_t)(npairs > 0 ? npairs : 1), sizeof(double));
+        for (int l = 0; l < nl; ++l) memcpy(p->hpl_pose + p->hpl_start[l], cand + lo_start[l], sizeof(int) * lfill[l]);
+        free(cand);
+        free(lfill);
+        free(lo_start);
     }
-    free(seen);
-    free(cnt_pairs);
+#undef OBS_POSE_VERTS
     p->b = (double*)calloc(p->np + p->nl + 1, sizeof(double));
     p->x = (double*)calloc(p->np + p->nl + 1, sizeof(double));
     p->diag_bak = (double*)calloc(p->np + p->nl + 1, sizeof(double));
@@ -842,7 +923,7 @@ void orc_destroy(orc_problem* p) {
     if (!p) return;
     free(p->kf); free(p->kf_bak); free(p->lm); free(p->lm_bak); free(p->obs); free(p->pri); free(p->vel);
     free(p->cam); free(p->cam_bak); free(p->poff); free(p->pdim); free(p->kf_hidx); free(p->lm_hidx); free(p->obs_err); free(p->obs_rho0); free(p->obs_J); free(p->pri_err); free(p->vel_err);
-    free(p->Hpp); free(p->Hll); free(p->hpl_start); free(p->hpl_pose); free(p->hpl_blk); free(p->b); free(p->x);
+    free(p->hpp_rowptr); free(p->hpp_col); free(p->hpp_blk); free(p->Hll); free(p->hpl_start); free(p->hpl_pose); free(p->hpl_blk); free(p->b); free(p->x);
     free(p->diag_bak);
     free(p);
 }
@@ -926,17 +1007,47 @@ void orc_last_obs_chi2(const orc_problem* p, double* obs_chi2) {
 }
 
 /* ------------------------------------------------------------------ buildSystem */
-/* add an (i,j) pose-pose block contribution (pdim[i] x pdim[j], row-major) into the upper triangle of
- * dense Hpp */
-static void hpp_add(orc_problem* p, int hi, int hj, const double* blk) {
-    const int n = p->np, di = p->pdim[hi], dj = p->pdim[hj], oi = p->poff[hi], oj = p->poff[hj];
-    if (hi <= hj) {
-        for (int r = 0; r < di; ++r)
-            for (int c = 0; c < dj; ++c) p->Hpp[(size_t)(oi + r) * n + oj + c] += blk[r * dj + c];
-    } else {   /* transposed block (hessianRowMajor) */
-        for (int r = 0; r < di; ++r)
-            for (int c = 0; c < dj; ++c) p->Hpp[(size_t)(oj + c) * n + oi + r] += blk[r * dj + c];
+/* the stored upper block (hi <= hj) of Hpp: pdim[hi] x pdim[hj], row-major */
+static double* hpp_block(const orc_problem* p, int hi, int hj) {
+    int a = p->hpp_rowptr[hi], b = p->hpp_rowptr[hi + 1];
+    while (a < b) {
+        const int m = (a + b) >> 1;
+        if (p->hpp_col[m] < hj) a = m + 1;
+        else b = m;
     }
+    if (a == p->hpp_rowptr[hi + 1] || p->hpp_col[a] != hj) {
+        fprintf(stderr, "oracle: Hpp block (%d, %d) outside the pattern\n", hi, hj);
+        abort();
+    }
+    return p->hpp_blk + (size_t)144 * a;
+}
+/* add an (i,j) pose-pose block contribution (pdim[i] x pdim[j], row-major) into the upper triangle of Hpp */
+static void hpp_add(orc_problem* p, int hi, int hj, const double* blk) {
+    const int di = p->pdim[hi], dj = p->pdim[hj];
+    if (hi <= hj) {
+        double* B = hpp_block(p, hi, hj);
+        for (int r = 0; r < di; ++r)
+            for (int c = 0; c < dj; ++c) B[r * dj + c] += blk[r * dj + c];
+    } else {   /* transposed block (hessianRowMajor) */
+        double* B = hpp_block(p, hj, hi);
+        for (int r = 0; r < di; ++r)
+            for (int c = 0; c < dj; ++c) B[c * di + r] += blk[r * dj + c];
+    }
+}
+/* element (i, i) of Hpp */
+static double* hpp_diag(const orc_problem* p, int h, int r) {
+    return hpp_block(p, h, h) + r * p->pdim[h] + r;
+}
+/* the upper blocks of Hpp into a dense n x n (upper block triangle, the lower part untouched) */
+static void hpp_dense_upper(const orc_problem* p, double* H) {
+    const size_t n = (size_t)p->np;
+    for (int hi = 0; hi < p->n_pose_blocks; ++hi)
+        for (int k = p->hpp_rowptr[hi]; k < p->hpp_rowptr[hi + 1]; ++k) {
+            const int hj = p->hpp_col[k], di = p->pdim[hi], dj = p->pdim[hj];
+            const double* B = p->hpp_blk + (size_t)144 * k;
+            for (int r = 0; r < di; ++r)
+                for (int c = 0; c < dj; ++c) H[(p->poff[hi] + r) * n + p->poff[hj] + c] = B[r * dj + c];
+        }
 }
 static double* hpl_block(orc_problem* p, int hp, int hl) {
     for (int k = p->hpl_start[hl]; k < p->hpl_start[hl + 1]; ++k)
@@ -945,8 +1056,7 @@ static double* hpl_block(orc_problem* p, int hp, int hl) {
 }
 
 static void build_system(orc_problem* p) {
-    int n = p->np;
-    memset(p->Hpp, 0, sizeof(double) * (size_t)n * n);
+    memset(p->hpp_blk, 0, sizeof(double) * 144 * (size_t)p->hpp_nblk);
     memset(p->Hll, 0, sizeof(double) * 9 * p->n_lm_blocks);
     memset(p->hpl_blk, 0, sizeof(double) * 36 * p->hpl_start[p->n_lm_blocks]);
     memset(p->b, 0, sizeof(double) * (p->np + p->nl));
@@ -960,7 +1070,7 @@ static void build_system(orc_problem* p) {
         double e = p->vel_err[i];
         /* J = [0_{1x6}, A], A = e_2 -> only column 8 */
         p->b[p->poff[h] + 8] -= om * e;
-        p->Hpp[(size_t)(p->poff[h] + 8) * n + p->poff[h] + 8] += om;
+        *hpp_diag(p, h, 8) += om;
     }
     for (int i = 0; i < p->n_prior; ++i) {   /* BaseBinaryEdge::constructQuadraticForm (base_binary_edge.hpp:54-120) */
         const lba_prior* e = &p->pri[i];
@@ -1016,15 +1126,18 @@ static void build_system(orc_problem* p) {
     }
     /* the observations' Jacobians in parallel (the OpenMP build: g2o's linearizeOplus over the active
      * edges, block_solver.hpp:378-380), then accumulated in edge order (bitwise the serial build's) */
+    for (int c0 = 0; c0 < p->n_obs; c0 += JCHUNK) {   /* (chunks: the Jacobians of all 6M observations of
+                                                         * config 4 would take 4.7 GB) */
+    const int c1 = p->n_obs - c0 < JCHUNK ? p->n_obs : c0 + JCHUNK;
 #ifdef _OPENMP
 #pragma omp parallel for schedule(static)
 #endif
-    for (int i = 0; i < p->n_obs; ++i) obs_jacobian(p, &p->obs[i], p->obs_J + (size_t)3 * JC * i);
-    for (int i = 0; i < p->n_obs; ++i) {
+    for (int i = c0; i < c1; ++i) obs_jacobian(p, &p->obs[i], p->obs_J + (size_t)3 * JC * (i - c0));
+    for (int i = c0; i < c1; ++i) {
         const lba_obs* o = &p->obs[i];
         int dim = obs_dim(o->kind);
         const double* e = p->obs_err + 3 * i;
-        const double* J = p->obs_J + (size_t)3 * JC * i;
+        const double* J = p->obs_J + (size_t)3 * JC * (i - c0);
         huber(chi2_of(e, dim, o->w), obs_delta(p, o->kind), rho);
         double s = rho[1] * o->w;                    /* robustInformation = rho' * Omega */
         double om_r[3];
@@ -1087,6 +1200,7 @@ static void build_system(orc_problem* p) {
             }
         }
     }
+    }
 }
 
 static void mirror_upper(double* H, int n) {
@@ -1098,7 +1212,8 @@ int orc_build_system(orc_problem* p, double* H_pp, double* b, double* H_ll) {
     compute_errors(p);
     build_system(p);
     if (H_pp) {
-        memcpy(H_pp, p->Hpp, sizeof(double) * (size_t)p->np * p->np);
+        memset(H_pp, 0, sizeof(double) * (size_t)p->np * p->np);
+        hpp_dense_upper(p, H_pp);
         mirror_upper(H_pp, p->np);
     }
     if (b) memcpy(b, p->b, sizeof(double) * (p->np + p->nl));
@@ -1181,13 +1296,19 @@ int orc_ldlt_solve(int n, const double* A, const double* b, double* x) {
 /* ------------------------------------------------------------------ BlockSolver::solve */
 static void set_lambda(orc_problem* p, double lambda) {   /* block_solver.hpp:564-589 */
     int n = p->np;
-    for (int i = 0; i < n; ++i) { p->diag_bak[i] = p->Hpp[(size_t)i * n + i]; p->Hpp[(size_t)i * n + i] += lambda; }
+    for (int h = 0; h < p->n_pose_blocks; ++h)
+        for (int r = 0; r < p->pdim[h]; ++r) {
+            double* d = hpp_diag(p, h, r);
+            p->diag_bak[p->poff[h] + r] = *d;
+            *d += lambda;
+        }
     for (int l = 0; l < p->n_lm_blocks; ++l)
         for (int d = 0; d < 3; ++d) { p->diag_bak[n + 3 * l + d] = p->Hll[9 * l + 4 * d]; p->Hll[9 * l + 4 * d] += lambda; }
 }
 static void restore_diagonal(orc_problem* p) {   /* block_solver.hpp:592-604 */
     int n = p->np;
-    for (int i = 0; i < n; ++i) p->Hpp[(size_t)i * n + i] = p->diag_bak[i];
+    for (int h = 0; h < p->n_pose_blocks; ++h)
+        for (int r = 0; r < p->pdim[h]; ++r) *hpp_diag(p, h, r) = p->diag_bak[p->poff[h] + r];
     for (int l = 0; l < p->n_lm_blocks; ++l)
         for (int d = 0; d < 3; ++d) p->Hll[9 * l + 4 * d] = p->diag_bak[n + 3 * l + d];
 }
@@ -1198,7 +1319,8 @@ static int block_solve(orc_problem* p) {
     double* coeff = (double*)calloc(n + 1, sizeof(double));
     double* Dinv = (double*)malloc(sizeof(double) * 9 * (nlb > 0 ? nlb : 1));
     double* dbl = (double*)malloc(sizeof(double) * 3 * (nlb > 0 ? nlb : 1));
-    memcpy(S, p->Hpp, sizeof(double) * (size_t)n * n);   /* Hschur = Hpp (upper blocks used) */
+    memset(S, 0, sizeof(double) * (size_t)n * n);
+    hpp_dense_upper(p, S);   /* Hschur = Hpp (upper blocks used) */
     /* (the OpenMP build: landmark inverses in parallel; the Schur complement with every pose block row
      * owned by one thread that walks the landmarks in order, so each entry of S and coeff receives its
      * terms in the serial order: bitwise the serial build's; block_solver.hpp:381-432,527) */
@@ -1288,13 +1410,19 @@ int orc_solve(orc_problem* p, double lambda, double* dx) {
 void orc_normal_residual(const orc_problem* p, double lambda, const double* dx, double* r) {
     const int n = p->np, nlb = p->n_lm_blocks;
     for (int i = 0; i < n + p->nl; ++i) r[i] = -p->b[i];
-    for (int i = 0; i < n; ++i) {
-        const double* Hi = p->Hpp + (size_t)i * n;
-        double acc = (Hi[i] + lambda) * dx[i];
-        for (int j = i + 1; j < n; ++j)
-            if (Hi[j] != 0.0) { acc += Hi[j] * dx[j]; r[j] += Hi[j] * dx[i]; }
-        r[i] += acc;
-    }
+    for (int hi = 0; hi < p->n_pose_blocks; ++hi)
+        for (int k = p->hpp_rowptr[hi]; k < p->hpp_rowptr[hi + 1]; ++k) {
+            const int hj = p->hpp_col[k], di = p->pdim[hi], dj = p->pdim[hj], oi = p->poff[hi], oj = p->poff[hj];
+            const double* B = p->hpp_blk + (size_t)144 * k;
+            for (int a = 0; a < di; ++a)
+                for (int c = 0; c < dj; ++c) {
+                    const double v = B[a * dj + c];
+                    if (hi == hj && c < a) continue;        /* a diagonal block's upper triangle */
+                    if (hi == hj && c == a) { r[oi + a] += (v + lambda) * dx[oi + a]; continue; }
+                    r[oi + a] += v * dx[oj + c];
+                    r[oj + c] += v * dx[oi + a];
+                }
+        }
     for (int l = 0; l < nlb; ++l) {
         const double* xl = dx + n + 3 * l;
         double* rl = r + n + 3 * l;
@@ -1347,7 +1475,8 @@ static void apply_update(orc_problem* p, const double* x) {
 static double compute_lambda_init(const orc_problem* p) {   /* levenberg.cpp:171-185 */
     if (p->cfg.lambda_init > 0) return p->cfg.lambda_init;
     double m = 0.0;
-    for (int i = 0; i < p->np; ++i) m = fmax(m, fabs(p->Hpp[(size_t)i * p->np + i]));
+    for (int h = 0; h < p->n_pose_blocks; ++h)
+        for (int r = 0; r < p->pdim[h]; ++r) m = fmax(m, fabs(*hpp_diag(p, h, r)));
     for (int l = 0; l < p->n_lm_blocks; ++l)
         for (int d = 0; d < 3; ++d) m = fmax(m, fabs(p->Hll[9 * l + 4 * d]));
     return p->cfg.tau * m;

@@ -28,38 +28,50 @@ def build(force=False):
 
 
 _lib = None
+_lib_omp = None
+LIB_OMP = os.path.join(HERE, "_build", "liblba_oracle_omp.so")
 
 
-def lib():
-    global _lib
+def lib(omp=False):
+    """The oracle library; omp=True: its OpenMP build (bitwise the serial build's results, the per-edge passes
+    on OMP_NUM_THREADS threads), loaded beside it for the full-size checks."""
+    global _lib, _lib_omp
+    if omp:
+        if _lib_omp is None:
+            build()
+            _lib_omp = _bind(ctypes.CDLL(LIB_OMP))
+        return _lib_omp
     if _lib is None:
         build()
-        L = ctypes.CDLL(LIB)
-        L.orc_create.restype = ctypes.c_void_p
-        L.orc_create.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p, ctypes.c_int] * 6
-        L.orc_destroy.argtypes = [ctypes.c_void_p]
-        L.orc_pose_dim.argtypes = [ctypes.c_void_p]
-        L.orc_lm_dim.argtypes = [ctypes.c_void_p]
-        L.orc_compute_errors.restype = ctypes.c_double
-        L.orc_compute_errors.argtypes = [ctypes.c_void_p, _dp, _dp]
-        L.orc_build_system.argtypes = [ctypes.c_void_p, _dp, _dp, _dp]
-        L.orc_solve.argtypes = [ctypes.c_void_p, ctypes.c_double, _dp]
-        L.orc_normal_residual.argtypes = [ctypes.c_void_p, ctypes.c_double, _dp, _dp]
-        L.orc_normal_residual.restype = None
-        L.orc_optimize.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(LbaStats)]
-        L.orc_get_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _dp]
-        L.orc_get_cams.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-        L.orc_depth_ok.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-        L.orc_last_obs_chi2.argtypes = [ctypes.c_void_p, _dp]
-        L.orc_last_obs_chi2.restype = None
-        L.orc_obs_linearize.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp]
-        L.orc_prior_linearize.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp, _dp]
-        for n in ("orc_se3_exp", "orc_se3_log", "orc_so3_exp", "orc_so3_log", "orc_right_jac_pose3",
-                  "orc_right_jac_pose3_inv", "orc_left_jac_pose3_q", "orc_gp_query_pose"):
-            getattr(L, n).restype = None
-        L.orc_ldlt_solve.argtypes = [ctypes.c_int, _dp, _dp, _dp]
-        _lib = L
+        _lib = _bind(ctypes.CDLL(LIB))
     return _lib
+
+
+def _bind(L):
+    L.orc_create.restype = ctypes.c_void_p
+    L.orc_create.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p, ctypes.c_int] * 6
+    L.orc_destroy.argtypes = [ctypes.c_void_p]
+    L.orc_pose_dim.argtypes = [ctypes.c_void_p]
+    L.orc_lm_dim.argtypes = [ctypes.c_void_p]
+    L.orc_compute_errors.restype = ctypes.c_double
+    L.orc_compute_errors.argtypes = [ctypes.c_void_p, _dp, _dp]
+    L.orc_build_system.argtypes = [ctypes.c_void_p, _dp, _dp, _dp]
+    L.orc_solve.argtypes = [ctypes.c_void_p, ctypes.c_double, _dp]
+    L.orc_normal_residual.argtypes = [ctypes.c_void_p, ctypes.c_double, _dp, _dp]
+    L.orc_normal_residual.restype = None
+    L.orc_optimize.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(LbaStats)]
+    L.orc_get_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _dp]
+    L.orc_get_cams.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    L.orc_depth_ok.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    L.orc_last_obs_chi2.argtypes = [ctypes.c_void_p, _dp]
+    L.orc_last_obs_chi2.restype = None
+    L.orc_obs_linearize.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp]
+    L.orc_prior_linearize.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp, _dp]
+    for n in ("orc_se3_exp", "orc_se3_log", "orc_so3_exp", "orc_so3_log", "orc_right_jac_pose3",
+              "orc_right_jac_pose3_inv", "orc_left_jac_pose3_q", "orc_gp_query_pose"):
+        getattr(L, n).restype = None
+    L.orc_ldlt_solve.argtypes = [ctypes.c_int, _dp, _dp, _dp]
+    return L
 
 
 def _d(a):
@@ -69,8 +81,9 @@ def _d(a):
 class Oracle:
     """g2o-semantics CPU restatement of LocalGPBA's optimisation on one window."""
 
-    def __init__(self, win, cfg=None, **cfg_over):
-        L = lib()
+    def __init__(self, win, cfg=None, omp=False, **cfg_over):
+        self._omp = omp
+        L = self._L = lib(omp)
         if cfg is None:
             kw = dict(win.cfg)
             kw.update(cfg_over)
@@ -87,82 +100,84 @@ class Oracle:
 
     def __del__(self):
         if getattr(self, "h", None):
-            lib().orc_destroy(self.h)
+            self._L.orc_destroy(self.h)
             self.h = None
 
     @property
     def pose_dim(self):
-        return lib().orc_pose_dim(self.h)
+        return self._L.orc_pose_dim(self.h)
 
     @property
     def lm_dim(self):
-        return lib().orc_lm_dim(self.h)
+        return self._L.orc_lm_dim(self.h)
 
     def errors(self):
         res = np.zeros((self.n_obs, 3))
         c2 = np.zeros(self.n_obs)
-        chi = lib().orc_compute_errors(self.h, _d(res), _d(c2))
+        chi = self._L.orc_compute_errors(self.h, _d(res), _d(c2))
         return chi, res, c2
 
-    def build_system(self):
+    def build_system(self, dense=True):
+        """(H_pp dense, b, H_ll); dense=False: H_pp only as the oracle's blocks (None returned), for systems
+        whose dense H_pp would not fit (config 4: 59988^2)."""
         np_ = self.pose_dim
-        H = np.zeros((np_, np_))
+        H = np.zeros((np_, np_)) if dense else None
         b = np.zeros(np_ + self.lm_dim)
         Hll = np.zeros((self.n_lm, 9))
-        lib().orc_build_system(self.h, _d(H), _d(b), _d(Hll))
+        self._L.orc_build_system(self.h, _d(H) if dense else None, _d(b), _d(Hll))
         return H, b, Hll
 
     def solve(self, lam):
         dx = np.zeros(self.pose_dim + self.lm_dim)
-        ok = lib().orc_solve(self.h, lam, _d(dx))
+        ok = self._L.orc_solve(self.h, lam, _d(dx))
         return bool(ok), dx
 
     def normal_residual(self, lam, dx):
         """(H + lam I) dx - b on the last build_system (size-independent step check)."""
         dx = np.ascontiguousarray(dx, float)
         r = np.zeros(self.pose_dim + self.lm_dim)
-        lib().orc_normal_residual(self.h, lam, _d(dx), _d(r))
+        self._L.orc_normal_residual(self.h, lam, _d(dx), _d(r))
         return r
 
     def optimize(self, iters):
         st = LbaStats()
-        n = lib().orc_optimize(self.h, iters, ctypes.byref(st))
+        n = self._L.orc_optimize(self.h, iters, ctypes.byref(st))
         return n, st
 
     def cams(self):
         c = np.array(self.win.cams, copy=True)
-        lib().orc_get_cams(self.h, ptr(c))
+        self._L.orc_get_cams(self.h, ptr(c))
         return c
 
     def state(self):
         from amc_lba.abi import KF_DTYPE
         kfs = np.zeros(self.n_kf, KF_DTYPE)
         lm = np.zeros((self.n_lm, 3))
-        lib().orc_get_state(self.h, ptr(kfs), _d(lm))
+        self._L.orc_get_state(self.h, ptr(kfs), _d(lm))
         return kfs, lm
 
     def last_obs_chi2(self):
         """chi2 of the last computed errors (after optimize: the last trial state), nothing recomputed."""
         c2 = np.zeros(self.n_obs)
-        lib().orc_last_obs_chi2(self.h, _d(c2))
+        self._L.orc_last_obs_chi2(self.h, _d(c2))
         return c2
 
     def depth_ok(self):
         ok = np.zeros(self.n_obs, np.uint8)
-        lib().orc_depth_ok(self.h, ptr(ok))
+        self._L.orc_depth_ok(self.h, ptr(ok))
         return ok
 
     def obs_linearize(self, i):
         e = np.zeros(3)
         J = np.zeros((3, 27))
-        d = lib().orc_obs_linearize(self.h, i, _d(e), _d(J))
+        d = self._L.orc_obs_linearize(self.h, i, _d(e), _d(J))
         return e[:d], J[:d]
 
     def prior_linearize(self, i):
         e = np.zeros(12)
         Ji = np.zeros((12, 12))
         Jj = np.zeros((12, 12))
-        lib().orc_prior_linearize(self.h, i, _d(e), _d(Ji), _d(Jj))
+        self._L.orc_prior_linearize(self.h, i, _d(e), _d(Ji), _d(Jj))
         return e, Ji, Jj
 
 

@@ -77,3 +77,12 @@ extern "C" void mh_right_jac_inv(const double* xi, double* J) { right_jac_inv(xi
 extern "C" void mh_prior(const lba_kf* a, const lba_kf* b, double* e, double* Ji, double* Jj) {
     prior_error_jac(mk(a->q, a->t), a->vel, a->time, mk(b->q, b->t), b->vel, b->time, e, Ji, Jj);
 }
+
+// Jr(xi) = [J, Q; 0, J] as one 6 x 6 (the layout lba_debug_lie returns from the device)
+extern "C" void mh_right_jac(const double* xi, double* Jr) {
+    double J[9], Q[9];
+    right_jac_blocks(xi, J, Q);
+    for (int r = 0; r < 6; ++r)
+        for (int c = 0; c < 6; ++c)
+            Jr[r * 6 + c] = r < 3 ? (c < 3 ? J[r * 3 + c] : Q[r * 3 + c - 3]) : (c >= 3 ? J[(r - 3) * 3 + c - 3] : 0.0);
+}

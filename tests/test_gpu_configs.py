@@ -1,10 +1,11 @@
 """BASELINE.json configs at their stated sizes that the per-window parity tests do not
 already cover: config 0 (the reference's CPU-runnable case, 10 KF / 2k landmarks / ~10k observations,
 one camera, no GP) against the oracle in full, and config 4 (5000 KF / 1M landmarks / ~6M observations,
-global BA shape) on one GPU through the size-independent checks (residuals against the oracle, LM
-descent, determinism) and partitioned over two ranks of an in-process group against the single problem.
-The oracle cannot build config 4's normal equations (a dense 59988^2 H_pp), so the step there is
-checked against the unpartitioned engine, whose solve the smaller configs pin to the oracle."""
+global BA shape) on one GPU: residuals, b and the damped step against the oracle (the oracle holds H_pp as
+g2o's block-sparse matrix, so config 4's normal equations fit: the step is checked through the size-independent
+normal-equation residual (H + lambda I) dx - b, as config 2's), LM descent and determinism; and partitioned over
+two ranks of an in-process group, both the replicated solve and the distributed (subtree) factorisation that
+bench.py runs over N GPUs, against the single problem."""
 import numpy as np
 import pytest
 
@@ -52,11 +53,24 @@ def cfg4():
 def test_cfg4_full_size_single_gpu(cfg4):
     win = cfg4
     assert len(win.kfs) == 5000 and len(win.lm) == 1000000
-    o = orc.Oracle(win)
+    o = orc.Oracle(win, omp=True)   # (the OpenMP build: bitwise the serial oracle, the edge passes threaded)
     chi_o, res_o, _ = o.errors()
-    del o
+    _, b_o, _ = o.build_system(dense=False)
     p = Problem(win, early_stop=0)
     assert p.pose_dim == 12 * 4999
+    # residuals and the gradient against the oracle, then one damped step (BlockSolver::solve at lambda0 with the
+    # sparse LDLT's replacement) through the normal-equation residual over the whole [pose | landmark] system
+    res, _, b, _ = p.linearize(dense=False)
+    assert np.linalg.norm(res - res_o) / np.linalg.norm(res_o) <= 1e-8
+    assert _rel(b, b_o) < 1e-9
+    lam = win.cfg["lambda_init"]
+    ok, dx = p.solve_step(lam)
+    assert ok
+    r = o.normal_residual(lam, dx)
+    rel_r = np.abs(r).max() / np.abs(b_o).max()
+    print(f"cfg4 step: |(H + lambda I) dx - b|_inf / |b|_inf = {rel_r:.2e}")
+    assert rel_r <= 1e-8, rel_r
+    del o, r, res, res_o
     # the reduced system and its factor are packed envelope tiles: device memory O(envelope) (dense
     # npad x npad storage of S and L alone would be 2 x 28.8 GB)
     info = p.solver_info()
@@ -100,3 +114,24 @@ def test_cfg4_full_size_two_rank_partition(cfg4):
     np.testing.assert_array_equal(kfs[0]["t"], kfs[1]["t"])   # every rank solved the same system
     assert _rel(kfs[0]["t"], kf["t"]) <= 1e-9
     assert _rel(lm_p, lm) <= 1e-9
+
+
+def test_cfg4_full_size_subtree_split(cfg4):
+    """The distributed factorisation bench.py runs for config 4 over N GPUs (--gba-solve split,
+    LBA_FLAG_SUBTREE_SOLVE: each rank factors its subtree of the nested dissection, the top separators' tiles
+    all-reduced per trial), at config 4's size over two ranks: one LM iteration equals the single problem's to
+    1e-9 (states gathered from the subtrees' owners)."""
+    from test_gpu_partition import run_split
+    win = cfg4
+    p = Problem(win, early_stop=0)
+    n, st = p.optimize(1)
+    kf, lm = p.state()
+    p.close()
+    res, kf_s, lm_s, own, infos = run_split(win, 2, 1)
+    assert (own >= 0).sum() > 0 and len(set(own[own >= 0])) == 2
+    for n_r, st_r in res:
+        assert n_r == n and st_r.trials == st.trials
+        assert abs(st_r.chi2_initial - st.chi2_initial) <= 1e-11 * st.chi2_initial
+        assert abs(st_r.chi2_final - st.chi2_final) <= 1e-7 * st.chi2_final
+    assert _rel(kf_s["t"], kf["t"]) <= 1e-9
+    assert _rel(lm_s, lm) <= 1e-9
