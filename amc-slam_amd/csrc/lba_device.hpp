@@ -81,7 +81,9 @@ enum { SEL_CUR = 2, SEL_NEXT = 3 };
 // launch gating in a queued optimisation: run always, unless the queue is done, or only when the
 // trial starts a new iteration
 enum { GATE_NONE = 0, GATE_TRIAL = 1, GATE_LIN = 2 };
-constexpr double LAMBDA_CTL = -1.0;   // lambda argument: take the controller's damping
+// lambda argument: take the controller's damping.  A NaN, so that every real damping a caller passes
+// (lba_solve_step at any lambda, negative ones included: BlockSolver::setLambda takes any value) is used as is
+constexpr double LAMBDA_CTL = __builtin_nan("");
 
 struct DevProblem {
     int n_kf, n_lm, n_obs, n_gp, n_pairs, n_tiles, n_pb, np, n_prior, n_vel, n_cam;

@@ -3136,7 +3136,8 @@ int lba_linearize(lba_problem* p, double* residuals, double* H_pp, double* b, do
         HIPCHK(hipSetDevice(p->cfg.device));
         const DevProblem& D = p->D;
         linearize(p, residuals ? 1 : 0);
-        assemble_layout(p, 0.0, ASM_FULL);
+        // (no H_pp asked for: b_p alone, without the dense np x np buffer; config 4's would be 28.8 GB)
+        assemble_layout(p, 0.0, H_pp ? ASM_FULL : ASM_DIAG);
         HIPCHK(hipGetLastError());
         const int np = p->np, nl = D.n_lm, npx = p->np_ext;
         std::vector<double> bp(np + 1), bl(3 * (size_t)nl + 1), hll(9 * (size_t)nl + 1), res(3 * (size_t)p->n_obs + 1);

@@ -97,7 +97,7 @@ __device__ __forceinline__ bool gated_off(const LMCtl* c, int gate) {
     return gate != GATE_NONE && (c->done || (gate == GATE_LIN && !c->need_lin));
 }
 __device__ __forceinline__ double damping(const DevProblem& P, double lambda) {
-    return lambda < 0.0 ? P.ctl->lambda : lambda;
+    return __builtin_isnan(lambda) ? P.ctl->lambda : lambda;   // (LAMBDA_CTL)
 }
 
 // element (r, c), r >= c, of the reduced system in factorisation order inside its tile of L (a structural

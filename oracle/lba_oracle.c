@@ -1502,6 +1502,7 @@ static int lm_iteration(orc_problem* p, int iteration, int* trials, int* fails, 
         apply_update(p, p->x);
         restore_diagonal(p);
         tempChi = compute_errors(p);
+        *last_chi = tempChi;   /* activeRobustChi2() of the last computed errors (the stats' chi2_final) */
         if (!ok2) { tempChi = DBL_MAX; (*fails)++; }
         rho = currentChi - tempChi;
         double scale = compute_scale(p) + 1e-3;
@@ -1521,7 +1522,6 @@ static int lm_iteration(orc_problem* p, int iteration, int* trials, int* fails, 
         qmax++;
     } while (rho < 0 && qmax < p->cfg.max_trials);
     *trials += qmax;
-    *last_chi = tempChi;
     if (qmax == p->cfg.max_trials || rho == 0) return LBA_RESULT_TERMINATE;
     if (p->cfg.early_stop) {
         if ((iniChi - currentChi) * 1e3 < iniChi) p->nBad++;
