@@ -1390,11 +1390,76 @@ __device__ __forceinline__ void piv_seq(double (&row)[CNB], double r, int lane, 
     }
 }
 
+// The same pivot sequence software-pipelined across pivots (bitwise the same results as piv_seq): the chain of
+// pivot J (the next pivot's diagonal, its reciprocal square root, the broadcast) is issued first, and the
+// rank-1 updates of pivot J - 1 on columns J + 1 .. E - 1 are interleaved into it, so the chain no longer waits
+// behind the DPP updates (which wait for their ds_bpermute broadcast, ~80 cycles) nor they behind the chain.
+// Column J + 1, the next pivot's, takes pivot J's update through a readlane broadcast right away.  The
+// diagonal the chain needs is tracked per lane (dg: the same fma sequence the lane's own diagonal entry
+// receives), so it never waits for a deferred update.  Every column still receives its updates one fma at a
+// time in pivot order.  Non-positive pivots show as a non-positive (or NaN) diagonal of L (see factor).
+template <int J, int E, int S>
+__device__ __forceinline__ void pipe_defer(double (&row)[CNB], double rp, double lp) {
+    // deferred update slot S of pivot J - 1: columns J + 1 + S*ND/5 .. J + 1 + (S+1)*ND/5 - 1
+    constexpr int B = E - 16;
+    constexpr int ND = J > B ? E - 1 - J : 0;
+#pragma unroll
+    for (int t = (S * ND) / 5; t < ((S + 1) * ND) / 5; ++t) {
+        switch (J + 1 + t) {   // (constant after unrolling: the DPP lane select is an immediate)
+#define LBA_PD(K) case K: fmac_bcast<K>(row[K], rp, lp); break;
+            LBA_PD(1) LBA_PD(2) LBA_PD(3) LBA_PD(4) LBA_PD(5) LBA_PD(6) LBA_PD(7) LBA_PD(8) LBA_PD(9) LBA_PD(10)
+            LBA_PD(11) LBA_PD(12) LBA_PD(13) LBA_PD(14) LBA_PD(15) LBA_PD(16) LBA_PD(17) LBA_PD(18) LBA_PD(19)
+            LBA_PD(20) LBA_PD(21) LBA_PD(22) LBA_PD(23) LBA_PD(24) LBA_PD(25) LBA_PD(26) LBA_PD(27) LBA_PD(28)
+            LBA_PD(29) LBA_PD(30) LBA_PD(31)
+#undef LBA_PD
+            default: break;
+        }
+    }
+}
+template <int J, int E>
+__device__ __forceinline__ void piv_pipe(double (&row)[CNB], double rn, double dg, double lp, double rp, int lane) {
+    constexpr int B = E - 16;
+    if constexpr (J < E) {
+        const double lij = row[J] * rn;   // lane J: sqrt(d); lanes > J: L(l, J)
+        row[J] = lij;
+        if constexpr (J + 1 < E) {
+            const double own = dg - lij * lij;       // lane J + 1: the next pivot (as piv_seq computes it)
+            const double dgn = fma(-lij, lij, dg);   // the lane's own diagonal entry after this pivot's update
+            double rep = 0.0;
+            if constexpr (J + 2 < E) rep = rep16<B>(lij, lane);
+            // (the scheduler would sink the ds_bpermute down to its first use, the deferred updates of the
+            // next window, and stall the chain there on its ~80-cycle return: keep it here)
+            __builtin_amdgcn_sched_barrier(0);
+            const double sL = readlane_d(lij, J + 1);
+            double c = __builtin_amdgcn_rsq(own);
+            pin(c);
+            pipe_defer<J, E, 0>(row, rp, lp);
+            double t = own * c;
+            pin(t);
+            pipe_defer<J, E, 1>(row, rp, lp);
+            double e = fma(-t, c, 1.0);
+            pin(e);
+            pipe_defer<J, E, 2>(row, rp, lp);
+            t = fma(0.375, e, 0.5);
+            const double m = c * e;
+            pin(t);
+            pipe_defer<J, E, 3>(row, rp, lp);
+            c = fma(m, t, c);
+            pin(c);
+            pipe_defer<J, E, 4>(row, rp, lp);
+            row[J + 1] = fma(-lij, sL, row[J + 1]);   // = fmac(-L(J+1, J), lij): piv_seq's first update
+            const double rnn = readlane_d(c, J + 1);
+            piv_pipe<J + 1, E>(row, rnn, dgn, lij, rep, lane);
+        }
+    }
+}
+
 // Between the halves: every stacked row's columns 16..31 -= (its columns 0..15) (rows 16..31's
 // columns 0..15)^T, i.e. A22 -= L21 L21^T and the tile rows' share, as 4 row tiles x 4 k-steps of
 // v_mfma_f64_16x16x4 on the wave's LDS staging buffer (columns 0..15 in, the product out through
 // columns 16..31).
-__device__ __forceinline__ void cross_update(double (&row)[CNB], double (*st)[CNB + 1], int lane) {
+__device__ __forceinline__ void cross_update(double (&row)[CNB], double (*st)[CNB + 1], int lane, double dg0 = 0.0,
+                                             double* dg2 = nullptr) {
 #pragma unroll
     for (int c = 0; c < 16; ++c) st[lane][c] = row[c];
     wave_sync();
@@ -1414,8 +1479,143 @@ __device__ __forceinline__ void cross_update(double (&row)[CNB], double (*st)[CN
 #pragma unroll
         for (int q = 0; q < 4; ++q) st[16 * t + kq + 4 * q][16 + lr] = acc[t][q];
     wave_sync();
+    // (lanes 16..31: the diagonal entry after the update, for piv_pipe's tracking; the first half did not
+    // touch columns 16..31, so it is the original entry minus the product, as row[lane] below)
+    if (dg2) *dg2 = dg0 - st[lane][lane & 31];
 #pragma unroll
     for (int c = 0; c < 16; ++c) row[16 + c] -= st[lane][16 + c];
+}
+
+// The stacked panel in `st` (rows 0..31 the diagonal block) factored by ONE wave: piv_pipe over the two
+// halves with the matrix-core cross update between them; bitwise the results of piv_seq / cross_update /
+// piv_seq.  bad: a non-positive (or NaN) pivot, seen as a diagonal entry of L that is not > 0 (a pivot
+// d <= 0 or NaN gives rsq(d) = NaN / inf, so L(J, J) = NaN; d > 0 gives L(J, J) = d rsq(d) > 0).
+__device__ __forceinline__ void factor_pipe(double (*st)[CNB + 1], int lane, bool& bad) {
+    double row[CNB];
+#pragma unroll
+    for (int c = 0; c < CNB; ++c) row[c] = st[lane][c];
+    const double dg0 = st[lane][lane & 31];
+    piv_pipe<0, 16>(row, readlane_d(rsqrt_nr(row[0]), 0), dg0, 0.0, 0.0, lane);
+    double dg2 = 0.0;
+    cross_update(row, st, lane, dg0, &dg2);
+    piv_pipe<16, CNB>(row, readlane_d(rsqrt_nr(row[16]), 16), dg2, 0.0, 0.0, lane);
+#pragma unroll
+    for (int c = 0; c < CNB; ++c) st[lane][c] = row[c];
+    wave_sync();
+    bad = lane < CNB && !(st[lane][lane & 31] > 0.0);
+}
+
+// The stacked panel factored by TWO waves (a pair of the workgroup: half = 0 / 1): wave 0 of the pair runs
+// piv_pipe over columns 0..15 and publishes every pivot column L(., J) to LDS (colbuf[J][lane], a flag
+// per PAIR_GROUP pivots); wave 1 holds columns 16..31 and applies each published column to them as it arrives
+// (one fma per entry and pivot, through the DPP row broadcast of colbuf[J][16 + (lane & 15)]; colbuf holds
+// columns 0..15, cflag 16 / PAIR_GROUP flags), in place of
+// the matrix-core cross update, then runs piv_pipe over columns 16..31.  The updates of the second half
+// thus run on the other SIMD while the first half's chain runs.  Rounding: every entry receives its rank-1
+// updates one fma at a time in pivot order (no matrix-core partial sums), so the factor differs from
+// factor_pipe's in the last bits of columns 16..31.  bad: as factor_pipe.  Both waves of the pair call it.
+constexpr int PAIR_GROUP = 4;   // pivot columns per flag
+template <int SLOT>
+__device__ __forceinline__ void pair_consume(double (&row)[CNB], double& dg, const double (*colbuf)[64], int g, int lane) {
+    double lij[PAIR_GROUP], rep[PAIR_GROUP];
+#pragma unroll
+    for (int u = 0; u < PAIR_GROUP; ++u) {
+        lij[u] = colbuf[g + u][lane];
+        rep[u] = colbuf[g + u][16 + (lane & 15)];
+    }
+#pragma unroll
+    for (int u = 0; u < PAIR_GROUP; ++u) {
+#pragma unroll
+        for (int c = 16; c < CNB; ++c) {
+            switch (c) {
+#define LBA_PC(K) case K: fmac_bcast<K>(row[K], rep[u], lij[u]); break;
+                LBA_PC(16) LBA_PC(17) LBA_PC(18) LBA_PC(19) LBA_PC(20) LBA_PC(21) LBA_PC(22) LBA_PC(23)
+                LBA_PC(24) LBA_PC(25) LBA_PC(26) LBA_PC(27) LBA_PC(28) LBA_PC(29) LBA_PC(30) LBA_PC(31)
+#undef LBA_PC
+                default: break;
+            }
+        }
+        dg = fma(-lij[u], lij[u], dg);
+    }
+    (void)SLOT;
+}
+template <int J>
+__device__ __forceinline__ void piv_pipe_pub(double (&row)[CNB], double rn, double dg, double lp, double rp, int lane,
+                                             double (*colbuf)[64], int* cflag, int tag);
+__device__ __forceinline__ void factor_pair(double (*st)[CNB + 1], double (*colbuf)[64], int* cflag, int tag, int half,
+                                            bool& bad) {
+    // (bad: the caller checks the diagonal of L once both waves have stored their columns, as factor_pipe)
+    bad = false;
+    const int lane = threadIdx.x & 63;
+    double row[CNB];
+    const double dg0 = st[lane][lane & 31];
+    if (half == 0) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) row[c] = st[lane][c];
+        piv_pipe_pub<0>(row, readlane_d(rsqrt_nr(row[0]), 0), dg0, 0.0, 0.0, lane, colbuf, cflag, tag);
+#pragma unroll
+        for (int c = 0; c < 16; ++c) st[lane][c] = row[c];
+    } else {
+#pragma unroll
+        for (int c = 16; c < CNB; ++c) row[c] = st[lane][c];
+        double dg = dg0;
+        for (int g = 0; g < 16; g += PAIR_GROUP) {
+            unsigned spins = 0;
+            while (__hip_atomic_load(cflag + g / PAIR_GROUP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != tag) {
+#ifdef LBA_PAIR_SLEEP
+                __builtin_amdgcn_s_sleep(LBA_PAIR_SLEEP);
+#endif
+                if (++spins > (1u << 24)) break;   // (bounded: never expected)
+            }
+            asm volatile("" ::: "memory");
+            pair_consume<0>(row, dg, colbuf, g, lane);
+        }
+        piv_pipe<16, CNB>(row, readlane_d(rsqrt_nr(row[16]), 16), dg, 0.0, 0.0, lane);
+#pragma unroll
+        for (int c = 16; c < CNB; ++c) st[lane][c] = row[c];
+    }
+}
+// piv_pipe<J, 16> that also publishes every pivot column for the pair's second wave (a flag per PAIR_GROUP)
+template <int J>
+__device__ __forceinline__ void piv_pipe_pub(double (&row)[CNB], double rn, double dg, double lp, double rp, int lane,
+                                             double (*colbuf)[64], int* cflag, int tag) {
+    constexpr int E = 16, B = 0;
+    if constexpr (J < E) {
+        const double lij = row[J] * rn;
+        row[J] = lij;
+        colbuf[J][lane] = lij;
+        if constexpr (J % PAIR_GROUP == PAIR_GROUP - 1) {
+            asm volatile("" ::: "memory");
+            __hip_atomic_store(cflag + J / PAIR_GROUP, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if constexpr (J + 1 < E) {
+            const double own = dg - lij * lij;
+            const double dgn = fma(-lij, lij, dg);
+            double rep = 0.0;
+            if constexpr (J + 2 < E) rep = rep16<B>(lij, lane);
+            __builtin_amdgcn_sched_barrier(0);
+            const double sL = readlane_d(lij, J + 1);
+            double c = __builtin_amdgcn_rsq(own);
+            pin(c);
+            pipe_defer<J, E, 0>(row, rp, lp);
+            double t = own * c;
+            pin(t);
+            pipe_defer<J, E, 1>(row, rp, lp);
+            double e = fma(-t, c, 1.0);
+            pin(e);
+            pipe_defer<J, E, 2>(row, rp, lp);
+            t = fma(0.375, e, 0.5);
+            const double m = c * e;
+            pin(t);
+            pipe_defer<J, E, 3>(row, rp, lp);
+            c = fma(m, t, c);
+            pin(c);
+            pipe_defer<J, E, 4>(row, rp, lp);
+            row[J + 1] = fma(-lij, sL, row[J + 1]);
+            const double rnn = readlane_d(c, J + 1);
+            piv_pipe_pub<J + 1>(row, rnn, dgn, lij, rep, lane, colbuf, cflag, tag);
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1634,12 +1834,26 @@ __device__ __forceinline__ d4 cf_mma_nn(const double (*X)[CNB + 1], const double
     return acc;
 }
 
+#ifndef LBA_CHOL_MODE
+// stacked panels: 1 one wave, factor_pipe (default; bitwise piv_seq's results); 0 one wave, piv_seq; 2 a pair of
+// waves, factor_pair (5.7k cycles against 7.0k alone on an idle CU, scripts/micro/piv_factor.hip, but no faster
+// inside k_chol_flow and different rounding: profiles/r4g_ab_factor_modes.txt, r4h_*)
+#define LBA_CHOL_MODE 1
+#endif
 __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
     __shared__ double Lt[3][CNB][CNB + 1];       // update operands L(j, p), L(i, p), L(k, p)
     __shared__ double stg[2][2 * CNB][CNB + 1];  // stacked panels of the factoring waves
     __shared__ long long s_ticket;
     __shared__ int s_ok;
+    __shared__ int cflag[2][16 / PAIR_GROUP];   // factor_pair's pivot-column flags, per pair of waves
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // factor_pair's pivot columns (16 x 64 per pair) share Lt's memory (no update operand is live while a
+    // panel is factored)
+    double (*colbuf0)[64] = reinterpret_cast<double (*)[64]>(&Lt[0][0][0]);
+    double (*colbuf1)[64] = colbuf0 + 16;
+    static_assert(sizeof(Lt) >= sizeof(double) * 2 * 16 * 64, "factor_pair column buffers");
+    int ftag = 0;   // factor rounds of this workgroup (the flags' tag)
+    if (tid < 2 * (16 / PAIR_GROUP)) cflag[tid / (16 / PAIR_GROUP)][tid % (16 / PAIR_GROUP)] = 0;
     const int rb = wave >> 1, cb = wave & 1, lr = lane & 15, kq = lane >> 4;
     const int n = a.n;
     // (the tile ids a task touches come precomputed with it, read into registers at the task's start or
@@ -1660,6 +1874,9 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
     };
     // one wave: two-level pivot sequence of its stacked panel in `st` (row r of lane r)
     auto factor = [&](double (*st)[CNB + 1], bool& bad) {
+#if LBA_CHOL_MODE == 1
+        factor_pipe(st, lane, bad);
+#else
         double row[CNB];
 #pragma unroll
         for (int c = 0; c < CNB; ++c) row[c] = st[lane][c];
@@ -1671,7 +1888,18 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
 #pragma unroll
         for (int c = 0; c < CNB; ++c) st[lane][c] = row[c];
         wave_sync();
+#endif
     };
+    (void)factor;
+    // waves 2 p, 2 p + 1 (p = pair): factor_pair of st; every thread calls it (one flag round per call)
+    auto factor_pairs = [&](double (*st0)[CNB + 1], double (*st1)[CNB + 1]) {
+        const int tg = ++ftag;
+        bool bad;
+        if (wave < 2) factor_pair(st0, colbuf0, cflag[0], tg, wave, bad);
+        else if (st1) factor_pair(st1, colbuf1, cflag[1], tg, wave - 2, bad);
+        __syncthreads();
+    };
+    (void)factor_pairs;
     const d4 z4 = {0.0, 0.0, 0.0, 0.0};
     while (true) {
         if (tid == 0) s_ticket = (long long)atomicAdd(a.head, 1ull);
@@ -2078,12 +2306,16 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
                 stage_quad(stg[1], CNB, qik);
             }
             __syncthreads();
+#if LBA_CHOL_MODE == 2
+            factor_pairs(stg[0], ik ? stg[1] : nullptr);   // (a bad pivot is reported by panel k's own task)
+#else
             if (wave == 0 || (wave == 1 && ik)) {
                 bool bad;
                 factor(stg[wave], bad);
                 (void)bad;   // (reported by panel k's own task)
             }
             __syncthreads();
+#endif
             if (tf) tf[6] = __builtin_amdgcn_s_memrealtime();
         };
         if (la && ((code >> 29) & 1)) factor_k();
@@ -2132,6 +2364,14 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             stage_quad(stg[0], CNB, qa);
             __syncthreads();
             if (tm) tm[4] = __builtin_amdgcn_s_memrealtime();
+#if LBA_CHOL_MODE == 2
+            {   // (a non-positive pivot of A(j,j) is reported by panel j's own task)
+                const unsigned long long c0 = tf ? clock64() : 0;
+                factor_pairs(stg[0], nullptr);
+                if (tf) tf[7] = clock64() - c0;
+                if (tm) tm[5] = __builtin_amdgcn_s_memrealtime();
+            }
+#else
             if (wave == 0) {
                 bool bad;
                 const unsigned long long c0 = tf ? clock64() : 0;
@@ -2141,6 +2381,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
                 (void)bad;   // (a non-positive pivot of A(j,j) is reported by panel j's own task)
             }
             __syncthreads();
+#endif
             // L(i, j) from the staged panel by all four waves (a quarter of the write-through bytes per
             // wave: the drain before the flag is a quarter as long as one wave storing the tile)
 #pragma unroll
@@ -2162,6 +2403,19 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
         }
         __syncthreads();
         if (tm) tm[4] = __builtin_amdgcn_s_memrealtime();
+#if LBA_CHOL_MODE == 2
+        {
+            const unsigned long long c0 = tf ? clock64() : 0;
+            factor_pairs(stg[0], nullptr);
+            if (tf) tf[7] = clock64() - c0;
+            // a non-positive (or NaN) pivot shows as a diagonal entry of L that is not > 0 (factor_pipe)
+            if (wave == 0) {
+                const bool bad = lane < CNB && !(stg[0][lane][lane & 31] > 0.0);
+                if (__ballot(bad) != 0 && lane == 0) *a.info = 1 + (int)p0;
+            }
+            if (tm) tm[5] = __builtin_amdgcn_s_memrealtime();
+        }
+#else
         if (wave == 0) {
             bool bad;
             const unsigned long long c0 = tf ? clock64() : 0;
@@ -2171,6 +2425,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             if (tm) tm[5] = __builtin_amdgcn_s_memrealtime();
         }
         __syncthreads();
+#endif
 #pragma unroll
         for (int m = 0; m < 4; ++m) {   // L_jj (plain: no reader in this launch), L_jj^-T, by all waves
             const int e = tid + 256 * m, r = e >> 5, c = e & 31;

@@ -7,4 +7,4 @@ NAME=$1; shift
 mkdir -p "$ROOT/amc-slam_amd/lib/exp"
 C=$ROOT/amc-slam_amd/csrc
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared "$@" "$C/lba_kernels.hip" "$C/lba_host.hip" \
-    "$C/lba_track.hip" -o "$ROOT/amc-slam_amd/lib/exp/$NAME.so" -lrccl
+    "$C/lba_track.hip" "$C/lba_debug.hip" -o "$ROOT/amc-slam_amd/lib/exp/$NAME.so" -lrccl
