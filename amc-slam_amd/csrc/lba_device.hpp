@@ -35,6 +35,7 @@ constexpr int KFP_STRIDE = 12;      // Rwb(9) twb(3)
 
 // tile limits (one workgroup of TILE_OBS threads per tile)
 constexpr int TILE_OBS = 128;
+constexpr int UPD_BLOCK_KFS = 64;   // keyframes per KF-block workgroup of k_update (its UPD_THREADS)
 constexpr int TILE_ROWS = 288;
 constexpr int TILE_PAIRS = 128;
 constexpr int TILE_LMS = 64;
@@ -257,6 +258,13 @@ struct DevProblem {
     double* chi_eval;       // [n_tiles + n_prior + n_vel + n_eprior]
     double* scale_part;     // [n_upd_blocks]
     int n_upd_blocks;
+    // fused trial evaluation (k_update with eval = 1): the regular tiles evaluate their observations at the trial
+    // state once the pose samples are made, extra workgroups the motion-prior / velocity edges (no heavy landmarks,
+    // no free extrinsics); upd_flag [n_gp + KF blocks]: a producer's epoch once its samples / states are stored,
+    // smp_prod [n_smp]: the producer of each pose sample (its GP pair, or the KF block of a KF pose sample)
+    int fuse_eval;
+    int* upd_flag;
+    const int* smp_prod;
     double* kbuf[2];        // kf state buffers [n_kf][KF_STRIDE] (current / trial, see LMCtl::cur)
     double* lbuf[2];        // landmark state buffers [n_lm][3]
     LMCtl* ctl;             // queued-optimisation controller
@@ -321,7 +329,12 @@ void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hi
 void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s, hipEvent_t e0 = nullptr,
                            hipEvent_t e1 = nullptr, int sel = 0, double lambda = 0.0);
 // the step + trial state + the trial state's pose samples (jac: with their Jacobian factors)
-void launch_update(const DevProblem& P, double lambda, int sel, int gate, int jac, hipStream_t s);
+// eval: with P.fuse_eval, also the trial state's errors (k_eval's chi_eval / ob_chi2), no k_eval launch needed;
+// update_grid: its workgroups; update_resident_blocks: k_update workgroups resident at once on the device
+int update_grid(const DevProblem& P, int eval);
+int update_resident_blocks(int device);
+void launch_update(const DevProblem& P, double lambda, int sel, int gate, int jac, hipStream_t s, int eval = 0,
+                   unsigned epoch = 0);
 // partitioned mode: this rank's trial sums into red4; envelope of S + bS + b_p into / out of env_buf
 void launch_partials(const DevProblem& P, hipStream_t s);
 void launch_env_pack(const DevProblem& P, int unpack, int gate, hipStream_t s);

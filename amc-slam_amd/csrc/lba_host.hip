@@ -94,6 +94,7 @@ struct lba_problem {
     size_t s_bytes = 0;           // device bytes of S + L (packed envelopes)
     unsigned long long fin_seq = 0;
     unsigned cf_epoch = 0;        // launches of the dataflow factorisation (its flags hold the epoch)
+    unsigned upd_epoch = 0;       // launches of k_update (the fused evaluation's producer flags hold the epoch)
     bool gps_fresh[2] = {false, false};   // state buffer s has its pose samples with Jacobian factors
     double lambda = -1.0, ni = 2.0;
     int nBad = 0;
@@ -1900,6 +1901,27 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.n_upd_blocks = D.n_gp + (n_kfs + 63) / 64 + n_stiles + (n_heavy + 63) / 64;
     if (D.n_upd_blocks == 0) D.n_upd_blocks = 1;
     D.scale_part = dalloc<double>(p, D.n_upd_blocks);
+    // the trial evaluation fused into k_update (LBA_NO_FUSED_EVAL: k_eval after it): not with heavy landmarks (their
+    // segment tiles and trial states are other workgroups') nor free extrinsics (the trial camera records); only
+    // when the whole k_update grid is resident at once (its evaluating workgroups wait for its producers), and
+    // not for partitioned problems (ranks of an in-process group share one device)
+    D.fuse_eval = (n_heavy == 0 && n_ext == 0 && p->part_n == 0 && std::getenv("LBA_NO_FUSED_EVAL") == nullptr) ? 1 : 0;
+    if (D.fuse_eval) {
+        static thread_local int resident = -1;   // (per device ordinal in practice: one value per process)
+        if (resident < 0) resident = update_resident_blocks(p->cfg.device);
+        if (update_grid(D, 1) > resident) D.fuse_eval = 0;
+    }
+    {   // the producer of every pose sample (fused evaluation): its GP pair, or the KF block of a KF pose sample
+        const int nkb = (n_kfs + UPD_BLOCK_KFS - 1) / UPD_BLOCK_KFS;
+        std::vector<int> prod(std::max(D.n_smp, 1), -1);
+        for (int g = 0; g < D.n_gp; ++g)
+            for (int s = gp_s0[g]; s < gp_s0[g + 1]; ++s) prod[s] = g;
+        for (int k = 0; k < n_kfs; ++k) prod[D.n_gps + k] = D.n_gp + k / UPD_BLOCK_KFS;
+        D.smp_prod = dupload(p, prod);
+        D.upd_flag = dalloc<int>(p, D.n_gp + nkb + 1);
+        HIPCHK(hipMemsetAsync(D.upd_flag, 0, sizeof(int) * (D.n_gp + nkb + 1), p->stream));
+        p->upd_epoch = 0;
+    }
     D.info = dalloc<int>(p, 1);
     D.ctl = dalloc<LMCtl>(p, 1);
     D.fin = dalloc<double>(p, 4);
@@ -2034,9 +2056,10 @@ void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs, bool s
     if (evs) HIPCHK(hipEventRecord(evs[2], p->stream));
     launch_solve(p, sweep ? p->ev[8] : nullptr, sweep ? p->ev[9] : nullptr, p->cur, lambda);
     if (evs) HIPCHK(hipEventRecord(evs[3], p->stream));
-    launch_update(D, lambda, p->cur, GATE_NONE, 1, p->stream);   // (+ the trial state's pose samples)
+    // (+ the trial state's pose samples, and with D.fuse_eval its errors)
+    launch_update(D, lambda, p->cur, GATE_NONE, 1, p->stream, evaluate ? 1 : 0, ++p->upd_epoch);
     p->gps_fresh[nx] = true;
-    if (evaluate) launch_eval(D, nx, GATE_NONE, 0, FIN_NONE, p->stream);
+    if (evaluate && !D.fuse_eval) launch_eval(D, nx, GATE_NONE, 0, FIN_NONE, p->stream);
     if (evs) HIPCHK(hipEventRecord(evs[4], p->stream));
     finalize_and_wait(p, sync || evs || sweep);
     p->linearized = false;
@@ -2139,8 +2162,8 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
             launch_solve(p, qe ? qe[2] : nullptr, qe ? qe[3] : nullptr, SEL_CUR, LAMBDA_CTL);
             // the step, the trial state and its pose samples with their Jacobian factors: the next
             // trial's linearisation reads them (no preparation launch)
-            launch_update(D, LAMBDA_CTL, SEL_CUR, GATE_TRIAL, 1, p->stream);
-            launch_eval(D, SEL_NEXT, GATE_TRIAL, 0, FIN_NONE, p->stream);
+            launch_update(D, LAMBDA_CTL, SEL_CUR, GATE_TRIAL, 1, p->stream, 1, ++p->upd_epoch);
+            if (!D.fuse_eval) launch_eval(D, SEL_NEXT, GATE_TRIAL, 0, FIN_NONE, p->stream);
             launch_fin(p, ++p->fin_seq, k == n - 1 ? FIN_QUEUED_PUBLISH : FIN_QUEUED);
             HIPCHK(hipGetLastError());
         }

@@ -219,21 +219,19 @@ __device__ __forceinline__ double lin_obs(const DevProblem& P, const double* gps
     return r0;
 }
 
-// Residual-only evaluation of one observation (computeError + robust chi2); returns rho(chi2).
+// Residual-only evaluation of one observation (computeError + robust chi2) at the body pose (Rwb, twb) and
+// landmark Xw; returns rho(chi2).
 template <int DIM>
-__device__ __forceinline__ double eval_obs(const DevProblem& P, const double* gps, const double* kst,
-                                           const double* lst, const double* camd, int o, const ObsIn& in, int cam,
-                                           bool gp) {
+__device__ __forceinline__ double eval_obs_at(const DevProblem& P, const double* Rwb, const double* twb, double bf,
+                                              const double* Xw, const double* camd, int o, const ObsIn& in, int cam) {
     CamD cd;
     load_cam(camd + (size_t)cam * CAMD_STRIDE, &cd);
-    double Rwb[9], twb[3];
-    const double bf = obs_pose(gps, kst, in, gp, Rwb, twb);
     double z[DIM];
 #pragma unroll
     for (int d = 0; d < DIM; ++d) z[d] = in.z[d];
     const double w = in.w;
     double Xb[3], Xc[3], e[DIM];
-    project_residual<DIM>(Rwb, twb, cd, lst + (size_t)in.lm * 3, z, bf, Xb, Xc, e);
+    project_residual<DIM>(Rwb, twb, cd, Xw, z, bf, Xb, Xc, e);
     double chi = 0.0;
 #pragma unroll
     for (int d = 0; d < DIM; ++d) chi += e[d] * (w * e[d]);
@@ -241,6 +239,14 @@ __device__ __forceinline__ double eval_obs(const DevProblem& P, const double* gp
     huber(chi, DIM == 3 ? P.huber_stereo : P.huber_mono, &r0, &r1);
     P.ob_chi2[o] = chi;
     return r0;
+}
+template <int DIM>
+__device__ __forceinline__ double eval_obs(const DevProblem& P, const double* gps, const double* kst,
+                                           const double* lst, const double* camd, int o, const ObsIn& in, int cam,
+                                           bool gp) {
+    double Rwb[9], twb[3];
+    const double bf = obs_pose(gps, kst, in, gp, Rwb, twb);
+    return eval_obs_at<DIM>(P, Rwb, twb, bf, lst + (size_t)in.lm * 3, camd, o, in, cam);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -258,6 +264,9 @@ constexpr int PREP_SCHUNK = 32;   // samples per pass (one lane each; LDS stagin
 // shm: PREP_SHM doubles of LDS (the caller's, so k_update's roles share one allocation)
 constexpr int PREP_PR = (sizeof(GPPair) / sizeof(double) + 1) & ~1;
 constexpr int PREP_SHM = PREP_PR + 36 + 36 + 8 + PREP_SCHUNK * (18 + 9 + 9 + 3);
+// WT: the sample poses (Rwb, twb) are stored write-through (sc1), for readers in other workgroups of the same
+// launch (k_update's fused evaluation)
+template <bool WT = false>
 __device__ __forceinline__ void gp_pair_prep(const DevProblem& P, double* gps, int i, const double* ka,
                                              const double* kb, int jac, double* shm,
                                              unsigned long long* pst = nullptr) {
@@ -324,7 +333,12 @@ __device__ __forceinline__ void gp_pair_prep(const DevProblem& P, double* gps, i
             double xi[6];
             GPScalars g;
             SE3 E;
-            gp_sample_pose(pr, c0 == s0 ? t_first : P.gps_t[c0 + tid], S->Rwb, S->twb, xi, &g, &E);
+            double Rl[9], tl[3];
+            gp_sample_pose(pr, c0 == s0 ? t_first : P.gps_t[c0 + tid], Rl, tl, xi, &g, &E);
+#pragma unroll
+            for (int j = 0; j < 9; ++j) stv<WT>(S->Rwb + j, Rl[j]);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) stv<WT>(S->twb + j, tl[j]);
             if (jac) {
                 const SE3 Em = se3_inv(E);                  // Ad(exp(-xi)) = [R', t'^ R'; 0, R']
                 double Ht[9];
@@ -372,14 +386,22 @@ __device__ __forceinline__ void gp_pair_prep(const DevProblem& P, double* gps, i
 #undef PREP_STAMP
 }
 
-// KF k's pose record (k_depth) and the KF's pose sample (its constant N was uploaded once)
+// KF k's pose record (k_depth) and the KF's pose sample (its constant N was uploaded once); WT: the sample
+// stored write-through (see gp_pair_prep)
+template <bool WT = false>
 __device__ __forceinline__ void kf_pose_record(const DevProblem& P, double* gps, int k, const double* kk) {
     double R[9];
     qmat(Quat{kk[0], kk[1], kk[2], kk[3]}, R);
     double* o = P.kfp_pose + (size_t)k * KFP_STRIDE;
     double* so = gps + (size_t)(P.n_gps + k) * GPS_STRIDE;
-    for (int j = 0; j < 9; ++j) o[j] = so[j] = R[j];
-    o[9] = so[9] = kk[4]; o[10] = so[10] = kk[5]; o[11] = so[11] = kk[6];
+    for (int j = 0; j < 9; ++j) {
+        o[j] = R[j];
+        stv<WT>(so + j, R[j]);
+    }
+    for (int j = 0; j < 3; ++j) {
+        o[9 + j] = kk[4 + j];
+        stv<WT>(so + 9 + j, kk[4 + j]);
+    }
 }
 
 // Pose samples of the state `sel`: one workgroup per GP pair, then KF pose records.
@@ -2451,6 +2473,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
 
 // ------------------------------------------------------------------------------------------------
 constexpr int UPD_THREADS = 64;     // one landmark (or KF) per thread: many small blocks for latency hiding
+static_assert(UPD_THREADS == UPD_BLOCK_KFS, "k_update's KF blocks (the host numbers the fused evaluation's producers)");
 
 // Trial state of a KF (state kc): Twb <- Twb exp(dxi), v += dv (G2oTypes.cc:41-46) with the step dx (12) =
 // the solved step, or the stale x when the factorisation failed (BlockSolver leaves x untouched, g2o then
@@ -2533,8 +2556,9 @@ constexpr int BS_SHM = TILE_SMP * 6 + TILE_OBS * 3;
 // (Latency-bound: every load a thread needs is issued in a few batches, each stage's index loads for all of its
 // tasks before their data loads, and the landmark's own inputs at entry, so a tile costs a handful of memory
 // round trips instead of one chain per task.)
+// (ltr, optional, LDS [TILE_LMS][3]: the tile's trial landmark positions, for the fused evaluation)
 __device__ double bs_tile(const DevProblem& P, int tile, int si, bool ok, double lambda, double* lo, double* shm,
-                          unsigned long long* stamp) {
+                          unsigned long long* stamp, double* ltr = nullptr) {
     double(*tsh)[6] = reinterpret_cast<double(*)[6]>(shm);                  // t_s per tile sample
     double(*vsh)[3] = reinterpret_cast<double(*)[3]>(shm + TILE_SMP * 6);   // G_o^T t per observation
     const int tid = threadIdx.x;
@@ -2639,11 +2663,110 @@ __device__ double bs_tile(const DevProblem& P, int tile, int si, bool ok, double
             xl[0] = xold[0]; xl[1] = xold[1]; xl[2] = xold[2];
         }
         for (int a = 0; a < 3; ++a) {
-            lo[3 * (size_t)l + a] = lv[a] + xl[a];
+            const double v = lv[a] + xl[a];
+            lo[3 * (size_t)l + a] = v;
+            if (ltr) ltr[3 * tid + a] = v;
             sc += xl[a] * (lambda * xl[a] + blv[a]);
         }
     }
     return sc;
+}
+
+#ifndef LBA_UPD_POLL_SLEEP
+#define LBA_UPD_POLL_SLEEP 2
+#endif
+// Fused evaluation (k_update, eval = 1): wait until the producers `prod` (one per lane, < 0: none; the GP pairs and
+// KF blocks whose pose samples / states the workgroup reads) have stored them write-through and set their flag to
+// this launch's epoch (lanes poll side by side; bounded, as k_chol_flow's waits)
+__device__ __forceinline__ void upd_wait(const DevProblem& P, int prod, unsigned epoch) {
+    // (one poll per distinct producer: a lane whose left neighbour waits for the same one stays quiet)
+    const int left = __shfl_up(prod, 1, 64);
+    if ((threadIdx.x & 63) > 0 && left == prod) prod = -1;
+    bool done = prod < 0;
+    unsigned spins = 0;
+    while (!__all(done)) {
+        if (!done) done = (unsigned)__hip_atomic_load((gi32_t*)(P.upd_flag + prod), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+        if (__all(done)) break;
+        __builtin_amdgcn_s_sleep(LBA_UPD_POLL_SLEEP);
+        if (++spins > (1u << 20)) break;   // (~0.5 s: never expected)
+    }
+    __syncthreads();
+}
+// ... and a producer (workgroup role `self`) reports its (write-through) stores done
+__device__ __forceinline__ void upd_publish(const DevProblem& P, int self, unsigned epoch) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store((gi32_t*)(P.upd_flag + self), (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The tile's observations at the trial state (k_eval's tile item: the same per-observation arithmetic and the same
+// reduction tree, so chi_eval / ob_chi2 are bitwise k_eval's): poses from the trial samples, landmarks from ltr
+// (this workgroup's back-substitution).  The samples are written in this launch, write-through, by other
+// workgroups; they are read with plain loads: no cache of this launch can hold an older copy (the caches are
+// invalidated at the launch's start and nothing reads the trial samples before the producers report), and
+// sc1 loads of these few hundred hot records from every tile cost more than the whole k_eval launch (+12 us).  Everything but the poses is loaded before
+// the wait for the samples (upd_wait_samples), so after it the tile is one round of loads from done.
+struct TrialObs {
+    ObsIn in;
+    int o, meta;
+    double bf;
+};
+__device__ __forceinline__ void eval_tile_prefetch(const DevProblem& P, int tile, int si, TrialObs (&to)[UPD_TILE_OBS_PER_THREAD]) {
+    const int tid = threadIdx.x;
+    const double* __restrict__ kst = P.kbuf[si];      // (bf: the same in both state buffers)
+    const int obs0 = P.tile_obs0[tile], nobs = P.tile_nobs[tile];
+#pragma unroll
+    for (int k = 0; k < UPD_TILE_OBS_PER_THREAD; ++k) {
+        const int ol = tid + UPD_THREADS * k;
+        to[k].o = ol < nobs ? obs0 + ol : -1;
+        if (ol < nobs) {
+            to[k].meta = P.ob_meta[obs0 + ol];
+            to[k].in = obs_in(P, obs0 + ol);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < UPD_TILE_OBS_PER_THREAD; ++k)
+        if (to[k].o >= 0) {
+            const bool gp = (to[k].meta & 15) <= LBA_STEREO_GP;
+            to[k].bf = kst[(size_t)(gp ? to[k].in.kfa : to[k].in.kfb) * KF_STRIDE + 14];
+        }
+}
+__device__ __forceinline__ void eval_tile_trial(const DevProblem& P, int tile, int si, const double* ltr,
+                                                const TrialObs (&to)[UPD_TILE_OBS_PER_THREAD]) {
+    const int tid = threadIdx.x;
+    const double* __restrict__ gpn = P.gpsb[si ^ 1];
+    const double* __restrict__ camd = P.camdb[si];    // (no free extrinsic: the same in both)
+    const int lm0 = P.tile_lm0[tile];
+    double Rwb[UPD_TILE_OBS_PER_THREAD][9], twb[UPD_TILE_OBS_PER_THREAD][3];
+#pragma unroll
+    for (int k = 0; k < UPD_TILE_OBS_PER_THREAD; ++k)
+        if (to[k].o >= 0) {
+            const double* S = gpn + (size_t)to[k].in.smp * GPS_STRIDE;
+#pragma unroll
+            for (int i = 0; i < 9; ++i) Rwb[k][i] = S[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) twb[k][i] = S[9 + i];
+        }
+    double rho[UPD_TILE_OBS_PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < UPD_TILE_OBS_PER_THREAD; ++k) {
+        rho[k] = 0.0;
+        if (to[k].o >= 0) {
+            const int kind = to[k].meta & 15, cam = to[k].meta >> 4;
+            const double* Xw = ltr + 3 * (to[k].in.lm - lm0);
+            rho[k] = (kind == LBA_STEREO_GP || kind == LBA_STEREO)
+                         ? eval_obs_at<3>(P, Rwb[k], twb[k], to[k].bf, Xw, camd, to[k].o, to[k].in, cam)
+                         : eval_obs_at<2>(P, Rwb[k], twb[k], to[k].bf, Xw, camd, to[k].o, to[k].in, cam);
+        }
+    }
+    // k_eval: one observation per thread of TILE_OBS = 2 x 64; block_sum = wave sums, then 0 + wave 0 + wave 1
+    static_assert(UPD_TILE_OBS_PER_THREAD == 2 && TILE_OBS == 2 * UPD_THREADS, "k_eval's reduction tree");
+    const double s0 = wave_sum(rho[0]), s1 = wave_sum(rho[1]);
+    if (tid == 0) {
+        double s = 0.0;
+        s += s0;
+        s += s1;
+        P.chi_eval[tile] = s;
+    }
 }
 
 // The step and the trial state (block_solver.hpp:461-482 back-substitution, sparse_optimizer.cpp:422-435
@@ -2662,10 +2785,23 @@ constexpr int UPD_GP_SHM = 2 * 12 + 2 * KF_STRIDE + 2 * (KF_STRIDE + 12) + PREP_
 constexpr int UPD_KF_SHM = UPD_THREADS * (12 + KF_STRIDE);
 constexpr int UPD_SHM = UPD_GP_SHM > UPD_KF_SHM ? (UPD_GP_SHM > BS_SHM ? UPD_GP_SHM : BS_SHM)
                                                 : (UPD_KF_SHM > BS_SHM ? UPD_KF_SHM : BS_SHM);
-__global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lambda_arg, int sel, int gate, int jac) {
+template <bool WT>
+__device__ void prior_eval_t(const DevProblem& P, const double* __restrict__ kst, int idx);
+// eval (with P.fuse_eval): the trial state's errors too.  The producers of the pose samples (the GP pairs and KF
+// blocks) store the samples / KF states write-through and report once they are stored; the regular tiles, after
+// their back-substitution, and the motion-prior / velocity items (workgroups after the update's) wait for all
+// producers and evaluate: k_eval's work in the same launch.  The host fuses only when the whole grid is resident
+// at once (P.fuse_eval, set from the occupancy), so a waiting workgroup never holds a slot a producer needs,
+// whatever the dispatch order.  (Roles from an atomic ticket instead, for any grid size, cost one same-address
+// atomic per workgroup: +10 us per trial at config 1, +700 us at config 2, profiles/r4i_ab_fused_eval_ticket_rejected.txt.)
+__global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lambda_arg, int sel, int gate, int jac,
+                                                        int eval, unsigned epoch) {
     __shared__ double red[UPD_THREADS / 64];
     __shared__ double ushm[UPD_SHM];
+    __shared__ double ltr[TILE_LMS * 3];
     if (gated_off(P.ctl, gate)) return;
+    const bool fused = eval && P.fuse_eval;
+    const int role = blockIdx.x;
     // diagnostics (LBA_PHASE_TIMING): s_memrealtime start / end of each workgroup in slots 14 / 15 of the
     // sweep's stamp rows (k_update runs after the sweep; n_upd_blocks <= n_tiles is checked)
     unsigned long long* ustamp = (P.tdbg_lin && threadIdx.x == 0 && (int)blockIdx.x < P.n_tiles)
@@ -2680,8 +2816,14 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
     double* gps = P.gpsb[si ^ 1];
     const bool ok = (*P.info == 0);
     const int nkb = (P.n_kf + UPD_THREADS - 1) / UPD_THREADS;
-    if ((int)blockIdx.x < P.n_gp) {
-        const int i = blockIdx.x;
+    if (role >= P.n_upd_blocks) {   // (fused) motion-prior / velocity edges of the trial state: the KF blocks
+        const int nkb_ = (P.n_kf + UPD_THREADS - 1) / UPD_THREADS;
+        upd_wait(P, (int)threadIdx.x < nkb_ ? P.n_gp + (int)threadIdx.x : -1, epoch);
+        prior_eval_t<false>(P, ko, (role - P.n_upd_blocks) * UPD_THREADS + threadIdx.x);   // (plain loads: see eval_tile_trial)
+        return;
+    }
+    if (role < P.n_gp) {
+        const int i = role;
         double* kdl = ushm;                    // [2][12]
         double* kab = ushm + 2 * 12;           // [2][KF_STRIDE]
         double* kin = ushm + 2 * 12 + 2 * KF_STRIDE;   // [2][KF_STRIDE + 12]: the two KFs' states and steps,
@@ -2703,16 +2845,19 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
         }
         __syncthreads();
 #ifndef LBA_EXP_NO_GPPREP
-        gp_pair_prep(P, gps, i, kab, kab + KF_STRIDE, jac, ushm + 2 * 12 + 2 * KF_STRIDE + 2 * (KF_STRIDE + 12),
-                     ustamp ? P.tdbg_lin + (size_t)blockIdx.x * 16 + 5 : nullptr);
+        gp_pair_prep<true>(P, gps, i, kab, kab + KF_STRIDE, jac, ushm + 2 * 12 + 2 * KF_STRIDE + 2 * (KF_STRIDE + 12),
+                           ustamp ? P.tdbg_lin + (size_t)blockIdx.x * 16 + 5 : nullptr);
 #endif
-        if (threadIdx.x == 0) P.scale_part[blockIdx.x] = 0.0;
+        if (fused) upd_publish(P, role, epoch);
+        if (ustamp) ustamp[-1] = __builtin_amdgcn_s_memrealtime();   // (slot 13: published)
+        if (threadIdx.x == 0) P.scale_part[role] = 0.0;
         if (ustamp) ustamp[1] = __builtin_amdgcn_s_memrealtime();
         return;
     }
     double sc = 0.0;
-    if ((int)blockIdx.x < P.n_gp + nkb) {
-        const int k = (blockIdx.x - P.n_gp) * UPD_THREADS + threadIdx.x;
+    bool tile_eval = false;
+    if (role < P.n_gp + nkb) {
+        const int k = (role - P.n_gp) * UPD_THREADS + threadIdx.x;
         if (k < P.n_kf) {
             const int h = P.kf_hidx[k], xc = P.kf_cam[k];
             // this KF's b_p rows and their owners, loaded before the first store (see kf_trial_state)
@@ -2727,8 +2872,8 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
             double* kn = ushm + 12 * UPD_THREADS + KF_STRIDE * threadIdx.x;
             kf_trial_state(kst + (size_t)k * KF_STRIDE, kf_step(P, h, ok), d, kn);
             double* kw = ko + (size_t)k * KF_STRIDE;
-            for (int j = 0; j < KF_STRIDE; ++j) kw[j] = kn[j];
-            kf_pose_record(P, gps, k, kn);
+            for (int j = 0; j < KF_STRIDE; ++j) stv<true>(kw + j, kn[j]);   // (write-through: the fused evaluation)
+            kf_pose_record<true>(P, gps, k, kn);
             if (xc >= 0) {   // a free extrinsic: the trial state's camera record (Tcb, intrinsics, Ad(Tbc))
                 const double* c0 = P.camdb[si] + (size_t)xc * CAMD_STRIDE;
                 SE3 T;
@@ -2744,12 +2889,14 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
                     if (adds[j]) sc += d[j] * (lambda * d[j] + bph[j]);
                 }
         }
-    } else if ((int)blockIdx.x < P.n_gp + nkb + P.n_stiles) {
-        sc = bs_tile(P, blockIdx.x - P.n_gp - nkb, si, ok, lambda, lo, ushm,
-                     ustamp ? P.tdbg_lin + (size_t)blockIdx.x * 16 + 5 : nullptr);
+        if (fused) upd_publish(P, role, epoch);
+    } else if (role < P.n_gp + nkb + P.n_stiles) {
+        sc = bs_tile(P, role - P.n_gp - nkb, si, ok, lambda, lo, ushm,
+                     ustamp ? P.tdbg_lin + (size_t)blockIdx.x * 16 + 5 : nullptr, fused ? ltr : nullptr);
+        tile_eval = fused;
     } else {
         // heavy landmarks (device indices n_lm - n_heavy ..): through their merged Hpl blocks
-        const int l = P.n_lm - P.n_heavy + (blockIdx.x - P.n_gp - nkb - P.n_stiles) * UPD_THREADS + threadIdx.x;
+        const int l = P.n_lm - P.n_heavy + (role - P.n_gp - nkb - P.n_stiles) * UPD_THREADS + threadIdx.x;
         if (l < P.n_lm) {
             double xl[3];
             double* xd = P.x + P.np + 3 * (size_t)l;
@@ -2779,12 +2926,28 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
         }
     }
     const double s = block_sum<UPD_THREADS>(sc, red);
-    if (threadIdx.x == 0) P.scale_part[blockIdx.x] = s;
+    if (threadIdx.x == 0) P.scale_part[role] = s;
+    if (tile_eval) {
+        TrialObs to[UPD_TILE_OBS_PER_THREAD];
+        eval_tile_prefetch(P, role - P.n_gp - nkb, si, to);
+        // the producers of the tile's pose samples (one sample per lane: TILE_SMP = UPD_THREADS)
+        const int tl = role - P.n_gp - nkb;
+        static_assert(TILE_SMP <= UPD_THREADS, "one tile sample per lane");
+        const int prod = (int)threadIdx.x < P.tile_nsmp[tl] ? P.smp_prod[P.tsm_smp[P.tile_smp0[tl] + threadIdx.x]] : -1;
+        if (ustamp) ustamp[-2] = __builtin_amdgcn_s_memrealtime();   // (slot 12: waiting)
+        upd_wait(P, prod, epoch);   // (its barrier also completes ltr)
+        if (ustamp) ustamp[-1] = __builtin_amdgcn_s_memrealtime();   // (slot 13: samples in)
+        eval_tile_trial(P, role - P.n_gp - nkb, si, ltr, to);
+    }
     if (ustamp) ustamp[1] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ------------------------------------------------------------------------------------------------
-__device__ void prior_eval(const DevProblem& P, const double* __restrict__ kst, int idx);
+template <bool WT>
+__device__ void prior_eval_t(const DevProblem& P, const double* __restrict__ kst, int idx);
+__device__ __forceinline__ void prior_eval(const DevProblem& P, const double* __restrict__ kst, int idx) {
+    prior_eval_t<false>(P, kst, idx);
+}
 
 // Robust chi2 of the state: one workgroup per observation tile, then workgroups of TILE_OBS prior /
 // velocity edges.  (The trial summary stays a separate k_finalize launch: having the last workgroup
@@ -2817,11 +2980,17 @@ __global__ __launch_bounds__(TILE_OBS) void k_eval(DevProblem P, int sel, int ga
     }
 }
 
-// motion-prior / velocity edge idx: robust chi2 of the state kst into chi_eval
-__device__ void prior_eval(const DevProblem& P, const double* __restrict__ kst, int idx) {
+// motion-prior / velocity edge idx: robust chi2 of the state kst into chi_eval (WT: the state read sc1, written
+// in this launch: k_update's fused evaluation)
+template <bool WT>
+__device__ void prior_eval_t(const DevProblem& P, const double* __restrict__ kst, int idx) {
     if (idx < P.n_prior) {
-        const double* ka = kst + (size_t)P.pri_a[idx] * KF_STRIDE;
-        const double* kb = kst + (size_t)P.pri_b[idx] * KF_STRIDE;
+        double ka[14], kb[14];
+#pragma unroll
+        for (int j = 0; j < 14; ++j) {
+            ka[j] = ldv<WT>(kst + (size_t)P.pri_a[idx] * KF_STRIDE + j);
+            kb[j] = ldv<WT>(kst + (size_t)P.pri_b[idx] * KF_STRIDE + j);
+        }
         double e[12], Om[144];
         prior_error_jac<double>(load_se3(ka), ka + 7, ka[13], load_se3(kb), kb + 7, kb[13], e, nullptr, nullptr);
         qi_inv(P.qcinv, kb[13] - ka[13], Om);
@@ -2836,14 +3005,15 @@ __device__ void prior_eval(const DevProblem& P, const double* __restrict__ kst, 
         P.chi_eval[P.n_tiles + idx] = r0;
     } else if (idx < P.n_prior + P.n_vel) {
         const int v = idx - P.n_prior;
-        const double ev = kst[(size_t)P.vel_kf[v] * KF_STRIDE + 9];
+        const double ev = ldv<WT>(kst + (size_t)P.vel_kf[v] * KF_STRIDE + 9);
         P.chi_eval[P.n_tiles + idx] = ev * (P.qcinv[14] * ev);
     } else if (idx < P.n_prior + P.n_vel + P.n_eprior) {   // EdgeExtrinsicPrior: e^T Om e
         const int q = idx - P.n_prior - P.n_vel;
         const double* ed = P.ep_data + 16 * (size_t)q;
         const double* kx = kst + (size_t)P.ep_kf[q] * KF_STRIDE;
         double e[3];
-        ext_prior_error_jac(Quat{kx[0], kx[1], kx[2], kx[3]}, Quat{ed[0], ed[1], ed[2], ed[3]}, e, nullptr);
+        ext_prior_error_jac(Quat{ldv<WT>(kx), ldv<WT>(kx + 1), ldv<WT>(kx + 2), ldv<WT>(kx + 3)},
+                            Quat{ed[0], ed[1], ed[2], ed[3]}, e, nullptr);
         double chi = 0.0;
         for (int i = 0; i < 3; ++i) {
             double s = 0.0;
@@ -3137,8 +3307,20 @@ void launch_cholesky_part(const DevProblem& P, int part, unsigned epoch, hipStre
     }
     launch_flow(a, P, s, e0, e1);
 }
-void launch_update(const DevProblem& P, double lambda, int sel, int gate, int jac, hipStream_t s) {
-    hipLaunchKernelGGL(k_update, dim3(P.n_upd_blocks), dim3(UPD_THREADS), 0, s, P, lambda, sel, gate, jac);
+int update_grid(const DevProblem& P, int eval) {
+    return P.n_upd_blocks + ((eval && P.fuse_eval) ? cdiv(P.n_prior + P.n_vel, UPD_THREADS) : 0);
+}
+int update_resident_blocks(int device) {
+    int per_cu = 0, ncu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_update, UPD_THREADS, 0) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
+    return per_cu * ncu;
+}
+void launch_update(const DevProblem& P, double lambda, int sel, int gate, int jac, hipStream_t s, int eval,
+                   unsigned epoch) {
+    const int fused = eval && P.fuse_eval;
+    const int nb = P.n_upd_blocks + (fused ? cdiv(P.n_prior + P.n_vel, UPD_THREADS) : 0);
+    hipLaunchKernelGGL(k_update, dim3(nb), dim3(UPD_THREADS), 0, s, P, lambda, sel, gate, jac, fused, epoch);
 }
 void launch_eval(const DevProblem& P, int sel, int gate, unsigned long long seq, int mode, hipStream_t s) {
     const int nb = P.n_tiles + cdiv(P.n_prior + P.n_vel + P.n_eprior, TILE_OBS);
