@@ -97,6 +97,8 @@ def lib():
             L.lba_solver_flops.argtypes = [vp, _dp]
         L.lba_device_bytes.argtypes = [vp]
         L.lba_device_bytes.restype = ctypes.c_int64
+        L.lba_setup_phases.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int32]
+        L.lba_setup_phases.restype = ctypes.c_int32
         L.lba_setup_host_profile.argtypes = [ctypes.POINTER(LbaConfig), vp, ctypes.c_int32, vp, ctypes.c_int32, vp,
                                              ctypes.c_int32, vp, ctypes.c_int32, vp, ctypes.c_int32, vp, ctypes.c_int32,
                                              _dp, _ip]
@@ -116,7 +118,7 @@ def exported_symbols():
             "lba_optimize", "lba_get_state", "lba_set_state", "lba_eval", "lba_trial_chi2", "lba_linearize", "lba_solve_step",
             "lba_pose_dim", "lba_set_partition", "lba_rccl_unique_id", "lba_set_partition_rccl", "lba_group_create",
             "lba_group_destroy", "lba_set_partition_group", "lba_get_cams", "lba_set_farm", "lba_set_farm_rccl",
-            "lba_set_farm_group", "lba_farm_plan", "lba_farm_exchange", "lba_farm_match", "lba_solver_info", "lba_solver_flops", "lba_device_bytes",
+            "lba_set_farm_group", "lba_farm_plan", "lba_farm_exchange", "lba_farm_match", "lba_solver_info", "lba_solver_flops", "lba_device_bytes", "lba_setup_phases",
             "lba_setup_host_profile", "lba_debug_pool_stress", "lba_debug_lie", "lba_partition_assign", "lba_kf_owner", "lba_split_info"]
 
 
@@ -354,6 +356,15 @@ class Problem:
         out = np.zeros(2, dtype=np.float64)
         self._check(lib().lba_solver_flops(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
         return float(out[0]), float(out[1])
+
+    SETUP_PHASES = ("order_pairs", "tiles", "slots_state", "upload", "solve_layout")
+
+    def setup_phases(self):
+        """lba_setup_phases: {phase: ms} of the last set-up."""
+        out = np.zeros(8)
+        k = lib().lba_setup_phases(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), 8)
+        self._check(min(k, 0))
+        return dict(zip(self.SETUP_PHASES, out[:k].tolist()))
 
     def device_bytes(self):
         """lba_device_bytes: device memory held by the problem's buffers."""

@@ -265,6 +265,13 @@ struct DevProblem {
     int fuse_eval;
     int* upd_flag;
     const int* smp_prod;
+    // fused expansion + assembly (k_exp_asm; no heavy landmarks, not partitioned): exp_flag [n_smp] a pose sample's
+    // epoch once its Hpp / b_p pieces are stored; hs_prod [n_hslots] / gs_prod [n_gslots] the sample that writes
+    // each slot (< 0: an edge item of k_lin_schur)
+    int fuse_asm;
+    int* exp_flag;
+    const int* hs_prod;
+    const int* gs_prod;
     double* kbuf[2];        // kf state buffers [n_kf][KF_STRIDE] (current / trial, see LMCtl::cur)
     double* lbuf[2];        // landmark state buffers [n_lm][3]
     LMCtl* ctl;             // queued-optimisation controller
@@ -325,6 +332,8 @@ void launch_lin_schur(const DevProblem& P, int sel, int gate, double lambda, int
 void launch_expand(const DevProblem& P, int sel, int gate, double lambda, int schur, hipStream_t s);
 enum { ASM_SCHUR = 1, ASM_FULL = 2, ASM_DIAG = 4 };
 void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hipStream_t s);
+// k_expand (schur) + k_assemble (ASM_SCHUR) of a trial in one launch (P.fuse_asm); epoch: one more than the last
+void launch_exp_asm(const DevProblem& P, int sel, int gate, double lambda, unsigned epoch, hipStream_t s);
 // (fused flow: sel / lambda of the expansion and assembly it runs first)
 void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s, hipEvent_t e0 = nullptr,
                            hipEvent_t e1 = nullptr, int sel = 0, double lambda = 0.0);

@@ -95,6 +95,7 @@ struct lba_problem {
     unsigned long long fin_seq = 0;
     unsigned cf_epoch = 0;        // launches of the dataflow factorisation (its flags hold the epoch)
     unsigned upd_epoch = 0;       // launches of k_update (the fused evaluation's producer flags hold the epoch)
+    unsigned asm_epoch = 0;       // launches of k_exp_asm (its expansions' flags hold the epoch)
     bool gps_fresh[2] = {false, false};   // state buffer s has its pose samples with Jacobian factors
     double lambda = -1.0, ni = 2.0;
     int nBad = 0;
@@ -1192,6 +1193,16 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             gl[2] = gfill[x]++;
         }
     }
+    // the pose sample that writes each Hpp / b_p slot (fused expansion + assembly; -1: an edge item)
+    std::vector<int> hs_prod(std::max(hs0[n_ublocks], 1), -1), gs_prod(std::max(gs0[n_pb], 1), -1);
+    for (int en = 0; en < n_smp; ++en) {
+        const int* sl = seg_slot.data() + SEG_STRIDE * (size_t)en;
+        const int* gl = seg_gslot.data() + GSEG_STRIDE * (size_t)en;
+        for (int q : {0, 1, 2, 4, 5, 6})
+            if (sl[q] >= 0) hs_prod[sl[q]] = en;
+        for (int q = 0; q < 3; ++q)
+            if (gl[q] >= 0) gs_prod[gl[q]] = en;
+    }
     // Schur partial blocks per (tile, KF pair) and rhs partials per (tile, KF)
     std::vector<int> scnt(n_ublocks + 1, 0), gpcnt(n_pb + 1, 0);
     for (int s = 0; s < n_sent; ++s) scnt[ublock_id(n_pb, sent_k1[s], sent_k2[s])]++;
@@ -1922,6 +1933,14 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         HIPCHK(hipMemsetAsync(D.upd_flag, 0, sizeof(int) * (D.n_gp + nkb + 1), p->stream));
         p->upd_epoch = 0;
     }
+    // k_expand + k_assemble of a trial in one launch (LBA_NO_FUSED_ASM: two): not with heavy landmarks (their merge
+    // is k_expand's), partitioned problems or the fused factorisation flow (which assembles S itself)
+    D.fuse_asm = (n_heavy == 0 && p->part_n == 0 && !D.cf_fused && std::getenv("LBA_NO_FUSED_ASM") == nullptr) ? 1 : 0;
+    D.hs_prod = dupload(p, hs_prod);
+    D.gs_prod = dupload(p, gs_prod);
+    D.exp_flag = dalloc<int>(p, std::max(D.n_smp, 1));
+    HIPCHK(hipMemsetAsync(D.exp_flag, 0, sizeof(int) * std::max(D.n_smp, 1), p->stream));
+    p->asm_epoch = 0;
     D.info = dalloc<int>(p, 1);
     D.ctl = dalloc<LMCtl>(p, 1);
     D.fin = dalloc<double>(p, 4);
@@ -2051,8 +2070,12 @@ void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs, bool s
     if (evs) HIPCHK(hipEventRecord(evs[1], p->stream));
     // (fused flow: the expansion and the assembly are k_chol_flow's first tasks; the phase events then time
     // them with the solve)
-    if (!D.cf_fused) launch_expand(D, p->cur, GATE_NONE, lambda, 1, p->stream);
-    assemble_layout(p, lambda, ASM_SCHUR, GATE_NONE, !D.cf_fused);
+    if (D.fuse_asm) {
+        launch_exp_asm(D, p->cur, GATE_NONE, lambda, ++p->asm_epoch, p->stream);
+    } else {
+        if (!D.cf_fused) launch_expand(D, p->cur, GATE_NONE, lambda, 1, p->stream);
+        assemble_layout(p, lambda, ASM_SCHUR, GATE_NONE, !D.cf_fused);
+    }
     if (evs) HIPCHK(hipEventRecord(evs[2], p->stream));
     launch_solve(p, sweep ? p->ev[8] : nullptr, sweep ? p->ev[9] : nullptr, p->cur, lambda);
     if (evs) HIPCHK(hipEventRecord(evs[3], p->stream));
@@ -2157,8 +2180,12 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
             }
             launch_lin_schur(D, SEL_CUR, GATE_TRIAL, LAMBDA_CTL, LS_SCHUR | LS_EDGES, p->stream, qe ? qe[0] : nullptr,
                              qe ? qe[1] : nullptr);
-            if (!D.cf_fused) launch_expand(D, SEL_CUR, GATE_TRIAL, LAMBDA_CTL, 1, p->stream);
-            assemble_layout(p, LAMBDA_CTL, ASM_SCHUR, GATE_NONE, !D.cf_fused);
+            if (D.fuse_asm) {
+                launch_exp_asm(D, SEL_CUR, GATE_TRIAL, LAMBDA_CTL, ++p->asm_epoch, p->stream);
+            } else {
+                if (!D.cf_fused) launch_expand(D, SEL_CUR, GATE_TRIAL, LAMBDA_CTL, 1, p->stream);
+                assemble_layout(p, LAMBDA_CTL, ASM_SCHUR, GATE_NONE, !D.cf_fused);
+            }
             launch_solve(p, qe ? qe[2] : nullptr, qe ? qe[3] : nullptr, SEL_CUR, LAMBDA_CTL);
             // the step, the trial state and its pose samples with their Jacobian factors: the next
             // trial's linearisation reads them (no preparation launch)
@@ -2617,6 +2644,13 @@ int lba_setup_host_profile(const lba_config* cfg, const lba_kf* kfs, int32_t n_k
         counts[4] = (int32_t)p.setup_hash;
     }
     return LBA_OK;
+}
+
+int32_t lba_setup_phases(const lba_problem* p, double* ms, int32_t n) {
+    if (!p || n < 0 || (n > 0 && !ms)) return LBA_E_ARG;
+    const int32_t k = std::min<int32_t>(n, (int32_t)p->setup_ms.size());
+    for (int32_t i = 0; i < k; ++i) ms[i] = p->setup_ms[i];
+    return k;
 }
 
 int64_t lba_device_bytes(const lba_problem* p) {

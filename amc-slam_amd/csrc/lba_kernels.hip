@@ -1124,18 +1124,48 @@ __device__ __forceinline__ double slot_sum(const double* __restrict__ x, int s0,
     return (v0 + v1) + (v2 + v3);
 }
 
-__global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, double lambda_arg, int flags, int gate) {
-    __shared__ double red[144 * RED_GROUPS];
+// (fused expansion + assembly) wait until the pose samples that write the slots [s0, s1) of a target (prod_of: the
+// sample of each slot, < 0: written by an earlier launch) have published this launch's epoch; bounded, as
+// k_chol_flow's waits
+__device__ __forceinline__ void exp_wait(const DevProblem& P, const int* prod_of, int s0, int s1, unsigned epoch) {
+    for (int s = s0 + (int)threadIdx.x; s < s1; s += (int)blockDim.x) {
+        const int q = prod_of[s];
+        if (q < 0) continue;
+        unsigned spins = 0;
+        while ((unsigned)__hip_atomic_load((gi32_t*)(P.exp_flag + q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 20)) break;   // (~0.5 s: never expected)
+        }
+    }
+    __syncthreads();
+}
+
+// One output of the assembly: S block asm_list[item] (item < n_asm) or the rhs of pose block item - n_asm.
+// FUSED (k_exp_asm): the Hpp / b_p partials come from expansion workgroups of the same launch, so the Schur
+// partials (an earlier launch's) are summed first, then the block waits for its samples (wait: the launch is not
+// gated off) and sums theirs -- the same operations in the same order as k_assemble, so S / bS are bitwise its.
+// The hslab slots of one block fill whole 128-byte lines of their own (1152 B each) and nothing reads them
+// before the wait, so plain loads see the write-through stores; gslab slots (96 B) share lines across pose
+// blocks, so they are loaded sc1.
+template <bool FUSED>
+__device__ __forceinline__ void assemble_item(const DevProblem& P, int item, double lambda, int flags, double* red, bool wait,
+                                              unsigned epoch) {
     const int tid = threadIdx.x;
-    if (gated_off(P.ctl, gate)) return;
-    const double lambda = damping(P, lambda_arg);
     const int n = P.npad;   // leading dimension of S
-    if ((int)blockIdx.x < P.n_asm) {
-        const int ub = P.asm_list[blockIdx.x];
+    if (item < P.n_asm) {
+        const int ub = P.asm_list[item];
         const int bi = P.ub_i[ub], bj = P.ub_j[ub];
         const int e = tid % 144, g = tid / 144;
-        double v = slot_sum<RED_GROUPS, 144>(P.hslab, P.hs0[ub] + g, P.hs0[ub + 1], e);
-        if (flags & ASM_SCHUR) v -= slot_sum<RED_GROUPS, 144>(P.sslab, P.ss0[ub] + g, P.ss0[ub + 1], e);
+        double v;
+        if constexpr (FUSED) {
+            const double sv = slot_sum<RED_GROUPS, 144>(P.sslab, P.ss0[ub] + g, P.ss0[ub + 1], e);
+            if (wait) exp_wait(P, P.hs_prod, P.hs0[ub], P.hs0[ub + 1], epoch);
+            v = slot_sum<RED_GROUPS, 144>(P.hslab, P.hs0[ub] + g, P.hs0[ub + 1], e);
+            v -= sv;
+        } else {
+            v = slot_sum<RED_GROUPS, 144>(P.hslab, P.hs0[ub] + g, P.hs0[ub + 1], e);
+            if (flags & ASM_SCHUR) v -= slot_sum<RED_GROUPS, 144>(P.sslab, P.ss0[ub] + g, P.ss0[ub + 1], e);
+        }
         red[tid] = v;
         __syncthreads();
         if (g == 0) {
@@ -1155,7 +1185,7 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
                 P.S[s_elem(P, max(rh, ch), min(rh, ch))] = t;
             }
         }
-        if ((flags & ASM_SCHUR) && blockIdx.x == 0)   // padding rows: identity (their owner)
+        if ((flags & ASM_SCHUR) && item == 0)   // padding rows: identity (their owner)
             for (int r = P.np + tid; r < n; r += 144 * RED_GROUPS) {
                 if (!row_adds(P, r)) continue;
                 const int rh = P.rpos[r];
@@ -1163,10 +1193,17 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
                 P.bS[rh] = 0.0;
             }
     } else {
-        const int k = blockIdx.x - P.n_asm;
+        const int k = item - P.n_asm;
         const int e = tid % 12, g = tid / 12;   // 48 groups
-        const double v = slot_sum<48, 12>(P.gslab, P.gs0[k] + g, P.gs0[k + 1], e);
-        const double w = (flags & ASM_SCHUR) ? slot_sum<48, 12>(P.gpslab, P.gps0[k] + g, P.gps0[k + 1], e) : 0.0;
+        double v, w;
+        if constexpr (FUSED) {
+            w = slot_sum<48, 12>(P.gpslab, P.gps0[k] + g, P.gps0[k + 1], e);
+            if (wait) exp_wait(P, P.gs_prod, P.gs0[k], P.gs0[k + 1], epoch);
+            v = slot_sum<48, 12, true>(P.gslab, P.gs0[k] + g, P.gs0[k + 1], e);
+        } else {
+            v = slot_sum<48, 12>(P.gslab, P.gs0[k] + g, P.gs0[k + 1], e);
+            w = (flags & ASM_SCHUR) ? slot_sum<48, 12>(P.gpslab, P.gps0[k] + g, P.gps0[k + 1], e) : 0.0;
+        }
         red[tid] = v;
         __syncthreads();
         double bpv = 0.0;
@@ -1185,6 +1222,36 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
             P.bS[rh] = bpv - t;   // bS = b_p - sum Hpl Dinv bl (factorisation order)
         }
     }
+}
+
+__global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, double lambda_arg, int flags, int gate) {
+    __shared__ double red[144 * RED_GROUPS];
+    if (gated_off(P.ctl, gate)) return;
+    assemble_item<false>(P, blockIdx.x, damping(P, lambda_arg), flags, red, false, 0);
+}
+
+// k_expand's sample expansions and k_assemble's outputs of a trial in one launch (P.fuse_asm: no heavy landmarks,
+// not partitioned): workgroups [0, n_smp) expand a pose sample each (sample_expand, its first PRI_THREADS threads),
+// store its Hpp / b_p pieces write-through and publish the launch's epoch in exp_flag; the assembly workgroups
+// after them sum their Schur partials meanwhile and then wait for just the samples their slots come from.  The
+// expansions are the lowest workgroup ids (dispatched first).  gate: the expansions' (k_expand's) gate -- when it
+// holds the launch off, the assembly still runs (as k_assemble does, on scratch) without waiting.
+__global__ __launch_bounds__(144 * RED_GROUPS) void k_exp_asm(DevProblem P, int sel, int gate, double lambda_arg, unsigned epoch) {
+    constexpr int SHM = PRI_SHM > 144 * RED_GROUPS ? PRI_SHM : 144 * RED_GROUPS;
+    __shared__ double shm[SHM];
+    const bool off = gated_off(P.ctl, gate);
+    const int tid = threadIdx.x;
+    if ((int)blockIdx.x < P.n_smp) {
+        if (off) return;
+        const int si = state_idx(P, sel);
+        double *Msh = shm, *Nsh = Msh + 144, *MN = Nsh + 216, *part = MN + 216;
+        sample_expand<true>(P, P.gpsb[si], P.camdb[si], blockIdx.x, Msh, Nsh, MN, part, tid < PRI_THREADS ? tid : (1 << 20));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store((gi32_t*)(P.exp_flag + blockIdx.x), (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    assemble_item<true>(P, blockIdx.x - P.n_smp, damping(P, lambda_arg), ASM_SCHUR, shm, !off, epoch);
 }
 
 // The fused flow's assembly work items (k_chol_flow prefix tasks, 256 threads): k_assemble's sums with the
@@ -3258,6 +3325,10 @@ void launch_lin_schur(const DevProblem& P, int sel, int gate, double lambda, int
 void launch_expand(const DevProblem& P, int sel, int gate, double lambda, int schur, hipStream_t s) {
     const int n = P.n_smp + P.n_heavy;
     if (n) hipLaunchKernelGGL(k_expand, dim3(n), dim3(PRI_THREADS), 0, s, P, sel, gate, lambda, schur);
+}
+void launch_exp_asm(const DevProblem& P, int sel, int gate, double lambda, unsigned epoch, hipStream_t s) {
+    const int n = P.n_smp + P.n_asm + P.n_pb;
+    if (n) hipLaunchKernelGGL(k_exp_asm, dim3(n), dim3(144 * RED_GROUPS), 0, s, P, sel, gate, lambda, epoch);
 }
 void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hipStream_t s) {
     const int n = P.n_asm + P.n_pb;

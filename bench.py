@@ -399,7 +399,7 @@ def main():
                           "timed region",
                 "rank_flops_share": si["rank_flops"] / max(si["system_flops"], 1.0)}
 
-    phase, set_problem_ms = None, None
+    phase, set_problem_ms, set_problem_phases = None, None, None
     if world == 1:
         # phase breakdown from a separate, untimed run with every phase evented
         prob.close()
@@ -415,7 +415,7 @@ def main():
         # outside the timed region above) + optimize(window_iters): time a set_problem on the engine
         kfs, lm, obs, pri, vel, cams = ph._keep
         L = amc_lba.lib()
-        sp = []   # (median of seven set-ups: one sample is at the mercy of the host's scheduling)
+        sp, sp_ph = [], []   # (median of seven set-ups: one sample is at the mercy of the host's scheduling)
         for _ in range(7):
             t_sp = time.perf_counter()
             rc = L.lba_set_problem(ph.h, amc_lba.ptr(kfs), len(kfs), amc_lba.ptr(lm), len(lm), amc_lba.ptr(obs),
@@ -423,7 +423,10 @@ def main():
                                    len(cams))
             torch.cuda.synchronize()
             sp.append((time.perf_counter() - t_sp) * 1e3 if rc == 0 else float("nan"))
+            if rc == 0:
+                sp_ph.append(ph.setup_phases())
         set_problem_ms = float(np.median(sp)) if all(np.isfinite(sp)) else None
+        set_problem_phases = ({k: float(np.median([d[k] for d in sp_ph])) for k in sp_ph[0]} if sp_ph else None)
         ph.close()
     if rank == 0:
         # window farm: every rank runs its own window (weak scaling); global BA: one problem (strong)
@@ -500,7 +503,8 @@ def main():
         if comm is not None:
             line["collective"] = comm
         if world == 1 and not gba:   # LocalGPBA-equivalent calls (optimize(window_iters))
-            calls = {"optimize_calls_per_s": value / args.window_iters, "set_problem_ms": set_problem_ms}
+            calls = {"optimize_calls_per_s": value / args.window_iters, "set_problem_ms": set_problem_ms,
+                     "set_problem_phases_ms": set_problem_phases}
             if set_problem_ms is not None:
                 calls["calls_per_s_with_set_problem"] = 1.0 / (args.window_iters / value + set_problem_ms * 1e-3)
             line["localgpba_calls"] = calls

@@ -41,3 +41,12 @@ if tl.any():
     print(f"  tiles: waiting from p50 {np.median(us(lin[tl, 12])):.2f}  max {us(lin[tl, 12]).max():.2f};  samples in p50 "
           f"{np.median(us(lin[tl, 13])):.2f}  max {us(lin[tl, 13]).max():.2f};  end p50 {np.median(us(en[tl])):.2f}  max "
           f"{us(en[tl]).max():.2f} us")
+# the GP pairs' preparation phases (gp_pair_prep's stamps 0..5 in slots 5..10): pair chain (log / Ad), Jr^-1, w2 / A1,
+# B1 / D, the sample poses + Jr (first chunk), the N blocks (last chunk)
+names = ("log+Ad", "Jr^-1", "w2/A1", "B1/D", "samples", "N")
+print("  GP pair prep stamps p50 (us): " + "  ".join(f"{n} {np.median(us(lin[gp, 5 + k])):.2f}" for k, n in enumerate(names)))
+kb = np.arange(nt) == gp.sum()   # the first KF block (its end = its publication)
+print(f"  KF block (row {gp.sum()}): start {us(st[kb]).max():.2f} end {us(en[kb]).max():.2f} us")
+if tl.any():
+    print(f"  tiles' back-substitution stamps: t_s done p50 {np.median(us(lin[tl, 5])):.2f}, landmarks done p50 "
+          f"{np.median(us(lin[tl, 6])):.2f} max {us(lin[tl, 6]).max():.2f} us")
