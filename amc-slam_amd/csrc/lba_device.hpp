@@ -35,7 +35,14 @@ constexpr int KFP_STRIDE = 12;      // Rwb(9) twb(3)
 
 // tile limits (one workgroup of TILE_OBS threads per tile)
 constexpr int TILE_OBS = 128;
-constexpr int UPD_BLOCK_KFS = 64;   // keyframes per KF-block workgroup of k_update (its UPD_THREADS)
+// in-launch hand-off flags (k_update's producers, k_exp_asm's expansions): one per 128-byte line, so the polls of
+// different producers' flags do not queue on one line
+#ifndef LBA_FLAG_STRIDE
+#define LBA_FLAG_STRIDE 32
+#endif
+constexpr int FLAG_STRIDE = LBA_FLAG_STRIDE;   // ints
+constexpr int UPD_BLOCK_KFS = 64;
+constexpr int TS_STRIDE = 16;        // doubles per pose sample's t_s record (one 128-byte line)   // keyframes per KF-block workgroup of k_update (its UPD_THREADS)
 constexpr int TILE_ROWS = 288;
 constexpr int TILE_PAIRS = 128;
 constexpr int TILE_LMS = 64;

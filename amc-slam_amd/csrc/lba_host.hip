@@ -1929,8 +1929,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             for (int s = gp_s0[g]; s < gp_s0[g + 1]; ++s) prod[s] = g;
         for (int k = 0; k < n_kfs; ++k) prod[D.n_gps + k] = D.n_gp + k / UPD_BLOCK_KFS;
         D.smp_prod = dupload(p, prod);
-        D.upd_flag = dalloc<int>(p, D.n_gp + nkb + 1);
-        HIPCHK(hipMemsetAsync(D.upd_flag, 0, sizeof(int) * (D.n_gp + nkb + 1), p->stream));
+        D.upd_flag = dalloc<int>(p, (size_t)FLAG_STRIDE * (D.n_gp + nkb + 1));
+        HIPCHK(hipMemsetAsync(D.upd_flag, 0, sizeof(int) * FLAG_STRIDE * (D.n_gp + nkb + 1), p->stream));
         p->upd_epoch = 0;
     }
     // k_expand + k_assemble of a trial in one launch (LBA_NO_FUSED_ASM: two): not with heavy landmarks (their merge
@@ -1938,8 +1938,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.fuse_asm = (n_heavy == 0 && p->part_n == 0 && !D.cf_fused && std::getenv("LBA_NO_FUSED_ASM") == nullptr) ? 1 : 0;
     D.hs_prod = dupload(p, hs_prod);
     D.gs_prod = dupload(p, gs_prod);
-    D.exp_flag = dalloc<int>(p, std::max(D.n_smp, 1));
-    HIPCHK(hipMemsetAsync(D.exp_flag, 0, sizeof(int) * std::max(D.n_smp, 1), p->stream));
+    D.exp_flag = dalloc<int>(p, (size_t)FLAG_STRIDE * std::max(D.n_smp, 1));
+    HIPCHK(hipMemsetAsync(D.exp_flag, 0, sizeof(int) * FLAG_STRIDE * std::max(D.n_smp, 1), p->stream));
     p->asm_epoch = 0;
     D.info = dalloc<int>(p, 1);
     D.ctl = dalloc<LMCtl>(p, 1);
@@ -2646,7 +2646,7 @@ int lba_setup_host_profile(const lba_config* cfg, const lba_kf* kfs, int32_t n_k
     return LBA_OK;
 }
 
-int32_t lba_setup_phases(const lba_problem* p, double* ms, int32_t n) {
+int lba_setup_phases(const lba_problem* p, double* ms, int32_t n) {
     if (!p || n < 0 || (n > 0 && !ms)) return LBA_E_ARG;
     const int32_t k = std::min<int32_t>(n, (int32_t)p->setup_ms.size());
     for (int32_t i = 0; i < k; ++i) ms[i] = p->setup_ms[i];

@@ -266,10 +266,15 @@ constexpr int PREP_PR = (sizeof(GPPair) / sizeof(double) + 1) & ~1;
 constexpr int PREP_SHM = PREP_PR + 36 + 36 + 8 + PREP_SCHUNK * (18 + 9 + 9 + 3);
 // WT: the sample poses (Rwb, twb) are stored write-through (sc1), for readers in other workgroups of the same
 // launch (k_update's fused evaluation)
-template <bool WT = false>
+// pub (optional): called by every thread once the last chunk's sample poses are stored (before their Jacobian
+// factors: k_update's fused evaluation reads only the poses), to publish them
+struct NoPub {
+    __device__ void operator()() const {}
+};
+template <bool WT = false, typename Pub = NoPub>
 __device__ __forceinline__ void gp_pair_prep(const DevProblem& P, double* gps, int i, const double* ka,
                                              const double* kb, int jac, double* shm,
-                                             unsigned long long* pst = nullptr) {
+                                             unsigned long long* pst = nullptr, Pub pub = Pub()) {
     GPPair& pr = *reinterpret_cast<GPPair*>(shm);
     double* AdI = shm + PREP_PR;
     double* ad2 = AdI + 36;
@@ -328,17 +333,20 @@ __device__ __forceinline__ void gp_pair_prep(const DevProblem& P, double* gps, i
     for (int c0 = s0; c0 < s1; c0 += PREP_SCHUNK) {
         const int ns = min(PREP_SCHUNK, s1 - c0);
         // one lane per sample: the interpolated pose T1 exp(xi) (gp_sample_pose), Ad(exp(xi)^-1), Jr(xi)
+        double xi[6];
+        GPScalars g;
+        SE3 E;
         if (tid < ns) {
             GPSample* S = reinterpret_cast<GPSample*>(gps + (size_t)(c0 + tid) * GPS_STRIDE);
-            double xi[6];
-            GPScalars g;
-            SE3 E;
             double Rl[9], tl[3];
             gp_sample_pose(pr, c0 == s0 ? t_first : P.gps_t[c0 + tid], Rl, tl, xi, &g, &E);
 #pragma unroll
             for (int j = 0; j < 9; ++j) stv<WT>(S->Rwb + j, Rl[j]);
 #pragma unroll
             for (int j = 0; j < 3; ++j) stv<WT>(S->twb + j, tl[j]);
+        }
+        if (c0 + PREP_SCHUNK >= s1) pub();   // (uniform: the last chunk)
+        if (tid < ns) {
             if (jac) {
                 const SE3 Em = se3_inv(E);                  // Ad(exp(-xi)) = [R', t'^ R'; 0, R']
                 double Ht[9];
@@ -1132,7 +1140,7 @@ __device__ __forceinline__ void exp_wait(const DevProblem& P, const int* prod_of
         const int q = prod_of[s];
         if (q < 0) continue;
         unsigned spins = 0;
-        while ((unsigned)__hip_atomic_load((gi32_t*)(P.exp_flag + q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+        while ((unsigned)__hip_atomic_load((gi32_t*)(P.exp_flag + (size_t)FLAG_STRIDE * q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
             __builtin_amdgcn_s_sleep(2);
             if (++spins > (1u << 20)) break;   // (~0.5 s: never expected)
         }
@@ -1248,7 +1256,7 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_exp_asm(DevProblem P, int 
         sample_expand<true>(P, P.gpsb[si], P.camdb[si], blockIdx.x, Msh, Nsh, MN, part, tid < PRI_THREADS ? tid : (1 << 20));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) __hip_atomic_store((gi32_t*)(P.exp_flag + blockIdx.x), (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) __hip_atomic_store((gi32_t*)(P.exp_flag + (size_t)FLAG_STRIDE * blockIdx.x), (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
     assemble_item<true>(P, blockIdx.x - P.n_smp, damping(P, lambda_arg), ASM_SCHUR, shm, !off, epoch);
@@ -2615,6 +2623,25 @@ __device__ __forceinline__ void bs_obs(const DevProblem& P, const double* gps, c
     for (int a = 0; a < 3; ++a) v[a] *= s;
 }
 
+// Row r of a pose sample's step t_s = N_s [x_a; x_b] (+ the extrinsic factor on x_e): N column c at 12 + 6 c; bk: the
+// sample's pose blocks (a, b, extrinsic) and camera.  (Formed per sample once, by k_update's GP-pair / KF-block
+// workgroups, and handed to the tiles through their flags, it made the fused k_update slower: the producers' chains
+// are the launch's other critical path, profiles/r4u_ab_ts_per_sample_rejected.txt.)
+__device__ __forceinline__ double ts_row(const DevProblem& P, const double* gps, const double* camd, int smp, int4 bk, int r) {
+    const double* N = gps + (size_t)smp * GPS_STRIDE + 12 + r;
+    const int hs[3] = {bk.x, bk.y, bk.z};
+    double acc = 0.0;
+#pragma unroll
+    for (int side = 0; side < 3; ++side) {
+        const int h = hs[side];
+        if (h < 0) continue;
+        const double* x = P.xsol + 12 * (size_t)h;
+        const double* Nc = side < 2 ? N + 6 * 12 * side : camd + (size_t)bk.w * CAMD_STRIDE + 16 + r;
+#pragma unroll
+        for (int c = 0; c < 12; ++c) acc += Nc[6 * c] * x[c];
+    }
+    return acc;
+}
 // The landmarks of regular tile `tile` (one UPD_THREADS workgroup): dx_l = Dinv_l (b_l - sum_{o of l} G_o^T t_s(o))
 // (block_solver.hpp:461-482), oplus, computeScale partial.  Returns this thread's scale term.
 constexpr int UPD_TILE_OBS_PER_THREAD = (TILE_OBS + 63) / 64;
@@ -2668,19 +2695,7 @@ __device__ double bs_tile(const DevProblem& P, int tile, int si, bool ok, double
 #pragma unroll
         for (int q = 0; q < UPD_TILE_TASKS_PER_THREAD; ++q) {
             const int task = tid + UPD_THREADS * q, r = task % 6;
-            acc[q] = 0.0;
-            if (sm[q] < 0) continue;
-            const double* N = gps + (size_t)sm[q] * GPS_STRIDE + 12 + r;
-            const int hs[3] = {bk[q].x, bk[q].y, bk[q].z};
-#pragma unroll
-            for (int side = 0; side < 3; ++side) {
-                const int h = hs[side];
-                if (h < 0) continue;
-                const double* x = P.xsol + 12 * (size_t)h;
-                const double* Nc = side < 2 ? N + 6 * 12 * side : camd + (size_t)bk[q].w * CAMD_STRIDE + 16 + r;
-#pragma unroll
-                for (int c = 0; c < 12; ++c) acc[q] += Nc[6 * c] * x[c];
-            }
+            acc[q] = sm[q] < 0 ? 0.0 : ts_row(P, gps, camd, sm[q], bk[q], r);
         }
 #pragma unroll
         for (int q = 0; q < UPD_TILE_TASKS_PER_THREAD; ++q)
@@ -2752,7 +2767,11 @@ __device__ __forceinline__ void upd_wait(const DevProblem& P, int prod, unsigned
     bool done = prod < 0;
     unsigned spins = 0;
     while (!__all(done)) {
-        if (!done) done = (unsigned)__hip_atomic_load((gi32_t*)(P.upd_flag + prod), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+        if (!done) {
+            const unsigned f = (unsigned)__hip_atomic_load((gi32_t*)(P.upd_flag + (size_t)FLAG_STRIDE * prod), __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+            done = f == epoch;
+        }
         if (__all(done)) break;
         __builtin_amdgcn_s_sleep(LBA_UPD_POLL_SLEEP);
         if (++spins > (1u << 20)) break;   // (~0.5 s: never expected)
@@ -2763,7 +2782,7 @@ __device__ __forceinline__ void upd_wait(const DevProblem& P, int prod, unsigned
 __device__ __forceinline__ void upd_publish(const DevProblem& P, int self, unsigned epoch) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store((gi32_t*)(P.upd_flag + self), (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store((gi32_t*)(P.upd_flag + (size_t)FLAG_STRIDE * self), (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // The tile's observations at the trial state (k_eval's tile item: the same per-observation arithmetic and the same
 // reduction tree, so chi_eval / ob_chi2 are bitwise k_eval's): poses from the trial samples, landmarks from ltr
@@ -2912,11 +2931,14 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
         }
         __syncthreads();
 #ifndef LBA_EXP_NO_GPPREP
+        // (the poses published as soon as they are stored, ahead of their Jacobian factors)
+        auto pub = [&]() {
+            if (fused) upd_publish(P, role, epoch);
+            if (ustamp) ustamp[-1] = __builtin_amdgcn_s_memrealtime();   // (slot 13: published)
+        };
         gp_pair_prep<true>(P, gps, i, kab, kab + KF_STRIDE, jac, ushm + 2 * 12 + 2 * KF_STRIDE + 2 * (KF_STRIDE + 12),
-                           ustamp ? P.tdbg_lin + (size_t)blockIdx.x * 16 + 5 : nullptr);
+                           ustamp ? P.tdbg_lin + (size_t)blockIdx.x * 16 + 5 : nullptr, pub);
 #endif
-        if (fused) upd_publish(P, role, epoch);
-        if (ustamp) ustamp[-1] = __builtin_amdgcn_s_memrealtime();   // (slot 13: published)
         if (threadIdx.x == 0) P.scale_part[role] = 0.0;
         if (ustamp) ustamp[1] = __builtin_amdgcn_s_memrealtime();
         return;
@@ -2925,6 +2947,9 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
     bool tile_eval = false;
     if (role < P.n_gp + nkb) {
         const int k = (role - P.n_gp) * UPD_THREADS + threadIdx.x;
+        // (diagnostics: stamps in slots 5 .. 8 of its row: start, trial states formed, stored, published)
+        unsigned long long* kst_stamp = ustamp ? P.tdbg_lin + (size_t)blockIdx.x * 16 + 5 : nullptr;
+        if (kst_stamp) kst_stamp[0] = __builtin_amdgcn_s_memrealtime();
         if (k < P.n_kf) {
             const int h = P.kf_hidx[k], xc = P.kf_cam[k];
             // this KF's b_p rows and their owners, loaded before the first store (see kf_trial_state)
@@ -2938,9 +2963,11 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
             double* d = ushm + 12 * threadIdx.x;
             double* kn = ushm + 12 * UPD_THREADS + KF_STRIDE * threadIdx.x;
             kf_trial_state(kst + (size_t)k * KF_STRIDE, kf_step(P, h, ok), d, kn);
+            if (kst_stamp) kst_stamp[1] = __builtin_amdgcn_s_memrealtime();
             double* kw = ko + (size_t)k * KF_STRIDE;
             for (int j = 0; j < KF_STRIDE; ++j) stv<true>(kw + j, kn[j]);   // (write-through: the fused evaluation)
             kf_pose_record<true>(P, gps, k, kn);
+            if (kst_stamp) kst_stamp[2] = __builtin_amdgcn_s_memrealtime();
             if (xc >= 0) {   // a free extrinsic: the trial state's camera record (Tcb, intrinsics, Ad(Tbc))
                 const double* c0 = P.camdb[si] + (size_t)xc * CAMD_STRIDE;
                 SE3 T;
@@ -2957,6 +2984,7 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
                 }
         }
         if (fused) upd_publish(P, role, epoch);
+        if (kst_stamp) kst_stamp[3] = __builtin_amdgcn_s_memrealtime();
     } else if (role < P.n_gp + nkb + P.n_stiles) {
         sc = bs_tile(P, role - P.n_gp - nkb, si, ok, lambda, lo, ushm,
                      ustamp ? P.tdbg_lin + (size_t)blockIdx.x * 16 + 5 : nullptr, fused ? ltr : nullptr);

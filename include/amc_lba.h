@@ -320,7 +320,7 @@ int64_t lba_device_bytes(const lba_problem* p);
 /* Wall time (ms) of the last lba_set_problem's phases: [0] activity, GP pairs and landmark order, [1] tiles,
  * [2] slab slots and device-order records, [3] host -> device upload, [4] the solve's layout (envelope plan,
  * flow tasks).  Writes min(n, phases) values and returns that count; LBA_E_ARG for a null problem. */
-int32_t lba_setup_phases(const lba_problem* p, double* ms, int32_t n);
+int lba_setup_phases(const lba_problem* p, double* ms, int32_t n);
 /* Dimension of the pose system (12 * number of non-fixed KFs + 6 * number of free extrinsics). */
 int lba_pose_dim(const lba_problem* p);
 /* Current camera extrinsics (write-back of the VertexExtrinsic estimates, src/Optimizer.cc:1419-1428):

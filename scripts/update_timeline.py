@@ -50,3 +50,5 @@ print(f"  KF block (row {gp.sum()}): start {us(st[kb]).max():.2f} end {us(en[kb]
 if tl.any():
     print(f"  tiles' back-substitution stamps: t_s done p50 {np.median(us(lin[tl, 5])):.2f}, landmarks done p50 "
           f"{np.median(us(lin[tl, 6])):.2f} max {us(lin[tl, 6]).max():.2f} us")
+print(f"  KF block stamps: start {us(lin[kb, 5]).max():.2f}, trial states {us(lin[kb, 6]).max():.2f}, stored "
+      f"{us(lin[kb, 7]).max():.2f}, published {us(lin[kb, 8]).max():.2f} us")
