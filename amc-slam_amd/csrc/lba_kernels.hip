@@ -1882,19 +1882,49 @@ __device__ __forceinline__ bool cf_wait_list(const CholFlow& a, int cnt, F flag,
     return *s_ok != 0;
 }
 
-// a 32 x 32 tile of handed-off data into registers (4 sc1 loads per thread), and from there to LDS
-__device__ __forceinline__ void cf_fetch(const double* src, int n, double (&r)[4]) {
+// Hand-offs of 32 x 32 tiles move 16 bytes per access (write-through sc1 buffer stores, sc1 buffer loads, all of a
+// thread's loads in flight together): thread t covers the element pairs e = 2 t + 512 m (m = 0, 1), row e >> 5,
+// columns e & 31 and the next.  An 8 KB tile handed from one workgroup to another (store, drain, flag, poll, load)
+// took 1.0-1.2 us this way against 1.7-1.8 us with 8-byte sc1 accesses (scripts/micro/handoff_lat.hip,
+// profiles/r4w_handoff_latency.txt).  tile_rsrc: a buffer over the tile (row stride ld doubles).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const double* p, int ld) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(8 * (31 * (long long)ld + CNB)), 0x00020000);
+}
+constexpr int BUF_SC1 = 16;   // buffer instruction cache policy: sc1
+__device__ __forceinline__ double lo_dbl(v4u q) { return __longlong_as_double(((long long)q.y << 32) | q.x); }
+__device__ __forceinline__ double hi_dbl(v4u q) { return __longlong_as_double(((long long)q.w << 32) | q.z); }
+// a 32 x 32 tile of handed-off data into registers (two 16-byte sc1 loads per thread), and from there to LDS
+__device__ __forceinline__ void cf_fetch(const double* src, int ld, double (&r)[4]) {
+    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(src, ld);
+    v4u q[2];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        const int e = threadIdx.x + 256 * m;
-        r[m] = ld_sc1(src + (size_t)(e >> 5) * n + (e & 31));
+    for (int m = 0; m < 2; ++m) {
+        const int e = 2 * (int)threadIdx.x + 512 * m;
+        q[m] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((e >> 5) * ld + (e & 31)) * 8, 0, BUF_SC1);
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        r[2 * m] = lo_dbl(q[m]);
+        r[2 * m + 1] = hi_dbl(q[m]);
     }
 }
 __device__ __forceinline__ void cf_put(double (*T)[CNB + 1], const double (&r)[4]) {
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        const int e = threadIdx.x + 256 * m;
-        T[e >> 5][e & 31] = r[m];
+    for (int m = 0; m < 2; ++m) {
+        const int e = 2 * (int)threadIdx.x + 512 * m;
+        T[e >> 5][e & 31] = r[2 * m];
+        T[e >> 5][(e & 31) + 1] = r[2 * m + 1];
+    }
+}
+// rows r0 .. r0 + 31 of a staged panel (LDS) out as a handed-off 32 x 32 tile (two 16-byte sc1 stores per thread)
+__device__ __forceinline__ void cf_store_tile(double* dst, int ld, const double (*T)[CNB + 1]) {
+    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(dst, ld);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        const int e = 2 * (int)threadIdx.x + 512 * m, r = e >> 5, c = e & 31;
+        const long long a0 = __double_as_longlong(T[r][c]), a1 = __double_as_longlong(T[r][c + 1]);
+        const v4u q = {(unsigned)a0, (unsigned)(a0 >> 32), (unsigned)a1, (unsigned)(a1 >> 32)};
+        __builtin_amdgcn_raw_buffer_store_b128(q, rs, (r * ld + c) * 8, 0, BUF_SC1);
     }
 }
 
@@ -1907,11 +1937,9 @@ __device__ __forceinline__ void cf_publish(const CholFlow& a, int* flag) {
 
 // 32 x 32 tile of a row-major matrix (leading dimension n) -> LDS, sc1 loads (handed-off data)
 __device__ __forceinline__ void cf_load_tile(const double* src, int n, double (*T)[CNB + 1]) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        const int e = threadIdx.x + 256 * m, r = e >> 5, c = e & 31;
-        T[r][c] = ld_sc1(src + (size_t)r * n + c);
-    }
+    double r[4];
+    cf_fetch(src, n, r);
+    cf_put(T, r);
 }
 
 // acc (this wave's quadrant) += X[rows of rb] Y[rows of cb]^T, K = 32
@@ -2481,11 +2509,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
 #endif
             // L(i, j) from the staged panel by all four waves (a quarter of the write-through bytes per
             // wave: the drain before the flag is a quarter as long as one wave storing the tile)
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const int e = tid + 256 * m, r = e >> 5, c = e & 31;
-                st_sc1(tile_at(a.Lm, t_ij) + r * CNB + c, stg[0][CNB + r][c]);
-            }
+            cf_store_tile(tile_at(a.Lm, t_ij), CNB, stg[0] + CNB);
             cf_publish(a, a.lready + t_ij);
             if (tm) tm[6] = __builtin_amdgcn_s_memrealtime();
             if (tf) tf[2] = __builtin_amdgcn_s_memrealtime();
@@ -2527,8 +2551,8 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
         for (int m = 0; m < 4; ++m) {   // L_jj (plain: no reader in this launch), L_jj^-T, by all waves
             const int e = tid + 256 * m, r = e >> 5, c = e & 31;
             tile_at(a.Lm, t_jj)[r * CNB + c] = (c <= r) ? stg[0][r][c] : 0.0;
-            st_sc1(a.LinvT + p0 * CNB + e, stg[0][CNB + r][c]);
         }
+        cf_store_tile(a.LinvT + p0 * CNB, CNB, stg[0] + CNB);
         cf_publish(a, a.fready + j);
         if (tm) tm[6] = __builtin_amdgcn_s_memrealtime();
         if (tf) tf[2] = __builtin_amdgcn_s_memrealtime();
