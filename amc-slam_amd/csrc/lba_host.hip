@@ -203,7 +203,7 @@ void dump_phase_times(lba_problem* p) {
     std::vector<unsigned long long> ch((size_t)nblk * 16), bs((size_t)nblk * 16);
     (void)hipMemcpy(ch.data(), D.tdbg_chol, ch.size() * 8, hipMemcpyDeviceToHost);
     (void)hipMemcpy(bs.data(), D.tdbg_bs, bs.size() * 8, hipMemcpyDeviceToHost);
-    std::vector<unsigned long long> cft((size_t)4096 * 8);
+    std::vector<unsigned long long> cft((size_t)4096 * CF_TDBG_STRIDE);
     (void)hipMemcpy(cft.data(), D.tdbg_cf, cft.size() * 8, hipMemcpyDeviceToHost);
     if (FILE* f = std::fopen(path, "wb")) {
         const int nt = D.n_tiles;
@@ -305,6 +305,10 @@ T* dupload(lba_problem* p, const std::vector<T>& v) {
 // (pass, piece), so a worker that arrives late takes no piece of a later pass for an earlier one; the caller
 // waits for the pieces to be finished, not for every worker to have looked in.  A pass that finds the pool
 // busy (another problem setting up on another thread) runs on its caller's thread alone.
+constexpr int SETUP_THREADS_MAX = 16;
+// the fixed number of pieces every parallel pass of the set-up splits its work into (the results do not depend on
+// the thread count; tiles never straddle a piece boundary)
+constexpr int SETUP_PIECES = 16;
 class SetupPool {
   public:
     static SetupPool& get() {
@@ -350,7 +354,7 @@ class SetupPool {
         int avail = (int)std::thread::hardware_concurrency();
         cpu_set_t cs;
         if (sched_getaffinity(0, sizeof(cs), &cs) == 0) avail = std::min(avail > 0 ? avail : CPU_COUNT(&cs), CPU_COUNT(&cs));
-        const int nt = v > 0 ? v : std::max(1, std::min(8, avail));
+        const int nt = v > 0 ? v : std::max(1, std::min(SETUP_THREADS_MAX, avail));
         for (int t = 1; t < nt; ++t)
             workers_.emplace_back([this] {
                 unsigned long long seen = 0;
@@ -634,7 +638,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         // distinct keys per pair are few: each of 8 observation pieces keeps up to KC distinct keys per pair
         // inline (flat arrays), more in a per-piece overflow list; then per pair the union, sorted
         const int ng = (int)gp_a.size();
-        constexpr int KC = 16, NPC = 8;
+        constexpr int KC = 16, NPC = SETUP_PIECES;
         std::vector<SKey> pk((size_t)NPC * std::max(ng, 1) * KC);
         std::vector<int> pc((size_t)NPC * std::max(ng, 1), 0);
         std::vector<std::vector<std::pair<int, SKey>>> pov(NPC);
@@ -670,8 +674,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             for (const SKey& k : ts[g]) { gps_t.push_back(k.first); gps_cam.push_back(k.second); keys.push_back(k); }
         }
         sub("  GP sample sort");
-        par_for(8, [&](int piece) {
-            for (int i = (int)((long long)n_obs * piece / 8); i < (int)((long long)n_obs * (piece + 1) / 8); ++i)
+        par_for(SETUP_PIECES, [&](int piece) {
+            for (int i = (int)((long long)n_obs * piece / SETUP_PIECES); i < (int)((long long)n_obs * (piece + 1) / SETUP_PIECES); ++i)
                 if (is_gp(obs[i].kind)) {
                     const int g = gp_of[i];
                     const SKey* b = keys.data() + gp_s0[g];
@@ -705,9 +709,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         for (int i = 0; i < n_obs; ++i) lo_of[fill[obs[i].lm]++] = i;
     }
     // per landmark: the span of non-fixed KFs observing it (device order key), heavy or not
-    std::vector<int> lmin(n_lm, INT_MAX), lmax(n_lm, INT_MAX);
+    std::vector<int> lmin(n_lm, INT_MAX), lmax(n_lm, INT_MAX), lm_npl(n_lm, 0);
     std::vector<char> heavy(n_lm, 0);
-    constexpr int SETUP_PIECES = 8;   // (fixed: the results do not depend on the thread count)
     par_for(SETUP_PIECES, [&](int piece) {
         // distinct pose blocks / samples of a landmark counted by stamping (stamp = landmark + 1)
         std::vector<int> kst_((size_t)std::max(n_pb, 1), 0), sst_((size_t)std::max(n_gps + n_kfs, 1), 0);
@@ -730,6 +733,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 if (sst_[sm] != l + 1) { sst_[sm] = l + 1; ++ns; }
             }
             heavy[l] = !tile_fits(lo0[l + 1] - lo0[l], nr, npl, 1, npl, ns, ne);
+            lm_npl[l] = npl;   // (its distinct pose blocks: its (KF, landmark) pairs below)
         }
     });
     sub("heavy classification");
@@ -788,14 +792,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         std::sort(ks.begin(), ks.end());
         ks.erase(std::unique(ks.begin(), ks.end()), ks.end());
     };
-    par_for(SETUP_PIECES, [&](int piece) {   // counts, then (after the prefix) the pairs themselves
-        std::vector<int> ks;
-        for (int d = (int)((long long)nl * piece / SETUP_PIECES); d < (int)((long long)nl * (piece + 1) / SETUP_PIECES); ++d) {
-            lm_blocks(d, ks);
-            lm_pair0[d + 1] = (int)ks.size();
-        }
-    });
-    for (int d = 0; d < nl; ++d) lm_pair0[d + 1] += lm_pair0[d];
+    // counts (the distinct pose blocks the heavy classification counted), then the pairs themselves
+    for (int d = 0; d < nl; ++d) lm_pair0[d + 1] = lm_pair0[d] + lm_npl[order[d]];
     const int n_pairs = lm_pair0[nl];
     pair_lm.resize(n_pairs);
     pair_kf.resize(n_pairs);
@@ -1028,23 +1026,53 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 d = e;
             }
         });
-        for (int piece = 0; piece < n_pieces; ++piece) {
-            const TileOut& T = outs[piece];
-            const int o_smp = (int)tsm_smp.size(), o_kf = (int)tkf_list.size(), o_sent = (int)sent_l1.size();
-            const int o_pr = (int)pair_rows.size(), o_lr = (int)lm_rows.size();
-            const int d0 = (int)((long long)n_reg * piece / n_pieces), d1 = (int)((long long)n_reg * (piece + 1) / n_pieces);
-            for (int q = lm_pair0[d0]; q < lm_pair0[d1]; ++q) pair_r0[q + 1] += o_pr;
-            for (int l = d0; l < d1; ++l) lm_r0[l + 1] += o_lr;
-            auto cat = [](std::vector<int>& dst, const std::vector<int>& src, int off) {
-                for (int v : src) dst.push_back(v + off);
+        // the pieces' lists concatenated: every output's per-piece offsets first, then the pieces copied in
+        // parallel (a serial element-wise concatenation cost most of the tiling's wall time on 16 threads)
+        {
+            std::vector<TileOut*> po(n_pieces);
+            for (int piece = 0; piece < n_pieces; ++piece) po[piece] = &outs[piece];
+            struct Cat {
+                std::vector<int>* dst;
+                std::vector<int> TileOut::*src;
+                int add;   // 0: values as they are; 1 / 2 / 3: + the piece's offset into tsm_smp / sent_l1 / tkf_list
             };
-            cat(t_obs0, T.t_obs0, 0); cat(t_nobs, T.t_nobs, 0); cat(t_lm0, T.t_lm0, 0); cat(t_nlm, T.t_nlm, 0);
-            cat(t_pair0, T.t_pair0, 0); cat(t_npair, T.t_npair, 0); cat(t_smp0, T.t_smp0, o_smp);
-            cat(t_nsmp, T.t_nsmp, 0); cat(t_sent0, T.t_sent0, o_sent); cat(t_nsent, T.t_nsent, 0);
-            cat(t_kf0, T.t_kf0, o_kf); cat(t_nkf, T.t_nkf, 0); cat(tkf_list, T.tkf_list, 0);
-            cat(tsm_smp, T.tsm_smp, 0); cat(tsm_rows, T.tsm_rows, 0); cat(sent_l1, T.sent_l1, 0);
-            cat(sent_l2, T.sent_l2, 0); cat(sent_k1, T.sent_k1, 0); cat(sent_k2, T.sent_k2, 0);
-            cat(pair_rows, T.pair_rows, 0); cat(lm_rows, T.lm_rows, 0);
+            const Cat cats[] = {
+                {&t_obs0, &TileOut::t_obs0, 0}, {&t_nobs, &TileOut::t_nobs, 0}, {&t_lm0, &TileOut::t_lm0, 0},
+                {&t_nlm, &TileOut::t_nlm, 0}, {&t_pair0, &TileOut::t_pair0, 0}, {&t_npair, &TileOut::t_npair, 0},
+                {&t_smp0, &TileOut::t_smp0, 1}, {&t_nsmp, &TileOut::t_nsmp, 0}, {&t_sent0, &TileOut::t_sent0, 2},
+                {&t_nsent, &TileOut::t_nsent, 0}, {&t_kf0, &TileOut::t_kf0, 3}, {&t_nkf, &TileOut::t_nkf, 0},
+                {&tkf_list, &TileOut::tkf_list, 0}, {&tsm_smp, &TileOut::tsm_smp, 0}, {&tsm_rows, &TileOut::tsm_rows, 0},
+                {&sent_l1, &TileOut::sent_l1, 0}, {&sent_l2, &TileOut::sent_l2, 0}, {&sent_k1, &TileOut::sent_k1, 0},
+                {&sent_k2, &TileOut::sent_k2, 0}, {&pair_rows, &TileOut::pair_rows, 0}, {&lm_rows, &TileOut::lm_rows, 0}};
+            constexpr int NC = (int)(sizeof(cats) / sizeof(cats[0]));
+            // off[c][piece]: where piece's part of output c starts
+            std::vector<std::vector<size_t>> off(NC, std::vector<size_t>(n_pieces + 1, 0));
+            for (int c = 0; c < NC; ++c) {
+                for (int piece = 0; piece < n_pieces; ++piece)
+                    off[c][piece + 1] = off[c][piece] + (po[piece]->*(cats[c].src)).size();
+                cats[c].dst->resize(off[c][n_pieces]);
+            }
+            auto at = [&](std::vector<int> TileOut::*m) {   // index of an output in cats
+                for (int c = 0; c < NC; ++c)
+                    if (cats[c].src == m) return c;
+                return -1;
+            };
+            const int c_smp = at(&TileOut::tsm_smp), c_sent = at(&TileOut::sent_l1), c_kf = at(&TileOut::tkf_list);
+            const int c_pr = at(&TileOut::pair_rows), c_lr = at(&TileOut::lm_rows);
+            par_for(n_pieces, [&](int piece) {
+                const TileOut& T = *po[piece];
+                for (int c = 0; c < NC; ++c) {
+                    const std::vector<int>& src = T.*(cats[c].src);
+                    const int a = cats[c].add == 1 ? (int)off[c_smp][piece] : cats[c].add == 2 ? (int)off[c_sent][piece]
+                                : cats[c].add == 3 ? (int)off[c_kf][piece] : 0;
+                    int* d = cats[c].dst->data() + off[c][piece];
+                    for (size_t k = 0; k < src.size(); ++k) d[k] = src[k] + a;
+                }
+                const int d0 = (int)((long long)n_reg * piece / n_pieces), d1 = (int)((long long)n_reg * (piece + 1) / n_pieces);
+                const int o_pr = (int)off[c_pr][piece], o_lr = (int)off[c_lr][piece];
+                for (int q = lm_pair0[d0]; q < lm_pair0[d1]; ++q) pair_r0[q + 1] += o_pr;
+                for (int l = d0; l < d1; ++l) lm_r0[l + 1] += o_lr;
+            });
         }
         n_stiles = (int)t_obs0.size();
         sub("regular tiles");
@@ -1391,8 +1419,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         const int nblk = (p->np + CHOL_NB - 1) / CHOL_NB + 1;
         D.tdbg_chol = dalloc<unsigned long long>(p, (size_t)nblk * 16);
         D.tdbg_bs = dalloc<unsigned long long>(p, (size_t)nblk * 16);
-        D.tdbg_cf = dalloc<unsigned long long>(p, (size_t)4096 * 8);
-        HIPCHK(hipMemset(D.tdbg_cf, 0, (size_t)4096 * 8 * 8));
+        D.tdbg_cf = dalloc<unsigned long long>(p, (size_t)4096 * CF_TDBG_STRIDE);
+        HIPCHK(hipMemset(D.tdbg_cf, 0, (size_t)4096 * CF_TDBG_STRIDE * 8));
         HIPCHK(hipMemset(D.tdbg_chol, 0, (size_t)nblk * 16 * 8));
         HIPCHK(hipMemset(D.tdbg_bs, 0, (size_t)nblk * 16 * 8));
     }

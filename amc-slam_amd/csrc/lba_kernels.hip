@@ -2366,7 +2366,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
         // diagnostics: stamps of panel j's task (slots 0..6) and of tile (j + 1, j) (slots 8..14)
         unsigned long long* tm = (a.tdbg && tid == 0 && (diag || i == j + 1)) ? a.tdbg + 16 * j + (diag ? 0 : 8) : nullptr;
         if (tm) tm[0] = __builtin_amdgcn_s_memrealtime();
-        unsigned long long* tf = (a.tdbg3 && tid == 0 && t < 4096) ? a.tdbg3 + 8 * t : nullptr;
+        unsigned long long* tf = (a.tdbg3 && tid == 0 && t < 4096) ? a.tdbg3 + (size_t)CF_TDBG_STRIDE * t : nullptr;
         if (tf) { tf[0] = __builtin_amdgcn_s_memrealtime(); tf[4] = i | (j << 12) | ((int)la << 24); }
         // the task's tiles: (j,j), (i,j), and with lookahead (k,k), (j,k), (i,k) (-1 when (i,k) is zero)
         const int t_jj = a.task_t[5 * t], t_ij = a.task_t[5 * t + 1], t_kk = a.task_t[5 * t + 2],
@@ -2451,6 +2451,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             const int e = a.plist[q];
             bool fj, fi, fk;
             rows(e, fj, fi, fk);
+            const bool waited = !have;
             if (!have) {
                 if (!ready(q, true)) { ok = false; break; }
                 if (tf) { tf[3] = __builtin_amdgcn_s_memrealtime(); tf[4] = (tf[4] & 0xffffffull) | ((unsigned long long)(la) << 24) | ((unsigned long long)(e & 0xffffff) << 32); }
@@ -2470,6 +2471,10 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
                 if (ik && fi) sub_mma(qik, cf_mma_nt(Lt[1], Lt[2], rb, cb, lr, kq, z4));
             }
             __syncthreads();
+            if (tf && q - q0 < 16) {
+                tf[8 + 2 * (q - q0)] = __builtin_amdgcn_s_memrealtime();
+                tf[9 + 2 * (q - q0)] = (unsigned long long)((e & 0xffffff) | ((int)waited << 24));
+            }
             if (la && ((e >> 27) & 1)) factor_k();
         }
         if (tf) tf[5] = __builtin_amdgcn_s_memrealtime();

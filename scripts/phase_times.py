@@ -38,8 +38,9 @@ def load(path):
         off += nb * 16 * 8
         bs = np.frombuffer(raw[off:off + nb * 16 * 8], np.uint64).reshape(nb, 16).astype(np.int64)
         off += nb * 16 * 8
-        if len(raw) >= off + 4096 * 8 * 8:
-            cft = np.frombuffer(raw[off:off + 4096 * 8 * 8], np.uint64).reshape(4096, 8).astype(np.int64)
+        W = 8 + 2 * 16   # CF_TDBG_STRIDE
+        if len(raw) >= off + 4096 * W * 8:
+            cft = np.frombuffer(raw[off:off + 4096 * W * 8], np.uint64).reshape(4096, W).astype(np.int64)
     return nt, lin, sch, shape, chol, bs, cft
 
 
@@ -177,6 +178,10 @@ def main():
                     ii, jj, la, pp = r[4] & 4095, (r[4] >> 12) & 4095, (r[4] >> 24) & 1, (r[4] >> 32) & 4095
                     out.append(f"     {tk:4d}: ({ii:2d},{jj:2d}) la={la} | {f(r[0]):7.2f} {f(r[3]):7.2f} (p={pp:2d}) "
                                f"{f(r[5]):7.2f} {f(r[6]):7.2f} {f(r[1]):7.2f} {f(r[2]):7.2f}  factor {r[7]} cycles")
+                    if ii == jj and len(r) > 8:   # the panel task's update list: entry end (panel, * = waited)
+                        ent = [f"{r[9 + 2 * e] & 0xffffff}{'*' if (r[9 + 2 * e] >> 24) & 1 else ''}:{f(r[8 + 2 * e]):.2f}"
+                               for e in range(16) if r[8 + 2 * e]]
+                        out.append("            entries " + " ".join(ent))
             chol = None
     if chol is not None:
         nst = int((chol[:, 0] != 0).sum())
