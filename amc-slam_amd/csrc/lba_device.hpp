@@ -42,8 +42,7 @@ constexpr int TILE_OBS = 128;
 #endif
 constexpr int FLAG_STRIDE = LBA_FLAG_STRIDE;   // ints
 constexpr int CF_TDBG_STRIDE = 8 + 2 * 16;     // diagnostics: u64 per k_chol_flow factor task
-constexpr int UPD_BLOCK_KFS = 64;
-constexpr int TS_STRIDE = 16;        // doubles per pose sample's t_s record (one 128-byte line)   // keyframes per KF-block workgroup of k_update (its UPD_THREADS)
+constexpr int UPD_BLOCK_KFS = 64;   // keyframes per KF-block workgroup of k_update (its UPD_THREADS)
 constexpr int TILE_ROWS = 288;
 constexpr int TILE_PAIRS = 128;
 constexpr int TILE_LMS = 64;
@@ -319,7 +318,7 @@ struct DevProblem {
     unsigned long long* tdbg_schur;   // [n_tiles][16] k_schur
     unsigned long long* tdbg_chol;    // [npad / CHOL_NB][16] k_chol_flow panel tasks
     unsigned long long* tdbg_cf;      // [4096][CF_TDBG_STRIDE] k_chol_flow factor tasks: stamps, i, j; then per update-list
-                                      // entry (the first 16): its end stamp and (panel | waited << 16)
+                                      // entry (the first 16): its end stamp and (panel | waited << 24)
     unsigned long long* tdbg_bs;      // [npad / CHOL_NB][16] k_chol_flow L^-1 tasks of the last rows
 };
 

@@ -714,25 +714,39 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     par_for(SETUP_PIECES, [&](int piece) {
         // distinct pose blocks / samples of a landmark counted by stamping (stamp = landmark + 1)
         std::vector<int> kst_((size_t)std::max(n_pb, 1), 0), sst_((size_t)std::max(n_gps + n_kfs, 1), 0);
+        // (plain pointers and per-landmark locals: through the vectors every int store could alias every int
+        // load, and the compiler reloaded the tables per observation)
+        int* __restrict__ kst = kst_.data();
+        int* __restrict__ sst = sst_.data();
+        const int* __restrict__ Hh = H.data();
+        const int* __restrict__ lo = lo_of.data();
+        const int* __restrict__ lz = lo0.data();
+        const int* __restrict__ so = smp_of.data();
+        const int* __restrict__ cslot = cam_slot.data();
         for (int l = (int)((long long)n_lm * piece / SETUP_PIECES); l < (int)((long long)n_lm * (piece + 1) / SETUP_PIECES); ++l) {
             if (!lm_act[l]) continue;
-            int nr = 0, ne = 0, npl = 0, ns = 0;
-            for (int q = lo0[l]; q < lo0[l + 1]; ++q) {
-                const lba_obs& o = obs[lo_of[q]];
-                const int hb = H[o.kf_b], ha = is_gp(o.kind) ? H[o.kf_a] : -1, hx = ext_block(o);
+            int nr = 0, ne = 0, npl = 0, ns = 0, mn = INT_MAX, mx = INT_MAX;
+            const int stamp = l + 1;
+            for (int q = lz[l]; q < lz[l + 1]; ++q) {
+                const int oi = lo[q];
+                const lba_obs& o = obs[oi];
+                const int hb = Hh[o.kf_b], ha = is_gp(o.kind) ? Hh[o.kf_a] : -1;
+                const int hx = (o.kind == LBA_MONO_GP && cslot[o.cam] >= 0) ? Hh[cslot[o.cam]] : -1;   // ext_block(o)
                 for (int k : {hb, ha})
                     if (k >= 0) {
-                        lmin[l] = lmin[l] == INT_MAX ? k : std::min(lmin[l], k);
-                        lmax[l] = lmax[l] == INT_MAX ? k : std::max(lmax[l], k);
+                        mn = mn == INT_MAX ? k : std::min(mn, k);
+                        mx = mx == INT_MAX ? k : std::max(mx, k);
                     }
                 for (int k : {hb, ha, hx})
-                    if (k >= 0 && kst_[k] != l + 1) { kst_[k] = l + 1; ++npl; }
+                    if (k >= 0 && kst[k] != stamp) { kst[k] = stamp; ++npl; }
                 ne += (hb >= 0) + (ha >= 0) + (hx >= 0);
                 nr += obs_dim(o.kind);
-                const int sm = smp_of[lo_of[q]];
-                if (sst_[sm] != l + 1) { sst_[sm] = l + 1; ++ns; }
+                const int sm = so[oi];
+                if (sst[sm] != stamp) { sst[sm] = stamp; ++ns; }
             }
-            heavy[l] = !tile_fits(lo0[l + 1] - lo0[l], nr, npl, 1, npl, ns, ne);
+            lmin[l] = mn;
+            lmax[l] = mx;
+            heavy[l] = !tile_fits(lz[l + 1] - lz[l], nr, npl, 1, npl, ns, ne);
             lm_npl[l] = npl;   // (its distinct pose blocks: its (KF, landmark) pairs below)
         }
     });

@@ -2583,14 +2583,13 @@ static_assert(UPD_THREADS == UPD_BLOCK_KFS, "k_update's KF blocks (the host numb
 // the solved step, or the stale x when the factorisation failed (BlockSolver leaves x untouched, g2o then
 // applies and pops it); dx null: a fixed KF.  One (non-inlined) function body for every caller, so every copy
 // of a state is bitwise identical.
-__device__ __forceinline__ const double* kf_step(const DevProblem& P, int h, bool ok) {
-    return h < 0 ? nullptr : (ok ? P.xsol : P.x) + 12 * (size_t)h;
-}
-// (Every input is loaded into registers before the first store: the outputs may alias nothing, but through
-// generic pointers the compiler cannot know that, and interleaved loads and stores serialise into one memory
-// round trip per element.)
-__device__ __attribute__((noinline)) void kf_trial_state(const double* __restrict__ kc, const double* __restrict__ dx,
-                                                         double* __restrict__ d, double* __restrict__ kn) {
+// A KF's trial state: kc its state, dx its step (x of the solve, or BlockSolver's stale x after a failed
+// factorisation; nullptr: fixed), d <- the step (dx may be d itself: every element is read before any is written),
+// kn <- the trial state.  (Every input is loaded into registers before the first store: through generic pointers
+// the compiler could not hoist a load above a store that might alias it, and interleaved loads and stores
+// serialise into one memory round trip per element.)
+__device__ __attribute__((noinline)) void kf_trial_state(const double* __restrict__ kc, const double* dx, double* d,
+                                                         double* __restrict__ kn) {
     double c[KF_STRIDE];
 #pragma unroll
     for (int j = 0; j < KF_STRIDE; ++j) c[j] = kc[j];
@@ -2652,29 +2651,35 @@ __device__ __forceinline__ void bs_obs(const DevProblem& P, const double* gps, c
     for (int a = 0; a < 3; ++a) v[a] *= s;
 }
 
-// Row r of a pose sample's step t_s = N_s [x_a; x_b] (+ the extrinsic factor on x_e): N column c at 12 + 6 c; bk: the
-// sample's pose blocks (a, b, extrinsic) and camera.  (Formed per sample once, by k_update's GP-pair / KF-block
-// workgroups, and handed to the tiles through their flags, it made the fused k_update slower: the producers' chains
-// are the launch's other critical path, profiles/r4u_ab_ts_per_sample_rejected.txt.)
-__device__ __forceinline__ double ts_row(const DevProblem& P, const double* gps, const double* camd, int smp, int4 bk, int r) {
-    const double* N = gps + (size_t)smp * GPS_STRIDE + 12 + r;
+// Rows r0, r0 + 1 (r0 even) of a pose sample's step t_s = N_s [x_a; x_b] (+ the extrinsic factor on x_e): N column c
+// at 12 + 6 c, so the two rows of a column are one 16-byte load; bk: the sample's pose blocks (a, b, extrinsic) and
+// camera.  Each row is summed in column order, as one row per task did.  (Formed per sample once, by k_update's
+// GP-pair / KF-block workgroups, and handed to the tiles through their flags, it made the fused k_update slower: the
+// producers' chains are the launch's other critical path, profiles/r4u_ab_ts_per_sample_rejected.txt.)
+__device__ __forceinline__ void ts_rows2(const DevProblem& P, const double* gps, const double* camd, int smp, int4 bk, int r0,
+                                         double& a0, double& a1) {
+    const double* N = gps + (size_t)smp * GPS_STRIDE + 12 + r0;
     const int hs[3] = {bk.x, bk.y, bk.z};
-    double acc = 0.0;
+    a0 = 0.0;
+    a1 = 0.0;
 #pragma unroll
     for (int side = 0; side < 3; ++side) {
         const int h = hs[side];
         if (h < 0) continue;
         const double* x = P.xsol + 12 * (size_t)h;
-        const double* Nc = side < 2 ? N + 6 * 12 * side : camd + (size_t)bk.w * CAMD_STRIDE + 16 + r;
+        const double* Nc = side < 2 ? N + 6 * 12 * side : camd + (size_t)bk.w * CAMD_STRIDE + 16 + r0;
 #pragma unroll
-        for (int c = 0; c < 12; ++c) acc += Nc[6 * c] * x[c];
+        for (int c = 0; c < 12; ++c) {
+            const double2 n2 = *reinterpret_cast<const double2*>(Nc + 6 * c);
+            a0 += n2.x * x[c];
+            a1 += n2.y * x[c];
+        }
     }
-    return acc;
 }
 // The landmarks of regular tile `tile` (one UPD_THREADS workgroup): dx_l = Dinv_l (b_l - sum_{o of l} G_o^T t_s(o))
 // (block_solver.hpp:461-482), oplus, computeScale partial.  Returns this thread's scale term.
 constexpr int UPD_TILE_OBS_PER_THREAD = (TILE_OBS + 63) / 64;
-constexpr int UPD_TILE_TASKS_PER_THREAD = (TILE_SMP * 6 + UPD_THREADS - 1) / UPD_THREADS;
+constexpr int UPD_TILE_TASKS_PER_THREAD = (TILE_SMP * 3 + UPD_THREADS - 1) / UPD_THREADS;   // (sample, row pair) tasks
 constexpr int BS_SHM = TILE_SMP * 6 + TILE_OBS * 3;
 // (Latency-bound: every load a thread needs is issued in a few batches, each stage's index loads for all of its
 // tasks before their data loads, and the landmark's own inputs at entry, so a tile costs a handful of memory
@@ -2704,33 +2709,37 @@ __device__ double bs_tile(const DevProblem& P, int tile, int si, bool ok, double
         lob0 = P.lm_obs0[l];
         lob1 = P.lm_obs0[l + 1];
     }
-    if (ok) {
+    // (run whatever the factorisation's status, read at the launch's start: branching on it would put that load's
+    // round trip ahead of every load below; after a failed factorisation the results go unused)
+    {
         const int ts0 = P.tile_smp0[tile], nts = P.tile_nsmp[tile];
         const int obs0 = P.tile_obs0[tile], nobs = P.tile_nobs[tile];
         const double* __restrict__ kst = P.kbuf[si];
         const double* __restrict__ gps = P.gpsb[si];
         const double* __restrict__ camd = P.camdb[si];
-        // t_s(r) = sum_c N_s(r, c) [x_a; x_b](c) (+ the extrinsic factor on x_e): N column c at 12 + 6 c
+        // t_s(r) = sum_c N_s(r, c) [x_a; x_b](c) (+ the extrinsic factor on x_e): one task per (sample, row pair)
         int sm[UPD_TILE_TASKS_PER_THREAD];
         int4 bk[UPD_TILE_TASKS_PER_THREAD];
 #pragma unroll
         for (int q = 0; q < UPD_TILE_TASKS_PER_THREAD; ++q) {
             const int task = tid + UPD_THREADS * q;
-            const bool in = task < nts * 6;
-            sm[q] = in ? P.tsm_smp[ts0 + task / 6] : -1;
-            bk[q] = in ? *reinterpret_cast<const int4*>(P.tsm_blk + 4 * (size_t)(ts0 + task / 6)) : make_int4(-1, -1, -1, -1);
+            const bool in = task < nts * 3;
+            sm[q] = in ? P.tsm_smp[ts0 + task / 3] : -1;
+            bk[q] = in ? *reinterpret_cast<const int4*>(P.tsm_blk + 4 * (size_t)(ts0 + task / 3)) : make_int4(-1, -1, -1, -1);
         }
-        double acc[UPD_TILE_TASKS_PER_THREAD];
+        double acc[UPD_TILE_TASKS_PER_THREAD][2];
 #pragma unroll
         for (int q = 0; q < UPD_TILE_TASKS_PER_THREAD; ++q) {
-            const int task = tid + UPD_THREADS * q, r = task % 6;
-            acc[q] = sm[q] < 0 ? 0.0 : ts_row(P, gps, camd, sm[q], bk[q], r);
+            const int task = tid + UPD_THREADS * q;
+            acc[q][0] = acc[q][1] = 0.0;
+            if (sm[q] >= 0) ts_rows2(P, gps, camd, sm[q], bk[q], 2 * (task % 3), acc[q][0], acc[q][1]);
         }
 #pragma unroll
         for (int q = 0; q < UPD_TILE_TASKS_PER_THREAD; ++q)
             if (sm[q] >= 0) {
                 const int task = tid + UPD_THREADS * q;
-                tsh[task / 6][task % 6] = acc[q];
+                tsh[task / 3][2 * (task % 3)] = acc[q][0];
+                tsh[task / 3][2 * (task % 3) + 1] = acc[q][1];
             }
         __syncthreads();
         if (stamp) stamp[0] = __builtin_amdgcn_s_memrealtime();
@@ -2946,10 +2955,13 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
         {
             const int t = threadIdx.x, side = t >= KF_STRIDE + 12 ? 1 : 0, e = t - side * (KF_STRIDE + 12);
             if (t < 2 * (KF_STRIDE + 12)) {
-                const int k = P.gp_hab[4 * i + side];
-                const double* dx = kf_step(P, P.gp_hab[4 * i + 2 + side], ok);
-                if (e < KF_STRIDE) kin[t] = kst[(size_t)k * KF_STRIDE + e];
-                else if (dx) kin[t] = dx[e - KF_STRIDE];
+                const int k = P.gp_hab[4 * i + side], h = P.gp_hab[4 * i + 2 + side];
+                if (e < KF_STRIDE) {
+                    kin[t] = kst[(size_t)k * KF_STRIDE + e];
+                } else if (h >= 0) {   // the step, both candidates loaded ahead of the status (no round trip on it)
+                    const double xs = P.xsol[12 * (size_t)h + e - KF_STRIDE], xo = P.x[12 * (size_t)h + e - KF_STRIDE];
+                    kin[t] = ok ? xs : xo;
+                }
             }
         }
         __syncthreads();
@@ -2991,7 +3003,13 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
             }
             double* d = ushm + 12 * threadIdx.x;
             double* kn = ushm + 12 * UPD_THREADS + KF_STRIDE * threadIdx.x;
-            kf_trial_state(kst + (size_t)k * KF_STRIDE, kf_step(P, h, ok), d, kn);
+            if (h >= 0)   // the step staged in d (both candidates loaded ahead of the status; d gets them anyway)
+#pragma unroll
+                for (int j = 0; j < 12; ++j) {
+                    const double xs = P.xsol[12 * (size_t)h + j], xo = P.x[12 * (size_t)h + j];
+                    d[j] = ok ? xs : xo;
+                }
+            kf_trial_state(kst + (size_t)k * KF_STRIDE, h >= 0 ? d : nullptr, d, kn);
             if (kst_stamp) kst_stamp[1] = __builtin_amdgcn_s_memrealtime();
             double* kw = ko + (size_t)k * KF_STRIDE;
             for (int j = 0; j < KF_STRIDE; ++j) stv<true>(kw + j, kn[j]);   // (write-through: the fused evaluation)
