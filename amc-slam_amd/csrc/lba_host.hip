@@ -81,6 +81,14 @@ struct lba_problem {
     // of the preprocessing; the next set_problem reuses it after its stream synchronisation
     std::vector<Alloc> pin_chunks;
     size_t pin_chunk = 0, pin_off = 0;
+    // the window's read-only arrays (dupload): bump-allocated in persistent device chunks, each with a pinned mirror;
+    // an array is copied into the mirror at its offset and the staged range since the last flush goes out as ONE
+    // host->device copy per chunk at every phase boundary (flush_uploads), instead of one copy per array (~65 per
+    // set-up, each a runtime call)
+    std::vector<Alloc> up_dev, up_pin;
+    std::vector<size_t> up_end;             // bytes staged in each chunk this set-up (the current one: up_off)
+    size_t up_chunk = 0, up_off = 0;        // allocation position
+    size_t up_fchunk = 0, up_foff = 0;      // flushed up to here
     // observation-sized host scratch arrays of set_problem, kept between calls: resizing to the same
     // length touches nothing (no allocation, page faults or zeroing per window; every element is written)
     std::vector<int> scr_i[16];
@@ -223,6 +231,12 @@ void release_all(lba_problem* p) {   // (lba_destroy)
     for (auto& a : p->allocs) (void)hipFree(a.ptr);
     p->allocs.clear();
     p->alloc_cursor = 0;
+    for (auto& a : p->up_dev) (void)hipFree(a.ptr);
+    for (auto& a : p->up_pin) (void)hipHostFree(a.ptr);
+    p->up_dev.clear();
+    p->up_pin.clear();
+    p->up_end.clear();
+    p->up_chunk = p->up_off = p->up_fchunk = p->up_foff = 0;
 }
 
 void free_all(lba_problem* p) {   // the buffers stay allocated for the next window's dalloc calls
@@ -230,6 +244,7 @@ void free_all(lba_problem* p) {   // the buffers stay allocated for the next win
     p->alloc_cursor = 0;
     p->pin_chunk = 0;
     p->pin_off = 0;
+    p->up_chunk = p->up_off = p->up_fchunk = p->up_foff = 0;
     p->kst[0] = p->kst[1] = p->lst[0] = p->lst[1] = nullptr;
     p->D = DevProblem{};
     p->has_problem = false;
@@ -276,9 +291,10 @@ void* pin_stage(lba_problem* p, size_t bytes) {
         p->pin_off = 0;
     }
 }
+// v into the device buffer d (at least v.size() elements), through the pinned staging chunks, asynchronously on the
+// problem's stream
 template <typename T>
-T* dupload(lba_problem* p, const std::vector<T>& v) {
-    T* d = dalloc<T>(p, v.size());
+void upload_into(lba_problem* p, T* d, const std::vector<T>& v) {
     if (!v.empty()) {
         const size_t bytes = v.size() * sizeof(T);
         void* st = pin_stage(p, bytes);
@@ -291,6 +307,52 @@ T* dupload(lba_problem* p, const std::vector<T>& v) {
             std::memcpy(st, v.data(), bytes);
         }
         HIPCHK(hipMemcpyAsync(d, st, bytes, hipMemcpyHostToDevice, p->stream));
+    }
+}
+// the staged part of the upload chunks since the last flush, one host->device copy per chunk
+void flush_uploads(lba_problem* p) {
+    while (p->up_fchunk < p->up_pin.size() && (p->up_fchunk < p->up_chunk || p->up_foff < p->up_off)) {
+        const size_t end = p->up_fchunk < p->up_chunk ? p->up_end[p->up_fchunk] : p->up_off;
+        if (end > p->up_foff)
+            HIPCHK(hipMemcpyAsync(static_cast<char*>(p->up_dev[p->up_fchunk].ptr) + p->up_foff,
+                                  static_cast<char*>(p->up_pin[p->up_fchunk].ptr) + p->up_foff, end - p->up_foff,
+                                  hipMemcpyHostToDevice, p->stream));
+        if (p->up_fchunk < p->up_chunk) {
+            ++p->up_fchunk;
+            p->up_foff = 0;
+        } else {
+            p->up_foff = end;
+        }
+    }
+}
+template <typename T>
+T* dupload(lba_problem* p, const std::vector<T>& v) {
+    const size_t bytes = ((std::max<size_t>(v.size(), 1) * sizeof(T)) + 255) & ~(size_t)255;
+    while (true) {
+        if (p->up_chunk == p->up_dev.size()) {
+            lba_problem::Alloc dv{nullptr, std::max<size_t>(bytes, (size_t)32 << 20)}, pn{nullptr, dv.bytes};
+            HIPCHK(hipMalloc(&dv.ptr, dv.bytes));
+            HIPCHK(hipHostMalloc(&pn.ptr, pn.bytes, hipHostMallocDefault));
+            p->up_dev.push_back(dv);
+            p->up_pin.push_back(pn);
+            p->up_end.push_back(0);
+        }
+        if (p->up_off + bytes <= p->up_dev[p->up_chunk].bytes) break;
+        p->up_end[p->up_chunk] = p->up_off;   // (the rest of this chunk stays unused)
+        ++p->up_chunk;
+        p->up_off = 0;
+    }
+    char* st = static_cast<char*>(p->up_pin[p->up_chunk].ptr) + p->up_off;
+    T* d = reinterpret_cast<T*>(static_cast<char*>(p->up_dev[p->up_chunk].ptr) + p->up_off);
+    p->up_off += bytes;
+    const size_t nb = v.size() * sizeof(T);
+    if (nb >= ((size_t)1 << 19)) {   // large arrays: the copy into pinned memory in 8 pieces
+        par_for(8, [&](int piece) {
+            const size_t b0 = nb * piece / 8, b1 = nb * (piece + 1) / 8;
+            std::memcpy(st + b0, reinterpret_cast<const char*>(v.data()) + b0, b1 - b0);
+        });
+    } else if (nb) {
+        std::memcpy(st, v.data(), nb);
     }
     return d;
 }
@@ -538,6 +600,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         tsub = now;
     };
     auto mark = [&](const char* what) {
+        if (p->stream) flush_uploads(p);   // (the arrays staged in this phase go out while the next one runs)
         const auto now = std::chrono::steady_clock::now();
         const double ms = std::chrono::duration<double, std::milli>(now - tlast).count();
         p->setup_ms.push_back(ms);
@@ -1428,15 +1491,15 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     if (std::getenv("LBA_PHASE_TIMING")) {
         D.tdbg_lin = dalloc<unsigned long long>(p, (size_t)n_tiles * 16);
         D.tdbg_schur = dalloc<unsigned long long>(p, (size_t)n_tiles * 16);
-        HIPCHK(hipMemset(D.tdbg_lin, 0, (size_t)n_tiles * 16 * 8));
-        HIPCHK(hipMemset(D.tdbg_schur, 0, (size_t)n_tiles * 16 * 8));
+        HIPCHK(hipMemsetAsync(D.tdbg_lin, 0, (size_t)n_tiles * 16 * 8, p->stream));
+        HIPCHK(hipMemsetAsync(D.tdbg_schur, 0, (size_t)n_tiles * 16 * 8, p->stream));
         const int nblk = (p->np + CHOL_NB - 1) / CHOL_NB + 1;
         D.tdbg_chol = dalloc<unsigned long long>(p, (size_t)nblk * 16);
         D.tdbg_bs = dalloc<unsigned long long>(p, (size_t)nblk * 16);
         D.tdbg_cf = dalloc<unsigned long long>(p, (size_t)4096 * CF_TDBG_STRIDE);
-        HIPCHK(hipMemset(D.tdbg_cf, 0, (size_t)4096 * CF_TDBG_STRIDE * 8));
-        HIPCHK(hipMemset(D.tdbg_chol, 0, (size_t)nblk * 16 * 8));
-        HIPCHK(hipMemset(D.tdbg_bs, 0, (size_t)nblk * 16 * 8));
+        HIPCHK(hipMemsetAsync(D.tdbg_cf, 0, (size_t)4096 * CF_TDBG_STRIDE * 8, p->stream));
+        HIPCHK(hipMemsetAsync(D.tdbg_chol, 0, (size_t)nblk * 16 * 8, p->stream));
+        HIPCHK(hipMemsetAsync(D.tdbg_bs, 0, (size_t)nblk * 16 * 8, p->stream));
     }
     D.seg_slot = dupload(p, seg_slot); D.seg_gslot = dupload(p, seg_gslot);
 
@@ -1835,7 +1898,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 D.cf_asm_item = dupload(p, aitem2);
                 D.cf_asm_tgt = dupload(p, atgt2);
                 D.cf_cnt = dalloc<int>(p, D.cf_ncnt);
-                HIPCHK(hipMemset(D.cf_cnt, 0, sizeof(int) * D.cf_ncnt));
+                HIPCHK(hipMemsetAsync(D.cf_cnt, 0, sizeof(int) * D.cf_ncnt, p->stream));
             }
             D.cf_tasks = dupload(p, tasks);
             D.cf_task_i = dupload(p, task_i);
@@ -1858,7 +1921,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             const size_t niv = band ? (size_t)NP + 1 : (size_t)std::max(NP * (NP + 1) / 2, 1);
             D.cf_linv = band ? nullptr : dalloc<double>(p, (size_t)npad * npad);
             D.cf_ivready = dalloc<int>(p, niv);
-            HIPCHK(hipMemset(D.cf_ivready, 0, sizeof(int) * niv));
+            HIPCHK(hipMemsetAsync(D.cf_ivready, 0, sizeof(int) * niv, p->stream));
             D.cf_xpos = band ? dalloc<double>(p, npad) : nullptr;
             D.cf_pl0 = dupload(p, pl0);
             D.cf_plist = dupload(p, plist);
@@ -1866,16 +1929,16 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             D.cf_lready = dalloc<int>(p, std::max(ntile, 1));
             D.cf_dready = dalloc<int>(p, std::max(NP, 1));
             D.cf_fready = dalloc<int>(p, std::max(NP, 1));
-            HIPCHK(hipMemset(D.cf_fready, 0, sizeof(int) * std::max(NP, 1)));
+            HIPCHK(hipMemsetAsync(D.cf_fready, 0, sizeof(int) * std::max(NP, 1), p->stream));
             D.cf_zready = dalloc<int>(p, std::max(NP, 1));
-            HIPCHK(hipMemset(D.cf_zready, 0, sizeof(int) * std::max(NP, 1)));
+            HIPCHK(hipMemsetAsync(D.cf_zready, 0, sizeof(int) * std::max(NP, 1), p->stream));
             D.cf_zv = band ? nullptr : dalloc<double>(p, std::max((size_t)NP * NP * CHOL_NB, (size_t)1));
             D.cf_head = dalloc<unsigned long long>(p, 2);   // (ticket counters of the split's two launches)
             D.cf_abort = dalloc<int>(p, 1);
-            HIPCHK(hipMemset(D.cf_lready, 0, sizeof(int) * std::max(ntile, 1)));
-            HIPCHK(hipMemset(D.cf_dready, 0, sizeof(int) * std::max(NP, 1)));
-            HIPCHK(hipMemset(D.cf_head, 0, 2 * sizeof(unsigned long long)));
-            HIPCHK(hipMemset(D.cf_abort, 0, sizeof(int)));
+            HIPCHK(hipMemsetAsync(D.cf_lready, 0, sizeof(int) * std::max(ntile, 1), p->stream));
+            HIPCHK(hipMemsetAsync(D.cf_dready, 0, sizeof(int) * std::max(NP, 1), p->stream));
+            HIPCHK(hipMemsetAsync(D.cf_head, 0, 2 * sizeof(unsigned long long), p->stream));
+            HIPCHK(hipMemsetAsync(D.cf_abort, 0, sizeof(int), p->stream));
         }
         D.cf_rowptr = dupload(p, pl.rowptr);
         D.cf_cols = dupload(p, pl.cols);
@@ -1938,14 +2001,14 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.bp = dalloc<double>(p, p->np + 1);
     D.xsol = dalloc<double>(p, npad + 1);
     D.bS = dalloc<double>(p, npad + 1);
-    HIPCHK(hipMemset(D.bS, 0, sizeof(double) * (npad + 1)));
+    HIPCHK(hipMemsetAsync(D.bS, 0, sizeof(double) * (npad + 1), p->stream));
     D.yv = dalloc<double>(p, npad + 1);
     // S and L start zero (k_assemble writes the identity of the padding rows every time)
-    HIPCHK(hipMemset(D.S, 0, sizeof(double) * (n_env_doubles + 1)));
-    HIPCHK(hipMemset(D.Lm, 0, sizeof(double) * (n_env_doubles + 1)));
-    HIPCHK(hipMemset(D.xsol, 0, sizeof(double) * (npad + 1)));
+    HIPCHK(hipMemsetAsync(D.S, 0, sizeof(double) * (n_env_doubles + 1), p->stream));
+    HIPCHK(hipMemsetAsync(D.Lm, 0, sizeof(double) * (n_env_doubles + 1), p->stream));
+    HIPCHK(hipMemsetAsync(D.xsol, 0, sizeof(double) * (npad + 1), p->stream));
     D.x = dalloc<double>(p, p->np + 3 * (size_t)nl + 1);
-    HIPCHK(hipMemset(D.x, 0, sizeof(double) * (p->np + 3 * (size_t)nl + 1)));   // BlockSolver::_x before any solve
+    HIPCHK(hipMemsetAsync(D.x, 0, sizeof(double) * (p->np + 3 * (size_t)nl + 1), p->stream));   // BlockSolver::_x before any solve
     const int nchi = n_tiles + D.n_prior + D.n_vel + D.n_eprior;
     D.chi_lin = dalloc<double>(p, nchi + 1);
     D.n_chi = nchi;
@@ -1989,16 +2052,17 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.ob_chi2 = dalloc<double>(p, std::max(n_obs, 1));
     D.ob_res = dalloc<double>(p, 3 * (size_t)std::max(n_obs, 1));
     D.depth_ok = dalloc<unsigned char>(p, std::max(n_obs, 1));
-    HIPCHK(hipMemset(D.info, 0, sizeof(int)));
+    HIPCHK(hipMemsetAsync(D.info, 0, sizeof(int), p->stream));
     for (int s = 0; s < 2; ++s) {
         p->kst[s] = dalloc<double>(p, kst.size());
         p->lst[s] = dalloc<double>(p, lst.size());
-        HIPCHK(hipMemcpy(p->kst[s], kst.data(), kst.size() * sizeof(double), hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(p->lst[s], lst.data(), lst.size() * sizeof(double), hipMemcpyHostToDevice));
+        upload_into(p, p->kst[s], kst);
+        upload_into(p, p->lst[s], lst);
         D.kbuf[s] = p->kst[s];
         D.lbuf[s] = p->lst[s];
     }
-    HIPCHK(hipMemset(D.ctl, 0, sizeof(LMCtl)));
+    HIPCHK(hipMemsetAsync(D.ctl, 0, sizeof(LMCtl), p->stream));
+    flush_uploads(p);
     HIPCHK(hipStreamSynchronize(p->stream));   // the staged uploads (dupload) have landed
     mark("solve layout");
     p->cur = 0;
@@ -2699,6 +2763,8 @@ int64_t lba_device_bytes(const lba_problem* p) {
     if (!p) return LBA_E_ARG;
     int64_t b = 0;
     for (size_t k = 0; k < p->alloc_cursor && k < p->allocs.size(); ++k) b += (int64_t)p->allocs[k].bytes;
+    for (size_t k = 0; k < p->up_chunk && k < p->up_end.size(); ++k) b += (int64_t)p->up_end[k];   // (the window's
+    b += (int64_t)p->up_off;                                                                          // read-only arrays)
     return b;
 }
 
