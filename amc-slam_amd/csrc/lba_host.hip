@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <queue>
 #include <limits>
 #include <map>
 #include <string>
@@ -964,9 +965,17 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         const int n_pieces = n_reg >= 256 * SETUP_PIECES ? SETUP_PIECES : 1;
         // LBA_TILE_OBS_CAP (experiments): a smaller observation budget per regular tile than the LDS allows
         const int obs_cap = std::getenv("LBA_TILE_OBS_CAP") ? std::max(1, std::atoi(std::getenv("LBA_TILE_OBS_CAP"))) : TILE_OBS;
+        // LBA_TILE_OBS_CAP_HEAD=<cap>:<pieces> (experiments): that budget in the first <pieces> pieces of the landmark order
+        // only (-<pieces>: the last ones), to make the cheap tiles, dispatched last, smaller (the sweep's second round)
+        int head_cap = obs_cap, head_pieces = 0;
+        if (const char* e = std::getenv("LBA_TILE_OBS_CAP_HEAD")) {
+            head_cap = std::max(1, std::atoi(e));
+            if (const char* c = std::strchr(e, ':')) head_pieces = std::atoi(c + 1);
+        }
         std::vector<TileOut> outs(n_pieces);
         par_for(n_pieces, [&](int piece) {
             TileOut& T = outs[piece];
+            const int cap = (head_pieces >= 0 ? piece < head_pieces : piece >= n_pieces + head_pieces) ? head_cap : obs_cap;
             const int d_end = (int)((long long)n_reg * (piece + 1) / n_pieces);
             int d = (int)((long long)n_reg * piece / n_pieces);
             // the tile's sample / KF sets grow by the landmark's new elements, found through membership
@@ -1009,7 +1018,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     const bool fits = tile_fits(nobs + no, rows + nr, npair + npl, nlmt + 1,
                                                 (int)(uni.size() + new_k.size()), (int)(usm.size() + new_s.size()),
                                                 nent + ne) &&
-                                      (nlmt == 0 || nobs + no <= obs_cap);
+                                      (nlmt == 0 || nobs + no <= cap);
                     for (int v : new_s) smark[v] = fits ? 1 : 0;
                     for (int k : new_k) kmark[k] = fits ? 1 : 0;
                     if (!fits) {
@@ -1412,6 +1421,28 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         mix(sslot); mix(tkf_gslot); mix(seg_slot); mix(ob_row);
         p->setup_hash = h;
         p->setup_tiles = n_tiles;
+        if (const char* e = std::getenv("LBA_TILE_SIM")) {   // (diagnostics) the sweep's predicted span: the tiles
+            // longest first by the cost model below (k_lin_schur's tile_perm) list-scheduled on <e> resident slots
+            const int slots = std::max(1, std::atoi(e));
+            std::vector<double> c(n_stiles);
+            double tot = 0.0;
+            for (int t = 0; t < n_stiles; ++t) {
+                c[t] = 0.027 * t_npair[t] + 0.775 * t_nlm[t] + 0.077 * t_nsent[t] + 1.807 * t_nkf[t];
+                tot += c[t];
+            }
+            std::sort(c.begin(), c.end(), std::greater<double>());
+            std::priority_queue<double, std::vector<double>, std::greater<double>> q;
+            for (int k = 0; k < slots; ++k) q.push(0.0);
+            double span = 0.0;
+            for (double x : c) {
+                const double t0 = q.top();
+                q.pop();
+                q.push(t0 + x);
+                span = std::max(span, t0 + x);
+            }
+            std::fprintf(stderr, "tile sim: %d tiles, %d Schur entries, model work %.0f us, span on %d slots %.1f us\n",
+                         n_stiles, n_sent, tot, slots, span);
+        }
         return LBA_OK;
     }
     // ---- device upload
