@@ -36,6 +36,14 @@
 
 using namespace lba;
 
+// the last panel pattern an engine planned (plan_panels_cached)
+struct PlanCache {
+    int NP = -1, NPk = -1;
+    std::string env;   // (the diagnostics' LBA_ND_* settings it was made under)
+    std::vector<std::vector<int>> lower;
+    lba_plan::Plan plan;
+};
+
 struct lba_problem {
     lba_config cfg{};
     std::string err;
@@ -71,6 +79,7 @@ struct lba_problem {
     uint32_t setup_hash = 0;      // (host_only) fingerprint of the tiling / slab layout
     int setup_tiles = 0;
     std::vector<double> setup_ms; // wall time of the set-up phases (order/pairs, tiles, slots/state, ...)
+    PlanCache plan_cache;
     // device buffers of the window, in set_problem's allocation order; the next set_problem reuses
     // them in the same order where they are large enough (LocalGPBA windows are alike call to call),
     // so a call pays no hipMalloc / hipFree
@@ -169,6 +178,23 @@ lba_plan::Plan plan_panels(int NP, int NPk, const std::vector<std::vector<int>>&
     const char* nm = std::getenv("LBA_ND_METHOD");
     return lba_plan::make_plan(NP, NPk, lower, lv ? std::atoi(lv) : 64, std::getenv("LBA_ND_NO_TAIL") == nullptr, 16,
                                nm ? std::atoi(nm) : 0);
+}
+// The same, remembering the last pattern planned on this engine: consecutive windows of a LocalGPBA sequence
+// usually couple their keyframes in the same band pattern, and the plan is a function of (NP, NPk, pattern) and the
+// diagnostics' environment alone (so a hit returns exactly what make_plan would)
+const lba_plan::Plan& plan_panels_cached(PlanCache& c, int NP, int NPk, const std::vector<std::vector<int>>& lower) {
+    std::string env;
+    for (const char* k : {"LBA_ND_LEVELS", "LBA_ND_METHOD", "LBA_ND_NO_TAIL"}) {
+        const char* v = std::getenv(k);
+        env += v ? std::string(v) + ";" : std::string("-;");
+    }
+    if (c.NP == NP && c.NPk == NPk && c.env == env && c.lower == lower) return c.plan;
+    c.plan = plan_panels(NP, NPk, lower);
+    c.NP = NP;
+    c.NPk = NPk;
+    c.env = env;
+    c.lower = lower;
+    return c.plan;
 }
 
 // Partitioned set-up: every rank reports the outcome of its host preprocessing in one all-reduce at a
@@ -1602,7 +1628,9 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     if (occ[(size_t)P * NP + Q] != 0.0 || Q == P) lower[P].push_back(Q);
             }
         }
-        const lba_plan::Plan pl = plan_panels(NP, NPk, lower);
+        sub("  S pattern");
+        const lba_plan::Plan& pl = plan_panels_cached(p->plan_cache, NP, NPk, lower);
+        sub("  dissection plan");
         p->chain = pl.chain;
         p->nd_tail = pl.tail;
         p->nd_levels = pl.levels;
@@ -1971,6 +1999,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             HIPCHK(hipMemsetAsync(D.cf_head, 0, 2 * sizeof(unsigned long long), p->stream));
             HIPCHK(hipMemsetAsync(D.cf_abort, 0, sizeof(int), p->stream));
         }
+        sub("  flow tasks");
         D.cf_rowptr = dupload(p, pl.rowptr);
         D.cf_cols = dupload(p, pl.cols);
         D.ppos = dupload(p, ppos);
@@ -2016,6 +2045,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     // goes to Sfull, allocated on first use)
     const size_t n_env_doubles = (size_t)D.n_ztiles * CHOL_NB * CHOL_NB;
     p->s_bytes = 2 * n_env_doubles * sizeof(double);
+    sub("  envelope + assembly lists");
     D.Lm = dalloc<double>(p, n_env_doubles + 1);
     D.LinvT = dalloc<double>(p, (size_t)npad * CHOL_NB + 1);
     // Hpl: only the heavy landmarks' canonical pairs, then the segment pairs (regular tiles keep theirs in LDS)
