@@ -59,7 +59,10 @@ constexpr int CHOL_NB = 32;         // Cholesky panel / tile width
 constexpr int CF_DENSE_MAX_NP = 192;   // panels up to which the L^-1-tile solve is allowed (np 6144)
 constexpr int CF_AUTO_BAND_NP = 64;    // above this many panels the substitution solve is the default
                                        // (measured crossover ~65 panels, profiles/r01zr_solve_sweep.txt)
-constexpr int RED_GROUPS = 4;       // reduction kernels: 4 groups x 144 threads
+#ifndef LBA_RED_GROUPS
+#define LBA_RED_GROUPS 4
+#endif
+constexpr int RED_GROUPS = LBA_RED_GROUPS;   // reduction kernels: 4 groups x 144 threads
 
 // Levenberg-Marquardt controller of a queued optimisation (lba_host.hip: optimize_queued).  The host
 // enqueues whole trials without waiting for their outcome; k_finalize applies g2o's acceptance rule

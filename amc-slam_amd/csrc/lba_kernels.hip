@@ -1177,7 +1177,9 @@ __device__ __forceinline__ void assemble_item(const DevProblem& P, int item, dou
         red[tid] = v;
         __syncthreads();
         if (g == 0) {
-            double t = red[e] + red[144 + e] + red[288 + e] + red[432 + e];
+            double t = red[e];
+#pragma unroll
+            for (int q = 1; q < RED_GROUPS; ++q) t += red[144 * q + e];   // (4 groups: ((a + b) + c) + d)
             const int i = e / 12, j = e % 12;
             const int r = 12 * bj + j, c = 12 * bi + i;   // element (row r, col c) of S, r >= c in blocks
             if (bi == bj && e % 13 == 0 && row_adds(P, r)) t += lambda;   // damping: added once over the ranks
@@ -1202,21 +1204,22 @@ __device__ __forceinline__ void assemble_item(const DevProblem& P, int item, dou
             }
     } else {
         const int k = item - P.n_asm;
-        const int e = tid % 12, g = tid / 12;   // 48 groups
+        constexpr int RG = 12 * RED_GROUPS;   // (48 groups of 12 threads)
+        const int e = tid % 12, g = tid / 12;
         double v, w;
         if constexpr (FUSED) {
-            w = slot_sum<48, 12>(P.gpslab, P.gps0[k] + g, P.gps0[k + 1], e);
+            w = slot_sum<RG, 12>(P.gpslab, P.gps0[k] + g, P.gps0[k + 1], e);
             if (wait) exp_wait(P, P.gs_prod, P.gs0[k], P.gs0[k + 1], epoch);
-            v = slot_sum<48, 12, true>(P.gslab, P.gs0[k] + g, P.gs0[k + 1], e);
+            v = slot_sum<RG, 12, true>(P.gslab, P.gs0[k] + g, P.gs0[k + 1], e);
         } else {
-            v = slot_sum<48, 12>(P.gslab, P.gs0[k] + g, P.gs0[k + 1], e);
-            w = (flags & ASM_SCHUR) ? slot_sum<48, 12>(P.gpslab, P.gps0[k] + g, P.gps0[k + 1], e) : 0.0;
+            v = slot_sum<RG, 12>(P.gslab, P.gs0[k] + g, P.gs0[k + 1], e);
+            w = (flags & ASM_SCHUR) ? slot_sum<RG, 12>(P.gpslab, P.gps0[k] + g, P.gps0[k + 1], e) : 0.0;
         }
         red[tid] = v;
         __syncthreads();
         double bpv = 0.0;
         if (tid < 12) {
-            for (int q = 0; q < 48; ++q) bpv += red[q * 12 + tid];
+            for (int q = 0; q < RG; ++q) bpv += red[q * 12 + tid];
             P.bp[12 * k + tid] = bpv;
         }
         __syncthreads();
@@ -1224,7 +1227,7 @@ __device__ __forceinline__ void assemble_item(const DevProblem& P, int item, dou
         __syncthreads();
         if (tid < 12) {
             double t = 0.0;
-            for (int q = 0; q < 48; ++q) t += red[q * 12 + tid];
+            for (int q = 0; q < RG; ++q) t += red[q * 12 + tid];
             const int r = 12 * k + tid;
             const int rh = (flags & ASM_FULL) ? r : P.rpos[r];
             P.bS[rh] = bpv - t;   // bS = b_p - sum Hpl Dinv bl (factorisation order)
