@@ -564,14 +564,22 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     if ((n_kf && !kfs) || (n_lm && !lm_xyz) || (n_obs && !obs) || (n_priors && !priors) || (n_vel && !vel_kfs) ||
         (n_cam && !cams))
         throw ApiError{LBA_E_ARG, "null array with non-zero size"};
-    // the first invalid observation (pieces in parallel; the serial pass below names it)
+    // the first invalid observation (pieces in parallel; the serial pass below names it).  The same pass counts each
+    // piece's observations per landmark (the counting sort into observations by landmark, below) and marks the
+    // keyframes the piece touches (activity): the caller's 64-byte records are read once for the three
+    constexpr int VP = SETUP_PIECES;
     int first_bad = n_obs;
+    const bool lm_hist = n_lm > 0 && (long long)n_lm * VP <= (8LL << 20);   // (else: the serial counting sort)
+    std::vector<int>& lm_cnt = scr_int(p, 13, lm_hist ? (size_t)VP * n_lm : 0);
+    std::vector<char> kf_mark((size_t)VP * std::max(n_kf, 1), 0);
     {
-        constexpr int VP = 8;
         int bad_at[VP];
         par_for(VP, [&](int piece) {
             const int i0 = (int)((long long)n_obs * piece / VP), i1 = (int)((long long)n_obs * (piece + 1) / VP);
             bad_at[piece] = n_obs;
+            int* hc = lm_hist ? lm_cnt.data() + (size_t)piece * n_lm : nullptr;
+            if (hc) std::fill(hc, hc + n_lm, 0);
+            char* km = kf_mark.data() + (size_t)piece * std::max(n_kf, 1);
             for (int i = i0; i < i1; ++i) {
                 const lba_obs& o = obs[i];
                 bool ok = o.kind >= LBA_MONO_GP && o.kind <= LBA_STEREO && o.kf_b >= 0 && o.kf_b < n_kf && o.lm >= 0 &&
@@ -580,6 +588,9 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     ok = o.kf_a >= 0 && o.kf_a < n_kf && o.kf_a != o.kf_b &&
                          std::fabs(kfs[o.kf_b].time - kfs[o.kf_a].time) > 1e-6;
                 if (!ok) { bad_at[piece] = i; break; }
+                if (hc) ++hc[o.lm];
+                km[o.kf_b] = 1;
+                if (is_gp(o.kind)) km[o.kf_a] = 1;
             }
         });
         for (int piece = 0; piece < VP; ++piece) first_bad = std::min(first_bad, bad_at[piece]);
@@ -645,11 +656,39 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     // ---- active vertices (SparseOptimizer::initializeOptimization: a vertex is active if an edge
     //      that is not all-fixed touches it, sparse_optimizer.cpp:197-267)
     std::vector<char> kf_act(n_kf, 0), lm_act(n_lm, 0);
-    for (int i = 0; i < n_obs; ++i) {
-        lm_act[obs[i].lm] = 1;
-        kf_act[obs[i].kf_b] = 1;
-        if (is_gp(obs[i].kind)) kf_act[obs[i].kf_a] = 1;
+    for (int piece = 0; piece < VP; ++piece)
+        for (int k = 0; k < n_kf; ++k) kf_act[k] |= kf_mark[(size_t)piece * std::max(n_kf, 1) + k];
+    // observations by original landmark (stable): a counting sort, the counts from the validation pass
+    std::vector<int> lo0(n_lm + 1, 0);
+    std::vector<int>& lo_of = scr_int(p, 1, n_obs);
+    if (lm_hist) {
+        par_for(VP, [&](int piece) {   // per landmark: its total, and every piece's offset (its earlier pieces' counts)
+            for (int l = (int)((long long)n_lm * piece / VP); l < (int)((long long)n_lm * (piece + 1) / VP); ++l) {
+                int run = 0;
+                for (int q = 0; q < VP; ++q) {
+                    int& c = lm_cnt[(size_t)q * n_lm + l];
+                    const int v = c;
+                    c = run;
+                    run += v;
+                }
+                lo0[l + 1] = run;
+            }
+        });
+        for (int l = 0; l < n_lm; ++l) lo0[l + 1] += lo0[l];
+        par_for(VP, [&](int piece) {
+            int* off = lm_cnt.data() + (size_t)piece * n_lm;
+            for (int i = (int)((long long)n_obs * piece / VP); i < (int)((long long)n_obs * (piece + 1) / VP); ++i) {
+                const int l = obs[i].lm;
+                lo_of[lo0[l] + off[l]++] = i;
+            }
+        });
+    } else {
+        for (int i = 0; i < n_obs; ++i) lo0[obs[i].lm + 1]++;
+        for (int l = 0; l < n_lm; ++l) lo0[l + 1] += lo0[l];
+        std::vector<int> fill(lo0.begin(), lo0.end() - 1);
+        for (int i = 0; i < n_obs; ++i) lo_of[fill[obs[i].lm]++] = i;
     }
+    for (int l = 0; l < n_lm; ++l) lm_act[l] = lo0[l + 1] > lo0[l];
     std::vector<lba_prior> pri;
     for (int i = 0; i < n_priors; ++i)
         if (!(kfs[priors[i].kf_a].fixed && kfs[priors[i].kf_b].fixed)) {
@@ -778,7 +817,10 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     // pose sample of every observation: its GP sample, or the KF pose record n_gps + kf_b
     const int n_gps = (int)gps_t.size(), n_smp = n_gps + n_kfs;
     std::vector<int>& smp_of = scr_int(p, 0, n_obs);
-    for (int i = 0; i < n_obs; ++i) smp_of[i] = is_gp(obs[i].kind) ? sample_of[i] : n_gps + obs[i].kf_b;
+    par_for(VP, [&](int piece) {
+        for (int i = (int)((long long)n_obs * piece / VP); i < (int)((long long)n_obs * (piece + 1) / VP); ++i)
+            smp_of[i] = is_gp(obs[i].kind) ? sample_of[i] : n_gps + obs[i].kf_b;
+    });
 
     // ---- heavy landmarks: a landmark whose observations / keyframes exceed one tile of k_lin_schur (a
     //      long track: LocalGPBA adds every observation of a local point, up to every keyframe of the
@@ -789,15 +831,6 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         return no <= TILE_OBS && nr <= TILE_ROWS && npair <= TILE_PAIRS && nlmt <= TILE_LMS && nkf <= TILE_KF &&
                ns <= TILE_SMP && ne <= TILE_PROWS;
     };
-    // observations by original landmark (stable)
-    std::vector<int> lo0(n_lm + 1, 0);
-    std::vector<int>& lo_of = scr_int(p, 1, n_obs);
-    for (int i = 0; i < n_obs; ++i) lo0[obs[i].lm + 1]++;
-    for (int l = 0; l < n_lm; ++l) lo0[l + 1] += lo0[l];
-    {
-        std::vector<int> fill(lo0.begin(), lo0.end() - 1);
-        for (int i = 0; i < n_obs; ++i) lo_of[fill[obs[i].lm]++] = i;
-    }
     // per landmark: the span of non-fixed KFs observing it (device order key), heavy or not
     std::vector<int> lmin(n_lm, INT_MAX), lmax(n_lm, INT_MAX), lm_npl(n_lm, 0);
     std::vector<char> heavy(n_lm, 0);
