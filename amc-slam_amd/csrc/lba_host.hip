@@ -738,22 +738,44 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     sub("checks + activity");
     // GP (prev KF, KF) pairs, numbered in order of first appearance; gp_of: each GP observation's pair
     // (per KF b a short list of its pairs: (KF a, pair index); usually one, the previous keyframe)
+    // (in parallel: every piece lists its distinct pairs in first-appearance order; the pieces' lists, merged in
+    // piece order, give the pairs in first appearance over all observations; then every GP observation's pair)
     std::vector<std::vector<std::pair<int, int>>> gp_by_b(n_kf);
     std::vector<int> gp_a, gp_b, gp_of(n_obs, -1);
-    for (int i = 0; i < n_obs; ++i)
-        if (is_gp(obs[i].kind)) {
-            auto& lst = gp_by_b[obs[i].kf_b];
-            int g = -1;
-            for (const auto& e : lst)
-                if (e.first == obs[i].kf_a) { g = e.second; break; }
-            if (g < 0) {
-                g = (int)gp_a.size();
-                lst.emplace_back(obs[i].kf_a, g);
-                gp_a.push_back(obs[i].kf_a);
-                gp_b.push_back(obs[i].kf_b);
+    {
+        std::vector<std::vector<std::pair<int, int>>> first(VP);   // per piece: (kf_a, kf_b) in first-appearance order
+        par_for(VP, [&](int piece) {
+            std::vector<std::vector<int>> seen_a(n_kf);   // per KF b: the KFs a this piece has listed
+            auto& out = first[piece];
+            for (int i = (int)((long long)n_obs * piece / VP); i < (int)((long long)n_obs * (piece + 1) / VP); ++i) {
+                const lba_obs& o = obs[i];
+                if (!is_gp(o.kind)) continue;
+                std::vector<int>& sa = seen_a[o.kf_b];
+                if (std::find(sa.begin(), sa.end(), o.kf_a) != sa.end()) continue;
+                sa.push_back(o.kf_a);
+                out.emplace_back(o.kf_a, o.kf_b);
             }
-            gp_of[i] = g;
-        }
+        });
+        for (int piece = 0; piece < VP; ++piece)
+            for (const auto& ab : first[piece]) {
+                auto& lst = gp_by_b[ab.second];
+                bool have = false;
+                for (const auto& e : lst)
+                    if (e.first == ab.first) { have = true; break; }
+                if (have) continue;
+                lst.emplace_back(ab.first, (int)gp_a.size());
+                gp_a.push_back(ab.first);
+                gp_b.push_back(ab.second);
+            }
+        par_for(VP, [&](int piece) {
+            for (int i = (int)((long long)n_obs * piece / VP); i < (int)((long long)n_obs * (piece + 1) / VP); ++i) {
+                const lba_obs& o = obs[i];
+                if (!is_gp(o.kind)) continue;
+                for (const auto& e : gp_by_b[o.kf_b])
+                    if (e.first == o.kf_a) { gp_of[i] = e.second; break; }
+            }
+        });
+    }
     sub("  GP pair numbering");
 
     // GP pose samples: distinct observation times per GP pair (one per camera time stamp in
