@@ -84,6 +84,7 @@ FLAG_BAND_SOLVE = 8        # reduced system solved by substitution after the fac
 FLAG_DENSE_SOLVE = 16      # force the L^-1-tile solve
 FLAG_TIME_SAMPLED = 32     # with FLAG_TIME_SWEEP (queued loop): events on every 10th trial only
 FLAG_SUBTREE_SOLVE = 64    # partitioned: distributed factorisation (window split by lba_partition_assign)
+FLAG_F32_RESIDUAL = 128    # per-observation projection / residual / Jacobian rows in fp32, sums in fp64
 
 
 def make_config(qc_diag=(0.02, 0.02, 0.02, 0.002, 0.002, 0.002), huber_mono=None, huber_stereo=None,

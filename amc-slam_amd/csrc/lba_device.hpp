@@ -273,6 +273,9 @@ struct DevProblem {
     // no free extrinsics); upd_flag [n_gp + KF blocks]: a producer's epoch once its samples / states are stored,
     // smp_prod [n_smp]: the producer of each pose sample (its GP pair, or the KF block of a KF pose sample)
     int fuse_eval;
+    // the fp32-residual option (LBA_FLAG_F32_RESIDUAL): the kernels' per-observation projection, residuals and
+    // Jacobian rows in fp32, every sum in fp64 (k_lin_schur / k_update / k_eval's <true> instantiations)
+    int f32res;
     int* upd_flag;
     const int* smp_prod;
     // fused expansion + assembly (k_exp_asm; no heavy landmarks, not partitioned): exp_flag [n_smp] a pose sample's

@@ -2137,6 +2137,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     // segment tiles and trial states are other workgroups') nor free extrinsics (the trial camera records); only
     // when the whole k_update grid is resident at once (its evaluating workgroups wait for its producers), and
     // not for partitioned problems (ranks of an in-process group share one device)
+    D.f32res = (p->cfg.flags & LBA_FLAG_F32_RESIDUAL) ? 1 : 0;
     D.fuse_eval = (n_heavy == 0 && n_ext == 0 && p->part_n == 0 && std::getenv("LBA_NO_FUSED_EVAL") == nullptr) ? 1 : 0;
     if (D.fuse_eval) {
         static thread_local int resident = -1;   // (per device ordinal in practice: one value per process)

@@ -178,7 +178,7 @@ __device__ __forceinline__ double obs_pose(const double* gps, const double* kst,
 // One observation of the linearisation (DIM compile-time so every per-row array stays in
 // registers): residual, Huber weight, the rows [J1 e Jp] into the LDS row buffer (J1 w.r.t. the
 // pose sample: the pose / velocity Jacobian J1 N is never formed, see k_linearize); returns rho(chi2).
-template <int DIM>
+template <int DIM, bool F32 = false>
 __device__ __forceinline__ double lin_obs(const DevProblem& P, const double* gps, const double* kst, const double* lst,
                                           const double* camd, int o, const ObsIn& in, int cam, bool gp, double* rows,
                                           double* rw, int write_res) {
@@ -192,14 +192,14 @@ __device__ __forceinline__ double lin_obs(const DevProblem& P, const double* gps
     for (int d = 0; d < DIM; ++d) z[d] = in.z[d];
     const double w = in.w;
     double Xb[3], Xc[3], e[DIM];
-    project_residual<DIM>(Rwb, twb, cd, Xw, z, bf, Xb, Xc, e);
+    project_residual_p<DIM, F32>(Rwb, twb, cd, Xw, z, bf, Xb, Xc, e);
     double chi = 0.0;
 #pragma unroll
     for (int d = 0; d < DIM; ++d) chi += e[d] * (w * e[d]);
     double r0, r1;
     huber(chi, DIM == 3 ? P.huber_stereo : P.huber_mono, &r0, &r1);
     double J1[6 * DIM], Jp[3 * DIM];
-    obs_j1<DIM>(Rwb, cd, Xb, Xc, bf, J1, Jp);
+    obs_j1_p<DIM, F32>(Rwb, cd, Xb, Xc, bf, J1, Jp);
     const double s = r1 * w;   // robustInformation = rho' * Omega (base_edge.h:96-102), Omega = w I
     const int row = P.ob_row[o] & 0xffff;
 #pragma unroll
@@ -221,7 +221,7 @@ __device__ __forceinline__ double lin_obs(const DevProblem& P, const double* gps
 
 // Residual-only evaluation of one observation (computeError + robust chi2) at the body pose (Rwb, twb) and
 // landmark Xw; returns rho(chi2).
-template <int DIM>
+template <int DIM, bool F32 = false>
 __device__ __forceinline__ double eval_obs_at(const DevProblem& P, const double* Rwb, const double* twb, double bf,
                                               const double* Xw, const double* camd, int o, const ObsIn& in, int cam) {
     CamD cd;
@@ -231,7 +231,7 @@ __device__ __forceinline__ double eval_obs_at(const DevProblem& P, const double*
     for (int d = 0; d < DIM; ++d) z[d] = in.z[d];
     const double w = in.w;
     double Xb[3], Xc[3], e[DIM];
-    project_residual<DIM>(Rwb, twb, cd, Xw, z, bf, Xb, Xc, e);
+    project_residual_p<DIM, F32>(Rwb, twb, cd, Xw, z, bf, Xb, Xc, e);
     double chi = 0.0;
 #pragma unroll
     for (int d = 0; d < DIM; ++d) chi += e[d] * (w * e[d]);
@@ -240,13 +240,13 @@ __device__ __forceinline__ double eval_obs_at(const DevProblem& P, const double*
     P.ob_chi2[o] = chi;
     return r0;
 }
-template <int DIM>
+template <int DIM, bool F32 = false>
 __device__ __forceinline__ double eval_obs(const DevProblem& P, const double* gps, const double* kst,
                                            const double* lst, const double* camd, int o, const ObsIn& in, int cam,
                                            bool gp) {
     double Rwb[9], twb[3];
     const double bf = obs_pose(gps, kst, in, gp, Rwb, twb);
-    return eval_obs_at<DIM>(P, Rwb, twb, bf, lst + (size_t)in.lm * 3, camd, o, in, cam);
+    return eval_obs_at<DIM, F32>(P, Rwb, twb, bf, lst + (size_t)in.lm * 3, camd, o, in, cam);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -708,6 +708,8 @@ static_assert(2 * TILE_PAIRS <= LS_THREADS && TILE_KF * TILE_KF <= LS_THREADS &&
                   TILE_LMS <= LS_THREADS && 2 * TILE_SMP <= LS_THREADS && TILE_PROWS <= LS_THREADS,
               "one staging element / Hpl half / KF-pair slot per thread");
 
+// F32: the fp32-residual option (LBA_FLAG_F32_RESIDUAL): phase 1's projection, residuals and Jacobian rows in fp32
+template <bool F32>
 __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int sel, int gate, double lambda_arg,
                                                              int mode) {
     __shared__ double U[LS_U];
@@ -792,8 +794,8 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
         const bool st = kind == LBA_STEREO_GP || kind == LBA_STEREO;
         orow[tid] = (orw & 0xffff) | ((st ? 3 : 2) << 16);
         const int wr = (mode & LS_RES) ? 1 : 0;
-        rho0 = st ? lin_obs<3>(P, gps, kst, lst, camd, o, in, cam, gp, rows, rw, wr)
-                  : lin_obs<2>(P, gps, kst, lst, camd, o, in, cam, gp, rows, rw, wr);
+        rho0 = st ? lin_obs<3, F32>(P, gps, kst, lst, camd, o, in, cam, gp, rows, rw, wr)
+                  : lin_obs<2, F32>(P, gps, kst, lst, camd, o, in, cam, gp, rows, rw, wr);
     }
     const double tchi = block_sum<LS_THREADS>(rho0, red);   // (its barrier also publishes rows / lists)
     if (tid == 0) P.chi_lin[tile] = tchi;
@@ -2619,7 +2621,7 @@ __device__ __attribute__((noinline)) void kf_trial_state(const double* __restric
 // G_o = rho' w sum_rows J1^T Jp (the observation's part of every Hpl block it feeds, k_lin_schur phase 3) and
 // t_s = N_s x (the step of the observation's pose sample), G_o^T t = rho' w sum_rows Jp^T (J1 t).  The
 // linearisation is recomputed at the state the sweep linearised (the same inputs and code as lin_obs).
-template <int DIM>
+template <int DIM, bool F32 = false>
 __device__ __forceinline__ void bs_obs(const DevProblem& P, const double* gps, const double* kst, const double* lst,
                                        const double* camd, const ObsIn& in, int cam, bool gp, const double* t,
                                        double* v) {
@@ -2632,14 +2634,14 @@ __device__ __forceinline__ void bs_obs(const DevProblem& P, const double* gps, c
     for (int d = 0; d < DIM; ++d) z[d] = in.z[d];
     const double w = in.w;
     double Xb[3], Xc[3], e[DIM];
-    project_residual<DIM>(Rwb, twb, cd, lst + (size_t)in.lm * 3, z, bf, Xb, Xc, e);
+    project_residual_p<DIM, F32>(Rwb, twb, cd, lst + (size_t)in.lm * 3, z, bf, Xb, Xc, e);
     double chi = 0.0;
 #pragma unroll
     for (int d = 0; d < DIM; ++d) chi += e[d] * (w * e[d]);
     double r0, r1;
     huber(chi, DIM == 3 ? P.huber_stereo : P.huber_mono, &r0, &r1);
     double J1[6 * DIM], Jp[3 * DIM];
-    obs_j1<DIM>(Rwb, cd, Xb, Xc, bf, J1, Jp);
+    obs_j1_p<DIM, F32>(Rwb, cd, Xb, Xc, bf, J1, Jp);
     const double s = r1 * w;
     v[0] = v[1] = v[2] = 0.0;
 #pragma unroll
@@ -2688,6 +2690,7 @@ constexpr int BS_SHM = TILE_SMP * 6 + TILE_OBS * 3;
 // tasks before their data loads, and the landmark's own inputs at entry, so a tile costs a handful of memory
 // round trips instead of one chain per task.)
 // (ltr, optional, LDS [TILE_LMS][3]: the tile's trial landmark positions, for the fused evaluation)
+template <bool F32>
 __device__ double bs_tile(const DevProblem& P, int tile, int si, bool ok, double lambda, double* lo, double* shm,
                           unsigned long long* stamp, double* ltr = nullptr) {
     double(*tsh)[6] = reinterpret_cast<double(*)[6]>(shm);                  // t_s per tile sample
@@ -2756,8 +2759,8 @@ __device__ double bs_tile(const DevProblem& P, int tile, int si, bool ok, double
                 const int kind = meta & 15, cam = meta >> 4;
                 const bool gp = kind <= LBA_STEREO_GP;
                 const double* t = tsh[orw >> 16];
-                if (kind == LBA_STEREO_GP || kind == LBA_STEREO) bs_obs<3>(P, gps, kst, lst, camd, in, cam, gp, t, vsh[ol]);
-                else bs_obs<2>(P, gps, kst, lst, camd, in, cam, gp, t, vsh[ol]);
+                if (kind == LBA_STEREO_GP || kind == LBA_STEREO) bs_obs<3, F32>(P, gps, kst, lst, camd, in, cam, gp, t, vsh[ol]);
+                else bs_obs<2, F32>(P, gps, kst, lst, camd, in, cam, gp, t, vsh[ol]);
             }
         }
         __syncthreads();
@@ -2857,6 +2860,7 @@ __device__ __forceinline__ void eval_tile_prefetch(const DevProblem& P, int tile
             to[k].bf = kst[(size_t)(gp ? to[k].in.kfa : to[k].in.kfb) * KF_STRIDE + 14];
         }
 }
+template <bool F32>
 __device__ __forceinline__ void eval_tile_trial(const DevProblem& P, int tile, int si, const double* ltr,
                                                 const TrialObs (&to)[UPD_TILE_OBS_PER_THREAD]) {
     const int tid = threadIdx.x;
@@ -2881,8 +2885,8 @@ __device__ __forceinline__ void eval_tile_trial(const DevProblem& P, int tile, i
             const int kind = to[k].meta & 15, cam = to[k].meta >> 4;
             const double* Xw = ltr + 3 * (to[k].in.lm - lm0);
             rho[k] = (kind == LBA_STEREO_GP || kind == LBA_STEREO)
-                         ? eval_obs_at<3>(P, Rwb[k], twb[k], to[k].bf, Xw, camd, to[k].o, to[k].in, cam)
-                         : eval_obs_at<2>(P, Rwb[k], twb[k], to[k].bf, Xw, camd, to[k].o, to[k].in, cam);
+                         ? eval_obs_at<3, F32>(P, Rwb[k], twb[k], to[k].bf, Xw, camd, to[k].o, to[k].in, cam)
+                         : eval_obs_at<2, F32>(P, Rwb[k], twb[k], to[k].bf, Xw, camd, to[k].o, to[k].in, cam);
         }
     }
     // k_eval: one observation per thread of TILE_OBS = 2 x 64; block_sum = wave sums, then 0 + wave 0 + wave 1
@@ -2921,6 +2925,7 @@ __device__ void prior_eval_t(const DevProblem& P, const double* __restrict__ kst
 // at once (P.fuse_eval, set from the occupancy), so a waiting workgroup never holds a slot a producer needs,
 // whatever the dispatch order.  (Roles from an atomic ticket instead, for any grid size, cost one same-address
 // atomic per workgroup: +10 us per trial at config 1, +700 us at config 2, profiles/r4i_ab_fused_eval_ticket_rejected.txt.)
+template <bool F32>
 __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lambda_arg, int sel, int gate, int jac,
                                                         int eval, unsigned epoch) {
     __shared__ double red[UPD_THREADS / 64];
@@ -3036,7 +3041,7 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
         if (fused) upd_publish(P, role, epoch);
         if (kst_stamp) kst_stamp[3] = __builtin_amdgcn_s_memrealtime();
     } else if (role < P.n_gp + nkb + P.n_stiles) {
-        sc = bs_tile(P, role - P.n_gp - nkb, si, ok, lambda, lo, ushm,
+        sc = bs_tile<F32>(P, role - P.n_gp - nkb, si, ok, lambda, lo, ushm,
                      ustamp ? P.tdbg_lin + (size_t)blockIdx.x * 16 + 5 : nullptr, fused ? ltr : nullptr);
         tile_eval = fused;
     } else {
@@ -3082,7 +3087,7 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
         if (ustamp) ustamp[-2] = __builtin_amdgcn_s_memrealtime();   // (slot 12: waiting)
         upd_wait(P, prod, epoch);   // (its barrier also completes ltr)
         if (ustamp) ustamp[-1] = __builtin_amdgcn_s_memrealtime();   // (slot 13: samples in)
-        eval_tile_trial(P, role - P.n_gp - nkb, si, ltr, to);
+        eval_tile_trial<F32>(P, role - P.n_gp - nkb, si, ltr, to);
     }
     if (ustamp) ustamp[1] = __builtin_amdgcn_s_memrealtime();
 }
@@ -3098,6 +3103,7 @@ __device__ __forceinline__ void prior_eval(const DevProblem& P, const double* __
 // velocity edges.  (The trial summary stays a separate k_finalize launch: having the last workgroup
 // do it needs a device-scope release per workgroup, i.e. an L2 writeback each on this multi-XCD
 // part, measured 3x slower than the extra launch.)
+template <bool F32>
 __global__ __launch_bounds__(TILE_OBS) void k_eval(DevProblem P, int sel, int gate) {
     __shared__ double red[TILE_OBS / 64];
     const int tile = blockIdx.x, tid = threadIdx.x;
@@ -3115,8 +3121,8 @@ __global__ __launch_bounds__(TILE_OBS) void k_eval(DevProblem P, int sel, int ga
             const ObsIn in = obs_in(P, o);
             const int kind = meta & 15, cam = meta >> 4;
             const bool gp = kind <= LBA_STEREO_GP;
-            rho0 = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? eval_obs<3>(P, gps, kst, lst, camd, o, in, cam, gp)
-                                                                 : eval_obs<2>(P, gps, kst, lst, camd, o, in, cam, gp);
+            rho0 = (kind == LBA_STEREO_GP || kind == LBA_STEREO) ? eval_obs<3, F32>(P, gps, kst, lst, camd, o, in, cam, gp)
+                                                                 : eval_obs<2, F32>(P, gps, kst, lst, camd, o, in, cam, gp);
         }
         const double s = block_sum<TILE_OBS>(rho0, red);
         if (tid == 0) P.chi_eval[tile] = s;
@@ -3396,9 +3402,11 @@ void launch_lin_schur(const DevProblem& P, int sel, int gate, double lambda, int
     const dim3 g(P.n_tiles + ne);
     if (g.x == 0) return;
     if (e0)   // the events carry the dispatch's own start / end timestamps
-        hipExtLaunchKernelGGL(k_lin_schur, g, dim3(LS_THREADS), 0, s, e0, e1, 0, P, sel, gate, lambda, mode);
+        hipExtLaunchKernelGGL(P.f32res ? k_lin_schur<true> : k_lin_schur<false>, g, dim3(LS_THREADS), 0, s, e0, e1, 0, P,
+                              sel, gate, lambda, mode);
     else
-        hipLaunchKernelGGL(k_lin_schur, g, dim3(LS_THREADS), 0, s, P, sel, gate, lambda, mode);
+        hipLaunchKernelGGL(P.f32res ? k_lin_schur<true> : k_lin_schur<false>, g, dim3(LS_THREADS), 0, s, P, sel, gate,
+                           lambda, mode);
 }
 void launch_expand(const DevProblem& P, int sel, int gate, double lambda, int schur, hipStream_t s) {
     const int n = P.n_smp + P.n_heavy;
@@ -3461,7 +3469,11 @@ int update_grid(const DevProblem& P, int eval) {
 }
 int update_resident_blocks(int device) {
     int per_cu = 0, ncu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_update, UPD_THREADS, 0) != hipSuccess) return 0;
+    int per_cu32 = 0;   // (the fp32-residual instantiation too: the fused evaluation needs either resident at once)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_update<false>, UPD_THREADS, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu32, k_update<true>, UPD_THREADS, 0) != hipSuccess)
+        return 0;
+    per_cu = per_cu < per_cu32 ? per_cu : per_cu32;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
     return per_cu * ncu;
 }
@@ -3469,11 +3481,12 @@ void launch_update(const DevProblem& P, double lambda, int sel, int gate, int ja
                    unsigned epoch) {
     const int fused = eval && P.fuse_eval;
     const int nb = P.n_upd_blocks + (fused ? cdiv(P.n_prior + P.n_vel, UPD_THREADS) : 0);
-    hipLaunchKernelGGL(k_update, dim3(nb), dim3(UPD_THREADS), 0, s, P, lambda, sel, gate, jac, fused, epoch);
+    hipLaunchKernelGGL(P.f32res ? k_update<true> : k_update<false>, dim3(nb), dim3(UPD_THREADS), 0, s, P, lambda, sel,
+                       gate, jac, fused, epoch);
 }
 void launch_eval(const DevProblem& P, int sel, int gate, unsigned long long seq, int mode, hipStream_t s) {
     const int nb = P.n_tiles + cdiv(P.n_prior + P.n_vel + P.n_eprior, TILE_OBS);
-    if (nb) hipLaunchKernelGGL(k_eval, dim3(nb), dim3(TILE_OBS), 0, s, P, sel, gate);
+    if (nb) hipLaunchKernelGGL(P.f32res ? k_eval<true> : k_eval<false>, dim3(nb), dim3(TILE_OBS), 0, s, P, sel, gate);
     if (mode != FIN_NONE) launch_finalize(P, seq, mode, s);
 }
 void launch_partials(const DevProblem& P, hipStream_t s) {

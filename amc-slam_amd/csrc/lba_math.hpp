@@ -538,16 +538,76 @@ LBA_HD void obs_j1(const double* Rwb, const CamD& c, const double* Xb, const dou
             Jp[r * 3 + j] = -(M[r * 3 + 0] * Rwb[j * 3 + 0] + M[r * 3 + 1] * Rwb[j * 3 + 1] + M[r * 3 + 2] * Rwb[j * 3 + 2]);
 }
 
+// fp32-residual option (LBA_FLAG_F32_RESIDUAL, BASELINE configs[4]: "fp32 residuals + fp64 accumulate"): the
+// same two functions with the projection, the residual and the Jacobian rows in fp32.  The world offset Xw - twb
+// stays fp64 (a trajectory kilometres long would otherwise lose millimetres to fp32 rounding before the
+// rotation); the results are widened to fp64 for the robust weight and every sum of J^T W J / J^T W e.
+template <int DIM>
+LBA_HD void project_residual_f32(const double* Rwb, const double* twb, const CamD& c, const double* Xw, const double* z,
+                                 double bf, double* Xb, double* Xc, double* e) {
+    const float d0 = (float)(Xw[0] - twb[0]), d1 = (float)(Xw[1] - twb[1]), d2 = (float)(Xw[2] - twb[2]);
+    float xb[3], xc[3];
+    for (int j = 0; j < 3; ++j) xb[j] = (float)Rwb[j] * d0 + (float)Rwb[3 + j] * d1 + (float)Rwb[6 + j] * d2;
+    for (int i = 0; i < 3; ++i)
+        xc[i] = (float)c.Rcb[i * 3] * xb[0] + (float)c.Rcb[i * 3 + 1] * xb[1] + (float)c.Rcb[i * 3 + 2] * xb[2] +
+                (float)c.tcb[i];
+    const float u = (float)c.fx * xc[0] / xc[2] + (float)c.cx;
+    const float v = (float)c.fy * xc[1] / xc[2] + (float)c.cy;
+    e[0] = (double)((float)z[0] - u);
+    e[1] = (double)((float)z[1] - v);
+    if (DIM == 3) e[2] = (double)((float)z[2] - (u - (float)bf * (1.0f / xc[2])));
+    for (int k = 0; k < 3; ++k) {
+        Xb[k] = (double)xb[k];
+        Xc[k] = (double)xc[k];
+    }
+}
+template <int DIM>
+LBA_HD void obs_j1_f32(const double* Rwb, const CamD& c, const double* Xb, const double* Xc, double bf, double* J1,
+                       double* Jp) {
+    const float x0 = (float)Xc[0], x1 = (float)Xc[1], x2 = (float)Xc[2];
+    const float iz = 1.0f / x2, fx = (float)c.fx, fy = (float)c.fy;
+    float Pj[9];
+    Pj[0] = fx * iz; Pj[1] = 0.0f; Pj[2] = -fx * x0 / (x2 * x2);
+    Pj[3] = 0.0f; Pj[4] = fy * iz; Pj[5] = -fy * x1 / (x2 * x2);
+    if (DIM == 3) { Pj[6] = Pj[0]; Pj[7] = Pj[1]; Pj[8] = Pj[2] + (float)bf * (1.0f / (x2 * x2)); }
+    float M[3 * DIM];
+    for (int r = 0; r < DIM; ++r)
+        for (int j = 0; j < 3; ++j)
+            M[r * 3 + j] = Pj[r * 3] * (float)c.Rcb[j] + Pj[r * 3 + 1] * (float)c.Rcb[3 + j] + Pj[r * 3 + 2] * (float)c.Rcb[6 + j];
+    const float b0 = (float)Xb[0], b1 = (float)Xb[1], b2 = (float)Xb[2];
+    const float H[9] = {0.0f, -b2, b1, b2, 0.0f, -b0, -b1, b0, 0.0f};
+    for (int r = 0; r < DIM; ++r)
+        for (int j = 0; j < 3; ++j) {
+            J1[r * 6 + j] = (double)M[r * 3 + j];
+            J1[r * 6 + 3 + j] = (double)(-(M[r * 3] * H[j] + M[r * 3 + 1] * H[3 + j] + M[r * 3 + 2] * H[6 + j]));
+            Jp[r * 3 + j] = (double)(-(M[r * 3] * (float)Rwb[j * 3] + M[r * 3 + 1] * (float)Rwb[j * 3 + 1] +
+                                      M[r * 3 + 2] * (float)Rwb[j * 3 + 2]));
+        }
+}
+// the projection of the requested precision (F32: the fp32-residual option)
+template <int DIM, bool F32>
+LBA_HD void project_residual_p(const double* Rwb, const double* twb, const CamD& c, const double* Xw, const double* z,
+                               double bf, double* Xb, double* Xc, double* e) {
+    if constexpr (F32) project_residual_f32<DIM>(Rwb, twb, c, Xw, z, bf, Xb, Xc, e);
+    else project_residual<DIM>(Rwb, twb, c, Xw, z, bf, Xb, Xc, e);
+}
+template <int DIM, bool F32>
+LBA_HD void obs_j1_p(const double* Rwb, const CamD& c, const double* Xb, const double* Xc, double bf, double* J1,
+                     double* Jp) {
+    if constexpr (F32) obs_j1_f32<DIM>(Rwb, c, Xb, Xc, bf, J1, Jp);
+    else obs_j1<DIM>(Rwb, c, Xb, Xc, bf, J1, Jp);
+}
+
 // Full Jacobian rows, columns [KF_a pose(6) vel(6) | KF_b pose(6) vel(6) | point(3)] (27):
 //   GP edges: pose/vel columns = J1 N (N of the observation's GP sample, stored transposed);
 //   EdgeMono/EdgeStereo: KF_b pose columns = J1, velocity columns 0.
 // Output row r: pose/vel columns 0..23 at J[r*ldJ + c], point columns at J[r*ldJ + pcol + j]
 // (host harness: ldJ 27, pcol 24).  The kernels keep J1 and reduce in the sample's space instead.
-template <int DIM, typename OutT, typename NT>
+template <int DIM, typename OutT, typename NT, bool F32 = false>
 LBA_HD void obs_jacobian(const double* Rwb, const CamD& c, const double* Xb, const double* Xc, double bf,
                          const NT* N, OutT* J, int ldJ, int pcol) {
     double J1[6 * DIM], Jp[3 * DIM];
-    obs_j1<DIM>(Rwb, c, Xb, Xc, bf, J1, Jp);
+    obs_j1_p<DIM, F32>(Rwb, c, Xb, Xc, bf, J1, Jp);
     for (int r = 0; r < DIM; ++r)
         for (int j = 0; j < 3; ++j) J[r * ldJ + pcol + j] = Jp[r * 3 + j];
     if (!N) {

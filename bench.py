@@ -241,6 +241,8 @@ def main():
                     help="reduced-system solve: L^-1 tiles (dense) or substitution (band); auto picks by size")
     ap.add_argument("--dry-launch", action="store_true",
                     help="with --gpus N > 1 and no launcher: print the rank launch and exit (no GPU)")
+    ap.add_argument("--f32-residual", action="store_true",
+                    help="BASELINE configs[4]'s fp32 residuals + fp64 accumulate (LBA_FLAG_F32_RESIDUAL; default fp64)")
     args = ap.parse_args()
     rc = launch_ranks(args, sys.argv[1:])
     if rc is not None:
@@ -269,6 +271,8 @@ def main():
     # factored by every rank); otherwise window farming (config 3) or a single window
     gba = args.config.startswith("cfg4")
     solve_flag = {"auto": 0, "band": amc_lba.abi.FLAG_BAND_SOLVE, "dense": amc_lba.abi.FLAG_DENSE_SOLVE}[args.solve]
+    if args.f32_residual:
+        solve_flag |= amc_lba.abi.FLAG_F32_RESIDUAL
     # the timed run records the dispatch timestamps of every k_lin_schur and k_chol_flow launch
     # (LBA_FLAG_TIME_SWEEP): the rooflines below are measured live, per launch, over the timed region
     flags = solve_flag | {"every": amc_lba.abi.FLAG_TIME_SWEEP, "off": 0,
@@ -463,7 +467,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if gba else "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f32 residuals + f64 accumulate" if args.f32_residual else "f64",
             "data": "synthetic (deterministic generator, amc_lba/synth.py, seed %d)" % args.seed,
             "config": {"workload": workload, "n_kf": int(len(W.kfs)), "n_opt_kf": int((W.kfs["fixed"] == 0).sum()),
                        "n_lm": int(len(W.lm)), "n_obs": int(len(W.obs)), "n_pairs": int(W.n_pairs),

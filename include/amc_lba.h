@@ -64,6 +64,11 @@ extern "C" {
                                      system (each rank factors its subtree of the nested dissection, the ranks
                                      sum their contributions to the top separators, every rank factors the
                                      top); the window must be split by lba_partition_assign */
+#define LBA_FLAG_F32_RESIDUAL 128 /* the fp32-residual option of BASELINE configs[4] ("fp32 residuals + fp64
+                                     accumulate"): each observation's projection, residual and Jacobian rows in
+                                     fp32 (the world offset Xw - twb in fp64), the robust weights and every sum of
+                                     H / b, the Schur complement and the solve in fp64; results within fp32
+                                     rounding of the fp64 path, not bitwise */
 
 /* LM termination codes in lba_stats.result (OptimizationAlgorithm::SolverResult) */
 #define LBA_RESULT_OK         0

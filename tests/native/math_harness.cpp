@@ -15,8 +15,9 @@ static SE3 mk(const double* q, const double* t) {
     return T;
 }
 
-extern "C" int mh_obs_linearize(const lba_kf* kfs, const double* lm, const lba_obs* o, const lba_cam* cams,
-                                double* err, double* J) {
+template <bool F32>
+static int obs_linearize(const lba_kf* kfs, const double* lm, const lba_obs* o, const lba_cam* cams, double* err,
+                         double* J) {
     const int dim = (o->kind == LBA_STEREO_GP || o->kind == LBA_STEREO) ? 3 : 2;
     const bool gp = (o->kind == LBA_MONO_GP || o->kind == LBA_STEREO_GP);
     Cam c;
@@ -52,13 +53,22 @@ extern "C" int mh_obs_linearize(const lba_kf* kfs, const double* lm, const lba_o
     const double* N = gp ? S.N : nullptr;
     err[2] = 0.0;
     if (dim == 3) {
-        project_residual<3>(Rwb, twb, cd, lm + 3 * o->lm, o->z, bf, Xb, Xc, err);
-        obs_jacobian<3>(Rwb, cd, Xb, Xc, bf, N, J, 27, 24);
+        project_residual_p<3, F32>(Rwb, twb, cd, lm + 3 * o->lm, o->z, bf, Xb, Xc, err);
+        obs_jacobian<3, double, double, F32>(Rwb, cd, Xb, Xc, bf, N, J, 27, 24);
     } else {
-        project_residual<2>(Rwb, twb, cd, lm + 3 * o->lm, o->z, bf, Xb, Xc, err);
-        obs_jacobian<2>(Rwb, cd, Xb, Xc, bf, N, J, 27, 24);
+        project_residual_p<2, F32>(Rwb, twb, cd, lm + 3 * o->lm, o->z, bf, Xb, Xc, err);
+        obs_jacobian<2, double, double, F32>(Rwb, cd, Xb, Xc, bf, N, J, 27, 24);
     }
     return dim;
+}
+extern "C" int mh_obs_linearize(const lba_kf* kfs, const double* lm, const lba_obs* o, const lba_cam* cams,
+                                double* err, double* J) {
+    return obs_linearize<false>(kfs, lm, o, cams, err, J);
+}
+// the fp32-residual option's per-observation math (LBA_FLAG_F32_RESIDUAL)
+extern "C" int mh_obs_linearize_f32(const lba_kf* kfs, const double* lm, const lba_obs* o, const lba_cam* cams,
+                                    double* err, double* J) {
+    return obs_linearize<true>(kfs, lm, o, cams, err, J);
 }
 
 extern "C" void mh_gp_scalars(double t1, double t2, double t, double* out3) {

@@ -79,3 +79,28 @@ def test_gp_scalars_vs_closed_form(harness):
         s = tau / T
         np.testing.assert_allclose(out, [3 * s * s - 2 * s ** 3, tau ** 2 * (tau - T) / T ** 2, tau * (1 - s) ** 2],
                                    rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.parametrize("seed,kw", [(1, {}), (2, {"stereo_frac": 1.0}), (4, {"gp": False, "n_cam": 1}),
+                                     (6, {"global_ba": True, "n_opt_kf": 40})])
+def test_obs_f32_residual_option_within_fp32_rounding(harness, seed, kw):
+    """The fp32-residual option (LBA_FLAG_F32_RESIDUAL, BASELINE configs[4]): each observation's projection,
+    residual and Jacobian rows in fp32 (the world offset Xw - twb in fp64).  Against the oracle's fp64 edge
+    (src/G2oTypes.cc:258-495): residuals within 2e-4 px, Jacobian rows within 2e-6 of their block maximum
+    (fp32's 6e-8 relative rounding through a handful of operations on pixel-scale values)."""
+    args = dict(n_opt_kf=6, n_lm=200, obs_per_lm=6, n_cam=4, gp=True, seed=seed)
+    args.update(kw)
+    win = make_window(**args)
+    o = orc.Oracle(win)
+    de, dj = 0.0, 0.0
+    for i in range(0, len(win.obs), max(1, len(win.obs) // 400)):
+        e0, J0 = o.obs_linearize(i)
+        e = np.zeros(3)
+        J = np.zeros((3, 27))
+        d = harness.mh_obs_linearize_f32(ptr(win.kfs), ptr(win.lm), ptr(win.obs[i:i + 1].copy()), ptr(win.cams),
+                                         _d(e), _d(J))
+        assert d == len(e0)
+        de = max(de, np.abs(e[:d] - e0).max())
+        dj = max(dj, np.abs(J[:d] - J0).max() / np.abs(J0).max())
+    assert 1e-7 < de <= 2e-4, de   # (above fp64 rounding: the fp32 path really ran)
+    assert dj <= 2e-6, dj
