@@ -128,3 +128,19 @@ def test_setup_pool_back_to_back_passes(threads):
     piece count (a pass with more pieces right after one with fewer is where a late worker of the old pass
     could claim a piece of the new one): every piece runs exactly once, inside its own pass."""
     assert _pool_stress(threads, 20000, 64) == 0
+
+
+def test_header_constants_match_the_python_mirror():
+    """Every LBA_FLAG_* bit, status code and observation kind the header defines has the same value in amc_lba.abi
+    (a caller of either side sets the same bits)."""
+    src = open(HEADER).read()
+    macros = {m: int(v) for m, v in re.findall(r"^#define\s+(LBA_\w+)\s+(-?\d+)", src, flags=re.M)}
+    flags = {m: v for m, v in macros.items() if m.startswith("LBA_FLAG_")}
+    assert "LBA_FLAG_F32_RESIDUAL" in flags
+    for m, v in flags.items():
+        assert getattr(abi, m[len("LBA_"):]) == v, m
+    assert len(set(flags.values())) == len(flags) and all(v & (v - 1) == 0 for v in flags.values())   # one bit each
+    for m in ("LBA_OK", "LBA_E_EMPTY", "LBA_E_SOLVE", "LBA_E_DIVERGED", "LBA_E_ARG", "LBA_E_HIP", "LBA_E_LIMIT"):
+        assert getattr(abi, m) == macros[m], m
+    for m in ("LBA_MONO_GP", "LBA_STEREO_GP", "LBA_MONO", "LBA_STEREO"):
+        assert getattr(abi, m[len("LBA_"):]) == macros[m], m
