@@ -10,6 +10,7 @@ import os
 
 import numpy as np
 
+from . import abi as _abi
 from .abi import (CAM_DTYPE, KF_DTYPE, OBS_DTYPE, PRIOR_DTYPE, LbaConfig, LbaStats, make_config,  # noqa: F401
                   ptr)
 
@@ -90,6 +91,7 @@ def lib():
         L.lba_farm_plan.argtypes = [vp, _lp, _ip, _lp, _ip, _ip]
         L.lba_farm_exchange.argtypes = [vp]
         L.lba_solver_info.argtypes = [vp, _ip]
+        L.lba_kernel_modes.argtypes = [vp, _ip]
         if hasattr(L, "lba_debug_pool_stress"):
             L.lba_debug_pool_stress.argtypes = [ctypes.c_int32, ctypes.c_int32]
             L.lba_debug_lie.argtypes = [ctypes.c_int32, ctypes.c_int32, _dp, _dp]
@@ -119,7 +121,7 @@ def exported_symbols():
             "lba_pose_dim", "lba_set_partition", "lba_rccl_unique_id", "lba_set_partition_rccl", "lba_group_create",
             "lba_group_destroy", "lba_set_partition_group", "lba_get_cams", "lba_set_farm", "lba_set_farm_rccl",
             "lba_set_farm_group", "lba_farm_plan", "lba_farm_exchange", "lba_farm_match", "lba_solver_info", "lba_solver_flops", "lba_device_bytes", "lba_setup_phases",
-            "lba_setup_host_profile", "lba_debug_pool_stress", "lba_debug_lie", "lba_partition_assign", "lba_kf_owner", "lba_split_info"]
+            "lba_kernel_modes", "lba_setup_host_profile", "lba_debug_pool_stress", "lba_debug_lie", "lba_partition_assign", "lba_kf_owner", "lba_split_info"]
 
 
 def setup_host_profile(win, **cfg_over):
@@ -167,6 +169,10 @@ def partition_assign(win, nranks, kf=False, **cfg_over):
     distributed factorisation (LBA_FLAG_SUBTREE_SOLVE).  Returns (lm_rank, prior_rank, vel_rank, panels) with
     panels = [panels of the system, panels in the top, columns of the largest subtree]; with kf=True also the
     keyframes' ranks (-1: the top or fixed)."""
+    if np.any(np.asarray(win.cams["ext_free"]) != 0):
+        # (the C call sees no cameras and plans the keyframe-only pattern; a partitioned set-up rejects free extrinsics)
+        raise LbaError(_abi.LBA_E_LIMIT, "partition_assign: free extrinsics (lba_cam.ext_free) are not supported in a "
+                                    "partitioned problem")
     kw = dict(win.cfg)
     kw.update(cfg_over)
     cfg = make_config(**kw)
@@ -350,6 +356,12 @@ class Problem:
         self._check(lib().lba_solver_info(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
         return dict(zip(("tail", "panels", "tiles", "band", "chain", "levels", "s_tiles", "fill"),
                         (int(v) for v in out)))
+
+    def kernel_modes(self):
+        """lba_kernel_modes: dict(fuse_eval, fuse_asm, f32res, update_grid)."""
+        out = np.zeros(4, dtype=np.int32)
+        self._check(lib().lba_kernel_modes(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return dict(zip(("fuse_eval", "fuse_asm", "f32res", "update_grid"), (int(v) for v in out)))
 
     def solver_flops(self):
         """lba_solver_flops: (factorisation, substitutions) algorithmic FLOPs of one solve."""

@@ -35,6 +35,7 @@ MONO_GP, STEREO_GP, MONO, STEREO = 0, 1, 2, 3
 
 # status codes
 LBA_OK, LBA_E_EMPTY, LBA_E_SOLVE, LBA_E_DIVERGED, LBA_E_ARG, LBA_E_HIP, LBA_E_LIMIT = 0, -1, -2, -3, -4, -5, -6
+LBA_E_TIMEOUT = -7
 
 
 class LbaConfig(ctypes.Structure):

@@ -26,6 +26,11 @@ def partition_window(win, rank, nranks, assign=None):
     replicated solve's split (l % nranks, edges on rank 0)."""
     if nranks <= 1:
         return win, np.arange(len(win.lm))
+    if np.any(np.asarray(win.cams["ext_free"]) != 0):
+        # a partitioned lba_set_problem rejects free extrinsics (LBA_E_LIMIT), and lba_partition_assign, which sees no
+        # cameras, plans the keyframe-only pattern: refuse the split up front rather than fail later on some rank
+        raise ValueError("partition_window: free extrinsics (lba_cam.ext_free) are not supported in a partitioned "
+                         "problem; optimise the extrinsic pass (bExtrinsic) on one GPU")
     if assign is None:
         lm_ids = np.arange(rank, len(win.lm), nranks)
         pri_keep = np.full(len(win.priors), rank == 0)

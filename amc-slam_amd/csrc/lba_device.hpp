@@ -96,6 +96,9 @@ enum { GATE_NONE = 0, GATE_TRIAL = 1, GATE_LIN = 2 };
 // (lba_solve_step at any lambda, negative ones included: BlockSolver::setLambda takes any value) is used as is
 constexpr double LAMBDA_CTL = __builtin_nan("");
 
+// fault codes (DevProblem::fault): which bounded wait timed out
+enum { FAULT_FLOW = 1, FAULT_EXP = 2, FAULT_UPD = 4 };
+
 struct DevProblem {
     int n_kf, n_lm, n_obs, n_gp, n_pairs, n_tiles, n_pb, np, n_prior, n_vel, n_cam;
     int npad;               // np rounded up to CHOL_NB: leading dimension of S / Lm (identity tail)
@@ -240,14 +243,6 @@ struct DevProblem {
     double* cf_zv;          // [NP][NP][CHOL_NB] shares Linv(i, k) b_k of the forward solve
     unsigned long long* cf_head;
     int* cf_abort;
-    // fused flow (unpartitioned): the expansion and the assembly run as k_chol_flow's first tasks
-    int cf_fused;
-    int* cf_cnt;            // [cf_ncnt] counters, zeroed by k_lin_schur (see CholFlow)
-    int cf_ncnt;
-    const int* cf_need;     // [cf_ncnt]
-    const int* cf_asm_item; // per assembly item: id | type << 28
-    const int* cf_asm_tgt;  // per assembly item: 4 counter indices
-    int cf_ntile;           // envelope tiles of the permuted system
     int cf_band;            // 1: solve by substitution tasks (no L^-1 tiles, large systems)
     double* cf_xpos;        // band solve: x in factorisation order (handed off between back tasks)
     double* LinvT;          // [npad / CHOL_NB][CHOL_NB][CHOL_NB] inverse diagonal blocks L_bb^-T (row-major)
@@ -290,6 +285,9 @@ struct DevProblem {
     LMCtl* ctl;             // queued-optimisation controller
     int* hlog;              // host-mapped [HLOG_CAP]: per queued trial, 1 if it relinearised
     int* info;              // [1] factorisation status
+    // [1] a bounded in-launch wait that gave up (FAULT_*, never expected): the data it waited for may be stale, so
+    // k_finalize publishes it (hfin[5]) and the host fails the call with LBA_E_TIMEOUT instead of using the results
+    int* fault;
     double* fin;            // [4] chi_lin, chi_eval, scale, info
     double* hfin;           // host-mapped coherent [4] copy of fin + [4] sequence number (as bits)
     double* ob_chi2;        // [n_obs]
@@ -348,9 +346,8 @@ enum { ASM_SCHUR = 1, ASM_FULL = 2, ASM_DIAG = 4 };
 void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hipStream_t s);
 // k_expand (schur) + k_assemble (ASM_SCHUR) of a trial in one launch (P.fuse_asm); epoch: one more than the last
 void launch_exp_asm(const DevProblem& P, int sel, int gate, double lambda, unsigned epoch, hipStream_t s);
-// (fused flow: sel / lambda of the expansion and assembly it runs first)
 void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s, hipEvent_t e0 = nullptr,
-                           hipEvent_t e1 = nullptr, int sel = 0, double lambda = 0.0);
+                           hipEvent_t e1 = nullptr);
 // the step + trial state + the trial state's pose samples (jac: with their Jacobian factors)
 // eval: with P.fuse_eval, also the trial state's errors (k_eval's chi_eval / ob_chi2), no k_eval launch needed;
 // update_grid: its workgroups; update_resident_blocks: k_update workgroups resident at once on the device

@@ -384,9 +384,10 @@ T* dupload(lba_problem* p, const std::vector<T>& v) {
     return d;
 }
 
-// f(i) for i in [0, n) on up to 8 host threads, at most the CPUs this process may run on (LBA_SETUP_THREADS
-// overrides; 1: serial; 16 threads measured no faster on a 16-CPU share of the GPU box, the serial parts of the
-// set-up dominate, profiles/r3ai_setup_threads.txt).  Callers split work into a fixed number of pieces, so the
+// f(i) for i in [0, n) on up to SETUP_THREADS_MAX (16) host threads, at most the CPUs this process may run on
+// (LBA_SETUP_THREADS overrides; 1: serial).  Round 3 measured 16 threads no faster than 8
+// (profiles/r3ai_setup_threads.txt); round 4's parallel tile-list concatenation and device-order records made
+// the 16-piece passes scale, and 16 is the default since (profiles/r4z_setup_phases.txt).  Callers split work into a fixed number of pieces, so the
 // results never depend on the thread count.  The workers persist (a set-up makes a dozen parallel passes;
 // spawning threads per pass cost ~0.1 ms each) and, after a pass, poll for the next one for a while before
 // they sleep: a set-up's passes follow each other within a millisecond, and an OS wake-up of the workers per
@@ -1044,19 +1045,11 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 t_nkf, tkf_list, tsm_smp, tsm_rows, sent_l1, sent_l2, sent_k1, sent_k2, pair_rows, lm_rows;
         };
         const int n_pieces = n_reg >= 256 * SETUP_PIECES ? SETUP_PIECES : 1;
-        // LBA_TILE_OBS_CAP (experiments): a smaller observation budget per regular tile than the LDS allows
-        const int obs_cap = std::getenv("LBA_TILE_OBS_CAP") ? std::max(1, std::atoi(std::getenv("LBA_TILE_OBS_CAP"))) : TILE_OBS;
-        // LBA_TILE_OBS_CAP_HEAD=<cap>:<pieces> (experiments): that budget in the first <pieces> pieces of the landmark order
-        // only (-<pieces>: the last ones), to make the cheap tiles, dispatched last, smaller (the sweep's second round)
-        int head_cap = obs_cap, head_pieces = 0;
-        if (const char* e = std::getenv("LBA_TILE_OBS_CAP_HEAD")) {
-            head_cap = std::max(1, std::atoi(e));
-            if (const char* c = std::strchr(e, ':')) head_pieces = std::atoi(c + 1);
-        }
+        const int obs_cap = TILE_OBS;
         std::vector<TileOut> outs(n_pieces);
         par_for(n_pieces, [&](int piece) {
             TileOut& T = outs[piece];
-            const int cap = (head_pieces >= 0 ? piece < head_pieces : piece >= n_pieces + head_pieces) ? head_cap : obs_cap;
+            const int cap = obs_cap;
             const int d_end = (int)((long long)n_reg * (piece + 1) / n_pieces);
             int d = (int)((long long)n_reg * piece / n_pieces);
             // the tile's sample / KF sets grow by the landmark's new elements, found through membership
@@ -1502,28 +1495,6 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         mix(sslot); mix(tkf_gslot); mix(seg_slot); mix(ob_row);
         p->setup_hash = h;
         p->setup_tiles = n_tiles;
-        if (const char* e = std::getenv("LBA_TILE_SIM")) {   // (diagnostics) the sweep's predicted span: the tiles
-            // longest first by the cost model below (k_lin_schur's tile_perm) list-scheduled on <e> resident slots
-            const int slots = std::max(1, std::atoi(e));
-            std::vector<double> c(n_stiles);
-            double tot = 0.0;
-            for (int t = 0; t < n_stiles; ++t) {
-                c[t] = 0.027 * t_npair[t] + 0.775 * t_nlm[t] + 0.077 * t_nsent[t] + 1.807 * t_nkf[t];
-                tot += c[t];
-            }
-            std::sort(c.begin(), c.end(), std::greater<double>());
-            std::priority_queue<double, std::vector<double>, std::greater<double>> q;
-            for (int k = 0; k < slots; ++k) q.push(0.0);
-            double span = 0.0;
-            for (double x : c) {
-                const double t0 = q.top();
-                q.pop();
-                q.push(t0 + x);
-                span = std::max(span, t0 + x);
-            }
-            std::fprintf(stderr, "tile sim: %d tiles, %d Schur entries, model work %.0f us, span on %d slots %.1f us\n",
-                         n_stiles, n_sent, tot, slots, span);
-        }
         return LBA_OK;
     }
     // ---- device upload
@@ -1777,7 +1748,6 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             // top's for a top column
             auto same_part = [&](int pp, int o) { return !split || own[pp] == o; };
             const std::vector<int>& rank = pl.rank;
-            const bool no_lookahead = std::getenv("LBA_CHOL_NO_LOOKAHEAD") != nullptr;
             auto by_rank = [&](int x, int y) { return rank[x] < rank[y]; };
             // row c's columns below the diagonal
             auto rowcols = [&](int c) {
@@ -1808,7 +1778,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     // lookahead over k = c - 1 when tile (c, k) exists and k is the last update of A(c, c)
                     // in update order (then every copy of a tile sees the same update order)
                     const int k = c - 1;
-                    bool la = !no_lookahead && k >= 0 && pl.nz(c, k) && same_part(k, own[c]);
+                    bool la = k >= 0 && pl.nz(c, k) && same_part(k, own[c]);
                     for (int pp : rcc)
                         if (la && pp != k && rank[pp] > rank[k]) la = false;
                     const int tcc = pl.tile_id(c, c), tic = i == c ? -1 : pl.tile_id(i, c);
@@ -1926,94 +1896,6 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 end_task();
             }
             if (NP >= (1 << 24)) throw ApiError{LBA_E_LIMIT, "internal: too many panels for the dataflow factorisation"};
-            // fused flow (LBA_FLOW_FUSED=1; one problem, not partitioned): the pose-sample expansions and
-            // heavy landmarks, then the assembly items (padding rows, rhs per pose block, S blocks) in the
-            // order the columns they feed are factored, ahead of the factor tasks; a counter per tile of L /
-            // panel rhs tells the factor tasks when their operands are assembled (the assembly items address
-            // the slabs with 32-bit buffer offsets)
-            const long long slab_max = 8LL * std::max((long long)n_hslots * 144, (long long)n_sslots * 144);
-            const bool fused = p->part_n == 0 && std::getenv("LBA_FLOW_FUSED") && slab_max < (1LL << 31);
-            D.cf_fused = fused ? 1 : 0;
-            D.cf_ntile = ntile;
-            D.cf_ncnt = 1 + ntile + NP;
-            if (fused) {
-                std::vector<int> need(D.cf_ncnt, 0), aitem, atgt, prefix;
-                std::vector<int> akey;   // assembly item -> first update rank among the columns it feeds
-                std::vector<int> tile_col(ntile);
-                for (int i = 0; i < NP; ++i)
-                    for (int q = pl.rowptr[i]; q < pl.rowptr[i + 1]; ++q) tile_col[q] = pl.cols[q];
-                need[0] = n_smp + n_heavy;
-                for (int e = 0; e < n_smp; ++e) prefix.push_back(e | (8 << 24));
-                for (int h = 0; h < n_heavy; ++h) prefix.push_back(h | (9 << 24));
-                auto tile_cnt = [&](int rh, int ch) {
-                    return 1 + pl.tile_id(std::max(rh, ch) / CHOL_NB, std::min(rh, ch) / CHOL_NB);
-                };
-                auto add_item = [&](int code, const std::vector<int>& tg, int key) {
-                    if (tg.size() > 4) throw ApiError{LBA_E_LIMIT, "internal: assembly item feeds more than 4 tiles"};
-                    aitem.push_back(code);
-                    for (int q = 0; q < 4; ++q) atgt.push_back(q < (int)tg.size() ? tg[q] : -1);
-                    for (int cc : tg) need[cc]++;
-                    akey.push_back(key);
-                };
-                auto uniq = [](std::vector<int> v) {
-                    std::sort(v.begin(), v.end());
-                    v.erase(std::unique(v.begin(), v.end()), v.end());
-                    return v;
-                };
-                auto col_rank = [&](int cc) {   // counter -> update rank of the column it belongs to
-                    if (cc > ntile) return rank[cc - 1 - ntile];
-                    return rank[tile_col[cc - 1]];
-                };
-                auto key_of = [&](const std::vector<int>& tg) {
-                    int kk = NP;
-                    for (int cc : tg) kk = std::min(kk, col_rank(cc));
-                    return kk;
-                };
-                if (npad > p->np) {   // padding rows
-                    std::vector<int> tg;
-                    for (int r = p->np; r < npad; ++r) {
-                        tg.push_back(tile_cnt(rpos[r], rpos[r]));
-                        tg.push_back(1 + ntile + rpos[r] / CHOL_NB);
-                    }
-                    tg = uniq(tg);
-                    add_item(0, tg, -1);
-                }
-                for (int k = 0; k < n_pb; ++k) {   // rhs of pose block k
-                    std::vector<int> tg;
-                    for (int r = 12 * k; r < 12 * k + 12; ++r) tg.push_back(1 + ntile + rpos[r] / CHOL_NB);
-                    tg = uniq(tg);
-                    add_item(k | (1 << 28), tg, key_of(tg));
-                }
-                for (int u = 0; u < n_ublocks; ++u) {   // S blocks (k_assemble's asm_list)
-                    if (!(hcnt[u] > 0 || scnt[u] > 0 || ub_i[u] == ub_j[u])) continue;
-                    std::vector<int> tg;
-                    for (int e = 0; e < 144; ++e) {
-                        const int i = e / 12, j = e % 12, r = 12 * ub_j[u] + j, cc = 12 * ub_i[u] + i;
-                        if (ub_i[u] != ub_j[u] || j >= i) tg.push_back(tile_cnt(rpos[r], rpos[cc]));
-                    }
-                    tg = uniq(tg);
-                    add_item(u | (2 << 28), tg, key_of(tg));
-                }
-                std::vector<int> ord(aitem.size());
-                for (size_t q = 0; q < ord.size(); ++q) ord[q] = (int)q;
-                std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return akey[x] < akey[y]; });
-                std::vector<int> aitem2, atgt2;
-                for (int q : ord) {
-                    prefix.push_back((int)aitem2.size() | (10 << 24));
-                    aitem2.push_back(aitem[q]);
-                    for (int w = 0; w < 4; ++w) atgt2.push_back(atgt[4 * q + w]);
-                }
-                const size_t npre = prefix.size();
-                tasks.insert(tasks.begin(), prefix.begin(), prefix.end());
-                task_i.insert(task_i.begin(), npre, 0);
-                task_t.insert(task_t.begin(), 5 * npre, -1);
-                pl0.insert(pl0.begin(), npre, 0);
-                D.cf_need = dupload(p, need);
-                D.cf_asm_item = dupload(p, aitem2);
-                D.cf_asm_tgt = dupload(p, atgt2);
-                D.cf_cnt = dalloc<int>(p, D.cf_ncnt);
-                HIPCHK(hipMemsetAsync(D.cf_cnt, 0, sizeof(int) * D.cf_ncnt, p->stream));
-            }
             D.cf_tasks = dupload(p, tasks);
             D.cf_task_i = dupload(p, task_i);
             D.cf_task_t = dupload(p, task_t);
@@ -2140,8 +2022,18 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.f32res = (p->cfg.flags & LBA_FLAG_F32_RESIDUAL) ? 1 : 0;
     D.fuse_eval = (n_heavy == 0 && n_ext == 0 && p->part_n == 0 && std::getenv("LBA_NO_FUSED_EVAL") == nullptr) ? 1 : 0;
     if (D.fuse_eval) {
-        static thread_local int resident = -1;   // (per device ordinal in practice: one value per process)
-        if (resident < 0) resident = update_resident_blocks(p->cfg.device);
+        // (the occupancy of k_update on this device, computed once per device ordinal; the guarantee is for one
+        // k_update launch on the device at a time -- problems of an in-process group, which share a device, never
+        // fuse -- see include/amc_lba.h, lba_set_problem)
+        static std::mutex res_mu;
+        static std::map<int, int> resident_of;
+        int resident;
+        {
+            std::lock_guard<std::mutex> lk(res_mu);
+            auto it = resident_of.find(p->cfg.device);
+            if (it == resident_of.end()) it = resident_of.emplace(p->cfg.device, update_resident_blocks(p->cfg.device)).first;
+            resident = it->second;
+        }
         if (update_grid(D, 1) > resident) D.fuse_eval = 0;
     }
     {   // the producer of every pose sample (fused evaluation): its GP pair, or the KF block of a KF pose sample
@@ -2157,13 +2049,15 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     }
     // k_expand + k_assemble of a trial in one launch (LBA_NO_FUSED_ASM: two): not with heavy landmarks (their merge
     // is k_expand's), partitioned problems or the fused factorisation flow (which assembles S itself)
-    D.fuse_asm = (n_heavy == 0 && p->part_n == 0 && !D.cf_fused && std::getenv("LBA_NO_FUSED_ASM") == nullptr) ? 1 : 0;
+    D.fuse_asm = (n_heavy == 0 && p->part_n == 0 && std::getenv("LBA_NO_FUSED_ASM") == nullptr) ? 1 : 0;
     D.hs_prod = dupload(p, hs_prod);
     D.gs_prod = dupload(p, gs_prod);
     D.exp_flag = dalloc<int>(p, (size_t)FLAG_STRIDE * std::max(D.n_smp, 1));
     HIPCHK(hipMemsetAsync(D.exp_flag, 0, sizeof(int) * FLAG_STRIDE * std::max(D.n_smp, 1), p->stream));
     p->asm_epoch = 0;
     D.info = dalloc<int>(p, 1);
+    D.fault = dalloc<int>(p, 1);
+    HIPCHK(hipMemsetAsync(D.fault, 0, sizeof(int), p->stream));
     D.ctl = dalloc<LMCtl>(p, 1);
     D.fin = dalloc<double>(p, 4);
     D.ob_chi2 = dalloc<double>(p, std::max(n_obs, 1));
@@ -2202,6 +2096,24 @@ void linearize(lba_problem* p, int write_res) {
     p->linearized = true;
 }
 
+// A bounded in-launch wait gave up (DevProblem::fault, never expected): the data it waited for may be stale, so
+// the call fails instead of returning results computed from it; the word is cleared for the next call
+[[noreturn]] void throw_fault(lba_problem* p, int code) {
+    HIPCHK(hipStreamSynchronize(p->stream));
+    HIPCHK(hipMemset(p->D.fault, 0, sizeof(int)));
+    throw ApiError{LBA_E_TIMEOUT, std::string("a device hand-off wait timed out (") +
+                                      ((code & FAULT_FLOW) ? " factorisation" : "") + ((code & FAULT_EXP) ? " assembly" : "") +
+                                      ((code & FAULT_UPD) ? " trial evaluation" : "") +
+                                      " ); the problem's state is undefined until the next lba_set_problem"};
+}
+// the same check after calls that do not publish a trial summary (one 4-byte read after the stream's work)
+void check_fault(lba_problem* p) {
+    int f = 0;
+    HIPCHK(hipMemcpyAsync(&f, p->D.fault, sizeof(int), hipMemcpyDeviceToHost, p->stream));
+    HIPCHK(hipStreamSynchronize(p->stream));
+    if (f) throw_fault(p, f);
+}
+
 // poll the published sequence number (see finalize_and_wait)
 void wait_seq(lba_problem* p, unsigned long long seq) {
     volatile unsigned long long* flag = reinterpret_cast<volatile unsigned long long*>(p->h_fin + 4);
@@ -2213,6 +2125,7 @@ void wait_seq(lba_problem* p, unsigned long long seq) {
         }
     }
     std::atomic_thread_fence(std::memory_order_acquire);
+    if (p->h_fin[5] != 0.0) throw_fault(p, (int)p->h_fin[5]);
 }
 
 // Publish the trial summary (k_finalize writes it into host-mapped memory) and wait for it by
@@ -2234,12 +2147,11 @@ void finalize_and_wait(lba_problem* p, bool sync, int eval_sel = -1) {
 
 // k_assemble into S (ASM_SCHUR: the factorisation-order packed envelope a trial factors), Sfull (ASM_FULL:
 // the natural dense H_pp of lba_linearize) or Sdiag (ASM_DIAG: its diagonal, computeLambdaInit)
-void assemble_layout(lba_problem* p, double lambda, int flags, int gate = GATE_NONE, bool launch = true) {
+void assemble_layout(lba_problem* p, double lambda, int flags, int gate = GATE_NONE) {
     if (flags & ASM_FULL) {   // the dense natural-order H_pp (lba_linearize): its own buffer, made on first use
         if (!p->D.Sfull) p->D.Sfull = dalloc<double>(p, (size_t)p->np * p->np + 1);
         HIPCHK(hipMemsetAsync(p->D.Sfull, 0, sizeof(double) * ((size_t)p->np * p->np), p->stream));
     }
-    if (!launch) return;   // (the fused flow assembles S itself)
     launch_assemble(p->D, lambda, flags, gate, p->stream);
     if ((flags & ASM_SCHUR) && p->part_n > 0 && !p->D.cf_split) {   // sum the ranks' reduced systems
         launch_env_pack(p->D, 0, gate, p->stream);
@@ -2257,7 +2169,7 @@ void launch_solve(lba_problem* p, hipEvent_t e0, hipEvent_t e1, int sel, double 
     const DevProblem& D = p->D;
     const unsigned epoch = ++p->cf_epoch;
     if (!D.cf_split) {
-        launch_cholesky_solve(D, GATE_NONE, epoch, p->stream, e0, e1, sel, lambda);
+        launch_cholesky_solve(D, GATE_NONE, epoch, p->stream, e0, e1);
         return;
     }
     launch_cholesky_part(D, 0, epoch, p->stream, e0, nullptr);
@@ -2291,13 +2203,11 @@ void trial(lba_problem* p, double lambda, bool evaluate, hipEvent_t* evs, bool s
     launch_lin_schur(D, p->cur, GATE_NONE, lambda, LS_SCHUR | LS_EDGES, p->stream, sweep ? p->ev[6] : nullptr,
                      sweep ? p->ev[7] : nullptr);
     if (evs) HIPCHK(hipEventRecord(evs[1], p->stream));
-    // (fused flow: the expansion and the assembly are k_chol_flow's first tasks; the phase events then time
-    // them with the solve)
     if (D.fuse_asm) {
         launch_exp_asm(D, p->cur, GATE_NONE, lambda, ++p->asm_epoch, p->stream);
     } else {
-        if (!D.cf_fused) launch_expand(D, p->cur, GATE_NONE, lambda, 1, p->stream);
-        assemble_layout(p, lambda, ASM_SCHUR, GATE_NONE, !D.cf_fused);
+        launch_expand(D, p->cur, GATE_NONE, lambda, 1, p->stream);
+        assemble_layout(p, lambda, ASM_SCHUR, GATE_NONE);
     }
     if (evs) HIPCHK(hipEventRecord(evs[2], p->stream));
     launch_solve(p, sweep ? p->ev[8] : nullptr, sweep ? p->ev[9] : nullptr, p->cur, lambda);
@@ -2406,8 +2316,8 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
             if (D.fuse_asm) {
                 launch_exp_asm(D, SEL_CUR, GATE_TRIAL, LAMBDA_CTL, ++p->asm_epoch, p->stream);
             } else {
-                if (!D.cf_fused) launch_expand(D, SEL_CUR, GATE_TRIAL, LAMBDA_CTL, 1, p->stream);
-                assemble_layout(p, LAMBDA_CTL, ASM_SCHUR, GATE_NONE, !D.cf_fused);
+                launch_expand(D, SEL_CUR, GATE_TRIAL, LAMBDA_CTL, 1, p->stream);
+                assemble_layout(p, LAMBDA_CTL, ASM_SCHUR, GATE_NONE);
             }
             launch_solve(p, qe ? qe[2] : nullptr, qe ? qe[3] : nullptr, SEL_CUR, LAMBDA_CTL);
             // the step, the trial state and its pose samples with their Jacobian factors: the next
@@ -2883,6 +2793,15 @@ int64_t lba_device_bytes(const lba_problem* p) {
     for (size_t k = 0; k < p->up_chunk && k < p->up_end.size(); ++k) b += (int64_t)p->up_end[k];   // (the window's
     b += (int64_t)p->up_off;                                                                          // read-only arrays)
     return b;
+}
+
+int lba_kernel_modes(const lba_problem* p, int32_t out[4]) {
+    if (!p || !out || !p->has_problem) return LBA_E_ARG;
+    out[0] = p->D.fuse_eval;
+    out[1] = p->D.fuse_asm;
+    out[2] = p->D.f32res;
+    out[3] = update_grid(p->D, 1);
+    return LBA_OK;
 }
 
 int lba_solver_info(const lba_problem* p, int32_t out[8]) {
@@ -3391,6 +3310,9 @@ int lba_eval(lba_problem* p, double* chi2_robust, double* obs_chi2, uint8_t* dep
             for (int i = 0; i < p->n_obs; ++i) depth_ok[i] = h[p->obs_dev[i]];
         }
         return LBA_OK;
+    } catch (const ApiError& e) {
+        p->err = e.msg;
+        return e.code;
     } catch (const HipError& e) {
         return map_error(p, e);
     }
@@ -3433,7 +3355,7 @@ int lba_linearize(lba_problem* p, double* residuals, double* H_pp, double* b, do
         if (residuals)
             HIPCHK(hipMemcpyAsync(res.data(), D.ob_res, 3 * (size_t)p->n_obs * sizeof(double), hipMemcpyDeviceToHost,
                                   p->stream));
-        HIPCHK(hipStreamSynchronize(p->stream));
+        check_fault(p);
         const std::vector<int>& X = p->pose_ext;   // internal pose index -> caller's (extrinsics 6 wide)
         if (H_pp)
             for (int i = 0; i < np; ++i)
@@ -3459,6 +3381,9 @@ int lba_linearize(lba_problem* p, double* residuals, double* H_pp, double* b, do
             for (int i = 0; i < p->n_obs; ++i)
                 for (int d = 0; d < 3; ++d) residuals[3 * (size_t)i + d] = res[3 * (size_t)p->obs_dev[i] + d];
         return npx;
+    } catch (const ApiError& e) {
+        p->err = e.msg;
+        return e.code;
     } catch (const HipError& e) {
         return map_error(p, e);
     }
@@ -3489,6 +3414,9 @@ int lba_solve_step(lba_problem* p, double lambda, double* dx) {
             }
         }
         return LBA_OK;
+    } catch (const ApiError& e) {
+        p->err = e.msg;
+        return e.code;
     } catch (const HipError& e) {
         return map_error(p, e);
     }

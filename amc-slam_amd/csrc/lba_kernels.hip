@@ -739,8 +739,6 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
                 P.cf_head[1] = 0;
             }
         }
-        if (P.cf_fused)   // the fused flow's expansion / assembly counters
-            for (int z = blockIdx.x * LS_THREADS + tid; z < P.cf_ncnt; z += gridDim.x * LS_THREADS) P.cf_cnt[z] = 0;
         const size_t nz = (size_t)P.n_ztiles * CHOL_NB * CHOL_NB;   // (S: the tiles of L)
         for (size_t z = (size_t)blockIdx.x * LS_THREADS + tid; z < nz; z += (size_t)gridDim.x * LS_THREADS) P.S[z] = 0.0;
     }
@@ -1144,7 +1142,10 @@ __device__ __forceinline__ void exp_wait(const DevProblem& P, const int* prod_of
         unsigned spins = 0;
         while ((unsigned)__hip_atomic_load((gi32_t*)(P.exp_flag + (size_t)FLAG_STRIDE * q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
             __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 20)) break;   // (~0.5 s: never expected)
+            if (++spins > (1u << 20)) {   // (~0.5 s: never expected) the slots may be stale: the call fails
+                __hip_atomic_fetch_or((gi32_t*)P.fault, FAULT_EXP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
         }
     }
     __syncthreads();
@@ -1267,89 +1268,7 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_exp_asm(DevProblem P, int 
     assemble_item<true>(P, blockIdx.x - P.n_smp, damping(P, lambda_arg), ASM_SCHUR, shm, !off, epoch);
 }
 
-// The fused flow's assembly work items (k_chol_flow prefix tasks, 256 threads): k_assemble's sums with the
-// slabs read as 16-byte sc1 buffer loads (the expansion tasks published part of them in the same launch),
-// one 16-byte chunk of a slot per thread and the slots of a target split over phases of threads, every
-// thread's loads in flight together (a work item's latency is what the factor tasks wait for); S / bS are
-// stored write-through for the factor tasks.  The fixed phase order makes the sums deterministic.
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const double* p, long long n_doubles) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(8 * n_doubles), 0x00020000);
-}
-// sum over slots s0, s0 + G, ... < s1 of the 16-byte chunk c of W-double slots
-template <int G, int W>
-__device__ __forceinline__ void chunk_sum(__amdgpu_buffer_rsrc_t r, int s0, int s1, int c, double& x, double& y) {
-    double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0, c0 = 0.0, c1 = 0.0, d0 = 0.0, d1 = 0.0;
-    auto ld = [&](int s, double& u, double& v) {
-        const v4u q = __builtin_amdgcn_raw_buffer_load_b128(r, (s * W + 2 * c) * 8, 0, 16);
-        u += __longlong_as_double(((long long)q.y << 32) | q.x);
-        v += __longlong_as_double(((long long)q.w << 32) | q.z);
-    };
-    int s = s0;
-    for (; s + 3 * G < s1; s += 4 * G) {
-        ld(s, a0, a1);
-        ld(s + G, b0, b1);
-        ld(s + 2 * G, c0, c1);
-        ld(s + 3 * G, d0, d1);
-    }
-    for (; s < s1; s += G) ld(s, a0, a1);
-    x = (a0 + b0) + (c0 + d0);
-    y = (a1 + b1) + (c1 + d1);
-}
-__device__ void asm_block_item(const DevProblem& P, int ub, double lambda, double* red) {
-    constexpr int PH = 3;   // slot phases (3 x 72 chunk threads)
-    const int tid = threadIdx.x;
-    const int bi = P.ub_i[ub], bj = P.ub_j[ub];
-    const int c = tid % 72, q = tid / 72;
-    if (q < PH) {
-        double hx, hy, sx, sy;
-        chunk_sum<PH, 144>(slab_rsrc(P.hslab, (long long)P.n_hslots * 144), P.hs0[ub] + q, P.hs0[ub + 1], c, hx, hy);
-        chunk_sum<PH, 144>(slab_rsrc(P.sslab, (long long)P.n_sslots * 144), P.ss0[ub] + q, P.ss0[ub + 1], c, sx, sy);
-        red[q * 144 + 2 * c] = hx - sx;
-        red[q * 144 + 2 * c + 1] = hy - sy;
-    }
-    __syncthreads();
-    if (tid < 144) {
-        const int e = tid;
-        double t = red[e] + red[144 + e] + red[288 + e];
-        if (bi == bj && e % 13 == 0) t += lambda;
-        const int i = e / 12, j = e % 12;
-        const int r = 12 * bj + j, cc = 12 * bi + i;
-        if (bi != bj || j >= i) {
-            const int rh = P.rpos[r], ch = P.rpos[cc];
-            st_sc1(P.S + s_elem(P, max(rh, ch), min(rh, ch)), t);
-        }
-    }
-}
-__device__ void asm_rhs_item(const DevProblem& P, int k, double* red) {
-    constexpr int PH = 42;   // slot phases (42 x 6 chunk threads)
-    const int tid = threadIdx.x;
-    const int c = tid % 6, q = tid / 6;
-    if (q < PH) {
-        double gx, gy, px, py;
-        chunk_sum<PH, 12>(slab_rsrc(P.gslab, (long long)P.n_gslots * 12), P.gs0[k] + q, P.gs0[k + 1], c, gx, gy);
-        chunk_sum<PH, 12>(slab_rsrc(P.gpslab, (long long)P.n_gpslots * 12), P.gps0[k] + q, P.gps0[k + 1], c, px, py);
-        red[q * 12 + 2 * c] = gx;
-        red[q * 12 + 2 * c + 1] = gy;
-        red[PH * 12 + q * 12 + 2 * c] = px;
-        red[PH * 12 + q * 12 + 2 * c + 1] = py;
-    }
-    __syncthreads();
-    if (tid < 12) {
-        double bpv = 0.0, t = 0.0;
-        for (int w = 0; w < PH; ++w) bpv += red[w * 12 + tid];
-        for (int w = 0; w < PH; ++w) t += red[PH * 12 + w * 12 + tid];
-        P.bp[12 * k + tid] = bpv;
-        st_sc1(P.bS + P.rpos[12 * k + tid], bpv - t);   // bS = b_p - sum Hpl Dinv bl (factorisation order)
-    }
-}
-__device__ void asm_pad_item(const DevProblem& P) {   // padding rows: identity, zero rhs
-    for (int r = P.np + (int)threadIdx.x; r < P.npad; r += 256) {
-        const int rh = P.rpos[r];
-        st_sc1(P.S + s_elem(P, rh, rh), 1.0);
-        st_sc1(P.bS + rh, 0.0);
-    }
-}
 
 // ------------------------------------------------------------------------------------------------
 // Dense Cholesky S = L L^T of the reduced camera system in its factorisation order (panels permuted
@@ -1387,36 +1306,6 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
     return fma(r * e, fma(0.375, e, 0.5), r);
 }
 
-// Panel pivot sequence over columns [J, E), generated at compile time (pivot J, update step T,
-// chain op OP) so every row[] index is a constant.  Pivot J: l = row[J] r; column J by readlane;
-// then the rank-1 update row[k] -= l cb[k] (J < k < E), with the next pivot's chain spread through it
-// in source order (the pins keep that order): d = row[J+1] - l^2 on lane J+1, rsq, the cubic step of
-// rsqrt_nr, readlane of r from lane J+1 (op s after update step floor(s NF / 6)).
-// The panel is factored as two 16-column halves (piv_seq<0, 16>, cross_update, piv_seq<16, 32>), so
-// the pivots' readlane broadcasts cover 2 x 120 entries instead of 496; the 256 products between the
-// halves go through the matrix cores.
-struct Pivot {
-    double lij, d, c, t, e, m, rn;
-};
-
-template <int J, int E, int T, int OP>
-__device__ __forceinline__ void piv_chain(Pivot& x) {
-    constexpr int NF = E - 1 - J;
-    if constexpr (OP < 6) {
-        if constexpr ((OP * NF) / 6 == T) {
-            if constexpr (OP == 0) { x.t = x.d * x.c; pin(x.t); }
-            else if constexpr (OP == 1) { x.e = fma(-x.t, x.c, 1.0); pin(x.e); }
-            else if constexpr (OP == 2) { x.t = fma(0.375, x.e, 0.5); x.m = x.c * x.e; pin(x.t); pin(x.m); }
-            else if constexpr (OP == 3) { x.c = fma(x.m, x.t, x.c); pin(x.c); }
-            else if constexpr (OP == 4) { x.rn = readlane_d(x.c, J + 1); pin(x.rn); }
-        }
-        piv_chain<J, E, T, OP + 1>(x);
-    }
-}
-
-#ifndef LBA_CHOL_DPP
-#define LBA_CHOL_DPP 1
-#endif
 // lane x <- v of lane B + (x & 15): the pivot column of one 16-row half of the diagonal block copied
 // into every 16-lane row of the wave, so the rank-1 update can read entry k with the DPP64 row
 // broadcast (row_newbcast: each lane of a row takes lane k & 15 of that row)
@@ -1436,63 +1325,11 @@ __device__ __forceinline__ void fmac_bcast(double& acc, double rep, double l) {
                  : "+v"(acc) : "v"(rep), "v"(l), "i"(K & 15));
 }
 
-template <int J, int E, int... T>
-__device__ __forceinline__ void piv_update(double (&row)[CNB], const double (&cb)[CNB], double rep, Pivot& x,
-                                           std::integer_sequence<int, T...>) {
-    constexpr int NF = E - 1 - J;
-    auto step = [&](auto tc) {
-        constexpr int t = decltype(tc)::value;
-#ifdef LBA_EXP_NO_UPDATE   // (micro-benchmark experiments only: the chain alone)
-        if constexpr (false) {
-#else
-        if constexpr (t < NF) {
-#endif
-#if LBA_CHOL_DPP
-            (void)cb;
-            fmac_bcast<J + 1 + t>(row[J + 1 + t], rep, x.lij);
-#else
-            (void)rep;
-            row[J + 1 + t] -= x.lij * cb[J + 1 + t];
-            pin(row[J + 1 + t]);
-#endif
-        }
-        if constexpr (J + 1 < E) piv_chain<J, E, t, 0>(x);
-    };
-    (step(std::integral_constant<int, T>{}), ...);
-}
-
-template <int J, int E>
-__device__ __forceinline__ void piv_seq(double (&row)[CNB], double r, int lane, bool& bad) {
-    static_assert((E - 16 <= J && J < E && E % 16 == 0) || J >= E, "pivot halves are 16 columns");
-    if constexpr (J < E) {
-        Pivot x;
-        x.lij = row[J] * r;   // lane J: sqrt(d); lanes > J: L(l, J)
-        row[J] = x.lij;
-        x.d = 1.0; x.c = 1.0; x.t = 0.0; x.e = 0.0; x.m = 0.0; x.rn = 1.0;
-        if constexpr (J + 1 < E) {
-            const double own = row[J + 1] - x.lij * x.lij;
-            bad = bad || (lane == J + 1 && !(own > 0.0));
-            x.c = __builtin_amdgcn_rsq(own);
-            x.d = own;
-        }
-        double cb[CNB];
-        double rep = 0.0;
-#if LBA_CHOL_DPP
-        // column J of this half (rows E-16 .. E-1 of the diagonal block) into every 16-lane row
-        if constexpr (J + 1 < E) rep = rep16<E - 16>(x.lij, lane);
-#else
-        // column J of L_pp by readlane into SGPRs (an LDS broadcast costs (E - 1 - J) doubles per lane
-        // of every factoring wave on the CU's shared LDS return path: no faster, measured)
-#pragma unroll
-        for (int k = J + 1; k < E; ++k) cb[k] = readlane_d(x.lij, k);
-#endif
-        constexpr int NT = (E - 1 - J) > 0 ? (E - 1 - J) : 1;
-        piv_update<J, E>(row, cb, rep, x, std::make_integer_sequence<int, NT>{});
-        piv_seq<J + 1, E>(row, x.rn, lane, bad);
-    }
-}
-
-// The same pivot sequence software-pipelined across pivots (bitwise the same results as piv_seq): the chain of
+// Panel pivot sequence over the columns [J, E) of one 16-column half, generated at compile time so every row[]
+// index is a constant: pivot J: l = row[J] r (r = 1/sqrt of the pivot); column J by broadcast; the rank-1 update
+// row[k] -= l L(k, J) (J < k < E).  The panel is factored as two halves (piv_pipe<0, 16>, cross_update on the
+// matrix cores, piv_pipe<16, 32>), so the broadcasts cover 2 x 120 entries instead of 496.  The sequence is
+// software-pipelined across pivots (round 2's unpipelined reference form gave bitwise these results): the chain of
 // pivot J (the next pivot's diagonal, its reciprocal square root, the broadcast) is issued first, and the
 // rank-1 updates of pivot J - 1 on columns J + 1 .. E - 1 are interleaved into it, so the chain no longer waits
 // behind the DPP updates (which wait for their ds_bpermute broadcast, ~80 cycles) nor they behind the chain.
@@ -1525,7 +1362,7 @@ __device__ __forceinline__ void piv_pipe(double (&row)[CNB], double rn, double d
         const double lij = row[J] * rn;   // lane J: sqrt(d); lanes > J: L(l, J)
         row[J] = lij;
         if constexpr (J + 1 < E) {
-            const double own = dg - lij * lij;       // lane J + 1: the next pivot (as piv_seq computes it)
+            const double own = dg - lij * lij;       // lane J + 1: the next pivot
             const double dgn = fma(-lij, lij, dg);   // the lane's own diagonal entry after this pivot's update
             double rep = 0.0;
             if constexpr (J + 2 < E) rep = rep16<B>(lij, lane);
@@ -1549,7 +1386,7 @@ __device__ __forceinline__ void piv_pipe(double (&row)[CNB], double rn, double d
             c = fma(m, t, c);
             pin(c);
             pipe_defer<J, E, 4>(row, rp, lp);
-            row[J + 1] = fma(-lij, sL, row[J + 1]);   // = fmac(-L(J+1, J), lij): piv_seq's first update
+            row[J + 1] = fma(-lij, sL, row[J + 1]);   // = fmac(-L(J+1, J), lij): the first update of column J + 1
             const double rnn = readlane_d(c, J + 1);
             piv_pipe<J + 1, E>(row, rnn, dgn, lij, rep, lane);
         }
@@ -1589,8 +1426,7 @@ __device__ __forceinline__ void cross_update(double (&row)[CNB], double (*st)[CN
 }
 
 // The stacked panel in `st` (rows 0..31 the diagonal block) factored by ONE wave: piv_pipe over the two
-// halves with the matrix-core cross update between them; bitwise the results of piv_seq / cross_update /
-// piv_seq.  bad: a non-positive (or NaN) pivot, seen as a diagonal entry of L that is not > 0 (a pivot
+// halves with the matrix-core cross update between them.  bad: a non-positive (or NaN) pivot, seen as a diagonal entry of L that is not > 0 (a pivot
 // d <= 0 or NaN gives rsq(d) = NaN / inf, so L(J, J) = NaN; d > 0 gives L(J, J) = d rsq(d) > 0).
 __device__ __forceinline__ void factor_pipe(double (*st)[CNB + 1], int lane, bool& bad) {
     double row[CNB];
@@ -1605,119 +1441,6 @@ __device__ __forceinline__ void factor_pipe(double (*st)[CNB + 1], int lane, boo
     for (int c = 0; c < CNB; ++c) st[lane][c] = row[c];
     wave_sync();
     bad = lane < CNB && !(st[lane][lane & 31] > 0.0);
-}
-
-// The stacked panel factored by TWO waves (a pair of the workgroup: half = 0 / 1): wave 0 of the pair runs
-// piv_pipe over columns 0..15 and publishes every pivot column L(., J) to LDS (colbuf[J][lane], a flag
-// per PAIR_GROUP pivots); wave 1 holds columns 16..31 and applies each published column to them as it arrives
-// (one fma per entry and pivot, through the DPP row broadcast of colbuf[J][16 + (lane & 15)]; colbuf holds
-// columns 0..15, cflag 16 / PAIR_GROUP flags), in place of
-// the matrix-core cross update, then runs piv_pipe over columns 16..31.  The updates of the second half
-// thus run on the other SIMD while the first half's chain runs.  Rounding: every entry receives its rank-1
-// updates one fma at a time in pivot order (no matrix-core partial sums), so the factor differs from
-// factor_pipe's in the last bits of columns 16..31.  bad: as factor_pipe.  Both waves of the pair call it.
-constexpr int PAIR_GROUP = 4;   // pivot columns per flag
-template <int SLOT>
-__device__ __forceinline__ void pair_consume(double (&row)[CNB], double& dg, const double (*colbuf)[64], int g, int lane) {
-    double lij[PAIR_GROUP], rep[PAIR_GROUP];
-#pragma unroll
-    for (int u = 0; u < PAIR_GROUP; ++u) {
-        lij[u] = colbuf[g + u][lane];
-        rep[u] = colbuf[g + u][16 + (lane & 15)];
-    }
-#pragma unroll
-    for (int u = 0; u < PAIR_GROUP; ++u) {
-#pragma unroll
-        for (int c = 16; c < CNB; ++c) {
-            switch (c) {
-#define LBA_PC(K) case K: fmac_bcast<K>(row[K], rep[u], lij[u]); break;
-                LBA_PC(16) LBA_PC(17) LBA_PC(18) LBA_PC(19) LBA_PC(20) LBA_PC(21) LBA_PC(22) LBA_PC(23)
-                LBA_PC(24) LBA_PC(25) LBA_PC(26) LBA_PC(27) LBA_PC(28) LBA_PC(29) LBA_PC(30) LBA_PC(31)
-#undef LBA_PC
-                default: break;
-            }
-        }
-        dg = fma(-lij[u], lij[u], dg);
-    }
-    (void)SLOT;
-}
-template <int J>
-__device__ __forceinline__ void piv_pipe_pub(double (&row)[CNB], double rn, double dg, double lp, double rp, int lane,
-                                             double (*colbuf)[64], int* cflag, int tag);
-__device__ __forceinline__ void factor_pair(double (*st)[CNB + 1], double (*colbuf)[64], int* cflag, int tag, int half,
-                                            bool& bad) {
-    // (bad: the caller checks the diagonal of L once both waves have stored their columns, as factor_pipe)
-    bad = false;
-    const int lane = threadIdx.x & 63;
-    double row[CNB];
-    const double dg0 = st[lane][lane & 31];
-    if (half == 0) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) row[c] = st[lane][c];
-        piv_pipe_pub<0>(row, readlane_d(rsqrt_nr(row[0]), 0), dg0, 0.0, 0.0, lane, colbuf, cflag, tag);
-#pragma unroll
-        for (int c = 0; c < 16; ++c) st[lane][c] = row[c];
-    } else {
-#pragma unroll
-        for (int c = 16; c < CNB; ++c) row[c] = st[lane][c];
-        double dg = dg0;
-        for (int g = 0; g < 16; g += PAIR_GROUP) {
-            unsigned spins = 0;
-            while (__hip_atomic_load(cflag + g / PAIR_GROUP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != tag) {
-#ifdef LBA_PAIR_SLEEP
-                __builtin_amdgcn_s_sleep(LBA_PAIR_SLEEP);
-#endif
-                if (++spins > (1u << 24)) break;   // (bounded: never expected)
-            }
-            asm volatile("" ::: "memory");
-            pair_consume<0>(row, dg, colbuf, g, lane);
-        }
-        piv_pipe<16, CNB>(row, readlane_d(rsqrt_nr(row[16]), 16), dg, 0.0, 0.0, lane);
-#pragma unroll
-        for (int c = 16; c < CNB; ++c) st[lane][c] = row[c];
-    }
-}
-// piv_pipe<J, 16> that also publishes every pivot column for the pair's second wave (a flag per PAIR_GROUP)
-template <int J>
-__device__ __forceinline__ void piv_pipe_pub(double (&row)[CNB], double rn, double dg, double lp, double rp, int lane,
-                                             double (*colbuf)[64], int* cflag, int tag) {
-    constexpr int E = 16, B = 0;
-    if constexpr (J < E) {
-        const double lij = row[J] * rn;
-        row[J] = lij;
-        colbuf[J][lane] = lij;
-        if constexpr (J % PAIR_GROUP == PAIR_GROUP - 1) {
-            asm volatile("" ::: "memory");
-            __hip_atomic_store(cflag + J / PAIR_GROUP, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        if constexpr (J + 1 < E) {
-            const double own = dg - lij * lij;
-            const double dgn = fma(-lij, lij, dg);
-            double rep = 0.0;
-            if constexpr (J + 2 < E) rep = rep16<B>(lij, lane);
-            __builtin_amdgcn_sched_barrier(0);
-            const double sL = readlane_d(lij, J + 1);
-            double c = __builtin_amdgcn_rsq(own);
-            pin(c);
-            pipe_defer<J, E, 0>(row, rp, lp);
-            double t = own * c;
-            pin(t);
-            pipe_defer<J, E, 1>(row, rp, lp);
-            double e = fma(-t, c, 1.0);
-            pin(e);
-            pipe_defer<J, E, 2>(row, rp, lp);
-            t = fma(0.375, e, 0.5);
-            const double m = c * e;
-            pin(t);
-            pipe_defer<J, E, 3>(row, rp, lp);
-            c = fma(m, t, c);
-            pin(c);
-            pipe_defer<J, E, 4>(row, rp, lp);
-            row[J + 1] = fma(-lij, sL, row[J + 1]);
-            const double rnn = readlane_d(c, J + 1);
-            piv_pipe_pub<J + 1>(row, rnn, dgn, lij, rep, lane, colbuf, cflag, tag);
-        }
-    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1761,6 +1484,7 @@ struct CholFlow {
     double* zv;          // [NP][NP][CNB] z(i, k) = Linv(i, k) b_k, the shares of y_i
     unsigned long long* head;   // ticket counter (zeroed by k_schur ahead of every trial)
     int* abort_flag;
+    int* fault;                 // DevProblem::fault: a timed-out wait also fails the call (FAULT_FLOW)
     unsigned long long* tdbg;   // diagnostics: per panel, s_memrealtime stamps of its task
     unsigned long long* tdbg2;  // diagnostics: stamps of the L^-1 tasks of the last two panel rows
     unsigned long long* tdbg3;  // diagnostics: per factor task (ticket < 4096): stamps, i, j
@@ -1773,50 +1497,7 @@ struct CholFlow {
     // band mode (kinds 4, 5): forward / back substitution tasks instead of L^-1 tiles
     double* xpos;        // [npad] x in factorisation order, handed off between back tasks
     int* xready;         // per panel: epoch once x_j is published
-    // fused mode (unpartitioned problems): the task list starts with the pose-sample expansions (kind 8),
-    // the heavy landmarks (kind 9) and the assembly of S / bS (kind 10), so the first panels factor while
-    // later blocks are still being assembled; counters instead of epoch flags (k_lin_schur zeroes them)
-    int fused;
-    int* cnt;            // [0] expansion tasks done, [1 + tile_id] assembly items done per envelope tile,
-                         // [1 + ntile + p] per panel rhs
-    const int* need;     // expected counts, same layout
-    const int* asm_item; // per assembly item: id | type << 28 (0: padding rows, 1: rhs of pose block id, 2: block ub)
-    const int* asm_tgt;  // per assembly item: 4 counter indices (-1: none)
-    int ntile;
-    int sel;             // state buffer of the expansion (SEL_CUR in the queued loop)
-    double lambda;       // damping (LAMBDA_CTL: the controller's)
 };
-
-// lanes 0..5 of wave 0 poll up to six counters (index < 0: none) until they reach their expected counts
-// (relaxed sc1 loads; bounded like cf_wait); the workgroup learns the result
-__device__ __forceinline__ bool cf_wait_cnt(const CholFlow& a, int c0, int c1, int c2, int c3, int c4, int c5,
-                                            int* s_ok) {
-    if (threadIdx.x < 64) {
-        const int l = threadIdx.x;
-        const int c = l == 0 ? c0 : l == 1 ? c1 : l == 2 ? c2 : l == 3 ? c3 : l == 4 ? c4 : l == 5 ? c5 : -1;
-        const int want = c >= 0 ? a.need[c] : 0;
-        bool done = c < 0;
-        bool ok = true;
-        for (unsigned spins = 0;; ++spins) {
-            if (!done) done = __hip_atomic_load((gi32_t*)(a.cnt + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want;
-            if (__all(done)) break;
-            if (spins > CF_SPIN_LIMIT ||
-                ((spins & 255) == 255 &&
-                 (unsigned)__hip_atomic_load((gi32_t*)a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch)) {
-                if (l == 0) {
-                    __hip_atomic_store((gi32_t*)a.abort_flag, (int)a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    *a.info = CF_TIMEOUT;
-                }
-                ok = false;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        if (l == 0) *s_ok = ok ? 1 : 0;
-    }
-    __syncthreads();
-    return *s_ok != 0;
-}
 
 // lanes 0..2 of wave 0 poll up to three flags (null = none) for `epoch` side by side (relaxed, agent
 // scope: one round trip when they are already set, not one per flag); the workgroup learns the result
@@ -1836,6 +1517,7 @@ __device__ __forceinline__ bool cf_wait(const CholFlow& a, const int* f1, const 
                 if (l == 0) {
                     __hip_atomic_store((gi32_t*)a.abort_flag, (int)a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     *a.info = CF_TIMEOUT;
+                    __hip_atomic_fetch_or((gi32_t*)a.fault, FAULT_FLOW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 ok = false;
                 break;
@@ -1877,6 +1559,7 @@ __device__ __forceinline__ bool cf_wait_list(const CholFlow& a, int cnt, F flag,
                  (unsigned)__hip_atomic_load((gi32_t*)a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch)) {
                 __hip_atomic_store((gi32_t*)a.abort_flag, (int)a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 *a.info = CF_TIMEOUT;
+                __hip_atomic_fetch_or((gi32_t*)a.fault, FAULT_FLOW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 *s_ok = 0;
                 break;
             }
@@ -1964,35 +1647,21 @@ __device__ __forceinline__ d4 cf_mma_nn(const double (*X)[CNB + 1], const double
     return acc;
 }
 
-#ifndef LBA_CHOL_MODE
-// stacked panels: 1 one wave, factor_pipe (default; bitwise piv_seq's results); 0 one wave, piv_seq; 2 a pair of
-// waves, factor_pair (5.7k cycles against 7.0k alone on an idle CU, scripts/micro/piv_factor.hip, but no faster
-// inside k_chol_flow and different rounding: profiles/r4g_ab_factor_modes.txt, r4h_*)
-#define LBA_CHOL_MODE 1
-#endif
 __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
     __shared__ double Lt[3][CNB][CNB + 1];       // update operands L(j, p), L(i, p), L(k, p)
     __shared__ double stg[2][2 * CNB][CNB + 1];  // stacked panels of the factoring waves
     __shared__ long long s_ticket;
     __shared__ int s_ok;
-    __shared__ int cflag[2][16 / PAIR_GROUP];   // factor_pair's pivot-column flags, per pair of waves
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // factor_pair's pivot columns (16 x 64 per pair) share Lt's memory (no update operand is live while a
-    // panel is factored)
-    double (*colbuf0)[64] = reinterpret_cast<double (*)[64]>(&Lt[0][0][0]);
-    double (*colbuf1)[64] = colbuf0 + 16;
-    static_assert(sizeof(Lt) >= sizeof(double) * 2 * 16 * 64, "factor_pair column buffers");
-    int ftag = 0;   // factor rounds of this workgroup (the flags' tag)
-    if (tid < 2 * (16 / PAIR_GROUP)) cflag[tid / (16 / PAIR_GROUP)][tid % (16 / PAIR_GROUP)] = 0;
     const int rb = wave >> 1, cb = wave & 1, lr = lane & 15, kq = lane >> 4;
     const int n = a.n;
     // (the tile ids a task touches come precomputed with it, read into registers at the task's start or
     // with its list entry, so no address on the chain waits for a table search)
     auto tile_at = [&](auto* base, int tid_) { return base + ((size_t)tid_ << 10); };
     auto tri_id = [&](int i, int j) { return i * (i + 1) / 2 + j; };
-    auto load_quad = [&](int tl, double (&q)[4]) {   // tile tl of S; sc1 loads: the fused assembly writes S in this launch
+    auto load_quad = [&](int tl, double (&q)[4]) {   // tile tl of S (assembled by an earlier launch)
 #pragma unroll
-        for (int m = 0; m < 4; ++m) q[m] = ld_sc1(tile_at(a.S, tl) + (rb * 16 + kq + 4 * m) * CNB + cb * 16 + lr);
+        for (int m = 0; m < 4; ++m) q[m] = tile_at(a.S, tl)[(rb * 16 + kq + 4 * m) * CNB + cb * 16 + lr];
     };
     auto stage_quad = [&](double (*T)[CNB + 1], int r0, const double (&q)[4]) {
 #pragma unroll
@@ -2003,33 +1672,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
         for (int m = 0; m < 4; ++m) q[m] -= p[m];
     };
     // one wave: two-level pivot sequence of its stacked panel in `st` (row r of lane r)
-    auto factor = [&](double (*st)[CNB + 1], bool& bad) {
-#if LBA_CHOL_MODE == 1
-        factor_pipe(st, lane, bad);
-#else
-        double row[CNB];
-#pragma unroll
-        for (int c = 0; c < CNB; ++c) row[c] = st[lane][c];
-        bad = lane == 0 && !(row[0] > 0.0);
-        piv_seq<0, 16>(row, readlane_d(rsqrt_nr(row[0]), 0), lane, bad);
-        cross_update(row, st, lane);
-        bad = bad || (lane == 16 && !(row[16] > 0.0));
-        piv_seq<16, CNB>(row, readlane_d(rsqrt_nr(row[16]), 16), lane, bad);
-#pragma unroll
-        for (int c = 0; c < CNB; ++c) st[lane][c] = row[c];
-        wave_sync();
-#endif
-    };
-    (void)factor;
-    // waves 2 p, 2 p + 1 (p = pair): factor_pair of st; every thread calls it (one flag round per call)
-    auto factor_pairs = [&](double (*st0)[CNB + 1], double (*st1)[CNB + 1]) {
-        const int tg = ++ftag;
-        bool bad;
-        if (wave < 2) factor_pair(st0, colbuf0, cflag[0], tg, wave, bad);
-        else if (st1) factor_pair(st1, colbuf1, cflag[1], tg, wave - 2, bad);
-        __syncthreads();
-    };
-    (void)factor_pairs;
+    auto factor = [&](double (*st)[CNB + 1], bool& bad) { factor_pipe(st, lane, bad); };
     const d4 z4 = {0.0, 0.0, 0.0, 0.0};
     while (true) {
         if (tid == 0) s_ticket = (long long)atomicAdd(a.head, 1ull);
@@ -2040,38 +1683,6 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
         const int code = a.tasks[t];
         const int j = code & 0xffffff, i = a.task_i[t];
         const int kind = (code >> 24) & 15;
-        if (kind >= 8) {
-            // ---------------------------------------------------- fused prefix: expansion / assembly
-            const int pl = code & 0xffffff;
-            double* shm = &stg[0][0][0];
-            if (kind == 8 || kind == 9) {   // pose sample pl (N^T M N) / heavy landmark pl, published
-                const int si = state_idx(P, a.sel);
-                if (kind == 8) {
-                    double *Msh = shm, *Nsh = Msh + 144, *MN = Nsh + 216, *part = MN + 216;
-                    sample_expand<true>(P, P.gpsb[si], P.camdb[si], pl, Msh, Nsh, MN, part, tid);
-                } else {
-                    heavy_item<true>(P, pl, damping(P, a.lambda), 1, shm);
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (tid == 0) __hip_atomic_fetch_add((gi32_t*)a.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                continue;
-            }
-            // assembly item pl, once every expansion is in; then one add per counter it feeds
-            if (!cf_wait_cnt(a, 0, -1, -1, -1, -1, -1, &s_ok)) return;
-            const int it = a.asm_item[pl], id = it & 0x0fffffff, ty = it >> 28;
-            if (ty == 0) asm_pad_item(P);
-            else if (ty == 1) asm_rhs_item(P, id, shm);
-            else asm_block_item(P, id, damping(P, a.lambda), shm);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid < 4) {
-                const int c = a.asm_tgt[4 * pl + tid];
-                if (c >= 0) __hip_atomic_fetch_add((gi32_t*)(a.cnt + c), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __syncthreads();   // (stg is the next task's LDS)
-            continue;
-        }
         const bool la = (code >> 28) & 1;   // factor task with lookahead over column k = j - 1
         if (kind == 1) {
             // ---------------------------------------------------- L^-1 tile (i, j), i > j:
@@ -2082,7 +1693,6 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             unsigned long long* tv = (a.tdbg2 && tid == 0 && i >= a.NP - 2) ? a.tdbg2 + 16 * j + 4 * (i - (a.NP - 2)) : nullptr;
             if (tv) tv[0] = __builtin_amdgcn_s_memrealtime();
             const int zr = tid >> 3, zc = (tid & 7) * 4;   // z(i, j): row zr, columns zc .. zc + 3
-            if (a.fused && !cf_wait_cnt(a, 1 + a.ntile + j, -1, -1, -1, -1, -1, &s_ok)) return;
             double bj[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) bj[u] = ld_sc1(a.b + j * CNB + zc + u);
@@ -2240,7 +1850,6 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
                 for (int u = 0; u < 4; ++u) acc += lv[u] * yk[u];
             }
             if (!cf_wait(a, a.fready + i, nullptr, &s_ok)) return;
-            if (a.fused && !cf_wait_cnt(a, 1 + a.ntile + i, -1, -1, -1, -1, -1, &s_ok)) return;
 #pragma unroll
             for (int m = 0; m < 4; ++m) {   // L_ii^-T -> Lt[2] in one round of loads
                 const int e = tid + 256 * m;
@@ -2377,11 +1986,6 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
         const int t_jj = a.task_t[5 * t], t_ij = a.task_t[5 * t + 1], t_kk = a.task_t[5 * t + 2],
                   t_jk = a.task_t[5 * t + 3], t_ik = a.task_t[5 * t + 4];
         const bool ik_env = la && !diag && t_ik >= 0;   // tile (i, j - 1) structurally non-zero
-        if (a.fused) {   // the tiles this task loads (and panel j's rhs) are assembled
-            if (!cf_wait_cnt(a, 1 + t_jj, diag ? -1 : 1 + t_ij, la ? 1 + t_kk : -1, la ? 1 + t_jk : -1,
-                             ik_env ? 1 + t_ik : -1, (diag && a.zv) ? 1 + a.ntile + j : -1, &s_ok))
-                return;
-        }
         double qd[4], qa[4];
         load_quad(t_jj, qd);
         if (!diag) load_quad(t_ij, qa);
@@ -2436,16 +2040,12 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
                 stage_quad(stg[1], CNB, qik);
             }
             __syncthreads();
-#if LBA_CHOL_MODE == 2
-            factor_pairs(stg[0], ik ? stg[1] : nullptr);   // (a bad pivot is reported by panel k's own task)
-#else
             if (wave == 0 || (wave == 1 && ik)) {
                 bool bad;
                 factor(stg[wave], bad);
                 (void)bad;   // (reported by panel k's own task)
             }
             __syncthreads();
-#endif
             if (tf) tf[6] = __builtin_amdgcn_s_memrealtime();
         };
         if (la && ((code >> 29) & 1)) factor_k();
@@ -2499,14 +2099,6 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             stage_quad(stg[0], CNB, qa);
             __syncthreads();
             if (tm) tm[4] = __builtin_amdgcn_s_memrealtime();
-#if LBA_CHOL_MODE == 2
-            {   // (a non-positive pivot of A(j,j) is reported by panel j's own task)
-                const unsigned long long c0 = tf ? clock64() : 0;
-                factor_pairs(stg[0], nullptr);
-                if (tf) tf[7] = clock64() - c0;
-                if (tm) tm[5] = __builtin_amdgcn_s_memrealtime();
-            }
-#else
             if (wave == 0) {
                 bool bad;
                 const unsigned long long c0 = tf ? clock64() : 0;
@@ -2516,7 +2108,6 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
                 (void)bad;   // (a non-positive pivot of A(j,j) is reported by panel j's own task)
             }
             __syncthreads();
-#endif
             // L(i, j) from the staged panel by all four waves (a quarter of the write-through bytes per
             // wave: the drain before the flag is a quarter as long as one wave storing the tile)
             cf_store_tile(tile_at(a.Lm, t_ij), CNB, stg[0] + CNB);
@@ -2534,19 +2125,6 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
         }
         __syncthreads();
         if (tm) tm[4] = __builtin_amdgcn_s_memrealtime();
-#if LBA_CHOL_MODE == 2
-        {
-            const unsigned long long c0 = tf ? clock64() : 0;
-            factor_pairs(stg[0], nullptr);
-            if (tf) tf[7] = clock64() - c0;
-            // a non-positive (or NaN) pivot shows as a diagonal entry of L that is not > 0 (factor_pipe)
-            if (wave == 0) {
-                const bool bad = lane < CNB && !(stg[0][lane][lane & 31] > 0.0);
-                if (__ballot(bad) != 0 && lane == 0) *a.info = 1 + (int)p0;
-            }
-            if (tm) tm[5] = __builtin_amdgcn_s_memrealtime();
-        }
-#else
         if (wave == 0) {
             bool bad;
             const unsigned long long c0 = tf ? clock64() : 0;
@@ -2556,7 +2134,6 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             if (tm) tm[5] = __builtin_amdgcn_s_memrealtime();
         }
         __syncthreads();
-#endif
 #pragma unroll
         for (int m = 0; m < 4; ++m) {   // L_jj (plain: no reader in this launch), L_jj^-T, by all waves
             const int e = tid + 256 * m, r = e >> 5, c = e & 31;
@@ -2818,7 +2395,10 @@ __device__ __forceinline__ void upd_wait(const DevProblem& P, int prod, unsigned
         }
         if (__all(done)) break;
         __builtin_amdgcn_s_sleep(LBA_UPD_POLL_SLEEP);
-        if (++spins > (1u << 20)) break;   // (~0.5 s: never expected)
+        if (++spins > (1u << 20)) {   // (~0.5 s: never expected) the samples may be stale: the call fails
+            if (!done) __hip_atomic_fetch_or((gi32_t*)P.fault, FAULT_UPD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
     }
     __syncthreads();
 }
@@ -2950,7 +2530,9 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
     const int nkb = (P.n_kf + UPD_THREADS - 1) / UPD_THREADS;
     if (role >= P.n_upd_blocks) {   // (fused) motion-prior / velocity edges of the trial state: the KF blocks
         const int nkb_ = (P.n_kf + UPD_THREADS - 1) / UPD_THREADS;
-        upd_wait(P, (int)threadIdx.x < nkb_ ? P.n_gp + (int)threadIdx.x : -1, epoch);
+        // (every KF block, UPD_THREADS of them per round: a prior may touch any keyframe)
+        for (int b0 = 0; b0 < nkb_; b0 += UPD_THREADS)
+            upd_wait(P, b0 + (int)threadIdx.x < nkb_ ? P.n_gp + b0 + (int)threadIdx.x : -1, epoch);
         prior_eval_t<false>(P, ko, (role - P.n_upd_blocks) * UPD_THREADS + threadIdx.x);   // (plain loads: see eval_tile_trial)
         return;
     }
@@ -3304,6 +2886,7 @@ __device__ void finalize_body(const DevProblem& P, unsigned long long seq, int m
     LMCtl ctl;
     if (tid == 0 && mode != FIN_INITIAL && mode != FIN_HOST) ctl = *P.ctl;
     const int info = P.part_n > 0 ? 0 : *P.info;
+    const int fault = *P.fault;
     if (P.part_n > 0) {   // partitioned: the all-reduced sums of every rank's k_partials
         sa = P.red4[0]; sb = P.red4[1]; sc = P.red4[2]; sinfo = P.red4[3];
     } else {
@@ -3331,6 +2914,7 @@ __device__ void finalize_body(const DevProblem& P, unsigned long long seq, int m
     if (P.hfin) {
         volatile double* h = P.hfin;
         for (int i = 0; i < 4; ++i) h[i] = v[i];
+        h[5] = (double)fault;
         __threadfence_system();
         __hip_atomic_store(reinterpret_cast<unsigned long long*>(P.hfin + 4), seq, __ATOMIC_RELEASE,
                            __HIP_MEMORY_SCOPE_SYSTEM);
@@ -3420,18 +3004,15 @@ void launch_assemble(const DevProblem& P, double lambda, int flags, int gate, hi
     const int n = P.n_asm + P.n_pb;
     if (n) hipLaunchKernelGGL(k_assemble, dim3(n), dim3(144 * RED_GROUPS), 0, s, P, lambda, flags, gate);
 }
-static CholFlow make_flow(const DevProblem& P, unsigned epoch, int sel, double lambda) {
+static CholFlow make_flow(const DevProblem& P, unsigned epoch) {
     CholFlow a;
     const int n = P.npad;   // multiple of CHOL_NB (identity tail)
-    a.fused = P.cf_fused;
-    a.cnt = P.cf_cnt; a.need = P.cf_need; a.asm_item = P.cf_asm_item; a.asm_tgt = P.cf_asm_tgt;
-    a.ntile = P.cf_ntile; a.sel = sel; a.lambda = lambda;
     a.n = n; a.NP = n / CHOL_NB; a.ntasks = P.cf_ntasks; a.epoch = epoch;
     a.tasks = P.cf_tasks; a.task_i = P.cf_task_i; a.task_t = P.cf_task_t; a.pl0 = P.cf_pl0;
     a.plist_t = P.cf_plist_t;
     a.plist = P.cf_plist;
     a.S = P.S; a.Lm = P.Lm; a.LinvT = P.LinvT; a.b = P.bS; a.yv = P.yv; a.info = P.info;
-    a.lready = P.cf_lready; a.dready = P.cf_dready; a.head = P.cf_head; a.abort_flag = P.cf_abort;
+    a.lready = P.cf_lready; a.dready = P.cf_dready; a.head = P.cf_head; a.abort_flag = P.cf_abort; a.fault = P.fault;
     a.tdbg = P.tdbg_chol;
     a.tdbg2 = P.tdbg_bs;
     a.tdbg3 = P.tdbg_cf;
@@ -3448,15 +3029,14 @@ static void launch_flow(const CholFlow& a, const DevProblem& P, hipStream_t s, h
     else
         hipLaunchKernelGGL(k_chol_flow, g, dim3(256), 0, s, a, P);
 }
-void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
-                           int sel, double lambda) {
+void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     (void)gate;
     if (P.npad == 0) return;
-    launch_flow(make_flow(P, epoch, sel, lambda), P, s, e0, e1);
+    launch_flow(make_flow(P, epoch), P, s, e0, e1);
 }
 void launch_cholesky_part(const DevProblem& P, int part, unsigned epoch, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     if (P.npad == 0) return;
-    CholFlow a = make_flow(P, epoch, SEL_CUR, LAMBDA_CTL);
+    CholFlow a = make_flow(P, epoch);
     if (part == 1) {
         a.tasks = P.cf_tasks2; a.task_i = P.cf_task_i2; a.task_t = P.cf_task_t2; a.pl0 = P.cf_pl02;
         a.plist = P.cf_plist2; a.plist_t = P.cf_plist_t2; a.ntasks = P.cf_ntasks2;

@@ -38,6 +38,9 @@ extern "C" {
 #define LBA_E_ARG          -4   /* invalid argument / malformed problem */
 #define LBA_E_HIP          -5   /* HIP runtime error */
 #define LBA_E_LIMIT        -6   /* problem exceeds a compiled limit (see lba_last_error) */
+#define LBA_E_TIMEOUT      -7   /* a bounded device hand-off wait gave up (never expected: e.g. a GPU shared with
+                                   another launch that keeps workgroups from being scheduled); the results are not
+                                   used and the problem's state is undefined until the next lba_set_problem */
 
 /* observation kinds (the reprojection edges of include/G2oTypes.h) */
 #define LBA_MONO_GP    0   /* EdgeMonoGPExtrinsic / EdgeMonoGP: 2-d, vertices (kf_a=prev KF, kf_b=KF, lm, the camera extrinsic: optimised when lba_cam.ext_free)
@@ -314,6 +317,10 @@ int lba_debug_lie(int32_t device, int32_t n, const double* in, double* out);
  * dependent chain (the depth of the elimination tree), out[5] levels of the nested dissection, out[6]
  * tiles of the lower triangle of S (the pattern before fill-in), out[7] fill-in tiles (out[2] - out[6]). */
 int lba_solver_info(const lba_problem* p, int32_t out[8]);
+/* The launch fusions the set-up chose (diagnostics and tests): out[0] 1 when the trial evaluation runs inside
+ * k_update (the whole grid resident at once), out[1] 1 when the pose samples' expansion and the assembly of S
+ * run as one launch (k_exp_asm), out[2] 1 for the fp32-residual kernels, out[3] the k_update grid. */
+int lba_kernel_modes(const lba_problem* p, int32_t out[4]);
 /* Algorithmic FLOPs of one solve of the reduced camera system, from the symbolic structure of L:
  * out[0] the tile factorisation (per column with m tiles below the diagonal: potrf + m trsm + m(m+1)/2
  * trailing tile updates), out[1] the forward and back substitutions. */

@@ -13,7 +13,7 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 run_pass() {   # name, counters...
   local name=$1; shift
-  timeout -s KILL 300 rocprofv3 --pmc "$@" --kernel-include-regex "$KERNEL" --output-format csv -d "$OUT/$name" -o pmc \
+  timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "$KERNEL" --output-format csv -d "$OUT/$name" -o pmc \
       -- python3 "$ROOT/bench.py" --config "${PMC_CONFIG:-cfg1_local_50kf}" --steps 10 --warmup 2 --no-cpu > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "pmc $name rc=$rc"
@@ -21,5 +21,5 @@ run_pass() {   # name, counters...
 }
 run_pass FETCH_SIZE FETCH_SIZE || exit 1
 run_pass WRITE_SIZE WRITE_SIZE || exit 1
-run_pass SQ SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT || exit 1
+run_pass SQ ${SQ_COUNTERS:-SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT} || exit 1
 python3 "$ROOT/scripts/pmc_summary.py" "$OUT" "$ROOT/gpurun_out/pmc_${KERNEL}_$TAG.json" "$KERNEL"

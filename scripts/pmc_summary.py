@@ -47,11 +47,20 @@ def main():
     sq_dir = os.path.join(src, "SQ")
     if os.path.isdir(sq_dir):
         sq = {}
-        for c in ("SQ_WAVES", "SQ_BUSY_CYCLES", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT"):
-            v = per_dispatch(sq_dir, c, kernel)
-            sq[c] = median(v)
+        names = set()
+        for f in glob.glob(os.path.join(sq_dir, "**", "*counter_collection.csv"), recursive=True):
+            names.update(r.get("Counter_Name") for r in csv.DictReader(open(f)))
+        for c in sorted(n for n in names if n):
+            sq[c] = median(per_dispatch(sq_dir, c, kernel))
         if sq.get("SQ_INSTS_LDS") and sq.get("SQ_LDS_BANK_CONFLICT") is not None:
             sq["lds_bank_conflict_per_lds_inst"] = sq["SQ_LDS_BANK_CONFLICT"] / sq["SQ_INSTS_LDS"]
+        if sq.get("SQ_INSTS_VALU_MFMA_MOPS_F64") is not None:
+            # MOPS are counted in units of 512 FLOPs (rocprofv3 -L); fp64 dense MFMA peak 78.6 TF/s
+            sq["mfma_f64_flops"] = 512.0 * sq["SQ_INSTS_VALU_MFMA_MOPS_F64"]
+        if sq.get("SQ_VALU_MFMA_BUSY_CYCLES") is not None and sq.get("GRBM_GUI_ACTIVE"):
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs: kernel cycles = /8; 1024 SIMDs
+            cyc = sq["GRBM_GUI_ACTIVE"] / 8.0
+            sq["mfma_busy_frac_of_all_simds"] = sq["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * 1024.0)
         out["sq_per_launch_median"] = sq
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out))

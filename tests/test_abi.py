@@ -140,7 +140,7 @@ def test_header_constants_match_the_python_mirror():
     for m, v in flags.items():
         assert getattr(abi, m[len("LBA_"):]) == v, m
     assert len(set(flags.values())) == len(flags) and all(v & (v - 1) == 0 for v in flags.values())   # one bit each
-    for m in ("LBA_OK", "LBA_E_EMPTY", "LBA_E_SOLVE", "LBA_E_DIVERGED", "LBA_E_ARG", "LBA_E_HIP", "LBA_E_LIMIT"):
+    for m in ("LBA_OK", "LBA_E_EMPTY", "LBA_E_SOLVE", "LBA_E_DIVERGED", "LBA_E_ARG", "LBA_E_HIP", "LBA_E_LIMIT", "LBA_E_TIMEOUT"):
         assert getattr(abi, m) == macros[m], m
     for m in ("LBA_MONO_GP", "LBA_STEREO_GP", "LBA_MONO", "LBA_STEREO"):
         assert getattr(abi, m[len("LBA_"):]) == macros[m], m

@@ -147,3 +147,24 @@ def test_subtree_split_layout_world2():
     summed = res[0][2]
     assert summed[1] == len(win.obs) and summed[2] == len(win.priors)
     assert abs(summed[0] - chi) <= 1e-12 * chi
+
+
+def test_partition_rejects_free_extrinsics():
+    """A partitioned problem takes no free extrinsic (a partitioned lba_set_problem returns LBA_E_LIMIT before it plans,
+    and lba_partition_assign plans the keyframe-only pattern): both Python entry points of the split refuse such a
+    window up front, with the reason, instead of a rank failing later with a stray-landmark error."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "amc-slam_amd")]
+    import amc_lba
+    from amc_lba.abi import LBA_E_LIMIT
+    from amc_lba.gba import partition_window
+    from amc_lba.synth import make_window, with_free_extrinsics
+    win = with_free_extrinsics(make_window(n_opt_kf=8, n_lm=400, obs_per_lm=6, n_cam=4, gp=True, stereo_frac=0.0,
+                                           seed=3))
+    with pytest.raises(amc_lba.LbaError) as ei:
+        amc_lba.partition_assign(win, 2)
+    assert ei.value.code == LBA_E_LIMIT and "extrinsic" in str(ei.value)
+    with pytest.raises(ValueError, match="extrinsic"):
+        partition_window(win, 0, 2)
+    assert partition_window(win, 0, 1)[0] is win   # (one rank: not partitioned)

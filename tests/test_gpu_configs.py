@@ -135,3 +135,62 @@ def test_cfg4_full_size_subtree_split(cfg4):
         assert abs(st_r.chi2_final - st.chi2_final) <= 1e-7 * st.chi2_final
     assert _rel(kf_s["t"], kf["t"]) <= 1e-9
     assert _rel(lm_s, lm) <= 1e-9
+
+
+def test_cfg4_f32_residual_single_gpu(cfg4):
+    """BASELINE config 4 as stated: "fp32 residuals + fp64 accumulate" (LBA_FLAG_F32_RESIDUAL) at full size on one GPU:
+    residuals and the gradient against the fp64 oracle, the damped step through the normal-equation residual of the
+    oracle's fp64 block-sparse system (<= 1e-4 of max |b|, as config 2), LM descent and determinism.  The edge is
+    EdgeMonoGP's (src/G2oTypes.cc:316-367) with the projection, residual and Jacobian rows in fp32."""
+    from amc_lba.abi import FLAG_F32_RESIDUAL
+    win = cfg4
+    o = orc.Oracle(win, omp=True)
+    chi_o, res_o, _ = o.errors()
+    _, b_o, _ = o.build_system(dense=False)
+    p = Problem(win, early_stop=0, flags=FLAG_F32_RESIDUAL)
+    assert p.kernel_modes()["f32res"] == 1
+    res, _, b, _ = p.linearize(dense=False)
+    dres = np.linalg.norm(res - res_o) / np.linalg.norm(res_o)
+    db = _rel(b, b_o)
+    lam = win.cfg["lambda_init"]
+    ok, dx = p.solve_step(lam)
+    r = o.normal_residual(lam, dx)
+    dr = np.abs(r).max() / np.abs(b_o).max()
+    del o, r, res, res_o
+    n, st = p.optimize(2)
+    kf, lm = p.state()
+    p.close()
+    print(f"cfg4 f32 residuals: residual {dres:.2e}  b {db:.2e}  normal residual {dr:.2e}  "
+          f"chi2 {st.chi2_initial:.6e} -> {st.chi2_final:.6e} (oracle chi2_0 {chi_o:.6e})")
+    assert 1e-9 < dres <= 1e-3, dres   # (fp32 arithmetic shows: not the fp64 path by accident)
+    assert db <= 1e-4, db
+    assert ok and dr <= 1e-4, dr
+    assert n == 2 and st.chi2_final < st.chi2_initial
+    assert abs(st.chi2_initial - chi_o) <= 1e-4 * chi_o
+    p2 = Problem(win, early_stop=0, flags=FLAG_F32_RESIDUAL)
+    n2, st2 = p2.optimize(2)
+    kf2, lm2 = p2.state()
+    p2.close()
+    assert st2.chi2_final == st.chi2_final and st2.trials == st.trials
+    np.testing.assert_array_equal(kf2["t"], kf["t"])
+    np.testing.assert_array_equal(lm2, lm)
+
+
+def test_cfg4_f32_residual_subtree_split(cfg4):
+    """Config 4's fp32-residual option under the two-rank distributed factorisation bench.py runs over N GPUs: one LM
+    iteration equals the single problem's (with the same option) to 1e-9."""
+    from amc_lba.abi import FLAG_F32_RESIDUAL
+    from test_gpu_partition import run_split
+    win = cfg4
+    p = Problem(win, early_stop=0, flags=FLAG_F32_RESIDUAL)
+    n, st = p.optimize(1)
+    kf, lm = p.state()
+    p.close()
+    res, kf_s, lm_s, own, infos = run_split(win, 2, 1, flags=FLAG_F32_RESIDUAL)
+    assert (own >= 0).sum() > 0 and len(set(own[own >= 0])) == 2
+    for n_r, st_r in res:
+        assert n_r == n and st_r.trials == st.trials
+        assert abs(st_r.chi2_initial - st.chi2_initial) <= 1e-11 * st.chi2_initial
+        assert abs(st_r.chi2_final - st.chi2_final) <= 1e-7 * st.chi2_final
+    assert _rel(kf_s["t"], kf["t"]) <= 1e-9
+    assert _rel(lm_s, lm) <= 1e-9
