@@ -21,6 +21,7 @@ exits with its status; rank 0's line is the job's line.  Under a launcher, WORLD
 --gpus.  --dry-launch prints the launch (command and rank environment) and exits.
 """
 import argparse
+import ctypes
 import glob
 import json
 import os
@@ -143,6 +144,27 @@ def schur_terms(win):
                 pairs.add((int(kk[a]), int(kk[b])))
     n_kf = int((~fixed).sum())
     return 72 * len(lm_ids) + 1152 * len(pairs) + 96 * n_kf, flops
+
+
+def pmc_summary(workload, kernel):
+    """The committed rocprofv3 PMC summary (scripts/pmc_linearize.sh + pmc_summary.py) of `kernel` for THIS library
+    build (its lib_sha256 must match the loaded library's digest): (dict, file name) or (None, why)."""
+    import amc_lba
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc_{kernel}_*.json")))
+    digest = amc_lba.lib_digest()
+    stale = []
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") != workload:
+            continue
+        if d.get("lib_sha256") != digest:
+            stale.append(os.path.basename(f))
+            continue
+        return d, os.path.basename(f)
+    return None, (f"no PMC summary of this library build ({digest}); stale: {stale}" if stale else "no PMC summary")
 
 
 def pmc_traffic(workload, kernel="k_lin_schur"):
@@ -356,6 +378,24 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
+    # per-kernel launch durations for the rooflines: the timed run carries events on one trial in ten only (they idle
+    # the device ~5 us each); a further, untimed optimize with events on every trial's k_lin_schur and k_chol_flow
+    # dispatches averages >= 20 launches of each (the same problem, continuing from the timed run's state)
+    meas_iters = max(20, args.window_iters)
+    cfg_m = amc_lba.abi.LbaConfig.from_buffer_copy(prob.cfg)
+    cfg_m.flags = (cfg_m.flags | amc_lba.abi.FLAG_TIME_SWEEP) & ~amc_lba.abi.FLAG_TIME_SAMPLED
+    prob._check(amc_lba.lib().lba_set_config(prob.h, ctypes.byref(cfg_m)))
+    mk_ms, mk_n, ms_ms, ms_n = 0.0, 0, 0.0, 0
+    while mk_n < meas_iters:
+        _, st_m = prob.optimize(args.window_iters)
+        mk_ms += st_m.ms_k_linearize
+        mk_n += st_m.n_k_linearize
+        ms_ms += st_m.ms_k_solve
+        ms_n += st_m.n_k_solve
+        if st_m.n_k_linearize == 0:
+            break
+    prob._check(amc_lba.lib().lba_set_config(prob.h, ctypes.byref(prob.cfg)))
+
     # the data-path collectives, measured after the timed region (untimed): the farm's window-boundary
     # exchange (pack, in-place ncclAllGather, unpack on the window's stream) and, for the distributed global-BA
     # factorisation, an RCCL all-reduce of the per-trial size over the same ranks
@@ -437,6 +477,12 @@ def main():
         total_iters = done if gba else done * world
         W = full if gba else win
         value = total_iters / dt
+        # launch averages from the dedicated run (the timed run's sampled events are reported beside them)
+        live_k_ms, live_s_ms = ms_k / max(n_k, 1), ms_s / max(n_s, 1)
+        if mk_n:
+            ms_k, n_k = mk_ms, mk_n
+        if ms_n:
+            ms_s, n_s = ms_ms, ms_n
         k_ms = ms_k / max(n_k, 1)
         B_schur, F_schur = schur_terms(win)
         B = sweep_bytes(win) + B_schur
@@ -452,6 +498,9 @@ def main():
                       "tiles below the diagonal 32^3/3 + 2 m 32^3 + m (m - 1) 32^3, plus two substitutions "
                       "(lba_solver_flops, exact for the symbolic structure); the dependent panel chain, not the "
                       "FLOPs, sets its time")
+        # SURVEY.md 8(d)'s algorithmic FLOPs of the dense solve: n^3 / 3 + 2 n^2, n = 12 n_kf_opt
+        F_s8d = npose ** 3 / 3.0 + 2.0 * npose ** 2
+        chol_pmc, chol_pmc_src = pmc_summary(args.config, "k_chol_flow")
         achieved = B / (k_ms * 1e-3) / 1e9 if n_k else None
         achieved_f = F / (k_ms * 1e-3) / 1e12 if n_k else None
         workload = f"{args.config}: {win.name or args.config} synthetic window"
@@ -495,15 +544,36 @@ def main():
             "roofline_hbm": {"kernel": "k_lin_schur", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                              "bytes_per_launch": B, "traffic": traffic, "traffic_source": traffic_src},
-            "roofline_solve": {"kernel": "k_chol_flow", "bound": "mfma", "flops_per_launch": F_solve,
-                               "achieved": F_solve / (s_ms * 1e-3) / 1e12 if n_s else None,
+            "roofline_solve": {"kernel": "k_chol_flow", "bound": "mfma", "flops_per_launch": F_s8d,
+                               "achieved": F_s8d / (s_ms * 1e-3) / 1e12 if n_s else None,
                                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                               "frac": (F_solve / (s_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS) if n_s else None,
-                               "avg_launch_ms": s_ms, "timed_launches": n_s, "note": solve_note,
+                               "frac": (F_s8d / (s_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS) if n_s else None,
+                               "traffic": (chol_pmc or {}).get("hbm_bytes_per_launch"), "traffic_source": chol_pmc_src,
+                               "avg_launch_ms": s_ms, "timed_launches": n_s,
+                               "flops_note": "SURVEY.md 8(d): n^3/3 + 2 n^2, n = 12 n_kf_opt (the dense LDLT's count)",
+                               "flops_structural": F_solve,
+                               "frac_structural": (F_solve / (s_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS) if n_s else None,
+                               "note": solve_note,
                                "solver": sinfo, "flops_factor": F_fac, "flops_substitution": F_sub},
+            "live_sampled_ms": {"k_lin_schur": live_k_ms, "k_chol_flow": live_s_ms,
+                                "note": "the timed run's own sampled dispatch events (one trial in ten)"},
             "trials_per_step": trials / max(done, 1),
             "phases_ms_per_step": phase,
         }
+        # the contract's `roofline` is the DOMINANT kernel's (the longer average launch); the sweep's stays beside it
+        line["roofline_sweep"] = line["roofline"]
+        if chol_pmc is not None:
+            sq = chol_pmc.get("sq_per_launch_median", {})
+            line["roofline_solve"]["mfma_pmc"] = {
+                "mfma_f64_flops_per_launch": sq.get("mfma_f64_flops"),
+                "mfma_busy_frac_of_all_simds": sq.get("mfma_busy_frac_of_all_simds"),
+                "SQ_INSTS_VALU_MFMA_F64": sq.get("SQ_INSTS_VALU_MFMA_F64"),
+                "SQ_INSTS_VALU_FMA_F64": sq.get("SQ_INSTS_VALU_FMA_F64"),
+                "source": chol_pmc_src}
+        if n_s and s_ms > k_ms:
+            line["roofline"] = dict(line["roofline_solve"], dominant=True)
+        else:
+            line["roofline"] = dict(line["roofline_sweep"], dominant=True)
         if comm is not None:
             line["collective"] = comm
         if world == 1 and not gba:   # LocalGPBA-equivalent calls (optimize(window_iters))

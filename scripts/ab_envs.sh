@@ -16,7 +16,7 @@ import json, sys
 for l in open(sys.argv[1]):
     if l.startswith('{'):
         d = json.loads(l)
-        print(f"{sys.argv[2]:34s} value {d['value']:9.2f}  ms/step {d['ms_per_step']:.4f}  sweep us {d['roofline']['avg_launch_ms'] * 1e3:8.2f}  "
+        print(f"{sys.argv[2]:34s} value {d['value']:9.2f}  ms/step {d['ms_per_step']:.4f}  sweep us {d.get('roofline_sweep', d['roofline'])['avg_launch_ms'] * 1e3:8.2f}  "
               f"solve us {d['roofline_solve']['avg_launch_ms'] * 1e3:8.2f}  trials/step {d['trials_per_step']:.2f}", flush=True)
 PY
   done

@@ -17,7 +17,7 @@ for s in "$@"; do
   case $s in
     list) (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 -L > $OLDPWD/gpurun_out/${T}_counters.txt 2>&1); rc=$? ;;
     bench) timeout -k 10 300 python bench.py --steps ${STEPS:-200} --warmup 10 --no-cpu > gpurun_out/${T}_bench.log 2>&1; rc=$?
-           grep '^{' gpurun_out/${T}_bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('value', round(d['value'],1), 'ms', round(d['ms_per_step']*1e3,2), 'sweep', round(d['roofline']['avg_launch_ms']*1e3,2), 'solve', round(d['roofline_solve']['avg_launch_ms']*1e3,2))" ;;
+           grep '^{' gpurun_out/${T}_bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('value', round(d['value'],1), 'ms', round(d['ms_per_step']*1e3,2), 'sweep', round(d.get('roofline_sweep', d['roofline'])['avg_launch_ms']*1e3,2), 'solve', round(d['roofline_solve']['avg_launch_ms']*1e3,2))" ;;
     drv) timeout -k 10 600 python bench.py > gpurun_out/${T}_drv.log 2>&1; rc=$?; tail -c 600 gpurun_out/${T}_drv.log ;;
     tests) timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q -rf --durations=15 --timeout 300 --timeout-method thread > gpurun_out/${T}_pytest.log 2>&1; rc=$?; tail -3 gpurun_out/${T}_pytest.log ;;
     quick) timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu ${TESTS:-tests/test_gpu_parity.py} > gpurun_out/${T}_quick.log 2>&1; rc=$?; tail -3 gpurun_out/${T}_quick.log ;;
