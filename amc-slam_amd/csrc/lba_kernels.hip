@@ -701,6 +701,9 @@ constexpr int LS_THREADS = 256;
 constexpr int LS_U = (TILE_PAIRS + 2) * 36;   // doubles: rows + weights while linearising, then Hpl / W
                                               // (+ two zero pairs after the tile's last: what phase 7
                                               // reads for absent (landmark, KF) pairs)
+// pidx rows padded by two shorts: a wave's lanes read entry m of up to ~6 different KF rows at once (phase 6's
+// tasks, phase 7's), which unpadded all fall on one LDS bank (-30 % bank-conflict cycles, profiles/r5k_*)
+constexpr int PIDX_STRIDE = TILE_LMS + 2;
 constexpr int DL_STRIDE = 12;   // per landmark in LDS: l10 l21 (l10 l21 - l20) 0 | D^-1 (3) 0 | u (3) 0
 static_assert(TILE_ROWS * (ROW_STRIDE + 1) <= LS_U, "the LDS rows alias the Hpl staging");
 static_assert(EDGE_SHM <= LS_U, "edge items run in the tile LDS");
@@ -724,7 +727,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
     __shared__ int lr0[TILE_LMS + 1];
     __shared__ int scode[TILE_SENT];             // Schur entry: tile-local KF l1 | l2 << 8 (l1 <= l2)
     __shared__ int sslt[TILE_SENT];              // its sslab slot
-    __shared__ __attribute__((aligned(16))) short pidx[TILE_KF * TILE_LMS];   // [tile KF][landmark]: tile-local pair, npair (a zero pair): none
+    __shared__ __attribute__((aligned(16))) short pidx[TILE_KF * PIDX_STRIDE];   // [tile KF][landmark]: tile-local pair, npair (a zero pair): none
     __shared__ unsigned char pm[TILE_PAIRS];     // tile-local landmark of a pair
     __shared__ double red[LS_THREADS / 64];
     if (gated_off(P.ctl, gate)) return;
@@ -776,7 +779,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
         if (tid <= npair) pr0[tid] = P.pair_r0[pair0 + tid] - q0;
         if (tid <= nlm) lr0[tid] = P.lm_r0[lm0 + tid] - m0;
         if (elim)
-            for (int t = tid; t < TILE_LMS * TILE_KF; t += LS_THREADS) pidx[t] = (short)npair;
+            for (int t = tid; t < PIDX_STRIDE * TILE_KF; t += LS_THREADS) pidx[t] = (short)npair;
     }
 
     // ---- phase 1: one observation per lane: residual, robust weight, rows [J1 e Jp] -> LDS
@@ -806,7 +809,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
         }
         if (tid < npair) {
             const int c = P.pair_lk[pair0 + tid];
-            pidx[(c & 255) * TILE_LMS + (c >> 8)] = (short)tid;
+            pidx[(c & 255) * PIDX_STRIDE + (c >> 8)] = (short)tid;
             pm[tid] = (unsigned char)(c >> 8);
         }
     }
@@ -971,8 +974,8 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
             rg = (t2 >> 1) & 3;
             ch = t2 & 1;
         }
-        const short* p1 = pidx + (scode[q] & 255) * TILE_LMS;
-        const short* p2 = pidx + (scode[q] >> 8) * TILE_LMS;
+        const short* p1 = pidx + (scode[q] & 255) * PIDX_STRIDE;
+        const short* p2 = pidx + (scode[q] >> 8) * PIDX_STRIDE;
         double acc[18];
 #pragma unroll
         for (int u = 0; u < 18; ++u) acc[u] = 0.0;
@@ -1005,7 +1008,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
         const int kf0 = P.tile_kf0[tile];
         for (int task = tid; task < nkf * 12; task += LS_THREADS) {
             const int l = task / 12, r = task - 12 * l;
-            const short* pr = pidx + l * TILE_LMS;
+            const short* pr = pidx + l * PIDX_STRIDE;
             double v0 = 0.0, v1 = 0.0;
             int m = 0;
             for (; m + 2 <= nlm; m += 2) {
@@ -2565,7 +2568,7 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
         // (the poses published as soon as they are stored, ahead of their Jacobian factors)
         auto pub = [&]() {
             if (fused) upd_publish(P, role, epoch);
-            if (ustamp) ustamp[-1] = __builtin_amdgcn_s_memrealtime();   // (slot 13: published)
+            if (ustamp) ustamp[-3] = __builtin_amdgcn_s_memrealtime();   // (slot 11: published)
         };
         gp_pair_prep<true>(P, gps, i, kab, kab + KF_STRIDE, jac, ushm + 2 * 12 + 2 * KF_STRIDE + 2 * (KF_STRIDE + 12),
                            ustamp ? P.tdbg_lin + (size_t)blockIdx.x * 16 + 5 : nullptr, pub);
@@ -2666,9 +2669,9 @@ __global__ __launch_bounds__(UPD_THREADS) void k_update(DevProblem P, double lam
         const int tl = role - P.n_gp - nkb;
         static_assert(TILE_SMP <= UPD_THREADS, "one tile sample per lane");
         const int prod = (int)threadIdx.x < P.tile_nsmp[tl] ? P.smp_prod[P.tsm_smp[P.tile_smp0[tl] + threadIdx.x]] : -1;
-        if (ustamp) ustamp[-2] = __builtin_amdgcn_s_memrealtime();   // (slot 12: waiting)
         upd_wait(P, prod, epoch);   // (its barrier also completes ltr)
-        if (ustamp) ustamp[-1] = __builtin_amdgcn_s_memrealtime();   // (slot 13: samples in)
+        if (ustamp) ustamp[-3] = __builtin_amdgcn_s_memrealtime();   // (slot 11: samples in; slots 12 / 13 are the
+                                                                     // sweep's start / end of the same row)
         eval_tile_trial<F32>(P, role - P.n_gp - nkb, si, ltr, to);
     }
     if (ustamp) ustamp[1] = __builtin_amdgcn_s_memrealtime();

@@ -27,6 +27,9 @@ for s in "$@"; do
     pmc) KERNEL=${KERNEL:-k_lin_schur} bash scripts/pmc_linearize.sh $T; rc=$? ;;
     pmcchol) KERNEL=k_chol_flow SQ_COUNTERS="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_FMA_F64 GRBM_GUI_ACTIVE" bash scripts/pmc_linearize.sh $T; rc=$? ;;
     micro) /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 scripts/micro/$MICRO.hip -o /tmp/$MICRO && timeout -k 10 120 /tmp/$MICRO > gpurun_out/${T}_$MICRO.txt 2>&1; rc=$?; cat gpurun_out/${T}_$MICRO.txt ;;
+    cfgs) rc=0; for c in ${CFGS:-cfg2_global_500kf cfg4_global_5k}; do
+            timeout -k 10 300 python bench.py --config $c --steps ${CSTEPS:-5} --warmup 2 --no-cpu > gpurun_out/${T}_bench_$c.log 2>&1 || { rc=$?; break; }
+            grep '^{' gpurun_out/${T}_bench_$c.log | tail -1; done ;;
     phases) timeout -k 10 300 python scripts/phase_times.py --out gpurun_out/${T}_phases.txt > gpurun_out/${T}_phases.log 2>&1; rc=$? ;;
     *) echo "unknown step $s"; rc=2 ;;
   esac

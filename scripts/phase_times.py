@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "amc-slam_amd"))
 
 LIN_PHASES = ["obs residual+J1 -> LDS", "sample M/g", "Hll/bl (+Dinv, LDL)", "Hpl = N^T G"]
-SCHUR_PHASES = ["W = Hpl L^-T", "S partials (MFMA)", "rhs partials"]
+SCHUR_PHASES = ["W = Hpl L^-T", "S partials (VALU)", "rhs partials"]
 SHAPE = ["nobs", "nsmp", "npair", "nlm", "nsent", "nkf"]
 
 
@@ -60,8 +60,10 @@ def report(name, stamps, phases, shape, out):
 
 
 def timeline(lin, shape, out):
-    """Wall-clock (s_memrealtime, 100 MHz) start / end of every tile workgroup of the last launch: the span,
-    how the tiles' start times spread (dispatch rounds) and which tiles end last."""
+    """Wall-clock (s_memrealtime, 100 MHz) start / end of every tile workgroup of the last relinearising launch
+    (slots 12 / 13; a gated launch returns before its first stamp and k_update's stamps of the same rows use
+    slots 5..11 / 14 / 15): the span, how the tiles' start times spread (dispatch rounds) and which tiles end
+    last."""
     st, en = lin[:, 12], lin[:, 13]
     ok = (st > 0) & (en > 0)
     if not ok.any():
