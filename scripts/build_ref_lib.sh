@@ -13,6 +13,8 @@ for f in $(git -C "$ROOT" ls-tree --name-only "$REF" amc-slam_amd/csrc/ include/
   git -C "$ROOT" show "$REF:$f" > "$TMP/$f"
 done
 C=$TMP/amc-slam_amd/csrc
+EXTRA=""
+[ -f "$C/lba_debug.hip" ] && EXTRA="$C/lba_debug.hip"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared "$C/lba_kernels.hip" "$C/lba_host.hip" \
-    "$C/lba_track.hip" -o "$ROOT/amc-slam_amd/lib/exp/$NAME.so" -lrccl
+    "$C/lba_track.hip" $EXTRA -o "$ROOT/amc-slam_amd/lib/exp/$NAME.so" -lrccl
 echo "built $ROOT/amc-slam_amd/lib/exp/$NAME.so from $REF"

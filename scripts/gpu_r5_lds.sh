@@ -16,6 +16,7 @@ args=()
 for v in "$@"; do if [ "$v" = main ]; then args+=(""); else args+=("AMC_LBA_LIB=$X/$v.so"); fi; done
 ROUNDS=${ROUNDS:-2} STEPS=${STEPS:-200} bash scripts/ab_envs.sh ${T}ab "${args[@]}" > gpurun_out/${T}_ab.txt 2>&1; rc=$?
 cat gpurun_out/${T}_ab.txt; [ $rc -eq 0 ] || exit $rc
+[ -n "${SKIP_PMC:-}" ] && exit 0
 for v in "$@"; do
   if [ "$v" = main ]; then unset AMC_LBA_LIB; else export AMC_LBA_LIB=$X/$v.so; fi
   (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS \

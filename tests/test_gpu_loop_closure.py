@@ -112,6 +112,30 @@ def test_loop_tail_shortens_the_chain_same_step():
         assert _rel(other[1], best[1]) <= 1e-8
 
 
+def test_dissection_depth_cap_same_step():
+    """LBA_ND_LEVELS caps the nested dissection's depth (0: the natural panel order, one dependent chain): the same
+    step on the config-1 window as the default plan, through a longer chain."""
+    win = make_config_window("cfg1_local_50kf")
+    lam = win.cfg["lambda_init"]
+
+    def run():
+        p = Problem(win)
+        p.linearize()
+        ok, dx = p.solve_step(lam)
+        assert ok
+        info = p.solver_info()
+        p.close()
+        return info, dx
+
+    best = run()
+    flat = _with_env("LBA_ND_LEVELS", "0", run)
+    one = _with_env("LBA_ND_LEVELS", "1", run)
+    assert flat[0]["levels"] == 0 and flat[0]["chain"] > best[0]["chain"]
+    assert one[0]["levels"] <= 1
+    for other in (flat, one):
+        assert _rel(other[1], best[1]) <= 1e-8
+
+
 def test_windows_without_a_loop_need_no_tail():
     for name in ("cfg1_local_50kf", "cfg0_cpu_plumbing"):
         p = Problem(make_config_window(name))
