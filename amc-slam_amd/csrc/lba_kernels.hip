@@ -472,25 +472,31 @@ __device__ void edge_item(const DevProblem& P, int sel, int idx, const int tid, 
 // slab slots (the same slots / transposition rule as the prior edges).  Equal to summing J^T W J
 // per observation row with J = J1 N (base_multi_edge.hpp:170-222) up to rounding.
 constexpr int PRI_THREADS = 256;
-constexpr int EXP_GROUPS = PRI_THREADS / SM_STRIDE;   // 9 partial sums per output
+// partial sums per output of the M / g reduction: k_exp_asm's 576 threads take one (group, output) each; k_expand's
+// 256 threads loop over the same (group, output) tasks, so both paths sum in the same order (bitwise the same)
+constexpr int EXP_GROUPS = 21;
 
 // A sample of a camera whose extrinsic is free also couples that extrinsic's block e: N is extended by the
 // camera's factor [Ad(Tbc) 0] (columns 24..35) and ae, be, ee, b_e follow the same way.
-template <bool WT>
+template <bool WT, int NT>
 __device__ void sample_expand(const DevProblem& P, const double* gps, const double* camd, int smp, double* Msh,
                               double* Nsh, double* MN, double* part, const int tid) {
     const int* sl = P.seg_slot + SEG_STRIDE * (size_t)smp;
     const int* gl = P.seg_gslot + GSEG_STRIDE * (size_t)smp;
+    // N(l, c) at Nsh[6 c + l]: the sample's part loaded with the slot tables (one memory round trip)
+    const double* Ng = gps + (size_t)smp * GPS_STRIDE + 12;
+    double nv = tid < 144 ? Ng[tid] : 0.0;
     if (sl[0] < 0 && sl[1] < 0 && sl[2] < 0 && sl[6] < 0) return;   // no optimisable vertex (uniform per workgroup)
     const int ncol = sl[6] >= 0 ? 36 : 24;
-    // M / g: group q of the 9 sums every 9th slot of its output (4 loads in flight), then a fixed
-    // combination order over the groups
-    if (tid < EXP_GROUPS * SM_STRIDE) {
-        const int q = tid / SM_STRIDE, o = tid - q * SM_STRIDE;
-        const int k0 = P.ms0[smp] + q, k1 = P.ms0[smp + 1];
+    if (tid >= 144 && tid < 6 * ncol) nv = camd[(size_t)sl[7] * CAMD_STRIDE + 16 + (tid - 144)];
+    // M / g: group q of the EXP_GROUPS sums every EXP_GROUPS-th slot of its output (4 loads in flight), then a
+    // fixed combination order over the groups
+    const int k1 = P.ms0[smp + 1];
+    for (int t = tid; t < EXP_GROUPS * SM_STRIDE; t += NT) {
+        const int q = t / SM_STRIDE, o = t - q * SM_STRIDE;
         const double* m = P.mslab + o;
         double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
-        int k = k0;
+        int k = P.ms0[smp] + q;
         for (; k + 3 * EXP_GROUPS < k1; k += 4 * EXP_GROUPS) {
             v0 += m[(size_t)k * SM_STRIDE];
             v1 += m[(size_t)(k + EXP_GROUPS) * SM_STRIDE];
@@ -498,11 +504,9 @@ __device__ void sample_expand(const DevProblem& P, const double* gps, const doub
             v3 += m[(size_t)(k + 3 * EXP_GROUPS) * SM_STRIDE];
         }
         for (; k < k1; k += EXP_GROUPS) v0 += m[(size_t)k * SM_STRIDE];
-        part[tid] = (v0 + v1) + (v2 + v3);
+        part[t] = (v0 + v1) + (v2 + v3);
     }
-    const double* Ng = gps + (size_t)smp * GPS_STRIDE + 12;
-    if (tid < 144) Nsh[tid] = Ng[tid];   // N(l, c) at Nsh[6 c + l]
-    else if (tid < 6 * ncol) Nsh[tid] = camd[(size_t)sl[7] * CAMD_STRIDE + 16 + (tid - 144)];
+    if (tid < 6 * ncol) Nsh[tid] = nv;
     __syncthreads();
     if (tid < SM_STRIDE) {
         double v = 0.0;
@@ -527,7 +531,7 @@ __device__ void sample_expand(const DevProblem& P, const double* gps, const doub
     // blocks aa, ab, bb, ae, be, ee: column offsets of their row / column vertex in N
     constexpr unsigned char boff_i[6] = {0, 0, 12, 0, 12, 24}, boff_j[6] = {0, 12, 12, 24, 24, 24};
     constexpr unsigned char bslot[6] = {0, 1, 2, 4, 5, 6};
-    for (int t = tid; t < (ncol == 36 ? 6 : 3) * 144; t += PRI_THREADS) {
+    for (int t = tid; t < (ncol == 36 ? 6 : 3) * 144; t += NT) {
         const int bk = t / 144, ij = t % 144, i = ij / 12, j = ij % 12;
         const int slot = sl[bslot[bk]];
         if (slot < 0) continue;
@@ -551,7 +555,7 @@ __device__ void sample_expand(const DevProblem& P, const double* gps, const doub
 
 // Work items of the prior / sample reduction: 0 .. n_prior + n_vel + n_eprior - 1 the EdgeGaussianPrior /
 // EdgeVelocity / EdgeExtrinsicPrior quadratic forms (edge_item, NT threads), then one per pose sample
-// (sample_expand, PRI_THREADS working threads; tid >= PRI_THREADS only takes part in the barriers).  In
+// (sample_expand over the workgroup's threads).  In
 // the queued loop the edge items run as extra workgroups of k_linearize and the samples as extra
 // workgroups of k_schur (they fill the slots the last tiles leave idle); k_prior_lin runs them all for
 // the host-driven paths.  shm: PRI_SHM doubles of LDS.
@@ -1101,7 +1105,7 @@ __global__ __launch_bounds__(PRI_THREADS) void k_expand(DevProblem P, int sel, i
     if ((int)blockIdx.x < P.n_smp) {
         const int si = state_idx(P, sel);
         double *Msh = shm, *Nsh = Msh + 144, *MN = Nsh + 216, *part = MN + 216;
-        sample_expand<false>(P, P.gpsb[si], P.camdb[si], blockIdx.x, Msh, Nsh, MN, part, threadIdx.x);
+        sample_expand<false, PRI_THREADS>(P, P.gpsb[si], P.camdb[si], blockIdx.x, Msh, Nsh, MN, part, threadIdx.x);
         return;
     }
     heavy_item<false>(P, blockIdx.x - P.n_smp, schur ? damping(P, lambda_arg) : 0.0, schur, shm);
@@ -1163,7 +1167,7 @@ __device__ __forceinline__ void exp_wait(const DevProblem& P, const int* prod_of
 // blocks, so they are loaded sc1.
 template <bool FUSED>
 __device__ __forceinline__ void assemble_item(const DevProblem& P, int item, double lambda, int flags, double* red, bool wait,
-                                              unsigned epoch) {
+                                              unsigned epoch, unsigned long long* xs = nullptr) {
     const int tid = threadIdx.x;
     const int n = P.npad;   // leading dimension of S
     if (item < P.n_asm) {
@@ -1173,7 +1177,9 @@ __device__ __forceinline__ void assemble_item(const DevProblem& P, int item, dou
         double v;
         if constexpr (FUSED) {
             const double sv = slot_sum<RED_GROUPS, 144>(P.sslab, P.ss0[ub] + g, P.ss0[ub + 1], e);
+            if (xs) xs[1] = __builtin_amdgcn_s_memrealtime() + (sv != sv);   // (diagnostics: the partials are in)
             if (wait) exp_wait(P, P.hs_prod, P.hs0[ub], P.hs0[ub + 1], epoch);
+            if (xs) xs[2] = __builtin_amdgcn_s_memrealtime();
             v = slot_sum<RED_GROUPS, 144>(P.hslab, P.hs0[ub] + g, P.hs0[ub + 1], e);
             v -= sv;
         } else {
@@ -1248,7 +1254,7 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_assemble(DevProblem P, dou
 }
 
 // k_expand's sample expansions and k_assemble's outputs of a trial in one launch (P.fuse_asm: no heavy landmarks,
-// not partitioned): workgroups [0, n_smp) expand a pose sample each (sample_expand, its first PRI_THREADS threads),
+// not partitioned): workgroups [0, n_smp) expand a pose sample each (sample_expand, all 576 threads),
 // store its Hpp / b_p pieces write-through and publish the launch's epoch in exp_flag; the assembly workgroups
 // after them sum their Schur partials meanwhile and then wait for just the samples their slots come from.  The
 // expansions are the lowest workgroup ids (dispatched first).  gate: the expansions' (k_expand's) gate -- when it
@@ -1258,17 +1264,25 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_exp_asm(DevProblem P, int 
     __shared__ double shm[SHM];
     const bool off = gated_off(P.ctl, gate);
     const int tid = threadIdx.x;
+    // diagnostics (LBA_PHASE_TIMING): s_memrealtime stamps in slots 8.. of the sweep's elimination stamp rows
+    // (expansions: start / expanded / published; assembly blocks: start / partials in / samples in / stored)
+    unsigned long long* xs = (P.tdbg_schur && tid == 0 && (int)blockIdx.x < P.n_tiles && !off)
+                                 ? P.tdbg_schur + (size_t)blockIdx.x * 16 + 8 : nullptr;
+    if (xs) xs[0] = __builtin_amdgcn_s_memrealtime();
     if ((int)blockIdx.x < P.n_smp) {
         if (off) return;
         const int si = state_idx(P, sel);
         double *Msh = shm, *Nsh = Msh + 144, *MN = Nsh + 216, *part = MN + 216;
-        sample_expand<true>(P, P.gpsb[si], P.camdb[si], blockIdx.x, Msh, Nsh, MN, part, tid < PRI_THREADS ? tid : (1 << 20));
+        sample_expand<true, 144 * RED_GROUPS>(P, P.gpsb[si], P.camdb[si], blockIdx.x, Msh, Nsh, MN, part, tid);
+        if (xs) xs[1] = __builtin_amdgcn_s_memrealtime();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) __hip_atomic_store((gi32_t*)(P.exp_flag + (size_t)FLAG_STRIDE * blockIdx.x), (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (xs) xs[2] = __builtin_amdgcn_s_memrealtime();
         return;
     }
-    assemble_item<true>(P, blockIdx.x - P.n_smp, damping(P, lambda_arg), ASM_SCHUR, shm, !off, epoch);
+    assemble_item<true>(P, blockIdx.x - P.n_smp, damping(P, lambda_arg), ASM_SCHUR, shm, !off, epoch, xs);
+    if (xs) xs[3] = __builtin_amdgcn_s_memrealtime();
 }
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));

@@ -125,6 +125,34 @@ def update_timeline(lin, n_gp, n_kfb, out):
                        f"duration mean {d.mean():6.2f} max {d.max():6.2f}")
 
 
+def exp_asm_timeline(sch, out):
+    """k_exp_asm workgroups of the last launch (slots 8.. of the elimination rows; workgroups below n_tiles only):
+    the sample expansions (start / expanded / published) and the assembly blocks (start / Schur partials in /
+    samples in / stored)."""
+    x = sch[:, 8:12]
+    live = x[:, 0] > 0
+    if not live.any():
+        return
+    t0 = x[live, 0].min()
+    exp = live & (x[:, 3] == 0) & (x[:, 2] > 0)
+    asm = live & (x[:, 3] > 0)
+    f = lambda v: (v - t0) / 100.0   # noqa: E731
+    out.append(f"== k_exp_asm timeline (us from the first workgroup's start): {exp.sum()} expansions, {asm.sum()} "
+               f"assembly blocks stamped")
+    if exp.any():
+        e = x[exp]
+        out.append(f"   expansions: start max {f(e[:, 0]).max():6.2f}  expanded mean {f(e[:, 1]).mean():6.2f} max "
+                   f"{f(e[:, 1]).max():6.2f}  published max {f(e[:, 2]).max():6.2f}")
+    if asm.any():
+        a = x[asm]
+        out.append(f"   assembly: start median {np.median(f(a[:, 0])):6.2f} max {f(a[:, 0]).max():6.2f}  partials in "
+                   f"median {np.median(f(a[:, 1])):6.2f}  samples in median {np.median(f(a[:, 2])):6.2f} max "
+                   f"{f(a[:, 2]).max():6.2f}  stored median {np.median(f(a[:, 3])):6.2f} max {f(a[:, 3]).max():6.2f}")
+        d = a[:, 1] - a[:, 0]
+        out.append(f"   assembly block durations (us): partial sums mean {d.mean() / 100:5.2f}, wait for samples mean "
+                   f"{(a[:, 2] - a[:, 1]).mean() / 100:5.2f}, rest mean {(a[:, 3] - a[:, 2]).mean() / 100:5.2f}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg1_local_50kf")
@@ -144,6 +172,7 @@ def main():
     report("k_lin_schur (linearisation)", lin, LIN_PHASES, shape, out)
     report("k_lin_schur (elimination)", sch, SCHUR_PHASES, shape, out)
     timeline(lin, shape, out)
+    exp_asm_timeline(sch, out)
     gp = win.obs["kind"] <= 1   # MONO_GP, STEREO_GP
     n_gp = len(set(zip(win.obs["kf_a"][gp].tolist(), win.obs["kf_b"][gp].tolist())))
     update_timeline(lin, n_gp, (len(win.kfs) + 63) // 64, out)
