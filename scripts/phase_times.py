@@ -148,9 +148,10 @@ def exp_asm_timeline(sch, out):
         out.append(f"   assembly: start median {np.median(f(a[:, 0])):6.2f} max {f(a[:, 0]).max():6.2f}  partials in "
                    f"median {np.median(f(a[:, 1])):6.2f}  samples in median {np.median(f(a[:, 2])):6.2f} max "
                    f"{f(a[:, 2]).max():6.2f}  stored median {np.median(f(a[:, 3])):6.2f} max {f(a[:, 3]).max():6.2f}")
-        d = a[:, 1] - a[:, 0]
-        out.append(f"   assembly block durations (us): partial sums mean {d.mean() / 100:5.2f}, wait for samples mean "
-                   f"{(a[:, 2] - a[:, 1]).mean() / 100:5.2f}, rest mean {(a[:, 3] - a[:, 2]).mean() / 100:5.2f}")
+        a = a[(a[:, 1] > 0) & (a[:, 2] > 0)]   # (the rhs blocks have no partial / sample stamps)
+        if len(a):
+            out.append(f"   S-block durations (us): partial sums mean {(a[:, 1] - a[:, 0]).mean() / 100:5.2f}, wait for "
+                       f"samples mean {(a[:, 2] - a[:, 1]).mean() / 100:5.2f}, rest mean {(a[:, 3] - a[:, 2]).mean() / 100:5.2f}")
 
 
 def main():
