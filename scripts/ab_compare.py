@@ -2,7 +2,7 @@
 comparison against the first variant) and LM iterations per second over repeated optimize(10) calls.
 
     python scripts/ab_compare.py --variant base: --variant dpp:AMC_LBA_LIB=amc-slam_amd/lib/exp/x.so \
-        --variant cap64:LBA_TILE_OBS_CAP=64 [--config cfg1_local_50kf] [--calls 30]
+        --variant unfused:LBA_NO_FUSED_EVAL=1 [--config cfg1_local_50kf] [--calls 30]
 
 Each variant runs in its own process (its environment selects the build and the set-up knobs).
 """

@@ -1,3 +1,5 @@
+// (Builds against the kernels of commit f8904ce or earlier: piv_seq and factor_pair were removed from the product
+// library in round 5; `git show f8904ce:amc-slam_amd/csrc/lba_kernels.hip` restores the version it includes.)
 // Single-wave instruction costs on gfx950 (one workgroup of 64 threads on an otherwise idle GPU), in
 // clock64 cycles per instruction: fp64 FMA (independent / dependent chain), v_readlane_b32 pairs feeding
 // an FMA, DPP64 row-broadcast FMA, ds_bpermute pairs; and the stacked 64 x 32 panel factorisation of

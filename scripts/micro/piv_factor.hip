@@ -1,3 +1,5 @@
+// (Builds against the kernels of commit f8904ce or earlier: piv_seq and factor_pair were removed from the product
+// library in round 5; `git show f8904ce:amc-slam_amd/csrc/lba_kernels.hip` restores the version it includes.)
 // The stacked 64 x 32 panel factorisation: the single-wave two-level sequence of k_chol_flow (piv_seq /
 // cross_update / piv_seq), its software-pipelined form (factor_pipe) and the pair of waves (factor_pair), on an idle GPU: cycles (clock64 of wave 0 between two workgroup barriers) and both results
 // against a long-double Cholesky on the host.
