@@ -179,57 +179,40 @@ def main():
     update_timeline(lin, n_gp, (len(win.kfs) + 63) // 64, out)
     np.savez_compressed(os.path.splitext(args.out)[0] + "_raw.npz", lin=lin, sch=sch, shape=shape)
     if chol is not None:
-        if os.environ.get("LBA_CHOL_STEPS") is None:   # k_chol_flow: s_memrealtime (100 MHz) stamps per panel
-            npan = int((chol[:, 0] != 0).sum())
-            c = chol[:npan].astype(np.int64)
-            t0 = c[:, 0].min()
-            out.append(f"== k_chol_flow panels (us from the first panel task start): start / own updates done / "
-                       f"- / - / factor start / factor end / published")
-            for j in range(npan):
-                v = [(c[j, k] - t0) / 100.0 if c[j, k] else float("nan") for k in range(7)]
-                out.append("   panel %3d: " % j + " ".join(f"{x:7.2f}" for x in v))
-                w = [(c[j, 8 + k] - t0) / 100.0 if c[j, 8 + k] else float("nan") for k in range(7)]
-                out.append("   (j+1,j)  : " + " ".join(f"{x:7.2f}" for x in w))
-            yx = [((c[j, 7] - t0) / 100.0, (c[j, 15] - t0) / 100.0) for j in range(npan)]
-            out.append("   forward block y_j published / solution block x_j written:")
-            out.append("   " + "  ".join(f"{j}:{y:.1f}/{x:.1f}" for j, (y, x) in enumerate(yx)))
-            b2 = bs[:npan].astype(np.int64)
-            for rr in range(2):
-                out.append(f"   L^-1 tiles of row {npan - 2 + rr}: j: start / terms done / L_ii^-1 out / published")
-                for j in range(npan - 2 + rr):
-                    v = [(b2[j, 4 * rr + k] - t0) / 100.0 if b2[j, 4 * rr + k] else float("nan") for k in range(4)]
-                    out.append(f"     {j:3d}: " + " ".join(f"{x:7.2f}" for x in v))
-            if cft is not None:
-                out.append("   factor tasks (ticket: i j lookahead | start / last blocking wait done (panel) / loop done / "
-                           "lookahead factors done / loop+lookahead done / published)")
-                for tk in range(4096):
-                    r = cft[tk]
-                    if r[0] == 0:
-                        continue
-                    f = lambda x: (x - t0) / 100.0 if x else float("nan")
-                    ii, jj, la, pp = r[4] & 4095, (r[4] >> 12) & 4095, (r[4] >> 24) & 1, (r[4] >> 32) & 4095
-                    out.append(f"     {tk:4d}: ({ii:2d},{jj:2d}) la={la} | {f(r[0]):7.2f} {f(r[3]):7.2f} (p={pp:2d}) "
-                               f"{f(r[5]):7.2f} {f(r[6]):7.2f} {f(r[1]):7.2f} {f(r[2]):7.2f}  factor {r[7]} cycles")
-                    if ii == jj and len(r) > 8:   # the panel task's update list: entry end (panel, * = waited)
-                        ent = [f"{r[9 + 2 * e] & 0xffffff}{'*' if (r[9 + 2 * e] >> 24) & 1 else ''}:{f(r[8 + 2 * e]):.2f}"
-                               for e in range(16) if r[8 + 2 * e]]
-                        out.append("            entries " + " ".join(ent))
-            chol = None
-    if chol is not None:
-        nst = int((chol[:, 0] != 0).sum())
-        c = chol[:nst]
-        out.append(f"== k_chol_step (last workgroup of each of {nst} steps), cycles: load / pivots / barrier / update")
-        for i in range(nst):
-            out.append(f"   step {i:3d}: {c[i, 1] - c[i, 0]:7d} {c[i, 2] - c[i, 1]:7d} {c[i, 3] - c[i, 2]:7d} "
-                       f"{c[i, 4] - c[i, 3]:7d}")
-        npan = int((bs[:, 0] != 0).sum())
-        nb = npan
-        b = bs[:nb + 1]
-        out.append(f"== k_chol_backsolve, cycles per block: diagonal solve / barrier wait / trailing GEMV")
-        for blk in range(nb - 1, -1, -1):
-            end = b[blk - 1, 0] if blk > 0 else 0
-            gemv = (end - b[blk, 2]) if blk > 0 else 0
-            out.append(f"   block {blk:3d}: {b[blk, 1] - b[blk, 0]:7d} {b[blk, 2] - b[blk, 1]:7d} {gemv:7d}")
+        npan = int((chol[:, 0] != 0).sum())
+        c = chol[:npan].astype(np.int64)
+        t0 = c[:, 0].min()
+        out.append(f"== k_chol_flow panels (us from the first panel task start): start / own updates done / "
+                   f"- / - / factor start / factor end / published")
+        for j in range(npan):
+            v = [(c[j, k] - t0) / 100.0 if c[j, k] else float("nan") for k in range(7)]
+            out.append("   panel %3d: " % j + " ".join(f"{x:7.2f}" for x in v))
+            w = [(c[j, 8 + k] - t0) / 100.0 if c[j, 8 + k] else float("nan") for k in range(7)]
+            out.append("   (j+1,j)  : " + " ".join(f"{x:7.2f}" for x in w))
+        yx = [((c[j, 7] - t0) / 100.0, (c[j, 15] - t0) / 100.0) for j in range(npan)]
+        out.append("   forward block y_j published / solution block x_j written:")
+        out.append("   " + "  ".join(f"{j}:{y:.1f}/{x:.1f}" for j, (y, x) in enumerate(yx)))
+        b2 = bs[:npan].astype(np.int64)
+        for rr in range(2):
+            out.append(f"   L^-1 tiles of row {npan - 2 + rr}: j: start / terms done / L_ii^-1 out / published")
+            for j in range(npan - 2 + rr):
+                v = [(b2[j, 4 * rr + k] - t0) / 100.0 if b2[j, 4 * rr + k] else float("nan") for k in range(4)]
+                out.append(f"     {j:3d}: " + " ".join(f"{x:7.2f}" for x in v))
+        if cft is not None:
+            out.append("   factor tasks (ticket: i j lookahead | start / last blocking wait done (panel) / loop done / "
+                       "lookahead factors done / loop+lookahead done / published)")
+            for tk in range(4096):
+                r = cft[tk]
+                if r[0] == 0:
+                    continue
+                f = lambda x: (x - t0) / 100.0 if x else float("nan")
+                ii, jj, la, pp = r[4] & 4095, (r[4] >> 12) & 4095, (r[4] >> 24) & 1, (r[4] >> 32) & 4095
+                out.append(f"     {tk:4d}: ({ii:2d},{jj:2d}) la={la} | {f(r[0]):7.2f} {f(r[3]):7.2f} (p={pp:2d}) "
+                           f"{f(r[5]):7.2f} {f(r[6]):7.2f} {f(r[1]):7.2f} {f(r[2]):7.2f}  factor {r[7]} cycles")
+                if ii == jj and len(r) > 8:   # the panel task's update list: entry end (panel, * = waited)
+                    ent = [f"{r[9 + 2 * e] & 0xffffff}{'*' if (r[9 + 2 * e] >> 24) & 1 else ''}:{f(r[8 + 2 * e]):.2f}"
+                           for e in range(16) if r[8 + 2 * e]]
+                    out.append("            entries " + " ".join(ent))
     text = "\n".join(out)
     print(text)
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
