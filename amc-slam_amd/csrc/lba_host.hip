@@ -103,6 +103,9 @@ struct lba_problem {
     // length touches nothing (no allocation, page faults or zeroing per window; every element is written)
     std::vector<int> scr_i[16];
     std::vector<double> scr_d[2];
+    // device ranges set_problem zeroes: collected, then cleared by ONE kernel launch at its end (k_zero_ranges)
+    // instead of one hipMemsetAsync each (~17 runtime calls and ~28 fill kernels per set-up)
+    std::vector<unsigned long long> zero_list;   // pairs: device address, 4-byte words
     double* h_fin = nullptr;      // host-mapped coherent [HFIN_DOUBLES]: trial summary [4], sequence
                                   // number [4], LMCtl mirror [8..] (queued optimisation)
     double* d_hfin = nullptr;     // its device address
@@ -544,6 +547,14 @@ bool inverse6(const double* A, double* R) {
     return true;
 }
 
+// a device range of set_problem's to be zeroed by the set-up's single k_zero_ranges launch (flush_zero_ranges); the
+// ranges are fresh buffers no upload of the set-up writes, so clearing them all at its end keeps the stream order
+void zero_later(lba_problem* p, void* d, size_t bytes) {
+    p->zero_list.push_back((unsigned long long)(uintptr_t)d);
+    p->zero_list.push_back((bytes + 3) / 4);   // (every range is a whole number of 4-byte words)
+}
+void flush_zero_ranges(lba_problem* p);
+
 inline int ublock_id(int n_pb, int bi, int bj) { return bi * n_pb - bi * (bi - 1) / 2 + (bj - bi); }
 
 // ------------------------------------------------------------------------------------------------
@@ -649,6 +660,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     p->status_entered = false;
     if (p->stream) HIPCHK(hipStreamSynchronize(p->stream));   // (the buffers are reused below)
     free_all(p);
+    p->zero_list.clear();
     p->n_kf = n_kf; p->n_lm = n_lm; p->n_obs = n_obs; p->n_cam = n_cam;
     p->lm_host.assign(lm_xyz, lm_xyz + 3 * (size_t)n_lm);
     p->kf_fixed.resize(n_kf);
@@ -1917,7 +1929,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             const size_t niv = band ? (size_t)NP + 1 : (size_t)std::max(NP * (NP + 1) / 2, 1);
             D.cf_linv = band ? nullptr : dalloc<double>(p, (size_t)npad * npad);
             D.cf_ivready = dalloc<int>(p, niv);
-            HIPCHK(hipMemsetAsync(D.cf_ivready, 0, sizeof(int) * niv, p->stream));
+            zero_later(p, D.cf_ivready, sizeof(int) * niv);
             D.cf_xpos = band ? dalloc<double>(p, npad) : nullptr;
             D.cf_pl0 = dupload(p, pl0);
             D.cf_plist = dupload(p, plist);
@@ -1925,16 +1937,16 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             D.cf_lready = dalloc<int>(p, std::max(ntile, 1));
             D.cf_dready = dalloc<int>(p, std::max(NP, 1));
             D.cf_fready = dalloc<int>(p, std::max(NP, 1));
-            HIPCHK(hipMemsetAsync(D.cf_fready, 0, sizeof(int) * std::max(NP, 1), p->stream));
+            zero_later(p, D.cf_fready, sizeof(int) * std::max(NP, 1));
             D.cf_zready = dalloc<int>(p, std::max(NP, 1));
-            HIPCHK(hipMemsetAsync(D.cf_zready, 0, sizeof(int) * std::max(NP, 1), p->stream));
+            zero_later(p, D.cf_zready, sizeof(int) * std::max(NP, 1));
             D.cf_zv = band ? nullptr : dalloc<double>(p, std::max((size_t)NP * NP * CHOL_NB, (size_t)1));
             D.cf_head = dalloc<unsigned long long>(p, 2);   // (ticket counters of the split's two launches)
             D.cf_abort = dalloc<int>(p, 1);
-            HIPCHK(hipMemsetAsync(D.cf_lready, 0, sizeof(int) * std::max(ntile, 1), p->stream));
-            HIPCHK(hipMemsetAsync(D.cf_dready, 0, sizeof(int) * std::max(NP, 1), p->stream));
-            HIPCHK(hipMemsetAsync(D.cf_head, 0, 2 * sizeof(unsigned long long), p->stream));
-            HIPCHK(hipMemsetAsync(D.cf_abort, 0, sizeof(int), p->stream));
+            zero_later(p, D.cf_lready, sizeof(int) * std::max(ntile, 1));
+            zero_later(p, D.cf_dready, sizeof(int) * std::max(NP, 1));
+            zero_later(p, D.cf_head, 2 * sizeof(unsigned long long));
+            zero_later(p, D.cf_abort, sizeof(int));
         }
         sub("  flow tasks");
         D.cf_rowptr = dupload(p, pl.rowptr);
@@ -1999,14 +2011,14 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.bp = dalloc<double>(p, p->np + 1);
     D.xsol = dalloc<double>(p, npad + 1);
     D.bS = dalloc<double>(p, npad + 1);
-    HIPCHK(hipMemsetAsync(D.bS, 0, sizeof(double) * (npad + 1), p->stream));
+    zero_later(p, D.bS, sizeof(double) * (npad + 1));
     D.yv = dalloc<double>(p, npad + 1);
     // S and L start zero (k_assemble writes the identity of the padding rows every time)
-    HIPCHK(hipMemsetAsync(D.S, 0, sizeof(double) * (n_env_doubles + 1), p->stream));
-    HIPCHK(hipMemsetAsync(D.Lm, 0, sizeof(double) * (n_env_doubles + 1), p->stream));
-    HIPCHK(hipMemsetAsync(D.xsol, 0, sizeof(double) * (npad + 1), p->stream));
+    zero_later(p, D.S, sizeof(double) * (n_env_doubles + 1));
+    zero_later(p, D.Lm, sizeof(double) * (n_env_doubles + 1));
+    zero_later(p, D.xsol, sizeof(double) * (npad + 1));
     D.x = dalloc<double>(p, p->np + 3 * (size_t)nl + 1);
-    HIPCHK(hipMemsetAsync(D.x, 0, sizeof(double) * (p->np + 3 * (size_t)nl + 1), p->stream));   // BlockSolver::_x before any solve
+    zero_later(p, D.x, sizeof(double) * (p->np + 3 * (size_t)nl + 1));   // BlockSolver::_x before any solve
     const int nchi = n_tiles + D.n_prior + D.n_vel + D.n_eprior;
     D.chi_lin = dalloc<double>(p, nchi + 1);
     D.n_chi = nchi;
@@ -2044,7 +2056,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         for (int k = 0; k < n_kfs; ++k) prod[D.n_gps + k] = D.n_gp + k / UPD_BLOCK_KFS;
         D.smp_prod = dupload(p, prod);
         D.upd_flag = dalloc<int>(p, (size_t)FLAG_STRIDE * (D.n_gp + nkb + 1));
-        HIPCHK(hipMemsetAsync(D.upd_flag, 0, sizeof(int) * FLAG_STRIDE * (D.n_gp + nkb + 1), p->stream));
+        zero_later(p, D.upd_flag, sizeof(int) * FLAG_STRIDE * (D.n_gp + nkb + 1));
         p->upd_epoch = 0;
     }
     // k_expand + k_assemble of a trial in one launch (LBA_NO_FUSED_ASM: two): not with heavy landmarks (their merge
@@ -2053,17 +2065,17 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
     D.hs_prod = dupload(p, hs_prod);
     D.gs_prod = dupload(p, gs_prod);
     D.exp_flag = dalloc<int>(p, (size_t)FLAG_STRIDE * std::max(D.n_smp, 1));
-    HIPCHK(hipMemsetAsync(D.exp_flag, 0, sizeof(int) * FLAG_STRIDE * std::max(D.n_smp, 1), p->stream));
+    zero_later(p, D.exp_flag, sizeof(int) * FLAG_STRIDE * std::max(D.n_smp, 1));
     p->asm_epoch = 0;
     D.info = dalloc<int>(p, 1);
     D.fault = dalloc<int>(p, 1);
-    HIPCHK(hipMemsetAsync(D.fault, 0, sizeof(int), p->stream));
+    zero_later(p, D.fault, sizeof(int));
     D.ctl = dalloc<LMCtl>(p, 1);
     D.fin = dalloc<double>(p, 4);
     D.ob_chi2 = dalloc<double>(p, std::max(n_obs, 1));
     D.ob_res = dalloc<double>(p, 3 * (size_t)std::max(n_obs, 1));
     D.depth_ok = dalloc<unsigned char>(p, std::max(n_obs, 1));
-    HIPCHK(hipMemsetAsync(D.info, 0, sizeof(int), p->stream));
+    zero_later(p, D.info, sizeof(int));
     for (int s = 0; s < 2; ++s) {
         p->kst[s] = dalloc<double>(p, kst.size());
         p->lst[s] = dalloc<double>(p, lst.size());
@@ -2072,9 +2084,10 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         D.kbuf[s] = p->kst[s];
         D.lbuf[s] = p->lst[s];
     }
-    HIPCHK(hipMemsetAsync(D.ctl, 0, sizeof(LMCtl), p->stream));
+    zero_later(p, D.ctl, sizeof(LMCtl));
+    flush_zero_ranges(p);
     flush_uploads(p);
-    HIPCHK(hipStreamSynchronize(p->stream));   // the staged uploads (dupload) have landed
+    HIPCHK(hipStreamSynchronize(p->stream));   // the staged uploads (dupload) have landed, the ranges are zero
     mark("solve layout");
     p->cur = 0;
     p->has_problem = true;
@@ -2086,6 +2099,18 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
 // ------------------------------------------------------------------------------------------------
 // computeActiveErrors + buildSystem at the current state (no elimination): H_pp / b_p pieces, Hpl,
 // Hll, bl (lba_linearize, computeLambdaInit)
+// the set-up's zero ranges in one launch: the (address, words) list is staged like every other upload, then the
+// kernel clears every range after the flush that carries the list
+void flush_zero_ranges(lba_problem* p) {
+    if (p->zero_list.empty()) return;
+    const int n = (int)(p->zero_list.size() / 2);
+    const unsigned long long* d = dupload(p, p->zero_list);
+    flush_uploads(p);
+    launch_zero_ranges(d, n, p->stream);
+    HIPCHK(hipGetLastError());
+    p->zero_list.clear();
+}
+
 void linearize(lba_problem* p, int write_res) {
     const DevProblem& D = p->D;
     if (!p->gps_fresh[p->cur]) launch_gp_prep(D, p->cur, 1, GATE_NONE, p->stream);

@@ -2943,6 +2943,19 @@ __global__ __launch_bounds__(256) void k_finalize(DevProblem P, unsigned long lo
     finalize_body<256>(P, seq, mode, red);
 }
 
+// lba_set_problem's zero ranges (pairs: address, 4-byte words), grid-stride over every range with vector stores
+__global__ __launch_bounds__(256) void k_zero_ranges(const unsigned long long* __restrict__ r, int n) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (int k = 0; k < n; ++k) {
+        unsigned* d = reinterpret_cast<unsigned*>(r[2 * k]);
+        const size_t words = r[2 * k + 1];
+        for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) d[i] = 0u;
+    }
+}
+void launch_zero_ranges(const unsigned long long* ranges, int n, hipStream_t s) {
+    if (n > 0) hipLaunchKernelGGL(k_zero_ranges, dim3(256), dim3(256), 0, s, ranges, n);
+}
+
 __global__ void k_ctl_init(DevProblem P, LMCtl c) {
     if (threadIdx.x == 0) *P.ctl = c;
 }
