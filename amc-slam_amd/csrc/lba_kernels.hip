@@ -1411,29 +1411,33 @@ __device__ __forceinline__ void piv_pipe(double (&row)[CNB], double rn, double d
 }
 
 // Between the halves: every stacked row's columns 16..31 -= (its columns 0..15) (rows 16..31's
-// columns 0..15)^T, i.e. A22 -= L21 L21^T and the tile rows' share, as 4 row tiles x 4 k-steps of
+// columns 0..15)^T, i.e. A22 -= L21 L21^T and the tile rows' share, as 3 row tiles (rows 16..63) x 4 k-steps of
 // v_mfma_f64_16x16x4 on the wave's LDS staging buffer (columns 0..15 in, the product out through
-// columns 16..31).
+// columns 16..31).  Rows 0..15 get no product: their columns 16..31 lie above the diagonal of L_jj, which no
+// reader takes (L_jj is stored masked), and the second half's pivots never read lanes 0..15.  An fp64 MFMA holds
+// its wave ≈75 cycles, so the fourth row tile cost ≈340 of the factor's ≈6.9k cycles (scripts/micro/factor_stages.hip;
+// issuing the k-steps inside the first half's pivots, or on a helper wave, gained nothing more:
+// profiles/r6b_factor_stages.txt).
 __device__ __forceinline__ void cross_update(double (&row)[CNB], double (*st)[CNB + 1], int lane, double dg0 = 0.0,
                                              double* dg2 = nullptr) {
 #pragma unroll
     for (int c = 0; c < 16; ++c) st[lane][c] = row[c];
     wave_sync();
     const int lr = lane & 15, kq = lane >> 4;
-    d4 acc[4];
+    d4 acc[3];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int t = 0; t < 3; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
         const double bv = st[16 + lr][4 * ks + kq];
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(st[16 * t + lr][4 * ks + kq], bv, acc[t], 0, 0, 0);
+        for (int t = 0; t < 3; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(st[16 * (t + 1) + lr][4 * ks + kq], bv, acc[t], 0, 0, 0);
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 3; ++t)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) st[16 * t + kq + 4 * q][16 + lr] = acc[t][q];
+        for (int q = 0; q < 4; ++q) st[16 * (t + 1) + kq + 4 * q][16 + lr] = acc[t][q];
     wave_sync();
     // (lanes 16..31: the diagonal entry after the update, for piv_pipe's tracking; the first half did not
     // touch columns 16..31, so it is the original entry minus the product, as row[lane] below)
