@@ -996,7 +996,8 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
             for (int i = 0; i < 3; ++i)
 #pragma unroll
                 for (int j = 0; j < 6; ++j)
-                    acc[i * 6 + j] += a[i * 3] * b[j * 3] + a[i * 3 + 1] * b[j * 3 + 1] + a[i * 3 + 2] * b[j * 3 + 2];
+                    acc[i * 6 + j] = fma(a[i * 3 + 2], b[j * 3 + 2],
+                                         fma(a[i * 3 + 1], b[j * 3 + 1], fma(a[i * 3], b[j * 3], acc[i * 6 + j])));
         }
         if (!LBA_INB(P, sslt[q], P.n_sslots, "sslab")) continue;
         double* o = P.sslab + (size_t)sslt[q] * 144 + (3 * rg) * 12 + 6 * ch;
