@@ -916,8 +916,8 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
                 for (int l = 0; l < 6; ++l) n[l] = Nc[6 * i + l];
 #pragma unroll
                 for (int a = 0; a < 3; ++a)
-                    hacc[i * 3 + a] += n[0] * g[a] + n[1] * g[3 + a] + n[2] * g[6 + a] + n[3] * g[9 + a] +
-                                       n[4] * g[12 + a] + n[5] * g[15 + a];
+                    hacc[i * 3 + a] = fma(n[5], g[15 + a], fma(n[4], g[12 + a], fma(n[3], g[9 + a],
+                                      fma(n[2], g[6 + a], fma(n[1], g[3 + a], fma(n[0], g[a], hacc[i * 3 + a]))))));
             }
         }
         // only the segment tiles of heavy landmarks store their Hpl (k_expand merges them); a regular tile's
@@ -1021,13 +1021,13 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
                 const double* w1 = U + pr[m + 1] * 36 + r * 3;
                 const double* u0 = Dl + m * DL_STRIDE + 8;
                 const double* u1 = u0 + DL_STRIDE;
-                v0 += w0[0] * u0[0] + w0[1] * u0[1] + w0[2] * u0[2];
-                v1 += w1[0] * u1[0] + w1[1] * u1[1] + w1[2] * u1[2];
+                v0 = fma(w0[2], u0[2], fma(w0[1], u0[1], fma(w0[0], u0[0], v0)));
+                v1 = fma(w1[2], u1[2], fma(w1[1], u1[1], fma(w1[0], u1[0], v1)));
             }
             if (m < nlm) {
                 const double* w0 = U + pr[m] * 36 + r * 3;
                 const double* u0 = Dl + m * DL_STRIDE + 8;
-                v0 += w0[0] * u0[0] + w0[1] * u0[1] + w0[2] * u0[2];
+                v0 = fma(w0[2], u0[2], fma(w0[1], u0[1], fma(w0[0], u0[0], v0)));
             }
             if (LBA_INB(P, P.tkf_gslot[kf0 + l], P.n_gpslots, "gpslab")) P.gpslab[(size_t)P.tkf_gslot[kf0 + l] * 12 + r] = v0 + v1;
         }
