@@ -91,6 +91,9 @@ def lib():
         L.lba_farm_plan.argtypes = [vp, _lp, _ip, _lp, _ip, _ip]
         L.lba_farm_exchange.argtypes = [vp]
         L.lba_solver_info.argtypes = [vp, _ip]
+        if hasattr(L, "lba_trial_state"):   # (absent from builds before it: A/B runs of older libraries)
+            L.lba_trial_state.argtypes = [vp, vp, _dp]
+            L.lba_debug_inject_fault.argtypes = [vp, ctypes.c_int32]
         L.lba_kernel_modes.argtypes = [vp, _ip]
         if hasattr(L, "lba_debug_pool_stress"):
             L.lba_debug_pool_stress.argtypes = [ctypes.c_int32, ctypes.c_int32]
@@ -384,6 +387,17 @@ class Problem:
 
     def farm_exchange(self):
         self._check(lib().lba_farm_exchange(self.h))
+
+    def trial_state(self):
+        """lba_trial_state: the last solve_step's trial estimate (the device's x (+) dx), the current one unchanged."""
+        kfs = np.zeros(self.n_kf, KF_DTYPE)
+        lm = np.zeros((self.n_lm, 3))
+        self._check(lib().lba_trial_state(self.h, ptr(kfs), _d(lm)))
+        return kfs, lm
+
+    def inject_fault(self, code):
+        """lba_debug_inject_fault: set the device fault word as a timed-out in-launch wait does."""
+        self._check(lib().lba_debug_inject_fault(self.h, int(code)))
 
     def set_state(self, kfs=None, lm=None):
         kfs = None if kfs is None else np.ascontiguousarray(kfs, dtype=KF_DTYPE)

@@ -51,6 +51,11 @@ constexpr int ROW_STRIDE = 10;      // LDS Jacobian row: J1(6) e(1) Jp(3) (J1: w
 constexpr int G_STRIDE = 18;        // per observation: G = rho' w sum_rows J1^T Jp (6 x 3, row-major)
 constexpr int SM_STRIDE = 27;       // per (tile, sample) partial: M = sum rho' w J1^T J1 (21, upper
                                     // row-major) and g = sum rho' w J1^T e (6)
+// slot pitches of the partial slabs in doubles: every slot fills whole 128-byte lines of its own, so a slot handed from
+// its producer to its consumer inside one launch (k_exp_asm's gslab pieces) shares no line with another target's
+// slots (hslab / sslab slots are 144 doubles = 9 lines already)
+constexpr int MS_PITCH = 32;        // mslab: 27 used
+constexpr int GS_PITCH = 16;        // gslab / gpslab: 12 used
 constexpr int TILE_SMP = 64;        // pose samples per tile (k_linearize stages their row runs)
 constexpr int TILE_PROWS = 2 * TILE_OBS;    // pair entry-list entries per tile (each obs feeds <= 2 pairs)
 constexpr int TILE_SENT = TILE_KF * (TILE_KF + 1) / 2;   // KF-pair Schur entries per tile
@@ -98,6 +103,8 @@ constexpr double LAMBDA_CTL = __builtin_nan("");
 
 // fault codes (DevProblem::fault): which bounded wait timed out
 enum { FAULT_FLOW = 1, FAULT_EXP = 2, FAULT_UPD = 4 };
+constexpr int RED_FAULT_BITS = 3;
+constexpr int RED_N = 4 + RED_FAULT_BITS;   // doubles of DevProblem::red4
 
 struct DevProblem {
     int n_kf, n_lm, n_obs, n_gp, n_pairs, n_tiles, n_pb, np, n_prior, n_vel, n_cam;
@@ -209,12 +216,12 @@ struct DevProblem {
     double huber_mono, huber_stereo, huber_prior;
     // work buffers
     double* gpsb[2];        // [n_smp][GPS_STRIDE] pose samples (Rwb twb N, lba::GPSample) of state buffer 0 / 1
-    double* mslab;          // [n_mslots][SM_STRIDE] per (tile, sample) M / g partials, sample-sorted
+    double* mslab;          // [n_mslots][MS_PITCH] per (tile, sample) M / g partials, sample-sorted
     double* kfp_pose;       // [n_kf][KFP_STRIDE] Rwb twb (same prefix as a sample)
     double* hslab;          // [n_hslots][144] Hpp partial blocks, target-sorted
-    double* gslab;          // [n_gslots][12] b_p partials, target-sorted
+    double* gslab;          // [n_gslots][GS_PITCH] b_p partials, target-sorted
     double* sslab;          // [n_sslots][144] Schur partial blocks, target-sorted
-    double* gpslab;         // [n_gpslots][12] Schur rhs partials, target-sorted
+    double* gpslab;         // [n_gpslots][GS_PITCH] Schur rhs partials, target-sorted
     double* Lm;             // Cholesky factor, the same tiles as S (lower)
     // dense solve in the factorisation (nested-dissection) order of the panels: position = ppos[natural],
     // natural = pnat[position]; pfirst = envelope of the permuted matrix
@@ -313,7 +320,8 @@ struct DevProblem {
     int cf_ntasks2;
     const int* top_tiles;   // tiles of L in the top columns (packed into env_buf ahead of bS / b_p)
     int n_top_tiles;
-    double* red4;           // [4] trial sums of this rank, all-reduced before k_finalize reads them
+    double* red4;           // [RED_N] trial sums of this rank, the factorisation status, then the fault word's bits,
+                            // all-reduced before k_finalize reads them
     double* env_buf;        // [n_env] (cf_split: the top tiles,) bS [npad], then b_p [np] (all-reduce buffer; replicated
                             // solve: S is all-reduced in place)
     long long n_env;

@@ -1616,12 +1616,12 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         D.gpsb[0] = dupload(p, g0);
         D.gpsb[1] = dupload(p, g0);
     }
-    D.mslab = dalloc<double>(p, (size_t)SM_STRIDE * std::max(n_mslots, 1));
+    D.mslab = dalloc<double>(p, (size_t)MS_PITCH * std::max(n_mslots, 1));
     D.kfp_pose = dalloc<double>(p, (size_t)KFP_STRIDE * std::max(n_kfs, 1));
     D.hslab = dalloc<double>(p, (size_t)144 * std::max(n_hslots, 1));
-    D.gslab = dalloc<double>(p, (size_t)12 * std::max(n_gslots, 1));
+    D.gslab = dalloc<double>(p, (size_t)GS_PITCH * std::max(n_gslots, 1));
     D.sslab = dalloc<double>(p, (size_t)144 * std::max(n_sslots, 1));
-    D.gpslab = dalloc<double>(p, (size_t)12 * std::max(n_gpslots, 1));
+    D.gpslab = dalloc<double>(p, (size_t)GS_PITCH * std::max(n_gpslots, 1));
     D.n_mslots = n_mslots; D.n_hslots = n_hslots; D.n_gslots = n_gslots; D.n_sslots = n_sslots; D.n_gpslots = n_gpslots;
     const int npad = (p->np + CHOL_NB - 1) / CHOL_NB * CHOL_NB;
     mark("upload");
@@ -1984,7 +1984,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             // bS, b_p (replicated solve: S is all-reduced in place; split: the top tiles lead the buffer)
             D.n_env = (long long)D.n_top_tiles * CHOL_NB * CHOL_NB + npad + p->np;
             D.env_buf = dalloc<double>(p, (size_t)D.n_env);
-            D.red4 = dalloc<double>(p, 4);
+            D.red4 = dalloc<double>(p, RED_N);
         }
         D.asm_list = dupload(p, asm_list);
         D.n_asm = (int)asm_list.size();
@@ -2125,7 +2125,10 @@ void linearize(lba_problem* p, int write_res) {
 // the call fails instead of returning results computed from it; the word is cleared for the next call
 [[noreturn]] void throw_fault(lba_problem* p, int code) {
     HIPCHK(hipStreamSynchronize(p->stream));
-    HIPCHK(hipMemset(p->D.fault, 0, sizeof(int)));
+    // (on the problem's own stream, which is non-blocking: a null-stream memset would not be ordered before the next
+    // call's kernels)
+    HIPCHK(hipMemsetAsync(p->D.fault, 0, sizeof(int), p->stream));
+    HIPCHK(hipStreamSynchronize(p->stream));
     throw ApiError{LBA_E_TIMEOUT, std::string("a device hand-off wait timed out (") +
                                       ((code & FAULT_FLOW) ? " factorisation" : "") + ((code & FAULT_EXP) ? " assembly" : "") +
                                       ((code & FAULT_UPD) ? " trial evaluation" : "") +
@@ -2208,7 +2211,7 @@ void launch_solve(lba_problem* p, hipEvent_t e0, hipEvent_t e1, int sel, double 
 void launch_fin(lba_problem* p, unsigned long long seq, int mode) {
     if (p->part_n > 0) {
         launch_partials(p->D, p->stream);
-        preduce(p, p->D.red4, 4);
+        preduce(p, p->D.red4, RED_N);
     }
     launch_finalize(p->D, seq, mode, p->stream);
 }
@@ -2592,6 +2595,18 @@ int lba_set_config(lba_problem* p, const lba_config* cfg) {
 const char* lba_last_error(const lba_problem* p) { return p ? p->err.c_str() : "null problem"; }
 
 int lba_pose_dim(const lba_problem* p) { return p && p->has_problem ? p->np_ext : 0; }
+
+int lba_debug_inject_fault(lba_problem* p, int32_t code) {
+    if (!p || !p->has_problem || code <= 0 || code > (FAULT_FLOW | FAULT_EXP | FAULT_UPD)) return LBA_E_ARG;
+    try {
+        HIPCHK(hipSetDevice(p->cfg.device));
+        HIPCHK(hipMemcpyAsync(p->D.fault, &code, sizeof(int), hipMemcpyHostToDevice, p->stream));
+        HIPCHK(hipStreamSynchronize(p->stream));
+        return LBA_OK;
+    } catch (const HipError& e) {
+        return map_error(p, e);
+    }
+}
 
 int lba_get_cams(lba_problem* p, lba_cam* cams_out) {
     if (!p || !p->has_problem || !cams_out) return LBA_E_ARG;
@@ -3247,14 +3262,14 @@ int lba_optimize(lba_problem* p, int32_t iters, volatile const int32_t* stop_fla
     }
 }
 
-int lba_get_state(lba_problem* p, lba_kf* kf_out, double* lm_out) {
+static int get_state_buf(lba_problem* p, int buf, lba_kf* kf_out, double* lm_out) {
     if (!p || !p->has_problem) return LBA_E_ARG;
     try {
         HIPCHK(hipSetDevice(p->cfg.device));
         std::vector<double> kst(KF_STRIDE * (size_t)std::max(p->n_kf, 1)), lst(3 * (size_t)std::max(p->n_lm_dev, 1));
-        HIPCHK(hipMemcpyAsync(kst.data(), p->kst[p->cur], KF_STRIDE * (size_t)p->n_kf * sizeof(double),
+        HIPCHK(hipMemcpyAsync(kst.data(), p->kst[buf], KF_STRIDE * (size_t)p->n_kf * sizeof(double),
                               hipMemcpyDeviceToHost, p->stream));
-        HIPCHK(hipMemcpyAsync(lst.data(), p->lst[p->cur], 3 * (size_t)p->n_lm_dev * sizeof(double),
+        HIPCHK(hipMemcpyAsync(lst.data(), p->lst[buf], 3 * (size_t)p->n_lm_dev * sizeof(double),
                               hipMemcpyDeviceToHost, p->stream));
         HIPCHK(hipStreamSynchronize(p->stream));
         if (kf_out)
@@ -3278,6 +3293,14 @@ int lba_get_state(lba_problem* p, lba_kf* kf_out, double* lm_out) {
     } catch (const HipError& e) {
         return map_error(p, e);
     }
+}
+
+int lba_get_state(lba_problem* p, lba_kf* kf_out, double* lm_out) {
+    return p ? get_state_buf(p, p->cur, kf_out, lm_out) : LBA_E_ARG;
+}
+
+int lba_trial_state(lba_problem* p, lba_kf* kf_out, double* lm_out) {
+    return p ? get_state_buf(p, 1 - p->cur, kf_out, lm_out) : LBA_E_ARG;
 }
 
 int lba_set_state(lba_problem* p, const lba_kf* kf_in, const double* lm_xyz) {

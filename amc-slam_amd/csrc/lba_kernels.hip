@@ -113,6 +113,31 @@ __device__ __forceinline__ size_t s_elem(const DevProblem& P, int r, int c) {
     return (size_t)lo * (CHOL_NB * CHOL_NB) + (r % CHOL_NB) * CHOL_NB + (c % CHOL_NB);
 }
 
+// Storage order of a Schur partial block (sslab slot, 144 doubles = 9 cache lines).  The sweep's S-partial phase
+// computes a 12 x 12 block as 8 tasks on 8 consecutive lanes, task L holding rows 3 (L >> 1) .. + 2 and columns
+// 6 (L & 1) .. + 5 (element u = 6 i + j of its 18); slot position f = 16 (u >> 1) + 2 L + (u & 1) puts the k-th pair
+// of every task into line k, so each of the task's 16-byte stores k = 0..8 writes, with its 7 neighbours, one whole
+// line (write-through stores of such lines, or 8-byte ones in the row-major layout, made the sweep 3 and 32 us slower:
+// profiles/r7_fold_rejected.txt).  The reductions sum position by position, so only the element a position holds
+// changes.
+__device__ __forceinline__ int spos_rc(int f) {   // (row << 4 | col) of slot position f
+    const int L = (f & 15) >> 1, u = 2 * (f >> 4) + (f & 1);
+    const int i = u / 6, j = u - 6 * i;
+    return ((3 * (L >> 1) + i) << 4) | (6 * (L & 1) + j);
+}
+__device__ __forceinline__ int spos_of(int r, int c) {   // slot position of element (r, c)
+    const int L = 2 * (r / 3) + c / 6, u = 6 * (r % 3) + c % 6;
+    return 16 * (u >> 1) + 2 * L + (u & 1);
+}
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+constexpr int BUF_SC1 = 16;   // buffer instruction cache policy: sc1
+// two doubles at p (16-byte aligned), one vector store (plain: the slabs are read by the next launch)
+__device__ __forceinline__ void st16(double* p, double a, double b) {
+    const dbl2 v = {a, b};
+    *reinterpret_cast<dbl2*>(p) = v;
+}
+
 __device__ __forceinline__ SE3 load_se3(const double* k) {
     SE3 T;
     T.q = Quat{k[0], k[1], k[2], k[3]};
@@ -457,7 +482,7 @@ __device__ __forceinline__ void smp_task(const DevProblem& P, const double* rows
         }
     }
     if (!LBA_INB(P, mslot, P.n_mslots, "mslab")) return;
-    double* m = P.mslab + (size_t)mslot * SM_STRIDE + 9 * CH;
+    double* m = P.mslab + (size_t)mslot * MS_PITCH + 9 * CH;
 #pragma unroll
     for (int q = 0; q < 9; ++q) m[q] = acc[q];
 }
@@ -498,12 +523,12 @@ __device__ void sample_expand(const DevProblem& P, const double* gps, const doub
         double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
         int k = P.ms0[smp] + q;
         for (; k + 3 * EXP_GROUPS < k1; k += 4 * EXP_GROUPS) {
-            v0 += m[(size_t)k * SM_STRIDE];
-            v1 += m[(size_t)(k + EXP_GROUPS) * SM_STRIDE];
-            v2 += m[(size_t)(k + 2 * EXP_GROUPS) * SM_STRIDE];
-            v3 += m[(size_t)(k + 3 * EXP_GROUPS) * SM_STRIDE];
+            v0 += m[(size_t)k * MS_PITCH];
+            v1 += m[(size_t)(k + EXP_GROUPS) * MS_PITCH];
+            v2 += m[(size_t)(k + 2 * EXP_GROUPS) * MS_PITCH];
+            v3 += m[(size_t)(k + 3 * EXP_GROUPS) * MS_PITCH];
         }
-        for (; k < k1; k += EXP_GROUPS) v0 += m[(size_t)k * SM_STRIDE];
+        for (; k < k1; k += EXP_GROUPS) v0 += m[(size_t)k * MS_PITCH];
         part[t] = (v0 + v1) + (v2 + v3);
     }
     if (tid < 6 * ncol) Nsh[tid] = nv;
@@ -548,7 +573,7 @@ __device__ void sample_expand(const DevProblem& P, const double* gps, const doub
             double v = 0.0;
 #pragma unroll
             for (int l = 0; l < 6; ++l) v += Nsh[6 * (12 * side + i) + l] * Msh[21 + l];
-            stv<WT>(P.gslab + (size_t)gl[side] * 12 + i, -v);
+            stv<WT>(P.gslab + (size_t)gl[side] * GS_PITCH + i, -v);
         }
     }
 }
@@ -606,7 +631,7 @@ __device__ void edge_item(const DevProblem& P, int sel, int idx, const int tid, 
             double v = 0.0;
             if (tid >= 3 && tid < 6)
                 for (int a = 0; a < 3; ++a) v += Ji[a * 3 + tid - 3] * We[a];
-            P.gslab[(size_t)gl[1] * 12 + tid] = -v;
+            P.gslab[(size_t)gl[1] * GS_PITCH + tid] = -v;
         }
         return;
     }
@@ -661,7 +686,7 @@ __device__ void edge_item(const DevProblem& P, int sel, int idx, const int tid, 
                 const double* A = side ? Jj : Ji;
                 double s = 0.0;
                 for (int k = 0; k < 12; ++k) s += A[k * 12 + i] * We[k];
-                P.gslab[(size_t)gl[side] * 12 + i] = -s;
+                P.gslab[(size_t)gl[side] * GS_PITCH + i] = -s;
             }
         }
     } else {
@@ -674,7 +699,7 @@ __device__ void edge_item(const DevProblem& P, int sel, int idx, const int tid, 
             return;
         double* H = P.hslab + (size_t)sl[2] * 144;
         for (int t = tid; t < 144; t += NT) H[t] = (t == 8 * 12 + 8) ? q22 : 0.0;
-        if (tid < 12) P.gslab[(size_t)gl[1] * 12 + tid] = (tid == 8) ? -q22 * ev : 0.0;
+        if (tid < 12) P.gslab[(size_t)gl[1] * GS_PITCH + tid] = (tid == 8) ? -q22 * ev : 0.0;
         if (tid == 0) P.chi_lin[P.n_tiles + idx] = ev * (q22 * ev);
     }
 }
@@ -962,22 +987,11 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
     //      needs no K padding, zero blocks or padded rows.  One task per (Schur entry, 3-row group,
     //      6-column half) keeps its 3 x 6 block of C in registers; every lane walks the tile's landmarks in
     //      the same order, so a wave's LDS reads of one step hit one landmark's pairs (broadcasts, few
-    //      bank conflicts) and D_m^-1 is one broadcast read.  The tile's nkf diagonal entries come first
-    //      with 6 tasks each: rows 6..11 x columns 0..5 of a diagonal block are strictly lower, never assembled
+    //      bank conflicts) and D_m^-1 is one broadcast read.  Every entry takes 8 consecutive lanes (a diagonal
+    //      entry's rows 6..11 x columns 0..5 too, though never assembled), which store its slot line by line (spos_of)
     const int nkf = P.tile_nkf[tile];
-    for (int task = tid; task < nsent * 8 - 2 * nkf; task += LS_THREADS) {
-        int q, rg, ch;
-        if (task < 6 * nkf) {
-            q = task / 6;
-            const int r6 = task - 6 * q;   // (rg, ch): (0,0) (0,1) (1,0) (1,1) (2,1) (3,1)
-            rg = r6 < 4 ? r6 >> 1 : r6 - 2;
-            ch = r6 < 4 ? r6 & 1 : 1;
-        } else {
-            const int t2 = task - 6 * nkf;
-            q = nkf + (t2 >> 3);
-            rg = (t2 >> 1) & 3;
-            ch = t2 & 1;
-        }
+    for (int task = tid; task < nsent * 8; task += LS_THREADS) {
+        const int q = task >> 3, rg = (task >> 1) & 3, ch = task & 1;
         const short* p1 = pidx + (scode[q] & 255) * PIDX_STRIDE;
         const short* p2 = pidx + (scode[q] >> 8) * PIDX_STRIDE;
         double acc[18];
@@ -1000,11 +1014,9 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
                                          fma(a[i * 3 + 1], b[j * 3 + 1], fma(a[i * 3], b[j * 3], acc[i * 6 + j])));
         }
         if (!LBA_INB(P, sslt[q], P.n_sslots, "sslab")) continue;
-        double* o = P.sslab + (size_t)sslt[q] * 144 + (3 * rg) * 12 + 6 * ch;
+        double* o = P.sslab + (size_t)sslt[q] * 144 + 2 * (task & 7);
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int j = 0; j < 6; ++j) o[i * 12 + j] = acc[i * 6 + j];
+        for (int k = 0; k < 9; ++k) st16(o + 16 * k, acc[2 * k], acc[2 * k + 1]);
     }
     LBA_TMARKI(P.tdbg_schur, tile, 2);
     // ---- phase 7: rhs partials: sum over the KF's landmarks of V(m,k) bl_m = W(m,k) u_m
@@ -1029,7 +1041,7 @@ __global__ __launch_bounds__(LS_THREADS, 3) void k_lin_schur(DevProblem P, int s
                 const double* u0 = Dl + m * DL_STRIDE + 8;
                 v0 = fma(w0[2], u0[2], fma(w0[1], u0[1], fma(w0[0], u0[0], v0)));
             }
-            if (LBA_INB(P, P.tkf_gslot[kf0 + l], P.n_gpslots, "gpslab")) P.gpslab[(size_t)P.tkf_gslot[kf0 + l] * 12 + r] = v0 + v1;
+            if (LBA_INB(P, P.tkf_gslot[kf0 + l], P.n_gpslots, "gpslab")) P.gpslab[(size_t)P.tkf_gslot[kf0 + l] * GS_PITCH + r] = v0 + v1;
         }
     }
     LBA_TMARKI(P.tdbg_schur, tile, 3);
@@ -1083,7 +1095,7 @@ __device__ void heavy_item(const DevProblem& P, int h, double lambda, int schur,
             vr[a] = v;
             g += v * HB[9 + a];
         }
-        stv<WT>(P.gpslab + (size_t)P.hp_gslot[hp0 + j] * 12 + r, g);
+        stv<WT>(P.gpslab + (size_t)P.hp_gslot[hp0 + j] * GS_PITCH + r, g);
     }
     __syncthreads();
     const int np2 = nhp * (nhp + 1) / 2, ss0 = P.hv_ss0[h];
@@ -1093,7 +1105,7 @@ __device__ void heavy_item(const DevProblem& P, int h, double lambda, int schur,
         while (rem >= nhp - a) { rem -= nhp - a; ++a; }
         const double* v = P.Vh + (size_t)(hp0 + a) * 36 + i * 3;
         const double* hb = Hpl + (size_t)(cp0 + a + rem) * 36 + jj * 3;
-        stv<WT>(P.sslab + (size_t)P.hv_sslot[ss0 + pp] * 144 + e, v[0] * hb[0] + v[1] * hb[1] + v[2] * hb[2]);
+        stv<WT>(P.sslab + (size_t)P.hv_sslot[ss0 + pp] * 144 + spos_of(i, jj), v[0] * hb[0] + v[1] * hb[1] + v[2] * hb[2]);
     }
 }
 
@@ -1174,17 +1186,18 @@ __device__ __forceinline__ void assemble_item(const DevProblem& P, int item, dou
     if (item < P.n_asm) {
         const int ub = P.asm_list[item];
         const int bi = P.ub_i[ub], bj = P.ub_j[ub];
-        const int e = tid % 144, g = tid / 144;
+        // lane (e, g): slot position e of the Schur partials, the same element's row-major position eh of the Hpp ones
+        const int e = tid % 144, g = tid / 144, rc = spos_rc(e), eh = 12 * (rc >> 4) + (rc & 15);
         double v;
         if constexpr (FUSED) {
             const double sv = slot_sum<RED_GROUPS, 144>(P.sslab, P.ss0[ub] + g, P.ss0[ub + 1], e);
             if (xs) xs[1] = __builtin_amdgcn_s_memrealtime() + (sv != sv);   // (diagnostics: the partials are in)
             if (wait) exp_wait(P, P.hs_prod, P.hs0[ub], P.hs0[ub + 1], epoch);
             if (xs) xs[2] = __builtin_amdgcn_s_memrealtime();
-            v = slot_sum<RED_GROUPS, 144>(P.hslab, P.hs0[ub] + g, P.hs0[ub + 1], e);
+            v = slot_sum<RED_GROUPS, 144>(P.hslab, P.hs0[ub] + g, P.hs0[ub + 1], eh);
             v -= sv;
         } else {
-            v = slot_sum<RED_GROUPS, 144>(P.hslab, P.hs0[ub] + g, P.hs0[ub + 1], e);
+            v = slot_sum<RED_GROUPS, 144>(P.hslab, P.hs0[ub] + g, P.hs0[ub + 1], eh);
             if (flags & ASM_SCHUR) v -= slot_sum<RED_GROUPS, 144>(P.sslab, P.ss0[ub] + g, P.ss0[ub + 1], e);
         }
         red[tid] = v;
@@ -1193,9 +1206,9 @@ __device__ __forceinline__ void assemble_item(const DevProblem& P, int item, dou
             double t = red[e];
 #pragma unroll
             for (int q = 1; q < RED_GROUPS; ++q) t += red[144 * q + e];   // (4 groups: ((a + b) + c) + d)
-            const int i = e / 12, j = e % 12;
+            const int i = rc >> 4, j = rc & 15;
             const int r = 12 * bj + j, c = 12 * bi + i;   // element (row r, col c) of S, r >= c in blocks
-            if (bi == bj && e % 13 == 0 && row_adds(P, r)) t += lambda;   // damping: added once over the ranks
+            if (bi == bj && i == j && row_adds(P, r)) t += lambda;   // damping: added once over the ranks
             if (flags & ASM_FULL) {                       // natural order, both triangles (dense np x np)
                 P.Sfull[(size_t)r * P.np + c] = t;
                 P.Sfull[(size_t)c * P.np + r] = t;
@@ -1221,12 +1234,12 @@ __device__ __forceinline__ void assemble_item(const DevProblem& P, int item, dou
         const int e = tid % 12, g = tid / 12;
         double v, w;
         if constexpr (FUSED) {
-            w = slot_sum<RG, 12>(P.gpslab, P.gps0[k] + g, P.gps0[k + 1], e);
+            w = slot_sum<RG, GS_PITCH>(P.gpslab, P.gps0[k] + g, P.gps0[k + 1], e);
             if (wait) exp_wait(P, P.gs_prod, P.gs0[k], P.gs0[k + 1], epoch);
-            v = slot_sum<RG, 12, true>(P.gslab, P.gs0[k] + g, P.gs0[k + 1], e);
+            v = slot_sum<RG, GS_PITCH, true>(P.gslab, P.gs0[k] + g, P.gs0[k + 1], e);
         } else {
-            v = slot_sum<RG, 12>(P.gslab, P.gs0[k] + g, P.gs0[k + 1], e);
-            w = (flags & ASM_SCHUR) ? slot_sum<RG, 12>(P.gpslab, P.gps0[k] + g, P.gps0[k + 1], e) : 0.0;
+            v = slot_sum<RG, GS_PITCH>(P.gslab, P.gs0[k] + g, P.gs0[k + 1], e);
+            w = (flags & ASM_SCHUR) ? slot_sum<RG, GS_PITCH>(P.gpslab, P.gps0[k] + g, P.gps0[k + 1], e) : 0.0;
         }
         red[tid] = v;
         __syncthreads();
@@ -1285,8 +1298,6 @@ __global__ __launch_bounds__(144 * RED_GROUPS) void k_exp_asm(DevProblem P, int 
     assemble_item<true>(P, blockIdx.x - P.n_smp, damping(P, lambda_arg), ASM_SCHUR, shm, !off, epoch, xs);
     if (xs) xs[3] = __builtin_amdgcn_s_memrealtime();
 }
-
-typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------------------------------------
 // Dense Cholesky S = L L^T of the reduced camera system in its factorisation order (panels permuted
@@ -1600,7 +1611,6 @@ __device__ __forceinline__ bool cf_wait_list(const CholFlow& a, int cnt, F flag,
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const double* p, int ld) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(8 * (31 * (long long)ld + CNB)), 0x00020000);
 }
-constexpr int BUF_SC1 = 16;   // buffer instruction cache policy: sc1
 __device__ __forceinline__ double lo_dbl(v4u q) { return __longlong_as_double(((long long)q.y << 32) | q.x); }
 __device__ __forceinline__ double hi_dbl(v4u q) { return __longlong_as_double(((long long)q.w << 32) | q.z); }
 // a 32 x 32 tile of handed-off data into registers (two 16-byte sc1 loads per thread), and from there to LDS
@@ -2871,6 +2881,10 @@ __global__ __launch_bounds__(256) void k_partials(DevProblem P) {
     trial_sums<256>(P, red, sa, sb, sc);
     if (threadIdx.x == 0) {
         P.red4[0] = sa; P.red4[1] = sb; P.red4[2] = sc; P.red4[3] = (double)(*P.info);
+        // the fault word's bits, one per slot: summed over the ranks, every rank sees every rank's fault and fails
+        // the call together (one rank alone throwing would leave the others in the next collective)
+        const int f = *P.fault;
+        for (int b = 0; b < RED_FAULT_BITS; ++b) P.red4[4 + b] = (double)((f >> b) & 1);
     }
 }
 
@@ -2908,9 +2922,11 @@ __device__ void finalize_body(const DevProblem& P, unsigned long long seq, int m
     LMCtl ctl;
     if (tid == 0 && mode != FIN_INITIAL && mode != FIN_HOST) ctl = *P.ctl;
     const int info = P.part_n > 0 ? 0 : *P.info;
-    const int fault = *P.fault;
+    int fault = *P.fault;
     if (P.part_n > 0) {   // partitioned: the all-reduced sums of every rank's k_partials
         sa = P.red4[0]; sb = P.red4[1]; sc = P.red4[2]; sinfo = P.red4[3];
+        fault = 0;
+        for (int b = 0; b < RED_FAULT_BITS; ++b) fault |= (P.red4[4 + b] != 0.0) << b;
     } else {
         trial_sums<NT>(P, red, sa, sb, sc);
         sinfo = (double)info;
@@ -3020,12 +3036,11 @@ void launch_lin_schur(const DevProblem& P, int sel, int gate, double lambda, int
     const int ne = (mode & LS_EDGES) ? P.n_prior + P.n_vel + P.n_eprior : 0;
     const dim3 g(P.n_tiles + ne);
     if (g.x == 0) return;
+    auto kern = P.f32res ? k_lin_schur<true> : k_lin_schur<false>;
     if (e0)   // the events carry the dispatch's own start / end timestamps
-        hipExtLaunchKernelGGL(P.f32res ? k_lin_schur<true> : k_lin_schur<false>, g, dim3(LS_THREADS), 0, s, e0, e1, 0, P,
-                              sel, gate, lambda, mode);
+        hipExtLaunchKernelGGL(kern, g, dim3(LS_THREADS), 0, s, e0, e1, 0, P, sel, gate, lambda, mode);
     else
-        hipLaunchKernelGGL(P.f32res ? k_lin_schur<true> : k_lin_schur<false>, g, dim3(LS_THREADS), 0, s, P, sel, gate,
-                           lambda, mode);
+        hipLaunchKernelGGL(kern, g, dim3(LS_THREADS), 0, s, P, sel, gate, lambda, mode);
 }
 void launch_expand(const DevProblem& P, int sel, int gate, double lambda, int schur, hipStream_t s) {
     const int n = P.n_smp + P.n_heavy;

@@ -236,6 +236,60 @@ def cpu_baseline(win, seconds):
                       f"(-O3, {threads} thread(s)), {dt:.1f} s"}
 
 
+def localgpba_map_calls(device, seconds=3.0, cpu_seconds=6.0, seed=7):
+    """The caller's real window (SURVEY.md 8(d), round-5 verdict item 6): Optimizer::LocalGPBA as LocalMapping calls it
+    (src/LocalMapping.cc:131, src/Optimizer.cc:713-1432) through the C++ host adapter lbamap_local_gpba -- the temporal
+    window of the newest keyframe (10 keyframes, or 25 with bLarge), its covisible / fixed keyframes and local points
+    from a synthetic 4-camera map, set-up, optimize(10), the outlier post-pass and the write-back, all in the call --
+    timed as calls/s, next to the same windows' LM on the CPU oracle (lbamap_build_window's flat window, optimize(10);
+    one thread, and the OpenMP build).  The map is updated by every call, as in the reference."""
+    from amc_lba import mapsnap as ms
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import orc
+    out = {}
+    snap = ms.make_map(n_kf=40, n_lm=8000, obs_per_lm=6, n_cam=4, seed=seed)
+    kf = 39
+    for large in (False, True):
+        m = ms.LocalGPBAMap(snap)
+        rc, res = m.local_gpba(kf, large=large, device=device)   # (first call: engine creation, JIT-free warm-up)
+        if rc != 0:
+            out["large" if large else "normal"] = {"error": f"rc {rc}: {m.error()}"}
+            continue
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds or n < 5:
+            rc, res = m.local_gpba(kf, large=large, device=device)
+            n += 1
+        dt = (time.perf_counter() - t0) / n
+        W, _, _, _ = m.build_window(kf, large=large)
+        t_b = time.perf_counter()
+        for _ in range(5):
+            m.build_window(kf, large=large)
+        t_build = (time.perf_counter() - t_b) / 5
+        m.close()
+        from amc_lba.abi import make_config
+        cfg = make_config(**W.cfg)
+        cpu = {}
+        for tag, lib_omp in (("1_thread", False), ("openmp", True)):
+            o = orc.Oracle(W, cfg=cfg, omp=lib_omp)
+            t_c, k = time.perf_counter(), 0
+            while time.perf_counter() - t_c < cpu_seconds / 2 or k < 1:
+                o = orc.Oracle(W, cfg=cfg, omp=lib_omp)
+                o.optimize(10)
+                k += 1
+            tc = (time.perf_counter() - t_c) / k
+            cpu[tag] = {"calls_per_s": 1.0 / (tc + t_build), "optimize_ms": tc * 1e3, "calls_timed": k}
+        cpu["openmp"]["threads"] = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+        out["large" if large else "normal"] = {
+            "keyframes": int(len(W.kfs)), "optimisable_kf": int((W.kfs["fixed"] == 0).sum()), "landmarks": int(len(W.lm)),
+            "observations": int(len(W.obs)), "gpu_calls_per_s": 1.0 / dt, "gpu_ms_per_call": dt * 1e3,
+            "calls_timed": n, "window_build_ms": t_build * 1e3, "cpu_oracle": cpu,
+            "speedup_vs_cpu_1_thread": cpu["1_thread"]["calls_per_s"] and (1.0 / dt) / cpu["1_thread"]["calls_per_s"]}
+    out["note"] = ("lbamap_local_gpba: window build + lba_set_problem + lba_optimize(10) + post-pass + write-back per "
+                   "call (synthetic 40-keyframe map, 8000 points, 4 cameras, newest keyframe); CPU: the same flat window "
+                   "through oracle/ (a C restatement of g2o's LM, not g2o itself) plus the adapter's window build")
+    return out
+
+
 def main():
     if os.environ.get("_BENCH_OMP_CHILD"):   # cpu_baseline_omp's child: the oracle alone, one JSON line
         ap = argparse.ArgumentParser()
@@ -593,11 +647,16 @@ def main():
             if set_problem_ms is not None:
                 calls["calls_per_s_with_set_problem"] = 1.0 / (args.window_iters / value + set_problem_ms * 1e-3)
             line["localgpba_calls"] = calls
+            if not args.no_cpu and args.config == "cfg1_local_50kf":
+                line["localgpba_map_calls"] = localgpba_map_calls(local)
         if not args.no_cpu and world == 1 and not gba:   # (the oracle's dense LDLT of S = 60000^2 is hours)
             line["cpu_baseline"] = cpu_baseline(win, args.cpu_seconds)
             # secondary: the OpenMP build of the oracle on this rank's share of the host's cores
+            # (OMP_NUM_THREADS: the GPU box's CPU share for one GPU, 16 on this pool; os.cpu_count() is the whole
+            # machine's, which the pool does not let one GPU's job occupy)
             omp_threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
             line["cpu_baseline_omp"] = cpu_baseline_omp(args.config, args.cpu_seconds, omp_threads)
+            line["cpu_baseline_omp"]["nproc"] = os.cpu_count()
             # speed-up against the best CPU baseline measured (both are ports of g2o's algorithm, oracle/,
             # not g2o itself: the reference's build is not available here)
             cands = [("port, 1 thread", line["cpu_baseline"].get("value"))]

@@ -293,6 +293,11 @@ int lba_linearize(lba_problem* p, double* residuals, double* H_pp, double* b, do
 /* One damped solve at lambda on the last linearisation: dx [np + 3*n_lm] (poses then
  * landmarks), BlockSolver::solve with setLambda/restoreDiagonal (block_solver.hpp:354-486). */
 int lba_solve_step(lba_problem* p, double lambda, double* dx);
+/* The trial state of the last lba_solve_step: the current estimate with that step applied by the device's update
+ * (VertexPoseVel / VertexSBAPointXYZ oplus, src/G2oTypes.cc:41-46, sparse_optimizer.cpp:422-435), i.e. what g2o's
+ * LM evaluates after push() + update() (optimization_algorithm_levenberg.cpp:94-103); the current estimate is not
+ * changed.  Same layout as lba_get_state. */
+int lba_trial_state(lba_problem* p, lba_kf* kf_out, double* lm_out);
 /* Diagnostics: the host preprocessing of lba_set_problem alone (device order, pairs, tiles, slabs; no device,
  * no GPU needed) on the given window; phase_ms: wall ms of the order/pairs, tiles and slots/state phases;
  * counts: device landmarks, pose blocks, pose dimension, tiles, a 32-bit fingerprint of the tiling and slab
@@ -310,6 +315,11 @@ int lba_debug_pool_stress(int32_t passes, int32_t max_pieces);
  * included) evaluated on `device` for n records in[13 n] = {xi[6], q[4] (x,y,z,w), t[3]}: out[85 n] =
  * {exp(xi) q[4] t[3], log(q, t)[6], Jr(xi)[36], Jr^-1(xi)[36]} (row-major). */
 int lba_debug_lie(int32_t device, int32_t n, const double* in, double* out);
+/* Diagnostics: set the problem's device fault word to `code` (1 factorisation, 2 assembly, 4 trial evaluation:
+ * the waits of one launch that gave up), as a bounded in-launch wait does when it times out.  The next call that
+ * reads the word (lba_optimize, lba_linearize, lba_solve_step, lba_eval) fails with LBA_E_TIMEOUT and clears it,
+ * so the failure path can be tested without a hang.  No LM work. */
+int lba_debug_inject_fault(lba_problem* p, int32_t code);
 /* How the reduced camera system is solved (after lba_set_problem), at the granularity of panels of
  * CHOL_NB = 32 rows: out[0] panels of the loop-closure tail (rows that reach back to the first panels,
  * ordered last), out[1] panels, out[2] stored 32 x 32 tiles of the factor L (fill-in included), out[3] 1

@@ -1568,6 +1568,21 @@ void orc_get_state(const orc_problem* p, lba_kf* kfs, double* lm_xyz) {
     if (lm_xyz) memcpy(lm_xyz, p->lm, sizeof(double) * 3 * p->n_lm);
 }
 
+/* Test hooks for a caller-driven LM (tests/test_gpu_configs.py: config 4 trial by trial): set the estimates (the
+ * inverse of orc_get_state; time, bf and fixed flags stay the set-up's), and apply a step dx [np + 3 nl] to them with
+ * SparseOptimizer::update's oplus (apply_update above, sparse_optimizer.cpp:422-435). */
+void orc_set_state(orc_problem* p, const lba_kf* kfs, const double* lm_xyz) {
+    if (kfs)
+        for (int i = 0; i < p->n_kf; ++i) {
+            kf_t* f = &p->kf[i];
+            f->Twb.q.x = kfs[i].q[0]; f->Twb.q.y = kfs[i].q[1]; f->Twb.q.z = kfs[i].q[2]; f->Twb.q.w = kfs[i].q[3];
+            memcpy(f->Twb.t, kfs[i].t, sizeof(double) * 3);
+            memcpy(f->vel, kfs[i].vel, sizeof(double) * 6);
+        }
+    if (lm_xyz) memcpy(p->lm, lm_xyz, sizeof(double) * 3 * p->n_lm);
+}
+void orc_apply_step(orc_problem* p, const double* dx) { apply_update(p, dx); }
+
 void orc_get_cams(const orc_problem* p, lba_cam* cams) {   /* cams holds the set-up cameras; Tbc updated */
     for (int c = 0; c < p->n_cam; ++c) {
         const se3* T = &p->cam[c].Tbc;

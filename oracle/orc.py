@@ -61,6 +61,10 @@ def _bind(L):
     L.orc_normal_residual.restype = None
     L.orc_optimize.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(LbaStats)]
     L.orc_get_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _dp]
+    L.orc_set_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _dp]
+    L.orc_set_state.restype = None
+    L.orc_apply_step.argtypes = [ctypes.c_void_p, _dp]
+    L.orc_apply_step.restype = None
     L.orc_get_cams.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     L.orc_depth_ok.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     L.orc_last_obs_chi2.argtypes = [ctypes.c_void_p, _dp]
@@ -155,6 +159,18 @@ class Oracle:
         lm = np.zeros((self.n_lm, 3))
         self._L.orc_get_state(self.h, ptr(kfs), _d(lm))
         return kfs, lm
+
+    def set_state(self, kfs, lm):
+        """Overwrite the estimates (keyframe q / t / velocity, landmarks); a caller-driven LM's linearisation point."""
+        kfs = np.ascontiguousarray(kfs)
+        lm = np.ascontiguousarray(lm, float)
+        self._L.orc_set_state(self.h, ptr(kfs), _d(lm))
+
+    def apply_step(self, dx):
+        """x <- x (+) dx (SparseOptimizer::update's oplus) for a step [pose_dim + lm_dim]."""
+        dx = np.ascontiguousarray(dx, float)
+        assert dx.shape == (self.pose_dim + self.lm_dim,)
+        self._L.orc_apply_step(self.h, _d(dx))
 
     def last_obs_chi2(self):
         """chi2 of the last computed errors (after optimize: the last trial state), nothing recomputed."""

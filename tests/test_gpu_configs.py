@@ -194,3 +194,75 @@ def test_cfg4_f32_residual_subtree_split(cfg4):
         assert abs(st_r.chi2_final - st.chi2_final) <= 1e-7 * st.chi2_final
     assert _rel(kf_s["t"], kf["t"]) <= 1e-9
     assert _rel(lm_s, lm) <= 1e-9
+
+
+def _lm_trials(win, flags, iters, tol_r, tol_chi):
+    """Config 4's LM driven trial by trial (OptimizationAlgorithmLevenberg::solve, levenberg.cpp:61-169), the GPU
+    doing every linearisation, damped solve and update, the oracle checking each trial at the GPU's linearisation
+    point: the step through the normal residual of the oracle's block-sparse system, the GPU's trial state's chi2
+    against the oracle's chi2 of that same state, and the accept / reject decision taken from either chi2 (they
+    must agree).  Returns per trial (iteration, lambda, normal residual, chi2 rel. difference, rho, accepted)."""
+    p = Problem(win, early_stop=0, flags=flags)
+    o = orc.Oracle(win, omp=True)
+    lam, ni = win.cfg["lambda_init"], 2.0
+    max_trials = 10
+    kf, lm = p.state()
+    chi_cur, _, _ = p.eval()
+    log = []
+    for it in range(iters):
+        o.set_state(kf, lm)
+        chi_o, _, _ = o.errors()
+        _, b_o, _ = o.build_system(dense=False)
+        assert abs(chi_cur - chi_o) <= tol_chi * chi_o, (it, chi_cur, chi_o)
+        bmax = np.abs(b_o).max()
+        q = 0
+        while True:
+            ok, dx = p.solve_step(lam)                      # linearise at the current state, eliminate, solve, update
+            assert ok
+            r = np.abs(o.normal_residual(lam, dx)).max() / bmax
+            assert r <= tol_r, (it, q, r)
+            kf_t, lm_t = p.trial_state()                    # the device's x (+) dx
+            o.set_state(kf_t, lm_t)
+            chi_ot, _, _ = o.errors()                       # the oracle's chi2 of the GPU's trial state
+            p.set_state(kf_t, lm_t)
+            chi_t, _, _ = p.eval()                          # the GPU's own
+            dchi = abs(chi_t - chi_ot) / chi_ot
+            assert dchi <= tol_chi, (it, q, chi_t, chi_ot)
+            scale = float(dx @ (lam * dx + b_o)) + 1e-3     # computeScale (levenberg.cpp:187-194)
+            rho, rho_o = (chi_cur - chi_t) / scale, (chi_cur - chi_ot) / scale
+            acc = rho > 0 and np.isfinite(chi_t)
+            assert acc == (rho_o > 0 and np.isfinite(chi_ot)), (it, q, rho, rho_o)
+            log.append((it, lam, r, dchi, rho, acc))
+            if acc:
+                alpha = min(1.0 - (2 * rho - 1) ** 3, 2.0 / 3.0)
+                lam *= max(1.0 / 3.0, alpha)
+                ni = 2.0
+                chi_cur, kf, lm = chi_t, kf_t, lm_t
+            else:
+                lam *= ni
+                ni *= 2.0
+                p.set_state(kf, lm)                         # pop: back to the linearisation point
+                o.set_state(kf, lm)
+            q += 1
+            if rho >= 0 or q >= max_trials:
+                break
+    p.close()
+    for e in log:
+        print("cfg4 trial: it %d  lambda %.3e  normal residual %.2e  chi2 diff %.2e  rho %+.4e  %s"
+              % (e[0], e[1], e[2], e[3], e[4], "accept" if e[5] else "reject"))
+    return log
+
+
+def test_cfg4_lm_trials_match_oracle(cfg4):
+    """Config 4 (fp64) past its first step: five LM iterations, every trial's damped step within 1e-8 of the oracle's
+    block-sparse system, every trial state's chi2 the oracle's to 1e-9, every accept / reject decision the oracle's."""
+    log = _lm_trials(cfg4, 0, 5, 1e-8, 1e-9)
+    assert sum(1 for e in log if e[5]) == 5
+
+
+def test_cfg4_f32_residual_lm_trials_match_oracle(cfg4):
+    """The same under LBA_FLAG_F32_RESIDUAL: steps within 1e-4 of the oracle's fp64 system, the fp32-residual chi2
+    within 1e-5 of the oracle's fp64 chi2 of the same state, the decisions the oracle's."""
+    from amc_lba.abi import FLAG_F32_RESIDUAL
+    log = _lm_trials(cfg4, FLAG_F32_RESIDUAL, 5, 1e-4, 1e-5)
+    assert sum(1 for e in log if e[5]) == 5
