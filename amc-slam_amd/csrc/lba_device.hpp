@@ -373,7 +373,7 @@ void launch_cholesky_part(const DevProblem& P, int part, unsigned epoch, hipStre
 enum { FIN_NONE = -1, FIN_HOST = 0, FIN_QUEUED = 1, FIN_QUEUED_PUBLISH = 2, FIN_INITIAL = 3 };
 void launch_finalize(const DevProblem& P, unsigned long long seq, int mode, hipStream_t s);
 // zero n device ranges (pairs: address, 4-byte words) in one launch (lba_set_problem's fresh buffers)
-void launch_zero_ranges(const unsigned long long* ranges, int n, hipStream_t s);
+void launch_zero_ranges(const unsigned long long* ranges, int n, size_t words, hipStream_t s);
 // residual evaluation of a state, then (mode != FIN_NONE) the trial summary (k_finalize)
 void launch_eval(const DevProblem& P, int sel, int gate, unsigned long long seq, int mode, hipStream_t s);
 void launch_ctl_init(const DevProblem& P, const LMCtl& c, hipStream_t s);

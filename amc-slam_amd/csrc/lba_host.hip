@@ -2104,9 +2104,11 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
 void flush_zero_ranges(lba_problem* p) {
     if (p->zero_list.empty()) return;
     const int n = (int)(p->zero_list.size() / 2);
+    size_t words = 0;
+    for (int k = 0; k < n; ++k) words += p->zero_list[2 * k + 1];
     const unsigned long long* d = dupload(p, p->zero_list);
     flush_uploads(p);
-    launch_zero_ranges(d, n, p->stream);
+    launch_zero_ranges(d, n, words, p->stream);
     HIPCHK(hipGetLastError());
     p->zero_list.clear();
 }

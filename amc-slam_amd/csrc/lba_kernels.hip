@@ -1175,9 +1175,10 @@ __device__ __forceinline__ void exp_wait(const DevProblem& P, const int* prod_of
 // FUSED (k_exp_asm): the Hpp / b_p partials come from expansion workgroups of the same launch, so the Schur
 // partials (an earlier launch's) are summed first, then the block waits for its samples (wait: the launch is not
 // gated off) and sums theirs -- the same operations in the same order as k_assemble, so S / bS are bitwise its.
-// The hslab slots of one block fill whole 128-byte lines of their own (1152 B each) and nothing reads them
-// before the wait, so plain loads see the write-through stores; gslab slots (96 B) share lines across pose
-// blocks, so they are loaded sc1.
+// The hand-off is MI355X_MICROARCH.md's sc1 form: the expansions store every Hpp / b_p piece write-through, drain
+// and set their flag; the blocks poll the flags and load every piece with sc1 loads (hslab and gslab slots fill
+// whole cache lines of their own).  An agent-scope acquire after the wait instead of the sc1 loads (here and in
+// k_update's upd_wait) cost 1.5-11 us per LM iteration (profiles/r7j_ab_acquire_rejected.txt).
 template <bool FUSED>
 __device__ __forceinline__ void assemble_item(const DevProblem& P, int item, double lambda, int flags, double* red, bool wait,
                                               unsigned epoch, unsigned long long* xs = nullptr) {
@@ -1194,7 +1195,7 @@ __device__ __forceinline__ void assemble_item(const DevProblem& P, int item, dou
             if (xs) xs[1] = __builtin_amdgcn_s_memrealtime() + (sv != sv);   // (diagnostics: the partials are in)
             if (wait) exp_wait(P, P.hs_prod, P.hs0[ub], P.hs0[ub + 1], epoch);
             if (xs) xs[2] = __builtin_amdgcn_s_memrealtime();
-            v = slot_sum<RED_GROUPS, 144>(P.hslab, P.hs0[ub] + g, P.hs0[ub + 1], eh);
+            v = slot_sum<RED_GROUPS, 144, true>(P.hslab, P.hs0[ub] + g, P.hs0[ub + 1], eh);
             v -= sv;
         } else {
             v = slot_sum<RED_GROUPS, 144>(P.hslab, P.hs0[ub] + g, P.hs0[ub + 1], eh);
@@ -2443,10 +2444,14 @@ __device__ __forceinline__ void upd_publish(const DevProblem& P, int self, unsig
 // The tile's observations at the trial state (k_eval's tile item: the same per-observation arithmetic and the same
 // reduction tree, so chi_eval / ob_chi2 are bitwise k_eval's): poses from the trial samples, landmarks from ltr
 // (this workgroup's back-substitution).  The samples are written in this launch, write-through, by other
-// workgroups; they are read with plain loads: no cache of this launch can hold an older copy (the caches are
-// invalidated at the launch's start and nothing reads the trial samples before the producers report), and
-// sc1 loads of these few hundred hot records from every tile cost more than the whole k_eval launch (+12 us).  Everything but the poses is loaded before
-// the wait for the samples (upd_wait_samples), so after it the tile is one round of loads from done.
+// workgroups; they are read with plain loads, which is safe without an acquire because no line holding a trial
+// pose is read in this launch before its producer's flag: the caches start the launch invalidated, a tile reads only
+// the first 96 bytes (Rwb, twb) of the records it waited for, and the bytes a pose's line shares with the previous
+// record are that record's Jacobian factor, which nothing reads in this launch.  The acquire fence the consumer
+// form would otherwise need cost 1.5-11 us per LM iteration (profiles/r7j_ab_acquire_rejected.txt), and sc1 loads
+// of these few hundred hot records from every tile more than the whole k_eval launch (+12 us).  Everything but
+// the poses is loaded before the wait for the samples (upd_wait_samples), so after it the tile is one round of
+// loads from done.
 struct TrialObs {
     ObsIn in;
     int o, meta;
@@ -2964,17 +2969,25 @@ __global__ __launch_bounds__(256) void k_finalize(DevProblem P, unsigned long lo
     finalize_body<256>(P, seq, mode, red);
 }
 
-// lba_set_problem's zero ranges (pairs: address, 4-byte words), grid-stride over every range with vector stores
+// lba_set_problem's zero ranges (pairs: address, 4-byte words), grid-stride over every range: the 16-byte-aligned body
+// of a range with 16-byte stores, its ragged head and tail with 4-byte ones
 __global__ __launch_bounds__(256) void k_zero_ranges(const unsigned long long* __restrict__ r, int n) {
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const size_t stride = (size_t)gridDim.x * blockDim.x, t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (int k = 0; k < n; ++k) {
         unsigned* d = reinterpret_cast<unsigned*>(r[2 * k]);
         const size_t words = r[2 * k + 1];
-        for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) d[i] = 0u;
+        const size_t head = min((size_t)(((16 - (r[2 * k] & 15)) & 15) / 4), words);   // words before a 16-byte boundary
+        const size_t nq = (words - head) / 4;
+        uint4* q = reinterpret_cast<uint4*>(d + head);
+        for (size_t i = t0; i < nq; i += stride) q[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (size_t i = t0; i < head; i += stride) d[i] = 0u;
+        for (size_t i = head + 4 * nq + t0; i < words; i += stride) d[i] = 0u;
     }
 }
-void launch_zero_ranges(const unsigned long long* ranges, int n, hipStream_t s) {
-    if (n > 0) hipLaunchKernelGGL(k_zero_ranges, dim3(256), dim3(256), 0, s, ranges, n);
+// words: the ranges' total, which sizes the grid (one 16-byte store per thread and pass, at most 2048 workgroups)
+void launch_zero_ranges(const unsigned long long* ranges, int n, size_t words, hipStream_t s) {
+    const size_t blocks = std::min<size_t>(2048, std::max<size_t>(1, (words / 4 + 255) / 256));
+    if (n > 0) hipLaunchKernelGGL(k_zero_ranges, dim3((unsigned)blocks), dim3(256), 0, s, ranges, n);
 }
 
 __global__ void k_ctl_init(DevProblem P, LMCtl c) {

@@ -1440,6 +1440,41 @@ void orc_normal_residual(const orc_problem* p, double lambda, const double* dx, 
     }
 }
 
+/* The same over |H + lambda I| |dx| + |b| (d): the componentwise (Oettli-Prager) backward error of the step is
+ * max_i |r_i| / d_i, which a backward-stable solve keeps near n eps however ill-conditioned the system is. */
+void orc_normal_residual_abs(const orc_problem* p, double lambda, const double* dx, double* d) {
+    const int n = p->np, nlb = p->n_lm_blocks;
+    for (int i = 0; i < n + p->nl; ++i) d[i] = fabs(p->b[i]);
+    for (int hi = 0; hi < p->n_pose_blocks; ++hi)
+        for (int k = p->hpp_rowptr[hi]; k < p->hpp_rowptr[hi + 1]; ++k) {
+            const int hj = p->hpp_col[k], di = p->pdim[hi], dj = p->pdim[hj], oi = p->poff[hi], oj = p->poff[hj];
+            const double* B = p->hpp_blk + (size_t)144 * k;
+            for (int a = 0; a < di; ++a)
+                for (int c = 0; c < dj; ++c) {
+                    const double v = fabs(B[a * dj + c]);
+                    if (hi == hj && c < a) continue;
+                    if (hi == hj && c == a) { d[oi + a] += fabs(B[a * dj + c] + lambda) * fabs(dx[oi + a]); continue; }
+                    d[oi + a] += v * fabs(dx[oj + c]);
+                    d[oj + c] += v * fabs(dx[oi + a]);
+                }
+        }
+    for (int l = 0; l < nlb; ++l) {
+        const double* xl = dx + n + 3 * l;
+        double* dl = d + n + 3 * l;
+        for (int a = 0; a < 3; ++a)
+            for (int e = 0; e < 3; ++e) dl[a] += fabs(p->Hll[9 * l + 3 * a + e] + (a == e ? lambda : 0.0)) * fabs(xl[e]);
+        for (int k = p->hpl_start[l]; k < p->hpl_start[l + 1]; ++k) {
+            const int i1 = p->hpl_pose[k];
+            const double* B = p->hpl_blk + 36 * k;
+            for (int a = 0; a < p->pdim[i1]; ++a)
+                for (int e = 0; e < 3; ++e) {
+                    d[p->poff[i1] + a] += fabs(B[a * 3 + e]) * fabs(xl[e]);
+                    dl[e] += fabs(B[a * 3 + e]) * fabs(dx[p->poff[i1] + a]);
+                }
+        }
+    }
+}
+
 /* ------------------------------------------------------------------ LM */
 static void push_state(orc_problem* p) {
     memcpy(p->kf_bak, p->kf, sizeof(kf_t) * p->n_kf);

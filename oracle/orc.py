@@ -59,6 +59,8 @@ def _bind(L):
     L.orc_solve.argtypes = [ctypes.c_void_p, ctypes.c_double, _dp]
     L.orc_normal_residual.argtypes = [ctypes.c_void_p, ctypes.c_double, _dp, _dp]
     L.orc_normal_residual.restype = None
+    L.orc_normal_residual_abs.argtypes = [ctypes.c_void_p, ctypes.c_double, _dp, _dp]
+    L.orc_normal_residual_abs.restype = None
     L.orc_optimize.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(LbaStats)]
     L.orc_get_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _dp]
     L.orc_set_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _dp]
@@ -142,6 +144,25 @@ class Oracle:
         r = np.zeros(self.pose_dim + self.lm_dim)
         self._L.orc_normal_residual(self.h, lam, _d(dx), _d(r))
         return r
+
+    def backward_error(self, lam, dx):
+        """Backward errors of a step on the last build_system, with r = (H + lam I) dx - b and A = H + lam I:
+        normwise |r|_inf / (|A|_inf |dx|_inf + |b|_inf) (near n eps for a backward-stable solve at any conditioning)
+        and componentwise max_i |r_i| / (|A| |dx| + |b|)_i (Oettli-Prager; the Schur-complement solve does not bound
+        it).  Returns (normwise, componentwise, r)."""
+        dx = np.ascontiguousarray(dx, float)
+        n = self.pose_dim + self.lm_dim
+        d = np.zeros(n)
+        self._L.orc_normal_residual_abs(self.h, lam, _d(dx), _d(d))
+        r = self.normal_residual(lam, dx)
+        ones = np.ones(n)
+        rows = np.zeros(n)
+        self._L.orc_normal_residual_abs(self.h, lam, _d(ones), _d(rows))
+        absb = np.abs(self.normal_residual(lam, np.zeros(n)))   # |b| (r at dx = 0 is -b)
+        a_inf = float(np.max(rows - absb))                       # max row sum of |A|
+        eta = float(np.abs(r).max() / (a_inf * np.abs(dx).max() + absb.max()))
+        omega = float(np.max(np.abs(r) / np.maximum(d, 1e-300)))
+        return eta, omega, r
 
     def optimize(self, iters):
         st = LbaStats()

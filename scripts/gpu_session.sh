@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-5 GPU session driver: every GPU step under its own time limit, chained so the first failure ends it.
-#   gpurun -- 'bash scripts/gpu_r5.sh TAG STEP...'
+# GPU session driver: every GPU step under its own time limit, chained so the first failure ends it.
+#   gpurun -- 'bash scripts/gpu_session.sh TAG STEP...'
 # steps: list (rocprofv3 -L), bench (200-step config-1 line), drv (driver-shaped 20-step bench with CPU baseline),
 #        tests (whole -m gpu suite), quick (parity subset), prof (kernel-trace stats), phases (in-kernel stamps)
 set -u
