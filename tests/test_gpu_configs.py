@@ -258,12 +258,13 @@ def _lm_trials(win, flags, iters, tol_w, tol_chi):
 
 
 def test_cfg4_lm_trials_match_oracle(cfg4):
-    """Config 4 (fp64) past its first step: five LM iterations; at every trial the damped step's normwise backward
-    error on the oracle's block-sparse system <= 1e-12 (and the first step's |r| / |b| <= 1e-8, as in
-    test_cfg4_full_size_single_gpu), the trial state's chi2 the oracle's to 1e-9, the decision the oracle's."""
-    log = _lm_trials(cfg4, 0, 5, 1e-12, 1e-9)
+    """Config 4 (fp64) past its first step: ten LM iterations (the bench's window, where the LM also rejects trials);
+    at every trial the damped step's normwise backward error on the oracle's block-sparse system <= 1e-12 (and the
+    first step's |r| / |b| <= 1e-8, as in test_cfg4_full_size_single_gpu), the trial state's chi2 the oracle's to
+    1e-9, the accept / reject decision the oracle's."""
+    log = _lm_trials(cfg4, 0, 10, 1e-12, 1e-9)
     assert log[0][3] <= 1e-8
-    assert sum(1 for e in log if e[6]) == 5
+    assert sum(1 for e in log if e[6]) >= 9
 
 
 def test_cfg4_f32_residual_lm_trials_match_oracle(cfg4):
