@@ -236,57 +236,71 @@ def cpu_baseline(win, seconds):
                       f"(-O3, {threads} thread(s)), {dt:.1f} s"}
 
 
-def localgpba_map_calls(device, seconds=3.0, cpu_seconds=6.0, seed=7):
+def localgpba_map_calls(device, passes=3, seed=7):
     """The caller's real window (SURVEY.md 8(d), round-5 verdict item 6): Optimizer::LocalGPBA as LocalMapping calls it
-    (src/LocalMapping.cc:131, src/Optimizer.cc:713-1432) through the C++ host adapter lbamap_local_gpba -- the temporal
-    window of the newest keyframe (10 keyframes, or 25 with bLarge), its covisible / fixed keyframes and local points
-    from a synthetic 4-camera map, set-up, optimize(10), the outlier post-pass and the write-back, all in the call --
-    timed as calls/s, next to the same windows' LM on the CPU oracle (lbamap_build_window's flat window, optimize(10);
-    one thread, and the OpenMP build).  The map is updated by every call, as in the reference."""
+    (src/LocalMapping.cc:131, once per new keyframe; src/Optimizer.cc:713-1432) through the C++ host adapter
+    lbamap_local_gpba -- the temporal window of the keyframe (10 keyframes, or 25 with bLarge), its covisible / fixed
+    keyframes and local points, set-up, optimize(10), the outlier post-pass and the write-back, all in the call -- on a
+    synthetic 40-keyframe, 4-camera map, called for keyframes 20..39 in order as the mapping thread would (every call
+    updates the map), `passes` times from a fresh map (the first call of a map creates its engine and is not timed).
+    Beside it the same windows' LM on the CPU oracle (lbamap_build_window's flat window from a fresh map, then
+    optimize(10); one thread, and the OpenMP build) on every fifth of those windows (the oracle takes seconds per
+    window).  The CPU rate counts the LM only (the adapter's window build, C++ in both, is reported beside it: through
+    Python here it is an upper bound)."""
     from amc_lba import mapsnap as ms
+    from amc_lba.abi import make_config
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import orc
-    out = {}
     snap = ms.make_map(n_kf=40, n_lm=8000, obs_per_lm=6, n_cam=4, seed=seed)
-    kf = 39
+    kfs = list(range(20, 40))
+    out = {}
     for large in (False, True):
+        times, bad = [], 0
+        for _ in range(passes):
+            m = ms.LocalGPBAMap(snap)
+            for i, kf in enumerate(kfs):
+                t = time.perf_counter()
+                rc, _ = m.local_gpba(kf, large=large, device=device)
+                dt = time.perf_counter() - t
+                bad += rc != 0
+                if i > 0:
+                    times.append(dt)
+            m.close()
         m = ms.LocalGPBAMap(snap)
-        rc, res = m.local_gpba(kf, large=large, device=device)   # (first call: engine creation, JIT-free warm-up)
-        if rc != 0:
-            out["large" if large else "normal"] = {"error": f"rc {rc}: {m.error()}"}
-            continue
-        n, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < seconds or n < 5:
-            rc, res = m.local_gpba(kf, large=large, device=device)
-            n += 1
-        dt = (time.perf_counter() - t0) / n
-        W, _, _, _ = m.build_window(kf, large=large)
-        t_b = time.perf_counter()
-        for _ in range(5):
-            m.build_window(kf, large=large)
-        t_build = (time.perf_counter() - t_b) / 5
+        wins, t_build = [], 0.0
+        for kf in kfs:
+            t = time.perf_counter()
+            W, _, _, _ = m.build_window(kf, large=large)
+            t_build += time.perf_counter() - t
+            wins.append(W)
         m.close()
-        from amc_lba.abi import make_config
-        cfg = make_config(**W.cfg)
+        t_build /= len(kfs)
         cpu = {}
+        sample = wins[4::5]
         for tag, lib_omp in (("1_thread", False), ("openmp", True)):
-            o = orc.Oracle(W, cfg=cfg, omp=lib_omp)
-            t_c, k = time.perf_counter(), 0
-            while time.perf_counter() - t_c < cpu_seconds / 2 or k < 1:
-                o = orc.Oracle(W, cfg=cfg, omp=lib_omp)
+            t_opt = 0.0
+            for W in sample:
+                o = orc.Oracle(W, cfg=make_config(**W.cfg), omp=lib_omp)
+                t = time.perf_counter()
                 o.optimize(10)
-                k += 1
-            tc = (time.perf_counter() - t_c) / k
-            cpu[tag] = {"calls_per_s": 1.0 / (tc + t_build), "optimize_ms": tc * 1e3, "calls_timed": k}
+                t_opt += time.perf_counter() - t
+            t_opt /= len(sample)
+            cpu[tag] = {"calls_per_s": 1.0 / t_opt, "optimize_ms": t_opt * 1e3, "windows": len(sample)}
         cpu["openmp"]["threads"] = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+        g = float(np.mean(times))
         out["large" if large else "normal"] = {
-            "keyframes": int(len(W.kfs)), "optimisable_kf": int((W.kfs["fixed"] == 0).sum()), "landmarks": int(len(W.lm)),
-            "observations": int(len(W.obs)), "gpu_calls_per_s": 1.0 / dt, "gpu_ms_per_call": dt * 1e3,
-            "calls_timed": n, "window_build_ms": t_build * 1e3, "cpu_oracle": cpu,
-            "speedup_vs_cpu_1_thread": cpu["1_thread"]["calls_per_s"] and (1.0 / dt) / cpu["1_thread"]["calls_per_s"]}
-    out["note"] = ("lbamap_local_gpba: window build + lba_set_problem + lba_optimize(10) + post-pass + write-back per "
-                   "call (synthetic 40-keyframe map, 8000 points, 4 cameras, newest keyframe); CPU: the same flat window "
-                   "through oracle/ (a C restatement of g2o's LM, not g2o itself) plus the adapter's window build")
+            "window_keyframes_mean": float(np.mean([len(W.kfs) for W in wins])),
+            "optimisable_kf_mean": float(np.mean([int((W.kfs["fixed"] == 0).sum()) for W in wins])),
+            "landmarks_mean": float(np.mean([len(W.lm) for W in wins])),
+            "observations_mean": float(np.mean([len(W.obs) for W in wins])),
+            "gpu_calls_per_s": 1.0 / g, "gpu_ms_per_call_mean": g * 1e3,
+            "gpu_ms_per_call_median": float(np.median(times)) * 1e3, "calls_timed": len(times), "failed_calls": bad,
+            "window_build_ms_python": t_build * 1e3, "cpu_oracle": cpu,
+            "speedup_vs_cpu_1_thread": (1.0 / g) / cpu["1_thread"]["calls_per_s"]}
+    out["note"] = ("lbamap_local_gpba per call: window build + lba_set_problem + lba_optimize(10) + post-pass + "
+                   "write-back (synthetic 40-keyframe map, 8000 points, 4 cameras, keyframes 20..39 in order); CPU: "
+                   "optimize(10) of the same windows (every fifth) through oracle/ (a C restatement of g2o's LM, not "
+                   "g2o itself), the window build not counted")
     return out
 
 
