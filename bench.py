@@ -338,8 +338,10 @@ def main():
     if rc is not None:
         sys.exit(rc)
     if os.environ.get("_BENCH_RANK_PROBE"):   # (tests: a launched rank reports its environment, no GPU)
-        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
-                                                          "HSA_ENABLE_IPC_MODE_LEGACY")}), flush=True)
+        # (one write(2) of the whole line, under PIPE_BUF: the ranks share the pipe, and print's separate writes of
+        # the text and the newline could interleave with another rank's)
+        os.write(1, (json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                                  "HSA_ENABLE_IPC_MODE_LEGACY")}) + "\n").encode())
         return
 
     import torch
