@@ -281,6 +281,18 @@ class Problem:
         self._check(L.lba_set_problem(self.h, ptr(kfs), len(kfs), ptr(lm), len(lm), ptr(obs), len(obs), ptr(pri),
                                       len(pri), ptr(vel), len(vel), ptr(cams), len(cams)))
 
+    def set_window(self, win):
+        """lba_set_problem with another window on the same engine (its device buffers and plan cache reused), as the
+        mapping thread's one problem per thread does; unpartitioned problems only."""
+        if self.group is not None:
+            raise ValueError("set_window: partitioned problems are set up collectively")
+        keep = tuple(np.ascontiguousarray(a) for a in (win.kfs, win.lm, win.obs, win.priors, win.vel_kfs, win.cams))
+        kfs, lm, obs, pri, vel, cams = keep
+        self._check(lib().lba_set_problem(self.h, ptr(kfs), len(kfs), ptr(lm), len(lm), ptr(obs), len(obs), ptr(pri),
+                                          len(pri), ptr(vel), len(vel), ptr(cams), len(cams)))
+        self.win, self._keep = win, keep
+        self.n_obs, self.n_lm, self.n_kf = len(win.obs), len(win.lm), len(win.kfs)
+
     def _check(self, rc, created=True):
         if rc < 0:
             msg = lib().lba_last_error(self.h).decode() if created and self.h else "lba_create failed"

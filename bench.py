@@ -275,6 +275,20 @@ def localgpba_map_calls(device, passes=3, seed=7):
             wins.append(W)
         m.close()
         t_build /= len(kfs)
+        # the call's two engine parts on the same windows (one engine, as the adapter's): lba_set_problem and
+        # lba_optimize(10); the rest of a call is the adapter's C++ window build, post-pass and write-back
+        import amc_lba
+        p = amc_lba.Problem(wins[0], device=device)
+        p.optimize(10)
+        t_set, t_opt10 = [], []
+        for W in wins[1:]:
+            t = time.perf_counter()
+            p.set_window(W)
+            t_set.append(time.perf_counter() - t)
+            t = time.perf_counter()
+            p.optimize(10)
+            t_opt10.append(time.perf_counter() - t)
+        p.close()
         cpu = {}
         sample = wins[4::5]
         for tag, lib_omp in (("1_thread", False), ("openmp", True)):
@@ -295,6 +309,8 @@ def localgpba_map_calls(device, passes=3, seed=7):
             "observations_mean": float(np.mean([len(W.obs) for W in wins])),
             "gpu_calls_per_s": 1.0 / g, "gpu_ms_per_call_mean": g * 1e3,
             "gpu_ms_per_call_median": float(np.median(times)) * 1e3, "calls_timed": len(times), "failed_calls": bad,
+            "engine_set_problem_ms_median": float(np.median(t_set)) * 1e3,
+            "engine_optimize10_ms_median": float(np.median(t_opt10)) * 1e3,
             "window_build_ms_python": t_build * 1e3, "cpu_oracle": cpu,
             "speedup_vs_cpu_1_thread": (1.0 / g) / cpu["1_thread"]["calls_per_s"]}
     out["note"] = ("lbamap_local_gpba per call: window build + lba_set_problem + lba_optimize(10) + post-pass + "

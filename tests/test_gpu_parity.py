@@ -248,3 +248,24 @@ def test_mfma_f64_layout(tmp_path):
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", src, "-o", exe])
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_engine_reuse_across_windows_is_bitwise_fresh():
+    """One engine, lba_set_problem with windows of different shapes one after another (the mapping thread's one
+    problem per thread): each window's LM run equals a fresh engine's bitwise (no state of the
+    previous window -- buffers, cached dissection plan, LM controller -- leaks into the next)."""
+    names = ("gp_small", "global_mid", "mono_only", "gp_small")
+    p = Problem(_win(names[0]))
+    for i, name in enumerate(names):
+        if i:
+            p.set_window(_win(name))
+        n, st = p.optimize(10)
+        kfs, lm = p.state()
+        q = Problem(_win(name))
+        n2, st2 = q.optimize(10)
+        kfs2, lm2 = q.state()
+        q.close()
+        assert (n, st.trials) == (n2, st2.trials), name
+        assert st.chi2_final == st2.chi2_final, name
+        assert kfs.tobytes() == kfs2.tobytes() and lm.tobytes() == lm2.tobytes(), name
+    p.close()
