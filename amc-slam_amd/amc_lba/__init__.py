@@ -286,7 +286,12 @@ class Problem:
         mapping thread's one problem per thread does; unpartitioned problems only."""
         if self.group is not None:
             raise ValueError("set_window: partitioned problems are set up collectively")
-        keep = tuple(np.ascontiguousarray(a) for a in (win.kfs, win.lm, win.obs, win.priors, win.vel_kfs, win.cams))
+        kw = dict(win.cfg)
+        kw.setdefault("device", self.cfg.device)
+        cfg = make_config(**kw)   # the window's own configuration, as the adapter sets it per call (lba_set_config)
+        self._check(lib().lba_set_config(self.h, ctypes.byref(cfg)))
+        self.cfg = cfg
+        keep =tuple(np.ascontiguousarray(a) for a in (win.kfs, win.lm, win.obs, win.priors, win.vel_kfs, win.cams))
         kfs, lm, obs, pri, vel, cams = keep
         self._check(lib().lba_set_problem(self.h, ptr(kfs), len(kfs), ptr(lm), len(lm), ptr(obs), len(obs), ptr(pri),
                                           len(pri), ptr(vel), len(vel), ptr(cams), len(cams)))

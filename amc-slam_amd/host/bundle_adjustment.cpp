@@ -132,8 +132,8 @@ void Optimizer::BuildBundleAdjustmentWindow(const std::vector<MultiKeyFrame*>& v
             E.push_back(Pending{o, tag});
         };
         int nEdges = 0;
-        const auto observations = pMP->GetObservations();
-        const auto observationsGP = pMP->GetGPObservations();
+        const auto& observations = pMP->ObservationsRef();
+        const auto& observationsGP = pMP->GPObservationsRef();
         for (const auto& kvo : observations) {   // keyframe observations (:157-232)
             MultiKeyFrame* pKFi = kvo.first;
             if (pKFi->isBad() || pKFi->mnId > maxKFid) continue;

@@ -83,6 +83,8 @@ public:
     MultiKeyFrame* mPrevKF = nullptr;
     MultiKeyFrame* mNextKF = nullptr;
     unsigned long mnBALocalForKF = 0, mnBAFixedForKF = 0;
+    unsigned long mnBAVertexStamp = 0;            // adapter: the window build that made this KF vertex mnBAVertex
+    int mnBAVertex = -1;
     // global BA results held back while a loop is being corrected (include/KeyFrame.h:365-370)
     SE3f mTbwGBA;
     float mVwbGBA[6] = {0, 0, 0, 0, 0, 0};
@@ -138,6 +140,11 @@ public:
     void SetWorldPos(const Vec3f& p) { mWorldPos = p; }
     std::map<MultiKeyFrame*, std::vector<int>, KFLess> GetObservations() const { return mObservations; }
     std::multimap<MultiKeyFrame*, GPObs, KFLess> GetGPObservations() const { return mObservationsForGPBA; }
+    // the same containers by reference, for the window builds: the reference's accessors copy them under the
+    // point's mutex (Tracking may add observations meanwhile); this map is read and changed only by the thread that
+    // calls the adapter, so the builds read them in place (no map / multimap copy per point)
+    const std::map<MultiKeyFrame*, std::vector<int>, KFLess>& ObservationsRef() const { return mObservations; }
+    const std::multimap<MultiKeyFrame*, GPObs, KFLess>& GPObservationsRef() const { return mObservationsForGPBA; }
     std::vector<int> GetIndexInKeyFrame(MultiKeyFrame* pKF) const;
     void AddObservation(MultiKeyFrame* pKF, int idx);          // src/MapPoint.cc:196-229
     void EraseObservation(MultiKeyFrame* pKF, int c);           // src/MapPoint.cc:275-315

@@ -15,6 +15,7 @@
 #include "optimizer.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -65,7 +66,7 @@ void Optimizer::BuildLocalGPBAWindow(MultiKeyFrame* pKF, bool bLarge, LocalGPBAW
     // ---- points seen by the temporal window (:750-767)
     std::list<MapPoint*>& lLocalMapPoints = W->lLocalMapPoints;
     auto collect = [&](MultiKeyFrame* K) {
-        const std::vector<MapPoint*> vpMPs = K->GetMapPointMatches();
+        const std::vector<MapPoint*>& vpMPs = K->mvpMapPoints;   // GetMapPointMatches(), read in place
         for (MapPoint* pMP : vpMPs)
             if (pMP && !pMP->isBad() && pMP->mnBALocalForKF != id) {
                 lLocalMapPoints.push_back(pMP);
@@ -102,7 +103,7 @@ void Optimizer::BuildLocalGPBAWindow(MultiKeyFrame* pKF, bool bLarge, LocalGPBAW
     // ---- fixed KFs observing the local points, at most 50 (:814-835)
     const size_t maxFixKF = 50;
     for (MapPoint* pMP : lLocalMapPoints) {
-        const auto observations = pMP->GetObservations();
+        const auto& observations = pMP->ObservationsRef();
         for (const auto& kv : observations) {
             MultiKeyFrame* pKFi = kv.first;
             if (pKFi->mnBALocalForKF != id && pKFi->mnBAFixedForKF != id) {
@@ -124,14 +125,17 @@ void Optimizer::BuildLocalGPBAWindow(MultiKeyFrame* pKF, bool bLarge, LocalGPBAW
     for (MultiKeyFrame* K : W->lpOptVisKFs) kv.push_back({K, false});
     for (MultiKeyFrame* K : lFixedKeyFrames) kv.push_back({K, true});
     std::stable_sort(kv.begin(), kv.end(), [](const auto& a, const auto& b) { return a.first->mnId < b.first->mnId; });
-    std::unordered_map<const MultiKeyFrame*, int> kidx;
+    // a keyframe's vertex index is stamped on it with this build's number (no hash lookup per observation)
+    static std::atomic<unsigned long> builds{0};
+    const unsigned long stamp = ++builds;
     for (const auto& e : kv) {
-        if (kidx.count(e.first)) continue;   // g2o addVertex refuses a duplicate id; the first one stays
-        kidx[e.first] = (int)W->kfs.size();
+        if (e.first->mnBAVertexStamp == stamp) continue;   // g2o addVertex refuses a duplicate id; the first one stays
+        e.first->mnBAVertexStamp = stamp;
+        e.first->mnBAVertex = (int)W->kfs.size();
         W->kfs.push_back(make_kf(e.first, e.second));
         W->kf_ids.push_back((int64_t)e.first->mnId);
     }
-    auto vtx = [&](const MultiKeyFrame* K) { auto it = kidx.find(K); return it == kidx.end() ? -1 : it->second; };
+    auto vtx = [stamp](const MultiKeyFrame* K) { return K->mnBAVertexStamp == stamp ? K->mnBAVertex : -1; };
 
     // EdgeVelocity on every temporal KF (:866-871), EdgeGaussianPrior between neighbours (:894-906)
     for (int i = 0; i < N; ++i) W->vel_kfs.push_back(vtx(vpOptimizableKFs[i]));
@@ -167,6 +171,9 @@ void Optimizer::BuildLocalGPBAWindow(MultiKeyFrame* pKF, bool bLarge, LocalGPBAW
         W->mp_ids.push_back((int64_t)P->mnId);
     }
     W->cam_obs.assign(nCam, 0);
+    W->obs.reserve(8 * mps.size());
+    W->obs_tag.reserve(8 * mps.size());
+    W->rows.reserve(8 * mps.size());
     const float thHuberMono = std::sqrt(5.991);     // :975-978
     const float thHuberStereo = std::sqrt(7.815);
     auto add = [&](int tag, int kind, int ka, int kb, int lm, int cam, double t, double u, double v, double ur, float w,
@@ -180,28 +187,44 @@ void Optimizer::BuildLocalGPBAWindow(MultiKeyFrame* pKF, bool bLarge, LocalGPBAW
         W->rows.push_back(LocalGPBAWindow::Row{K, P, g, cam});
         W->n_edges[tag]++;
     };
+    // the GP segments of the loop below, in its order (i = N-1 .. 1): keyframe, its vertex, its next keyframe's
+    struct GPSeg { MultiKeyFrame* K; int a, b; };
+    std::vector<GPSeg> segs;
+    for (int i = (int)vpOptimizableKFs.size() - 1; i > 0; --i) {
+        MultiKeyFrame* pKFi = vpOptimizableKFs[i];
+        if (!pKFi->mNextKF) continue;
+        const int a = vtx(pKFi), b = vtx(pKFi->mNextKF);
+        if (b < 0) continue;
+        segs.push_back({pKFi, a, b});
+    }
+    std::vector<std::pair<int, const GPObs*>> gp_hits;
     for (size_t m = 0; m < mps.size(); ++m) {
         MapPoint* pMP = mps[m];
         const int l = lidx[m];
-        const auto observations = pMP->GetObservations();
-        const auto observationsGP = pMP->GetGPObservations();
+        const auto& observations = pMP->ObservationsRef();
+        const auto& observationsGP = pMP->GPObservationsRef();
 
-        // GP observations of non-keyframes between pKFi and pKFi->mNextKF (:1027-1101)
-        for (int i = (int)vpOptimizableKFs.size() - 1; i > 0; --i) {
-            MultiKeyFrame* pKFi = vpOptimizableKFs[i];
-            if (!pKFi->mNextKF) continue;
-            const int a = vtx(pKFi), b = vtx(pKFi->mNextKF);
-            if (b < 0) continue;
-            auto range = observationsGP.equal_range(pKFi);
-            for (auto it = range.first; it != range.second; ++it) {
-                const GPObs& g = it->second;
-                const float unc2 = cams[g.cam].uncertainty2();
-                const float invSigma2 = (*pKFi->mvInvLevelSigma2)[g.obs.octave] / unc2;
-                if (g.ur >= 0)
-                    add(1, LBA_STEREO_GP, a, b, l, g.cam, g.time, g.obs.x, g.obs.y, g.ur, invSigma2, pKFi, pMP, g);
-                else
-                    add(0, LBA_MONO_GP, a, b, l, g.cam, g.time, g.obs.x, g.obs.y, 0.0, invSigma2, pKFi, pMP, g);
-            }
+        // GP observations of non-keyframes between pKFi and pKFi->mNextKF (:1027-1101).  The reference takes
+        // equal_range(pKFi) for every segment i = N-1 .. 1; one pass over the point's entries, stably ordered by
+        // segment, adds the same edges in the same order (a multimap keeps equal keys in insertion order)
+        gp_hits.clear();
+        for (const auto& e : observationsGP)
+            for (size_t s = 0; s < segs.size(); ++s)
+                if (segs[s].K == e.first) {
+                    gp_hits.push_back({(int)s, &e.second});
+                    break;
+                }
+        std::stable_sort(gp_hits.begin(), gp_hits.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+        for (const auto& h : gp_hits) {
+            const GPSeg& sg = segs[h.first];
+            MultiKeyFrame* pKFi = sg.K;
+            const GPObs& g = *h.second;
+            const float unc2 = cams[g.cam].uncertainty2();
+            const float invSigma2 = (*pKFi->mvInvLevelSigma2)[g.obs.octave] / unc2;
+            if (g.ur >= 0)
+                add(1, LBA_STEREO_GP, sg.a, sg.b, l, g.cam, g.time, g.obs.x, g.obs.y, g.ur, invSigma2, pKFi, pMP, g);
+            else
+                add(0, LBA_MONO_GP, sg.a, sg.b, l, g.cam, g.time, g.obs.x, g.obs.y, 0.0, invSigma2, pKFi, pMP, g);
         }
 
         // keyframe observations (:1104-1206)

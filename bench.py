@@ -280,11 +280,12 @@ def localgpba_map_calls(device, passes=3, seed=7):
         import amc_lba
         p = amc_lba.Problem(wins[0], device=device)
         p.optimize(10)
-        t_set, t_opt10 = [], []
+        t_set, t_opt10, ph = [], [], []
         for W in wins[1:]:
             t = time.perf_counter()
             p.set_window(W)
             t_set.append(time.perf_counter() - t)
+            ph.append(p.setup_phases())
             t = time.perf_counter()
             p.optimize(10)
             t_opt10.append(time.perf_counter() - t)
@@ -311,6 +312,7 @@ def localgpba_map_calls(device, passes=3, seed=7):
             "gpu_ms_per_call_median": float(np.median(times)) * 1e3, "calls_timed": len(times), "failed_calls": bad,
             "engine_set_problem_ms_median": float(np.median(t_set)) * 1e3,
             "engine_optimize10_ms_median": float(np.median(t_opt10)) * 1e3,
+            "engine_set_problem_phases_ms_median": {k: float(np.median([d[k] for d in ph])) for k in ph[0]},
             "window_build_ms_python": t_build * 1e3, "cpu_oracle": cpu,
             "speedup_vs_cpu_1_thread": (1.0 / g) / cpu["1_thread"]["calls_per_s"]}
     out["note"] = ("lbamap_local_gpba per call: window build + lba_set_problem + lba_optimize(10) + post-pass + "
