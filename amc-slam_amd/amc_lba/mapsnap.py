@@ -333,7 +333,7 @@ class LbamapResult(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "status", "n_opt_kf", "n_vis_kf", "n_fixed_kf", "n_mp", "n_edges_mono_gp", "n_edges_stereo_gp", "n_edges_mono",
         "n_edges_stereo", "n_edges_mono_gp_kf", "n_erased_gp", "n_erased", "n_set_bad", "iterations")] + [
-        ("chi2_initial", ctypes.c_double), ("chi2_final", ctypes.c_double)]
+        ("chi2_initial", ctypes.c_double), ("chi2_final", ctypes.c_double), ("ms_phase", ctypes.c_double * 4)]
 
 
 class LbamapBAResult(ctypes.Structure):

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -278,10 +279,17 @@ void Optimizer::BuildLocalGPBAWindow(MultiKeyFrame* pKF, bool bLarge, LocalGPBAW
 int Optimizer::LocalGPBA(MultiKeyFrame* pKF, Map* pMap, const lbamap_options& opt, lba_problem* problem,
                          lbamap_result* out) {
     lbamap_result res{};
+    auto t_last = std::chrono::steady_clock::now();
+    auto lap = [&](int k) {   // res.ms_phase[k] += the wall time since the previous lap
+        const auto t = std::chrono::steady_clock::now();
+        res.ms_phase[k] += std::chrono::duration<double, std::milli>(t - t_last).count();
+        t_last = t;
+    };
     const bool bLarge = opt.large != 0;
     const unsigned long id = pKF->mnId;
     LocalGPBAWindow W;
     BuildLocalGPBAWindow(pKF, bLarge, &W);
+    lap(0);
     res.n_opt_kf = (int)W.vpOptimizableKFs.size();
     res.n_vis_kf = (int)W.lpOptVisKFs.size();
     res.n_fixed_kf = (int)W.lFixedKeyFrames.size();
@@ -300,8 +308,10 @@ int Optimizer::LocalGPBA(MultiKeyFrame* pKF, Map* pMap, const lbamap_options& op
         rc = lba_set_problem(problem, W.kfs.data(), (int)W.kfs.size(), W.lm.data(), (int)W.mp_ids.size(), W.obs.data(),
                              (int)W.obs.size(), W.priors.data(), (int)W.priors.size(), W.vel_kfs.data(),
                              (int)W.vel_kfs.size(), W.cams.data(), (int)W.cams.size());
+    lap(1);
     lba_stats st{};
     if (rc >= 0) rc = lba_optimize(problem, 10, nullptr, &st);   // opt_it1 = 10 (:1218)
+    lap(2);
     if (rc < 0) {
         res.status = rc;
         if (out) *out = res;
@@ -323,7 +333,9 @@ int Optimizer::LocalGPBA(MultiKeyFrame* pKF, Map* pMap, const lbamap_options& op
             rc = lba_set_problem(problem, kf_now.data(), (int)kf_now.size(), lm_now.data(), (int)W.mp_ids.size(),
                                  W.obs.data(), (int)W.obs.size(), W.priors.data(), (int)W.priors.size(),
                                  W.vel_kfs.data(), (int)W.vel_kfs.size(), W.cams.data(), (int)W.cams.size());
+        lap(1);
         if (rc >= 0) rc = lba_optimize(problem, opt_it2, nullptr, &st);
+        lap(2);
         if (rc < 0) {
             res.status = rc;
             if (out) *out = res;
@@ -438,6 +450,7 @@ int Optimizer::LocalGPBA(MultiKeyFrame* pKF, Map* pMap, const lbamap_options& op
     }
     pMap->IncreaseChangeIndex();
     (void)id;
+    lap(3);
     res.status = LBA_OK;
     if (out) *out = res;
     return LBA_OK;

@@ -255,16 +255,17 @@ def localgpba_map_calls(device, passes=3, seed=7):
     kfs = list(range(20, 40))
     out = {}
     for large in (False, True):
-        times, bad = [], 0
+        times, parts, bad = [], [], 0
         for _ in range(passes):
             m = ms.LocalGPBAMap(snap)
             for i, kf in enumerate(kfs):
                 t = time.perf_counter()
-                rc, _ = m.local_gpba(kf, large=large, device=device)
+                rc, res = m.local_gpba(kf, large=large, device=device)
                 dt = time.perf_counter() - t
                 bad += rc != 0
                 if i > 0:
                     times.append(dt)
+                    parts.append(list(res.ms_phase))
             m.close()
         m = ms.LocalGPBAMap(snap)
         wins, t_build = [], 0.0
@@ -310,6 +311,8 @@ def localgpba_map_calls(device, passes=3, seed=7):
             "observations_mean": float(np.mean([len(W.obs) for W in wins])),
             "gpu_calls_per_s": 1.0 / g, "gpu_ms_per_call_mean": g * 1e3,
             "gpu_ms_per_call_median": float(np.median(times)) * 1e3, "calls_timed": len(times), "failed_calls": bad,
+            "call_parts_ms_median": dict(zip(("window_build", "set_problem", "optimize", "post_pass_write_back"),
+                                             np.median(np.array(parts), axis=0).tolist())),
             "engine_set_problem_ms_median": float(np.median(t_set)) * 1e3,
             "engine_optimize10_ms_median": float(np.median(t_opt10)) * 1e3,
             "engine_set_problem_phases_ms_median": {k: float(np.median([d[k] for d in ph])) for k in ph[0]},

@@ -139,6 +139,10 @@ typedef struct lbamap_result {
     int32_t n_set_bad;                  /* map points that became bad while erasing */
     int32_t iterations;
     double  chi2_initial, chi2_final;   /* err, err_end (Optimizer.cc:1221-1253) */
+    double  ms_phase[4];                /* wall ms of the call's parts: window build (graph construction, :717-1208),
+                                           lba_set_problem, lba_optimize (both passes with bExtrinsic), outlier
+                                           post-pass + write-back (:1257-1431); the reference's LocalMapping keeps
+                                           such timers (vtime, src/LocalMapping.cc:129-135) */
 } lbamap_result;
 
 /* What BundleAdjustment / GlobalBundleAdjustemnt did (src/Optimizer.cc:53-367). */
