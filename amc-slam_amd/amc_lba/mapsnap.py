@@ -320,7 +320,8 @@ def make_map(n_kf=30, n_lm=3000, obs_per_lm=6, n_cam=4, n_gp_frames=1, gp_obs_fr
 
 # ------------------------------------------------------------------ ctypes binding
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-MAP_LIB_PATH = os.path.join(PKG_DIR, "lib", "libamc_lba_map.so")
+# AMC_LBA_MAP_LIB: another build of the adapter (A/B of two builds: scripts/cmp_map_libs.py)
+MAP_LIB_PATH = os.environ.get("AMC_LBA_MAP_LIB") or os.path.join(PKG_DIR, "lib", "libamc_lba_map.so")
 _lib = None
 
 
@@ -348,7 +349,8 @@ def map_lib():
         if not os.path.exists(MAP_LIB_PATH):
             raise RuntimeError(f"{MAP_LIB_PATH} not built: run python -c 'import __graft_entry__ as g; g.build()'")
         from . import check_fresh
-        check_fresh("map")
+        if not os.environ.get("AMC_LBA_MAP_LIB"):
+            check_fresh("map")
         L = ctypes.CDLL(MAP_LIB_PATH)
         vp = ctypes.c_void_p
         L.lbamap_load.argtypes = [ctypes.POINTER(vp), ctypes.c_char_p, ctypes.c_size_t]

@@ -193,7 +193,7 @@ void MapPoint::EraseGPObservation(MultiKeyFrame* pKF, const GPObs& o) {   // src
 }
 
 void MapPoint::SetBadFlag() {   // src/MapPoint.cc:356-386
-    auto obs = mObservations;
+    auto obs = std::move(mObservations);
     mbBad = true;
     mObservations.clear();
     for (auto& kv : obs)
@@ -204,7 +204,7 @@ void MapPoint::SetBadFlag() {   // src/MapPoint.cc:356-386
 
 void MapPoint::UpdateNormalAndDepth() {   // src/MapPoint.cc:611-686
     if (mbBad) return;
-    const auto observations = mObservations;
+    const auto& observations = mObservations;   // (the reference copies it under the point's mutex; read in place)
     MultiKeyFrame* pRefKF = mpRefKF;
     const Vec3f Pos = mWorldPos;
     if (observations.empty()) return;

@@ -170,6 +170,7 @@ void Optimizer::BuildLocalGPBAWindow(MultiKeyFrame* pKF, bool bLarge, LocalGPBAW
         const Vec3f X = P->GetWorldPos();
         W->lm.push_back((double)X.x); W->lm.push_back((double)X.y); W->lm.push_back((double)X.z);
         W->mp_ids.push_back((int64_t)P->mnId);
+        W->mp_vtx.push_back(P);
     }
     W->cam_obs.assign(nCam, 0);
     W->obs.reserve(8 * mps.size());
@@ -427,8 +428,8 @@ int Optimizer::LocalGPBA(MultiKeyFrame* pKF, Map* pMap, const lbamap_options& op
     };
     for (int i = (int)W.vpOptimizableKFs.size() - 1; i >= 0; --i) set_pose(W.vpOptimizableKFs[i]);
     for (MultiKeyFrame* K : W.lpOptVisKFs) set_pose(K);
-    for (size_t r = 0; r < W.mp_ids.size(); ++r) {
-        MapPoint* P = pMap->mp_by_id(W.mp_ids[r]);
+    for (size_t r = 0; r < W.mp_vtx.size(); ++r) {
+        MapPoint* P = W.mp_vtx[r];
         P->SetWorldPos(Vec3f{(float)lm_out[3 * r], (float)lm_out[3 * r + 1], (float)lm_out[3 * r + 2]});
     }
     for (MapPoint* P : W.lLocalMapPoints) P->UpdateNormalAndDepth();   // in lLocalMapPoints order (:1412-1416)

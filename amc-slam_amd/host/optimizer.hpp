@@ -26,6 +26,7 @@ struct LocalGPBAWindow {
     std::vector<int64_t> kf_ids;
     std::vector<double> lm;
     std::vector<int64_t> mp_ids;
+    std::vector<MapPoint*> mp_vtx;          // the point of each landmark vertex (mp_ids' order)
     std::vector<lba_obs> obs;
     std::vector<int32_t> obs_tag;           // 0 MonoGP, 1 StereoGP, 2 Mono, 3 Stereo, 4 MonoGP at KF time
     std::vector<lba_prior> priors;
