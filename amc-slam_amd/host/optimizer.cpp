@@ -65,7 +65,8 @@ void Optimizer::BuildLocalGPBAWindow(MultiKeyFrame* pKF, bool bLarge, LocalGPBAW
     int N = (int)vpOptimizableKFs.size();
 
     // ---- points seen by the temporal window (:750-767)
-    std::list<MapPoint*>& lLocalMapPoints = W->lLocalMapPoints;
+    std::vector<MapPoint*>& lLocalMapPoints = W->lLocalMapPoints;
+    lLocalMapPoints.reserve(4096);
     auto collect = [&](MultiKeyFrame* K) {
         const std::vector<MapPoint*>& vpMPs = K->mvpMapPoints;   // GetMapPointMatches(), read in place
         for (MapPoint* pMP : vpMPs)
@@ -77,7 +78,7 @@ void Optimizer::BuildLocalGPBAWindow(MultiKeyFrame* pKF, bool bLarge, LocalGPBAW
     for (int i = 0; i < N; ++i) collect(vpOptimizableKFs[i]);
 
     // ---- fixed keyframe: the previous KF of the window (:769-782)
-    std::list<MultiKeyFrame*>& lFixedKeyFrames = W->lFixedKeyFrames;
+    std::vector<MultiKeyFrame*>& lFixedKeyFrames = W->lFixedKeyFrames;
     if (vpOptimizableKFs.back()->mPrevKF) {
         lFixedKeyFrames.push_back(vpOptimizableKFs.back()->mPrevKF);
         vpOptimizableKFs.back()->mPrevKF->mnBAFixedForKF = id;
@@ -159,7 +160,7 @@ void Optimizer::BuildLocalGPBAWindow(MultiKeyFrame* pKF, bool bLarge, LocalGPBAW
     }
 
     // ---- point vertices and reprojection edges (:1012-1208)
-    std::vector<MapPoint*> mps(lLocalMapPoints.begin(), lLocalMapPoints.end());
+    const std::vector<MapPoint*>& mps = lLocalMapPoints;
     std::vector<int> mp_order(mps.size());
     for (size_t i = 0; i < mps.size(); ++i) mp_order[i] = (int)i;
     std::stable_sort(mp_order.begin(), mp_order.end(), [&](int a, int b) { return mps[a]->mnId < mps[b]->mnId; });

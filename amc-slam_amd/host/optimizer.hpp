@@ -19,8 +19,9 @@ namespace amc_slam {
 // the post-pass needs (the reference's vpEdgeKF* / vpMapPointEdge* / vpGPObs* vectors).
 struct LocalGPBAWindow {
     std::vector<MultiKeyFrame*> vpOptimizableKFs;
-    std::list<MultiKeyFrame*> lpOptVisKFs, lFixedKeyFrames;
-    std::list<MapPoint*> lLocalMapPoints;
+    // (the reference's std::lists, as vectors: the same appends and iteration order, no allocation per element)
+    std::vector<MultiKeyFrame*> lpOptVisKFs, lFixedKeyFrames;
+    std::vector<MapPoint*> lLocalMapPoints;
 
     std::vector<lba_kf> kfs;
     std::vector<int64_t> kf_ids;
