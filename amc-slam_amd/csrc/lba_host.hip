@@ -1049,41 +1049,29 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 if (dhx[o] == k) pair_rows.push_back((o - obase) | (2 << 16));
             }
         };
-        // regular tiles: the landmarks [0, n_reg) in SETUP_PIECES contiguous pieces, each tiled greedily on
-        // its own thread into piece-local lists (tiles never straddle a piece boundary, so the tiling is the
-        // same for any thread count), then concatenated with their offsets
+        // regular tiles: the landmarks [0, n_reg) in SETUP_PIECES contiguous pieces, each cut greedily into tiles
+        // on its own thread (tiles never straddle a piece boundary, so the tiling is the same for any thread
+        // count).  The tiles' lists depend only on their own landmarks: they are built in a second pass, in
+        // parallel over runs of consecutive tiles, and concatenated with their offsets.  (A window below 256
+        // landmarks per piece is one piece: its cut is serial, its lists -- most of the work -- are not.)
         struct TileOut {
             std::vector<int> t_obs0, t_nobs, t_lm0, t_nlm, t_pair0, t_npair, t_smp0, t_nsmp, t_sent0, t_nsent, t_kf0,
                 t_nkf, tkf_list, tsm_smp, tsm_rows, sent_l1, sent_l2, sent_k1, sent_k2, pair_rows, lm_rows;
         };
         const int n_pieces = n_reg >= 256 * SETUP_PIECES ? SETUP_PIECES : 1;
         const int obs_cap = TILE_OBS;
-        std::vector<TileOut> outs(n_pieces);
+        // pass 1, the cut: the first landmark of every tile, per piece
+        std::vector<std::vector<int>> cut(n_pieces);
         par_for(n_pieces, [&](int piece) {
-            TileOut& T = outs[piece];
             const int cap = obs_cap;
             const int d_end = (int)((long long)n_reg * (piece + 1) / n_pieces);
             int d = (int)((long long)n_reg * piece / n_pieces);
             // the tile's sample / KF sets grow by the landmark's new elements, found through membership
-            // marks (1: in the tile, 2: new for the landmark being tried); uni is sorted once the tile closes
+            // marks (1: in the tile, 2: new for the landmark being tried)
             std::vector<int> uni, usm, new_s, new_k;
             std::vector<char> kmark((size_t)std::max(n_pb, 1), 0), smark((size_t)std::max(n_smp, 1), 0);
-            std::vector<int> sloc_v((size_t)std::max(n_smp, 1), 0);   // sample -> its rank in the closed tile
-            int* sloc = sloc_v.data();
-            int srows[TILE_SMP + 1];
             uni.reserve(TILE_PAIRS + 8);
             usm.reserve(TILE_SMP + 8);
-            {   // capacity for the piece's share of the outputs (no regrowth while tiling)
-                const int no_p = lobs0[d_end] - lobs0[d], np_p = lm_pair0[d_end] - lm_pair0[d];
-                const int nt_est = no_p / 64 + 8;
-                T.pair_rows.reserve((size_t)np_p * 4 + 16);
-                T.lm_rows.reserve((size_t)no_p * 3 + 16);
-                T.tsm_smp.reserve((size_t)nt_est * TILE_SMP / 2);
-                T.tsm_rows.reserve((size_t)nt_est * TILE_SMP / 2);
-                T.sent_l1.reserve((size_t)nt_est * 48); T.sent_l2.reserve((size_t)nt_est * 48);
-                T.sent_k1.reserve((size_t)nt_est * 48); T.sent_k2.reserve((size_t)nt_est * 48);
-                T.tkf_list.reserve((size_t)nt_est * TILE_KF);
-            }
             while (d < d_end) {
                 int nobs = 0, rows = 0, npair = 0, nlmt = 0, nent = 0;
                 uni.clear();
@@ -1119,6 +1107,54 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 }
                 for (int v : usm) smark[v] = 0;
                 for (int k : uni) kmark[k] = 0;
+                cut[piece].push_back(d);
+                d = e;
+            }
+        });
+        std::vector<int> tl_d;   // tile t: landmarks [tl_d[t], tl_d[t + 1])
+        for (const auto& c : cut) tl_d.insert(tl_d.end(), c.begin(), c.end());
+        const int n_rt = (int)tl_d.size();
+        tl_d.push_back(n_reg);
+        // pass 2, the lists: n_runs runs of consecutive tiles
+        const int n_runs = std::min(SETUP_PIECES, n_rt);
+        auto run_t0 = [&](int r) { return (int)((long long)n_rt * r / n_runs); };
+        std::vector<TileOut> outs(n_runs);
+        par_for(n_runs, [&](int run) {
+            TileOut& T = outs[run];
+            const int ta = run_t0(run), tb = run_t0(run + 1);
+            std::vector<int> uni, usm;
+            std::vector<char> kmark((size_t)std::max(n_pb, 1), 0), smark((size_t)std::max(n_smp, 1), 0);
+            std::vector<int> sloc_v((size_t)std::max(n_smp, 1), 0);   // sample -> its rank in the tile
+            int* sloc = sloc_v.data();
+            int srows[TILE_SMP + 1];
+            uni.reserve(TILE_PAIRS + 8);
+            usm.reserve(TILE_SMP + 8);
+            {   // capacity for the run's share of the outputs (no regrowth while building)
+                const int la = tl_d[ta], lb = tl_d[tb];
+                const int no_p = lobs0[lb] - lobs0[la], np_p = lm_pair0[lb] - lm_pair0[la];
+                const int nt_est = tb - ta + 1;
+                T.pair_rows.reserve((size_t)np_p * 4 + 16);
+                T.lm_rows.reserve((size_t)no_p * 3 + 16);
+                T.tsm_smp.reserve((size_t)nt_est * TILE_SMP / 2);
+                T.tsm_rows.reserve((size_t)nt_est * TILE_SMP / 2);
+                T.sent_l1.reserve((size_t)nt_est * 48); T.sent_l2.reserve((size_t)nt_est * 48);
+                T.sent_k1.reserve((size_t)nt_est * 48); T.sent_k2.reserve((size_t)nt_est * 48);
+                T.tkf_list.reserve((size_t)nt_est * TILE_KF);
+            }
+            for (int t = ta; t < tb; ++t) {
+                const int d = tl_d[t], e = tl_d[t + 1];
+                const int nobs = lobs0[e] - lobs0[d], npair = lm_pair0[e] - lm_pair0[d], nlmt = e - d;
+                // the tile's pose blocks (uni) and pose samples (usm), sorted
+                uni.clear();
+                usm.clear();
+                for (int l = d; l < e; ++l) {
+                    for (int q = lobs0[l]; q < lobs0[l + 1]; ++q)
+                        if (!smark[dsmp[q]]) { smark[dsmp[q]] = 1; usm.push_back(dsmp[q]); }
+                    for (int k : lm_kfs[l])
+                        if (!kmark[k]) { kmark[k] = 1; uni.push_back(k); }
+                }
+                for (int v : usm) smark[v] = 0;
+                for (int k : uni) kmark[k] = 0;
                 std::sort(uni.begin(), uni.end());
                 std::sort(usm.begin(), usm.end());
                 for (size_t i = 0; i < usm.size(); ++i) sloc[usm[i]] = (int)i;
@@ -1149,7 +1185,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 }
                 T.t_nsmp.push_back((int)T.tsm_smp.size() - T.t_smp0.back());
                 // entry lists per pair, row lists per landmark, the pairs' tile-local (KF, landmark);
-                // pair_r0 / lm_r0 hold piece-local offsets until the concatenation below
+                // pair_r0 / lm_r0 hold run-local offsets until the concatenation below
                 for (int l = d; l < e; ++l) {
                     for (int q = lm_pair0[l]; q < lm_pair0[l + 1]; ++q) {
                         const int k = pair_kf[q];
@@ -1195,18 +1231,17 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                             }
                     T.t_nsent.push_back(nen);
                 }
-                d = e;
             }
         });
-        // the pieces' lists concatenated: every output's per-piece offsets first, then the pieces copied in
-        // parallel (a serial element-wise concatenation cost most of the tiling's wall time on 16 threads)
+        // the runs' lists concatenated: every output's per-run offsets first, then the runs copied in parallel
+        // (a serial element-wise concatenation cost most of the tiling's wall time on 16 threads)
         {
-            std::vector<TileOut*> po(n_pieces);
-            for (int piece = 0; piece < n_pieces; ++piece) po[piece] = &outs[piece];
+            std::vector<TileOut*> po(n_runs);
+            for (int run = 0; run < n_runs; ++run) po[run] = &outs[run];
             struct Cat {
                 std::vector<int>* dst;
                 std::vector<int> TileOut::*src;
-                int add;   // 0: values as they are; 1 / 2 / 3: + the piece's offset into tsm_smp / sent_l1 / tkf_list
+                int add;   // 0: values as they are; 1 / 2 / 3: + the run's offset into tsm_smp / sent_l1 / tkf_list
             };
             const Cat cats[] = {
                 {&t_obs0, &TileOut::t_obs0, 0}, {&t_nobs, &TileOut::t_nobs, 0}, {&t_lm0, &TileOut::t_lm0, 0},
@@ -1217,12 +1252,12 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 {&sent_l1, &TileOut::sent_l1, 0}, {&sent_l2, &TileOut::sent_l2, 0}, {&sent_k1, &TileOut::sent_k1, 0},
                 {&sent_k2, &TileOut::sent_k2, 0}, {&pair_rows, &TileOut::pair_rows, 0}, {&lm_rows, &TileOut::lm_rows, 0}};
             constexpr int NC = (int)(sizeof(cats) / sizeof(cats[0]));
-            // off[c][piece]: where piece's part of output c starts
-            std::vector<std::vector<size_t>> off(NC, std::vector<size_t>(n_pieces + 1, 0));
+            // off[c][run]: where the run's part of output c starts
+            std::vector<std::vector<size_t>> off(NC, std::vector<size_t>(n_runs + 1, 0));
             for (int c = 0; c < NC; ++c) {
-                for (int piece = 0; piece < n_pieces; ++piece)
-                    off[c][piece + 1] = off[c][piece] + (po[piece]->*(cats[c].src)).size();
-                cats[c].dst->resize(off[c][n_pieces]);
+                for (int run = 0; run < n_runs; ++run)
+                    off[c][run + 1] = off[c][run] + (po[run]->*(cats[c].src)).size();
+                cats[c].dst->resize(off[c][n_runs]);
             }
             auto at = [&](std::vector<int> TileOut::*m) {   // index of an output in cats
                 for (int c = 0; c < NC; ++c)
@@ -1231,17 +1266,17 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             };
             const int c_smp = at(&TileOut::tsm_smp), c_sent = at(&TileOut::sent_l1), c_kf = at(&TileOut::tkf_list);
             const int c_pr = at(&TileOut::pair_rows), c_lr = at(&TileOut::lm_rows);
-            par_for(n_pieces, [&](int piece) {
-                const TileOut& T = *po[piece];
+            par_for(n_runs, [&](int run) {
+                const TileOut& T = *po[run];
                 for (int c = 0; c < NC; ++c) {
                     const std::vector<int>& src = T.*(cats[c].src);
-                    const int a = cats[c].add == 1 ? (int)off[c_smp][piece] : cats[c].add == 2 ? (int)off[c_sent][piece]
-                                : cats[c].add == 3 ? (int)off[c_kf][piece] : 0;
-                    int* d = cats[c].dst->data() + off[c][piece];
+                    const int a = cats[c].add == 1 ? (int)off[c_smp][run] : cats[c].add == 2 ? (int)off[c_sent][run]
+                                : cats[c].add == 3 ? (int)off[c_kf][run] : 0;
+                    int* d = cats[c].dst->data() + off[c][run];
                     for (size_t k = 0; k < src.size(); ++k) d[k] = src[k] + a;
                 }
-                const int d0 = (int)((long long)n_reg * piece / n_pieces), d1 = (int)((long long)n_reg * (piece + 1) / n_pieces);
-                const int o_pr = (int)off[c_pr][piece], o_lr = (int)off[c_lr][piece];
+                const int d0 = tl_d[run_t0(run)], d1 = tl_d[run_t0(run + 1)];
+                const int o_pr = (int)off[c_pr][run], o_lr = (int)off[c_lr][run];
                 for (int q = lm_pair0[d0]; q < lm_pair0[d1]; ++q) pair_r0[q + 1] += o_pr;
                 for (int l = d0; l < d1; ++l) lm_r0[l + 1] += o_lr;
             });
@@ -1505,6 +1540,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         };
         mix(t_obs0); mix(t_lm0); mix(tsm_meta); mix(pair_rows); mix(lm_rows); mix(pair_lk); mix(sent_l1); mix(sent_l2);
         mix(sslot); mix(tkf_gslot); mix(seg_slot); mix(ob_row);
+        mix(t_nobs); mix(t_nlm); mix(t_pair0); mix(t_npair); mix(t_smp0); mix(t_nsmp); mix(t_sent0); mix(t_nsent);
+        mix(t_kf0); mix(t_nkf); mix(tkf_list); mix(sent_k1); mix(sent_k2); mix(pair_r0); mix(lm_r0);
         p->setup_hash = h;
         p->setup_tiles = n_tiles;
         return LBA_OK;
