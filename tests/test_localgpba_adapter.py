@@ -183,10 +183,16 @@ def _compare_after(got, exp, info):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kf_id,large", [(29, False), (20, True)])
 def test_local_gpba_matches_oracle(snap4, kf_id, large):
+    import time
     m = ms.LocalGPBAMap(snap4)
+    t0 = time.perf_counter()
     rc, res = m.local_gpba(kf_id, large=large)
+    wall_ms = (time.perf_counter() - t0) * 1e3
     st, exp, info = olg.local_gpba(snap4, kf_id, large)
     assert rc == st == 0, m.error()
+    # the call's part timings (lbamap_result.ms_phase): each part ran, and together they fit in the call
+    parts = list(res.ms_phase)
+    assert all(x > 0 for x in parts) and sum(parts) <= wall_ms, (parts, wall_ms)
     assert res.iterations == info["iterations"]
     assert abs(res.chi2_initial - info["chi2_initial"]) <= 1e-8 * info["chi2_initial"]
     assert abs(res.chi2_final - info["chi2_final"]) <= 1e-7 * info["chi2_final"]
