@@ -625,7 +625,7 @@ def main():
                                         "top per trial)" if args.gba_solve == "split" else
                                         f"landmark partition x{world} (RCCL all-reduce per trial)") if gba else
                                        f"window farm x{world}") if world > 1 else "single window",
-                       "setup_s": t_setup},
+                       "window_build_and_setup_s": t_setup},   # (the synthetic window generation in Python + lba_set_problem)
             # the sweep's algorithmic intensity (F / B ~ 44 FLOP/B at config 1) is above the fp64 ridge point
             # (78.6 TF / 8 TB/s ~ 10 FLOP/B): its roofline is fp64 compute; the HBM view is kept beside it
             "roofline": {"bound": "mfma", "kernel": "k_lin_schur", "achieved": achieved_f,
