@@ -1059,7 +1059,10 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 t_nkf, tkf_list, tsm_smp, tsm_rows, sent_l1, sent_l2, sent_k1, sent_k2, pair_rows, lm_rows;
         };
         const int n_pieces = n_reg >= 256 * SETUP_PIECES ? SETUP_PIECES : 1;
-        const int obs_cap = TILE_OBS;
+#ifndef LBA_TILE_OBS_CAP
+#define LBA_TILE_OBS_CAP TILE_OBS
+#endif
+        const int obs_cap = LBA_TILE_OBS_CAP;   // (a smaller cap: A/B builds only, scripts/exp_build.sh)
         // pass 1, the cut: the first landmark of every tile, per piece
         std::vector<std::vector<int>> cut(n_pieces);
         par_for(n_pieces, [&](int piece) {
