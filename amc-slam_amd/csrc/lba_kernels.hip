@@ -2985,8 +2985,11 @@ __global__ __launch_bounds__(256) void k_zero_ranges(const unsigned long long* _
     }
 }
 // words: the ranges' total, which sizes the grid (one 16-byte store per thread and pass, at most 2048 workgroups)
+#ifndef LBA_ZERO_MAX_BLOCKS
+#define LBA_ZERO_MAX_BLOCKS 2048
+#endif
 void launch_zero_ranges(const unsigned long long* ranges, int n, size_t words, hipStream_t s) {
-    const size_t blocks = std::min<size_t>(2048, std::max<size_t>(1, (words / 4 + 255) / 256));
+    const size_t blocks = std::min<size_t>(LBA_ZERO_MAX_BLOCKS, std::max<size_t>(1, (words / 4 + 255) / 256));
     if (n > 0) hipLaunchKernelGGL(k_zero_ranges, dim3((unsigned)blocks), dim3(256), 0, s, ranges, n);
 }
 
