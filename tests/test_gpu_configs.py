@@ -197,7 +197,7 @@ def test_cfg4_f32_residual_subtree_split(cfg4):
 
 
 def _lm_trials(win, flags, iters, tol_w, tol_chi):
-    """Config 4's LM driven trial by trial (OptimizationAlgorithmLevenberg::solve, levenberg.cpp:61-169), the GPU
+    """A global-BA window's LM driven trial by trial (OptimizationAlgorithmLevenberg::solve, levenberg.cpp:61-169), the GPU
     doing every linearisation, damped solve and update, the oracle checking each trial at the GPU's linearisation
     point: the step's normwise backward error on the oracle's block-sparse system (|r| / (|A| |dx| + |b|), inf-norms,
     A = H + lambda I, r = A dx - b: a backward-stable solve keeps it near n eps at any conditioning, where |r| / |b|
@@ -233,8 +233,8 @@ def _lm_trials(win, flags, iters, tol_w, tol_chi):
             scale = float(dx @ (lam * dx + b_o)) + 1e-3     # computeScale (levenberg.cpp:187-194)
             rho, rho_o = (chi_cur - chi_t) / scale, (chi_cur - chi_ot) / scale
             acc = rho > 0 and np.isfinite(chi_t)
-            print("cfg4 trial: it %d  lambda %.3e  backward error %.2e (componentwise %.2e)  |r|/|b| %.2e  |dx| %.2e  "
-                  "chi2 diff %.2e  rho %+.4e  %s" % (it, lam, w, w_c, rb, np.abs(dx).max(), dchi, rho,
+            print("%s trial: it %d  lambda %.3e  backward error %.2e (componentwise %.2e)  |r|/|b| %.2e  |dx| %.2e  "
+                  "chi2 diff %.2e  rho %+.4e  %s" % (win.name, it, lam, w, w_c, rb, np.abs(dx).max(), dchi, rho,
                                                     "accept" if acc else "reject"), flush=True)
             assert w <= tol_w, (it, q, w)
             assert dchi <= tol_chi, (it, q, chi_t, chi_ot)
@@ -274,3 +274,11 @@ def test_cfg4_f32_residual_lm_trials_match_oracle(cfg4):
     from amc_lba.abi import FLAG_F32_RESIDUAL
     log = _lm_trials(cfg4, FLAG_F32_RESIDUAL, 5, 1e-6, 1e-5)
     assert sum(1 for e in log if e[6]) == 5
+
+
+def test_cfg2_lm_trials_match_oracle():
+    """Config 2 (global BA, 500 KF / 200k landmarks / 1.2M observations, the banded solve) through the same trial-by-trial
+    check as config 4: ten LM iterations, every step's normwise backward error on the oracle's block-sparse system
+    <= 1e-12, every trial state's chi2 the oracle's to 1e-9, every accept / reject decision the oracle's."""
+    log = _lm_trials(make_config_window("cfg2_global_500kf"), 0, 10, 1e-12, 1e-9)
+    assert sum(1 for e in log if e[6]) >= 9
