@@ -320,6 +320,7 @@ def make_map(n_kf=30, n_lm=3000, obs_per_lm=6, n_cam=4, n_gp_frames=1, gp_obs_fr
 
 # ------------------------------------------------------------------ ctypes binding
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LBAMAP_ABI_VERSION = 2   # include/amc_lba_map.h: the structs below (LbamapResult with ms_phase)
 # AMC_LBA_MAP_LIB: another build of the adapter (A/B of two builds: scripts/cmp_map_libs.py)
 MAP_LIB_PATH = os.environ.get("AMC_LBA_MAP_LIB") or os.path.join(PKG_DIR, "lib", "libamc_lba_map.so")
 _lib = None
@@ -352,6 +353,8 @@ def map_lib():
         if not os.environ.get("AMC_LBA_MAP_LIB"):
             check_fresh("map")
         L = ctypes.CDLL(MAP_LIB_PATH)
+        if hasattr(L, "lbamap_abi_version") and L.lbamap_abi_version() != LBAMAP_ABI_VERSION:
+            raise RuntimeError(f"{MAP_LIB_PATH}: adapter ABI {L.lbamap_abi_version()}, this binding {LBAMAP_ABI_VERSION}")
         vp = ctypes.c_void_p
         L.lbamap_load.argtypes = [ctypes.POINTER(vp), ctypes.c_char_p, ctypes.c_size_t]
         L.lbamap_free.argtypes = [vp]
@@ -377,7 +380,7 @@ def map_lib():
 
 
 def exported_symbols():
-    return ["lbamap_load", "lbamap_free", "lbamap_last_error", "lbamap_snapshot_size", "lbamap_save",
+    return ["lbamap_abi_version", "lbamap_load", "lbamap_free", "lbamap_last_error", "lbamap_snapshot_size", "lbamap_save",
             "lbamap_local_gpba", "lbamap_build_window", "lbamap_global_ba", "lbamap_global_ba_thread", "lbamap_kf_gba", "lbamap_mp_gba",
             "lbamap_build_ba_window"]
 

@@ -21,6 +21,8 @@ struct lbamap {
 
 extern "C" {
 
+int lbamap_abi_version(void) { return LBAMAP_ABI_VERSION; }
+
 int lbamap_load(lbamap** out, const void* bytes, size_t n_bytes) {
     if (!out || !bytes) return LBA_E_ARG;
     *out = nullptr;

@@ -41,7 +41,8 @@
 extern "C" {
 #endif
 
-#define LBAMAP_VERSION   2
+#define LBAMAP_VERSION   2      /* the snapshot format */
+#define LBAMAP_ABI_VERSION 2    /* the adapter's structs: 2: lbamap_result gained ms_phase[4] */
 #define LBAMAP_MAX_CAM   8
 #define LBAMAP_MAX_LEVEL 16
 
@@ -159,6 +160,8 @@ typedef struct lbamap_ba_result {
 typedef struct lbamap lbamap;   /* opaque: the loaded map + a reusable lba_problem */
 
 /* Load a snapshot (bytes as laid out above).  Returns LBA_OK or LBA_E_ARG. */
+/* LBAMAP_ABI_VERSION of the library: a caller built against another header must not pass its structs. */
+int    lbamap_abi_version(void);
 int    lbamap_load(lbamap** out, const void* bytes, size_t n_bytes);
 void   lbamap_free(lbamap* m);
 const char* lbamap_last_error(const lbamap* m);

@@ -140,6 +140,12 @@ def _c_sizeof(struct):
     return int(subprocess.run([exe], capture_output=True, text=True, check=True).stdout)
 
 
+def test_map_abi_version_matches_header():
+    """The adapter's struct version (lbamap_abi_version) is the header's LBAMAP_ABI_VERSION and the binding's."""
+    v = int(re.search(r"#define LBAMAP_ABI_VERSION\s+(\d+)", open(MAP_HEADER).read()).group(1))
+    assert ms.map_lib().lbamap_abi_version() == v == ms.LBAMAP_ABI_VERSION
+
+
 def test_map_abi_exports():
     L = ms.map_lib()
     src = re.sub(r"/\*.*?\*/", "", open(MAP_HEADER).read(), flags=re.S)
