@@ -86,7 +86,7 @@ struct LMCtl {
     int nbad, trials, failures, result;
     int max_trials, early_stop;
     int slot;                  // trials finalised (queue position)
-    int pad2;
+    int chi0_lin;              // 1: chi0 is still to be taken from the first trial (its chi2 at the linearisation point)
 };
 constexpr int LMCTL_DOUBLES = sizeof(LMCtl) / sizeof(double);
 static_assert(sizeof(LMCtl) % sizeof(double) == 0, "LMCtl mirrors into a double array");
@@ -370,7 +370,7 @@ void launch_env_pack(const DevProblem& P, int unpack, int gate, hipStream_t s);
 // and the back substitution) of k_chol_flow (same epoch for both)
 void launch_cholesky_part(const DevProblem& P, int part, unsigned epoch, hipStream_t s, hipEvent_t e0 = nullptr,
                           hipEvent_t e1 = nullptr);
-enum { FIN_NONE = -1, FIN_HOST = 0, FIN_QUEUED = 1, FIN_QUEUED_PUBLISH = 2, FIN_INITIAL = 3 };
+enum { FIN_NONE = -1, FIN_HOST = 0, FIN_QUEUED = 1, FIN_QUEUED_PUBLISH = 2 };
 void launch_finalize(const DevProblem& P, unsigned long long seq, int mode, hipStream_t s);
 // zero n device ranges (pairs: address, 4-byte words) in one launch (lba_set_problem's fresh buffers)
 void launch_zero_ranges(const unsigned long long* ranges, int n, size_t words, hipStream_t s);

@@ -2346,13 +2346,12 @@ int optimize_queued(lba_problem* p, int iters, lba_stats* st) {
     c.max_trials = p->cfg.max_trials;
     c.early_stop = p->cfg.early_stop;
     c.result = LBA_RESULT_OK;
+    c.chi0_lin = 1;   // chi2 of the starting state: the first trial's, at its linearisation point (lm_decide)
     launch_ctl_init(D, c, p->stream);
     // starting state: poses + GP samples (with the Jacobian factors the first linearisation uses; a
-    // previous queue left them for both state buffers), chi2
+    // previous queue left them for both state buffers)
     if (!p->gps_fresh[p->cur]) launch_gp_prep(D, p->cur, 1, GATE_NONE, p->stream);
     p->gps_fresh[p->cur] = true;
-    launch_eval(D, p->cur, GATE_NONE, 0, FIN_NONE, p->stream);
-    launch_fin(p, 0, FIN_INITIAL);
     int issued = 0;
     std::vector<char> timed(tsweep ? HLOG_CAP : 0, 0);   // trials whose dispatches carry events
     const LMCtl* hc = reinterpret_cast<const LMCtl*>(p->h_fin + 8);
@@ -2443,8 +2442,10 @@ int optimize(lba_problem* p, int iters, volatile const int32_t* stop, lba_stats*
     if (!stop && iters > 0 && !(p->cfg.flags & (LBA_FLAG_TIME_PHASES | LBA_FLAG_HOST_LOOP)))
         return optimize_queued(p, iters, st);
     const auto t0 = std::chrono::steady_clock::now();
-    s.chi2_initial = eval_current(p);
-    double last_chi = s.chi2_initial;
+    // chi2 of the starting state: the first trial's at its linearisation point (as the queued loop takes it);
+    // evaluated on its own only when no trial runs (a stop flag already set)
+    bool have_chi0 = false;
+    double last_chi = 0.0;
     int it = 0, result = LBA_RESULT_OK;
     const bool tphase = (p->cfg.flags & LBA_FLAG_TIME_PHASES) != 0;
     const bool tsweep = tphase || (p->cfg.flags & LBA_FLAG_TIME_SWEEP) != 0;
@@ -2461,6 +2462,7 @@ int optimize(lba_problem* p, int iters, volatile const int32_t* stop, lba_stats*
         do {
             trial(p, p->lambda, true, tphase ? p->ev : nullptr, tsweep, false);
             if (qmax == 0) currentChi = iniChi = p->h_fin[0];
+            if (!have_chi0) { s.chi2_initial = p->h_fin[0]; have_chi0 = true; }
             if (tphase) {   // (ms_linearize: the fused linearisation + elimination)
                 s.ms_linearize += elapsed(p->ev[0], p->ev[1]);
                 s.ms_schur += elapsed(p->ev[1], p->ev[2]);
@@ -2508,6 +2510,7 @@ int optimize(lba_problem* p, int iters, volatile const int32_t* stop, lba_stats*
         if (result != LBA_RESULT_OK && p->cfg.early_stop) break;
     }
     HIPCHK(hipStreamSynchronize(p->stream));
+    if (!have_chi0) last_chi = s.chi2_initial = eval_current(p);
     s.iterations = it;
     s.result = result;
     s.chi2_final = last_chi;

@@ -2807,6 +2807,9 @@ __device__ void lm_decide(LMCtl& c, double chi_lin, double chi_trial, double sca
     if (hlog) hlog[c.slot % HLOG_CAP] = c.done ? 0 : 1;   // whether the trial's gated kernels ran
     c.slot++;
     if (c.done) return;
+    // chi2 of the starting state (g2o's activeRobustChi2 before optimize): the first trial's chi2 at its
+    // linearisation point, which is that state (no evaluation launch of its own ahead of the queue)
+    if (c.chi0_lin) { c.chi0 = chi_lin; c.chi0_lin = 0; }
     if (c.qmax == 0) c.cur_chi = c.ini_chi = chi_lin;
     double temp = chi_trial;
     c.last_chi = chi_trial;
@@ -2916,8 +2919,7 @@ __global__ __launch_bounds__(256) void k_env_pack(DevProblem P, int unpack, int 
 }
 
 // mode (FIN_*): host-driven trial (publish the summary); queued trial (decide, and publish the
-// controller mirror when it is the last trial of a batch); starting-state evaluation of a queue
-// (chi2 only, into the controller)
+// controller mirror when it is the last trial of a batch)
 template <int NT>
 __device__ void finalize_body(const DevProblem& P, unsigned long long seq, int mode, double* red) {
     const int tid = threadIdx.x;
@@ -2925,7 +2927,7 @@ __device__ void finalize_body(const DevProblem& P, unsigned long long seq, int m
     // the controller and the factorisation status are loaded ahead of the sums (they do not change in this
     // launch): the decision then waits for one round of loads, not three
     LMCtl ctl;
-    if (tid == 0 && mode != FIN_INITIAL && mode != FIN_HOST) ctl = *P.ctl;
+    if (tid == 0 && mode != FIN_HOST) ctl = *P.ctl;
     const int info = P.part_n > 0 ? 0 : *P.info;
     int fault = *P.fault;
     if (P.part_n > 0) {   // partitioned: the all-reduced sums of every rank's k_partials
@@ -2938,10 +2940,6 @@ __device__ void finalize_body(const DevProblem& P, unsigned long long seq, int m
     }
     if (tid != 0) return;
     const double v[4] = {sa, sb, sc, sinfo};
-    if (mode == FIN_INITIAL) {
-        P.ctl->chi0 = sb;
-        return;
-    }
     if (mode == FIN_HOST) {
         for (int i = 0; i < 4; ++i) P.fin[i] = v[i];
     } else {
