@@ -90,12 +90,12 @@ def test_null_arguments_rejected():
     assert L.lba_get_state(None, None, None) == abi.LBA_E_ARG
 
 
-def _layout(threads):
+def _layout(threads, window="make_config_window('cfg1_local_50kf')"):
     import subprocess
     import sys
     code = ("import sys; sys.path.insert(0, 'amc-slam_amd'); import amc_lba; "
-            "from amc_lba.synth import make_config_window; "
-            "ms, c = amc_lba.setup_host_profile(make_config_window('cfg1_local_50kf')); print(*c)")
+            "from amc_lba.synth import make_config_window, make_window; "
+            f"ms, c = amc_lba.setup_host_profile({window}); print(*c)")
     env = dict(os.environ, LBA_SETUP_THREADS=str(threads))
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True,
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -109,6 +109,16 @@ def test_set_problem_host_layout_independent_of_threads():
     assert one == eight
     n_lm, n_pb, np_, tiles, _ = (int(x) for x in one)
     assert n_lm == 20000 and n_pb == 50 and np_ == 600 and 900 < tiles < 1200
+
+
+def test_set_problem_host_layout_small_window_independent_of_threads():
+    """The same for a LocalGPBA-sized window (3000 landmarks: below 256 per piece, so its tiles are cut in one piece
+    and their lists built in parallel runs of tiles) -- the layout fingerprint covers every tile list."""
+    w = "make_window(n_opt_kf=11, n_lm=3000, obs_per_lm=6, n_cam=4, gp=True, seed=21)"
+    one, eight = _layout(1, w), _layout(8, w)
+    assert one == eight
+    n_lm, n_pb, np_, tiles, _ = (int(x) for x in one)
+    assert n_lm == 3000 and tiles > 16   # more tiles than set-up pieces: the runs split the list building
 
 
 def _pool_stress(threads, passes, pieces):
