@@ -2058,6 +2058,30 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             if (fi) cf_fetch(tile_at(a.Lm, a.plist_t[3 * q + 1]), CNB, ri);
             if (fk) cf_fetch(tile_at(a.Lm, a.plist_t[3 * q + 2]), CNB, rk);
         };
+        // entries [q0, known] of the list are published: tested up to 16 entries at a time (one flag per lane, one
+        // round trip); a published flag stays so, so a list of long-published tiles costs one round trip per 16
+        // entries instead of one per entry ahead of its products
+        const int q0 = a.pl0[t], q1 = a.pl0[t + 1];
+        int known = q0 - 1;
+        auto test_ahead = [&](int upto) {   // extend `known` towards `upto` (non-blocking)
+            if (known >= upto) return;
+            const int first = known + 1, last = min(first + 15, q1 - 1);
+            if (threadIdx.x < 64) {
+                const int l = threadIdx.x, q = first + l / 3, part = l % 3;
+                bool done = true;
+                if (l < 48 && q <= last) {
+                    bool fj, fi, fk;
+                    rows(a.plist[q], fj, fi, fk);
+                    if (part == 0 ? fj : (part == 1 ? fi : fk))
+                        done = (unsigned)__hip_atomic_load((gi32_t*)(a.lready + a.plist_t[3 * q + part]), __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT) == a.epoch;
+                }
+                const unsigned long long nb = __ballot(!done);   // lanes of entries not yet published
+                if (l == 0) s_ok = nb ? first + (int)(__builtin_ctzll(nb) / 3) - 1 : last;
+            }
+            __syncthreads();
+            known = s_ok;   // (the next write of s_ok comes after a barrier that follows this read)
+        };
         bool ok = true;
         // lookahead: column k's two tiles are factored as soon as their own updates are in (after the list
         // entry marked with bit 27, or before the first entry when the task's bit 29 says none updates them),
@@ -2084,7 +2108,6 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
         if (la && ((code >> 29) & 1)) factor_k();
         // the panels in update order (the same order in every task: the copies of a tile stay bitwise
         // identical)
-        const int q0 = a.pl0[t], q1 = a.pl0[t + 1];
         for (int q = q0; q < q1; ++q) {
             const int e = a.plist[q];
             bool fj, fi, fk;
@@ -2092,6 +2115,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             const bool waited = !have;
             if (!have) {
                 if (!ready(q, true)) { ok = false; break; }
+                known = max(known, q);
                 if (tf) { tf[3] = __builtin_amdgcn_s_memrealtime(); tf[4] = (tf[4] & 0xffffffull) | ((unsigned long long)(la) << 24) | ((unsigned long long)(e & 0xffffff) << 32); }
                 fetch(q);
             }
@@ -2099,7 +2123,8 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             if (fi) cf_put(Lt[1], ri);
             if (fk) cf_put(Lt[2], rk);
             __syncthreads();
-            have = q + 1 < q1 && ready(q + 1, false);
+            if (q + 1 < q1) test_ahead(q + 1);
+            have = q + 1 < q1 && q + 1 <= known;
             if (have) fetch(q + 1);
             if (fj) sub_mma(qd, cf_mma_nt(Lt[0], Lt[0], rb, cb, lr, kq, z4));
             if (fi && fj) sub_mma(qa, cf_mma_nt(Lt[1], Lt[0], rb, cb, lr, kq, z4));
