@@ -338,9 +338,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=None,
-                    help="untimed LM iterations before the timed ones (default: 100 for the local windows, ~20 ms of "
-                         "work that brings the GPU to its steady clocks -- 5 left the 20-step value ~2 %% low, "
-                         "profiles/r8g_warmup.txt; 2 for the global-BA configs, whose iterations take ms each)")
+                    help="untimed LM iterations before the timed ones (default: 100 for config 1, ~20 ms of work that "
+                         "brings the GPU to its steady clocks -- 5 left the 20-step value ~2 %% low, "
+                         "profiles/r8g_warmup.txt; 5 for config 0, whose small window converges within 100 and then "
+                         "rejects trials; 2 for the global-BA configs, whose iterations take ms each)")
     ap.add_argument("--config", default="cfg1_local_50kf")
     ap.add_argument("--window-iters", type=int, default=10, help="LM iterations per window (LocalGPBA optimize(10))")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -359,7 +360,7 @@ def main():
                     help="BASELINE configs[4]'s fp32 residuals + fp64 accumulate (LBA_FLAG_F32_RESIDUAL; default fp64)")
     args = ap.parse_args()
     if args.warmup is None:   # (from the name: nothing may load the library before launch_ranks)
-        args.warmup = 2 if "global" in args.config else 100
+        args.warmup = 100 if args.config == "cfg1_local_50kf" else (2 if "global" in args.config else 5)
     rc = launch_ranks(args, sys.argv[1:])
     if rc is not None:
         sys.exit(rc)
