@@ -1778,6 +1778,12 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
         // Distributed factorisation: list A (launch 0) holds this rank's subtree columns and its contributions to
         // the top, list B (launch 1) the top columns (updated from top panels only: the subtrees' updates are summed
         // into the top tiles between the launches) and the back substitution of the top and this rank's columns.
+#ifndef LBA_CF_LA_MAX_LIST   // (A/B builds only, scripts/exp_build.sh)
+#define LBA_CF_LA_MAX_LIST 16
+#endif
+#ifndef LBA_CF_LA_BAND
+#define LBA_CF_LA_BAND 0
+#endif
         {
             struct TaskList {
                 std::vector<int> tasks, task_i, task_t, pl0{0}, plist, plist_t;
@@ -1829,8 +1835,14 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 for (int i : rows) {   // factor tiles of column c (the diagonal first)
                     // lookahead over k = c - 1 when tile (c, k) exists and k is the last update of A(c, c)
                     // in update order (then every copy of a tile sees the same update order)
+                    // and only in dense mode, on a short list of its own: a lookahead task applies 5 tile products
+                    // per entry instead of 2.  A band-mode solve has thousands of tasks on 512 workgroups, so the
+                    // redundant products of column k cost more than the hand-off they save (config 2's solve
+                    // 465 -> 357 us, config 4's 3.25 -> 2.25 ms without them, profiles/r8p_ab_lookahead.txt);
+                    // config 1's few tasks (dense mode, lists <= 16) keep it: it is their chain
                     const int k = c - 1;
-                    bool la = k >= 0 && pl.nz(c, k) && same_part(k, own[c]);
+                    bool la = k >= 0 && pl.nz(c, k) && same_part(k, own[c]) && (LBA_CF_LA_BAND || !band) &&
+                              (int)rcc.size() <= LBA_CF_LA_MAX_LIST;
                     for (int pp : rcc)
                         if (la && pp != k && rank[pp] > rank[k]) la = false;
                     const int tcc = pl.tile_id(c, c), tic = i == c ? -1 : pl.tile_id(i, c);
