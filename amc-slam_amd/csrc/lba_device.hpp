@@ -251,7 +251,7 @@ struct DevProblem {
     unsigned long long* cf_head;
     int* cf_abort;
     int cf_band;            // 1: solve by substitution tasks (no L^-1 tiles, large systems)
-    double* cf_xpos;        // band solve: x in factorisation order (handed off between back tasks)
+    unsigned long long* cf_xg;   // band solve: x in factorisation order as {epoch, half} granules (back tasks)
     double* LinvT;          // [npad / CHOL_NB][CHOL_NB][CHOL_NB] inverse diagonal blocks L_bb^-T (row-major)
     double* Hpl;
     double* Hll;

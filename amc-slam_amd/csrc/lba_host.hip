@@ -1982,7 +1982,8 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
             D.cf_linv = band ? nullptr : dalloc<double>(p, (size_t)npad * npad);
             D.cf_ivready = dalloc<int>(p, niv);
             zero_later(p, D.cf_ivready, sizeof(int) * niv);
-            D.cf_xpos = band ? dalloc<double>(p, npad) : nullptr;
+            D.cf_xg = band ? dalloc<unsigned long long>(p, 2 * (size_t)npad) : nullptr;
+            if (band) zero_later(p, D.cf_xg, sizeof(unsigned long long) * 2 * (size_t)npad);
             D.cf_pl0 = dupload(p, pl0);
             D.cf_plist = dupload(p, plist);
             D.cf_plist_t = dupload(p, plist_t);

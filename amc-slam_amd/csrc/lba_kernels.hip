@@ -70,6 +70,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));   // v_mfma_f64_16x16x4 a
 // tasks publish; the standalone kernels do not need to).
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 typedef __attribute__((address_space(1))) int gi32_t;
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 
 __device__ __forceinline__ double ld_sc1(const double* p) {
     return __longlong_as_double((long long)__hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -1529,8 +1530,8 @@ struct CholFlow {
     double* xout;        // the solution, natural order
     const int* rnat;     // natural row of a factorisation row
     // band mode (kinds 4, 5): forward / back substitution tasks instead of L^-1 tiles
-    double* xpos;        // [npad] x in factorisation order, handed off between back tasks
-    int* xready;         // per panel: epoch once x_j is published
+    unsigned long long* xg;   // [2 npad] x in factorisation order, handed off between back tasks as 8-byte granules
+                              // {epoch << 32 | one half of a double}: the data is its own flag
 };
 
 // lanes 0..2 of wave 0 poll up to three flags (null = none) for `epoch` side by side (relaxed, agent
@@ -1904,6 +1905,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
                 st_sc1(a.yv + i * CNB + tid, y);
             }
             cf_publish(a, a.dready + i);
+            if (a.tdbg && tid == 0) a.tdbg[16 * i + 7] = __builtin_amdgcn_s_memrealtime();
             continue;
         }
         if (kind == 5) {
@@ -1914,7 +1916,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             // factorisation published them long before), so the chain from x_i to x_j is one hand-off,
             // the dot products and the publication
             const int c = tid & 31, g = tid >> 5;
-            constexpr int MT = 4;   // terms held in registers (the rest are fetched behind their x_i)
+            constexpr int MT = 4;   // terms held in registers (the rest are fetched as they come, ahead of their x_i)
             const int q0 = a.pl0[t], nt = a.pl0[t + 1] - q0;
             if (!cf_wait(a, a.fready + j, a.dready + j, &s_ok)) return;
 #pragma unroll
@@ -1923,37 +1925,69 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
                 Lt[0][e >> 5][e & 31] = ld_sc1(a.LinvT + (size_t)j * CNB * CNB + e);
             }
             const double yj = tid < CNB ? ld_sc1(a.yv + j * CNB + tid) : 0.0;
+            // every term's tile L(i, j) published (one poll per term, side by side: one round trip for the list)
+            if (!cf_wait_list(a, nt, [&](int q) { return a.lready + a.plist_t[3 * (q0 + q)]; }, &s_ok)) return;
             double lv[MT][4];
 #pragma unroll
             for (int q = 0; q < MT; ++q)
                 if (q < nt) {
                     const int tl = a.plist_t[3 * (q0 + q)];
-                    if (!cf_wait(a, a.lready + tl, nullptr, &s_ok)) return;
 #pragma unroll
                     for (int u = 0; u < 4; ++u) lv[q][u] = ld_sc1(tile_at(a.Lm, tl) + (4 * g + u) * CNB + c);
                 }
+            // x_i of a term: wave 0 polls its 64 granules (one per lane, one round trip: the flag is the data) and
+            // hands the 32 values to the workgroup in LDS (xs[q & 1]: a buffer is rewritten two terms later, behind
+            // the barrier of the term between)
+            double(*xs)[CNB] = reinterpret_cast<double(*)[CNB]>(&Lt[1][8][0]);
+            auto take_x = [&](int ii, double* dst) {
+                if (tid < 64) {
+                    const gu64_t* gp = (const gu64_t*)(a.xg + (size_t)ii * 2 * CNB + tid);
+                    unsigned long long v = 0;
+                    bool ok = true;
+                    for (unsigned spins = 0;; ++spins) {
+                        v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (__all((unsigned)(v >> 32) == a.epoch)) break;
+                        if (spins > CF_SPIN_LIMIT ||
+                            ((spins & 255) == 255 &&
+                             (unsigned)__hip_atomic_load((gi32_t*)a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch)) {
+                            if (tid == 0) {
+                                __hip_atomic_store((gi32_t*)a.abort_flag, (int)a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                *a.info = CF_TIMEOUT;
+                                __hip_atomic_fetch_or((gi32_t*)a.fault, FAULT_FLOW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            }
+                            ok = false;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    const unsigned lo = (unsigned)v, hi = (unsigned)__shfl_xor((int)lo, 1);   // lane 2r: low half
+                    if ((tid & 1) == 0) dst[tid >> 1] = __longlong_as_double(((long long)hi << 32) | lo);
+                    if (tid == 0) s_ok = ok ? 1 : 0;
+                }
+                __syncthreads();
+                return s_ok != 0;
+            };
             double acc = 0.0;
 #pragma unroll
             for (int q = 0; q < MT; ++q)
                 if (q < nt) {
                     const int ii = a.plist[q0 + q] & 0xffffff;
-                    if (!cf_wait(a, a.xready + ii, nullptr, &s_ok)) return;
+                    if (!take_x(ii, xs[q & 1])) return;
                     double xi[4];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) xi[u] = ld_sc1(a.xpos + ii * CNB + 4 * g + u);
+                    for (int u = 0; u < 4; ++u) xi[u] = xs[q & 1][4 * g + u];
 #pragma unroll
                     for (int u = 0; u < 4; ++u) acc += lv[q][u] * xi[u];
                 }
             for (int q = MT; q < nt; ++q) {
                 const int ii = a.plist[q0 + q] & 0xffffff;
                 const int tl = a.plist_t[3 * (q0 + q)];
-                if (!cf_wait(a, a.lready + tl, a.xready + ii, &s_ok)) return;
                 double l4[4], xi[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    l4[u] = ld_sc1(tile_at(a.Lm, tl) + (4 * g + u) * CNB + c);
-                    xi[u] = ld_sc1(a.xpos + ii * CNB + 4 * g + u);
-                }
+                for (int u = 0; u < 4; ++u) l4[u] = ld_sc1(tile_at(a.Lm, tl) + (4 * g + u) * CNB + c);
+                if (!take_x(ii, xs[q & 1])) return;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) xi[u] = xs[q & 1][4 * g + u];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) acc += l4[u] * xi[u];
             }
@@ -1970,10 +2004,14 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
                 double x = 0.0;
 #pragma unroll 8
                 for (int rr = 0; rr < CNB; ++rr) x += Lt[0][tid][rr] * Lt[2][0][rr];
-                st_sc1(a.xpos + j * CNB + tid, x);
+                const unsigned long long xb = (unsigned long long)__double_as_longlong(x), tag = (unsigned long long)a.epoch << 32;
+                gu64_t* gp = (gu64_t*)(a.xg + (size_t)j * 2 * CNB + 2 * tid);
+                __hip_atomic_store(gp, tag | (xb & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(gp + 1, tag | (xb >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 a.xout[a.rnat[j * CNB + tid]] = x;
             }
-            cf_publish(a, a.xready + j);
+            __syncthreads();
+            if (a.tdbg && tid == 0) a.tdbg[16 * j + 15] = __builtin_amdgcn_s_memrealtime();
             continue;
         }
         if (kind == 3) {
@@ -3107,7 +3145,7 @@ static CholFlow make_flow(const DevProblem& P, unsigned epoch) {
     a.tdbg3 = P.tdbg_cf;
     a.Linv = P.cf_linv; a.ivready = P.cf_ivready; a.xout = P.xsol; a.rnat = P.rnat; a.fready = P.cf_fready;
     a.zready = P.cf_zready; a.zv = P.cf_zv;
-    a.xpos = P.cf_xpos; a.xready = P.cf_ivready;
+    a.xg = P.cf_xg;
     return a;
 }
 static void launch_flow(const CholFlow& a, const DevProblem& P, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {

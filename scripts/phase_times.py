@@ -192,6 +192,14 @@ def main():
         yx = [((c[j, 7] - t0) / 100.0, (c[j, 15] - t0) / 100.0) for j in range(npan)]
         out.append("   forward block y_j published / solution block x_j written:")
         out.append("   " + "  ".join(f"{j}:{y:.1f}/{x:.1f}" for j, (y, x) in enumerate(yx)))
+        pub = [(c[j, 6] - t0) / 100.0 for j in range(npan) if c[j, 6]]
+        ys = [y for y, _ in yx if c[0, 7] and y > 0]
+        xs = [x for _, x in yx if x > 0]
+        if pub and ys and xs:   # the solve's tail after the factorisation (band mode: the substitution chains)
+            order = sorted(range(npan), key=lambda j: yx[j][1])
+            out.append(f"   tail: last panel published {max(pub):.2f}, last y_j {max(ys):.2f}, last x_j {max(xs):.2f}; "
+                       "x_j in completion order (first 24): " +
+                       " ".join(f"{j}:{yx[j][1]:.1f}" for j in order[:24]))
         b2 = bs[:npan].astype(np.int64)
         for rr in range(2):
             out.append(f"   L^-1 tiles of row {npan - 2 + rr}: j: start / terms done / L_ii^-1 out / published")
