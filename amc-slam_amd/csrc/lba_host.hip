@@ -1781,9 +1781,6 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
 #ifndef LBA_CF_LA_MAX_LIST   // (A/B builds only, scripts/exp_build.sh)
 #define LBA_CF_LA_MAX_LIST 16
 #endif
-#ifndef LBA_CF_LA_BAND
-#define LBA_CF_LA_BAND 0
-#endif
         {
             struct TaskList {
                 std::vector<int> tasks, task_i, task_t, pl0{0}, plist, plist_t;
@@ -1839,9 +1836,10 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                     // per entry instead of 2.  A band-mode solve has thousands of tasks on 512 workgroups, so the
                     // redundant products of column k cost more than the hand-off they save (config 2's solve
                     // 465 -> 357 us, config 4's 3.25 -> 2.25 ms without them, profiles/r8p_ab_lookahead.txt);
-                    // config 1's few tasks (dense mode, lists <= 16) keep it: it is their chain
+                    // config 1's few tasks (dense mode, lists <= 16) keep it: it is their chain.  (The band
+                    // kernel, k_chol_flow_band, has no lookahead path.)
                     const int k = c - 1;
-                    bool la = k >= 0 && pl.nz(c, k) && same_part(k, own[c]) && (LBA_CF_LA_BAND || !band) &&
+                    bool la = k >= 0 && pl.nz(c, k) && same_part(k, own[c]) && !band &&
                               (int)rcc.size() <= LBA_CF_LA_MAX_LIST;
                     for (int pp : rcc)
                         if (la && pp != k && rank[pp] > rank[k]) la = false;

@@ -1681,9 +1681,16 @@ __device__ __forceinline__ d4 cf_mma_nn(const double (*X)[CNB + 1], const double
     return acc;
 }
 
-__global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
+#ifndef LBA_CF_BAND_WAVES   // waves per SIMD the band kernel is compiled for (A/B builds only)
+#define LBA_CF_BAND_WAVES 2
+#endif
+// BAND: the substitution solve's kernel (kinds 0, 4, 5, 6, 7, no lookahead: the host gives none in band mode); the
+// L^-1 solve's kernel (kinds 0 with or without lookahead, 1, 2, 3, 4) otherwise
+template <bool BAND>
+__device__ __forceinline__ void chol_flow_body(const CholFlow& a, const DevProblem& P) {
+    (void)P;
     __shared__ double Lt[3][CNB][CNB + 1];       // update operands L(j, p), L(i, p), L(k, p)
-    __shared__ double stg[2][2 * CNB][CNB + 1];  // stacked panels of the factoring waves
+    __shared__ double stg[BAND ? 1 : 2][2 * CNB][CNB + 1];  // stacked panels of the factoring waves
     __shared__ long long s_ticket;
     __shared__ int s_ok;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1717,8 +1724,8 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
         const int code = a.tasks[t];
         const int j = code & 0xffffff, i = a.task_i[t];
         const int kind = (code >> 24) & 15;
-        const bool la = (code >> 28) & 1;   // factor task with lookahead over column k = j - 1
-        if (kind == 1) {
+        const bool la = !BAND && ((code >> 28) & 1);   // factor task with lookahead over column k = j - 1
+        if (!BAND && kind == 1) {
             // ---------------------------------------------------- L^-1 tile (i, j), i > j:
             // Linv(i,j) = -L_ii^-1 sum_k L(i,k) Linv(k,j) over the list's k (Linv(j,j) = LinvT_j^T)
             const d4 z = {0.0, 0.0, 0.0, 0.0};
@@ -1780,7 +1787,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             if (tv) tv[3] = __builtin_amdgcn_s_memrealtime();
             continue;
         }
-        if (kind == 2) {
+        if (!BAND && kind == 2) {
             // ---------------------------------------------------- x_j = sum_r Linv(r,j)^T y_r over the list's
             // r (Linv(j,j)^T = LinvT_j), into xsol in natural panel order.  Each term's tile is fetched as
             // soon as it is published, ahead of y_r.
@@ -1822,7 +1829,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             __syncthreads();
             continue;
         }
-        if (kind == 6) {
+        if (BAND && kind == 6) {
             // ---------------------------------------------------- distributed factorisation, part 0: this rank's
             // contribution to top tile (i, j), S(i,j) -= sum over its subtree panels p (the list) of L(i,p) L(j,p)^T
             // (the ranks' S tiles of the top are all-reduced before part 1 factors them)
@@ -1842,7 +1849,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             for (int m = 0; m < 4; ++m) Sq[(rb * 16 + kq + 4 * m) * CNB + cb * 16 + lr] -= acc[m];
             continue;
         }
-        if (kind == 7) {
+        if (BAND && kind == 7) {
             // ---------------------------------------------------- distributed factorisation, part 0: this rank's
             // contribution to the top rhs block i, bS_i -= sum over its subtree panels p (the list) of L(i,p) y_p
             const int r = tid & 31, g = tid >> 5;
@@ -1908,7 +1915,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             if (a.tdbg && tid == 0) a.tdbg[16 * i + 7] = __builtin_amdgcn_s_memrealtime();
             continue;
         }
-        if (kind == 5) {
+        if (BAND && kind == 5) {
             // ---------------------------------------------------- band mode, back substitution:
             // x_j = L_jj^-T (y_j - sum_i L(i,j)^T x_i) over the list's rows i > j (completion order);
             // thread (c, g) takes output c, rows 4g .. 4g + 3 of every term.  Everything that is not an
@@ -2014,7 +2021,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             if (a.tdbg && tid == 0) a.tdbg[16 * j + 15] = __builtin_amdgcn_s_memrealtime();
             continue;
         }
-        if (kind == 3) {
+        if (!BAND && kind == 3) {
             // ---------------------------------------------------- y_i = sum_k z(i, k) over the list's k
             // (z(i, k) = Linv(i, k) b_k, made by the tasks of Linv(i, k) and panel i): the forward solve
             // without a chain through the panels
@@ -2131,13 +2138,13 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
             stage_quad(stg[0], 0, qk);
             stage_quad(stg[0], CNB, qjk);
             if (ik) {
-                stage_quad(stg[1], 0, qk);
-                stage_quad(stg[1], CNB, qik);
+                stage_quad(stg[BAND ? 0 : 1], 0, qk);
+                stage_quad(stg[BAND ? 0 : 1], CNB, qik);
             }
             __syncthreads();
             if (wave == 0 || (wave == 1 && ik)) {
                 bool bad;
-                factor(stg[wave], bad);
+                factor(stg[BAND ? 0 : wave], bad);
                 (void)bad;   // (reported by panel k's own task)
             }
             __syncthreads();
@@ -2181,7 +2188,7 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
         if (tf) tf[5] = __builtin_amdgcn_s_memrealtime();
         if (ok && la) {   // the update from column k (factored above)
             sub_mma(qd, cf_mma_nt(stg[0] + CNB, stg[0] + CNB, rb, cb, lr, kq, z4));
-            if (ik) sub_mma(qa, cf_mma_nt(stg[1] + CNB, stg[0] + CNB, rb, cb, lr, kq, z4));
+            if (ik) sub_mma(qa, cf_mma_nt(stg[BAND ? 0 : 1] + CNB, stg[0] + CNB, rb, cb, lr, kq, z4));
             __syncthreads();
             if (tm) tm[2] = __builtin_amdgcn_s_memrealtime();
         }
@@ -2252,6 +2259,12 @@ __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) {
         cf_publish(a, a.zready + j);
     }
 }
+
+// the L^-1 solve (dense mode: config 1's few tasks, one workgroup per CU with the lookahead's registers)
+__global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) { chol_flow_body<false>(a, P); }
+// the substitution solve (band mode: thousands of tasks; no lookahead, so two workgroups fit a CU)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LBA_CF_BAND_WAVES, LBA_CF_BAND_WAVES)))
+void k_chol_flow_band(CholFlow a, DevProblem P) { chol_flow_body<true>(a, P); }
 
 // ------------------------------------------------------------------------------------------------
 constexpr int UPD_THREADS = 64;     // one landmark (or KF) per thread: many small blocks for latency hiding
@@ -3151,10 +3164,11 @@ static CholFlow make_flow(const DevProblem& P, unsigned epoch) {
 static void launch_flow(const CholFlow& a, const DevProblem& P, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const dim3 g(min(a.ntasks, 512));
     if (g.x == 0) return;
+    auto kern = P.cf_band ? k_chol_flow_band : k_chol_flow;
     if (e0 || e1)
-        hipExtLaunchKernelGGL(k_chol_flow, g, dim3(256), 0, s, e0, e1, 0, a, P);
+        hipExtLaunchKernelGGL(kern, g, dim3(256), 0, s, e0, e1, 0, a, P);
     else
-        hipLaunchKernelGGL(k_chol_flow, g, dim3(256), 0, s, a, P);
+        hipLaunchKernelGGL(kern, g, dim3(256), 0, s, a, P);
 }
 void launch_cholesky_solve(const DevProblem& P, int gate, unsigned epoch, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     (void)gate;
