@@ -1681,8 +1681,8 @@ __device__ __forceinline__ d4 cf_mma_nn(const double (*X)[CNB + 1], const double
     return acc;
 }
 
-#ifndef LBA_CF_BAND_WAVES   // waves per SIMD the band kernel is compiled for (A/B builds only)
-#define LBA_CF_BAND_WAVES 2
+#ifndef LBA_CF_BAND_WAVES   // waves per SIMD the band kernel is compiled for (A/B builds only; 3 spills and is
+#define LBA_CF_BAND_WAVES 2   // slower, profiles/r8t_ab_chol_waves.txt)
 #endif
 // BAND: the substitution solve's kernel (kinds 0, 4, 5, 6, 7, no lookahead: the host gives none in band mode); the
 // L^-1 solve's kernel (kinds 0 with or without lookahead, 1, 2, 3, 4) otherwise
@@ -2260,7 +2260,8 @@ __device__ __forceinline__ void chol_flow_body(const CholFlow& a, const DevProbl
     }
 }
 
-// the L^-1 solve (dense mode: config 1's few tasks, one workgroup per CU with the lookahead's registers)
+// the L^-1 solve (dense mode: config 1's few tasks, one workgroup per CU with the lookahead's registers; compiled for
+// 2 waves per SIMD it spills and config 1's solve takes 99 instead of 77 us, profiles/r8t_ab_chol_waves.txt)
 __global__ __launch_bounds__(256) void k_chol_flow(CholFlow a, DevProblem P) { chol_flow_body<false>(a, P); }
 // the substitution solve (band mode: thousands of tasks; no lookahead, so two workgroups fit a CU)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LBA_CF_BAND_WAVES, LBA_CF_BAND_WAVES)))
@@ -3162,7 +3163,9 @@ static CholFlow make_flow(const DevProblem& P, unsigned epoch) {
     return a;
 }
 static void launch_flow(const CholFlow& a, const DevProblem& P, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    const dim3 g(min(a.ntasks, 512));
+    // persistent workgroups: as many as are resident at once (256 CUs; the dense kernel fits one per CU, the
+    // extra ones start as the others leave and find no tickets)
+    const dim3 g(min(a.ntasks, 256 * max(2, P.cf_band ? LBA_CF_BAND_WAVES : 1)));
     if (g.x == 0) return;
     auto kern = P.cf_band ? k_chol_flow_band : k_chol_flow;
     if (e0 || e1)
