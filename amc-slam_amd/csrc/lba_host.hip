@@ -1975,7 +1975,7 @@ int set_problem(lba_problem* p, const lba_kf* kfs, int n_kf, const double* lm_xy
                 p->split_tasks[0] = D.cf_ntasks;
                 p->split_tasks[1] = D.cf_ntasks2;
             }
-            // band mode: no L^-1 tiles; ivready then flags the back-substituted blocks x_j
+            // band mode: no L^-1 tiles (ivready unused: x_j goes to the back tasks as granules, cf_xg)
             const size_t niv = band ? (size_t)NP + 1 : (size_t)std::max(NP * (NP + 1) / 2, 1);
             D.cf_linv = band ? nullptr : dalloc<double>(p, (size_t)npad * npad);
             D.cf_ivready = dalloc<int>(p, niv);
